@@ -1,0 +1,616 @@
+// capi.hip — implementation of the C ABI declared in include/bwagpu.h.
+//
+// One context = one device.  It owns the HBM-resident reference (pac +
+// contig table), the scoring options, and BWAGPU_NUM_SLOTS independent
+// submission slots, each with its own HIP stream, device buffers, pinned
+// host staging and events — the MI355X form of the reference's two
+// ping-ponged SWTask objects (src/fpga/FPGAPipeline.cpp:373-386,
+// SWTask.cpp:40-104).  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine.h"
+
+using namespace bwagpu;
+
+namespace {
+
+struct DevBuf {  // grow-only device buffer
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n + n / 4, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+struct HostBuf {  // grow-only pinned host buffer
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n + n / 4, 4096);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+// layout of one batch inside a slot's single input allocation
+struct InLayout {
+  size_t seq_off, seq, rco, cso, rid, frac, seeds, total;
+  void make(const bwagpu_batch_t& b) {
+    size_t o = 0;
+    auto take = [&](size_t n) {
+      size_t at = o;
+      o += (n + 255) & ~(size_t)255;
+      return at;
+    };
+    seq_off = take(sizeof(int64_t) * (size_t)(b.n_reads + 1));
+    rco = take(sizeof(int32_t) * (size_t)(b.n_reads + 1));
+    cso = take(sizeof(int32_t) * (size_t)(b.n_chains + 1));
+    rid = take(sizeof(int32_t) * (size_t)b.n_chains);
+    frac = take(sizeof(float) * (size_t)b.n_chains);
+    seeds = take(sizeof(bwagpu_seed_t) * (size_t)b.n_seeds);
+    seq = take((size_t)b.seq_bytes);
+    total = o;
+  }
+};
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+  DevBuf d_in, d_win, d_srt, d_out, d_n, d_stats, d_lists, d_counts;
+  HostBuf h_in, h_out, h_n, h_stats;
+  bool busy = false;
+  int32_t n_reads = 0, n_seeds = 0;
+  std::chrono::steady_clock::time_point t_submit;
+  bwagpu_stats_t last{};
+  int64_t h2d = 0, d2h = 0;
+};
+
+}  // namespace
+
+struct bwagpu_ctx {
+  int device = 0;
+  DevOpt opt{};
+  DevRef ref{};
+  bool own_pac = false;
+  void* d_pac = nullptr;
+  int64_t* d_ann_off = nullptr;
+  int32_t* d_ann_len = nullptr;
+  int watchdog_ms = 10000;
+  Slot slot[BWAGPU_NUM_SLOTS];
+  std::string err;
+};
+
+namespace {
+
+int fail(bwagpu_ctx_t* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(bwagpu_ctx_t* c, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return fail(c, BWAGPU_E_NOMEM, m);
+  return fail(c, BWAGPU_E_DEVICE, m);
+}
+
+#define HIPC(call, what)                             \
+  do {                                               \
+    hipError_t e_ = (call);                          \
+    if (e_ != hipSuccess) return hip_fail(ctx, e_, what); \
+  } while (0)
+
+bool make_opt(const bwagpu_opt_t* o, DevOpt* d, std::string* why) {
+  if (!o) { *why = "opt is NULL"; return false; }
+  if (o->e_del <= 0 || o->e_ins <= 0) { *why = "gap extension penalties must be > 0"; return false; }
+  if (o->w < 0 || o->a < 0) { *why = "negative band width or match score"; return false; }
+  memset(d, 0, sizeof(*d));
+  d->a = o->a;
+  d->o_del = o->o_del;
+  d->e_del = o->e_del;
+  d->o_ins = o->o_ins;
+  d->e_ins = o->e_ins;
+  d->oe_del = o->o_del + o->e_del;
+  d->oe_ins = o->o_ins + o->e_ins;
+  d->pen_clip5 = o->pen_clip5;
+  d->pen_clip3 = o->pen_clip3;
+  d->w = o->w;
+  d->zdrop = o->zdrop;
+  int mx = 0;  // ksw.c:397-398 — max over the m*m matrix, starting from 0
+  for (int i = 0; i < 25; ++i) mx = std::max<int>(mx, o->mat[i]);
+  d->max_mat = mx;
+  memcpy(d->mat, o->mat, 25);
+  return true;
+}
+
+int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, bwagpu_ctx_t** out,
+                  bwagpu_ctx_t** made) {
+  if (!out || !bns || bns->l_pac <= 0 || bns->n_seqs <= 0 || !bns->ann_offset || !bns->ann_len)
+    return BWAGPU_E_INVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return BWAGPU_E_NODEVICE;
+  if (device < 0 || device >= n) return BWAGPU_E_NODEVICE;
+  bwagpu_ctx_t* ctx = new (std::nothrow) bwagpu_ctx_t();
+  if (!ctx) return BWAGPU_E_NOMEM;
+  std::string why;
+  if (!make_opt(opt, &ctx->opt, &why)) {
+    delete ctx;
+    return BWAGPU_E_INVAL;
+  }
+  ctx->device = device;
+  *made = ctx;
+  HIPC(hipSetDevice(device), "hipSetDevice");
+  HIPC(hipMalloc(&ctx->d_ann_off, sizeof(int64_t) * bns->n_seqs), "hipMalloc(ann_offset)");
+  HIPC(hipMalloc(&ctx->d_ann_len, sizeof(int32_t) * bns->n_seqs), "hipMalloc(ann_len)");
+  HIPC(hipMemcpy(ctx->d_ann_off, bns->ann_offset, sizeof(int64_t) * bns->n_seqs, hipMemcpyHostToDevice),
+       "upload ann_offset");
+  HIPC(hipMemcpy(ctx->d_ann_len, bns->ann_len, sizeof(int32_t) * bns->n_seqs, hipMemcpyHostToDevice),
+       "upload ann_len");
+  for (auto& s : ctx->slot) {
+    HIPC(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+    HIPC(hipEventCreate(&s.ev0), "hipEventCreate");
+    HIPC(hipEventCreate(&s.ev1), "hipEventCreate");
+    HIPC(hipEventCreate(&s.ev2), "hipEventCreate");
+    HIPC(hipEventCreate(&s.ev3), "hipEventCreate");
+  }
+  ctx->ref.l_pac = bns->l_pac;
+  ctx->ref.n_seqs = bns->n_seqs;
+  ctx->ref.ann_offset = ctx->d_ann_off;
+  ctx->ref.ann_len = ctx->d_ann_len;
+  return BWAGPU_OK;
+}
+
+void destroy_ctx(bwagpu_ctx_t* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  for (auto& s : ctx->slot) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    s.d_in.release(); s.d_win.release(); s.d_srt.release(); s.d_out.release(); s.d_n.release();
+    s.d_stats.release(); s.d_lists.release(); s.d_counts.release();
+    s.h_in.release(); s.h_out.release(); s.h_n.release(); s.h_stats.release();
+    if (s.ev0) (void)hipEventDestroy(s.ev0);
+    if (s.ev1) (void)hipEventDestroy(s.ev1);
+    if (s.ev2) (void)hipEventDestroy(s.ev2);
+    if (s.ev3) (void)hipEventDestroy(s.ev3);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  if (ctx->own_pac && ctx->d_pac) (void)hipFree(ctx->d_pac);
+  if (ctx->d_ann_off) (void)hipFree(ctx->d_ann_off);
+  if (ctx->d_ann_len) (void)hipFree(ctx->d_ann_len);
+  delete ctx;
+}
+
+// validate the flattened batch on the host (cheap O(n) checks so that a
+// malformed batch is an E_INVAL here, never an out-of-bounds access on device)
+int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b) {
+  if (!b) return fail(ctx, BWAGPU_E_INVAL, "batch is NULL");
+  if (b->n_reads < 0 || b->n_chains < 0 || b->n_seeds < 0 || b->seq_bytes < 0)
+    return fail(ctx, BWAGPU_E_INVAL, "negative batch dimension");
+  if (b->n_reads == 0) return BWAGPU_OK;
+  if (!b->seq_off || !b->read_chain_off || !b->chain_seed_off)
+    return fail(ctx, BWAGPU_E_INVAL, "NULL offset array");
+  if (b->seq_off[0] != 0 || b->seq_off[b->n_reads] != b->seq_bytes)
+    return fail(ctx, BWAGPU_E_INVAL, "seq_off does not span seq_bytes");
+  if (b->read_chain_off[0] != 0 || b->read_chain_off[b->n_reads] != b->n_chains)
+    return fail(ctx, BWAGPU_E_INVAL, "read_chain_off does not span n_chains");
+  if (b->chain_seed_off[0] != 0 || b->chain_seed_off[b->n_chains] != b->n_seeds)
+    return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off does not span n_seeds");
+  for (int r = 0; r < b->n_reads; ++r) {
+    int64_t l = b->seq_off[r + 1] - b->seq_off[r];
+    if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
+    if (l > BWAGPU_MAX_READ_LEN) {
+      char m[128];
+      snprintf(m, sizeof m, "read %d has length %lld > %d", r, (long long)l, BWAGPU_MAX_READ_LEN);
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, m);
+    }
+    if (b->read_chain_off[r + 1] < b->read_chain_off[r]) return fail(ctx, BWAGPU_E_INVAL, "read_chain_off not monotone");
+  }
+  if (b->n_chains && (!b->chain_rid || !b->chain_frac_rep)) return fail(ctx, BWAGPU_E_INVAL, "NULL chain array");
+  if (b->n_seeds && !b->seeds) return fail(ctx, BWAGPU_E_INVAL, "NULL seeds");
+  if (b->seq_bytes && !b->seq) return fail(ctx, BWAGPU_E_INVAL, "NULL seq");
+  for (int c = 0; c < b->n_chains; ++c)
+    if (b->chain_seed_off[c + 1] < b->chain_seed_off[c]) return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off not monotone");
+  // seeds must lie inside their read and inside [0, 2*l_pac)
+  const int64_t two = ctx->ref.l_pac << 1;
+  for (int r = 0; r < b->n_reads; ++r) {
+    const int l = (int)(b->seq_off[r + 1] - b->seq_off[r]);
+    for (int c = b->read_chain_off[r]; c < b->read_chain_off[r + 1]; ++c)
+      for (int k = b->chain_seed_off[c]; k < b->chain_seed_off[c + 1]; ++k) {
+        const bwagpu_seed_t& s = b->seeds[k];
+        if (s.qbeg < 0 || s.len <= 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > two)
+          return fail(ctx, BWAGPU_E_INVAL, "seed outside its read or the reference");
+      }
+  }
+  return BWAGPU_OK;
+}
+
+// LDS row-buffer bytes per group for reads up to lq_max (see rows_needed)
+int tb_bytes_for(const DevOpt& o, int lq_max) {
+  const int eb = std::max(o.pen_clip5, o.pen_clip3);
+  const int cap = std::max(band_cap(lq_max, o.max_mat, eb, o.o_ins, o.e_ins),
+                           band_cap(lq_max, o.max_mat, eb, o.o_del, o.e_del));
+  const int we = std::min(o.w << 1, cap);
+  const int n = lq_max + we + 2;
+  return (n + 15) & ~15;
+}
+
+// enqueue prep + binning + the per-variant kernels for a batch whose arrays
+// are already in device memory
+int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwagpu_alnreg_t* d_out,
+                      int32_t* d_n, int64_t* d_stats, hipStream_t st) {
+  HIPC(s.d_win.ensure(sizeof(ChainWin) * (size_t)std::max(db.n_chains, 1)), "hipMalloc(win)");
+  HIPC(s.d_srt.ensure(sizeof(uint64_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(srt)");
+  HIPC(s.d_lists.ensure(sizeof(int32_t) * (size_t)kNumVariants * std::max(db.n_reads, 1)), "hipMalloc(lists)");
+  HIPC(s.d_counts.ensure(sizeof(int32_t) * 16), "hipMalloc(counts)");
+  HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * 16, st), "memset counts");
+  if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
+  HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, 0, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(), d_stats, st),
+       "chain_prep launch");
+  HIPC(launch_bin_reads(db, s.d_counts.as<int32_t>(), s.d_lists.as<int32_t>(), d_stats, st), "bin launch");
+  for (int v = 0; v < kNumVariants; ++v) {
+    const int lqv = std::min(lq_max, kVariants[v].max_len());
+    const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
+    const int gpb = kBlock / kVariants[v].G;
+    if ((size_t)tb * gpb > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
+    HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, s.d_lists.as<int32_t>() + (size_t)v * db.n_reads,
+                          s.d_counts.as<int32_t>() + v, db.n_reads, tb, s.d_win.as<ChainWin>(),
+                          s.d_srt.as<uint64_t>(), d_out, d_n, d_stats, st),
+         "chain2aln launch");
+  }
+  return BWAGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bwagpu_abi_version(void) { return BWAGPU_ABI_VERSION; }
+
+int bwagpu_device_count(int* n) {
+  if (!n) return BWAGPU_E_INVAL;
+  int k = 0;
+  if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+  *n = k;
+  return k > 0 ? BWAGPU_OK : BWAGPU_E_NODEVICE;
+}
+
+int bwagpu_create(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t* pac_host,
+                  bwagpu_ctx_t** out) {
+  if (!pac_host) return BWAGPU_E_INVAL;
+  bwagpu_ctx_t* ctx = nullptr;
+  int rc = create_common(device, opt, bns, out, &ctx);
+  if (rc == BWAGPU_OK) {
+    const size_t pac_bytes = (size_t)(bns->l_pac / 4 + 1);  // bwa.c:281-282
+    hipError_t e = hipMalloc(&ctx->d_pac, pac_bytes);
+    if (e == hipSuccess) {
+      ctx->own_pac = true;
+      e = hipMemcpy(ctx->d_pac, pac_host, pac_bytes, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) rc = hip_fail(ctx, e, "pac upload");
+    ctx->ref.pac = (const uint8_t*)ctx->d_pac;
+  }
+  if (rc != BWAGPU_OK) {
+    destroy_ctx(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return BWAGPU_OK;
+}
+
+int bwagpu_create_resident(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const void* pac_device,
+                           bwagpu_ctx_t** out) {
+  if (!pac_device) return BWAGPU_E_INVAL;
+  bwagpu_ctx_t* ctx = nullptr;
+  int rc = create_common(device, opt, bns, out, &ctx);
+  if (rc != BWAGPU_OK) {
+    destroy_ctx(ctx);
+    return rc;
+  }
+  ctx->d_pac = (void*)pac_device;
+  ctx->own_pac = false;
+  ctx->ref.pac = (const uint8_t*)pac_device;
+  *out = ctx;
+  return BWAGPU_OK;
+}
+
+int bwagpu_destroy(bwagpu_ctx_t* ctx) {
+  if (!ctx) return BWAGPU_E_INVAL;
+  destroy_ctx(ctx);
+  return BWAGPU_OK;
+}
+
+const char* bwagpu_last_error(const bwagpu_ctx_t* ctx) { return ctx ? ctx->err.c_str() : "NULL context"; }
+
+int bwagpu_set_watchdog_ms(bwagpu_ctx_t* ctx, int ms) {
+  if (!ctx || ms < 0) return BWAGPU_E_INVAL;
+  ctx->watchdog_ms = ms;
+  return BWAGPU_OK;
+}
+
+int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b) {
+  if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
+  Slot& s = ctx->slot[slot];
+  if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
+  int rc = check_batch(ctx, b);
+  if (rc) return rc;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  s.t_submit = std::chrono::steady_clock::now();
+  s.n_reads = b->n_reads;
+  s.n_seeds = b->n_seeds;
+  InLayout L;
+  L.make(*b);
+  HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
+  HIPC(s.d_in.ensure(L.total), "hipMalloc(in)");
+  HIPC(s.d_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipMalloc(out)");
+  HIPC(s.d_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipMalloc(out_n)");
+  HIPC(s.d_stats.ensure(sizeof(int64_t) * ST_N), "hipMalloc(stats)");
+  HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipHostMalloc(out)");
+  HIPC(s.h_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipHostMalloc(out_n)");
+  HIPC(s.h_stats.ensure(sizeof(int64_t) * ST_N), "hipHostMalloc(stats)");
+  // stage into pinned memory so the caller's buffers are free on return
+  char* h = s.h_in.as<char>();
+  int lq_max = 0;
+  if (b->n_reads) {
+    memcpy(h + L.seq_off, b->seq_off, sizeof(int64_t) * (size_t)(b->n_reads + 1));
+    memcpy(h + L.rco, b->read_chain_off, sizeof(int32_t) * (size_t)(b->n_reads + 1));
+    for (int r = 0; r < b->n_reads; ++r) lq_max = std::max<int>(lq_max, (int)(b->seq_off[r + 1] - b->seq_off[r]));
+  }
+  memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
+  if (b->n_chains) {
+    memcpy(h + L.rid, b->chain_rid, sizeof(int32_t) * (size_t)b->n_chains);
+    memcpy(h + L.frac, b->chain_frac_rep, sizeof(float) * (size_t)b->n_chains);
+  }
+  if (b->n_seeds) memcpy(h + L.seeds, b->seeds, sizeof(bwagpu_seed_t) * (size_t)b->n_seeds);
+  if (b->seq_bytes) memcpy(h + L.seq, b->seq, (size_t)b->seq_bytes);
+
+  hipStream_t st = s.stream;
+  HIPC(hipEventRecord(s.ev0, st), "event");
+  HIPC(hipMemcpyAsync(s.d_in.p, s.h_in.p, L.total, hipMemcpyHostToDevice, st), "H2D batch");
+  HIPC(hipMemsetAsync(s.d_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset stats");
+  char* d = s.d_in.as<char>();
+  DevBatch db;
+  db.n_reads = b->n_reads;
+  db.n_chains = b->n_chains;
+  db.n_seeds = b->n_seeds;
+  db.seq_off = (const int64_t*)(d + L.seq_off);
+  db.seq = (const uint8_t*)(d + L.seq);
+  db.read_chain_off = (const int32_t*)(d + L.rco);
+  db.chain_seed_off = (const int32_t*)(d + L.cso);
+  db.chain_rid = (const int32_t*)(d + L.rid);
+  db.chain_frac_rep = (const float*)(d + L.frac);
+  db.seeds = (const bwagpu_seed_t*)(d + L.seeds);
+  HIPC(hipEventRecord(s.ev1, st), "event");
+  rc = enqueue_chain2aln(ctx, s, db, lq_max, s.d_out.as<bwagpu_alnreg_t>(), s.d_n.as<int32_t>(),
+                         s.d_stats.as<int64_t>(), st);
+  if (rc) return rc;
+  HIPC(hipEventRecord(s.ev2, st), "event");
+  if (b->n_seeds)
+    HIPC(hipMemcpyAsync(s.h_out.p, s.d_out.p, sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds, hipMemcpyDeviceToHost, st),
+         "D2H regions");
+  if (b->n_reads)
+    HIPC(hipMemcpyAsync(s.h_n.p, s.d_n.p, sizeof(int32_t) * (size_t)b->n_reads, hipMemcpyDeviceToHost, st),
+         "D2H counts");
+  HIPC(hipMemcpyAsync(s.h_stats.p, s.d_stats.p, sizeof(int64_t) * ST_N, hipMemcpyDeviceToHost, st), "D2H stats");
+  HIPC(hipEventRecord(s.ev3, st), "event");
+  s.h2d = (int64_t)L.total;
+  s.d2h = (int64_t)(sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds + sizeof(int32_t) * (size_t)b->n_reads);
+  s.busy = true;
+  return BWAGPU_OK;
+}
+
+int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs, int32_t* out_n) {
+  if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
+  Slot& s = ctx->slot[slot];
+  if (!s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot has no batch in flight");
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  // watchdog (SWTask::finish, SWTask.cpp:162-169): poll the completion event
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    hipError_t q = hipEventQuery(s.ev3);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) {
+      s.busy = false;
+      return hip_fail(ctx, q, "batch execution");
+    }
+    if (ctx->watchdog_ms > 0 &&
+        std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+            ctx->watchdog_ms) {
+      return fail(ctx, BWAGPU_E_HANG, "watchdog: batch did not finish in time");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  s.busy = false;
+  const int64_t* st = s.h_stats.as<int64_t>();
+  float k_ms = 0, t_ms = 0;
+  (void)hipEventElapsedTime(&k_ms, s.ev1, s.ev2);
+  (void)hipEventElapsedTime(&t_ms, s.ev0, s.ev3);
+  s.last.kernel_ms = k_ms;
+  s.last.total_ms = t_ms;
+  s.last.cells = st[ST_CELLS];
+  s.last.rows = st[ST_ROWS];
+  s.last.ext_calls = st[ST_CALLS];
+  s.last.h2d_bytes = s.h2d;
+  s.last.d2h_bytes = s.d2h;
+  if (st[ST_ERR] & ERR_RID)
+    return fail(ctx, BWAGPU_E_RESULTS, "a chain's first seed is not inside contig chain_rid (bwamem.c:669 assert)");
+  if (st[ST_ERR] & ERR_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_READ_LEN");
+  if (out_n && s.n_reads) memcpy(out_n, s.h_n.p, sizeof(int32_t) * (size_t)s.n_reads);
+  if (out_regs && s.n_seeds) memcpy(out_regs, s.h_out.p, sizeof(bwagpu_alnreg_t) * (size_t)s.n_seeds);
+  return BWAGPU_OK;
+}
+
+int bwagpu_chain2aln(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, bwagpu_alnreg_t* out_regs, int32_t* out_n) {
+  int rc = bwagpu_chain2aln_submit(ctx, 0, b);
+  if (rc) return rc;
+  return bwagpu_chain2aln_wait(ctx, 0, out_regs, out_n);
+}
+
+int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwagpu_alnreg_t* dev_out,
+                            int32_t* dev_n, int64_t* dev_stats, void* stream) {
+  if (!ctx || !db_in || !dev_out || !dev_n) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  Slot& s = ctx->slot[0];
+  hipStream_t st = stream ? (hipStream_t)stream : s.stream;
+  DevBatch db;
+  db.n_reads = db_in->n_reads;
+  db.n_chains = db_in->n_chains;
+  db.n_seeds = db_in->n_seeds;
+  db.seq_off = db_in->seq_off;
+  db.seq = db_in->seq;
+  db.read_chain_off = db_in->read_chain_off;
+  db.chain_seed_off = db_in->chain_seed_off;
+  db.chain_rid = db_in->chain_rid;
+  db.chain_frac_rep = db_in->chain_frac_rep;
+  db.seeds = db_in->seeds;
+  int64_t* stats = dev_stats;
+  if (!stats) {
+    HIPC(s.d_stats.ensure(sizeof(int64_t) * ST_N), "hipMalloc(stats)");
+    stats = s.d_stats.as<int64_t>();
+    HIPC(hipMemsetAsync(stats, 0, sizeof(int64_t) * ST_N, st), "memset stats");
+  }
+  // reads are bounded by BWAGPU_MAX_READ_LEN; the LDS row buffer is sized for it
+  return enqueue_chain2aln(ctx, s, db, BWAGPU_MAX_READ_LEN, dev_out, dev_n, stats, st);
+}
+
+int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* tasks, const uint8_t* qpool,
+                        int64_t qpool_len, const uint8_t* tpool, int64_t tpool_len, bwagpu_ext_result_t* results) {
+  if (!ctx || n < 0 || (n && (!tasks || !results))) return BWAGPU_E_INVAL;
+  if (n == 0) return BWAGPU_OK;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  // validate and bin on the host
+  std::vector<int32_t> lists[kNumVariants];
+  bool t5 = false;
+  int lq_max = 1;
+  for (int32_t k = 0; k < n; ++k) {
+    const bwagpu_ext_task_t& t = tasks[k];
+    if (t.qlen < 0 || t.tlen < 0 || t.qoff < 0 || t.toff < 0 || t.qoff + t.qlen > qpool_len ||
+        t.toff + t.tlen > tpool_len || t.w < 0)
+      return fail(ctx, BWAGPU_E_INVAL, "task outside its pools");
+    if (t.qlen + 1 > kVariants[kNumVariants - 1].max_len()) return fail(ctx, BWAGPU_E_UNSUPPORTED, "qlen too long");
+    int v = kNumVariants - 1;
+    for (int i = kNumVariants - 1; i >= 0; --i)
+      if (t.qlen + 1 <= kVariants[i].max_len()) v = i;
+    lists[v].push_back(k);
+    lq_max = std::max(lq_max, t.qlen + 1);
+  }
+  for (int64_t i = 0; i < tpool_len && !t5; ++i) t5 = tpool[i] > 3;
+  for (int64_t i = 0; i < qpool_len; ++i)
+    if (qpool[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "query base > 4");
+  for (int64_t i = 0; i < tpool_len; ++i)
+    if (tpool[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "target base > 4");
+  // LDS rows needed per task (rows_needed on the host) -> per-variant max
+  Slot& s = ctx->slot[0];
+  hipStream_t st = s.stream;
+  DevBuf d_tasks, d_list, d_q, d_t, d_res, d_stats;
+  auto cleanup = [&]() {
+    d_tasks.release(); d_list.release(); d_q.release(); d_t.release(); d_res.release(); d_stats.release();
+  };
+  auto ck = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(ctx, e, what);
+    }
+    return 0;
+  };
+  int rc;
+  if ((rc = ck(d_tasks.ensure(sizeof(bwagpu_ext_task_t) * n), "hipMalloc"))) return rc;
+  if ((rc = ck(d_list.ensure(sizeof(int32_t) * n), "hipMalloc"))) return rc;
+  if ((rc = ck(d_q.ensure((size_t)qpool_len + 1), "hipMalloc"))) return rc;
+  if ((rc = ck(d_t.ensure((size_t)tpool_len + 1), "hipMalloc"))) return rc;
+  if ((rc = ck(d_res.ensure(sizeof(bwagpu_ext_result_t) * n), "hipMalloc"))) return rc;
+  if ((rc = ck(d_stats.ensure(sizeof(int64_t) * ST_N), "hipMalloc"))) return rc;
+  if ((rc = ck(hipMemcpyAsync(d_tasks.p, tasks, sizeof(bwagpu_ext_task_t) * n, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+  if (qpool_len && (rc = ck(hipMemcpyAsync(d_q.p, qpool, (size_t)qpool_len, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+  if (tpool_len && (rc = ck(hipMemcpyAsync(d_t.p, tpool, (size_t)tpool_len, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+  if ((rc = ck(hipMemsetAsync(d_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset"))) return rc;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, st);
+  int32_t off = 0;
+  std::vector<int32_t> all;
+  for (int v = 0; v < kNumVariants; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
+  if ((rc = ck(hipMemcpyAsync(d_list.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+  for (int v = 0; v < kNumVariants; ++v) {
+    const int32_t nv = (int32_t)lists[v].size();
+    if (nv) {
+      int rows = 16;
+      for (int32_t k : lists[v]) {
+        const bwagpu_ext_task_t& t = tasks[k];
+        int mi = band_cap(t.qlen, ctx->opt.max_mat, t.end_bonus, ctx->opt.o_ins, ctx->opt.e_ins);
+        int md = band_cap(t.qlen, ctx->opt.max_mat, t.end_bonus, ctx->opt.o_del, ctx->opt.e_del);
+        int we = std::min(t.w, std::min(mi, md));
+        rows = std::max(rows, std::min(t.tlen, t.qlen + we + 1));
+      }
+      const int tb = (rows + 15) & ~15;
+      const int gpb = kBlock / kVariants[v].G;
+      if ((size_t)tb * gpb > 64 * 1024) {
+        cleanup();
+        return fail(ctx, BWAGPU_E_UNSUPPORTED, "task needs too many LDS rows");
+      }
+      hipError_t e = launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off,
+                                   nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
+                                   d_stats.as<int64_t>(), st);
+      if ((rc = ck(e, "extend launch"))) return rc;
+    }
+    off += nv;
+  }
+  (void)hipEventRecord(e1, st);
+  int64_t hs[ST_N];
+  if ((rc = ck(hipMemcpyAsync(results, d_res.p, sizeof(bwagpu_ext_result_t) * n, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+  if ((rc = ck(hipMemcpyAsync(hs, d_stats.p, sizeof(hs), hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+  if ((rc = ck(hipStreamSynchronize(st), "extend batch"))) return rc;
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  s.last = bwagpu_stats_t{};
+  s.last.kernel_ms = ms;
+  s.last.cells = hs[ST_CELLS];
+  s.last.rows = hs[ST_ROWS];
+  s.last.ext_calls = hs[ST_CALLS];
+  cleanup();
+  return BWAGPU_OK;
+}
+
+int bwagpu_last_stats(const bwagpu_ctx_t* ctx, int slot, bwagpu_stats_t* out) {
+  if (!ctx || !out || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
+  *out = ctx->slot[slot].last;
+  return BWAGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,81 @@
+// engine.h — shared declarations between the HIP kernels (sw_kernels.hip) and
+// the C-ABI implementation (capi.hip).  Internal; not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bwagpu.h"
+
+namespace bwagpu {
+
+// Scoring parameters in the form the kernels use (from bwagpu_opt_t).
+struct DevOpt {
+  int a, o_del, e_del, o_ins, e_ins, oe_del, oe_ins;
+  int pen_clip5, pen_clip3, w, zdrop, max_mat;
+  int8_t mat[28];
+};
+
+// Per-chain window computed by the prep kernel: [lo, hi) in the 2-strand
+// coordinate space, already clipped like bns_fetch_seq (bntseq.c:421-446).
+struct ChainWin {
+  int64_t lo, hi;
+};
+
+// Device views of one flattened batch (pointers are device pointers).
+struct DevBatch {
+  int32_t n_reads, n_chains, n_seeds;
+  const int64_t* seq_off;
+  const uint8_t* seq;
+  const int32_t* read_chain_off;
+  const int32_t* chain_seed_off;
+  const int32_t* chain_rid;
+  const float* chain_frac_rep;
+  const bwagpu_seed_t* seeds;
+};
+
+struct DevRef {
+  int64_t l_pac;
+  int32_t n_seqs;
+  const uint8_t* pac;
+  const int64_t* ann_offset;
+  const int32_t* ann_len;
+};
+
+// stats words (int64): [0] cells [1] rows [2] ext calls [3] error flags
+enum { ST_CELLS = 0, ST_ROWS = 1, ST_CALLS = 2, ST_ERR = 3, ST_N = 4 };
+enum { ERR_RID = 1, ERR_LEN = 2 };
+
+// Kernel variants: G lanes per read ("group"), C = max DP columns per lane.
+// A read of length l needs G*C >= l (+1 column for eh[qlen], qlen <= l-1).
+struct Variant {
+  int G, C;
+  int max_len() const { return G * C; }
+};
+constexpr int kNumVariants = 3;
+extern const Variant kVariants[kNumVariants];
+constexpr int kBlock = 256;  // threads per workgroup (4 waves)
+
+// host-side launchers (sw_kernels.hip)
+hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, int64_t lq_cap,
+                             ChainWin* win, uint64_t* srt, int64_t* stats, hipStream_t st);
+hipError_t launch_bin_reads(const DevBatch& b, int32_t* counts, int32_t* lists, int64_t* stats,
+                            hipStream_t st);
+// read_list/d_count: device list of read indices and its length (from
+// launch_bin_reads); max_list bounds the grid
+hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b,
+                            const int32_t* read_list, const int32_t* d_count, int32_t max_list,
+                            int tb_bytes, const ChainWin* win, uint64_t* srt, bwagpu_alnreg_t* out,
+                            int32_t* out_n, int64_t* stats, hipStream_t st);
+hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
+                         const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
+                         const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,
+                         bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
+
+// rows a task can touch: the band is empty once i - w >= qlen (ksw.c:417-419),
+// so rows i <= qlen + w are the most ever read (the last one only to break)
+__host__ __device__ inline int band_cap(int qlen, int max_mat, int end_bonus, int o, int e) {
+  int l = (int)((double)(qlen * max_mat + end_bonus - o) / e + 1.);
+  return l > 1 ? l : 1;
+}
+
+}  // namespace bwagpu

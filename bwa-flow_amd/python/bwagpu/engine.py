@@ -1,0 +1,184 @@
+"""Python host mirror of the engine: flattened read batches and a per-device
+Engine wrapping the C ABI.  Used by tests, smoke() and bench.py; the C++ host
+(bwa-flow_amd/host/) uses the same ABI directly."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+
+
+class BwaGpuError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{abi.ERR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None or a.size == 0 else a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class Batch:
+    """One ChainsRecord (src/Pipeline.h:46-57) in flattened form, see bwagpu_batch_t."""
+    seq_off: np.ndarray         # int64 [n_reads+1]
+    seq: np.ndarray             # uint8 nt4
+    read_chain_off: np.ndarray  # int32 [n_reads+1]
+    chain_seed_off: np.ndarray  # int32 [n_chains+1]
+    chain_rid: np.ndarray       # int32 [n_chains]
+    chain_frac_rep: np.ndarray  # float32 [n_chains]
+    seeds: np.ndarray           # SEED_DTYPE [n_seeds]
+
+    def __post_init__(self):
+        self.seq_off = np.ascontiguousarray(self.seq_off, np.int64)
+        self.seq = np.ascontiguousarray(self.seq, np.uint8)
+        self.read_chain_off = np.ascontiguousarray(self.read_chain_off, np.int32)
+        self.chain_seed_off = np.ascontiguousarray(self.chain_seed_off, np.int32)
+        self.chain_rid = np.ascontiguousarray(self.chain_rid, np.int32)
+        self.chain_frac_rep = np.ascontiguousarray(self.chain_frac_rep, np.float32)
+        self.seeds = np.ascontiguousarray(self.seeds, abi.SEED_DTYPE)
+
+    @property
+    def n_reads(self) -> int:
+        return len(self.seq_off) - 1
+
+    @property
+    def n_chains(self) -> int:
+        return len(self.chain_seed_off) - 1
+
+    @property
+    def n_seeds(self) -> int:
+        return len(self.seeds)
+
+    def read_seed_off(self) -> np.ndarray:
+        """first output slot of every read: chain_seed_off[read_chain_off[r]]"""
+        return self.chain_seed_off[self.read_chain_off[:-1]]
+
+    def to_c(self) -> abi.BatchC:
+        b = abi.BatchC()
+        b.n_reads, b.n_chains, b.n_seeds = self.n_reads, self.n_chains, self.n_seeds
+        b.seq_bytes = int(self.seq_off[-1]) if self.n_reads >= 0 else 0
+        b.seq_off = _ptr(self.seq_off)
+        b.seq = _ptr(self.seq)
+        b.read_chain_off = _ptr(self.read_chain_off)
+        b.chain_seed_off = _ptr(self.chain_seed_off)
+        b.chain_rid = _ptr(self.chain_rid)
+        b.chain_frac_rep = _ptr(self.chain_frac_rep)
+        b.seeds = _ptr(self.seeds)
+        return b
+
+    def subset(self, reads) -> "Batch":
+        """a new batch holding the given reads (in the given order)"""
+        reads = np.asarray(reads, np.int64)
+        so, rco, cso = self.seq_off, self.read_chain_off, self.chain_seed_off
+        seq_parts, seed_parts, rid, fr = [], [], [], []
+        seq_off, rc_off, cs_off = [0], [0], [0]
+        for r in reads:
+            seq_parts.append(self.seq[so[r]:so[r + 1]])
+            seq_off.append(seq_off[-1] + int(so[r + 1] - so[r]))
+            for c in range(rco[r], rco[r + 1]):
+                seed_parts.append(self.seeds[cso[c]:cso[c + 1]])
+                cs_off.append(cs_off[-1] + int(cso[c + 1] - cso[c]))
+                rid.append(self.chain_rid[c])
+                fr.append(self.chain_frac_rep[c])
+            rc_off.append(len(rid))
+        return Batch(np.array(seq_off), np.concatenate(seq_parts) if seq_parts else np.zeros(0, np.uint8),
+                     np.array(rc_off), np.array(cs_off), np.array(rid, np.int32), np.array(fr, np.float32),
+                     np.concatenate(seed_parts) if seed_parts else np.zeros(0, abi.SEED_DTYPE))
+
+
+def unflatten(batch: Batch, regs: np.ndarray, n: np.ndarray) -> list[np.ndarray]:
+    """per-read region arrays (each the read's mem_alnreg_v contents in order)"""
+    off = batch.read_seed_off()
+    return [regs[off[r]:off[r] + n[r]] for r in range(batch.n_reads)]
+
+
+def compact(batch: Batch, regs: np.ndarray, n: np.ndarray) -> np.ndarray:
+    """concatenate the regions of all reads in read order"""
+    parts = unflatten(batch, regs, n)
+    return np.concatenate(parts) if parts else np.zeros(0, abi.ALNREG_DTYPE)
+
+
+class Engine:
+    """One device context (bwagpu_create).  There is no CPU path behind it."""
+
+    def __init__(self, device: int, opt: dict, l_pac: int, ann_offset, ann_len, pac=None,
+                 pac_device_ptr: int | None = None):
+        self.lib = abi.load()
+        self.opt = abi.opt_from_dict(opt)
+        self._ann_off = np.ascontiguousarray(ann_offset, np.int64)
+        self._ann_len = np.ascontiguousarray(ann_len, np.int32)
+        self.bns = abi.Bns(int(l_pac), len(self._ann_off), 0, _ptr(self._ann_off), _ptr(self._ann_len))
+        self.ctx = C.c_void_p()
+        if pac_device_ptr is not None:
+            rc = self.lib.bwagpu_create_resident(device, C.byref(self.opt), C.byref(self.bns),
+                                                 C.c_void_p(pac_device_ptr), C.byref(self.ctx))
+        else:
+            self._pac = np.ascontiguousarray(pac, np.uint8)
+            if len(self._pac) < int(l_pac) // 4 + 1:
+                raise ValueError("pac shorter than l_pac/4+1 bytes")
+            rc = self.lib.bwagpu_create(device, C.byref(self.opt), C.byref(self.bns), _ptr(self._pac),
+                                        C.byref(self.ctx))
+        if rc != abi.OK:
+            raise BwaGpuError(rc, "bwagpu_create failed")
+
+    def close(self):
+        if self.ctx:
+            self.lib.bwagpu_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != abi.OK:
+            raise BwaGpuError(rc, f"{what}: {self.lib.bwagpu_last_error(self.ctx).decode()}")
+
+    def set_watchdog_ms(self, ms: int):
+        self._check(self.lib.bwagpu_set_watchdog_ms(self.ctx, int(ms)), "set_watchdog_ms")
+
+    def chain2aln(self, batch: Batch):
+        """-> (regs[n_seeds] ALNREG_DTYPE, n[n_reads] int32)"""
+        regs = np.zeros(max(batch.n_seeds, 1), abi.ALNREG_DTYPE)
+        n = np.zeros(max(batch.n_reads, 1), np.int32)
+        bc = batch.to_c()
+        self._check(self.lib.bwagpu_chain2aln(self.ctx, C.byref(bc), _ptr(regs), _ptr(n)), "chain2aln")
+        return regs[:batch.n_seeds], n[:batch.n_reads]
+
+    def submit(self, slot: int, batch: Batch):
+        bc = batch.to_c()
+        self._check(self.lib.bwagpu_chain2aln_submit(self.ctx, slot, C.byref(bc)), "submit")
+
+    def wait(self, slot: int, batch: Batch):
+        regs = np.zeros(max(batch.n_seeds, 1), abi.ALNREG_DTYPE)
+        n = np.zeros(max(batch.n_reads, 1), np.int32)
+        self._check(self.lib.bwagpu_chain2aln_wait(self.ctx, slot, _ptr(regs), _ptr(n)), "wait")
+        return regs[:batch.n_seeds], n[:batch.n_reads]
+
+    def chain2aln_device(self, dev_batch: abi.BatchC, dev_out: int, dev_n: int, dev_stats: int | None,
+                         stream: int | None):
+        self._check(self.lib.bwagpu_chain2aln_device(self.ctx, C.byref(dev_batch), C.c_void_p(dev_out),
+                                                     C.c_void_p(dev_n),
+                                                     C.c_void_p(dev_stats) if dev_stats else None,
+                                                     C.c_void_p(stream) if stream else None),
+                    "chain2aln_device")
+
+    def extend_batch(self, tasks: np.ndarray, qpool: np.ndarray, tpool: np.ndarray) -> np.ndarray:
+        tasks = np.ascontiguousarray(tasks, abi.EXT_TASK_DTYPE)
+        qpool = np.ascontiguousarray(qpool, np.uint8)
+        tpool = np.ascontiguousarray(tpool, np.uint8)
+        res = np.zeros(max(len(tasks), 1), abi.EXT_RES_DTYPE)
+        self._check(self.lib.bwagpu_extend_batch(self.ctx, len(tasks), _ptr(tasks), _ptr(qpool), len(qpool),
+                                                 _ptr(tpool), len(tpool), _ptr(res)), "extend_batch")
+        return res[:len(tasks)]
+
+    def last_stats(self, slot: int = 0) -> dict:
+        s = abi.Stats()
+        self._check(self.lib.bwagpu_last_stats(self.ctx, slot, C.byref(s)), "last_stats")
+        return {k: getattr(s, k) for k, _ in abi.Stats._fields_}

@@ -1,0 +1,204 @@
+/*
+ * bwagpu.h — C ABI of the MI355X seed-extension engine.
+ *
+ * This is the drop-in boundary that takes the place of bwa-flow's FPGA
+ * Smith-Waterman back end (the files under src/fpga/).  Everything crossing it is plain C:
+ * POD structs, pointers and sizes, integer return codes, no exceptions.
+ *
+ * What each entry point replaces in the reference (file:line into
+ * falcon-computing/bwa-flow):
+ *
+ *   bwagpu_create / bwagpu_create_resident
+ *       BWAOCLEnv::BWAOCLEnv + initPAC (src/fpga/BWAOCLEnv.h:41-114): bring up
+ *       one device, make the 2-bit reference resident on it.  The reference
+ *       uploads a forward+revcomp pac with a blocking clEnqueueWriteBuffer per
+ *       device (BWAOCLEnv.h:92, 293-312); here only bwa's forward pac
+ *       (bwa.c:281-282 layout, bntseq.c:225 bit order) is resident and the
+ *       reverse strand is computed in-kernel.  _resident takes a pac that is
+ *       already in HBM (e.g. broadcast over xGMI with RCCL by the host).
+ *   bwagpu_chain2aln_submit
+ *       SWTask::start -> XCLAgent::writeInput + clEnqueueTask(sw_top)
+ *       (src/fpga/SWTask.cpp:106-152, xlnx/XCLAgent.cpp:51,89-106): stage one
+ *       packed read batch into a slot's buffers and launch asynchronously.
+ *   bwagpu_chain2aln_wait
+ *       SWTask::finish -> XCLAgent::readOutput + processOutput
+ *       (SWTask.cpp:154-180, XCLAgent.cpp:64, FPGAPipeline.cpp:29-130): wait
+ *       with a watchdog and return finished mem_alnreg_t records.
+ *   bwagpu_chain2aln
+ *       submit + wait; the per-batch body of ChainsToRegionsFPGA::compute
+ *       (FPGAPipeline.cpp:367-579) with the semantics of the CPU stage
+ *       ChainsToRegions::compute (src/Pipeline.cpp:503-544) ->
+ *       mem_chain2aln (bwa/bwamem.c:641-795) for every chain of every read.
+ *   bwagpu_chain2aln_device
+ *       the same launch with every input/output already in device memory
+ *       (benchmarks, multi-stream hosts).
+ *   bwagpu_extend_batch
+ *       a batch of independent ksw_extend2 calls (bwa/ksw.c:380-479); the
+ *       task-level granularity of the FPGA kernel's seed_proc
+ *       (src/fpga/kernel/smithwaterman.cpp:318-445) but with ksw_extend2's
+ *       exact semantics (z-drop, band trimming, runtime scoring).
+ *   bwagpu_last_error
+ *       the what() of fpgaHangError / fpgaResultsError / std::runtime_error
+ *       (src/util.h:16-32, OpenCLEnv.h:21-31).
+ *   bwagpu_destroy
+ *       BWAOCLEnv::~BWAOCLEnv (main.cpp:376-387).
+ *
+ * Results are bit-identical to the reference CPU path: every field that
+ * mem_chain2aln writes (rb,re,qb,qe,rid,score,truesc,w,seedcov,seedlen0,
+ * frac_rep), all other fields zero, regions in the same order.
+ */
+#ifndef BWAGPU_H
+#define BWAGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BWAGPU_ABI_VERSION 1
+
+/* return codes */
+enum {
+  BWAGPU_OK = 0,
+  BWAGPU_E_INVAL = 1,       /* bad argument / malformed batch                       */
+  BWAGPU_E_NOMEM = 2,       /* host or device allocation failed (FPGAPipeline.cpp:383-391) */
+  BWAGPU_E_DEVICE = 3,      /* HIP runtime error (OpenCLEnv.h:21-31 analogue)       */
+  BWAGPU_E_HANG = 4,        /* watchdog expired (fpgaHangError, SWTask.cpp:116-122)  */
+  BWAGPU_E_RESULTS = 5,     /* device flagged an inconsistent input/result
+                               (fpgaResultsError, FPGAPipeline.cpp:72; also the
+                               reference's assert(c->rid == rid), bwamem.c:669)     */
+  BWAGPU_E_UNSUPPORTED = 6, /* read longer than BWAGPU_MAX_READ_LEN                  */
+  BWAGPU_E_NODEVICE = 7     /* no HIP device / not built for this device             */
+};
+
+/* longest read (bp) the device kernels accept; longer reads -> E_UNSUPPORTED */
+#define BWAGPU_MAX_READ_LEN 1023
+/* number of independent in-flight slots per context (ping-pong, FPGAPipeline.cpp:373-386) */
+#define BWAGPU_NUM_SLOTS 2
+
+/* The fields of mem_opt_t (bwa/bwamem.h:26-58) that mem_chain2aln/ksw_extend2 read. */
+typedef struct {
+  int32_t a, b;          /* match score, mismatch penalty (used by cal_max_gap)   */
+  int32_t o_del, e_del;  /* deletion open/extend                                  */
+  int32_t o_ins, e_ins;  /* insertion open/extend                                 */
+  int32_t pen_clip5, pen_clip3;
+  int32_t w;             /* band width                                            */
+  int32_t zdrop;         /* z-dropoff                                             */
+  int8_t mat[25];        /* 5x5 scoring matrix (bwa_fill_scmat, bwa/bwa.c:109-118) */
+  int8_t pad_[3];
+} bwagpu_opt_t;
+
+/* == mem_seed_t (src/bwa_wrapper.h:62-66, bwa/bwamem.c:174-178), 24 bytes */
+typedef struct {
+  int64_t rbeg;
+  int32_t qbeg, len;
+  int32_t score;
+  int32_t pad_;
+} bwagpu_seed_t;
+
+/* == mem_alnreg_t (bwa/bwamem.h:60-79), 88 bytes, same offsets */
+typedef struct {
+  int64_t rb, re;
+  int32_t qb, qe;
+  int32_t rid;
+  int32_t score, truesc, sub, alt_sc, csub, sub_n;
+  int32_t w, seedcov, secondary, secondary_all, seedlen0;
+  uint32_t n_comp_is_alt; /* n_comp:30, is_alt:2 — always 0 from mem_chain2aln */
+  float frac_rep;
+  uint64_t hash;
+} bwagpu_alnreg_t;
+
+/* The parts of bntseq_t (bwa/bntseq.h:55-66) the path reads. */
+typedef struct {
+  int64_t l_pac;
+  int32_t n_seqs;
+  int32_t pad_;
+  const int64_t *ann_offset; /* [n_seqs] bntann1_t.offset */
+  const int32_t *ann_len;    /* [n_seqs] bntann1_t.len    */
+} bwagpu_bns_t;
+
+/*
+ * One read batch (one ChainsRecord, src/Pipeline.h:46-57) in flattened form.
+ * Read r has l_seq = seq_off[r+1]-seq_off[r] nt4 bases (0..4, already
+ * converted in place as bwa_wrapper.cpp:124-125 does), chains
+ * read_chain_off[r] .. read_chain_off[r+1]-1; chain c has seeds
+ * chain_seed_off[c] .. chain_seed_off[c+1]-1 in mem_chain_t order, its
+ * mem_chain_t.rid and .frac_rep.
+ * Output: the regions of read r are written to
+ *   out_regs[chain_seed_off[read_chain_off[r]] + k], k < out_n[r]
+ * (a read never yields more regions than it has seeds), in the order
+ * mem_chain2aln appends them to the read's mem_alnreg_v.
+ */
+typedef struct {
+  int32_t n_reads, n_chains, n_seeds, pad_;
+  int64_t seq_bytes;
+  const int64_t *seq_off;        /* [n_reads+1]  */
+  const uint8_t *seq;            /* [seq_bytes]  */
+  const int32_t *read_chain_off; /* [n_reads+1]  */
+  const int32_t *chain_seed_off; /* [n_chains+1] */
+  const int32_t *chain_rid;      /* [n_chains]   */
+  const float *chain_frac_rep;   /* [n_chains]   */
+  const bwagpu_seed_t *seeds;    /* [n_seeds]    */
+} bwagpu_batch_t;
+
+/* One ksw_extend2 call: query = qpool[qoff..qoff+qlen), target = tpool[toff..toff+tlen). */
+typedef struct {
+  int64_t qoff, toff;
+  int32_t qlen, tlen;
+  int32_t w, end_bonus, zdrop, h0;
+} bwagpu_ext_task_t;
+
+/* ksw_extend2 outputs: return value and *qle,*tle,*gtle,*gscore,*max_off */
+typedef struct {
+  int32_t score, qle, tle, gtle, gscore, max_off;
+} bwagpu_ext_result_t;
+
+/* per-launch statistics of the last finished launch on a slot */
+typedef struct {
+  double kernel_ms;      /* HIP-event time of the extension kernel(s)            */
+  double total_ms;       /* H2D + kernel + D2H wall (submit..wait)               */
+  int64_t cells;         /* evaluated DP cells: sum over executed rows of
+                            (end-beg) exactly as ksw.c:424 counts them            */
+  int64_t rows;          /* executed DP rows                                     */
+  int64_t ext_calls;     /* ksw_extend2-equivalent calls                         */
+  int64_t h2d_bytes, d2h_bytes;
+} bwagpu_stats_t;
+
+typedef struct bwagpu_ctx bwagpu_ctx_t;
+
+int bwagpu_abi_version(void);
+int bwagpu_device_count(int *n);
+
+int bwagpu_create(int device, const bwagpu_opt_t *opt, const bwagpu_bns_t *bns,
+                  const uint8_t *pac_host, bwagpu_ctx_t **ctx);
+int bwagpu_create_resident(int device, const bwagpu_opt_t *opt, const bwagpu_bns_t *bns,
+                           const void *pac_device, bwagpu_ctx_t **ctx);
+int bwagpu_destroy(bwagpu_ctx_t *ctx);
+const char *bwagpu_last_error(const bwagpu_ctx_t *ctx);
+
+/* watchdog for _wait in milliseconds (default 10000, SWTask.cpp:116-122); 0 = none */
+int bwagpu_set_watchdog_ms(bwagpu_ctx_t *ctx, int ms);
+
+int bwagpu_chain2aln_submit(bwagpu_ctx_t *ctx, int slot, const bwagpu_batch_t *batch);
+int bwagpu_chain2aln_wait(bwagpu_ctx_t *ctx, int slot, bwagpu_alnreg_t *out_regs, int32_t *out_n);
+int bwagpu_chain2aln(bwagpu_ctx_t *ctx, const bwagpu_batch_t *batch, bwagpu_alnreg_t *out_regs,
+                     int32_t *out_n);
+/* all pointers in dev_batch / dev_out / dev_n are device pointers; stream is a
+   hipStream_t (NULL = the context's slot-0 stream); asynchronous; dev_stats
+   (device, 4 x int64: cells, rows, ext_calls, error flag) may be NULL */
+int bwagpu_chain2aln_device(bwagpu_ctx_t *ctx, const bwagpu_batch_t *dev_batch,
+                            bwagpu_alnreg_t *dev_out, int32_t *dev_n, int64_t *dev_stats,
+                            void *stream);
+
+int bwagpu_extend_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_ext_task_t *tasks,
+                        const uint8_t *qpool, int64_t qpool_len, const uint8_t *tpool,
+                        int64_t tpool_len, bwagpu_ext_result_t *results);
+
+int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BWAGPU_H */

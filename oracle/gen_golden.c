@@ -1,0 +1,338 @@
+/*
+ * gen_golden.c — TEST INFRASTRUCTURE ONLY: golden-vector generator.
+ *
+ * Linked (Makefile -> _ref/gen_golden) against the REFERENCE's bwa objects
+ * compiled from /root/reference/bwa.  It
+ *   1. writes a synthetic multi-contig reference (iid ACGT + diverged
+ *      interspersed repeats + tandem repeats + N runs) and indexes it with the
+ *      reference's own bwa_idx_build (bwa/bwtindex.c:256),
+ *   2. simulates reads (pairs, ~N(400,40) fragments, 0.8% subs, 0.1% indels,
+ *      some Ns, chimeras, junk and contig-straddling fragments),
+ *   3. seeds + chains each read with the reference's own code exactly as
+ *      bwa-flow's SeqsToChains does (src/bwa_wrapper.cpp:110-113:
+ *      mem_chain -> mem_chain_flt -> mem_flt_chained_seeds),
+ *   4. runs the reference mem_chain2aln (bwa/bwamem.c:641-795) per chain the
+ *      way ChainsToRegions::compute does (src/Pipeline.cpp:514-529), recording
+ *      every ksw_extend2 call through -Wl,--wrap, and
+ *   5. dumps everything as raw little-endian arrays into <outdir>/ for
+ *      gen_golden.py to pack into tests/golden/*.npz.
+ *
+ * usage: gen_golden <outdir> <seed> <n_pairs> <len_mode:150|100|250|mix> <opt_mode:0|1>
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bntseq.h"
+#include "bwa.h"
+#include "bwamem.h"
+#include "bwt.h"
+#include "kvec.h"
+
+typedef struct {
+  int64_t rbeg;
+  int32_t qbeg, len;
+  int score;
+} seed_t;
+typedef struct {
+  int n, m, first, rid;
+  uint32_t w : 29, kept : 2, is_alt : 1;
+  float frac_rep;
+  int64_t pos;
+  seed_t *seeds;
+} chain_t; /* == mem_chain_t, bwamem.c:180-186 */
+typedef struct { size_t n, m; chain_t *a; } chain_v;
+
+chain_v mem_chain(const mem_opt_t *opt, const bwt_t *bwt, const bntseq_t *bns, int len,
+                  const uint8_t *seq, void *buf);
+int mem_chain_flt(const mem_opt_t *opt, int n_chn, chain_t *a);
+void mem_flt_chained_seeds(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, int l_query,
+                           const uint8_t *query, int n_chn, chain_t *a);
+void mem_chain2aln(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, int l_query,
+                   const uint8_t *query, const chain_t *c, mem_alnreg_v *av);
+int bwa_idx_build(const char *fa, const char *prefix, int algo_type, int block_size);
+
+/* ---------------- RNG (splitmix64) ---------------- */
+static uint64_t rng_s;
+static uint64_t rnd(void)
+{
+  uint64_t z = (rng_s += 0x9e3779b97f4a7c15ULL);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+static double urand(void) { return (rnd() >> 11) * (1.0 / 9007199254740992.0); }
+static int irand(int n) { return (int)(urand() * n); }
+static double nrand(void)
+{
+  double u = urand() + 1e-300, v = urand();
+  return sqrt(-2 * log(u)) * cos(2 * M_PI * v);
+}
+
+/* ---------------- ksw_extend2 recorder ---------------- */
+typedef struct { int32_t qlen, tlen, w, end_bonus, zdrop, h0; int64_t qoff, toff; } rtask_t;
+typedef struct { int32_t score, qle, tle, gtle, gscore, max_off; } rres_t;
+static kvec_t(rtask_t) g_tasks;
+static kvec_t(rres_t) g_res;
+static kvec_t(uint8_t) g_qpool, g_tpool;
+static int g_rec = 1;
+
+int __real_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
+                       const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                       int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle, int *gscore,
+                       int *max_off);
+int __wrap_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
+                       const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                       int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle, int *gscore,
+                       int *max_off)
+{
+  int r = __real_ksw_extend2(qlen, query, tlen, target, m, mat, o_del, e_del, o_ins, e_ins, w,
+                             end_bonus, zdrop, h0, qle, tle, gtle, gscore, max_off);
+  if (g_rec) {
+    rtask_t t = {qlen, tlen, w, end_bonus, zdrop, h0, (int64_t)g_qpool.n, (int64_t)g_tpool.n};
+    rres_t o = {r, *qle, *tle, *gtle, *gscore, *max_off};
+    for (int i = 0; i < qlen; ++i) kv_push(uint8_t, g_qpool, query[i]);
+    for (int i = 0; i < tlen; ++i) kv_push(uint8_t, g_tpool, target[i]);
+    kv_push(rtask_t, g_tasks, t);
+    kv_push(rres_t, g_res, o);
+  }
+  return r;
+}
+
+/* ---------------- reference genome ---------------- */
+static const char ACGT[] = "ACGT";
+
+static char *make_genome(int n_ctg, const int *ctg_len, int64_t *total)
+{
+  int64_t L = 0;
+  for (int i = 0; i < n_ctg; ++i) L += ctg_len[i];
+  char *g = (char *)malloc(L + 1);
+  for (int64_t i = 0; i < L; ++i) g[i] = ACGT[rnd() & 3];
+  /* interspersed repeats: 40 copies of 10 families, 1% diverged */
+  for (int fam = 0; fam < 10; ++fam) {
+    int len = 300 + irand(2700);
+    int64_t src = (int64_t)(urand() * (L - len));
+    for (int c = 0; c < 4; ++c) {
+      int64_t dst = (int64_t)(urand() * (L - len));
+      for (int k = 0; k < len; ++k) g[dst + k] = urand() < 0.01 ? ACGT[rnd() & 3] : g[src + k];
+    }
+  }
+  /* tandem repeats */
+  for (int t = 0; t < 30; ++t) {
+    int per = 2 + irand(49), len = 200 + irand(800);
+    int64_t dst = (int64_t)(urand() * (L - len));
+    for (int k = per; k < len; ++k) g[dst + k] = urand() < 0.005 ? ACGT[rnd() & 3] : g[dst + k - per];
+  }
+  /* N runs (bwa turns them into random bases + holes, bntseq.c:261) */
+  for (int t = 0; t < 12; ++t) {
+    int len = 10 + irand(300);
+    int64_t dst = (int64_t)(urand() * (L - len));
+    memset(g + dst, 'N', len);
+  }
+  g[L] = 0;
+  *total = L;
+  return g;
+}
+
+static int nt4(char c)
+{
+  switch (c) {
+    case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3;
+    default: return 4;
+  }
+}
+static char comp(char c)
+{
+  switch (c) {
+    case 'A': return 'T'; case 'C': return 'G'; case 'G': return 'C'; case 'T': return 'A';
+    default: return 'N';
+  }
+}
+
+/* copy `len` bases of g starting at p (forward) with errors into out; returns length */
+static int mutate(const char *src, int n, char *out, int cap)
+{
+  int o = 0;
+  for (int i = 0; i < n && o < cap; ++i) {
+    double u = urand();
+    if (u < 0.0005) out[o++] = 'N';
+    else if (u < 0.0005 + 0.008) { char c; do c = ACGT[rnd() & 3]; while (c == src[i]); out[o++] = c; }
+    else if (u < 0.0005 + 0.008 + 0.0005) { /* deletion of 1-3 */
+      i += irand(3);
+    } else if (u < 0.0005 + 0.008 + 0.001) { /* insertion of 1-3 then the base */
+      int k = 1 + irand(3);
+      while (k-- && o < cap) out[o++] = ACGT[rnd() & 3];
+      if (o < cap) out[o++] = src[i];
+    } else out[o++] = src[i];
+  }
+  return o;
+}
+
+static void wr(const char *dir, const char *name, const void *p, size_t sz)
+{
+  char fn[4096];
+  snprintf(fn, sizeof fn, "%s/%s.bin", dir, name);
+  FILE *f = fopen(fn, "wb");
+  if (!f) { perror(fn); exit(1); }
+  if (sz && fwrite(p, 1, sz, f) != sz) { perror(fn); exit(1); }
+  fclose(f);
+}
+
+int main(int argc, char *argv[])
+{
+  if (argc < 6) {
+    fprintf(stderr, "usage: gen_golden <outdir> <seed> <n_pairs> <150|100|250|mix> <opt_mode>\n");
+    return 1;
+  }
+  const char *dir = argv[1];
+  rng_s = strtoull(argv[2], 0, 10);
+  int n_pairs = atoi(argv[3]);
+  const char *lm = argv[4];
+  int opt_mode = atoi(argv[5]);
+  char fa[4096];
+  int ctg_len[3] = {500000, 300000, 200000};
+  int64_t G;
+
+  bwa_verbose = 1;
+  uint64_t read_seed = rng_s;
+  rng_s = 1234; /* the genome is the same for every fixture */
+  char *g = make_genome(3, ctg_len, &G);
+  rng_s = read_seed;
+  snprintf(fa, sizeof fa, "%s/ref.fa", dir);
+  FILE *f = fopen(fa, "w");
+  int64_t off = 0;
+  for (int c = 0; c < 3; ++c) {
+    fprintf(f, ">chr%d\n", c + 1);
+    for (int64_t i = 0; i < ctg_len[c]; i += 60) {
+      int64_t n = ctg_len[c] - i < 60 ? ctg_len[c] - i : 60;
+      fwrite(g + off + i, 1, n, f);
+      fputc('\n', f);
+    }
+    off += ctg_len[c];
+  }
+  fclose(f);
+  bwa_idx_build(fa, fa, BWTALGO_AUTO, 10000000);
+  bwaidx_t *idx = bwa_idx_load(fa, BWA_IDX_ALL);
+  if (!idx) { fprintf(stderr, "index load failed\n"); return 1; }
+
+  mem_opt_t *opt = mem_opt_init();
+  if (opt_mode == 1) { /* non-default scoring exercises every opt field */
+    opt->a = 2; opt->b = 5; opt->o_del = 7; opt->e_del = 2; opt->o_ins = 5; opt->e_ins = 3;
+    opt->w = 30; opt->zdrop = 40; opt->pen_clip5 = 3; opt->pen_clip3 = 9;
+    bwa_fill_scmat(opt->a, opt->b, opt->mat);
+  } else if (opt_mode == 2) { /* small band + aggressive z-drop: retries and breaks */
+    opt->w = 8; opt->zdrop = 15; opt->pen_clip5 = opt->pen_clip3 = 1;
+  }
+
+  kvec_t(int64_t) seq_off;
+  kvec_t(uint8_t) seq;
+  kvec_t(int32_t) rco, cso, crid, nreg;
+  kvec_t(float) cfr;
+  kvec_t(seed_t) seeds;
+  kvec_t(mem_alnreg_t) regs;
+  kv_init(seq_off); kv_init(seq); kv_init(rco); kv_init(cso); kv_init(crid); kv_init(cfr);
+  kv_init(seeds); kv_init(regs); kv_init(nreg);
+  kv_push(int64_t, seq_off, 0);
+  kv_push(int32_t, rco, 0);
+  kv_push(int32_t, cso, 0);
+
+  char *buf = (char *)malloc(4096), *frag = (char *)malloc(8192);
+  for (int p = 0; p < n_pairs; ++p) {
+    int L;
+    if (!strcmp(lm, "mix")) L = (int[]){100, 150, 250}[p % 3];
+    else L = atoi(lm);
+    int fl = (int)(400 + 40 * nrand());
+    if (fl < L + 10) fl = L + 10;
+    if (fl > 4000) fl = 4000;
+    int64_t pos;
+    if (urand() < 0.02) { /* straddle / hug a contig junction */
+      int c = irand(2);
+      int64_t j = 0;
+      for (int k = 0; k <= c; ++k) j += ctg_len[k];
+      pos = j - irand(fl);
+    } else pos = (int64_t)(urand() * (G - fl));
+    if (pos < 0) pos = 0;
+    if (pos + fl > G) pos = G - fl;
+    memcpy(frag, g + pos, fl);
+    int strand = rnd() & 1;
+    for (int e = 0; e < 2; ++e) {
+      int n;
+      double kind = urand();
+      if (kind < 0.005) { /* junk read: no chains */
+        n = L;
+        for (int i = 0; i < n; ++i) buf[i] = ACGT[rnd() & 3];
+      } else {
+        char tmp[4096];
+        int fwd = (e == 0) ^ strand;
+        if (fwd) memcpy(tmp, frag, L);
+        else for (int i = 0; i < L; ++i) tmp[i] = comp(frag[fl - 1 - i]);
+        if (kind < 0.015) { /* chimera: second half from elsewhere */
+          int64_t q = (int64_t)(urand() * (G - L));
+          memcpy(tmp + L / 2, g + q, L - L / 2);
+        }
+        n = mutate(tmp, L, buf, L + 16);
+        if (n > L) n = L;
+      }
+      uint8_t q[4096];
+      for (int i = 0; i < n; ++i) q[i] = (uint8_t)nt4(buf[i]);
+      for (int i = 0; i < n; ++i) kv_push(uint8_t, seq, q[i]);
+      kv_push(int64_t, seq_off, (int64_t)seq.n);
+
+      g_rec = 0;
+      chain_v chn = mem_chain(opt, idx->bwt, idx->bns, n, q, 0);
+      chn.n = mem_chain_flt(opt, (int)chn.n, chn.a);
+      mem_flt_chained_seeds(opt, idx->bns, idx->pac, n, q, (int)chn.n, chn.a);
+      g_rec = 1;
+      mem_alnreg_v av;
+      kv_init(av);
+      for (size_t c = 0; c < chn.n; ++c) {
+        chain_t *ch = &chn.a[c];
+        for (int s = 0; s < ch->n; ++s) kv_push(seed_t, seeds, ch->seeds[s]);
+        kv_push(int32_t, cso, (int32_t)seeds.n);
+        kv_push(int32_t, crid, ch->rid);
+        kv_push(float, cfr, ch->frac_rep);
+        mem_chain2aln(opt, idx->bns, idx->pac, n, q, ch, &av);
+        free(ch->seeds);
+      }
+      free(chn.a);
+      kv_push(int32_t, rco, (int32_t)crid.n);
+      kv_push(int32_t, nreg, (int32_t)av.n);
+      for (size_t k = 0; k < av.n; ++k) kv_push(mem_alnreg_t, regs, av.a[k]);
+      free(av.a);
+    }
+  }
+
+  /* opt in bwagpu_opt_t order */
+  int32_t ov[10] = {opt->a, opt->b, opt->o_del, opt->e_del, opt->o_ins, opt->e_ins,
+                    opt->pen_clip5, opt->pen_clip3, opt->w, opt->zdrop};
+  wr(dir, "opt_int", ov, sizeof ov);
+  wr(dir, "opt_mat", opt->mat, 25);
+  int64_t lp = idx->bns->l_pac;
+  wr(dir, "l_pac", &lp, 8);
+  int64_t *aoff = (int64_t *)malloc(8 * idx->bns->n_seqs);
+  int32_t *alen = (int32_t *)malloc(4 * idx->bns->n_seqs);
+  for (int i = 0; i < idx->bns->n_seqs; ++i) { aoff[i] = idx->bns->anns[i].offset; alen[i] = idx->bns->anns[i].len; }
+  wr(dir, "ann_offset", aoff, 8 * idx->bns->n_seqs);
+  wr(dir, "ann_len", alen, 4 * idx->bns->n_seqs);
+  wr(dir, "pac", idx->pac, (size_t)(lp / 4 + 1));
+  wr(dir, "seq_off", seq_off.a, 8 * seq_off.n);
+  wr(dir, "seq", seq.a, seq.n);
+  wr(dir, "read_chain_off", rco.a, 4 * rco.n);
+  wr(dir, "chain_seed_off", cso.a, 4 * cso.n);
+  wr(dir, "chain_rid", crid.a, 4 * crid.n);
+  wr(dir, "chain_frac_rep", cfr.a, 4 * cfr.n);
+  wr(dir, "seeds", seeds.a, sizeof(seed_t) * seeds.n);
+  wr(dir, "reg_n", nreg.a, 4 * nreg.n);
+  wr(dir, "regs", regs.a, sizeof(mem_alnreg_t) * regs.n);
+  wr(dir, "tasks", g_tasks.a, sizeof(rtask_t) * g_tasks.n);
+  wr(dir, "task_res", g_res.a, sizeof(rres_t) * g_res.n);
+  wr(dir, "qpool", g_qpool.a, g_qpool.n);
+  wr(dir, "tpool", g_tpool.a, g_tpool.n);
+  fprintf(stderr, "[gen_golden] reads=%zu chains=%zu seeds=%zu regions=%zu ksw_calls=%zu sizeof(alnreg)=%zu\n",
+          seq_off.n - 1, crid.n, seeds.n, regs.n, g_tasks.n, sizeof(mem_alnreg_t));
+  bwa_idx_destroy(idx);
+  free(opt);
+  free(g);
+  return 0;
+}

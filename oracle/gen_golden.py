@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""TEST INFRASTRUCTURE ONLY — regenerate tests/golden/*.npz from the reference.
+
+Runs oracle/_ref/gen_golden (the reference's own bwa C: index, seeding,
+chaining, mem_chain2aln, ksw_extend2 — see gen_golden.c) and the reference
+ksw_extend2 on randomised edge-case tasks (via oracle/_ref/libbwaref.so), and
+packs inputs + reference outputs as numpy .npz fixtures (no pickles).
+
+    make -C oracle && python oracle/gen_golden.py
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.normpath(os.path.join(HERE, ".."))
+GOLD = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, HERE)
+import oracle  # noqa: E402
+from oracle import abi  # noqa: E402
+
+RTASK = np.dtype([("qlen", "<i4"), ("tlen", "<i4"), ("w", "<i4"), ("end_bonus", "<i4"), ("zdrop", "<i4"),
+                  ("h0", "<i4"), ("qoff", "<i8"), ("toff", "<i8")])
+
+# name -> (read seed, pairs, read-length mode, opt mode)
+CHAIN_SETS = {
+    "c1_default": (42, 1000, "150", 0),
+    "c5_mixed": (7, 450, "mix", 0),
+    "opt1_scoring": (11, 400, "150", 1),
+    "opt2_band": (13, 400, "150", 2),
+}
+N_TASKS_KEEP = 1200
+
+
+def rd(d, name, dt):
+    return np.fromfile(os.path.join(d, name + ".bin"), dtype=dt)
+
+
+def subsample_tasks(tasks, res, qpool, tpool, n, rng):
+    idx = np.sort(rng.choice(len(tasks), size=min(n, len(tasks)), replace=False))
+    out_t = np.zeros(len(idx), abi.EXT_TASK_DTYPE)
+    qs, ts, qo, to = [], [], 0, 0
+    for k, i in enumerate(idx):
+        t = tasks[i]
+        qs.append(qpool[t["qoff"]:t["qoff"] + t["qlen"]])
+        ts.append(tpool[t["toff"]:t["toff"] + t["tlen"]])
+        out_t[k] = (qo, to, t["qlen"], t["tlen"], t["w"], t["end_bonus"], t["zdrop"], t["h0"])
+        qo += int(t["qlen"])
+        to += int(t["tlen"])
+    r = np.zeros(len(idx), abi.EXT_RES_DTYPE)
+    for f in abi.EXT_RES_DTYPE.names:
+        r[f] = res[f][idx]
+    return out_t, r, np.concatenate(qs).astype(np.uint8), np.concatenate(ts).astype(np.uint8)
+
+
+def gen_chain_set(name, seed, pairs, lm, om, tmp, rng):
+    d = os.path.join(tmp, name)
+    os.makedirs(d, exist_ok=True)
+    subprocess.run([os.path.join(HERE, "_ref", "gen_golden"), d, str(seed), str(pairs), lm, str(om)], check=True)
+    oi = rd(d, "opt_int", np.int32)
+    opt = dict(zip(["a", "b", "o_del", "e_del", "o_ins", "e_ins", "pen_clip5", "pen_clip3", "w", "zdrop"],
+                   oi.tolist()))
+    mat = rd(d, "opt_mat", np.int8)
+    ref = dict(l_pac=rd(d, "l_pac", np.int64), ann_offset=rd(d, "ann_offset", np.int64),
+               ann_len=rd(d, "ann_len", np.int32), pac=rd(d, "pac", np.uint8))
+    tasks = rd(d, "tasks", RTASK)
+    res = rd(d, "task_res", abi.EXT_RES_DTYPE)
+    t2, r2, q2, tp2 = subsample_tasks(tasks, res, rd(d, "qpool", np.uint8), rd(d, "tpool", np.uint8),
+                                      N_TASKS_KEEP, rng)
+    np.savez_compressed(
+        os.path.join(GOLD, name + ".npz"),
+        opt_int=oi, opt_mat=mat,
+        seq_off=rd(d, "seq_off", np.int64), seq=rd(d, "seq", np.uint8),
+        read_chain_off=rd(d, "read_chain_off", np.int32), chain_seed_off=rd(d, "chain_seed_off", np.int32),
+        chain_rid=rd(d, "chain_rid", np.int32), chain_frac_rep=rd(d, "chain_frac_rep", np.float32),
+        seeds=rd(d, "seeds", abi.SEED_DTYPE), reg_n=rd(d, "reg_n", np.int32), regs=rd(d, "regs", abi.ALNREG_DTYPE),
+        tasks=t2, task_res=r2, qpool=q2, tpool=tp2)
+    print(f"[gen_golden] {name}: reads={len(rd(d, 'seq_off', np.int64)) - 1} regions={len(rd(d, 'regs', abi.ALNREG_DTYPE))} "
+          f"tasks kept={len(t2)}/{len(tasks)}")
+    return opt, mat, ref
+
+
+def edge_tasks(rng, n, allow_t5):
+    """randomised ksw_extend2 calls covering the corners of ksw.c:380-479"""
+    tasks = np.zeros(n, abi.EXT_TASK_DTYPE)
+    qs, ts, qo, to = [], [], 0, 0
+    special_q = [0, 1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 159, 160, 161, 255, 256, 257, 511, 700, 1022]
+    for k in range(n):
+        u = rng.random()
+        if u < 0.25:
+            ql = int(rng.choice(special_q))
+        elif u < 0.8:
+            ql = int(rng.integers(1, 160))
+        else:
+            ql = int(rng.integers(1, 300))
+        q = rng.integers(0, 4, ql).astype(np.uint8)
+        if rng.random() < 0.3 and ql:
+            q[rng.random(ql) < 0.03] = 4
+        mode = rng.random()
+        if mode < 0.15:
+            tl = int(rng.integers(0, 4))
+            t = rng.integers(0, 4, tl).astype(np.uint8)
+        elif mode < 0.3:
+            tl = int(rng.integers(0, 400))
+            t = rng.integers(0, 4, tl).astype(np.uint8)
+        else:  # a diverged copy of the query, with indels and a random tail
+            t = []
+            for b in q:
+                x = rng.random()
+                if x < 0.02:
+                    continue
+                if x < 0.04:
+                    t.extend(rng.integers(0, 4, int(rng.integers(1, 4))).tolist())
+                t.append(int(rng.integers(0, 4)) if (b == 4 or rng.random() < 0.03) else int(b))
+            t.extend(rng.integers(0, 4, int(rng.integers(0, 120))).tolist())
+            if rng.random() < 0.15 and len(t) > 20:  # a junk middle triggers z-drop
+                a = int(rng.integers(5, len(t) - 5))
+                t[a:a + 40] = rng.integers(0, 4, 40).tolist()
+            t = np.array(t, np.uint8)
+            tl = len(t)
+        if allow_t5 and tl and rng.random() < 0.2:
+            t[rng.random(tl) < 0.05] = 4
+        w = int(rng.choice([1, 2, 5, 10, 30, 100, 200, 300]))
+        zd = int(rng.choice([0, 0, 5, 20, 100, 200]))
+        eb = int(rng.integers(0, 11))
+        h0 = int(rng.choice([1, 2, 5, 19, 30, 60, 150, 300]))
+        tasks[k] = (qo, to, ql, tl, w, eb, zd, h0)
+        qs.append(q)
+        ts.append(t)
+        qo += ql
+        to += tl
+    return tasks, np.concatenate(qs).astype(np.uint8), np.concatenate(ts).astype(np.uint8)
+
+
+def main():
+    if oracle.ref_lib() is None or not os.path.exists(os.path.join(HERE, "_ref", "gen_golden")):
+        sys.exit("build the reference first: make -C oracle")
+    os.makedirs(GOLD, exist_ok=True)
+    rng = np.random.default_rng(2024)
+    with tempfile.TemporaryDirectory() as tmp:
+        ref = None
+        for name, (seed, pairs, lm, om) in CHAIN_SETS.items():
+            _, _, ref = gen_chain_set(name, seed, pairs, lm, om, tmp, rng)
+        np.savez_compressed(os.path.join(GOLD, "ref.npz"), **ref)
+    # ksw_extend2 edge cases through the reference's own ksw_extend2
+    opts = {
+        "ksw_edge_default": abi.default_opt(),
+        "ksw_edge_scoring": dict(a=2, b=5, o_del=7, e_del=2, o_ins=5, e_ins=3, pen_clip5=3, pen_clip3=9, w=30,
+                                 zdrop=40, mat=abi.fill_scmat(2, 5)),
+        "ksw_edge_matrix": dict(a=3, b=2, o_del=4, e_del=1, o_ins=9, e_ins=2, pen_clip5=0, pen_clip3=0, w=50,
+                                zdrop=60, mat=np.array([3, -2, -1, -2, -1, -2, 2, -2, -1, 0, -1, -2, 4, -3, -2,
+                                                        -2, -1, -3, 3, -1, -1, 0, -2, -1, 1], np.int8)),
+    }
+    for name, opt in opts.items():
+        tasks, qp, tp = edge_tasks(rng, 1500, allow_t5=True)
+        res, _ = oracle.extend("ref", opt, tasks, qp, tp)
+        np.savez_compressed(os.path.join(GOLD, name + ".npz"),
+                            opt_int=np.array([opt[k] for k in ("a", "b", "o_del", "e_del", "o_ins", "e_ins",
+                                                               "pen_clip5", "pen_clip3", "w", "zdrop")], np.int32),
+                            opt_mat=np.asarray(opt["mat"], np.int8), tasks=tasks, task_res=res, qpool=qp, tpool=tp)
+        print(f"[gen_golden] {name}: tasks={len(tasks)} q={len(qp)} t={len(tp)}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes access to the CPU checkers.
+
+  liboracle.so         our clean-room C restatement (oracle/ksw_ext.c, chain2aln.c)
+  _ref/libbwaref.so    the reference's own bwa C (compiled from /root/reference/bwa
+                       by oracle/Makefile) behind ref_shim.c
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module.  The product (bwa-flow_amd/) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "bwa-flow_amd", "python"))
+from bwagpu import abi  # noqa: E402  (record dtypes / ABI structs only)
+from bwagpu.engine import Batch, _ptr  # noqa: E402
+
+_VP = C.c_void_p
+_libs: dict = {}
+
+
+def _load(name: str, path: str):
+    if name in _libs:
+        return _libs[name]
+    if not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    _libs[name] = lib
+    return lib
+
+
+def oracle_lib():
+    lib = _load("oracle", os.path.join(HERE, "liboracle.so"))
+    if lib is None:
+        raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle`")
+    lib.oracle_chain2aln_batch.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, C.POINTER(abi.BatchC),
+                                           _VP, _VP, C.c_int, _VP]
+    lib.oracle_chain2aln_batch.restype = C.c_int
+    lib.oracle_extend_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
+    lib.oracle_extend_batch.restype = C.c_int
+    return lib
+
+
+def ref_lib():
+    """the reference's own code, or None when _ref/ was not built/shipped"""
+    lib = _load("ref", os.path.join(HERE, "_ref", "libbwaref.so"))
+    if lib is None:
+        return None
+    lib.ref_chain2aln_batch.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, C.POINTER(abi.BatchC),
+                                        _VP, _VP, C.c_int]
+    lib.ref_chain2aln_batch.restype = C.c_int
+    lib.ref_extend_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP]
+    lib.ref_extend_batch.restype = C.c_int
+    lib.ref_abi_check.restype = C.c_int
+    return lib
+
+
+class Ref:
+    """reference genome in bwa's form: forward 2-bit pac + contig table"""
+
+    def __init__(self, l_pac, ann_offset, ann_len, pac):
+        self.l_pac = int(l_pac)
+        self.ann_offset = np.ascontiguousarray(ann_offset, np.int64)
+        self.ann_len = np.ascontiguousarray(ann_len, np.int32)
+        self.pac = np.ascontiguousarray(pac, np.uint8)
+        self.bns = abi.Bns(self.l_pac, len(self.ann_offset), 0, _ptr(self.ann_offset), _ptr(self.ann_len))
+
+
+def chain2aln(which: str, opt: dict, ref: Ref, batch: Batch, n_threads: int = 1):
+    """CPU mem_chain2aln over a batch -> (regs, n, stats[cells, rows, calls] or None)"""
+    o = abi.opt_from_dict(opt)
+    regs = np.zeros(max(batch.n_seeds, 1), abi.ALNREG_DTYPE)
+    n = np.zeros(max(batch.n_reads, 1), np.int32)
+    bc = batch.to_c()
+    if which == "oracle":
+        st = np.zeros(3, np.int64)
+        rc = oracle_lib().oracle_chain2aln_batch(C.byref(o), C.byref(ref.bns), _ptr(ref.pac), C.byref(bc),
+                                                 _ptr(regs), _ptr(n), n_threads, _ptr(st))
+    elif which == "ref":
+        lib = ref_lib()
+        if lib is None:
+            raise RuntimeError("oracle/_ref/libbwaref.so not available")
+        st = None
+        rc = lib.ref_chain2aln_batch(C.byref(o), C.byref(ref.bns), _ptr(ref.pac), C.byref(bc), _ptr(regs),
+                                     _ptr(n), n_threads)
+    else:
+        raise ValueError(which)
+    if rc != 0:
+        raise RuntimeError(f"{which} chain2aln failed rc={rc}")
+    return regs[:batch.n_seeds], n[:batch.n_reads], st
+
+
+def extend(which: str, opt: dict, tasks, qpool, tpool):
+    o = abi.opt_from_dict(opt)
+    tasks = np.ascontiguousarray(tasks, abi.EXT_TASK_DTYPE)
+    qpool = np.ascontiguousarray(qpool, np.uint8)
+    tpool = np.ascontiguousarray(tpool, np.uint8)
+    res = np.zeros(max(len(tasks), 1), abi.EXT_RES_DTYPE)
+    if which == "oracle":
+        cells = np.zeros(2, np.int64)
+        oracle_lib().oracle_extend_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool),
+                                         _ptr(res), _ptr(cells))
+        return res[:len(tasks)], cells
+    lib = ref_lib()
+    if lib is None:
+        raise RuntimeError("oracle/_ref/libbwaref.so not available")
+    lib.ref_extend_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool), _ptr(res))
+    return res[:len(tasks)], None

@@ -1,0 +1,142 @@
+/*
+ * ref_shim.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * Batch shim over the REFERENCE's own mem_chain2aln / ksw_extend2, compiled
+ * from /root/reference/bwa (see Makefile: _ref/libbwaref.so).  It exposes the
+ * same flattened-batch signature as oracle_chain2aln_batch so that tests can
+ * check the restatement (liboracle.so) and the GPU path against the real
+ * reference, and bench.py can time the reference on the host as the
+ * cpu_baseline ("kind": "reference").
+ *
+ * Per read it does exactly what ChainsToRegions::compute does
+ * (src/Pipeline.cpp:511-530): kv_init the read's mem_alnreg_v and call
+ * mem_chain2aln for each of its chains in order.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bntseq.h"
+#include "bwamem.h"
+#include "ksw.h"
+#include "kvec.h"
+#include "bwagpu.h"
+
+/* mem_chain_t / mem_chain_v are private to bwamem.c (bwamem.c:180-188);
+   this is the same declaration bwa-flow makes in src/bwa_wrapper.h:68-80 */
+typedef struct {
+  int n, m, first, rid;
+  uint32_t w : 29, kept : 2, is_alt : 1;
+  float frac_rep;
+  int64_t pos;
+  bwagpu_seed_t *seeds; /* layout-identical to mem_seed_t */
+} ref_chain_t;
+
+void mem_chain2aln(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, int l_query,
+                   const uint8_t *query, const ref_chain_t *c, mem_alnreg_v *av);
+
+int ref_abi_check(void) { return (int)(sizeof(mem_alnreg_t) * 1000 + sizeof(bwagpu_seed_t)); }
+
+static void fill_opt(const bwagpu_opt_t *o, mem_opt_t *mo)
+{
+  mem_opt_t *d = mem_opt_init();
+  *mo = *d;
+  free(d);
+  mo->a = o->a; mo->b = o->b;
+  mo->o_del = o->o_del; mo->e_del = o->e_del;
+  mo->o_ins = o->o_ins; mo->e_ins = o->e_ins;
+  mo->pen_clip5 = o->pen_clip5; mo->pen_clip3 = o->pen_clip3;
+  mo->w = o->w; mo->zdrop = o->zdrop;
+  memcpy(mo->mat, o->mat, 25);
+}
+
+typedef struct {
+  const mem_opt_t *opt;
+  const bntseq_t *bns;
+  const uint8_t *pac;
+  const bwagpu_batch_t *b;
+  bwagpu_alnreg_t *out;
+  int32_t *out_n;
+  int r0, r1;
+} rjob_t;
+
+static void *rjob(void *arg)
+{
+  rjob_t *J = (rjob_t *)arg;
+  const bwagpu_batch_t *b = J->b;
+  for (int r = J->r0; r < J->r1; ++r) {
+    mem_alnreg_v av;
+    int c0 = b->read_chain_off[r], c1 = b->read_chain_off[r + 1];
+    int lq = (int)(b->seq_off[r + 1] - b->seq_off[r]);
+    kv_init(av);
+    for (int c = c0; c < c1; ++c) {
+      ref_chain_t ch;
+      memset(&ch, 0, sizeof(ch));
+      ch.n = ch.m = b->chain_seed_off[c + 1] - b->chain_seed_off[c];
+      ch.rid = b->chain_rid[c];
+      ch.frac_rep = b->chain_frac_rep[c];
+      ch.seeds = (bwagpu_seed_t *)(b->seeds + b->chain_seed_off[c]);
+      mem_chain2aln(J->opt, J->bns, J->pac, lq, b->seq + b->seq_off[r], &ch, &av);
+    }
+    memcpy(J->out + b->chain_seed_off[c0], av.a, av.n * sizeof(mem_alnreg_t));
+    J->out_n[r] = (int32_t)av.n;
+    free(av.a);
+  }
+  return 0;
+}
+
+int ref_chain2aln_batch(const bwagpu_opt_t *o, const bwagpu_bns_t *gb, const uint8_t *pac,
+                        const bwagpu_batch_t *batch, bwagpu_alnreg_t *out_regs, int32_t *out_n,
+                        int n_threads)
+{
+  mem_opt_t opt;
+  bntseq_t bns;
+  bntann1_t *anns;
+  int nt = n_threads < 1 ? 1 : n_threads;
+  rjob_t *jobs;
+  pthread_t *th;
+
+  fill_opt(o, &opt);
+  memset(&bns, 0, sizeof(bns));
+  bns.l_pac = gb->l_pac;
+  bns.n_seqs = gb->n_seqs;
+  anns = (bntann1_t *)calloc((size_t)gb->n_seqs, sizeof(bntann1_t));
+  for (int i = 0; i < gb->n_seqs; ++i) {
+    anns[i].offset = gb->ann_offset[i];
+    anns[i].len = gb->ann_len[i];
+    anns[i].name = (char *)"ref";
+  }
+  bns.anns = anns;
+
+  if (nt > batch->n_reads) nt = batch->n_reads > 0 ? batch->n_reads : 1;
+  jobs = (rjob_t *)calloc((size_t)nt, sizeof(rjob_t));
+  th = (pthread_t *)calloc((size_t)nt, sizeof(pthread_t));
+  for (int t = 0; t < nt; ++t) {
+    jobs[t].opt = &opt; jobs[t].bns = &bns; jobs[t].pac = pac; jobs[t].b = batch;
+    jobs[t].out = out_regs; jobs[t].out_n = out_n;
+    jobs[t].r0 = (int)((int64_t)batch->n_reads * t / nt);
+    jobs[t].r1 = (int)((int64_t)batch->n_reads * (t + 1) / nt);
+  }
+  if (nt == 1) rjob(&jobs[0]);
+  else {
+    for (int t = 0; t < nt; ++t) pthread_create(&th[t], 0, rjob, &jobs[t]);
+    for (int t = 0; t < nt; ++t) pthread_join(th[t], 0);
+  }
+  free(jobs);
+  free(th);
+  free(anns);
+  return 0;
+}
+
+int ref_extend_batch(const bwagpu_opt_t *o, int32_t n_tasks, const bwagpu_ext_task_t *tasks,
+                     const uint8_t *qpool, const uint8_t *tpool, bwagpu_ext_result_t *results)
+{
+  for (int32_t k = 0; k < n_tasks; ++k) {
+    const bwagpu_ext_task_t *t = &tasks[k];
+    bwagpu_ext_result_t *r = &results[k];
+    r->score = ksw_extend2(t->qlen, qpool + t->qoff, t->tlen, tpool + t->toff, 5, o->mat, o->o_del,
+                           o->e_del, o->o_ins, o->e_ins, t->w, t->end_bonus, t->zdrop, t->h0,
+                           &r->qle, &r->tle, &r->gtle, &r->gscore, &r->max_off);
+  }
+  return 0;
+}

@@ -1,0 +1,161 @@
+"""GPU parity: the HIP engine, called through its C ABI, reproduces the
+reference bit for bit.
+
+* golden chain sets (reference seeding + mem_chain2aln): every mem_alnreg_t
+  byte, region order and per-read count
+* recorded + randomised ksw_extend2 calls: all six outputs
+* the double-buffered submit/wait slots, the device-pointer entry, empty and
+  ragged batches, and the reference's error conditions
+* larger synthetic batches against the oracle (same seeded inputs)
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import golden_io as G
+import oracle
+from bwagpu import abi
+from bwagpu.engine import Batch, BwaGpuError, Engine, compact
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def refd():
+    return G.load_ref()
+
+
+def make_engine(refd, opt):
+    return Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
+
+
+@pytest.mark.parametrize("name", G.CHAIN_SETS)
+def test_chain_sets_bit_exact(refd, name):
+    opt, batch, want, want_n = G.load_chain_set(name)
+    eng = make_engine(refd, opt)
+    regs, n = eng.chain2aln(batch)
+    assert np.array_equal(n, want_n), f"{int((n != want_n).sum())} reads with a different region count"
+    assert G.region_mismatch(compact(batch, regs, n), want) is None
+    st = eng.last_stats()
+    assert st["cells"] > 0 and st["kernel_ms"] > 0
+    eng.close()
+
+
+@pytest.mark.parametrize("name", G.CHAIN_SETS + G.KSW_SETS)
+def test_ksw_extend2_tasks_bit_exact(refd, name):
+    opt, tasks, want, qp, tp = G.load_tasks(name)
+    eng = make_engine(refd, opt)
+    got = eng.extend_batch(tasks, qp, tp)
+    g, w = got.view(np.int32).reshape(-1, 6), want.view(np.int32).reshape(-1, 6)
+    bad = np.nonzero((g != w).any(axis=1))[0]
+    assert len(bad) == 0, f"{len(bad)} tasks differ; first {tasks[bad[0]]}: got {got[bad[0]]} want {want[bad[0]]}"
+    # the evaluated-cell count agrees with the oracle's count of ksw.c:424 iterations
+    _, cells = oracle.extend("oracle", opt, tasks, qp, tp)
+    st = eng.last_stats()
+    assert st["cells"] == cells[0] and st["rows"] == cells[1]
+    eng.close()
+
+
+def test_cell_and_call_counts_match_oracle(refd):
+    opt, batch, _, _ = G.load_chain_set("c1_default")
+    eng = make_engine(refd, opt)
+    eng.chain2aln(batch)
+    st = eng.last_stats()
+    ref = oracle.Ref(refd["l_pac"], refd["ann_offset"], refd["ann_len"], refd["pac"])
+    _, _, ost = oracle.chain2aln("oracle", opt, ref, batch)
+    assert (st["cells"], st["rows"], st["ext_calls"]) == tuple(int(x) for x in ost)
+
+
+def test_slots_double_buffered(refd):
+    opt, batch, want, want_n = G.load_chain_set("c1_default")
+    eng = make_engine(refd, opt)
+    half = batch.n_reads // 2
+    b0 = batch.subset(range(half))
+    b1 = batch.subset(range(half, batch.n_reads))
+    eng.submit(0, b0)
+    eng.submit(1, b1)
+    with pytest.raises(BwaGpuError):  # a slot holds one batch at a time
+        eng.submit(0, b0)
+    r1, n1 = eng.wait(1, b1)
+    r0, n0 = eng.wait(0, b0)
+    got = np.concatenate([compact(b0, r0, n0), compact(b1, r1, n1)])
+    assert G.region_mismatch(got, want) is None
+    eng.close()
+
+
+def test_reordered_and_ragged_batches(refd):
+    opt, batch, want, want_n = G.load_chain_set("c5_mixed")
+    eng = make_engine(refd, opt)
+    rng = np.random.default_rng(5)
+    perm = rng.permutation(batch.n_reads)
+    sub = batch.subset(perm)
+    regs, n = eng.chain2aln(sub)
+    off = np.concatenate([[0], np.cumsum(want_n)])
+    exp = np.concatenate([want[off[r]:off[r + 1]] for r in perm])
+    assert G.region_mismatch(compact(sub, regs, n), exp) is None
+    # empty batch, one read, reads with no chains only
+    empty = batch.subset([])
+    r, n = eng.chain2aln(empty)
+    assert len(r) == 0 and len(n) == 0
+    nochain = [i for i in range(batch.n_reads) if batch.read_chain_off[i + 1] == batch.read_chain_off[i]][:5]
+    r, n = eng.chain2aln(batch.subset(nochain))
+    assert (n == 0).all()
+    one = batch.subset([int(np.argmax(want_n))])
+    r, n = eng.chain2aln(one)
+    assert n[0] == want_n.max()
+    eng.close()
+
+
+def test_error_conditions(refd):
+    opt, batch, _, _ = G.load_chain_set("c1_default")
+    eng = make_engine(refd, opt)
+    # a chain whose rid does not hold its first seed: the reference asserts (bwamem.c:669)
+    sub = batch.subset(range(20))
+    bad = Batch(sub.seq_off, sub.seq, sub.read_chain_off, sub.chain_seed_off,
+                (sub.chain_rid + 1) % len(refd["ann_len"]), sub.chain_frac_rep, sub.seeds)
+    with pytest.raises(BwaGpuError) as e:
+        eng.chain2aln(bad)
+    assert e.value.code == abi.E_RESULTS
+    # the engine keeps working after a failed batch
+    regs, n = eng.chain2aln(sub)
+    assert n.sum() > 0
+    # reads longer than BWAGPU_MAX_READ_LEN are refused up front
+    long = Batch(np.array([0, 1100]), np.zeros(1100, np.uint8), np.array([0, 0]), np.array([0]),
+                 np.zeros(0, np.int32), np.zeros(0, np.float32), np.zeros(0, abi.SEED_DTYPE))
+    with pytest.raises(BwaGpuError) as e:
+        eng.chain2aln(long)
+    assert e.value.code == abi.E_UNSUPPORTED
+    # malformed offsets
+    mal = Batch(np.array([0, 5]), np.zeros(5, np.uint8), np.array([0, 1]), np.array([0]),
+                np.zeros(0, np.int32), np.zeros(0, np.float32), np.zeros(0, abi.SEED_DTYPE))
+    with pytest.raises(BwaGpuError) as e:
+        eng.chain2aln(mal)
+    assert e.value.code == abi.E_INVAL
+    eng.close()
+
+
+def test_device_entry_point_with_torch_buffers(refd):
+    torch = pytest.importorskip("torch")
+    opt, batch, want, want_n = G.load_chain_set("opt2_band")
+    eng = make_engine(refd, opt)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(batch, k)).view(np.uint8)).to(dev)
+         for k in ("seq_off", "seq", "read_chain_off", "chain_seed_off", "chain_rid", "chain_frac_rep", "seeds")}
+    out = torch.zeros(batch.n_seeds * 88, dtype=torch.uint8, device=dev)
+    n = torch.zeros(batch.n_reads, dtype=torch.int32, device=dev)
+    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    bc = abi.BatchC()
+    bc.n_reads, bc.n_chains, bc.n_seeds = batch.n_reads, batch.n_chains, batch.n_seeds
+    bc.seq_bytes = int(batch.seq_off[-1])
+    for k in t:
+        setattr(bc, k, t[k].data_ptr())
+    stream = torch.cuda.current_stream().cuda_stream
+    eng.chain2aln_device(bc, out.data_ptr(), n.data_ptr(), stats.data_ptr(), stream)
+    torch.cuda.synchronize()
+    regs = out.cpu().numpy().view(abi.ALNREG_DTYPE)
+    nn = n.cpu().numpy()
+    assert np.array_equal(nn, want_n)
+    assert G.region_mismatch(compact(batch, regs, nn), want) is None
+    assert int(stats[0]) > 0 and int(stats[3]) == 0
+    eng.close()
