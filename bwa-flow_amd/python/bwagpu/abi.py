@@ -97,6 +97,14 @@ def load() -> C.CDLL:
     if _lib is not None:
         return _lib
     p = lib_path()
+    # one HIP runtime per process: when PyTorch is present its bundled
+    # libamdhip64.so.7 must be the one our library binds to (same soname), so
+    # import it first; a second runtime would hide the GPU from torch.
+    if os.environ.get("BWAGPU_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
     if not os.path.exists(p):
         raise RuntimeError(f"bwagpu: HIP engine library missing at {p}; run __graft_entry__.build()")
     lib = C.CDLL(p)

@@ -1,0 +1,256 @@
+// synth.cpp — synthetic workload generator for bench.py (lib/libsynth.so).
+//
+// There is no network and no GRCh38/chr21 in this environment, so the
+// benchmark configurations of BASELINE.json are reproduced with seeded
+// synthetic data of the same shape:
+//   * a reference of the requested length in bwa's forward 2-bit pac layout
+//     (bntseq.c:225, l_pac/4+1 bytes) split into contigs, iid ACGT plus
+//     diverged interspersed repeats and tandem repeats;
+//   * read pairs (~N(400,40) fragments, 0.8% substitutions, 0.1% 1-3 bp
+//     indels, 0.05% N) of 100/150/250 bp or a mix;
+//   * per read, the chains bwa's SeqsToChains would hand to ChainsToRegions
+//     on a unique reference: every maximal exact match of >= min_seed_len bases
+//     between the read and its true origin becomes a seed {rbeg in the 2-strand
+//     coordinate, qbeg, len, score=len} (bwamem.c:294 sets score = len), all
+//     seeds of a read form one chain on the origin contig; a fraction of reads
+//     additionally get a repeat chain (a seed copied to another locus), and
+//     chimeric reads get two chains.
+// This is input generation only; the stage under test is libbwagpu.so.
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "bwagpu.h"
+
+namespace {
+
+struct Rng {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+  }
+  double u() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+  int i(int n) { return (int)(u() * n); }
+  double n() {
+    double a = u() + 1e-300, b = u();
+    return sqrt(-2 * log(a)) * cos(2 * M_PI * b);
+  }
+};
+
+inline int get2(const uint8_t* pac, int64_t k) { return pac[k >> 2] >> ((~k & 3) << 1) & 3; }
+inline void set2(uint8_t* pac, int64_t k, int c) { pac[k >> 2] |= (uint8_t)(c << ((~k & 3) << 1)); }
+
+}  // namespace
+
+extern "C" {
+
+// Build a reference of total_len bases in n_ctg contigs.  pac must hold
+// total_len/4+1 zeroed bytes; ann_off/ann_len get n_ctg entries.
+int synth_ref(uint64_t seed, int64_t total_len, int n_ctg, uint8_t* pac, int64_t* ann_off, int32_t* ann_len) {
+  if (total_len <= 0 || n_ctg <= 0 || !pac) return -1;
+  Rng g{seed};
+  std::vector<uint8_t> s((size_t)total_len);
+  for (auto& b : s) b = (uint8_t)(g.next() & 3);
+  // interspersed repeats (~2% of the genome), 1% diverged
+  int64_t rep = total_len / 50;
+  for (int64_t done = 0; done < rep;) {
+    int len = 300 + g.i(2700);
+    if (len >= total_len / 4) break;
+    int64_t src = (int64_t)(g.u() * (double)(total_len - len));
+    for (int c = 0; c < 3; ++c) {
+      int64_t dst = (int64_t)(g.u() * (double)(total_len - len));
+      for (int k = 0; k < len; ++k) s[dst + k] = g.u() < 0.01 ? (uint8_t)(g.next() & 3) : s[src + k];
+      done += len;
+    }
+  }
+  // tandem repeats
+  for (int64_t t = 0; t < total_len / 100000 + 1; ++t) {
+    int per = 2 + g.i(49), len = 200 + g.i(800);
+    if (len >= total_len) break;
+    int64_t dst = (int64_t)(g.u() * (double)(total_len - len));
+    for (int k = per; k < len; ++k) s[dst + k] = g.u() < 0.005 ? (uint8_t)(g.next() & 3) : s[dst + k - per];
+  }
+  memset(pac, 0, (size_t)(total_len / 4 + 1));
+  for (int64_t k = 0; k < total_len; ++k) set2(pac, k, s[k]);
+  int64_t off = 0;
+  for (int c = 0; c < n_ctg; ++c) {
+    int64_t len = total_len / n_ctg + (c == n_ctg - 1 ? total_len % n_ctg : 0);
+    ann_off[c] = off;
+    ann_len[c] = (int32_t)len;
+    off += len;
+  }
+  return 0;
+}
+
+// Upper bounds for synth_reads outputs.
+void synth_bounds(int n_pairs, int len_mode, int64_t* max_seq, int32_t* max_chains, int32_t* max_seeds) {
+  const int L = len_mode == 0 ? 250 : len_mode;
+  *max_seq = (int64_t)2 * n_pairs * L;
+  *max_chains = 2 * n_pairs * 3;
+  *max_seeds = 2 * n_pairs * (L / 19 + 4) * 2;
+}
+
+// Simulate n_pairs read pairs and their chains.  len_mode: 100/150/250, or 0
+// for equal thirds of 100/150/250 (BASELINE config 5).  Outputs follow
+// bwagpu_batch_t; sizes are returned through *n_*.  Returns 0 or -1.
+int synth_reads(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const int32_t* ann_len, int n_ctg,
+                uint64_t seed, int n_pairs, int len_mode, int min_seed_len, int64_t* seq_off, uint8_t* seq,
+                int32_t* read_chain_off, int32_t* chain_seed_off, int32_t* chain_rid, float* chain_frac_rep,
+                bwagpu_seed_t* seeds, int32_t* n_reads_out, int32_t* n_chains_out, int32_t* n_seeds_out) {
+  Rng g{seed ^ 0x5eedULL};
+  int64_t so = 0;
+  int32_t nr = 0, nc = 0, ns = 0;
+  seq_off[0] = 0;
+  read_chain_off[0] = 0;
+  chain_seed_off[0] = 0;
+  std::vector<uint8_t> frag, rd, fwdr;
+  std::vector<int64_t> pos;  // per read base: 2-strand ref coordinate, or -1
+  auto ctg_of = [&](int64_t f) {
+    int lo = 0, hi = n_ctg - 1;
+    while (lo < hi) {
+      int m = (lo + hi + 1) >> 1;
+      if (ann_off[m] <= f) lo = m;
+      else hi = m - 1;
+    }
+    return lo;
+  };
+  for (int p = 0; p < n_pairs; ++p) {
+    const int L = len_mode == 0 ? (p % 3 == 0 ? 100 : p % 3 == 1 ? 150 : 250) : len_mode;
+    int fl = (int)(400 + 40 * g.n());
+    fl = std::max(fl, L + 10);
+    fl = std::min<int64_t>(fl, l_pac - 1);
+    const int ctg = g.i(n_ctg);
+    if (ann_len[ctg] <= fl + 1) continue;
+    const int64_t start = ann_off[ctg] + (int64_t)(g.u() * (double)(ann_len[ctg] - fl));
+    const int strand = (int)(g.next() & 1);
+    for (int e = 0; e < 2; ++e) {
+      const bool fwd = ((e == 0) ^ strand) != 0;
+      // the read before errors, with the 2-strand coordinate of each base
+      fwdr.assign(L, 0);
+      std::vector<int64_t> p0(L);
+      for (int i = 0; i < L; ++i) {
+        if (fwd) {
+          int64_t f = start + i;
+          fwdr[i] = (uint8_t)get2(pac, f);
+          p0[i] = f;
+        } else {
+          int64_t f = start + fl - 1 - i;
+          fwdr[i] = (uint8_t)(3 - get2(pac, f));
+          p0[i] = (l_pac << 1) - 1 - f;
+        }
+      }
+      // errors
+      rd.clear();
+      pos.clear();
+      for (int i = 0; i < L && (int)rd.size() < L; ++i) {
+        double u = g.u();
+        if (u < 0.0005) {
+          rd.push_back(4);
+          pos.push_back(-1);
+        } else if (u < 0.0085) {
+          rd.push_back((uint8_t)((fwdr[i] + 1 + g.i(3)) & 3));
+          pos.push_back(-1);
+        } else if (u < 0.009) {
+          i += g.i(3);
+        } else if (u < 0.0095) {
+          int k = 1 + g.i(3);
+          while (k-- && (int)rd.size() < L) {
+            rd.push_back((uint8_t)(g.next() & 3));
+            pos.push_back(-1);
+          }
+          if ((int)rd.size() < L) {
+            rd.push_back(fwdr[i]);
+            pos.push_back(p0[i]);
+          }
+        } else {
+          rd.push_back(fwdr[i]);
+          pos.push_back(p0[i]);
+        }
+      }
+      const bool chimera = g.u() < 0.01;
+      if (chimera) {  // second half from a random locus (forward)
+        int64_t q = (int64_t)(g.u() * (double)(l_pac - L));
+        for (int i = L / 2; i < (int)rd.size(); ++i) {
+          rd[i] = (uint8_t)get2(pac, q + i);
+          pos[i] = q + i;
+        }
+      }
+      const int n = (int)rd.size();
+      memcpy(seq + so, rd.data(), n);
+      so += n;
+      seq_off[nr + 1] = so;
+      // maximal exact matches along the true alignment -> seeds
+      auto emit_chain = [&](int a_begin, int a_end) {
+        int32_t s0 = ns;
+        int i = a_begin;
+        int rid = -1;
+        while (i < a_end) {
+          if (pos[i] < 0) { ++i; continue; }
+          int j = i + 1;
+          while (j < a_end && pos[j] == pos[j - 1] + 1 &&
+                 ((pos[j] < l_pac) == (pos[i] < l_pac)))
+            ++j;
+          const int len = j - i;
+          if (len >= min_seed_len) {
+            int64_t f = pos[i] < l_pac ? pos[i] : (l_pac << 1) - 1 - (pos[i] + len - 1);
+            int64_t fe = f + len - 1;
+            int c0 = ctg_of(f), c1 = ctg_of(fe);
+            if (c0 == c1 && (rid < 0 || rid == c0)) {
+              rid = c0;
+              bwagpu_seed_t s;
+              s.rbeg = pos[i];
+              s.qbeg = i;
+              s.len = len;
+              s.score = len;
+              s.pad_ = 0;
+              seeds[ns++] = s;
+            }
+          }
+          i = j;
+        }
+        if (ns > s0) {
+          chain_rid[nc] = rid;
+          chain_frac_rep[nc] = 0.f;
+          chain_seed_off[++nc] = ns;
+        }
+      };
+      if (chimera) {
+        emit_chain(0, L / 2);
+        emit_chain(L / 2, n);
+      } else {
+        emit_chain(0, n);
+      }
+      // a repeat copy of the longest seed elsewhere (secondary chain)
+      if (nc > read_chain_off[nr] && g.u() < 0.1) {
+        const int32_t c = nc - 1;
+        int best = chain_seed_off[c];
+        for (int k = chain_seed_off[c]; k < chain_seed_off[c + 1]; ++k)
+          if (seeds[k].len > seeds[best].len) best = k;
+        bwagpu_seed_t s = seeds[best];
+        const int64_t f = (int64_t)(g.u() * (double)(l_pac - s.len - 1));
+        const int cc = ctg_of(f);
+        if (ctg_of(f + s.len - 1) == cc) {
+          s.rbeg = f;
+          s.score = s.len;
+          seeds[ns++] = s;
+          chain_rid[nc] = cc;
+          chain_frac_rep[nc] = 0.25f;
+          chain_seed_off[++nc] = ns;
+        }
+      }
+      read_chain_off[++nr] = nc;
+    }
+  }
+  *n_reads_out = nr;
+  *n_chains_out = nc;
+  *n_seeds_out = ns;
+  return 0;
+}
+
+}  // extern "C"
