@@ -91,7 +91,7 @@ struct InLayout {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
-  DevBuf d_in, d_win, d_srt, d_out, d_n, d_stats, d_lists, d_counts;
+  DevBuf d_in, d_win, d_srt, d_out, d_n, d_stats, d_lists, d_counts, d_sort_tmp;
   HostBuf h_in, h_out, h_n, h_stats;
   bool busy = false;
   int32_t n_reads = 0, n_seeds = 0;
@@ -200,7 +200,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   for (auto& s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     s.d_in.release(); s.d_win.release(); s.d_srt.release(); s.d_out.release(); s.d_n.release();
-    s.d_stats.release(); s.d_lists.release(); s.d_counts.release();
+    s.d_stats.release(); s.d_lists.release(); s.d_counts.release(); s.d_sort_tmp.release();
     s.h_in.release(); s.h_out.release(); s.h_n.release(); s.h_stats.release();
     if (s.ev0) (void)hipEventDestroy(s.ev0);
     if (s.ev1) (void)hipEventDestroy(s.ev1);
@@ -274,21 +274,34 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
                       int32_t* d_n, int64_t* d_stats, hipStream_t st) {
   HIPC(s.d_win.ensure(sizeof(ChainWin) * (size_t)std::max(db.n_chains, 1)), "hipMalloc(win)");
   HIPC(s.d_srt.ensure(sizeof(uint64_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(srt)");
-  HIPC(s.d_lists.ensure(sizeof(int32_t) * (size_t)kNumVariants * std::max(db.n_reads, 1)), "hipMalloc(lists)");
+  const size_t nr = (size_t)std::max(db.n_reads, 1);
+  // keys_in | vals_in | keys_out | vals_out, n_reads each
+  HIPC(s.d_lists.ensure(4 * sizeof(int32_t) * nr), "hipMalloc(lists)");
+  uint32_t* keys_in = s.d_lists.as<uint32_t>();
+  int32_t* vals_in = (int32_t*)(keys_in + nr);
+  uint32_t* keys_out = (uint32_t*)(vals_in + nr);
+  int32_t* vals_out = (int32_t*)(keys_out + nr);
+  size_t tmp_bytes = 0;
+  HIPC(sort_reads(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out, std::max(db.n_reads, 1), st),
+       "sort size query");
+  HIPC(s.d_sort_tmp.ensure(tmp_bytes), "hipMalloc(sort temp)");
   HIPC(s.d_counts.ensure(sizeof(int32_t) * 16), "hipMalloc(counts)");
   HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * 16, st), "memset counts");
   if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
   HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, 0, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(), d_stats, st),
        "chain_prep launch");
-  HIPC(launch_bin_reads(db, s.d_counts.as<int32_t>(), s.d_lists.as<int32_t>(), d_stats, st), "bin launch");
+  HIPC(launch_read_keys(db, keys_in, vals_in, s.d_counts.as<int32_t>(), d_stats, st), "read_keys launch");
+  if (db.n_reads) {
+    size_t tb2 = s.d_sort_tmp.cap;
+    HIPC(sort_reads(s.d_sort_tmp.p, tb2, keys_in, keys_out, vals_in, vals_out, db.n_reads, st), "sort reads");
+  }
   for (int v = 0; v < kNumVariants; ++v) {
     const int lqv = std::min(lq_max, kVariants[v].max_len());
     const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
     const int gpb = kBlock / kVariants[v].G;
     if ((size_t)tb * gpb > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
-    HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, s.d_lists.as<int32_t>() + (size_t)v * db.n_reads,
-                          s.d_counts.as<int32_t>() + v, db.n_reads, tb, s.d_win.as<ChainWin>(),
-                          s.d_srt.as<uint64_t>(), d_out, d_n, d_stats, st),
+    HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, vals_out, s.d_counts.as<int32_t>(), db.n_reads, tb,
+                          s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(), d_out, d_n, d_stats, st),
          "chain2aln launch");
   }
   return BWAGPU_OK;
@@ -576,7 +589,7 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
         int we = std::min(t.w, std::min(mi, md));
         rows = std::max(rows, std::min(t.tlen, t.qlen + we + 1));
       }
-      const int tb = (rows + 15) & ~15;
+      const int tb = (rows + 2 + 15) & ~15;
       const int gpb = kBlock / kVariants[v].G;
       if ((size_t)tb * gpb > 64 * 1024) {
         cleanup();

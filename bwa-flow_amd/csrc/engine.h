@@ -58,10 +58,15 @@ constexpr int kBlock = 256;  // threads per workgroup (4 waves)
 // host-side launchers (sw_kernels.hip)
 hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, int64_t lq_cap,
                              ChainWin* win, uint64_t* srt, int64_t* stats, hipStream_t st);
-hipError_t launch_bin_reads(const DevBatch& b, int32_t* counts, int32_t* lists, int64_t* stats,
+// per-read sort keys [variant | task shape] + per-variant counts
+hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, int32_t* counts, int64_t* stats,
                             hipStream_t st);
-// read_list/d_count: device list of read indices and its length (from
-// launch_bin_reads); max_list bounds the grid
+// stable radix sort of (key, read) pairs (rocPRIM)
+hipError_t sort_reads(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                      const int32_t* vals_in, int32_t* vals_out, int n, hipStream_t st);
+// read_list: reads sorted by key; d_count: per-variant counts (device); the
+// variant's reads start at the sum of the lower variants' counts; max_list
+// bounds the grid
 hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b,
                             const int32_t* read_list, const int32_t* d_count, int32_t max_list,
                             int tb_bytes, const ChainWin* win, uint64_t* srt, bwagpu_alnreg_t* out,

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
+#include <algorithm>
+
 #include "engine.h"
 
 namespace bwagpu {
@@ -38,6 +40,18 @@ namespace bwagpu {
 const Variant kVariants[kNumVariants] = {{16, 10}, {32, 8}, {64, 16}};
 
 // ---------------------------------------------------------------- group ops
+// Cross-lane primitives restricted to one group.  G = 16 is exactly one DPP
+// row, so everything is a DPP-modified VALU op (row_shr / row_ror): no LDS
+// crossbar round trip on the per-row critical path.  Wider groups fall back to
+// ds_bpermute-based shuffles.
+constexpr int DPP_ROW_SHR(int n) { return 0x110 + n; }
+constexpr int DPP_ROW_ROR(int n) { return 0x120 + n; }
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xF, 0xF, false);
+}
+
 template <int G>
 struct Grp {
   static __device__ __forceinline__ int lane() { return (int)(threadIdx.x & (G - 1)); }
@@ -49,11 +63,6 @@ struct Grp {
   static __device__ __forceinline__ int gmin(int v) {
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, G));
-    return v;
-  }
-  static __device__ __forceinline__ long long gsum64(long long v) {
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, G);
     return v;
   }
   // max over lanes strictly below this one; `ident` for lane 0
@@ -70,6 +79,55 @@ struct Grp {
   static __device__ __forceinline__ int up1(int v) { return __shfl_up(v, 1, G); }
   static __device__ __forceinline__ int bcast(int v, int src) { return __shfl(v, src, G); }
 };
+
+template <>
+struct Grp<16> {
+  // every step is `x = op(x, dpp(x))` with old == x, the form LLVM's DPP
+  // combiner folds into one v_{max,min}_i32_dpp (lanes whose DPP source lies
+  // outside the row keep x)
+  static __device__ __forceinline__ int lane() { return (int)(threadIdx.x & 15); }
+  static __device__ __forceinline__ int gmax(int v) {
+    v = max(v, dpp<DPP_ROW_ROR(8)>(v, v));
+    v = max(v, dpp<DPP_ROW_ROR(4)>(v, v));
+    v = max(v, dpp<DPP_ROW_ROR(2)>(v, v));
+    return max(v, dpp<DPP_ROW_ROR(1)>(v, v));
+  }
+  static __device__ __forceinline__ int gmin(int v) {
+    v = min(v, dpp<DPP_ROW_ROR(8)>(v, v));
+    v = min(v, dpp<DPP_ROW_ROR(4)>(v, v));
+    v = min(v, dpp<DPP_ROW_ROR(2)>(v, v));
+    return min(v, dpp<DPP_ROW_ROR(1)>(v, v));
+  }
+  static __device__ __forceinline__ int excl_max(int v, int ident) {
+    v = max(v, dpp<DPP_ROW_SHR(1)>(v, v));
+    v = max(v, dpp<DPP_ROW_SHR(2)>(v, v));
+    v = max(v, dpp<DPP_ROW_SHR(4)>(v, v));
+    v = max(v, dpp<DPP_ROW_SHR(8)>(v, v));
+    return dpp<DPP_ROW_SHR(1)>(ident, v);
+  }
+  static __device__ __forceinline__ int up1(int v) { return dpp<DPP_ROW_SHR(1)>(v, v); }
+  static __device__ __forceinline__ int bcast(int v, int src) { return __shfl(v, src, 16); }
+};
+
+// wave-uniform max of a group-uniform value over the wave's ACTIVE groups (for
+// loop bounds every active group of the wave can share: a scalar branch
+// instead of per-lane masking).  Groups of one wave may be at different points
+// of the read loop, so inactive groups' registers hold unrelated values: read
+// each group's lane 0 with v_readlane and keep it only if EXEC says it is live.
+template <int G>
+__device__ __forceinline__ int wave_umax(int v) {
+  const unsigned long long ex = __builtin_amdgcn_read_exec();
+  int m = 0;
+#pragma unroll
+  for (int k = 0; k < 64 / G; ++k)
+    if ((ex >> (k * G)) & 1ull) m = max(m, __builtin_amdgcn_readlane(v, k * G));
+  return m;
+}
+
+__device__ __forceinline__ long long grp_sum64(long long v, int G) {
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, G);
+  return v;
+}
 
 __device__ __forceinline__ int pac_base2(const uint8_t* __restrict__ pac, int64_t l_pac, int64_t x) {
   // 2-strand coordinate -> base (bns_get_seq, bntseq.c:398-419)
@@ -99,124 +157,159 @@ constexpr int NEG = -(1 << 29);
 
 // ----------------------------------------------------------- ksw_extend2
 // One ksw_extend2 call (bwa/ksw.c:380-479) on a group of G lanes.
-//   qcol(j)  -> query base of column j (0..4)
-//   tb       -> LDS row buffer holding target bases for rows [0, nrows)
-// The caller has filled tb for every row the call can reach.
-template <int G, int C, bool T5, typename QF>
-__device__ ExtOut extend_group(const DevOpt& o, int qlen, QF qcol, int tlen, const uint8_t* tb, int w,
-                               int end_bonus, int zdrop, int h0, Tally& tl) {
+//   query column j = qp[qa + qd*j]  (qd = -1 walks the read leftwards)
+//   tb             = LDS row buffer holding the target base of every row the
+//                    call can reach (filled by the caller)
+// Lane r owns columns [r*Cd, r*Cd+Cd), Cd = ceil((qlen+1)/G) <= C; column
+// qlen is eh[qlen] of the reference.  Column loops run to the wave-uniform
+// CdW = max Cd over the wave's groups, so they branch on scalars.
+template <int G, int C, bool T5>
+__device__ __forceinline__ ExtOut extend_group(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
+                                            int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
+                                            int h0, Tally& tl) {
   using GR = Grp<G>;
   const int r = GR::lane();
-  const int Cd = (qlen + G) / G;  // ceil((qlen+1)/G) <= C
-  const int jb = r * Cd;          // first column of this lane
+  const int Cd = (qlen + G) / G;
+  const int CdW = wave_umax<G>(Cd);
+  const int jb = r * Cd;  // first column of this lane
+  // hi / Cd as a multiply-shift: exact for hi < 1024, Cd <= 16
+  const int cd_inv = (65536 + Cd - 1) / Cd;
   const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
 
-  int hh[C], ee[C];
+  int hh[C], ee[C], jE[C], jm1E[C];
   uint32_t pf[C];
   uint32_t pf4[T5 ? C : 1];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    const int j = jb + c;
-    int qb = (c < Cd && j < qlen) ? qcol(j) : 0;
-    const int8_t* m = o.mat;
-    pf[c] = (uint32_t)(uint8_t)m[qb] | (uint32_t)(uint8_t)m[5 + qb] << 8 |
-            (uint32_t)(uint8_t)m[10 + qb] << 16 | (uint32_t)(uint8_t)m[15 + qb] << 24;
-    if (T5) pf4[c] = (uint32_t)(uint8_t)m[20 + qb];
-    // row -1 of eh[] (ksw.c:392-395): H(-1,-1)=h0, then an insertion gap
-    int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
-    hh[c] = (c < Cd && j <= qlen) ? v : 0;
-    ee[c] = 0;
+    if (c < CdW) {
+      const int j = jb + c;
+      const int qb = (c < Cd && j < qlen) ? qp[qa + qd * j] : 0;
+      const int8_t* m = o.mat;
+      // query profile of this column for target bases 0..3 (4 x int8)
+      pf[c] = (uint32_t)(uint8_t)m[qb] | (uint32_t)(uint8_t)m[5 + qb] << 8 |
+              (uint32_t)(uint8_t)m[10 + qb] << 16 | (uint32_t)(uint8_t)m[15 + qb] << 24;
+      if (T5) pf4[c] = (uint32_t)(uint8_t)m[20 + qb];
+      // row -1 of eh[] (ksw.c:392-395): H(-1,-1)=h0, then an insertion gap
+      const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
+      hh[c] = (c < Cd && j <= qlen) ? v : 0;
+      ee[c] = 0;
+      // scan offsets: u_j = t_j + j*e_ins; columns past this lane's block never
+      // contribute (NEG), F_j = max_{k<j} u_k - (j-1)*e_ins
+      jE[c] = c < Cd ? j * e_ins : NEG;
+      jm1E[c] = (j - 1) * e_ins;
+    }
   }
-  // band clamp (ksw.c:399-407)
-  {
-    int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
-    int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
+  {  // band clamp (ksw.c:399-407)
+    const int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
+    const int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
     w = min(w, min(mi, md));
   }
 
   int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0, lo = 0, hi = qlen;
-  long long cells = 0, rows = 0;
+  int cells = 0, rows = 0;
+  int tnext = tlen > 0 ? tb[0] : 0;
   for (int i = 0; i < tlen; ++i) {
-    const int t = tb[i];
+    const int t = tnext;
+    tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
     lo = max(lo, i - w);
     hi = min(min(hi, i + w + 1), qlen);
     const int left0 = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
     const int sh = (t & 3) << 3;
+    // this lane's in-band columns: clo <= c < chi; cend = the column of eh[hi]
+    const int clo = max(lo - jb, 0), chi = min(hi - jb, Cd), cend = hi - jb;
+    const bool empty = hi <= lo;
 
-    int M[C], pu[C], H[C], En[C];
-    int run = NEG, rkey = 0;
+    // pass 1: M = H(i-1,j-1)+S (0 if H(i-1,j-1)==0), u = t + j*e_ins for the F scan
+    int M[C], U[C];
+    int run = NEG;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const int j = jb + c;
-      const bool inb = c < Cd && j >= lo && j < hi;
-      int s;
-      if (T5 && t == 4) s = (int)(int8_t)(pf4[c] & 0xff);
-      else s = (int)(int8_t)((pf[c] >> sh) & 0xff);
-      const int m = hh[c] ? hh[c] + s : 0;
-      M[c] = m;
-      const int u = c < Cd ? (inb ? max(m - oe_ins, 0) : 0) + j * e_ins : NEG;
-      run = max(run, u);
-      pu[c] = run;
-    }
-    const int ex = GR::excl_max(run, NEG);
-    int lastH = 0;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int j = jb + c;
-      const bool inb = c < Cd && j >= lo && j < hi;
-      const int pprev = c == 0 ? ex : max(ex, pu[c - 1]);
-      const int f = j == 0 ? 0 : pprev - (j - 1) * e_ins;
-      const int h = max(max(M[c], ee[c]), f);
-      H[c] = h;
-      En[c] = max(ee[c] - e_del, max(M[c] - oe_del, 0));
-      if (inb) rkey = max(rkey, (h << 10) | j);
-      if (c == Cd - 1) lastH = h;
-    }
-    rkey = GR::gmax(rkey);
-    const int hl = GR::up1(lastH);
-    int nzf = INT_MAX, nzl = -1;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const int j = jb + c;
-      if (c < Cd) {
-        int hleft = c == 0 ? hl : H[c - 1];
-        if (j == lo) hleft = left0;
-        if (j >= lo && j < hi) {
-          hh[c] = hleft;
-          ee[c] = En[c];
-        } else if (j == hi) {
-          hh[c] = hi > lo ? hleft : left0;
-          ee[c] = 0;
-        }
-        const bool nz = (hh[c] | ee[c]) != 0;
-        if (nz && j >= lo && j < hi) nzf = min(nzf, j);
-        if (nz && j >= lo && j <= hi) nzl = max(nzl, j);
+      if (c < CdW) {
+        int sc;
+        if (T5 && t == 4) sc = (int)(int8_t)(pf4[c] & 0xff);
+        else sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
+        const int m = hh[c] ? hh[c] + sc : 0;
+        M[c] = m;
+        const bool inb = c >= clo && c < chi;
+        const int u = (inb ? max(m - oe_ins, 0) : 0) + jE[c];
+        U[c] = u;
+        run = max(run, u);
       }
     }
-    rows += 1;
-    if (hi > lo) cells += hi - lo;
-    if (max(lo, hi) == qlen) {  // ksw.c:450-453 — h1 now sits in eh[hi]
-      const int own = hi / Cd, slot = hi - own * Cd;
-      int v = 0;
+    // F(i,j) = max_{k<j} u_k - (j-1)*e_ins  (the reference's f recurrence, ksw.c:444-447;
+    // at j == 0 it comes out negative, which max(M, E>=0, F) ignores exactly like F=0)
+    int run2 = GR::excl_max(run, NEG);
+
+    // pass 2: H, E, row max key; next-row state of each column (ksw.c:429,449):
+    //   in band:  eh[j] <- {H(i,j-1) (first-column value at j == lo), E(i+1,j)}
+    //   j == hi:  eh[hi] <- {H(i,hi-1) (first-column value if the band is empty), 0}
+    int prevH = 0, lastH = 0, rkey = 0, en0 = 0, hcol = 0;
 #pragma unroll
-      for (int c = 0; c < C; ++c)
-        if (c == slot) v = hh[c];
-      const int h1 = GR::bcast(v, own);
-      if (!(esc > h1)) ei = i;
-      esc = max(esc, h1);
+    for (int c = 0; c < C; ++c) {
+      if (c < CdW) {
+        const int j = jb + c;
+        const bool inb = c >= clo && c < chi;
+        const int f = run2 - jm1E[c];
+        run2 = max(run2, U[c]);
+        const int h = max(max(M[c], ee[c]), f);
+        const int en = max(max(ee[c] - e_del, M[c] - oe_del), 0);
+        rkey = max(rkey, inb ? ((h << 10) | j) : 0);
+        if (c == 0) {
+          en0 = en;
+        } else {
+          const bool isend = c == cend;
+          const int hnew = (j == lo || (isend && empty)) ? left0 : prevH;
+          hh[c] = (inb || isend) ? hnew : hh[c];
+          ee[c] = inb ? en : (isend ? 0 : ee[c]);
+          hcol = isend ? hh[c] : hcol;
+        }
+        prevH = h;
+        lastH = c == Cd - 1 ? h : lastH;
+      }
     }
+    {  // column 0 of the lane takes the previous lane's last H
+      const int hl = GR::up1(lastH);
+      const bool inb = 0 >= clo && 0 < chi;
+      const bool isend = cend == 0;
+      const int hnew = (jb == lo || (isend && empty)) ? left0 : hl;
+      hh[0] = (inb || isend) ? hnew : hh[0];
+      ee[0] = inb ? en0 : (isend ? 0 : ee[0]);
+      hcol = isend ? hh[0] : hcol;
+    }
+    rkey = GR::gmax(rkey);
+    rows += 1;
+    cells += empty ? 0 : hi - lo;
     const int mrow = rkey >> 10, mj = rkey & 1023;
+    {  // ksw.c:450-453; h1 now sits in eh[hi]
+      const bool endrow = max(lo, hi) == qlen;
+      const int h1 = GR::bcast(hcol, (hi * cd_inv) >> 16);  // owner lane of column hi
+      ei = (endrow && !(esc > h1)) ? i : ei;
+      esc = endrow ? max(esc, h1) : esc;
+    }
     if (mrow == 0) break;
-    if (mrow > best) {
-      best = mrow;
-      bi = i;
-      bj = mj;
-      off = max(off, abs(mj - i));
-    } else if (zdrop > 0) {
+    const bool better = mrow > best;
+    {
       const int di = i - bi, dj = mj - bj;
       const int drop = di > dj ? best - mrow - (di - dj) * e_del : best - mrow - (dj - di) * e_ins;
-      if (drop > zdrop) break;
+      if (!better && zdrop > 0 && drop > zdrop) break;
     }
+    off = better ? max(off, abs(mj - i)) : off;
+    bi = better ? i : bi;
+    bj = better ? mj : bj;
+    best = better ? mrow : best;
+    // zero-trim the band (ksw.c:466-469): first non-zero column in [lo,hi),
+    // last non-zero column in [lo,hi]
+    uint32_t nzb = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (c < CdW) nzb |= (uint32_t)min((uint32_t)(hh[c] | ee[c]), 1u) << c;
+    const int cincl = min(cend + 1, Cd);
+    const uint32_t mlo = clo >= 32 ? 0u : ~0u << clo;
+    const uint32_t mhi = chi <= 0 ? 0u : (chi >= 32 ? ~0u : (1u << chi) - 1u);
+    const uint32_t mhi2 = cincl <= 0 ? 0u : (cincl >= 32 ? ~0u : (1u << cincl) - 1u);
+    const uint32_t bf = nzb & mlo & mhi, bl = nzb & mlo & mhi2;
+    int nzf = bf ? jb + __builtin_ctz(bf) : INT_MAX;
+    int nzl = bl ? jb + 31 - __builtin_clz(bl) : -1;
     nzf = GR::gmin(nzf);
     nzl = GR::gmax(nzl);
     const int nlo = nzf == INT_MAX ? hi : nzf;
@@ -351,10 +444,14 @@ __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, D
   }
 }
 
-// ------------------------------------------------------------ binning
-// Reads go to the narrowest kernel variant whose G*C covers their length;
-// per-variant lists are appended with one wave-aggregated atomic per variant.
-__global__ void __launch_bounds__(256) bin_reads_kernel(DevBatch b, int32_t* counts, int32_t* lists,
+// ------------------------------------------------------------ read order
+// Each read gets a sort key: [variant | shape], variant = narrowest kernel
+// whose G*C covers the read, shape = (left, right) query lengths of the first
+// chain's top seed — the first extension mem_chain2aln performs.  Sorting by it
+// puts reads whose DP tasks have similar row counts and column widths into the
+// same wave (a wave runs as long as its slowest group).  Reads without chains
+// sort last.  Per-variant counts are appended with wave-aggregated atomics.
+__global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* keys, int32_t* vals, int32_t* counts,
                                                         int64_t* stats) {
   const int rd = blockIdx.x * blockDim.x + threadIdx.x;
   int v = -1;
@@ -362,27 +459,38 @@ __global__ void __launch_bounds__(256) bin_reads_kernel(DevBatch b, int32_t* cou
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
     for (int k = kNumVariants - 1; k >= 0; --k)
       if (lq <= kVariants[k].G * kVariants[k].C) v = k;
-    if (v < 0) atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_LEN);
+    uint32_t shape = 0x3fff;
+    const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
+    for (int c = c0; c < c1; ++c) {
+      const int s0 = b.chain_seed_off[c], s1 = b.chain_seed_off[c + 1];
+      if (s1 == s0) continue;
+      int best = s0;
+      for (int k = s0 + 1; k < s1; ++k)
+        if (b.seeds[k].score >= b.seeds[best].score) best = k;
+      const bwagpu_seed_t t = b.seeds[best];
+      const int left = min(t.qbeg, 1023) >> 3, right = min(lq - t.qbeg - t.len, 1023) >> 3;
+      shape = (uint32_t)(left << 7 | right);
+      break;
+    }
+    if (v < 0) {
+      atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_LEN);
+      v = kNumVariants - 1;
+    }
+    keys[rd] = (uint32_t)v << 14 | shape;
+    vals[rd] = rd;
   }
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int k = 0; k < kNumVariants; ++k) {
     const unsigned long long m = __ballot(v == k);
-    if (m == 0) continue;
-    const int leader = __ffsll((long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&counts[k], __popcll(m));
-    base = __shfl(base, leader, 64);
-    if (v == k) {
-      const int pos = base + __popcll(m & ((1ull << lane) - 1));
-      lists[(size_t)k * b.n_reads + pos] = rd;
-    }
+    if (m != 0 && lane == __ffsll((long long)m) - 1) atomicAdd(&counts[k], __popcll(m));
   }
 }
 
-hipError_t launch_bin_reads(const DevBatch& b, int32_t* counts, int32_t* lists, int64_t* stats, hipStream_t st) {
+hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, int32_t* counts, int64_t* stats,
+                            hipStream_t st) {
   if (b.n_reads == 0) return hipSuccess;
-  hipLaunchKernelGGL(bin_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, counts, lists, stats);
+  hipLaunchKernelGGL(read_keys_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, keys, vals, counts, stats);
   return hipGetLastError();
 }
 
@@ -390,7 +498,7 @@ hipError_t launch_bin_reads(const DevBatch& b, int32_t* counts, int32_t* lists, 
 template <int G, int C>
 __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref, DevBatch b,
                                                            const int32_t* __restrict__ read_list,
-                                                           const int32_t* __restrict__ n_list_p, int tb_bytes,
+                                                           const int32_t* __restrict__ counts, int variant, int tb_bytes,
                                                            const ChainWin* __restrict__ win,
                                                            uint64_t* srt, bwagpu_alnreg_t* out,
                                                            int32_t* out_n, int64_t* stats) {
@@ -399,13 +507,14 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
   constexpr int GPB = kBlock / G;
   const int gib = threadIdx.x / G;
   const int r = GR::lane();
-  const int li = blockIdx.x * GPB + gib;
-  const int n_list = *n_list_p;
+  int base = 0;
+  for (int v = 0; v < variant; ++v) base += counts[v];
+  const int n_list = counts[variant];
   Tally tl{0, 0, 0};
   uint8_t* tb = lds + gib * tb_bytes;
 
-  if (li < n_list) {
-    const int rd = read_list[li];
+  for (int li = blockIdx.x * GPB + gib; li < n_list; li += gridDim.x * GPB) {
+    const int rd = read_list[base + li];
     const int64_t qoff = b.seq_off[rd];
     const int lq = (int)(b.seq_off[rd + 1] - qoff);
     const uint8_t* q = b.seq + qoff;
@@ -485,76 +594,56 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
           }
         }
 
-        // ---- extend this seed (bwamem.c:717-792)
-        int score, truesc, qb, qe, aw0 = o.w, aw1 = o.w;
-        int64_t rb, re;
-        if (s.qbeg) {
-          const int qlen = s.qbeg;
-          const int tlen = (int)(s.rbeg - cw.lo);
-          const int h0 = s.len * o.a;
-          auto qf = [&](int j) { return (int)q[s.qbeg - 1 - j]; };
+        // ---- extend this seed (bwamem.c:717-792): side 0 = left, 1 = right.
+        // One call site for ksw_extend2 so the DP body is instantiated once.
+        int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
+        int aw[2] = {o.w, o.w};
+        int64_t rb = s.rbeg, re = s.rbeg + s.len;
+#pragma nounroll
+        for (int side = 0; side < 2; ++side) {
+          const bool left = side == 0;
+          if (left && s.qbeg == 0) {  // bwamem.c:753
+            score = truesc = s.len * o.a;
+            continue;
+          }
+          if (!left && s.qbeg + s.len == lq) continue;  // bwamem.c:781
+          const int qlen = left ? s.qbeg : lq - (s.qbeg + s.len);
+          const int64_t x0 = left ? s.rbeg - 1 : s.rbeg + s.len;
+          const int dir = left ? -1 : 1;
+          const int tlen = left ? (int)(s.rbeg - cw.lo) : (int)(cw.hi - x0);
+          const int qa = left ? s.qbeg - 1 : s.qbeg + s.len;
+          const int eb = left ? o.pen_clip5 : o.pen_clip3;
+          const int h0 = left ? s.len * o.a : score;
+          sc0 = score;
           ExtOut x{};
-          score = -1;
-          for (int t = 0; t < 2; ++t) {
+          for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY (bwamem.c:639)
             const int prev = score;
-            aw0 = o.w << t;
-            const int nr = rows_needed(o, qlen, tlen, aw0, o.pen_clip5);
-            fill_target<G>(tb, ref, s.rbeg - 1, -1, nr);
-            x = extend_group<G, C, false>(o, qlen, qf, tlen, tb, aw0, o.pen_clip5, o.zdrop, h0, tl);
+            aw[side] = o.w << t;
+            const int nr = rows_needed(o, qlen, tlen, aw[side], eb);
+            fill_target<G>(tb, ref, x0, dir, nr);
+            x = extend_group<G, C, false>(o, qlen, q, qa, dir, tlen, tb, aw[side], eb, o.zdrop, h0, tl);
             score = x.score;
-            if (score == prev || x.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+            if (score == prev || x.max_off < (aw[side] >> 1) + (aw[side] >> 2)) break;
           }
-          if (x.gscore <= 0 || x.gscore <= score - o.pen_clip5) {
-            qb = s.qbeg - x.qle;
-            rb = s.rbeg - x.tle;
-            truesc = score;
+          const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+          if (left) {
+            qb = local ? s.qbeg - x.qle : 0;
+            rb = s.rbeg - (local ? x.tle : x.gtle);
+            truesc = local ? score : x.gscore;
           } else {
-            qb = 0;
-            rb = s.rbeg - x.gtle;
-            truesc = x.gscore;
+            qe = local ? qa + x.qle : lq;
+            re = x0 + (local ? x.tle : x.gtle);
+            truesc += (local ? score : x.gscore) - sc0;
           }
-        } else {
-          score = truesc = s.len * o.a;
-          qb = 0;
-          rb = s.rbeg;
         }
-        if (s.qbeg + s.len != lq) {
-          const int qe0 = s.qbeg + s.len;
-          const int64_t tstart = s.rbeg + s.len;
-          const int qlen = lq - qe0;
-          const int tlen = (int)(cw.hi - tstart);
-          const int sc0 = score;
-          auto qf = [&](int j) { return (int)q[qe0 + j]; };
-          ExtOut x{};
-          for (int t = 0; t < 2; ++t) {
-            const int prev = score;
-            aw1 = o.w << t;
-            const int nr = rows_needed(o, qlen, tlen, aw1, o.pen_clip3);
-            fill_target<G>(tb, ref, tstart, 1, nr);
-            x = extend_group<G, C, false>(o, qlen, qf, tlen, tb, aw1, o.pen_clip3, o.zdrop, sc0, tl);
-            score = x.score;
-            if (score == prev || x.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
-          }
-          if (x.gscore <= 0 || x.gscore <= score - o.pen_clip3) {
-            qe = qe0 + x.qle;
-            re = tstart + x.tle;
-            truesc += score - sc0;
-          } else {
-            qe = lq;
-            re = tstart + x.gtle;
-            truesc += x.gscore - sc0;
-          }
-        } else {
-          qe = lq;
-          re = s.rbeg + s.len;
-        }
+        const int aw0 = aw[0], aw1 = aw[1];
         // seedcov (bwamem.c:784-788)
         long long cov = 0;
         for (int i = r; i < ns; i += G) {
           const bwagpu_seed_t t = sd[i];
           if (t.qbeg >= qb && t.qbeg + t.len <= qe && t.rbeg >= rb && t.rbeg + t.len <= re) cov += t.len;
         }
-        cov = GR::gsum64(cov);
+        cov = grp_sum64(cov, G);
         if (r == 0) {
           bwagpu_alnreg_t a;
           a.rb = rb;
@@ -579,8 +668,8 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
       }
     }
     if (r == 0) out_n[rd] = nreg;
-    if (r != 0) tl = Tally{0, 0, 0};
   }
+  if (r != 0) tl = Tally{0, 0, 0};
   block_stats<G>(tl, stats);
 }
 
@@ -613,8 +702,7 @@ __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_e
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      auto qf = [&](int j) { return (int)q[j]; };
-      x = extend_group<G, C, T5>(o, t.qlen, qf, t.tlen, tb, t.w, t.end_bonus, t.zdrop, t.h0, tl);
+      x = extend_group<G, C, T5>(o, t.qlen, q, 0, 1, t.tlen, tb, t.w, t.end_bonus, t.zdrop, t.h0, tl);
     }
     if (r == 0) res[k] = bwagpu_ext_result_t{x.score, x.qle, x.tle, x.gtle, x.gscore, x.max_off};
     if (r != 0) tl = Tally{0, 0, 0};
@@ -633,12 +721,13 @@ hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch&
 
 template <int G, int C>
 static hipError_t launch_c2a_t(const DevOpt& o, const DevRef& ref, const DevBatch& b, const int32_t* list,
-                               const int32_t* cnt, int32_t n, int tb, const ChainWin* win, uint64_t* srt,
+                               const int32_t* cnt, int variant, int32_t n, int tb, const ChainWin* win, uint64_t* srt,
                                bwagpu_alnreg_t* out, int32_t* out_n, int64_t* stats, hipStream_t st) {
   constexpr int GPB = kBlock / G;
-  const int nb = (n + GPB - 1) / GPB;
+  // grid-stride over the (device-side) list: the count is only known on the GPU
+  const int nb = std::min((n + GPB - 1) / GPB, 2048);
   hipLaunchKernelGGL((chain2aln_kernel<G, C>), dim3(nb), dim3(kBlock), (size_t)GPB * tb, st, o, ref, b, list, cnt,
-                     tb, win, srt, out, out_n, stats);
+                     variant, tb, win, srt, out, out_n, stats);
   return hipGetLastError();
 }
 
@@ -648,9 +737,9 @@ hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, con
                             int64_t* stats, hipStream_t st) {
   if (max_list == 0) return hipSuccess;
   switch (variant) {
-    case 0: return launch_c2a_t<16, 10>(o, ref, b, read_list, d_count, max_list, tb_bytes, win, srt, out, out_n, stats, st);
-    case 1: return launch_c2a_t<32, 8>(o, ref, b, read_list, d_count, max_list, tb_bytes, win, srt, out, out_n, stats, st);
-    case 2: return launch_c2a_t<64, 16>(o, ref, b, read_list, d_count, max_list, tb_bytes, win, srt, out, out_n, stats, st);
+    case 0: return launch_c2a_t<16, 10>(o, ref, b, read_list, d_count, 0, max_list, tb_bytes, win, srt, out, out_n, stats, st);
+    case 1: return launch_c2a_t<32, 8>(o, ref, b, read_list, d_count, 1, max_list, tb_bytes, win, srt, out, out_n, stats, st);
+    case 2: return launch_c2a_t<64, 16>(o, ref, b, read_list, d_count, 2, max_list, tb_bytes, win, srt, out, out_n, stats, st);
   }
   return hipErrorInvalidValue;
 }

@@ -1,0 +1,13 @@
+# PMC passes on a short bench run (one counter group per pass, no tracing domains)
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc
+mkdir -p $OUT
+cd /tmp
+rocprofv3 -L > $OUT/counters.txt 2>&1 || true
+B="python3 $GRAFT_REPO_ROOT/bench.py --pairs 100000 --steps 4 --warmup 1 --no-cpu"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d $OUT/a -o a --output-format csv -- $B > $OUT/a.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d $OUT/b -o b --output-format csv -- $B > $OUT/b.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/c -o c --output-format csv -- $B > $OUT/c.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/d -o d --output-format csv -- $B > $OUT/d.log 2>&1
+echo "pmc rc=$?" > $OUT/rc.txt
