@@ -285,8 +285,9 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   HIPC(sort_reads(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out, std::max(db.n_reads, 1), st),
        "sort size query");
   HIPC(s.d_sort_tmp.ensure(tmp_bytes), "hipMalloc(sort temp)");
-  HIPC(s.d_counts.ensure(sizeof(int32_t) * 16), "hipMalloc(counts)");
-  HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * 16, st), "memset counts");
+  // [0..15] per-variant read counts, [16 + 8v + xcc] per-XCD queue heads
+  HIPC(s.d_counts.ensure(sizeof(int32_t) * 64), "hipMalloc(counts)");
+  HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * 64, st), "memset counts");
   if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
   HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, 0, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(), d_stats, st),
        "chain_prep launch");
@@ -617,6 +618,13 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   s.last.rows = hs[ST_ROWS];
   s.last.ext_calls = hs[ST_CALLS];
   cleanup();
+  return BWAGPU_OK;
+}
+
+int bwagpu_debug_set_trace(bwagpu_ctx_t* ctx, void* dev_ptr) {
+  if (!ctx) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  HIPC(set_trace(dev_ptr), "set trace");
   return BWAGPU_OK;
 }
 

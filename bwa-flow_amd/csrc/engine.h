@@ -76,6 +76,9 @@ hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,
                          bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
 
+// diagnostics: per-read trace buffer (device pointer, 8 x u32 per read; NULL = off)
+hipError_t set_trace(void* dev_ptr);
+
 // rows a task can touch: the band is empty once i - w >= qlen (ksw.c:417-419),
 // so rows i <= qlen + w are the most ever read (the last one only to break)
 __host__ __device__ inline int band_cap(int qlen, int max_mat, int end_bonus, int o, int e) {

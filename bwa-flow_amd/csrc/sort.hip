@@ -11,8 +11,8 @@ namespace bwagpu {
 
 hipError_t sort_reads(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                       const int32_t* vals_in, int32_t* vals_out, int n, hipStream_t st) {
-  // keys use 16 bits: [variant:2 | left:7 | right:7]
-  return rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (unsigned)n, 0, 16, st);
+  // keys use 18 bits: [variant:2 | 0xffff - cost:16]
+  return rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (unsigned)n, 0, 18, st);
 }
 
 }  // namespace bwagpu

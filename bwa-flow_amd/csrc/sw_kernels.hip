@@ -37,7 +37,7 @@
 
 namespace bwagpu {
 
-const Variant kVariants[kNumVariants] = {{16, 10}, {32, 8}, {64, 16}};
+const Variant kVariants[kNumVariants] = {{64, 3}, {64, 4}, {64, 16}};
 
 // ---------------------------------------------------------------- group ops
 // Cross-lane primitives restricted to one group.  G = 16 is exactly one DPP
@@ -80,34 +80,95 @@ struct Grp {
   static __device__ __forceinline__ int bcast(int v, int src) { return __shfl(v, src, G); }
 };
 
+// DPP-fused max/min: `x = op(x, x[from DPP source lane])` in ONE instruction.
+// With bound_ctrl off, lanes whose DPP source lies outside the row are not
+// written, i.e. keep x — the identity for a scan.  The leading s_nop covers the
+// VALU-write -> DPP-read hazard (inline asm is opaque to the hazard recognizer).
+#define BWAGPU_DPP_OP(name, op, ctrl)                                                                    \
+  __device__ __forceinline__ int name(int x) {                                                          \
+    asm volatile("s_nop 1\n\t" op " %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf" : "+v"(x));        \
+    return x;                                                                                           \
+  }
+BWAGPU_DPP_OP(max_shr1, "v_max_i32_dpp", "row_shr:1")
+BWAGPU_DPP_OP(max_shr2, "v_max_i32_dpp", "row_shr:2")
+BWAGPU_DPP_OP(max_shr4, "v_max_i32_dpp", "row_shr:4")
+BWAGPU_DPP_OP(max_shr8, "v_max_i32_dpp", "row_shr:8")
+BWAGPU_DPP_OP(max_ror8, "v_max_i32_dpp", "row_ror:8")
+BWAGPU_DPP_OP(max_ror4, "v_max_i32_dpp", "row_ror:4")
+BWAGPU_DPP_OP(max_ror2, "v_max_i32_dpp", "row_ror:2")
+BWAGPU_DPP_OP(max_ror1, "v_max_i32_dpp", "row_ror:1")
+BWAGPU_DPP_OP(min_ror8, "v_min_i32_dpp", "row_ror:8")
+BWAGPU_DPP_OP(min_ror4, "v_min_i32_dpp", "row_ror:4")
+BWAGPU_DPP_OP(min_ror2, "v_min_i32_dpp", "row_ror:2")
+BWAGPU_DPP_OP(min_ror1, "v_min_i32_dpp", "row_ror:1")
+#undef BWAGPU_DPP_OP
+// cross-row steps of a 64-lane reduction/scan: row_bcast:15 feeds lane 15 of
+// rows 0/2 into rows 1/3, row_bcast:31 feeds lane 31 into rows 2/3
+#define BWAGPU_DPP_BC(name, op, ctrl, rmask)                                                             \
+  __device__ __forceinline__ int name(int x) {                                                          \
+    asm volatile("s_nop 1\n\t" op " %0, %0, %0 " ctrl " row_mask:" rmask " bank_mask:0xf" : "+v"(x));  \
+    return x;                                                                                           \
+  }
+BWAGPU_DPP_BC(max_bc15, "v_max_i32_dpp", "row_bcast:15", "0xa")
+BWAGPU_DPP_BC(max_bc31, "v_max_i32_dpp", "row_bcast:31", "0xc")
+BWAGPU_DPP_BC(min_bc15, "v_min_i32_dpp", "row_bcast:15", "0xa")
+BWAGPU_DPP_BC(min_bc31, "v_min_i32_dpp", "row_bcast:31", "0xc")
+#undef BWAGPU_DPP_BC
+constexpr int DPP_WAVE_SHR1 = 0x138;
+
 template <>
 struct Grp<16> {
-  // every step is `x = op(x, dpp(x))` with old == x, the form LLVM's DPP
-  // combiner folds into one v_{max,min}_i32_dpp (lanes whose DPP source lies
-  // outside the row keep x)
   static __device__ __forceinline__ int lane() { return (int)(threadIdx.x & 15); }
-  static __device__ __forceinline__ int gmax(int v) {
-    v = max(v, dpp<DPP_ROW_ROR(8)>(v, v));
-    v = max(v, dpp<DPP_ROW_ROR(4)>(v, v));
-    v = max(v, dpp<DPP_ROW_ROR(2)>(v, v));
-    return max(v, dpp<DPP_ROW_ROR(1)>(v, v));
-  }
-  static __device__ __forceinline__ int gmin(int v) {
-    v = min(v, dpp<DPP_ROW_ROR(8)>(v, v));
-    v = min(v, dpp<DPP_ROW_ROR(4)>(v, v));
-    v = min(v, dpp<DPP_ROW_ROR(2)>(v, v));
-    return min(v, dpp<DPP_ROW_ROR(1)>(v, v));
-  }
+  static __device__ __forceinline__ int gmax(int v) { return max_ror1(max_ror2(max_ror4(max_ror8(v)))); }
+  static __device__ __forceinline__ int gmin(int v) { return min_ror1(min_ror2(min_ror4(min_ror8(v)))); }
+  // inclusive row scan, then shift by one with `ident` entering lane 0
   static __device__ __forceinline__ int excl_max(int v, int ident) {
-    v = max(v, dpp<DPP_ROW_SHR(1)>(v, v));
-    v = max(v, dpp<DPP_ROW_SHR(2)>(v, v));
-    v = max(v, dpp<DPP_ROW_SHR(4)>(v, v));
-    v = max(v, dpp<DPP_ROW_SHR(8)>(v, v));
+    v = max_shr8(max_shr4(max_shr2(max_shr1(v))));
     return dpp<DPP_ROW_SHR(1)>(ident, v);
   }
   static __device__ __forceinline__ int up1(int v) { return dpp<DPP_ROW_SHR(1)>(v, v); }
   static __device__ __forceinline__ int bcast(int v, int src) { return __shfl(v, src, 16); }
 };
+
+// G = 64: one read per wave.  Reductions end in v_readlane, so every
+// group-uniform quantity of the DP (band, maxima, break tests) lives in SGPRs
+// and the row bookkeeping runs on the scalar unit.
+template <>
+struct Grp<64> {
+  static __device__ __forceinline__ int lane() { return (int)(threadIdx.x & 63); }
+  static __device__ __forceinline__ int gmax(int v) {
+    v = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(v))))));
+    return __builtin_amdgcn_readlane(v, 63);
+  }
+  static __device__ __forceinline__ int gmin(int v) {
+    v = min_bc31(min_bc15(min_ror1(min_ror2(min_ror4(min_ror8(v))))));
+    return __builtin_amdgcn_readlane(v, 63);
+  }
+  static __device__ __forceinline__ int excl_max(int v, int ident) {
+    v = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(v))))));
+    return dpp<DPP_WAVE_SHR1>(ident, v);
+  }
+  static __device__ __forceinline__ int up1(int v) { return dpp<DPP_WAVE_SHR1>(v, v); }
+  static __device__ __forceinline__ int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+};
+
+// a group-uniform value made visibly uniform to the compiler when a group is
+// the whole wave (then it lives in an SGPR)
+template <int G>
+__device__ __forceinline__ int guni(int x) {
+  if constexpr (G == 64) return __builtin_amdgcn_readfirstlane(x);
+  else return x;
+}
+template <int G>
+__device__ __forceinline__ int64_t guni64(int64_t x) {
+  if constexpr (G == 64) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)((uint64_t)hi << 32 | lo);
+  } else {
+    return x;
+  }
+}
 
 // wave-uniform max of a group-uniform value over the wave's ACTIVE groups (for
 // loop bounds every active group of the wave can share: a scalar branch
@@ -168,6 +229,14 @@ __device__ __forceinline__ ExtOut extend_group(const DevOpt& o, int qlen, const 
                                             int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
                                             int h0, Tally& tl) {
   using GR = Grp<G>;
+  qlen = guni<G>(qlen);
+  qa = guni<G>(qa);
+  qd = guni<G>(qd);
+  tlen = guni<G>(tlen);
+  w = guni<G>(w);
+  end_bonus = guni<G>(end_bonus);
+  zdrop = guni<G>(zdrop);
+  h0 = guni<G>(h0);
   const int r = GR::lane();
   const int Cd = (qlen + G) / G;
   const int CdW = wave_umax<G>(Cd);
@@ -323,6 +392,166 @@ __device__ __forceinline__ ExtOut extend_group(const DevOpt& o, int qlen, const 
   return ExtOut{best, bj + 1, bi + 1, ei + 1, esc, off};
 }
 
+// ------------------------------------------------ ksw_extend2, one read per wave
+// The G = 64 form used by every production kernel.  Columns are STRIDED over
+// the wave: lane r holds columns j = 64c + r of segments c < CD (CD =
+// ceil((qlen+1)/64), a compile-time constant picked by extend_wave_dispatch).
+// Consequences:
+//  * each segment is one wave-wide row slice: the in-band test, the non-zero
+//    test and the row-max key are 64-bit lane masks / one wave reduction, and
+//    every band/maximum/break quantity is a scalar (SGPR) value;
+//  * the F scan runs segment after segment, each segment's exclusive prefix
+//    seeded with the running maximum (a scalar carry) of the ones before it;
+//    columns past qlen sit after every real column and need no masking;
+//  * the reference's special eh[] writes (eh[lo].h = first-column value,
+//    eh[hi] = {h1, 0}, ksw.c:420-429,449) are single-lane selects.
+template <int CD, bool T5>
+__device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
+                                              int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
+                                              int h0, Tally& tl) {
+  const int r = (int)(threadIdx.x & 63);
+  const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
+  int hh[CD], ee[CD];
+  uint32_t pf[CD];
+  uint32_t pf4[T5 ? CD : 1];
+#pragma unroll
+  for (int c = 0; c < CD; ++c) {
+    const int j = 64 * c + r;
+    const int qb = j < qlen ? qp[qa + qd * j] : 0;
+    const int8_t* m = o.mat;
+    pf[c] = (uint32_t)(uint8_t)m[qb] | (uint32_t)(uint8_t)m[5 + qb] << 8 |
+            (uint32_t)(uint8_t)m[10 + qb] << 16 | (uint32_t)(uint8_t)m[15 + qb] << 24;
+    if (T5) pf4[c] = (uint32_t)(uint8_t)m[20 + qb];
+    // row -1 of eh[] (ksw.c:392-395): H(-1,-1)=h0, then an insertion gap
+    const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
+    hh[c] = j <= qlen ? v : 0;
+    ee[c] = 0;
+  }
+  const int jE0 = r * e_ins;  // u_j = t_j + j*e_ins ; F_j = max_{k<j} u_k - (j-1)*e_ins
+  {  // band clamp (ksw.c:399-407)
+    const int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
+    const int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
+    w = min(w, min(mi, md));
+  }
+  int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0, lo = 0, hi = qlen;
+  int cells = 0, rows = 0;
+  int tnext = tlen > 0 ? tb[0] : 0;
+  for (int i = 0; i < tlen; ++i) {
+    const int t = __builtin_amdgcn_readfirstlane(tnext);
+    tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
+    lo = max(lo, i - w);
+    hi = min(min(hi, i + w + 1), qlen);
+    const int left0 = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
+    const int sh = (t & 3) << 3;
+
+    // pass 1 + segmented exclusive max-scan of u
+    int M[CD], EX[CD];
+    uint64_t inbm[CD];
+    int carry = NEG;
+#pragma unroll
+    for (int c = 0; c < CD; ++c) {
+      const bool inb = r >= lo - 64 * c && r < hi - 64 * c;
+      inbm[c] = __builtin_amdgcn_ballot_w64(inb);
+      int sc;
+      if (T5 && t == 4) sc = (int)(int8_t)(pf4[c] & 0xff);
+      else sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
+      const int m = hh[c] ? hh[c] + sc : 0;
+      M[c] = m;
+      const int u = (inb ? max(m - oe_ins, 0) : 0) + jE0 + 64 * c * e_ins;
+      int x = c == 0 ? u : max(u, carry);
+      x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
+      EX[c] = dpp<DPP_WAVE_SHR1>(carry, x);  // lane 0 takes the carry from the segments before
+      carry = __builtin_amdgcn_readlane(x, 63);
+    }
+    // pass 2: H, E, row-max key, next-row state
+    int rk = 0, prev63 = 0, h1 = left0;
+    const int seg_hi = hi >> 6, seg_lo = lo >> 6;
+#pragma unroll
+    for (int c = 0; c < CD; ++c) {
+      const bool inb = (inbm[c] >> r) & 1ull;
+      const int f = EX[c] - jE0 - (64 * c - 1) * e_ins;
+      const int h = max(max(M[c], ee[c]), f);
+      const int en = max(max(ee[c] - e_del, M[c] - oe_del), 0);
+      rk = max(rk, inb ? ((h << 10) + 64 * c + r) : 0);
+      const int hs = dpp<DPP_WAVE_SHR1>(prev63, h);  // H(i, j-1)
+      prev63 = __builtin_amdgcn_readlane(h, 63);
+      if (c == seg_hi && hi > lo) h1 = __builtin_amdgcn_readlane(hs, hi & 63);  // H(i, hi-1)
+      hh[c] = inb ? hs : hh[c];
+      ee[c] = inb ? en : ee[c];
+    }
+    // eh[lo].h = first-column value (only matters when lo < hi), eh[hi] = {h1, 0}
+#pragma unroll
+    for (int c = 0; c < CD; ++c) {
+      if (c == seg_lo && lo < hi) hh[c] = r == (lo & 63) ? left0 : hh[c];
+      if (c == seg_hi) {
+        hh[c] = r == (hi & 63) ? h1 : hh[c];
+        ee[c] = r == (hi & 63) ? 0 : ee[c];
+      }
+    }
+    rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
+    rk = __builtin_amdgcn_readlane(rk, 63);
+    rows += 1;
+    cells += hi > lo ? hi - lo : 0;
+    if (max(lo, hi) == qlen) {  // ksw.c:450-453
+      if (!(esc > h1)) ei = i;
+      esc = max(esc, h1);
+    }
+    const int mrow = rk >> 10, mj = rk & 1023;
+    if (mrow == 0) break;
+    if (mrow > best) {
+      best = mrow;
+      bi = i;
+      bj = mj;
+      off = max(off, abs(mj - i));
+    } else if (zdrop > 0) {
+      const int di = i - bi, dj = mj - bj;
+      const int drop = di > dj ? best - mrow - (di - dj) * e_del : best - mrow - (dj - di) * e_ins;
+      if (drop > zdrop) break;
+    }
+    // zero-trim the band (ksw.c:466-469): first non-zero column in [lo,hi),
+    // last non-zero column in [lo,hi]
+    int nlo = hi, jl = -1;
+#pragma unroll
+    for (int c = 0; c < CD; ++c) {
+      const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[c] | ee[c]) != 0);
+      const uint64_t f = nz & inbm[c];
+      uint64_t l = f;
+      if (c == seg_hi) l |= nz & (1ull << (hi & 63));
+      if (f && nlo == hi) nlo = 64 * c + __builtin_ctzll(f);
+      if (l) jl = 64 * c + 63 - __builtin_clzll(l);
+    }
+    if (jl < 0) jl = nlo - 1;
+    lo = nlo;
+    hi = min(jl + 2, qlen);
+  }
+  tl.cells += cells;
+  tl.rows += rows;
+  tl.calls += 1;
+  return ExtOut{best, bj + 1, bi + 1, ei + 1, esc, off};
+}
+
+// CD is uniform per call (qlen is): one compiled body per segment count
+template <int C, bool T5>
+__device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp,
+                                                    int qa, int qd, int tlen, const uint8_t* tb, int w,
+                                                    int end_bonus, int zdrop, int h0, Tally& tl) {
+  qlen = __builtin_amdgcn_readfirstlane(qlen);
+  qa = __builtin_amdgcn_readfirstlane(qa);
+  qd = __builtin_amdgcn_readfirstlane(qd);
+  tlen = __builtin_amdgcn_readfirstlane(tlen);
+  w = __builtin_amdgcn_readfirstlane(w);
+  end_bonus = __builtin_amdgcn_readfirstlane(end_bonus);
+  zdrop = __builtin_amdgcn_readfirstlane(zdrop);
+  h0 = __builtin_amdgcn_readfirstlane(h0);
+  const int cd = (qlen + 64) >> 6;  // ceil((qlen+1)/64)
+#define EXT_SEG(n) \
+  if (n <= C && cd == n) return extend_wave<(n <= C ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
+  EXT_SEG(1) EXT_SEG(2) EXT_SEG(3) EXT_SEG(4) EXT_SEG(5) EXT_SEG(6) EXT_SEG(7) EXT_SEG(8)
+  EXT_SEG(9) EXT_SEG(10) EXT_SEG(11) EXT_SEG(12) EXT_SEG(13) EXT_SEG(14) EXT_SEG(15) EXT_SEG(16)
+#undef EXT_SEG
+  return ExtOut{-1, 0, 0, 0, -1, 0};  // unreachable: cd <= C by construction
+}
+
 // rows that extend_group can read for (qlen, w, end_bonus)
 __device__ __forceinline__ int rows_needed(const DevOpt& o, int qlen, int tlen, int w, int end_bonus) {
   int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, o.e_ins);
@@ -331,10 +560,34 @@ __device__ __forceinline__ int rows_needed(const DevOpt& o, int qlen, int tlen, 
   return min(tlen, qlen + we + 1);
 }
 
+// Gather the target rows of one extension into the group's LDS row buffer:
+// row k is 2-strand coordinate x0 + dir*k.  Loop bounds are group-uniform and
+// the body branch-free (tail lanes re-write row n-1), and eight loads per lane
+// are issued before any is consumed: one HBM round trip per 8*G rows.
 template <int G>
 __device__ __forceinline__ void fill_target(uint8_t* tb, const DevRef& ref, int64_t x0, int dir, int n) {
   const int r = Grp<G>::lane();
-  for (int k = r; k < n; k += G) tb[k] = (uint8_t)pac_base2(ref.pac, ref.l_pac, x0 + (int64_t)dir * k);
+  const int64_t two1 = (ref.l_pac << 1) - 1;
+  for (int base = 0; base < n; base += 8 * G) {
+    uint32_t raw[8];
+    int sh[8];
+    bool rev[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int kk = min(base + m * G + r, n - 1);
+      const int64_t x = x0 + (int64_t)dir * kk;
+      rev[m] = x >= ref.l_pac;
+      const int64_t f = rev[m] ? two1 - x : x;
+      raw[m] = ref.pac[f >> 2];
+      sh[m] = (int)((~f & 3) << 1);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int kk = min(base + m * G + r, n - 1);
+      const int b = (raw[m] >> sh[m]) & 3;
+      tb[kk] = (uint8_t)(rev[m] ? 3 - b : b);
+    }
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -445,12 +698,13 @@ __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, D
 }
 
 // ------------------------------------------------------------ read order
-// Each read gets a sort key: [variant | shape], variant = narrowest kernel
-// whose G*C covers the read, shape = (left, right) query lengths of the first
-// chain's top seed — the first extension mem_chain2aln performs.  Sorting by it
-// puts reads whose DP tasks have similar row counts and column widths into the
-// same wave (a wave runs as long as its slowest group).  Reads without chains
-// sort last.  Per-variant counts are appended with wave-aggregated atomics.
+// Each read gets a sort key [variant | 0xffff - estimated cost], so one
+// ascending sort groups reads by kernel variant and orders each variant's
+// reads by DEcreasing expected DP work — longest-processing-time-first for
+// the dynamic per-XCD work queue of chain2aln_kernel, which keeps the tail of
+// the launch short.  The estimate uses the first chain's top seed (the first
+// extension mem_chain2aln performs): rows ~ qlen + 16 per side, each row
+// costing ~1 + qlen/64 wave-wide segments.  Reads without chains sort last.
 __global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* keys, int32_t* vals, int32_t* counts,
                                                         int64_t* stats) {
   const int rd = blockIdx.x * blockDim.x + threadIdx.x;
@@ -459,24 +713,26 @@ __global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* ke
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
     for (int k = kNumVariants - 1; k >= 0; --k)
       if (lq <= kVariants[k].G * kVariants[k].C) v = k;
-    uint32_t shape = 0x3fff;
+    uint32_t cost = 0;
     const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
+    int nseed = 0;
     for (int c = c0; c < c1; ++c) {
       const int s0 = b.chain_seed_off[c], s1 = b.chain_seed_off[c + 1];
-      if (s1 == s0) continue;
+      nseed += s1 - s0;
+      if (s1 == s0 || cost) continue;
       int best = s0;
       for (int k = s0 + 1; k < s1; ++k)
         if (b.seeds[k].score >= b.seeds[best].score) best = k;
       const bwagpu_seed_t t = b.seeds[best];
-      const int left = min(t.qbeg, 1023) >> 3, right = min(lq - t.qbeg - t.len, 1023) >> 3;
-      shape = (uint32_t)(left << 7 | right);
-      break;
+      const int left = t.qbeg, right = lq - t.qbeg - t.len;
+      cost = (uint32_t)((left ? (left + 16) * (1 + left / 64) : 0) + (right ? (right + 16) * (1 + right / 64) : 0) + 8);
     }
+    cost += (uint32_t)(c1 - c0) * 8 + (uint32_t)nseed;
     if (v < 0) {
       atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_LEN);
       v = kNumVariants - 1;
     }
-    keys[rd] = (uint32_t)v << 14 | shape;
+    keys[rd] = (uint32_t)v << 16 | (0xffffu - min(cost, 0xffffu));
     vals[rd] = rd;
   }
   const int lane = threadIdx.x & 63;
@@ -494,6 +750,13 @@ hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, in
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------ diagnostics
+// Optional per-read trace (bwagpu_debug_set_trace): 8 words per read index:
+// start/end s_memrealtime (100 MHz), DP rows, DP cells, HW_ID, XCC_ID.
+__device__ uint32_t* g_trace = nullptr;
+
+hipError_t set_trace(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p)); }
+
 // ------------------------------------------------------------ chain2aln
 template <int G, int C>
 __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref, DevBatch b,
@@ -504,91 +767,116 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
                                                            int32_t* out_n, int64_t* stats) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   using GR = Grp<G>;
-  constexpr int GPB = kBlock / G;
-  const int gib = threadIdx.x / G;
+  const int gib = guni<G>(threadIdx.x / G);
   const int r = GR::lane();
   int base = 0;
   for (int v = 0; v < variant; ++v) base += counts[v];
   const int n_list = counts[variant];
   Tally tl{0, 0, 0};
   uint8_t* tb = lds + gib * tb_bytes;
+  // Dynamic work queue, one head per XCD (counts[16 + 8*variant + shard]):
+  // shard x holds list positions x, x+8, x+16, ... (costliest first).  A wave
+  // starts on its own XCD's shard, so each head sees ~1/8 of the dequeues
+  // (MI355X_MICROARCH.md, "dequeue"), and moves on to the other shards when
+  // it runs dry — placement is never assumed, every position is taken exactly
+  // once by whichever waves exist.  A relaxed load skips exhausted heads.
+  const int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;  // HW_REG_XCC_ID
+  int32_t* heads = const_cast<int32_t*>(counts) + 16 + 8 * variant;
+  int shard = xcc, tried = 0;
+  const int leader = (gib * G) & 63;
 
-  for (int li = blockIdx.x * GPB + gib; li < n_list; li += gridDim.x * GPB) {
-    const int rd = read_list[base + li];
-    const int64_t qoff = b.seq_off[rd];
-    const int lq = (int)(b.seq_off[rd + 1] - qoff);
+  for (;;) {
+    int li = -1;
+    while (tried < 8) {
+      int32_t* h = heads + shard;
+      if ((__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / G) * 8 + shard < n_list) {
+        // every lane of the group adds 1: the compiler folds this into ONE
+        // wave-level atomic of the active-lane count (Guideline 12), so a
+        // group's increment is exactly G and its lane 0 sees the old value
+        const int slot = atomicAdd(h, 1);
+        li = (guni<G>(__shfl(slot, leader, 64)) / G) * 8 + shard;
+        if (li < n_list) break;
+      }
+      li = -1;
+      shard = (shard + 1) & 7;
+      ++tried;
+    }
+    if (li < 0) break;
+    const int rd = guni<G>(read_list[base + li]);
+    uint32_t* const trace = g_trace;
+    const uint64_t t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const long long tr_cells = tl.cells, tr_rows = tl.rows;
+    const int64_t qoff = guni64<G>(b.seq_off[rd]);
+    const int lq = guni<G>((int)(b.seq_off[rd + 1] - qoff));
     const uint8_t* q = b.seq + qoff;
-    const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
+    const int c0 = guni<G>(b.read_chain_off[rd]), c1 = guni<G>(b.read_chain_off[rd + 1]);
     bwagpu_alnreg_t* av = out + b.chain_seed_off[c0];
     int nreg = 0;
     for (int c = c0; c < c1; ++c) {
-      const int s0 = b.chain_seed_off[c], ns = b.chain_seed_off[c + 1] - s0;
+      const int s0 = guni<G>(b.chain_seed_off[c]), ns = guni<G>(b.chain_seed_off[c + 1]) - s0;
       if (ns == 0) continue;
-      const ChainWin cw = win[c];
+      ChainWin cw = win[c];
+      cw.lo = guni64<G>(cw.lo);
+      cw.hi = guni64<G>(cw.hi);
       if (cw.hi < cw.lo) continue;  // flagged by prep (reference would assert)
-      const int rid = b.chain_rid[c];
+      const int rid = guni<G>(b.chain_rid[c]);
       const float frac_rep = b.chain_frac_rep[c];
       uint64_t* key = srt + s0;
       const bwagpu_seed_t* sd = b.seeds + s0;
       for (int k = ns - 1; k >= 0; --k) {
         mem_fence_group();
         const uint64_t kk = __hip_atomic_load(&key[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const bwagpu_seed_t s = sd[(uint32_t)kk];
-        // containment test against the read's regions so far (bwamem.c:678-697)
+        bwagpu_seed_t s = sd[guni<G>((int)(uint32_t)kk)];
+        s.rbeg = guni64<G>(s.rbeg);
+        s.qbeg = guni<G>(s.qbeg);
+        s.len = guni<G>(s.len);
+        // containment test against the read's regions so far (bwamem.c:678-697).
+        // Lanes test regions in parallel; loop bounds are uniform and bodies
+        // branch-free so the read's control flow stays scalar.
         int hit = INT_MAX;
-        for (int base = 0; base < nreg && hit == INT_MAX; base += G) {
+        for (int base = 0; base < nreg; base += G) {
           const int i = base + r;
-          bool p = false;
-          if (i < nreg) {
-            const bwagpu_alnreg_t* pr = &av[i];
-            const int64_t prb = __hip_atomic_load(&pr->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int64_t pre = __hip_atomic_load(&pr->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int pqb = __hip_atomic_load(&pr->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int pqe = __hip_atomic_load(&pr->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int pw = __hip_atomic_load(&pr->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int psl = __hip_atomic_load(&pr->seedlen0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (!(s.rbeg < prb || s.rbeg + s.len > pre || s.qbeg < pqb || s.qbeg + s.len > pqe) &&
-                !(s.len - psl > .1 * lq)) {
-              int qd = s.qbeg - pqb;
-              int64_t rd64 = s.rbeg - prb;
-              int g = max_gap_len(o, qd < rd64 ? qd : (int)rd64);
-              int bw = g < pw ? g : pw;
-              if (qd - rd64 < bw && rd64 - qd < bw) p = true;
-              else {
-                qd = pqe - (s.qbeg + s.len);
-                rd64 = pre - (s.rbeg + s.len);
-                g = max_gap_len(o, qd < rd64 ? qd : (int)rd64);
-                bw = g < pw ? g : pw;
-                if (qd - rd64 < bw && rd64 - qd < bw) p = true;
-              }
-            }
-          }
-          hit = GR::gmin(p ? i : INT_MAX);
+          const bwagpu_alnreg_t* pr = &av[min(i, nreg - 1)];
+          const int64_t prb = __hip_atomic_load(&pr->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int64_t pre = __hip_atomic_load(&pr->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int pqb = __hip_atomic_load(&pr->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int pqe = __hip_atomic_load(&pr->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int pw = __hip_atomic_load(&pr->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int psl = __hip_atomic_load(&pr->seedlen0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const bool inside = !(s.rbeg < prb || s.rbeg + s.len > pre || s.qbeg < pqb || s.qbeg + s.len > pqe) &&
+                              !(s.len - psl > .1 * lq);
+          // ahead of the seed ...
+          const int qd1 = s.qbeg - pqb;
+          const int64_t rd1 = s.rbeg - prb;
+          const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
+          const int bw1 = g1 < pw ? g1 : pw;
+          // ... and behind it
+          const int qd2 = pqe - (s.qbeg + s.len);
+          const int64_t rd2 = pre - (s.rbeg + s.len);
+          const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
+          const int bw2 = g2 < pw ? g2 : pw;
+          const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+          hit = guni<G>(GR::gmin(i < nreg && inside && near ? i : INT_MAX));
+          if (hit != INT_MAX) break;
         }
         if (hit != INT_MAX) {
           // overlapping-seed check among seeds already visited (bwamem.c:698-707)
           int ov = INT_MAX;
-          for (int base = k + 1; base < ns && ov == INT_MAX; base += G) {
+          for (int base = k + 1; base < ns; base += G) {
             const int i = base + r;
-            bool p = false;
-            if (i < ns) {
-              const uint64_t ki = __hip_atomic_load(&key[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (ki != 0) {
-                const bwagpu_seed_t t = sd[(uint32_t)ki];
-                if (!(t.len < s.len * .95)) {
-                  if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
-                      (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg)
-                    p = true;
-                  else if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
-                           (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg)
-                    p = true;
-                }
-              }
-            }
-            ov = GR::gmin(p ? i : INT_MAX);
+            const uint64_t ki = __hip_atomic_load(&key[min(i, ns - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const bwagpu_seed_t t = sd[(uint32_t)ki];
+            const bool a = s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
+                           (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg;
+            const bool b2 = t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
+                            (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg;
+            const bool p = i < ns && ki != 0 && !(t.len < s.len * .95) && (a || b2);
+            ov = guni<G>(GR::gmin(p ? i : INT_MAX));
+            if (ov != INT_MAX) break;
           }
           if (ov == INT_MAX) {  // skip; mark like srt[k] = 0 (bwamem.c:709)
-            if (r == 0) __hip_atomic_store(&key[k], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // every lane stores the same word: no lane-divergent branch in the read's control flow
+            __hip_atomic_store(&key[k], (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             mem_fence_group();
             continue;
           }
@@ -621,7 +909,7 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
             aw[side] = o.w << t;
             const int nr = rows_needed(o, qlen, tlen, aw[side], eb);
             fill_target<G>(tb, ref, x0, dir, nr);
-            x = extend_group<G, C, false>(o, qlen, q, qa, dir, tlen, tb, aw[side], eb, o.zdrop, h0, tl);
+            x = extend_wave_dispatch<C, false>(o, qlen, q, qa, dir, tlen, tb, aw[side], eb, o.zdrop, h0, tl);
             score = x.score;
             if (score == prev || x.max_off < (aw[side] >> 1) + (aw[side] >> 2)) break;
           }
@@ -639,35 +927,49 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
         const int aw0 = aw[0], aw1 = aw[1];
         // seedcov (bwamem.c:784-788)
         long long cov = 0;
-        for (int i = r; i < ns; i += G) {
-          const bwagpu_seed_t t = sd[i];
-          if (t.qbeg >= qb && t.qbeg + t.len <= qe && t.rbeg >= rb && t.rbeg + t.len <= re) cov += t.len;
+        for (int base = 0; base < ns; base += G) {
+          const int i = base + r;
+          const bwagpu_seed_t t = sd[min(i, ns - 1)];
+          const bool in = i < ns && t.qbeg >= qb && t.qbeg + t.len <= qe && t.rbeg >= rb && t.rbeg + t.len <= re;
+          cov += in ? t.len : 0;
         }
         cov = grp_sum64(cov, G);
-        if (r == 0) {
-          bwagpu_alnreg_t a;
-          a.rb = rb;
-          a.re = re;
-          a.qb = qb;
-          a.qe = qe;
-          a.rid = rid;
-          a.score = score;
-          a.truesc = truesc;
-          a.sub = a.alt_sc = a.csub = a.sub_n = 0;
-          a.w = aw0 > aw1 ? aw0 : aw1;
-          a.seedcov = (int)cov;
-          a.secondary = a.secondary_all = 0;
-          a.seedlen0 = s.len;
-          a.n_comp_is_alt = 0;
-          a.frac_rep = frac_rep;
-          a.hash = 0;
-          av[nreg] = a;
+        {  // the 88-byte mem_alnreg_t as 22 dwords, lane d writes dword d (lanes >= 21 repeat the last)
+          const int d = r % G < 21 ? r % G : 21;
+          uint32_t v = 0;
+          v = d == 0 ? (uint32_t)rb : v;
+          v = d == 1 ? (uint32_t)((uint64_t)rb >> 32) : v;
+          v = d == 2 ? (uint32_t)re : v;
+          v = d == 3 ? (uint32_t)((uint64_t)re >> 32) : v;
+          v = d == 4 ? (uint32_t)qb : v;
+          v = d == 5 ? (uint32_t)qe : v;
+          v = d == 6 ? (uint32_t)rid : v;
+          v = d == 7 ? (uint32_t)score : v;
+          v = d == 8 ? (uint32_t)truesc : v;
+          v = d == 13 ? (uint32_t)(aw0 > aw1 ? aw0 : aw1) : v;
+          v = d == 14 ? (uint32_t)cov : v;
+          v = d == 17 ? (uint32_t)s.len : v;
+          v = d == 19 ? __float_as_uint(frac_rep) : v;
+          reinterpret_cast<uint32_t*>(&av[nreg])[d] = v;
         }
         ++nreg;
         mem_fence_group();
       }
     }
-    if (r == 0) out_n[rd] = nreg;
+    out_n[rd] = nreg;  // same value from every lane
+    if (trace) {
+      const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+      const int d = r % G < 7 ? r % G : 7;
+      uint32_t v = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      v = d == 0 ? (uint32_t)t_start : v;
+      v = d == 1 ? (uint32_t)(t_start >> 32) : v;
+      v = d == 2 ? (uint32_t)t_end : v;
+      v = d == 3 ? (uint32_t)(t_end >> 32) : v;
+      v = d == 4 ? (uint32_t)(tl.rows - tr_rows) : v;
+      v = d == 5 ? (uint32_t)(tl.cells - tr_cells) : v;
+      v = d == 6 ? __builtin_amdgcn_s_getreg((31 << 11) | 4) : v;  // HW_REG_HW_ID
+      trace[(size_t)rd * 8 + d] = v;
+    }
   }
   if (r != 0) tl = Tally{0, 0, 0};
   block_stats<G>(tl, stats);
@@ -698,11 +1000,14 @@ __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_e
       x = ExtOut{-1, 0, 0, 0, -1, 0};  // reference asserts h0 > 0 (ksw.c:385)
     } else {
       const int nr = rows_needed(o, t.qlen, t.tlen, t.w, t.end_bonus);
-      for (int i = r; i < nr; i += G) tb[i] = tp[i];
+      for (int base = 0; base < nr; base += G) {
+        const int i = min(base + r, nr - 1);
+        tb[i] = tp[i];
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      x = extend_group<G, C, T5>(o, t.qlen, q, 0, 1, t.tlen, tb, t.w, t.end_bonus, t.zdrop, t.h0, tl);
+      x = extend_wave_dispatch<C, T5>(o, t.qlen, q, 0, 1, t.tlen, tb, t.w, t.end_bonus, t.zdrop, t.h0, tl);
     }
     if (r == 0) res[k] = bwagpu_ext_result_t{x.score, x.qle, x.tle, x.gtle, x.gscore, x.max_off};
     if (r != 0) tl = Tally{0, 0, 0};
@@ -724,7 +1029,7 @@ static hipError_t launch_c2a_t(const DevOpt& o, const DevRef& ref, const DevBatc
                                const int32_t* cnt, int variant, int32_t n, int tb, const ChainWin* win, uint64_t* srt,
                                bwagpu_alnreg_t* out, int32_t* out_n, int64_t* stats, hipStream_t st) {
   constexpr int GPB = kBlock / G;
-  // grid-stride over the (device-side) list: the count is only known on the GPU
+  // persistent-style grid: the waves pull reads from the device-side queue
   const int nb = std::min((n + GPB - 1) / GPB, 2048);
   hipLaunchKernelGGL((chain2aln_kernel<G, C>), dim3(nb), dim3(kBlock), (size_t)GPB * tb, st, o, ref, b, list, cnt,
                      variant, tb, win, srt, out, out_n, stats);
@@ -737,8 +1042,8 @@ hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, con
                             int64_t* stats, hipStream_t st) {
   if (max_list == 0) return hipSuccess;
   switch (variant) {
-    case 0: return launch_c2a_t<16, 10>(o, ref, b, read_list, d_count, 0, max_list, tb_bytes, win, srt, out, out_n, stats, st);
-    case 1: return launch_c2a_t<32, 8>(o, ref, b, read_list, d_count, 1, max_list, tb_bytes, win, srt, out, out_n, stats, st);
+    case 0: return launch_c2a_t<64, 3>(o, ref, b, read_list, d_count, 0, max_list, tb_bytes, win, srt, out, out_n, stats, st);
+    case 1: return launch_c2a_t<64, 4>(o, ref, b, read_list, d_count, 1, max_list, tb_bytes, win, srt, out, out_n, stats, st);
     case 2: return launch_c2a_t<64, 16>(o, ref, b, read_list, d_count, 2, max_list, tb_bytes, win, srt, out, out_n, stats, st);
   }
   return hipErrorInvalidValue;
@@ -764,8 +1069,8 @@ hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t, const b
     return t5 ? launch_ext_t<G, C, true>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st) \
               : launch_ext_t<G, C, false>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st);
   switch (variant) {
-    EXT_CASE(0, 16, 10)
-    EXT_CASE(1, 32, 8)
+    EXT_CASE(0, 64, 3)
+    EXT_CASE(1, 64, 4)
     EXT_CASE(2, 64, 16)
   }
 #undef EXT_CASE

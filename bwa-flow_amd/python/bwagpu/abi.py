@@ -82,6 +82,7 @@ PROTOS = {
     "bwagpu_chain2aln_device": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP, _VP, _VP]),
     "bwagpu_extend_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),
     "bwagpu_last_stats": (C.c_int, [_VP, C.c_int, C.POINTER(Stats)]),
+    "bwagpu_debug_set_trace": (C.c_int, [_VP, _VP]),
 }
 
 _lib = None

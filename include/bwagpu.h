@@ -198,6 +198,13 @@ int bwagpu_extend_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_ext_tas
 
 int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
 
+/* diagnostics: while dev_ptr != NULL every chain2aln launch on this device
+   writes 8 x uint32 per read index r at dev_ptr[8r..8r+7]: start and end
+   s_memrealtime (100 MHz, lo/hi), DP rows, DP cells, HW_ID, XCC_ID.
+   Not part of the reference interface (the reference logs stage wall times
+   with getUs(), src/util.h:34-40). */
+int bwagpu_debug_set_trace(bwagpu_ctx_t *ctx, void *dev_ptr);
+
 #ifdef __cplusplus
 }
 #endif
