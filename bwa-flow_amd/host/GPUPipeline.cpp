@@ -1,0 +1,214 @@
+// GPUPipeline.cpp — see GPUPipeline.h.
+#include "GPUPipeline.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <deque>
+#include <stdexcept>
+#include <thread>
+
+#ifdef BWAFLOW_NATIVE_HEADERS
+#include "Pipeline.h"
+#else
+#include "cpu_stage.h"
+#endif
+
+// ------------------------------------------------------------------ GPUEnv
+GPUEnv::GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* pac, int max_devices,
+               int watchdog_ms) {
+  int n = 0;
+  const int rc = bwagpu_device_count(&n);
+  if (rc != BWAGPU_OK) {
+    status_ = "no GPU device (bwagpu_device_count rc=" + std::to_string(rc) + ")";
+    return;
+  }
+  for (int d = 0; d < n && d < max_devices; ++d) {
+    bwagpu_ctx_t* c = nullptr;
+    const int r = bwagpu_create(d, &opt, &bns, pac, &c);
+    if (r != BWAGPU_OK) {
+      status_ += "device " + std::to_string(d) + ": " + (c ? bwagpu_last_error(c) : "create failed") + "; ";
+      if (c) bwagpu_destroy(c);
+      continue;
+    }
+    bwagpu_set_watchdog_ms(c, watchdog_ms);  // fpgaHangError's 10 s watchdog (SWTask.cpp:116-122)
+    ctx_.push_back(c);
+  }
+  if (status_.empty()) status_ = std::to_string(ctx_.size()) + " device(s)";
+}
+
+GPUEnv::~GPUEnv() {
+  for (auto* c : ctx_) bwagpu_destroy(c);
+}
+
+// --------------------------------------------------------------- FlatBatch
+void FlatBatch::pack(const ChainsRecord& rec) {
+  const int nr = rec.batch_num;
+  seq_off.assign(1, 0);
+  read_chain_off.assign(1, 0);
+  chain_seed_off.assign(1, 0);
+  seq.clear();
+  chain_rid.clear();
+  chain_frac_rep.clear();
+  seeds.clear();
+  for (int i = 0; i < nr; ++i) {
+    const bseq1_t& s = rec.seqs[i];
+    seq.insert(seq.end(), (const uint8_t*)s.seq, (const uint8_t*)s.seq + s.l_seq);
+    seq_off.push_back((int64_t)seq.size());
+    const mem_chain_v& cv = rec.chains[i];
+    for (size_t j = 0; j < cv.n; ++j) {
+      const mem_chain_t& c = cv.a[j];
+      chain_rid.push_back(c.rid);
+      chain_frac_rep.push_back(c.frac_rep);
+      for (int k = 0; k < c.n; ++k) {
+        bwagpu_seed_t t{};
+        t.rbeg = c.seeds[k].rbeg;
+        t.qbeg = c.seeds[k].qbeg;
+        t.len = c.seeds[k].len;
+        t.score = c.seeds[k].score;
+        seeds.push_back(t);
+      }
+      chain_seed_off.push_back((int32_t)seeds.size());
+    }
+    read_chain_off.push_back((int32_t)chain_rid.size());
+  }
+  regs.assign(seeds.size() ? seeds.size() : 1, bwagpu_alnreg_t{});
+  n.assign(nr ? nr : 1, 0);
+  c = bwagpu_batch_t{};
+  c.n_reads = nr;
+  c.n_chains = (int32_t)chain_rid.size();
+  c.n_seeds = (int32_t)seeds.size();
+  c.seq_bytes = seq_off.back();
+  c.seq_off = seq_off.data();
+  c.seq = seq.data();
+  c.read_chain_off = read_chain_off.data();
+  c.chain_seed_off = chain_seed_off.data();
+  c.chain_rid = chain_rid.data();
+  c.chain_frac_rep = chain_frac_rep.data();
+  c.seeds = seeds.data();
+}
+
+mem_alnreg_v* FlatBatch::unpack(int batch_num) const {
+  mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
+  if (!av) throw std::runtime_error("Memory allocation failed");
+  for (int i = 0; i < batch_num; ++i) {
+    const size_t k = (size_t)n[i];
+    av[i].n = av[i].m = k;
+    av[i].a = nullptr;
+    if (k) {
+      av[i].a = (mem_alnreg_t*)malloc(sizeof(mem_alnreg_t) * k);
+      if (!av[i].a) throw std::runtime_error("Memory allocation failed");
+      memcpy(av[i].a, &regs[chain_seed_off[read_chain_off[i]]], sizeof(mem_alnreg_t) * k);
+    }
+  }
+  return av;
+}
+
+void freeChainsRecordChains(mem_chain_v* chains, int batch_num) {
+  if (!chains) return;
+  for (int i = 0; i < batch_num; ++i) {
+    for (size_t j = 0; j < chains[i].n; ++j) free(chains[i].a[j].seeds);
+    free(chains[i].a);
+  }
+  free(chains);
+}
+
+// ------------------------------------------------------- ChainsToRegionsGPU
+RegionsRecord ChainsToRegionsGPU::on_cpu(const ChainsRecord& rec) {
+  // finishUpOnCPU (FPGAPipeline.cpp:526-551): the whole record goes through
+  // the CPU stage's body; a GPU batch is all-or-nothing, so start_seq = 0
+  if (!cpu_stage_) throw std::runtime_error("GPU SW stage failed and no CPU stage to fall back to");
+  n_cpu_.fetch_add(1);
+  return cpu_stage_->compute(rec);
+}
+
+void ChainsToRegionsGPU::retire() {
+  // the last accelerator worker switches the CPU stage's accx dispatch off
+  // (FPGAPipeline.cpp:402-405, 528-529): queued records drain back to the CPU
+  if (--n_active_ == 0 && cpu_stage_) cpu_stage_->setUseAccx(false);
+}
+
+void ChainsToRegionsGPU::compute(int wid) {
+  bwagpu_ctx_t* ctx = env_ ? env_->ctx(wid) : nullptr;
+  if (!ctx) {  // no device for this worker: leave every record to the CPU
+    retire();
+    return;
+  }
+  // two records in flight (the SWTask ping-pong, FPGAPipeline.cpp:374-386):
+  // record k uses slot k&1; waits are FIFO, so that slot is free again
+  struct Job {
+    ChainsRecord rec;
+    FlatBatch flat;
+    int slot;
+  };
+  std::deque<Job> inflight;
+  long long submitted = 0;
+  bool more = true;
+  auto fail_all = [&](const char* what, int rc) {
+    // fpgaHangError / fpgaResultsError path: recompute what is in flight on
+    // the CPU, push it, retire this worker
+    (void)what;
+    (void)rc;
+    for (auto& j : inflight) pushOutput(on_cpu(j.rec));
+    inflight.clear();
+    retire();
+  };
+  for (;;) {
+    if (more && inflight.size() < BWAGPU_NUM_SLOTS) {
+      ChainsRecord rec;
+      bool ready = getInput(rec);
+      if (!ready && inflight.empty()) {
+        while (!ready && !isFinal()) {  // poll like FPGAPipeline.cpp:394-399
+          std::this_thread::sleep_for(std::chrono::microseconds(10));
+          ready = getInput(rec);
+        }
+      }
+      if (!ready && isFinal()) {
+        ready = getInput(rec);  // a record may have landed just before the final flag
+        if (!ready) more = false;
+      }
+      if (ready) {
+        inflight.push_back(Job{rec, FlatBatch{}, (int)(submitted & 1)});
+        Job& j = inflight.back();
+        j.flat.pack(j.rec);
+        const int rc = bwagpu_chain2aln_submit(ctx, j.slot, &j.flat.c);
+        if (rc == BWAGPU_E_UNSUPPORTED || rc == BWAGPU_E_INVAL) {
+          // this record only (e.g. a read longer than BWAGPU_MAX_READ_LEN):
+          // CPU path for it, the device stays in service
+          ChainsRecord r = j.rec;
+          inflight.pop_back();
+          pushOutput(on_cpu(r));
+          continue;
+        }
+        if (rc != BWAGPU_OK) {
+          fail_all("submit", rc);
+          return;
+        }
+        ++submitted;
+        continue;  // fill both slots before waiting
+      }
+    }
+    if (inflight.empty()) {
+      if (!more) break;
+      continue;
+    }
+    Job& j = inflight.front();
+    const int rc = bwagpu_chain2aln_wait(ctx, j.slot, j.flat.regs.data(), j.flat.n.data());
+    if (rc != BWAGPU_OK) {
+      fail_all("wait", rc);
+      return;
+    }
+    RegionsRecord out;
+    out.start_idx = j.rec.start_idx;
+    out.batch_num = j.rec.batch_num;
+    out.seqs = j.rec.seqs;
+    out.alnreg = j.flat.unpack(j.rec.batch_num);
+    freeChainsRecordChains(j.rec.chains, j.rec.batch_num);
+    out.chains = nullptr;
+    n_gpu_.fetch_add(1);
+    inflight.pop_front();
+    pushOutput(out);
+  }
+  retire();
+}

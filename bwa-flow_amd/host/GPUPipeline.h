@@ -1,0 +1,95 @@
+// GPUPipeline.h — the GPU back end of bwa-flow's SW stage (stage 4,
+// ChainsRecord -> RegionsRecord), in the place of src/fpga/FPGAPipeline.h.
+//
+//   GPUEnv               ~ BWAOCLEnv (src/fpga/BWAOCLEnv.h:41-114): one
+//                          bwagpu context per device, reference resident
+//   ChainsToRegionsGPU   ~ ChainsToRegionsFPGA (FPGAPipeline.h:14-31,
+//                          FPGAPipeline.cpp:367-579): same base class, same
+//                          constructor (n workers = n devices, CPU stage for
+//                          fallback), same compute(wid) protocol
+//
+// Results are bit-identical to ChainsToRegions::compute (src/Pipeline.cpp:
+// 503-544), including ownership: chains are freed and the output record's
+// chains is NULL; alnreg and every alnreg[i].a are malloc'd (freeAligns,
+// bwa_wrapper.cpp:824-830, can free them).
+#pragma once
+#include <atomic>
+#include <string>
+#include <vector>
+
+#include "bwagpu.h"
+#include "records.h"
+#ifdef BWAFLOW_NATIVE_HEADERS
+#include "kflow/MapPartitionStage.h"  // the reference's kestrelFlow
+#else
+#include "kflow.h"  // std::thread mirror of it
+#endif
+
+#ifndef COMPUTE_DEPTH
+#define COMPUTE_DEPTH 64
+#endif
+
+class ChainsToRegions;  // the CPU stage (src/Pipeline.h:162-171 / cpu_stage.h)
+
+// One bwagpu context per usable device.  Devices that fail to initialise are
+// skipped (their workers retire at once, like an FPGA env with fewer PEs).
+class GPUEnv {
+ public:
+  GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* pac, int max_devices = 8,
+         int watchdog_ms = 10000);
+  ~GPUEnv();
+  GPUEnv(const GPUEnv&) = delete;
+  GPUEnv& operator=(const GPUEnv&) = delete;
+
+  int num_devices() const { return (int)ctx_.size(); }
+  bwagpu_ctx_t* ctx(int i) const { return i >= 0 && i < (int)ctx_.size() ? ctx_[i] : nullptr; }
+  const std::string& status() const { return status_; }
+
+ private:
+  std::vector<bwagpu_ctx_t*> ctx_;
+  std::string status_;
+};
+
+// A ChainsRecord flattened into the ABI's offset arrays (bwagpu_batch_t).
+struct FlatBatch {
+  std::vector<int64_t> seq_off;
+  std::vector<uint8_t> seq;
+  std::vector<int32_t> read_chain_off, chain_seed_off, chain_rid;
+  std::vector<float> chain_frac_rep;
+  std::vector<bwagpu_seed_t> seeds;
+  std::vector<bwagpu_alnreg_t> regs;  // output slots (one per seed)
+  std::vector<int32_t> n;             // regions per read
+  bwagpu_batch_t c{};
+
+  void pack(const ChainsRecord& rec);  // ~ packReadData (FPGAPipeline.cpp:194-343)
+  // ~ processOutput (FPGAPipeline.cpp:29-130): regions into malloc'd mem_alnreg_v
+  mem_alnreg_v* unpack(int batch_num) const;
+};
+
+// frees the chains of a record the way ChainsToRegions::compute does
+void freeChainsRecordChains(mem_chain_v* chains, int batch_num);
+
+class ChainsToRegionsGPU
+    : public kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH> {
+ public:
+  ChainsToRegionsGPU(int n = 1, ChainsToRegions* stage = nullptr, GPUEnv* env = nullptr)
+      : kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH>(n, false),
+        n_active_(n),
+        cpu_stage_(stage),
+        env_(env) {}
+
+  void compute(int wid) override;
+
+  // counters (tests / logging)
+  int records_on_gpu() const { return n_gpu_.load(); }
+  int records_on_cpu() const { return n_cpu_.load(); }
+
+ private:
+  RegionsRecord on_cpu(const ChainsRecord& rec);
+  void retire();
+
+  std::atomic<int> n_active_;
+  ChainsToRegions* cpu_stage_;
+  GPUEnv* env_;
+  std::atomic<int> n_gpu_{0}, n_cpu_{0};
+};

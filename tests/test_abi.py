@@ -4,6 +4,7 @@ No compute calls here (no GPU in the CPU tier)."""
 import ctypes as C
 import os
 import re
+import shutil
 import subprocess
 import tempfile
 
@@ -36,8 +37,12 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_library_is_gfx950_code_object():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", abi.lib_path()],
-                         capture_output=True, text=True, cwd=tempfile.gettempdir())
+    # llvm-objdump extracts the bundled code objects next to its input: work on a copy
+    with tempfile.TemporaryDirectory() as td:
+        lib = os.path.join(td, "libbwagpu.so")
+        shutil.copy(abi.lib_path(), lib)
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                             capture_output=True, text=True, cwd=td)
     assert "gfx950" in (out.stdout + out.stderr)
 
 
