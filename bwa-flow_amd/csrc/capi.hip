@@ -91,7 +91,7 @@ struct InLayout {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
-  DevBuf d_in, d_win, d_srt, d_out, d_n, d_stats, d_lists, d_counts, d_sort_tmp;
+  DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts, d_sort_tmp;
   HostBuf h_in, h_out, h_n, h_stats;
   bool busy = false;
   int32_t n_reads = 0, n_seeds = 0;
@@ -154,6 +154,12 @@ bool make_opt(const bwagpu_opt_t* o, DevOpt* d, std::string* why) {
   for (int i = 0; i < 25; ++i) mx = std::max<int>(mx, o->mat[i]);
   d->max_mat = mx;
   memcpy(d->mat, o->mat, 25);
+  for (int q = 0; q < 5; ++q) {
+    uint32_t w = 0;
+    for (int t = 0; t < 4; ++t) w |= (uint32_t)(uint8_t)o->mat[t * 5 + q] << (8 * t);
+    d->qprof[q] = w;
+    d->qprof4[q] = o->mat[20 + q];
+  }
   return true;
 }
 
@@ -199,7 +205,8 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   (void)hipSetDevice(ctx->device);
   for (auto& s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    s.d_in.release(); s.d_win.release(); s.d_srt.release(); s.d_out.release(); s.d_n.release();
+    s.d_in.release(); s.d_win.release(); s.d_srt.release(); s.d_prog.release(); s.d_desc.release();
+    s.d_out.release(); s.d_n.release();
     s.d_stats.release(); s.d_lists.release(); s.d_counts.release(); s.d_sort_tmp.release();
     s.h_in.release(); s.h_out.release(); s.h_n.release(); s.h_stats.release();
     if (s.ev0) (void)hipEventDestroy(s.ev0);
@@ -274,7 +281,9 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
                       int32_t* d_n, int64_t* d_stats, hipStream_t st) {
   HIPC(s.d_win.ensure(sizeof(ChainWin) * (size_t)std::max(db.n_chains, 1)), "hipMalloc(win)");
   HIPC(s.d_srt.ensure(sizeof(uint64_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(srt)");
+  HIPC(s.d_prog.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(prog)");
   const size_t nr = (size_t)std::max(db.n_reads, 1);
+  HIPC(s.d_desc.ensure(sizeof(ReadDesc) * nr), "hipMalloc(desc)");
   // keys_in | vals_in | keys_out | vals_out, n_reads each
   HIPC(s.d_lists.ensure(4 * sizeof(int32_t) * nr), "hipMalloc(lists)");
   uint32_t* keys_in = s.d_lists.as<uint32_t>();
@@ -289,21 +298,32 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   HIPC(s.d_counts.ensure(sizeof(int32_t) * 64), "hipMalloc(counts)");
   HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * 64, st), "memset counts");
   if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
-  HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, 0, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(), d_stats, st),
+  HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(),
+                         s.d_prog.as<bwagpu_seed_t>(), d_stats, st),
        "chain_prep launch");
   HIPC(launch_read_keys(db, keys_in, vals_in, s.d_counts.as<int32_t>(), d_stats, st), "read_keys launch");
   if (db.n_reads) {
     size_t tb2 = s.d_sort_tmp.cap;
     HIPC(sort_reads(s.d_sort_tmp.p, tb2, keys_in, keys_out, vals_in, vals_out, db.n_reads, st), "sort reads");
+    HIPC(launch_read_desc(db, vals_out, s.d_desc.as<ReadDesc>(), st), "read_desc launch");
   }
+  C2AArgs a;
+  a.read_list = vals_out;
+  a.desc = s.d_desc.as<ReadDesc>();
+  a.counts = s.d_counts.as<int32_t>();
+  a.win = s.d_win.as<ChainWin>();
+  a.srt = s.d_srt.as<uint64_t>();
+  a.prog = s.d_prog.as<bwagpu_seed_t>();
+  a.out = d_out;
+  a.out_n = d_n;
+  a.stats = d_stats;
   for (int v = 0; v < kNumVariants; ++v) {
     const int lqv = std::min(lq_max, kVariants[v].max_len());
     const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
-    const int gpb = kBlock / kVariants[v].G;
-    if ((size_t)tb * gpb > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
-    HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, vals_out, s.d_counts.as<int32_t>(), db.n_reads, tb,
-                          s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(), d_out, d_n, d_stats, st),
-         "chain2aln launch");
+    const size_t lds = kVariants[v].fast ? (size_t)(kBlock / 64) * (kSeqLds + 2 * tb)
+                                         : (size_t)tb * (kBlock / kVariants[v].G);
+    if (lds > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
+    HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, db.n_reads, tb, a, st), "chain2aln launch");
   }
   return BWAGPU_OK;
 }

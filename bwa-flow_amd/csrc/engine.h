@@ -13,6 +13,23 @@ struct DevOpt {
   int a, o_del, e_del, o_ins, e_ins, oe_del, oe_ins;
   int pen_clip5, pen_clip3, w, zdrop, max_mat;
   int8_t mat[28];
+  // query profile words: qprof[q] byte t = mat[t*5 + q] (t = target base 0..3),
+  // qprof4[q] = mat[20 + q] (target N; only bare task lists can hold one —
+  // targets fetched from the pac are 0..3).  Kernel arguments, so the DP picks
+  // its scores with register selects instead of loads.
+  uint32_t qprof[5];
+  int32_t qprof4[5];
+};
+
+// One read in processing order (chain2aln_fast_kernel), written after the sort.
+struct ReadDesc {
+  int64_t qoff;    // first base in seq
+  int32_t rd;      // read index
+  int32_t lq;      // read length
+  int32_t c0;      // first chain
+  int32_t nch;     // chains
+  int32_t s0;      // first seed slot (= first output slot)
+  int32_t ns;      // seeds over all chains
 };
 
 // Per-chain window computed by the prep kernel: [lo, hi) in the 2-strand
@@ -49,15 +66,20 @@ enum { ERR_RID = 1, ERR_LEN = 2 };
 // A read of length l needs G*C >= l (+1 column for eh[qlen], qlen <= l-1).
 struct Variant {
   int G, C;
+  bool fast;  // chain2aln_fast_kernel (register-resident read) vs the generic kernel
   int max_len() const { return G * C; }
 };
+// limits of the fast kernel: one lane per seed / chain / region of a read
+constexpr int kFastMaxSeeds = 64;
+constexpr int kFastMaxChains = 64;
+constexpr int kSeqLds = 256;  // LDS bytes for the read's bases (fast variants: lq <= 256)
 constexpr int kNumVariants = 3;
 extern const Variant kVariants[kNumVariants];
 constexpr int kBlock = 256;  // threads per workgroup (4 waves)
 
 // host-side launchers (sw_kernels.hip)
-hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, int64_t lq_cap,
-                             ChainWin* win, uint64_t* srt, int64_t* stats, hipStream_t st);
+hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, ChainWin* win, uint64_t* srt,
+                             bwagpu_seed_t* prog, int64_t* stats, hipStream_t st);
 // per-read sort keys [variant | task shape] + per-variant counts
 hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, int32_t* counts, int64_t* stats,
                             hipStream_t st);
@@ -67,10 +89,22 @@ hipError_t sort_reads(void* temp, size_t& temp_bytes, const uint32_t* keys_in, u
 // read_list: reads sorted by key; d_count: per-variant counts (device); the
 // variant's reads start at the sum of the lower variants' counts; max_list
 // bounds the grid
-hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b,
-                            const int32_t* read_list, const int32_t* d_count, int32_t max_list,
-                            int tb_bytes, const ChainWin* win, uint64_t* srt, bwagpu_alnreg_t* out,
-                            int32_t* out_n, int64_t* stats, hipStream_t st);
+// everything a chain2aln launch reads/writes besides the batch itself
+struct C2AArgs {
+  const int32_t* read_list;   // reads in processing order (sorted by key)
+  const ReadDesc* desc;       // the same order, as descriptors (fast kernel)
+  int32_t* counts;            // [0..15] per-variant counts, [16 + 8v + xcc] queue heads
+  const ChainWin* win;        // per chain
+  uint64_t* srt;              // per seed, sorted keys (generic kernel)
+  const bwagpu_seed_t* prog;  // per seed, processing order, pad_ = 1 for key 0 (fast kernel)
+  bwagpu_alnreg_t* out;
+  int32_t* out_n;
+  int64_t* stats;
+};
+hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b, int32_t max_list,
+                            int tb_bytes, const C2AArgs& a, hipStream_t st);
+// descriptors of the sorted reads
+hipError_t launch_read_desc(const DevBatch& b, const int32_t* sorted_reads, ReadDesc* desc, hipStream_t st);
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,

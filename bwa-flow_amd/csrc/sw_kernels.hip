@@ -37,7 +37,7 @@
 
 namespace bwagpu {
 
-const Variant kVariants[kNumVariants] = {{64, 3}, {64, 4}, {64, 16}};
+const Variant kVariants[kNumVariants] = {{64, 3, true}, {64, 4, true}, {64, 16, false}};
 
 // ---------------------------------------------------------------- group ops
 // Cross-lane primitives restricted to one group.  G = 16 is exactly one DPP
@@ -206,6 +206,25 @@ __device__ __forceinline__ int max_gap_len(const DevOpt& o, int qlen) {
   return l < (o.w << 1) ? l : (o.w << 1);
 }
 
+// query profile of base q (0..4): byte t = mat[t*5 + q]; selects over kernel
+// arguments (SGPRs), no memory traffic
+__device__ __forceinline__ uint32_t qprof_word(const DevOpt& o, int q) {
+  uint32_t v = o.qprof[0];
+  v = q == 1 ? o.qprof[1] : v;
+  v = q == 2 ? o.qprof[2] : v;
+  v = q == 3 ? o.qprof[3] : v;
+  v = q == 4 ? o.qprof[4] : v;
+  return v;
+}
+__device__ __forceinline__ int qprof4_val(const DevOpt& o, int q) {
+  int v = o.qprof4[0];
+  v = q == 1 ? o.qprof4[1] : v;
+  v = q == 2 ? o.qprof4[2] : v;
+  v = q == 3 ? o.qprof4[3] : v;
+  v = q == 4 ? o.qprof4[4] : v;
+  return v;
+}
+
 struct ExtOut {
   int score, qle, tle, gtle, gscore, max_off;
 };
@@ -215,182 +234,6 @@ struct Tally {
 };
 
 constexpr int NEG = -(1 << 29);
-
-// ----------------------------------------------------------- ksw_extend2
-// One ksw_extend2 call (bwa/ksw.c:380-479) on a group of G lanes.
-//   query column j = qp[qa + qd*j]  (qd = -1 walks the read leftwards)
-//   tb             = LDS row buffer holding the target base of every row the
-//                    call can reach (filled by the caller)
-// Lane r owns columns [r*Cd, r*Cd+Cd), Cd = ceil((qlen+1)/G) <= C; column
-// qlen is eh[qlen] of the reference.  Column loops run to the wave-uniform
-// CdW = max Cd over the wave's groups, so they branch on scalars.
-template <int G, int C, bool T5>
-__device__ __forceinline__ ExtOut extend_group(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
-                                            int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
-                                            int h0, Tally& tl) {
-  using GR = Grp<G>;
-  qlen = guni<G>(qlen);
-  qa = guni<G>(qa);
-  qd = guni<G>(qd);
-  tlen = guni<G>(tlen);
-  w = guni<G>(w);
-  end_bonus = guni<G>(end_bonus);
-  zdrop = guni<G>(zdrop);
-  h0 = guni<G>(h0);
-  const int r = GR::lane();
-  const int Cd = (qlen + G) / G;
-  const int CdW = wave_umax<G>(Cd);
-  const int jb = r * Cd;  // first column of this lane
-  // hi / Cd as a multiply-shift: exact for hi < 1024, Cd <= 16
-  const int cd_inv = (65536 + Cd - 1) / Cd;
-  const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
-
-  int hh[C], ee[C], jE[C], jm1E[C];
-  uint32_t pf[C];
-  uint32_t pf4[T5 ? C : 1];
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    if (c < CdW) {
-      const int j = jb + c;
-      const int qb = (c < Cd && j < qlen) ? qp[qa + qd * j] : 0;
-      const int8_t* m = o.mat;
-      // query profile of this column for target bases 0..3 (4 x int8)
-      pf[c] = (uint32_t)(uint8_t)m[qb] | (uint32_t)(uint8_t)m[5 + qb] << 8 |
-              (uint32_t)(uint8_t)m[10 + qb] << 16 | (uint32_t)(uint8_t)m[15 + qb] << 24;
-      if (T5) pf4[c] = (uint32_t)(uint8_t)m[20 + qb];
-      // row -1 of eh[] (ksw.c:392-395): H(-1,-1)=h0, then an insertion gap
-      const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
-      hh[c] = (c < Cd && j <= qlen) ? v : 0;
-      ee[c] = 0;
-      // scan offsets: u_j = t_j + j*e_ins; columns past this lane's block never
-      // contribute (NEG), F_j = max_{k<j} u_k - (j-1)*e_ins
-      jE[c] = c < Cd ? j * e_ins : NEG;
-      jm1E[c] = (j - 1) * e_ins;
-    }
-  }
-  {  // band clamp (ksw.c:399-407)
-    const int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
-    const int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
-    w = min(w, min(mi, md));
-  }
-
-  int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0, lo = 0, hi = qlen;
-  int cells = 0, rows = 0;
-  int tnext = tlen > 0 ? tb[0] : 0;
-  for (int i = 0; i < tlen; ++i) {
-    const int t = tnext;
-    tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
-    lo = max(lo, i - w);
-    hi = min(min(hi, i + w + 1), qlen);
-    const int left0 = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
-    const int sh = (t & 3) << 3;
-    // this lane's in-band columns: clo <= c < chi; cend = the column of eh[hi]
-    const int clo = max(lo - jb, 0), chi = min(hi - jb, Cd), cend = hi - jb;
-    const bool empty = hi <= lo;
-
-    // pass 1: M = H(i-1,j-1)+S (0 if H(i-1,j-1)==0), u = t + j*e_ins for the F scan
-    int M[C], U[C];
-    int run = NEG;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (c < CdW) {
-        int sc;
-        if (T5 && t == 4) sc = (int)(int8_t)(pf4[c] & 0xff);
-        else sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
-        const int m = hh[c] ? hh[c] + sc : 0;
-        M[c] = m;
-        const bool inb = c >= clo && c < chi;
-        const int u = (inb ? max(m - oe_ins, 0) : 0) + jE[c];
-        U[c] = u;
-        run = max(run, u);
-      }
-    }
-    // F(i,j) = max_{k<j} u_k - (j-1)*e_ins  (the reference's f recurrence, ksw.c:444-447;
-    // at j == 0 it comes out negative, which max(M, E>=0, F) ignores exactly like F=0)
-    int run2 = GR::excl_max(run, NEG);
-
-    // pass 2: H, E, row max key; next-row state of each column (ksw.c:429,449):
-    //   in band:  eh[j] <- {H(i,j-1) (first-column value at j == lo), E(i+1,j)}
-    //   j == hi:  eh[hi] <- {H(i,hi-1) (first-column value if the band is empty), 0}
-    int prevH = 0, lastH = 0, rkey = 0, en0 = 0, hcol = 0;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (c < CdW) {
-        const int j = jb + c;
-        const bool inb = c >= clo && c < chi;
-        const int f = run2 - jm1E[c];
-        run2 = max(run2, U[c]);
-        const int h = max(max(M[c], ee[c]), f);
-        const int en = max(max(ee[c] - e_del, M[c] - oe_del), 0);
-        rkey = max(rkey, inb ? ((h << 10) | j) : 0);
-        if (c == 0) {
-          en0 = en;
-        } else {
-          const bool isend = c == cend;
-          const int hnew = (j == lo || (isend && empty)) ? left0 : prevH;
-          hh[c] = (inb || isend) ? hnew : hh[c];
-          ee[c] = inb ? en : (isend ? 0 : ee[c]);
-          hcol = isend ? hh[c] : hcol;
-        }
-        prevH = h;
-        lastH = c == Cd - 1 ? h : lastH;
-      }
-    }
-    {  // column 0 of the lane takes the previous lane's last H
-      const int hl = GR::up1(lastH);
-      const bool inb = 0 >= clo && 0 < chi;
-      const bool isend = cend == 0;
-      const int hnew = (jb == lo || (isend && empty)) ? left0 : hl;
-      hh[0] = (inb || isend) ? hnew : hh[0];
-      ee[0] = inb ? en0 : (isend ? 0 : ee[0]);
-      hcol = isend ? hh[0] : hcol;
-    }
-    rkey = GR::gmax(rkey);
-    rows += 1;
-    cells += empty ? 0 : hi - lo;
-    const int mrow = rkey >> 10, mj = rkey & 1023;
-    {  // ksw.c:450-453; h1 now sits in eh[hi]
-      const bool endrow = max(lo, hi) == qlen;
-      const int h1 = GR::bcast(hcol, (hi * cd_inv) >> 16);  // owner lane of column hi
-      ei = (endrow && !(esc > h1)) ? i : ei;
-      esc = endrow ? max(esc, h1) : esc;
-    }
-    if (mrow == 0) break;
-    const bool better = mrow > best;
-    {
-      const int di = i - bi, dj = mj - bj;
-      const int drop = di > dj ? best - mrow - (di - dj) * e_del : best - mrow - (dj - di) * e_ins;
-      if (!better && zdrop > 0 && drop > zdrop) break;
-    }
-    off = better ? max(off, abs(mj - i)) : off;
-    bi = better ? i : bi;
-    bj = better ? mj : bj;
-    best = better ? mrow : best;
-    // zero-trim the band (ksw.c:466-469): first non-zero column in [lo,hi),
-    // last non-zero column in [lo,hi]
-    uint32_t nzb = 0;
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-      if (c < CdW) nzb |= (uint32_t)min((uint32_t)(hh[c] | ee[c]), 1u) << c;
-    const int cincl = min(cend + 1, Cd);
-    const uint32_t mlo = clo >= 32 ? 0u : ~0u << clo;
-    const uint32_t mhi = chi <= 0 ? 0u : (chi >= 32 ? ~0u : (1u << chi) - 1u);
-    const uint32_t mhi2 = cincl <= 0 ? 0u : (cincl >= 32 ? ~0u : (1u << cincl) - 1u);
-    const uint32_t bf = nzb & mlo & mhi, bl = nzb & mlo & mhi2;
-    int nzf = bf ? jb + __builtin_ctz(bf) : INT_MAX;
-    int nzl = bl ? jb + 31 - __builtin_clz(bl) : -1;
-    nzf = GR::gmin(nzf);
-    nzl = GR::gmax(nzl);
-    const int nlo = nzf == INT_MAX ? hi : nzf;
-    const int jl = nzl >= 0 ? nzl : nlo - 1;
-    lo = nlo;
-    hi = min(jl + 2, qlen);
-  }
-  tl.cells += cells;
-  tl.rows += rows;
-  tl.calls += 1;
-  return ExtOut{best, bj + 1, bi + 1, ei + 1, esc, off};
-}
 
 // ------------------------------------------------ ksw_extend2, one read per wave
 // The G = 64 form used by every production kernel.  Columns are STRIDED over
@@ -418,10 +261,8 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   for (int c = 0; c < CD; ++c) {
     const int j = 64 * c + r;
     const int qb = j < qlen ? qp[qa + qd * j] : 0;
-    const int8_t* m = o.mat;
-    pf[c] = (uint32_t)(uint8_t)m[qb] | (uint32_t)(uint8_t)m[5 + qb] << 8 |
-            (uint32_t)(uint8_t)m[10 + qb] << 16 | (uint32_t)(uint8_t)m[15 + qb] << 24;
-    if (T5) pf4[c] = (uint32_t)(uint8_t)m[20 + qb];
+    pf[c] = qprof_word(o, qb);
+    if (T5) pf4[c] = (uint32_t)(uint8_t)qprof4_val(o, qb);
     // row -1 of eh[] (ksw.c:392-395): H(-1,-1)=h0, then an insertion gap
     const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
     hh[c] = j <= qlen ? v : 0;
@@ -622,7 +463,7 @@ __device__ void block_stats(const Tally& tl, int64_t* stats) {
 // (bwamem.c:648-668, with bns_fetch_seq's contig clipping) and the seed order
 // (srt[] = score<<32|i ascending, bwamem.c:671-674).
 __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, DevBatch b, ChainWin* win,
-                                                         uint64_t* srt, int64_t* stats) {
+                                                         uint64_t* srt, bwagpu_seed_t* prog, int64_t* stats) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= b.n_chains) return;
   const int s0 = b.chain_seed_off[c], s1 = b.chain_seed_off[c + 1], ns = s1 - s0;
@@ -695,6 +536,15 @@ __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, D
     a[n] = t;
     sift(0, n);
   }
+  // the seeds in processing order (descending key, bwamem.c:676); pad_ flags
+  // the key that is 0 from the start, which the overlap test skips like a
+  // marked seed (bwamem.c:700)
+  for (int t = 0; t < ns; ++t) {
+    const uint64_t k = a[ns - 1 - t];
+    bwagpu_seed_t v = b.seeds[s0 + (uint32_t)k];
+    v.pad_ = k == 0 ? 1 : 0;
+    prog[s0 + t] = v;
+  }
 }
 
 // ------------------------------------------------------------ read order
@@ -711,10 +561,12 @@ __global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* ke
   int v = -1;
   if (rd < b.n_reads) {
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
-    for (int k = kNumVariants - 1; k >= 0; --k)
-      if (lq <= kVariants[k].G * kVariants[k].C) v = k;
-    uint32_t cost = 0;
     const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
+    const int nseeds = b.chain_seed_off[c1] - b.chain_seed_off[c0];
+    const bool small = nseeds <= kFastMaxSeeds && c1 - c0 <= kFastMaxChains;
+    for (int k = kNumVariants - 1; k >= 0; --k)
+      if (lq <= kVariants[k].G * kVariants[k].C && (small || !kVariants[k].fast)) v = k;
+    uint32_t cost = 0;
     int nseed = 0;
     for (int c = c0; c < c1; ++c) {
       const int s0 = b.chain_seed_off[c], s1 = b.chain_seed_off[c + 1];
@@ -747,6 +599,31 @@ hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, in
                             hipStream_t st) {
   if (b.n_reads == 0) return hipSuccess;
   hipLaunchKernelGGL(read_keys_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, keys, vals, counts, stats);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ read descriptors
+// The sorted read order as self-contained descriptors: the fast kernel loads
+// one with a single scalar load instead of a chain of dependent lookups.
+__global__ void __launch_bounds__(256) read_desc_kernel(DevBatch b, const int32_t* __restrict__ sorted,
+                                                        ReadDesc* desc) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.n_reads) return;
+  const int rd = sorted[p];
+  ReadDesc d;
+  d.qoff = b.seq_off[rd];
+  d.rd = rd;
+  d.lq = (int)(b.seq_off[rd + 1] - d.qoff);
+  d.c0 = b.read_chain_off[rd];
+  d.nch = b.read_chain_off[rd + 1] - d.c0;
+  d.s0 = b.chain_seed_off[d.c0];
+  d.ns = b.chain_seed_off[d.c0 + d.nch] - d.s0;
+  desc[p] = d;
+}
+
+hipError_t launch_read_desc(const DevBatch& b, const int32_t* sorted, ReadDesc* desc, hipStream_t st) {
+  if (b.n_reads == 0) return hipSuccess;
+  hipLaunchKernelGGL(read_desc_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, sorted, desc);
   return hipGetLastError();
 }
 
@@ -975,6 +852,264 @@ __global__ void __launch_bounds__(kBlock) chain2aln_kernel(DevOpt o, DevRef ref,
   block_stats<G>(tl, stats);
 }
 
+// ------------------------------------------------------------ chain2aln, fast
+// Both extensions' target rows of one seed in ONE HBM round trip: left rows
+// x0l - k (k < nl) into tbl, right rows x0r + k (k < nr) into tbr.
+__device__ __forceinline__ void fill_two(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
+                                         const DevRef& ref) {
+  const int r = (int)(threadIdx.x & 63);
+  const int64_t two1 = (ref.l_pac << 1) - 1;
+  const int n = max(nl, nr);
+  for (int base = 0; base < n; base += 256) {
+    uint32_t raw[8];
+    int sh[8], kk[8];
+    bool rev[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const bool left = m < 4;
+      const int nn = left ? nl : nr;
+      const int k = min(base + (m & 3) * 64 + r, max(nn - 1, 0));
+      kk[m] = k;
+      const int64_t x = left ? x0l - k : x0r + k;
+      rev[m] = x >= ref.l_pac;
+      int64_t f = rev[m] ? two1 - x : x;
+      f = f < 0 ? 0 : (f >= ref.l_pac ? ref.l_pac - 1 : f);  // only for an empty side (nn == 0)
+      raw[m] = ref.pac[f >> 2];
+      sh[m] = (int)((~f & 3) << 1);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int bse = (raw[m] >> sh[m]) & 3;
+      const uint8_t v = (uint8_t)(rev[m] ? 3 - bse : bse);
+      if (m < 4) {
+        if (nl > 0) tbl[kk[m]] = v;
+      } else {
+        if (nr > 0) tbr[kk[m]] = v;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), l);
+  return (int64_t)((uint64_t)hi << 32 | lo);
+}
+
+// mem_chain2aln for reads of <= 256 bp with <= 64 seeds and chains: one read
+// per wave with the whole read register-resident, so a read costs one round
+// trip for its data (descriptor, seeds, chains, bases — issued together) plus
+// one per extended seed (both target windows), instead of a dependent load
+// chain per seed:
+//   lane i   holds the read's i-th seed in processing order (prog, written by
+//            chain_prep_kernel: chains in order, seeds by descending key),
+//            chain i's window/rid/frac_rep/seed range, and region i once made;
+//   LDS      holds the read's bases (the query of both extensions) and the two
+//            target row buffers.
+// Containment (bwamem.c:678-697), the overlap test (698-707) and seedcov
+// (784-788) are lane-parallel tests + one ballot / reduction.  Work is pulled
+// from the per-XCD queue heads; the next ticket is taken while the current
+// read runs.
+template <int C>
+__global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
+                                                                int variant, int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int r = (int)(threadIdx.x & 63);
+  const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint8_t* const sq = lds + wib * (kSeqLds + 2 * tb_bytes);
+  uint8_t* const tbl = sq + kSeqLds;
+  uint8_t* const tbr = tbl + tb_bytes;
+  int base = 0;
+  for (int v = 0; v < variant; ++v) base += a.counts[v];
+  const int n_list = a.counts[variant];
+  Tally tl{0, 0, 0};
+  // queue: shard x holds list positions x, x+8, ... (see chain2aln_kernel);
+  // all 64 lanes add 1 -> one wave-level atomic of 64, lane 0 sees the old value
+  const int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;  // HW_REG_XCC_ID
+  int32_t* const heads = a.counts + 16 + 8 * variant;
+  int shard = xcc, tried = 0;
+  int li = -1;
+  while (tried < 8) {
+    const int slot = atomicAdd(heads + shard, 1);
+    li = (__builtin_amdgcn_readfirstlane(slot) >> 6) * 8 + shard;
+    if (li < n_list) break;
+    li = -1;
+    shard = (shard + 1) & 7;
+    ++tried;
+  }
+
+  while (li >= 0) {
+    const int slot_next = atomicAdd(heads + shard, 1);  // consumed at the end of this read
+    const ReadDesc d = a.desc[base + li];
+    const int rd = __builtin_amdgcn_readfirstlane(d.rd);
+    const int lq = __builtin_amdgcn_readfirstlane(d.lq);
+    const int nch = __builtin_amdgcn_readfirstlane(d.nch);
+    const int ns = __builtin_amdgcn_readfirstlane(d.ns);
+    const int s0 = __builtin_amdgcn_readfirstlane(d.s0);
+    int nreg = 0;
+    if (ns > 0) {
+      // ---- the read's data, all loads issued before any is used
+      const bwagpu_seed_t* pg = a.prog + s0;
+      const int ie = min(r, ns - 1);
+      const int64_t p_rb = pg[ie].rbeg;
+      const int p_qb = pg[ie].qbeg, p_len = pg[ie].len, p_flag = pg[ie].pad_;
+      const int cc = d.c0 + min(r, nch - 1);
+      const int c_s0 = b.chain_seed_off[cc] - s0, c_s1 = b.chain_seed_off[cc + 1] - s0;
+      const ChainWin c_w = a.win[cc];
+      const int c_rid = b.chain_rid[cc];
+      const float c_frac = b.chain_frac_rep[cc];
+      {
+        const uint8_t* q = b.seq + d.qoff;
+        uint32_t wv = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wv |= (uint32_t)q[min(4 * r + k, lq - 1)] << (8 * k);
+        reinterpret_cast<uint32_t*>(sq)[r] = wv;  // 64 lanes x 4 B = kSeqLds
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      // regions made so far: lane i holds region i
+      int64_t R_rb = 0, R_re = 0;
+      int R_qb = 0, R_qe = 0, R_w = 0, R_sl = 0, R_sc = 0, R_tsc = 0, R_cov = 0, R_rid = 0;
+      float R_frac = 0.f;
+      uint64_t skipped = 0;  // srt[k] = 0 marks (bwamem.c:709), by program position
+
+      for (int c = 0; c < nch; ++c) {
+        const int cs0 = __builtin_amdgcn_readlane(c_s0, c), cs1 = __builtin_amdgcn_readlane(c_s1, c);
+        if (cs1 == cs0) continue;
+        const int64_t clo = readlane64(c_w.lo, c), chi = readlane64(c_w.hi, c);
+        if (chi < clo) continue;  // flagged by prep (the reference would assert)
+        const int rid = __builtin_amdgcn_readlane(c_rid, c);
+        const float frac = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c_frac), c));
+        for (int e = cs0; e < cs1; ++e) {
+          const int64_t srb = readlane64(p_rb, e);
+          const int sqb = __builtin_amdgcn_readlane(p_qb, e), slen = __builtin_amdgcn_readlane(p_len, e);
+          if (nreg > 0) {
+            // containment in an existing region (bwamem.c:678-697), one region per lane
+            const bool inside = !(srb < R_rb || srb + slen > R_re || sqb < R_qb || sqb + slen > R_qe) &&
+                                !(slen - R_sl > .1 * lq);
+            const int qd1 = sqb - R_qb;
+            const int64_t rd1 = srb - R_rb;
+            const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
+            const int bw1 = g1 < R_w ? g1 : R_w;
+            const int qd2 = R_qe - (sqb + slen);
+            const int64_t rd2 = R_re - (srb + slen);
+            const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
+            const int bw2 = g2 < R_w ? g2 : R_w;
+            const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+            if (__builtin_amdgcn_ballot_w64(r < nreg && inside && near) != 0) {
+              // an overlapping seed among those already visited (bwamem.c:698-707)
+              const bool a1 = sqb <= p_qb && sqb + slen - p_qb >= slen >> 2 && (int64_t)(p_qb - sqb) != p_rb - srb;
+              const bool b1 = p_qb <= sqb && p_qb + p_len - sqb >= slen >> 2 && (int64_t)(sqb - p_qb) != srb - p_rb;
+              const bool live = r >= cs0 && r < e && !((skipped >> r) & 1ull) && p_flag == 0;
+              if (__builtin_amdgcn_ballot_w64(live && !(p_len < slen * .95) && (a1 || b1)) == 0) {
+                skipped |= 1ull << e;
+                continue;
+              }
+            }
+          }
+          // ---- extend (bwamem.c:717-792); both target windows in one round trip
+          const int qlenL = sqb, qlenR = lq - (sqb + slen);
+          const int64_t x0L = srb - 1, x0R = srb + slen;
+          const int tlenL = (int)(srb - clo), tlenR = (int)(chi - x0R);
+          fill_two(tbl, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0, tbr, x0R,
+                   qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref);
+          int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
+          int aw[2] = {o.w, o.w};
+          int64_t rb = srb, re = srb + slen;
+#pragma nounroll
+          for (int side = 0; side < 2; ++side) {
+            const bool left = side == 0;
+            if (left && sqb == 0) {  // bwamem.c:753
+              score = truesc = slen * o.a;
+              continue;
+            }
+            if (!left && qlenR == 0) continue;  // bwamem.c:781
+            const int qlen = left ? qlenL : qlenR;
+            const int64_t x0 = left ? x0L : x0R;
+            const int tlen = left ? tlenL : tlenR;
+            const int qa = left ? sqb - 1 : sqb + slen;
+            const int eb = left ? o.pen_clip5 : o.pen_clip3;
+            const int h0 = left ? slen * o.a : score;
+            uint8_t* const tb = left ? tbl : tbr;
+            sc0 = score;
+            ExtOut x{};
+            for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY (bwamem.c:639)
+              const int prev = score;
+              aw[side] = o.w << t;
+              x = extend_wave_dispatch<C, false>(o, qlen, sq, qa, left ? -1 : 1, tlen, tb, aw[side], eb, o.zdrop,
+                                                 h0, tl);
+              score = x.score;
+              if (score == prev || x.max_off < (aw[side] >> 1) + (aw[side] >> 2)) break;
+            }
+            const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+            if (left) {
+              qb = local ? sqb - x.qle : 0;
+              rb = srb - (local ? x.tle : x.gtle);
+              truesc = local ? score : x.gscore;
+            } else {
+              qe = local ? qa + x.qle : lq;
+              re = x0 + (local ? x.tle : x.gtle);
+              truesc += (local ? score : x.gscore) - sc0;
+            }
+          }
+          // seedcov over the chain's seeds (bwamem.c:784-788)
+          const bool in = r >= cs0 && r < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
+          const long long cov = grp_sum64(in ? p_len : 0, 64);
+          const bool me = r == nreg;
+          R_rb = me ? rb : R_rb;
+          R_re = me ? re : R_re;
+          R_qb = me ? qb : R_qb;
+          R_qe = me ? qe : R_qe;
+          R_w = me ? (aw[0] > aw[1] ? aw[0] : aw[1]) : R_w;
+          R_sl = me ? slen : R_sl;
+          R_sc = me ? score : R_sc;
+          R_tsc = me ? truesc : R_tsc;
+          R_cov = me ? (int)cov : R_cov;
+          R_rid = me ? rid : R_rid;
+          R_frac = me ? frac : R_frac;
+          ++nreg;
+        }
+      }
+      // ---- the read's mem_alnreg_v, lane i writes region i (88 B, rest zero: bwamem.c:718)
+      if (r < nreg) {
+        uint2* dst = reinterpret_cast<uint2*>(a.out + s0 + r);
+        dst[0] = make_uint2((uint32_t)R_rb, (uint32_t)((uint64_t)R_rb >> 32));
+        dst[1] = make_uint2((uint32_t)R_re, (uint32_t)((uint64_t)R_re >> 32));
+        dst[2] = make_uint2((uint32_t)R_qb, (uint32_t)R_qe);
+        dst[3] = make_uint2((uint32_t)R_rid, (uint32_t)R_sc);
+        dst[4] = make_uint2((uint32_t)R_tsc, 0u);
+        dst[5] = make_uint2(0u, 0u);
+        dst[6] = make_uint2(0u, (uint32_t)R_w);
+        dst[7] = make_uint2((uint32_t)R_cov, 0u);
+        dst[8] = make_uint2(0u, (uint32_t)R_sl);
+        dst[9] = make_uint2(0u, __float_as_uint(R_frac));
+        dst[10] = make_uint2(0u, 0u);
+      }
+    }
+    a.out_n[rd] = nreg;  // same value from every lane
+    li = (__builtin_amdgcn_readfirstlane(slot_next) >> 6) * 8 + shard;
+    if (li >= n_list) {
+      li = -1;
+      shard = (shard + 1) & 7;
+      ++tried;
+      while (tried < 8) {
+        const int slot = atomicAdd(heads + shard, 1);
+        li = (__builtin_amdgcn_readfirstlane(slot) >> 6) * 8 + shard;
+        if (li < n_list) break;
+        li = -1;
+        shard = (shard + 1) & 7;
+        ++tried;
+      }
+    }
+  }
+  if (r != 0) tl = Tally{0, 0, 0};
+  block_stats<64>(tl, a.stats);
+}
+
 // ------------------------------------------------------------ extend batch
 template <int G, int C, bool T5>
 __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_ext_task_t* __restrict__ tasks,
@@ -1016,35 +1151,53 @@ __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_e
 }
 
 // ------------------------------------------------------------ launchers
-hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, int64_t,
-                             ChainWin* win, uint64_t* srt, int64_t* stats, hipStream_t st) {
+hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, ChainWin* win, uint64_t* srt,
+                             bwagpu_seed_t* prog, int64_t* stats, hipStream_t st) {
   if (b.n_chains == 0) return hipSuccess;
   const int nb = (b.n_chains + 255) / 256;
-  hipLaunchKernelGGL(chain_prep_kernel, dim3(nb), dim3(256), 0, st, o, ref, b, win, srt, stats);
+  hipLaunchKernelGGL(chain_prep_kernel, dim3(nb), dim3(256), 0, st, o, ref, b, win, srt, prog, stats);
+  return hipGetLastError();
+}
+
+// resident workgroups of a kernel over the whole device (persistent grids)
+template <typename K>
+static int resident_blocks(K kernel, size_t lds) {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds) != hipSuccess || per < 1) per = 1;
+  return per * ncu;
+}
+
+template <int C>
+static hipError_t launch_c2a_fast(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n,
+                                  int tb, const C2AArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)(kBlock / 64) * (kSeqLds + 2 * tb);
+  static int cap = 0;  // per instantiation; same device kind everywhere
+  if (!cap) cap = resident_blocks(chain2aln_fast_kernel<C>, lds);
+  const int nb = std::min((n + 3) / 4, cap);
+  hipLaunchKernelGGL((chain2aln_fast_kernel<C>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, variant, tb);
   return hipGetLastError();
 }
 
 template <int G, int C>
-static hipError_t launch_c2a_t(const DevOpt& o, const DevRef& ref, const DevBatch& b, const int32_t* list,
-                               const int32_t* cnt, int variant, int32_t n, int tb, const ChainWin* win, uint64_t* srt,
-                               bwagpu_alnreg_t* out, int32_t* out_n, int64_t* stats, hipStream_t st) {
+static hipError_t launch_c2a_t(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n, int tb,
+                               const C2AArgs& a, hipStream_t st) {
   constexpr int GPB = kBlock / G;
   // persistent-style grid: the waves pull reads from the device-side queue
   const int nb = std::min((n + GPB - 1) / GPB, 2048);
-  hipLaunchKernelGGL((chain2aln_kernel<G, C>), dim3(nb), dim3(kBlock), (size_t)GPB * tb, st, o, ref, b, list, cnt,
-                     variant, tb, win, srt, out, out_n, stats);
+  hipLaunchKernelGGL((chain2aln_kernel<G, C>), dim3(nb), dim3(kBlock), (size_t)GPB * tb, st, o, ref, b, a.read_list,
+                     a.counts, variant, tb, a.win, a.srt, a.out, a.out_n, a.stats);
   return hipGetLastError();
 }
 
-hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b,
-                            const int32_t* read_list, const int32_t* d_count, int32_t max_list, int tb_bytes,
-                            const ChainWin* win, uint64_t* srt, bwagpu_alnreg_t* out, int32_t* out_n,
-                            int64_t* stats, hipStream_t st) {
+hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b, int32_t max_list,
+                            int tb_bytes, const C2AArgs& a, hipStream_t st) {
   if (max_list == 0) return hipSuccess;
   switch (variant) {
-    case 0: return launch_c2a_t<64, 3>(o, ref, b, read_list, d_count, 0, max_list, tb_bytes, win, srt, out, out_n, stats, st);
-    case 1: return launch_c2a_t<64, 4>(o, ref, b, read_list, d_count, 1, max_list, tb_bytes, win, srt, out, out_n, stats, st);
-    case 2: return launch_c2a_t<64, 16>(o, ref, b, read_list, d_count, 2, max_list, tb_bytes, win, srt, out, out_n, stats, st);
+    case 0: return launch_c2a_fast<3>(o, ref, b, 0, max_list, tb_bytes, a, st);
+    case 1: return launch_c2a_fast<4>(o, ref, b, 1, max_list, tb_bytes, a, st);
+    case 2: return launch_c2a_t<64, 16>(o, ref, b, 2, max_list, tb_bytes, a, st);
   }
   return hipErrorInvalidValue;
 }
