@@ -900,210 +900,232 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 }
 
 // mem_chain2aln for reads of <= 256 bp with <= 64 seeds and chains: one read
-// per wave with the whole read register-resident, so a read costs one round
-// trip for its data (descriptor, seeds, chains, bases — issued together) plus
-// one per extended seed (both target windows), instead of a dependent load
-// chain per seed:
+// per wave, the whole read register- or LDS-resident:
 //   lane i   holds the read's i-th seed in processing order (prog, written by
-//            chain_prep_kernel: chains in order, seeds by descending key),
-//            chain i's window/rid/frac_rep/seed range, and region i once made;
-//   LDS      holds the read's bases (the query of both extensions) and the two
-//            target row buffers.
+//            chain_prep_kernel: chains in order, seeds by descending key) and
+//            chain i's window / rid / frac_rep / seed range;
+//   LDS      holds the read's bases (the query of both extensions), the two
+//            target row buffers and the read's regions as 88-byte records.
 // Containment (bwamem.c:678-697), the overlap test (698-707) and seedcov
-// (784-788) are lane-parallel tests + one ballot / reduction.  Work is pulled
-// from the per-XCD queue heads; the next ticket is taken while the current
-// read runs.
+// (784-788) are lane-parallel tests + one ballot / reduction.
+// Scheduling is static: reads are cost-sorted (read_keys_kernel) and dealt to
+// the resident waves in zig-zag rounds, so every wave knows its next read and
+// loads that read's descriptor and lane data while the current read runs (the
+// loads go out after the current read's first target fill, so no fill waits
+// on them).  No queue atomics, no dependent load chain on the critical path.
+struct ReadLanes {
+  int64_t p_rb;
+  int p_qb, p_len, p_flag;
+  int c_s0, c_s1;
+  int64_t c_lo, c_hi;
+  int c_rid;
+  float c_frac;
+  uint32_t seqw;  // read bases 4r .. 4r+3
+};
+
+__device__ __forceinline__ ReadLanes load_read_lanes(const DevBatch& b, const C2AArgs& a, const ReadDesc& d,
+                                                     int r) {
+  ReadLanes x;
+  const bwagpu_seed_t* pg = a.prog + d.s0 + min(r, d.ns - 1);
+  x.p_rb = pg->rbeg;
+  x.p_qb = pg->qbeg;
+  x.p_len = pg->len;
+  x.p_flag = pg->pad_;
+  const int cc = d.c0 + min(r, d.nch - 1);
+  x.c_s0 = b.chain_seed_off[cc] - d.s0;
+  x.c_s1 = b.chain_seed_off[cc + 1] - d.s0;
+  const ChainWin w = a.win[cc];
+  x.c_lo = w.lo;
+  x.c_hi = w.hi;
+  x.c_rid = b.chain_rid[cc];
+  x.c_frac = b.chain_frac_rep[cc];
+  const uint8_t* q = b.seq + d.qoff;
+  uint32_t wv = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) wv |= (uint32_t)q[min(4 * r + k, d.lq - 1)] << (8 * k);
+  x.seqw = wv;
+  return x;
+}
+
+__device__ __forceinline__ ReadDesc uniform_desc(const ReadDesc& d) {
+  ReadDesc u;
+  u.qoff = (int64_t)((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)d.qoff >> 32)) << 32 |
+                     __builtin_amdgcn_readfirstlane((uint32_t)d.qoff));
+  u.rd = __builtin_amdgcn_readfirstlane(d.rd);
+  u.lq = __builtin_amdgcn_readfirstlane(d.lq);
+  u.c0 = __builtin_amdgcn_readfirstlane(d.c0);
+  u.nch = __builtin_amdgcn_readfirstlane(d.nch);
+  u.s0 = __builtin_amdgcn_readfirstlane(d.s0);
+  u.ns = __builtin_amdgcn_readfirstlane(d.ns);
+  return u;
+}
+
+constexpr int kRegBytes = 88 * kFastMaxSeeds;  // LDS region records per wave
+
 template <int C>
 __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
                                                                 int variant, int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int r = (int)(threadIdx.x & 63);
   const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint8_t* const sq = lds + wib * (kSeqLds + 2 * tb_bytes);
+  uint8_t* const wl = lds + wib * (kRegBytes + kSeqLds + 2 * tb_bytes);
+  uint32_t* const regs = reinterpret_cast<uint32_t*>(wl);  // region k: dwords [22k, 22k+22)
+  uint8_t* const sq = wl + kRegBytes;
   uint8_t* const tbl = sq + kSeqLds;
   uint8_t* const tbr = tbl + tb_bytes;
   int base = 0;
   for (int v = 0; v < variant; ++v) base += a.counts[v];
   const int n_list = a.counts[variant];
   Tally tl{0, 0, 0};
-  // queue: shard x holds list positions x, x+8, ... (see chain2aln_kernel);
-  // all 64 lanes add 1 -> one wave-level atomic of 64, lane 0 sees the old value
-  const int xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;  // HW_REG_XCC_ID
-  int32_t* const heads = a.counts + 16 + 8 * variant;
-  int shard = xcc, tried = 0;
-  int li = -1;
-  while (tried < 8) {
-    const int slot = atomicAdd(heads + shard, 1);
-    li = (__builtin_amdgcn_readfirstlane(slot) >> 6) * 8 + shard;
-    if (li < n_list) break;
-    li = -1;
-    shard = (shard + 1) & 7;
-    ++tried;
-  }
-
-  while (li >= 0) {
-    const int slot_next = atomicAdd(heads + shard, 1);  // consumed at the end of this read
-    const ReadDesc d = a.desc[base + li];
-    const int rd = __builtin_amdgcn_readfirstlane(d.rd);
-    const int lq = __builtin_amdgcn_readfirstlane(d.lq);
-    const int nch = __builtin_amdgcn_readfirstlane(d.nch);
-    const int ns = __builtin_amdgcn_readfirstlane(d.ns);
-    const int s0 = __builtin_amdgcn_readfirstlane(d.s0);
-    int nreg = 0;
-    if (ns > 0) {
-      // ---- the read's data, all loads issued before any is used
-      const bwagpu_seed_t* pg = a.prog + s0;
-      const int ie = min(r, ns - 1);
-      const int64_t p_rb = pg[ie].rbeg;
-      const int p_qb = pg[ie].qbeg, p_len = pg[ie].len, p_flag = pg[ie].pad_;
-      const int cc = d.c0 + min(r, nch - 1);
-      const int c_s0 = b.chain_seed_off[cc] - s0, c_s1 = b.chain_seed_off[cc + 1] - s0;
-      const ChainWin c_w = a.win[cc];
-      const int c_rid = b.chain_rid[cc];
-      const float c_frac = b.chain_frac_rep[cc];
-      {
-        const uint8_t* q = b.seq + d.qoff;
-        uint32_t wv = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) wv |= (uint32_t)q[min(4 * r + k, lq - 1)] << (8 * k);
-        reinterpret_cast<uint32_t*>(sq)[r] = wv;  // 64 lanes x 4 B = kSeqLds
+  // static zig-zag deal over the resident waves (cost-sorted list: LPT-like)
+  const int NW = (int)gridDim.x * (kBlock / 64), W = (int)blockIdx.x * (kBlock / 64) + wib;
+  auto pos = [&](int round) { return round * NW + ((round & 1) ? NW - 1 - W : W); };
+  int round = 0;
+  if (pos(0) < n_list) {
+    ReadDesc d = uniform_desc(a.desc[base + pos(0)]);
+    ReadLanes cur{};
+    if (d.ns > 0) cur = load_read_lanes(b, a, d, r);
+    for (;;) {
+      const bool has_next = pos(round + 1) < n_list;
+      ReadDesc dn{};
+      if (has_next) dn = uniform_desc(a.desc[base + pos(round + 1)]);
+      ReadLanes nxt{};
+      bool fetched = !has_next || dn.ns == 0;
+      const int rd = d.rd, lq = d.lq, nch = d.nch, ns = d.ns, s0 = d.s0;
+      int nreg = 0;
+      if (ns > 0) {
+        reinterpret_cast<uint32_t*>(sq)[r] = cur.seqw;  // 64 lanes x 4 B = kSeqLds
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      // regions made so far: lane i holds region i
-      int64_t R_rb = 0, R_re = 0;
-      int R_qb = 0, R_qe = 0, R_w = 0, R_sl = 0, R_sc = 0, R_tsc = 0, R_cov = 0, R_rid = 0;
-      float R_frac = 0.f;
-      uint64_t skipped = 0;  // srt[k] = 0 marks (bwamem.c:709), by program position
-
-      for (int c = 0; c < nch; ++c) {
-        const int cs0 = __builtin_amdgcn_readlane(c_s0, c), cs1 = __builtin_amdgcn_readlane(c_s1, c);
-        if (cs1 == cs0) continue;
-        const int64_t clo = readlane64(c_w.lo, c), chi = readlane64(c_w.hi, c);
-        if (chi < clo) continue;  // flagged by prep (the reference would assert)
-        const int rid = __builtin_amdgcn_readlane(c_rid, c);
-        const float frac = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c_frac), c));
-        for (int e = cs0; e < cs1; ++e) {
-          const int64_t srb = readlane64(p_rb, e);
-          const int sqb = __builtin_amdgcn_readlane(p_qb, e), slen = __builtin_amdgcn_readlane(p_len, e);
-          if (nreg > 0) {
-            // containment in an existing region (bwamem.c:678-697), one region per lane
-            const bool inside = !(srb < R_rb || srb + slen > R_re || sqb < R_qb || sqb + slen > R_qe) &&
-                                !(slen - R_sl > .1 * lq);
-            const int qd1 = sqb - R_qb;
-            const int64_t rd1 = srb - R_rb;
-            const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
-            const int bw1 = g1 < R_w ? g1 : R_w;
-            const int qd2 = R_qe - (sqb + slen);
-            const int64_t rd2 = R_re - (srb + slen);
-            const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
-            const int bw2 = g2 < R_w ? g2 : R_w;
-            const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
-            if (__builtin_amdgcn_ballot_w64(r < nreg && inside && near) != 0) {
-              // an overlapping seed among those already visited (bwamem.c:698-707)
-              const bool a1 = sqb <= p_qb && sqb + slen - p_qb >= slen >> 2 && (int64_t)(p_qb - sqb) != p_rb - srb;
-              const bool b1 = p_qb <= sqb && p_qb + p_len - sqb >= slen >> 2 && (int64_t)(sqb - p_qb) != srb - p_rb;
-              const bool live = r >= cs0 && r < e && !((skipped >> r) & 1ull) && p_flag == 0;
-              if (__builtin_amdgcn_ballot_w64(live && !(p_len < slen * .95) && (a1 || b1)) == 0) {
-                skipped |= 1ull << e;
-                continue;
+        const int64_t p_rb = cur.p_rb;
+        const int p_qb = cur.p_qb, p_len = cur.p_len, p_flag = cur.p_flag;
+        uint64_t skipped = 0;  // srt[k] = 0 marks (bwamem.c:709), by program position
+        for (int c = 0; c < nch; ++c) {
+          const int cs0 = __builtin_amdgcn_readlane(cur.c_s0, c), cs1 = __builtin_amdgcn_readlane(cur.c_s1, c);
+          if (cs1 == cs0) continue;
+          const int64_t clo = readlane64(cur.c_lo, c), chi = readlane64(cur.c_hi, c);
+          if (chi < clo) continue;  // flagged by prep (the reference would assert)
+          const int rid = __builtin_amdgcn_readlane(cur.c_rid, c);
+          const float frac = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.c_frac), c));
+          for (int e = cs0; e < cs1; ++e) {
+            const int64_t srb = readlane64(p_rb, e);
+            const int sqb = __builtin_amdgcn_readlane(p_qb, e), slen = __builtin_amdgcn_readlane(p_len, e);
+            if (nreg > 0) {
+              // containment in an existing region (bwamem.c:678-697), one region per lane
+              const uint32_t* g = regs + 22 * min(r, nreg - 1);
+              const int64_t R_rb = (int64_t)((uint64_t)g[1] << 32 | g[0]);
+              const int64_t R_re = (int64_t)((uint64_t)g[3] << 32 | g[2]);
+              const int R_qb = (int)g[4], R_qe = (int)g[5], R_w = (int)g[13], R_sl = (int)g[17];
+              const bool inside = !(srb < R_rb || srb + slen > R_re || sqb < R_qb || sqb + slen > R_qe) &&
+                                  !(slen - R_sl > .1 * lq);
+              const int qd1 = sqb - R_qb;
+              const int64_t rd1 = srb - R_rb;
+              const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
+              const int bw1 = g1 < R_w ? g1 : R_w;
+              const int qd2 = R_qe - (sqb + slen);
+              const int64_t rd2 = R_re - (srb + slen);
+              const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
+              const int bw2 = g2 < R_w ? g2 : R_w;
+              const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+              if (__builtin_amdgcn_ballot_w64(r < nreg && inside && near) != 0) {
+                // an overlapping seed among those already visited (bwamem.c:698-707)
+                const bool a1 = sqb <= p_qb && sqb + slen - p_qb >= slen >> 2 && (int64_t)(p_qb - sqb) != p_rb - srb;
+                const bool b1 = p_qb <= sqb && p_qb + p_len - sqb >= slen >> 2 && (int64_t)(sqb - p_qb) != srb - p_rb;
+                const bool live = r >= cs0 && r < e && !((skipped >> r) & 1ull) && p_flag == 0;
+                if (__builtin_amdgcn_ballot_w64(live && !(p_len < slen * .95) && (a1 || b1)) == 0) {
+                  skipped |= 1ull << e;
+                  continue;
+                }
               }
             }
-          }
-          // ---- extend (bwamem.c:717-792); both target windows in one round trip
-          const int qlenL = sqb, qlenR = lq - (sqb + slen);
-          const int64_t x0L = srb - 1, x0R = srb + slen;
-          const int tlenL = (int)(srb - clo), tlenR = (int)(chi - x0R);
-          fill_two(tbl, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0, tbr, x0R,
-                   qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref);
-          int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
-          int aw[2] = {o.w, o.w};
-          int64_t rb = srb, re = srb + slen;
+            // ---- extend (bwamem.c:717-792); both target windows in one round trip
+            const int qlenL = sqb, qlenR = lq - (sqb + slen);
+            const int64_t x0L = srb - 1, x0R = srb + slen;
+            const int tlenL = (int)(srb - clo), tlenR = (int)(chi - x0R);
+            fill_two(tbl, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0, tbr, x0R,
+                     qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref);
+            if (!fetched) {  // the next read's lanes, in flight during this seed's DP
+              nxt = load_read_lanes(b, a, dn, r);
+              fetched = true;
+            }
+            int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
+            int aw[2] = {o.w, o.w};
+            int64_t rb = srb, re = srb + slen;
 #pragma nounroll
-          for (int side = 0; side < 2; ++side) {
-            const bool left = side == 0;
-            if (left && sqb == 0) {  // bwamem.c:753
-              score = truesc = slen * o.a;
-              continue;
+            for (int side = 0; side < 2; ++side) {
+              const bool left = side == 0;
+              if (left && sqb == 0) {  // bwamem.c:753
+                score = truesc = slen * o.a;
+                continue;
+              }
+              if (!left && qlenR == 0) continue;  // bwamem.c:781
+              const int qlen = left ? qlenL : qlenR;
+              const int64_t x0 = left ? x0L : x0R;
+              const int tlen = left ? tlenL : tlenR;
+              const int qa = left ? sqb - 1 : sqb + slen;
+              const int eb = left ? o.pen_clip5 : o.pen_clip3;
+              const int h0 = left ? slen * o.a : score;
+              uint8_t* const tb = left ? tbl : tbr;
+              sc0 = score;
+              ExtOut x{};
+              for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY (bwamem.c:639)
+                const int prev = score;
+                aw[side] = o.w << t;
+                x = extend_wave_dispatch<C, false>(o, qlen, sq, qa, left ? -1 : 1, tlen, tb, aw[side], eb, o.zdrop,
+                                                   h0, tl);
+                score = x.score;
+                if (score == prev || x.max_off < (aw[side] >> 1) + (aw[side] >> 2)) break;
+              }
+              const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+              if (left) {
+                qb = local ? sqb - x.qle : 0;
+                rb = srb - (local ? x.tle : x.gtle);
+                truesc = local ? score : x.gscore;
+              } else {
+                qe = local ? qa + x.qle : lq;
+                re = x0 + (local ? x.tle : x.gtle);
+                truesc += (local ? score : x.gscore) - sc0;
+              }
             }
-            if (!left && qlenR == 0) continue;  // bwamem.c:781
-            const int qlen = left ? qlenL : qlenR;
-            const int64_t x0 = left ? x0L : x0R;
-            const int tlen = left ? tlenL : tlenR;
-            const int qa = left ? sqb - 1 : sqb + slen;
-            const int eb = left ? o.pen_clip5 : o.pen_clip3;
-            const int h0 = left ? slen * o.a : score;
-            uint8_t* const tb = left ? tbl : tbr;
-            sc0 = score;
-            ExtOut x{};
-            for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY (bwamem.c:639)
-              const int prev = score;
-              aw[side] = o.w << t;
-              x = extend_wave_dispatch<C, false>(o, qlen, sq, qa, left ? -1 : 1, tlen, tb, aw[side], eb, o.zdrop,
-                                                 h0, tl);
-              score = x.score;
-              if (score == prev || x.max_off < (aw[side] >> 1) + (aw[side] >> 2)) break;
+            // seedcov over the chain's seeds (bwamem.c:784-788)
+            const bool in = r >= cs0 && r < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
+            const long long cov = grp_sum64(in ? p_len : 0, 64);
+            // region nreg as its 88-byte record (rest zero: bwamem.c:718), lane d writes dword d
+            {
+              const int dw = r < 21 ? r : 21;
+              uint32_t v = 0;
+              v = dw == 0 ? (uint32_t)rb : v;
+              v = dw == 1 ? (uint32_t)((uint64_t)rb >> 32) : v;
+              v = dw == 2 ? (uint32_t)re : v;
+              v = dw == 3 ? (uint32_t)((uint64_t)re >> 32) : v;
+              v = dw == 4 ? (uint32_t)qb : v;
+              v = dw == 5 ? (uint32_t)qe : v;
+              v = dw == 6 ? (uint32_t)rid : v;
+              v = dw == 7 ? (uint32_t)score : v;
+              v = dw == 8 ? (uint32_t)truesc : v;
+              v = dw == 13 ? (uint32_t)(aw[0] > aw[1] ? aw[0] : aw[1]) : v;
+              v = dw == 14 ? (uint32_t)cov : v;
+              v = dw == 17 ? (uint32_t)slen : v;
+              v = dw == 19 ? __float_as_uint(frac) : v;
+              regs[22 * nreg + dw] = v;
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            const bool local = x.gscore <= 0 || x.gscore <= score - eb;
-            if (left) {
-              qb = local ? sqb - x.qle : 0;
-              rb = srb - (local ? x.tle : x.gtle);
-              truesc = local ? score : x.gscore;
-            } else {
-              qe = local ? qa + x.qle : lq;
-              re = x0 + (local ? x.tle : x.gtle);
-              truesc += (local ? score : x.gscore) - sc0;
-            }
+            ++nreg;
           }
-          // seedcov over the chain's seeds (bwamem.c:784-788)
-          const bool in = r >= cs0 && r < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
-          const long long cov = grp_sum64(in ? p_len : 0, 64);
-          const bool me = r == nreg;
-          R_rb = me ? rb : R_rb;
-          R_re = me ? re : R_re;
-          R_qb = me ? qb : R_qb;
-          R_qe = me ? qe : R_qe;
-          R_w = me ? (aw[0] > aw[1] ? aw[0] : aw[1]) : R_w;
-          R_sl = me ? slen : R_sl;
-          R_sc = me ? score : R_sc;
-          R_tsc = me ? truesc : R_tsc;
-          R_cov = me ? (int)cov : R_cov;
-          R_rid = me ? rid : R_rid;
-          R_frac = me ? frac : R_frac;
-          ++nreg;
         }
+        // ---- the read's mem_alnreg_v: LDS records -> global, dword-parallel
+        uint32_t* const dst = reinterpret_cast<uint32_t*>(a.out + s0);
+        for (int k = r; k < 22 * nreg; k += 64) dst[k] = regs[k];
       }
-      // ---- the read's mem_alnreg_v, lane i writes region i (88 B, rest zero: bwamem.c:718)
-      if (r < nreg) {
-        uint2* dst = reinterpret_cast<uint2*>(a.out + s0 + r);
-        dst[0] = make_uint2((uint32_t)R_rb, (uint32_t)((uint64_t)R_rb >> 32));
-        dst[1] = make_uint2((uint32_t)R_re, (uint32_t)((uint64_t)R_re >> 32));
-        dst[2] = make_uint2((uint32_t)R_qb, (uint32_t)R_qe);
-        dst[3] = make_uint2((uint32_t)R_rid, (uint32_t)R_sc);
-        dst[4] = make_uint2((uint32_t)R_tsc, 0u);
-        dst[5] = make_uint2(0u, 0u);
-        dst[6] = make_uint2(0u, (uint32_t)R_w);
-        dst[7] = make_uint2((uint32_t)R_cov, 0u);
-        dst[8] = make_uint2(0u, (uint32_t)R_sl);
-        dst[9] = make_uint2(0u, __float_as_uint(R_frac));
-        dst[10] = make_uint2(0u, 0u);
-      }
-    }
-    a.out_n[rd] = nreg;  // same value from every lane
-    li = (__builtin_amdgcn_readfirstlane(slot_next) >> 6) * 8 + shard;
-    if (li >= n_list) {
-      li = -1;
-      shard = (shard + 1) & 7;
-      ++tried;
-      while (tried < 8) {
-        const int slot = atomicAdd(heads + shard, 1);
-        li = (__builtin_amdgcn_readfirstlane(slot) >> 6) * 8 + shard;
-        if (li < n_list) break;
-        li = -1;
-        shard = (shard + 1) & 7;
-        ++tried;
-      }
+      a.out_n[rd] = nreg;  // same value from every lane
+      if (!has_next) break;
+      if (!fetched) nxt = load_read_lanes(b, a, dn, r);
+      d = dn;
+      cur = nxt;
+      ++round;
     }
   }
   if (r != 0) tl = Tally{0, 0, 0};
@@ -1172,7 +1194,7 @@ static int resident_blocks(K kernel, size_t lds) {
 template <int C>
 static hipError_t launch_c2a_fast(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n,
                                   int tb, const C2AArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(kBlock / 64) * (kSeqLds + 2 * tb);
+  const size_t lds = (size_t)(kBlock / 64) * (kRegBytes + kSeqLds + 2 * tb);
   static int cap = 0;  // per instantiation; same device kind everywhere
   if (!cap) cap = resident_blocks(chain2aln_fast_kernel<C>, lds);
   const int nb = std::min((n + 3) / 4, cap);
