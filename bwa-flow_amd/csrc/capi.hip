@@ -320,7 +320,7 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   for (int v = 0; v < kNumVariants; ++v) {
     const int lqv = std::min(lq_max, kVariants[v].max_len());
     const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
-    const size_t lds = kVariants[v].fast ? (size_t)(kBlock / 64) * (88 * kFastMaxSeeds + kSeqLds + 2 * tb)
+    const size_t lds = kVariants[v].fast ? (size_t)(kBlock / 64) * fast_wave_lds(tb)
                                          : (size_t)tb * (kBlock / kVariants[v].G);
     if (lds > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
     HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, db.n_reads, tb, a, st), "chain2aln launch");

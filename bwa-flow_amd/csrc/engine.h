@@ -70,8 +70,8 @@ struct Variant {
   int max_len() const { return G * C; }
 };
 // limits of the fast kernel: one lane per seed / chain / region of a read
-constexpr int kFastMaxSeeds = 64;
-constexpr int kFastMaxChains = 64;
+constexpr int kFastMaxSeeds = 32;
+constexpr int kFastMaxChains = 32;
 constexpr int kSeqLds = 256;  // LDS bytes for the read's bases (fast variants: lq <= 256)
 constexpr int kNumVariants = 3;
 extern const Variant kVariants[kNumVariants];
@@ -103,6 +103,8 @@ struct C2AArgs {
 };
 hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b, int32_t max_list,
                             int tb_bytes, const C2AArgs& a, hipStream_t st);
+// LDS bytes per wave of chain2aln_fast_kernel for target row buffers of tb bytes
+size_t fast_wave_lds(int tb);
 // descriptors of the sorted reads
 hipError_t launch_read_desc(const DevBatch& b, const int32_t* sorted_reads, ReadDesc* desc, hipStream_t st);
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,

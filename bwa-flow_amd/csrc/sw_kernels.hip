@@ -899,68 +899,105 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
   return (int64_t)((uint64_t)hi << 32 | lo);
 }
 
-// mem_chain2aln for reads of <= 256 bp with <= 64 seeds and chains: one read
-// per wave, the whole read register- or LDS-resident:
-//   lane i   holds the read's i-th seed in processing order (prog, written by
-//            chain_prep_kernel: chains in order, seeds by descending key) and
-//            chain i's window / rid / frac_rep / seed range;
-//   LDS      holds the read's bases (the query of both extensions), the two
-//            target row buffers and the read's regions as 88-byte records.
+// mem_chain2aln for reads of <= 256 bp with <= 32 seeds and chains: one read
+// per wave, the read's data in a per-wave LDS table, not in registers:
+//   table    the read's seeds in processing order (prog, written by
+//            chain_prep_kernel: chains in order, seeds by descending key), its
+//            chains' seed ranges / windows / rid / frac_rep, and its bases (the
+//            query of both extensions) — filled by global_load_lds DMA;
+//   regions  the read's mem_alnreg_t records so far (88 B each);
+//   tbl/tbr  the target rows of the current seed's left / right extension.
 // Containment (bwamem.c:678-697), the overlap test (698-707) and seedcov
-// (784-788) are lane-parallel tests + one ballot / reduction.
+// (784-788) are lane-parallel tests (lane i: region i or seed i) + a ballot or
+// a reduction.
 // Scheduling is static: reads are cost-sorted (read_keys_kernel) and dealt to
-// the resident waves in zig-zag rounds, so every wave knows its next read and
-// loads that read's descriptor and lane data while the current read runs (the
-// loads go out after the current read's first target fill, so no fill waits
-// on them).  No queue atomics, no dependent load chain on the critical path.
-struct ReadLanes {
-  int64_t p_rb;
-  int p_qb, p_len, p_flag;
-  int c_s0, c_s1;
-  int64_t c_lo, c_hi;
-  int c_rid;
-  float c_frac;
-  uint32_t seqw;  // read bases 4r .. 4r+3
+// the resident waves in zig-zag rounds, so a wave knows its next read and DMAs
+// that read's table (double-buffered) while the current read's DP runs; the
+// DMA goes out after the current read's first target fill, so no fill waits
+// on it.  No queue atomics and no dependent load chain on the critical path.
+constexpr int kTabLanes = kFastMaxSeeds;  // seeds / chains per read (<= 64)
+struct LaneTab {                          // byte offsets inside one table, [field][lane]
+  static constexpr int RBL = 0;                      // prog: rbeg low / high dword, qbeg, len, pad_
+  static constexpr int RBH = RBL + 4 * kTabLanes;
+  static constexpr int QB = RBH + 4 * kTabLanes;
+  static constexpr int LEN = QB + 4 * kTabLanes;
+  static constexpr int FLAG = LEN + 4 * kTabLanes;
+  static constexpr int CS0 = FLAG + 4 * kTabLanes;   // chain_seed_off[c]
+  static constexpr int CS1 = CS0 + 4 * kTabLanes;    // chain_seed_off[c + 1]
+  static constexpr int WIN = CS1 + 4 * kTabLanes;    // ChainWin (16 B / lane)
+  static constexpr int RID = WIN + 16 * kTabLanes;
+  static constexpr int FRAC = RID + 4 * kTabLanes;
+  static constexpr int SEQ = FRAC + 4 * kTabLanes;   // the read's bases from dword (qoff & ~3): 128 dwords
+  static constexpr int BYTES = SEQ + 2 * kSeqLds;
 };
+static_assert(LaneTab::WIN % 16 == 0 && LaneTab::BYTES % 16 == 0, "table alignment");
 
-__device__ __forceinline__ ReadLanes load_read_lanes(const DevBatch& b, const C2AArgs& a, const ReadDesc& d,
-                                                     int r) {
-  ReadLanes x;
-  const bwagpu_seed_t* pg = a.prog + d.s0 + min(r, d.ns - 1);
-  x.p_rb = pg->rbeg;
-  x.p_qb = pg->qbeg;
-  x.p_len = pg->len;
-  x.p_flag = pg->pad_;
-  const int cc = d.c0 + min(r, d.nch - 1);
-  x.c_s0 = b.chain_seed_off[cc] - d.s0;
-  x.c_s1 = b.chain_seed_off[cc + 1] - d.s0;
-  const ChainWin w = a.win[cc];
-  x.c_lo = w.lo;
-  x.c_hi = w.hi;
-  x.c_rid = b.chain_rid[cc];
-  x.c_frac = b.chain_frac_rep[cc];
-  const uint8_t* q = b.seq + d.qoff;
-  uint32_t wv = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) wv |= (uint32_t)q[min(4 * r + k, d.lq - 1)] << (8 * k);
-  x.seqw = wv;
-  return x;
+#define BWAGPU_GLDS(gptr, lptr, SIZE)                                                                   \
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(gptr),            \
+                                   (void __attribute__((address_space(3)))*)(lptr), SIZE, 0, 0)
+
+// DMA read d's table (d uniform, d.ns > 0) into tab
+__device__ __forceinline__ void fetch_table(uint8_t* tab, const DevBatch& b, const C2AArgs& a, const ReadDesc& d,
+                                            int r) {
+  if (r < kTabLanes) {
+    const uint32_t* pg = reinterpret_cast<const uint32_t*>(a.prog + d.s0 + min(r, d.ns - 1));
+    BWAGPU_GLDS(pg + 0, tab + LaneTab::RBL, 4);
+    BWAGPU_GLDS(pg + 1, tab + LaneTab::RBH, 4);
+    BWAGPU_GLDS(pg + 2, tab + LaneTab::QB, 4);
+    BWAGPU_GLDS(pg + 3, tab + LaneTab::LEN, 4);
+    BWAGPU_GLDS(pg + 5, tab + LaneTab::FLAG, 4);
+    const int cc = d.c0 + min(r, d.nch - 1);
+    BWAGPU_GLDS(b.chain_seed_off + cc, tab + LaneTab::CS0, 4);
+    BWAGPU_GLDS(b.chain_seed_off + cc + 1, tab + LaneTab::CS1, 4);
+    BWAGPU_GLDS(a.win + cc, tab + LaneTab::WIN, 16);
+    BWAGPU_GLDS(b.chain_rid + cc, tab + LaneTab::RID, 4);
+    BWAGPU_GLDS(b.chain_frac_rep + cc, tab + LaneTab::FRAC, 4);
+  }
+  // bases by aligned dwords (a 1-byte LDS DMA writes a whole dword per lane):
+  // the read starts at byte (qoff & 3) of the SEQ area; the last dword read is
+  // the one holding the read's last base
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(b.seq) + (d.qoff >> 2);
+  const int last = (int)(((d.qoff & 3) + d.lq - 1) >> 2);
+  BWAGPU_GLDS(q + min(r, last), tab + LaneTab::SEQ, 4);
+  BWAGPU_GLDS(q + min(64 + r, last), tab + LaneTab::SEQ + 256, 4);
+}
+
+__device__ __forceinline__ void wait_dma() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int lds_i32(const uint8_t* p) { return *reinterpret_cast<const int*>(p); }
+__device__ __forceinline__ int64_t lds_i64(const uint8_t* p) {
+  const uint32_t lo = *reinterpret_cast<const uint32_t*>(p), hi = *reinterpret_cast<const uint32_t*>(p + 4);
+  return (int64_t)((uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ int64_t tab_rb(const uint8_t* tab, int i) {
+  const uint32_t lo = *reinterpret_cast<const uint32_t*>(tab + LaneTab::RBL + 4 * i);
+  const uint32_t hi = *reinterpret_cast<const uint32_t*>(tab + LaneTab::RBH + 4 * i);
+  return (int64_t)((uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)((uint64_t)hi << 32 | lo);
 }
 
 __device__ __forceinline__ ReadDesc uniform_desc(const ReadDesc& d) {
   ReadDesc u;
-  u.qoff = (int64_t)((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)d.qoff >> 32)) << 32 |
-                     __builtin_amdgcn_readfirstlane((uint32_t)d.qoff));
-  u.rd = __builtin_amdgcn_readfirstlane(d.rd);
-  u.lq = __builtin_amdgcn_readfirstlane(d.lq);
-  u.c0 = __builtin_amdgcn_readfirstlane(d.c0);
-  u.nch = __builtin_amdgcn_readfirstlane(d.nch);
-  u.s0 = __builtin_amdgcn_readfirstlane(d.s0);
-  u.ns = __builtin_amdgcn_readfirstlane(d.ns);
+  u.qoff = uni64(d.qoff);
+  u.rd = uni(d.rd);
+  u.lq = uni(d.lq);
+  u.c0 = uni(d.c0);
+  u.nch = uni(d.nch);
+  u.s0 = uni(d.s0);
+  u.ns = uni(d.ns);
   return u;
 }
 
 constexpr int kRegBytes = 88 * kFastMaxSeeds;  // LDS region records per wave
+constexpr int kFastWaveLds(int tb) { return 2 * LaneTab::BYTES + kRegBytes + 2 * tb; }
 
 template <int C>
 __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
@@ -968,10 +1005,10 @@ __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int r = (int)(threadIdx.x & 63);
   const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint8_t* const wl = lds + wib * (kRegBytes + kSeqLds + 2 * tb_bytes);
-  uint32_t* const regs = reinterpret_cast<uint32_t*>(wl);  // region k: dwords [22k, 22k+22)
-  uint8_t* const sq = wl + kRegBytes;
-  uint8_t* const tbl = sq + kSeqLds;
+  uint8_t* const wl = lds + wib * kFastWaveLds(tb_bytes);
+  uint8_t* const tabs = wl;  // two tables
+  uint32_t* const regs = reinterpret_cast<uint32_t*>(wl + 2 * LaneTab::BYTES);  // region k: dwords [22k, 22k+22)
+  uint8_t* const tbl = wl + 2 * LaneTab::BYTES + kRegBytes;
   uint8_t* const tbr = tbl + tb_bytes;
   int base = 0;
   for (int v = 0; v < variant; ++v) base += a.counts[v];
@@ -983,34 +1020,33 @@ __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef
   int round = 0;
   if (pos(0) < n_list) {
     ReadDesc d = uniform_desc(a.desc[base + pos(0)]);
-    ReadLanes cur{};
-    if (d.ns > 0) cur = load_read_lanes(b, a, d, r);
+    if (d.ns > 0) fetch_table(tabs, b, a, d, r);
     for (;;) {
+      uint8_t* const tab = tabs + (round & 1) * LaneTab::BYTES;
+      uint8_t* const ntab = tabs + ((round + 1) & 1) * LaneTab::BYTES;
       const bool has_next = pos(round + 1) < n_list;
       ReadDesc dn{};
       if (has_next) dn = uniform_desc(a.desc[base + pos(round + 1)]);
-      ReadLanes nxt{};
       bool fetched = !has_next || dn.ns == 0;
       const int rd = d.rd, lq = d.lq, nch = d.nch, ns = d.ns, s0 = d.s0;
       int nreg = 0;
       if (ns > 0) {
-        reinterpret_cast<uint32_t*>(sq)[r] = cur.seqw;  // 64 lanes x 4 B = kSeqLds
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int64_t p_rb = cur.p_rb;
-        const int p_qb = cur.p_qb, p_len = cur.p_len, p_flag = cur.p_flag;
+        wait_dma();  // this read's table has landed
+        const uint8_t* const sq = tab + LaneTab::SEQ + (d.qoff & 3);
         uint64_t skipped = 0;  // srt[k] = 0 marks (bwamem.c:709), by program position
         for (int c = 0; c < nch; ++c) {
-          const int cs0 = __builtin_amdgcn_readlane(cur.c_s0, c), cs1 = __builtin_amdgcn_readlane(cur.c_s1, c);
+          const int cs0 = uni(lds_i32(tab + LaneTab::CS0 + 4 * c)) - s0;
+          const int cs1 = uni(lds_i32(tab + LaneTab::CS1 + 4 * c)) - s0;
           if (cs1 == cs0) continue;
-          const int64_t clo = readlane64(cur.c_lo, c), chi = readlane64(cur.c_hi, c);
+          const int64_t clo = uni64(lds_i64(tab + LaneTab::WIN + 16 * c));
+          const int64_t chi = uni64(lds_i64(tab + LaneTab::WIN + 16 * c + 8));
           if (chi < clo) continue;  // flagged by prep (the reference would assert)
-          const int rid = __builtin_amdgcn_readlane(cur.c_rid, c);
-          const float frac = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur.c_frac), c));
+          const int rid = uni(lds_i32(tab + LaneTab::RID + 4 * c));
+          const float frac = __int_as_float(uni(lds_i32(tab + LaneTab::FRAC + 4 * c)));
           for (int e = cs0; e < cs1; ++e) {
-            const int64_t srb = readlane64(p_rb, e);
-            const int sqb = __builtin_amdgcn_readlane(p_qb, e), slen = __builtin_amdgcn_readlane(p_len, e);
+            const int64_t srb = uni64(tab_rb(tab, e));
+            const int sqb = uni(lds_i32(tab + LaneTab::QB + 4 * e));
+            const int slen = uni(lds_i32(tab + LaneTab::LEN + 4 * e));
             if (nreg > 0) {
               // containment in an existing region (bwamem.c:678-697), one region per lane
               const uint32_t* g = regs + 22 * min(r, nreg - 1);
@@ -1029,7 +1065,12 @@ __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef
               const int bw2 = g2 < R_w ? g2 : R_w;
               const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
               if (__builtin_amdgcn_ballot_w64(r < nreg && inside && near) != 0) {
-                // an overlapping seed among those already visited (bwamem.c:698-707)
+                // an overlapping seed among those already visited (bwamem.c:698-707), seed per lane
+                const int rr = min(r, kTabLanes - 1);
+                const int64_t p_rb = tab_rb(tab, rr);
+                const int p_qb = lds_i32(tab + LaneTab::QB + 4 * rr);
+                const int p_len = lds_i32(tab + LaneTab::LEN + 4 * rr);
+                const int p_flag = lds_i32(tab + LaneTab::FLAG + 4 * rr);
                 const bool a1 = sqb <= p_qb && sqb + slen - p_qb >= slen >> 2 && (int64_t)(p_qb - sqb) != p_rb - srb;
                 const bool b1 = p_qb <= sqb && p_qb + p_len - sqb >= slen >> 2 && (int64_t)(sqb - p_qb) != srb - p_rb;
                 const bool live = r >= cs0 && r < e && !((skipped >> r) & 1ull) && p_flag == 0;
@@ -1045,8 +1086,8 @@ __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef
             const int tlenL = (int)(srb - clo), tlenR = (int)(chi - x0R);
             fill_two(tbl, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0, tbr, x0R,
                      qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref);
-            if (!fetched) {  // the next read's lanes, in flight during this seed's DP
-              nxt = load_read_lanes(b, a, dn, r);
+            if (!fetched) {  // the next read's table, in flight during this seed's DP
+              fetch_table(ntab, b, a, dn, r);
               fetched = true;
             }
             int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
@@ -1088,9 +1129,17 @@ __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef
                 truesc += (local ? score : x.gscore) - sc0;
               }
             }
-            // seedcov over the chain's seeds (bwamem.c:784-788)
-            const bool in = r >= cs0 && r < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
-            const long long cov = grp_sum64(in ? p_len : 0, 64);
+            // seedcov over the chain's seeds (bwamem.c:784-788), seed per lane
+            long long cov;
+            {
+              const int rr = min(r, kTabLanes - 1);
+              const int64_t p_rb = tab_rb(tab, rr);
+              const int p_qb = lds_i32(tab + LaneTab::QB + 4 * rr);
+              const int p_len = lds_i32(tab + LaneTab::LEN + 4 * rr);
+              const bool in =
+                  r >= cs0 && r < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
+              cov = grp_sum64(in ? p_len : 0, 64);
+            }
             // region nreg as its 88-byte record (rest zero: bwamem.c:718), lane d writes dword d
             {
               const int dw = r < 21 ? r : 21;
@@ -1122,9 +1171,8 @@ __global__ void __launch_bounds__(kBlock) chain2aln_fast_kernel(DevOpt o, DevRef
       }
       a.out_n[rd] = nreg;  // same value from every lane
       if (!has_next) break;
-      if (!fetched) nxt = load_read_lanes(b, a, dn, r);
+      if (!fetched) fetch_table(ntab, b, a, dn, r);
       d = dn;
-      cur = nxt;
       ++round;
     }
   }
@@ -1191,10 +1239,12 @@ static int resident_blocks(K kernel, size_t lds) {
   return per * ncu;
 }
 
+size_t fast_wave_lds(int tb) { return (size_t)kFastWaveLds(tb); }
+
 template <int C>
 static hipError_t launch_c2a_fast(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n,
                                   int tb, const C2AArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)(kBlock / 64) * (kRegBytes + kSeqLds + 2 * tb);
+  const size_t lds = (size_t)(kBlock / 64) * kFastWaveLds(tb);
   static int cap = 0;  // per instantiation; same device kind everywhere
   if (!cap) cap = resident_blocks(chain2aln_fast_kernel<C>, lds);
   const int nb = std::min((n + 3) / 4, cap);
