@@ -257,9 +257,11 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   int hh[CD], ee[CD];
   uint32_t pf[CD];
   uint32_t pf4[T5 ? CD : 1];
+  int Kc[CD], jEc[CD], Fc[CD], jc[CD];
 #pragma unroll
   for (int c = 0; c < CD; ++c) {
     const int j = 64 * c + r;
+    jc[c] = j;
     const int qb = j < qlen ? qp[qa + qd * j] : 0;
     pf[c] = qprof_word(o, qb);
     if (T5) pf4[c] = (uint32_t)(uint8_t)qprof4_val(o, qb);
@@ -267,8 +269,11 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
     hh[c] = j <= qlen ? v : 0;
     ee[c] = 0;
+    // F scan constants: u_j = t_j + j*e_ins, F_j = max_{k<j} u_k - (j-1)*e_ins
+    jEc[c] = j * e_ins;
+    Kc[c] = j * e_ins - oe_ins;    // u_j = max(M_j + Kc, jEc) in band, jEc outside
+    Fc[c] = e_ins - j * e_ins;     // F_j = EX_j + Fc
   }
-  const int jE0 = r * e_ins;  // u_j = t_j + j*e_ins ; F_j = max_{k<j} u_k - (j-1)*e_ins
   {  // band clamp (ksw.c:399-407)
     const int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
     const int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
@@ -280,61 +285,66 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   for (int i = 0; i < tlen; ++i) {
     const int t = __builtin_amdgcn_readfirstlane(tnext);
     tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
-    lo = max(lo, i - w);
-    hi = min(min(hi, i + w + 1), qlen);
+    lo = __builtin_amdgcn_readfirstlane(max(lo, i - w));
+    hi = __builtin_amdgcn_readfirstlane(min(min(hi, i + w + 1), qlen));
+    const int wd = hi > lo ? hi - lo : 0;  // in band: (unsigned)(j - lo) < wd
     const int left0 = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
     const int sh = (t & 3) << 3;
 
     // pass 1 + segmented exclusive max-scan of u
     int M[CD], EX[CD];
-    uint64_t inbm[CD];
+    bool inb[CD];
     int carry = NEG;
 #pragma unroll
     for (int c = 0; c < CD; ++c) {
-      const bool inb = r >= lo - 64 * c && r < hi - 64 * c;
-      inbm[c] = __builtin_amdgcn_ballot_w64(inb);
+      inb[c] = (unsigned)(jc[c] - lo) < (unsigned)wd;
       int sc;
       if (T5 && t == 4) sc = (int)(int8_t)(pf4[c] & 0xff);
       else sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
       const int m = hh[c] ? hh[c] + sc : 0;
       M[c] = m;
-      const int u = (inb ? max(m - oe_ins, 0) : 0) + jE0 + 64 * c * e_ins;
+      const int u = inb[c] ? max(m + Kc[c], jEc[c]) : jEc[c];
       int x = c == 0 ? u : max(u, carry);
       x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
       EX[c] = dpp<DPP_WAVE_SHR1>(carry, x);  // lane 0 takes the carry from the segments before
-      carry = __builtin_amdgcn_readlane(x, 63);
+      if (c + 1 < CD) carry = __builtin_amdgcn_readlane(x, 63);
     }
     // pass 2: H, E, row-max key, next-row state
-    int rk = 0, prev63 = 0, h1 = left0;
-    const int seg_hi = hi >> 6, seg_lo = lo >> 6;
+    int rk = 0, prev63 = 0;
+    int h1c[CD];
 #pragma unroll
     for (int c = 0; c < CD; ++c) {
-      const bool inb = (inbm[c] >> r) & 1ull;
-      const int f = EX[c] - jE0 - (64 * c - 1) * e_ins;
+      const int f = EX[c] + Fc[c];
       const int h = max(max(M[c], ee[c]), f);
       const int en = max(max(ee[c] - e_del, M[c] - oe_del), 0);
-      rk = max(rk, inb ? ((h << 10) + 64 * c + r) : 0);
+      rk = max(rk, inb[c] ? (h << 10 | jc[c]) : 0);
       const int hs = dpp<DPP_WAVE_SHR1>(prev63, h);  // H(i, j-1)
-      prev63 = __builtin_amdgcn_readlane(h, 63);
-      if (c == seg_hi && hi > lo) h1 = __builtin_amdgcn_readlane(hs, hi & 63);  // H(i, hi-1)
-      hh[c] = inb ? hs : hh[c];
-      ee[c] = inb ? en : ee[c];
+      if (c + 1 < CD) prev63 = __builtin_amdgcn_readlane(h, 63);
+      h1c[c] = __builtin_amdgcn_readlane(hs, (hi - 64 * c) & 63);  // H(i, hi-1) if hi is in segment c
+      hh[c] = inb[c] ? hs : hh[c];
+      ee[c] = inb[c] ? en : ee[c];
     }
-    // eh[lo].h = first-column value (only matters when lo < hi), eh[hi] = {h1, 0}
+    // h1 = H(i, hi-1), or the first-column value when the band is empty
+    int h1 = h1c[0];
+#pragma unroll
+    for (int c = 1; c < CD; ++c) h1 = (hi >> 6) == c ? h1c[c] : h1;
+    h1 = hi > lo ? h1 : left0;
+    // eh[lo].h = first-column value (only when lo < hi), eh[hi] = {h1, 0}:
+    // single-lane writes at uniform targets; a target outside [0,64) hits no lane
+    const int tlo = hi > lo ? lo : -1;
 #pragma unroll
     for (int c = 0; c < CD; ++c) {
-      if (c == seg_lo && lo < hi) hh[c] = r == (lo & 63) ? left0 : hh[c];
-      if (c == seg_hi) {
-        hh[c] = r == (hi & 63) ? h1 : hh[c];
-        ee[c] = r == (hi & 63) ? 0 : ee[c];
-      }
+      hh[c] = r == tlo - 64 * c ? left0 : hh[c];
+      const bool at_hi = r == hi - 64 * c;
+      hh[c] = at_hi ? h1 : hh[c];
+      ee[c] = at_hi ? 0 : ee[c];
     }
     rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
     rk = __builtin_amdgcn_readlane(rk, 63);
     rows += 1;
-    cells += hi > lo ? hi - lo : 0;
+    cells += wd;
     if (max(lo, hi) == qlen) {  // ksw.c:450-453
-      if (!(esc > h1)) ei = i;
+      ei = esc > h1 ? ei : i;
       esc = max(esc, h1);
     }
     const int mrow = rk >> 10, mj = rk & 1023;
@@ -353,13 +363,13 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     // last non-zero column in [lo,hi]
     int nlo = hi, jl = -1;
 #pragma unroll
-    for (int c = 0; c < CD; ++c) {
+    for (int c = CD - 1; c >= 0; --c) {
       const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[c] | ee[c]) != 0);
-      const uint64_t f = nz & inbm[c];
-      uint64_t l = f;
-      if (c == seg_hi) l |= nz & (1ull << (hi & 63));
-      if (f && nlo == hi) nlo = 64 * c + __builtin_ctzll(f);
-      if (l) jl = 64 * c + 63 - __builtin_clzll(l);
+      const uint64_t f = nz & __builtin_amdgcn_ballot_w64(inb[c]);
+      const int hc = hi - 64 * c;
+      const uint64_t l = f | (nz & ((unsigned)hc < 64u ? 1ull << hc : 0ull));
+      nlo = f ? 64 * c + __builtin_ctzll(f) : nlo;  // descending c: the lowest segment wins
+      jl = (jl < 0 && l) ? 64 * c + 63 - __builtin_clzll(l) : jl;
     }
     if (jl < 0) jl = nlo - 1;
     lo = nlo;
