@@ -277,7 +277,7 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   {  // band clamp (ksw.c:399-407)
     const int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
     const int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
-    w = min(w, min(mi, md));
+    w = __builtin_amdgcn_readfirstlane(min(w, min(mi, md)));
   }
   int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0, lo = 0, hi = qlen;
   int cells = 0, rows = 0;
