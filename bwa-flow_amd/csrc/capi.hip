@@ -91,7 +91,7 @@ struct InLayout {
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
-  DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts, d_sort_tmp;
+  DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   HostBuf h_in, h_out, h_n, h_stats;
   bool busy = false;
   int32_t n_reads = 0, n_seeds = 0;
@@ -207,7 +207,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     s.d_in.release(); s.d_win.release(); s.d_srt.release(); s.d_prog.release(); s.d_desc.release();
     s.d_out.release(); s.d_n.release();
-    s.d_stats.release(); s.d_lists.release(); s.d_counts.release(); s.d_sort_tmp.release();
+    s.d_stats.release(); s.d_lists.release(); s.d_counts.release();
     s.h_in.release(); s.h_out.release(); s.h_n.release(); s.h_stats.release();
     if (s.ev0) (void)hipEventDestroy(s.ev0);
     if (s.ev1) (void)hipEventDestroy(s.ev1);
@@ -284,31 +284,24 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   HIPC(s.d_prog.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(prog)");
   const size_t nr = (size_t)std::max(db.n_reads, 1);
   HIPC(s.d_desc.ensure(sizeof(ReadDesc) * nr), "hipMalloc(desc)");
-  // keys_in | vals_in | keys_out | vals_out, n_reads each
-  HIPC(s.d_lists.ensure(4 * sizeof(int32_t) * nr), "hipMalloc(lists)");
-  uint32_t* keys_in = s.d_lists.as<uint32_t>();
-  int32_t* vals_in = (int32_t*)(keys_in + nr);
-  uint32_t* keys_out = (uint32_t*)(vals_in + nr);
-  int32_t* vals_out = (int32_t*)(keys_out + nr);
-  size_t tmp_bytes = 0;
-  HIPC(sort_reads(nullptr, tmp_bytes, keys_in, keys_out, vals_in, vals_out, std::max(db.n_reads, 1), st),
-       "sort size query");
-  HIPC(s.d_sort_tmp.ensure(tmp_bytes), "hipMalloc(sort temp)");
-  // [0..15] per-variant read counts, [16 + 8v + xcc] per-XCD queue heads
-  HIPC(s.d_counts.ensure(sizeof(int32_t) * 64), "hipMalloc(counts)");
-  HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * 64, st), "memset counts");
+  // bins | read_list, n_reads each
+  HIPC(s.d_lists.ensure(2 * sizeof(int32_t) * nr), "hipMalloc(lists)");
+  int32_t* bins = s.d_lists.as<int32_t>();
+  int32_t* read_list = bins + nr;
+  // [0..15] per-variant read counts, [16 + 8v + xcc] queue heads (generic
+  // kernel), [64 .. 64 + 3*256) read-order histogram
+  constexpr size_t kCountWords = 64 + 3 * 256;
+  HIPC(s.d_counts.ensure(sizeof(int32_t) * kCountWords), "hipMalloc(counts)");
+  HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * kCountWords, st), "memset counts");
   if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
   HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(),
                          s.d_prog.as<bwagpu_seed_t>(), d_stats, st),
        "chain_prep launch");
-  HIPC(launch_read_keys(db, keys_in, vals_in, s.d_counts.as<int32_t>(), d_stats, st), "read_keys launch");
-  if (db.n_reads) {
-    size_t tb2 = s.d_sort_tmp.cap;
-    HIPC(sort_reads(s.d_sort_tmp.p, tb2, keys_in, keys_out, vals_in, vals_out, db.n_reads, st), "sort reads");
-    HIPC(launch_read_desc(db, vals_out, s.d_desc.as<ReadDesc>(), st), "read_desc launch");
-  }
+  HIPC(launch_read_order(db, bins, s.d_counts.as<int32_t>() + 64, s.d_counts.as<int32_t>(), s.d_desc.as<ReadDesc>(),
+                         read_list, d_stats, st),
+       "read order launch");
   C2AArgs a;
-  a.read_list = vals_out;
+  a.read_list = read_list;
   a.desc = s.d_desc.as<ReadDesc>();
   a.counts = s.d_counts.as<int32_t>();
   a.win = s.d_win.as<ChainWin>();

@@ -80,12 +80,11 @@ constexpr int kBlock = 256;  // threads per workgroup (4 waves)
 // host-side launchers (sw_kernels.hip)
 hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, ChainWin* win, uint64_t* srt,
                              bwagpu_seed_t* prog, int64_t* stats, hipStream_t st);
-// per-read sort keys [variant | task shape] + per-variant counts
-hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, int32_t* counts, int64_t* stats,
-                            hipStream_t st);
-// stable radix sort of (key, read) pairs (rocPRIM)
-hipError_t sort_reads(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                      const int32_t* vals_in, int32_t* vals_out, int n, hipStream_t st);
+// read order for the wave kernels: counting sort by [variant | cost] that
+// writes read_list[pos] and desc[pos] (bins: n_reads scratch, hist: 3*256
+// zeroed counters, counts: per-variant read counts)
+hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, int32_t* counts, ReadDesc* desc,
+                             int32_t* list, int64_t* stats, hipStream_t st);
 // read_list: reads sorted by key; d_count: per-variant counts (device); the
 // variant's reads start at the sum of the lower variants' counts; max_list
 // bounds the grid
@@ -105,8 +104,7 @@ hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, con
                             int tb_bytes, const C2AArgs& a, hipStream_t st);
 // LDS bytes per wave of chain2aln_fast_kernel for target row buffers of tb bytes
 size_t fast_wave_lds(int tb);
-// descriptors of the sorted reads
-hipError_t launch_read_desc(const DevBatch& b, const int32_t* sorted_reads, ReadDesc* desc, hipStream_t st);
+
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,

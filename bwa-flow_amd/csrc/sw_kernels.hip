@@ -558,24 +558,39 @@ __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, D
 }
 
 // ------------------------------------------------------------ read order
-// Each read gets a sort key [variant | 0xffff - estimated cost], so one
-// ascending sort groups reads by kernel variant and orders each variant's
-// reads by DEcreasing expected DP work — longest-processing-time-first for
-// the dynamic per-XCD work queue of chain2aln_kernel, which keeps the tail of
-// the launch short.  The estimate uses the first chain's top seed (the first
-// extension mem_chain2aln performs): rows ~ qlen + 16 per side, each row
-// costing ~1 + qlen/64 wave-wide segments.  Reads without chains sort last.
-__global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* keys, int32_t* vals, int32_t* counts,
+// Reads are dealt to the wave kernels in order [variant | cost, descending]:
+// grouped by kernel variant (read length -> columns per lane; seed/chain
+// counts -> fast or generic kernel), and within a variant longest-first
+// (LPT), so the static deal of chain2aln_fast_kernel ends with short reads.
+// The cost estimate uses the first chain's top seed (the first extension
+// mem_chain2aln performs): rows ~ qlen + 16 per side, each row costing
+// ~1 + qlen/64 wave-wide segments.  The order is a counting sort over
+// kNumVariants x kCostBins bins (histogram -> scan -> scatter), which also
+// writes each read's descriptor in its slot.
+constexpr int kCostBins = 256;
+constexpr int kBins = kNumVariants * kCostBins;
+
+__device__ __forceinline__ int read_variant(const DevBatch& b, int rd, int lq) {
+  const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
+  const int nseeds = b.chain_seed_off[c1] - b.chain_seed_off[c0];
+  const bool small = nseeds <= kFastMaxSeeds && c1 - c0 <= kFastMaxChains;
+  int v = -1;
+  for (int k = kNumVariants - 1; k >= 0; --k)
+    if (lq <= kVariants[k].G * kVariants[k].C && (small || !kVariants[k].fast)) v = k;
+  return v;
+}
+
+__global__ void __launch_bounds__(256) read_bins_kernel(DevBatch b, int32_t* bins, int32_t* hist, int32_t* counts,
                                                         int64_t* stats) {
+  __shared__ int h[kBins];
+  for (int k = threadIdx.x; k < kBins; k += blockDim.x) h[k] = 0;
+  __syncthreads();
   const int rd = blockIdx.x * blockDim.x + threadIdx.x;
   int v = -1;
   if (rd < b.n_reads) {
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+    v = read_variant(b, rd, lq);
     const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
-    const int nseeds = b.chain_seed_off[c1] - b.chain_seed_off[c0];
-    const bool small = nseeds <= kFastMaxSeeds && c1 - c0 <= kFastMaxChains;
-    for (int k = kNumVariants - 1; k >= 0; --k)
-      if (lq <= kVariants[k].G * kVariants[k].C && (small || !kVariants[k].fast)) v = k;
     uint32_t cost = 0;
     int nseed = 0;
     for (int c = c0; c < c1; ++c) {
@@ -594,8 +609,9 @@ __global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* ke
       atomicOr((unsigned long long*)&stats[ST_ERR], (unsigned long long)ERR_LEN);
       v = kNumVariants - 1;
     }
-    keys[rd] = (uint32_t)v << 16 | (0xffffu - min(cost, 0xffffu));
-    vals[rd] = rd;
+    const int bin = v * kCostBins + (kCostBins - 1 - (int)min(cost >> 2, (uint32_t)(kCostBins - 1)));
+    bins[rd] = bin;
+    atomicAdd(&h[bin], 1);
   }
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -603,23 +619,57 @@ __global__ void __launch_bounds__(256) read_keys_kernel(DevBatch b, uint32_t* ke
     const unsigned long long m = __ballot(v == k);
     if (m != 0 && lane == __ffsll((long long)m) - 1) atomicAdd(&counts[k], __popcll(m));
   }
+  __syncthreads();
+  for (int k = threadIdx.x; k < kBins; k += blockDim.x)
+    if (h[k]) atomicAdd(&hist[k], h[k]);
 }
 
-hipError_t launch_read_keys(const DevBatch& b, uint32_t* keys, int32_t* vals, int32_t* counts, int64_t* stats,
-                            hipStream_t st) {
-  if (b.n_reads == 0) return hipSuccess;
-  hipLaunchKernelGGL(read_keys_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, keys, vals, counts, stats);
-  return hipGetLastError();
+// exclusive scan of the kBins bin counts, in place (one block)
+__global__ void __launch_bounds__(256) bin_scan_kernel(int32_t* hist) {
+  __shared__ int part[256];
+  constexpr int per = (kBins + 255) / 256;
+  const int t = threadIdx.x;
+  int v[per], sum = 0;
+#pragma unroll
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    v[k] = i < kBins ? hist[i] : 0;
+    sum += v[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int x = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+#pragma unroll
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i < kBins) hist[i] = run;
+    run += v[k];
+  }
 }
 
-// ------------------------------------------------------------ read descriptors
-// The sorted read order as self-contained descriptors: the fast kernel loads
-// one with a single scalar load instead of a chain of dependent lookups.
-__global__ void __launch_bounds__(256) read_desc_kernel(DevBatch b, const int32_t* __restrict__ sorted,
-                                                        ReadDesc* desc) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= b.n_reads) return;
-  const int rd = sorted[p];
+__global__ void __launch_bounds__(256) read_scatter_kernel(DevBatch b, const int32_t* __restrict__ bins,
+                                                           int32_t* offs, ReadDesc* desc, int32_t* list) {
+  // ranks within the block from an LDS histogram, one global reservation per
+  // (block, bin): hot bins see a few hundred global atomics, not one per read
+  __shared__ int lh[kBins];
+  __shared__ int lbase[kBins];
+  for (int k = threadIdx.x; k < kBins; k += blockDim.x) lh[k] = 0;
+  __syncthreads();
+  const int rd = blockIdx.x * blockDim.x + threadIdx.x;
+  const int bin = rd < b.n_reads ? bins[rd] : 0;
+  const int rank = rd < b.n_reads ? atomicAdd(&lh[bin], 1) : 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < kBins; k += blockDim.x)
+    if (lh[k]) lbase[k] = atomicAdd(&offs[k], lh[k]);
+  __syncthreads();
+  if (rd >= b.n_reads) return;
+  const int p = lbase[bin] + rank;
   ReadDesc d;
   d.qoff = b.seq_off[rd];
   d.rd = rd;
@@ -629,11 +679,16 @@ __global__ void __launch_bounds__(256) read_desc_kernel(DevBatch b, const int32_
   d.s0 = b.chain_seed_off[d.c0];
   d.ns = b.chain_seed_off[d.c0 + d.nch] - d.s0;
   desc[p] = d;
+  list[p] = rd;
 }
 
-hipError_t launch_read_desc(const DevBatch& b, const int32_t* sorted, ReadDesc* desc, hipStream_t st) {
+hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, int32_t* counts, ReadDesc* desc,
+                             int32_t* list, int64_t* stats, hipStream_t st) {
   if (b.n_reads == 0) return hipSuccess;
-  hipLaunchKernelGGL(read_desc_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, sorted, desc);
+  const int nb = (b.n_reads + 255) / 256;
+  hipLaunchKernelGGL(read_bins_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, counts, stats);
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(256), 0, st, hist);
+  hipLaunchKernelGGL(read_scatter_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, desc, list);
   return hipGetLastError();
 }
 
@@ -920,7 +975,7 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 // Containment (bwamem.c:678-697), the overlap test (698-707) and seedcov
 // (784-788) are lane-parallel tests (lane i: region i or seed i) + a ballot or
 // a reduction.
-// Scheduling is static: reads are cost-sorted (read_keys_kernel) and dealt to
+// Scheduling is static: reads are cost-sorted (read_bins_kernel) and dealt to
 // the resident waves in zig-zag rounds, so a wave knows its next read and DMAs
 // that read's table (double-buffered) while the current read's DP runs; the
 // DMA goes out after the current read's first target fill, so no fill waits
