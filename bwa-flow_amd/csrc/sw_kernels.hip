@@ -80,40 +80,50 @@ struct Grp {
   static __device__ __forceinline__ int bcast(int v, int src) { return __shfl(v, src, G); }
 };
 
-// DPP-fused max/min: `x = op(x, x[from DPP source lane])` in ONE instruction.
-// With bound_ctrl off, lanes whose DPP source lies outside the row are not
-// written, i.e. keep x — the identity for a scan.  The leading s_nop covers the
-// VALU-write -> DPP-read hazard (inline asm is opaque to the hazard recognizer).
-#define BWAGPU_DPP_OP(name, op, ctrl)                                                                    \
-  __device__ __forceinline__ int name(int x) {                                                          \
-    asm volatile("s_nop 1\n\t" op " %0, %0, %0 " ctrl " row_mask:0xf bank_mask:0xf" : "+v"(x));        \
-    return x;                                                                                           \
+// DPP max/min steps: `x = op(x, x[DPP source lane])` as ONE v_max_i32_dpp.
+// Lanes whose source lies outside the row (or whose row is masked off) keep
+// x — the identity for a scan or a reduction.  Inline asm, because the
+// update_dpp builtin + max is not folded by the backend's DPP combiner here
+// (measured: +23 VALU per CD=1 row); the asm carries its own s_nop for the
+// VALU-write -> DPP-read hazard.  BWAGPU_BUILTIN_DPP selects the builtin form.
+constexpr int DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143;
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int dpp_max(int x) {
+  return max(x, __builtin_amdgcn_update_dpp(x, x, CTRL, RMASK, 0xF, false));
+}
+template <int CTRL, int RMASK>
+__device__ __forceinline__ int dpp_min(int x) {
+  return min(x, __builtin_amdgcn_update_dpp(x, x, CTRL, RMASK, 0xF, false));
+}
+#ifndef BWAGPU_BUILTIN_DPP
+#define BWAGPU_DPP(name, op, ctrl, rmask, fn)                                                         \
+  __device__ __forceinline__ int name(int x) {                                                        \
+    asm volatile("s_nop 1\n\t" op " %0, %0, %0 " ctrl " row_mask:" rmask " bank_mask:0xf" : "+v"(x)); \
+    return x;                                                                                         \
   }
-BWAGPU_DPP_OP(max_shr1, "v_max_i32_dpp", "row_shr:1")
-BWAGPU_DPP_OP(max_shr2, "v_max_i32_dpp", "row_shr:2")
-BWAGPU_DPP_OP(max_shr4, "v_max_i32_dpp", "row_shr:4")
-BWAGPU_DPP_OP(max_shr8, "v_max_i32_dpp", "row_shr:8")
-BWAGPU_DPP_OP(max_ror8, "v_max_i32_dpp", "row_ror:8")
-BWAGPU_DPP_OP(max_ror4, "v_max_i32_dpp", "row_ror:4")
-BWAGPU_DPP_OP(max_ror2, "v_max_i32_dpp", "row_ror:2")
-BWAGPU_DPP_OP(max_ror1, "v_max_i32_dpp", "row_ror:1")
-BWAGPU_DPP_OP(min_ror8, "v_min_i32_dpp", "row_ror:8")
-BWAGPU_DPP_OP(min_ror4, "v_min_i32_dpp", "row_ror:4")
-BWAGPU_DPP_OP(min_ror2, "v_min_i32_dpp", "row_ror:2")
-BWAGPU_DPP_OP(min_ror1, "v_min_i32_dpp", "row_ror:1")
-#undef BWAGPU_DPP_OP
-// cross-row steps of a 64-lane reduction/scan: row_bcast:15 feeds lane 15 of
-// rows 0/2 into rows 1/3, row_bcast:31 feeds lane 31 into rows 2/3
-#define BWAGPU_DPP_BC(name, op, ctrl, rmask)                                                             \
-  __device__ __forceinline__ int name(int x) {                                                          \
-    asm volatile("s_nop 1\n\t" op " %0, %0, %0 " ctrl " row_mask:" rmask " bank_mask:0xf" : "+v"(x));  \
-    return x;                                                                                           \
-  }
-BWAGPU_DPP_BC(max_bc15, "v_max_i32_dpp", "row_bcast:15", "0xa")
-BWAGPU_DPP_BC(max_bc31, "v_max_i32_dpp", "row_bcast:31", "0xc")
-BWAGPU_DPP_BC(min_bc15, "v_min_i32_dpp", "row_bcast:15", "0xa")
-BWAGPU_DPP_BC(min_bc31, "v_min_i32_dpp", "row_bcast:31", "0xc")
-#undef BWAGPU_DPP_BC
+#else
+#define BWAGPU_DPP(name, op, ctrl, rmask, fn) \
+  __device__ __forceinline__ int name(int x) { return fn(x); }
+#endif
+BWAGPU_DPP(max_shr1, "v_max_i32_dpp", "row_shr:1", "0xf", (dpp_max<DPP_ROW_SHR(1), 0xF>))
+BWAGPU_DPP(max_shr2, "v_max_i32_dpp", "row_shr:2", "0xf", (dpp_max<DPP_ROW_SHR(2), 0xF>))
+BWAGPU_DPP(max_shr4, "v_max_i32_dpp", "row_shr:4", "0xf", (dpp_max<DPP_ROW_SHR(4), 0xF>))
+BWAGPU_DPP(max_shr8, "v_max_i32_dpp", "row_shr:8", "0xf", (dpp_max<DPP_ROW_SHR(8), 0xF>))
+BWAGPU_DPP(max_ror8, "v_max_i32_dpp", "row_ror:8", "0xf", (dpp_max<DPP_ROW_ROR(8), 0xF>))
+BWAGPU_DPP(max_ror4, "v_max_i32_dpp", "row_ror:4", "0xf", (dpp_max<DPP_ROW_ROR(4), 0xF>))
+BWAGPU_DPP(max_ror2, "v_max_i32_dpp", "row_ror:2", "0xf", (dpp_max<DPP_ROW_ROR(2), 0xF>))
+BWAGPU_DPP(max_ror1, "v_max_i32_dpp", "row_ror:1", "0xf", (dpp_max<DPP_ROW_ROR(1), 0xF>))
+BWAGPU_DPP(min_ror8, "v_min_i32_dpp", "row_ror:8", "0xf", (dpp_min<DPP_ROW_ROR(8), 0xF>))
+BWAGPU_DPP(min_ror4, "v_min_i32_dpp", "row_ror:4", "0xf", (dpp_min<DPP_ROW_ROR(4), 0xF>))
+BWAGPU_DPP(min_ror2, "v_min_i32_dpp", "row_ror:2", "0xf", (dpp_min<DPP_ROW_ROR(2), 0xF>))
+BWAGPU_DPP(min_ror1, "v_min_i32_dpp", "row_ror:1", "0xf", (dpp_min<DPP_ROW_ROR(1), 0xF>))
+// cross-row steps: row_bcast:15 feeds lane 15 of rows 0/2 into rows 1/3,
+// row_bcast:31 feeds lane 31 into rows 2/3
+BWAGPU_DPP(max_bc15, "v_max_i32_dpp", "row_bcast:15", "0xa", (dpp_max<DPP_BCAST15, 0xA>))
+BWAGPU_DPP(max_bc31, "v_max_i32_dpp", "row_bcast:31", "0xc", (dpp_max<DPP_BCAST31, 0xC>))
+BWAGPU_DPP(min_bc15, "v_min_i32_dpp", "row_bcast:15", "0xa", (dpp_min<DPP_BCAST15, 0xA>))
+BWAGPU_DPP(min_bc31, "v_min_i32_dpp", "row_bcast:31", "0xc", (dpp_min<DPP_BCAST31, 0xC>))
+#undef BWAGPU_DPP
 constexpr int DPP_WAVE_SHR1 = 0x138;
 
 template <>
