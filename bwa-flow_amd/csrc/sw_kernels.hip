@@ -349,6 +349,21 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       hh[c] = at_hi ? h1 : hh[c];
       ee[c] = at_hi ? 0 : ee[c];
     }
+    // zero-trim of the band for the next row (ksw.c:466-469), computed ahead of
+    // the row-max reduction (independent of it; applied only if no break):
+    // first non-zero column in [lo,hi), last non-zero column in [lo,hi]
+    int nlo = hi, jl = -1;
+#pragma unroll
+    for (int c = CD - 1; c >= 0; --c) {
+      const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[c] | ee[c]) != 0);
+      const uint64_t f = nz & __builtin_amdgcn_ballot_w64(inb[c]);
+      const int hc = hi - 64 * c;
+      const uint64_t l = f | (nz & ((unsigned)hc < 64u ? 1ull << hc : 0ull));
+      nlo = f ? 64 * c + __builtin_ctzll(f) : nlo;  // descending c: the lowest segment wins
+      jl = (jl < 0 && l) ? 64 * c + 63 - __builtin_clzll(l) : jl;
+    }
+    if (jl < 0) jl = nlo - 1;
+    const int nhi = min(jl + 2, qlen);
     rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
     rk = __builtin_amdgcn_readlane(rk, 63);
     rows += 1;
@@ -369,21 +384,8 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       const int drop = di > dj ? best - mrow - (di - dj) * e_del : best - mrow - (dj - di) * e_ins;
       if (drop > zdrop) break;
     }
-    // zero-trim the band (ksw.c:466-469): first non-zero column in [lo,hi),
-    // last non-zero column in [lo,hi]
-    int nlo = hi, jl = -1;
-#pragma unroll
-    for (int c = CD - 1; c >= 0; --c) {
-      const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[c] | ee[c]) != 0);
-      const uint64_t f = nz & __builtin_amdgcn_ballot_w64(inb[c]);
-      const int hc = hi - 64 * c;
-      const uint64_t l = f | (nz & ((unsigned)hc < 64u ? 1ull << hc : 0ull));
-      nlo = f ? 64 * c + __builtin_ctzll(f) : nlo;  // descending c: the lowest segment wins
-      jl = (jl < 0 && l) ? 64 * c + 63 - __builtin_clzll(l) : jl;
-    }
-    if (jl < 0) jl = nlo - 1;
     lo = nlo;
-    hi = min(jl + 2, qlen);
+    hi = nhi;
   }
   tl.cells += cells;
   tl.rows += rows;
