@@ -235,6 +235,10 @@ __device__ __forceinline__ int qprof4_val(const DevOpt& o, int q) {
   return v;
 }
 
+// Optional per-read trace (bwagpu_debug_set_trace): 8 words per read index:
+// start/end s_memrealtime (100 MHz), DP rows, DP cells, HW_ID, XCC_ID.
+__device__ uint32_t* g_trace = nullptr;
+
 struct ExtOut {
   int score, qle, tle, gtle, gscore, max_off;
 };
@@ -390,6 +394,13 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   tl.cells += cells;
   tl.rows += rows;
   tl.calls += 1;
+#ifdef BWAGPU_CD_STATS
+  if (g_trace && r == 0) {  // diagnostics: rows / cells / calls per segment count
+    atomicAdd(&g_trace[4 * CD + 0], (uint32_t)rows);
+    atomicAdd(&g_trace[4 * CD + 1], (uint32_t)cells);
+    atomicAdd(&g_trace[4 * CD + 2], 1u);
+  }
+#endif
   return ExtOut{best, bj + 1, bi + 1, ei + 1, esc, off};
 }
 
@@ -705,9 +716,7 @@ hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, in
 }
 
 // ------------------------------------------------------------ diagnostics
-// Optional per-read trace (bwagpu_debug_set_trace): 8 words per read index:
-// start/end s_memrealtime (100 MHz), DP rows, DP cells, HW_ID, XCC_ID.
-__device__ uint32_t* g_trace = nullptr;
+
 
 hipError_t set_trace(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p)); }
 
