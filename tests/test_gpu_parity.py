@@ -159,3 +159,57 @@ def test_device_entry_point_with_torch_buffers(refd):
     assert G.region_mismatch(compact(batch, regs, nn), want) is None
     assert int(stats[0]) > 0 and int(stats[3]) == 0
     eng.close()
+
+
+@pytest.mark.parametrize("len_mode,min_seed,pairs", [(150, 19, 800), (0, 19, 600), (250, 12, 400), (400, 12, 300),
+                                                     (700, 8, 150), (1000, 8, 60)])
+def test_synthetic_batches_vs_oracle(len_mode, min_seed, pairs):
+    """seeded synthetic reads of every kernel variant's shape — 100-256 bp on
+    the fast kernel, > 32 seeds (short min seed length) and 257-1023 bp on the
+    generic kernel — against the oracle on the same inputs, bit for bit"""
+    from bwagpu.synth import SynthRef, synth_batch
+    ref = SynthRef(77, 2_000_000, 3)
+    b = synth_batch(ref, 5 + len_mode, pairs, len_mode, min_seed)
+    opt = abi.default_opt()
+    eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
+    regs, n = eng.chain2aln(b)
+    st = eng.last_stats()
+    R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
+    oregs, on, ostats = oracle.chain2aln("oracle", opt, R, b, n_threads=4)
+    assert np.array_equal(n, on), f"{int((n != on).sum())} reads with a different region count"
+    assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
+    assert (st["cells"], st["rows"], st["ext_calls"]) == tuple(int(x) for x in ostats[:3])
+    eng.close()
+
+
+def split_seeds(b: Batch, piece: int) -> Batch:
+    """every seed cut into exact sub-matches of `piece` bases (score = length):
+    valid mem_chain2aln input with many seeds per chain"""
+    seeds, cso = [], [0]
+    for c in range(b.n_chains):
+        for s in b.seeds[b.chain_seed_off[c]:b.chain_seed_off[c + 1]]:
+            for k in range(0, int(s["len"]), piece):
+                ln = min(piece, int(s["len"]) - k)
+                seeds.append((int(s["rbeg"]) + k, int(s["qbeg"]) + k, ln, ln, 0))
+        cso.append(len(seeds))
+    arr = np.array(seeds, dtype=abi.SEED_DTYPE) if seeds else np.zeros(0, abi.SEED_DTYPE)
+    return Batch(b.seq_off, b.seq, b.read_chain_off, np.array(cso, np.int32), b.chain_rid, b.chain_frac_rep, arr)
+
+
+@pytest.mark.parametrize("len_mode,piece", [(150, 6), (250, 9), (400, 14)])
+def test_many_seed_reads_vs_oracle(len_mode, piece):
+    """reads with more seeds or chains than the fast kernel keeps per wave
+    (> 32) go to the generic kernel; both against the oracle"""
+    from bwagpu.synth import SynthRef, synth_batch
+    ref = SynthRef(78, 1_000_000, 2)
+    b = split_seeds(synth_batch(ref, 9 + len_mode, 120, len_mode), piece)
+    spr = b.chain_seed_off[b.read_chain_off[1:]] - b.chain_seed_off[b.read_chain_off[:-1]]
+    assert (spr > 32).any() and (spr <= 32).any()
+    opt = abi.default_opt()
+    eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
+    regs, n = eng.chain2aln(b)
+    R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
+    oregs, on, _ = oracle.chain2aln("oracle", opt, R, b, n_threads=4)
+    assert np.array_equal(n, on)
+    assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
+    eng.close()
