@@ -64,3 +64,72 @@ def synth_batch(ref: SynthRef, seed: int, n_pairs: int, len_mode: int = 150, min
         raise RuntimeError("synth_reads failed")
     r, c, s = nr.value, nc.value, ns.value
     return Batch(seq_off[:r + 1], seq[:seq_off[r]], rco[:r + 1], cso[:c + 1], rid[:c], fr[:c], seeds[:s])
+
+
+def _mutate(rng, q, sub=0.03, indel=0.01):
+    """a diverged copy of q: substitutions, 1-3 base indels, N kept as N"""
+    out = []
+    r = rng.random(len(q))
+    for k, b in enumerate(q.tolist()):
+        x = r[k]
+        if x < indel / 2:
+            continue
+        if x < indel:
+            out.extend(rng.integers(0, 4, int(rng.integers(1, 4))).tolist())
+        out.append(int(rng.integers(0, 4)) if (b < 4 and rng.random() < sub) else b)
+    return np.array(out, np.uint8)
+
+
+def mate_rescue_tasks(rng, n, a=1, min_seed_len=19, qlens=(150,), win=(300, 700), p_hit=0.6, p_two=0.15,
+                      p_n=0.02, xtra_mode="matesw"):
+    """ksw_align2 tasks shaped like mem_matesw's (bwa/bwamem_pair.c:131-151):
+    the mate (length from qlens) against a reference window of
+    (high - low) + l_ms bases; with probability p_hit the window holds a
+    diverged copy of the mate (a rescue), with p_two a second partial copy
+    (the 2nd-best score path), otherwise random sequence.
+
+    xtra_mode "matesw": XSUBO|XSTART|(l_ms*a < 250 ? XBYTE : 0)|min_seed_len*a
+    (exactly what mem_matesw passes); "mix": also plain, XBYTE-saturating,
+    XSTOP and XSTART-only calls.  Returns (tasks, qpool, tpool)."""
+    tasks = np.zeros(n, abi.ALIGN2_TASK_DTYPE)
+    qs, ts, qo, to = [], [], 0, 0
+    for k in range(n):
+        ql = int(qlens[int(rng.integers(0, len(qlens)))])
+        q = rng.integers(0, 4, ql).astype(np.uint8)
+        if p_n and ql:
+            q[rng.random(ql) < p_n] = 4
+        tl = int(rng.integers(win[0], win[1] + 1)) + ql
+        t = rng.integers(0, 4, tl).astype(np.uint8)
+        if rng.random() < p_hit and ql:
+            m = _mutate(rng, q)
+            if rng.random() < 0.25:  # partially outside the window: a clipped hit
+                cut = int(rng.integers(0, max(1, len(m) // 2)))
+                m = m[cut:] if rng.random() < 0.5 else m[:len(m) - cut]
+            p = int(rng.integers(0, max(1, tl - len(m))))
+            t[p:p + len(m)] = m[:tl - p]
+            if rng.random() < p_two:
+                m2 = _mutate(rng, q, sub=0.06)[: int(rng.integers(max(1, ql // 4), ql + 1))]
+                p2 = int(rng.integers(0, max(1, tl - len(m2))))
+                t[p2:p2 + len(m2)] = m2[:tl - p2]
+        if p_n and tl:
+            t[rng.random(tl) < p_n / 4] = 4
+        xtra = abi.KSW_XSUBO | abi.KSW_XSTART | (abi.KSW_XBYTE if ql * a < 250 else 0) | (min_seed_len * a)
+        if xtra_mode == "mix":
+            u = rng.random()
+            if u < 0.1:
+                xtra = 0
+            elif u < 0.2:
+                xtra = abi.KSW_XBYTE | abi.KSW_XSTART
+            elif u < 0.3:
+                xtra = abi.KSW_XSTOP | int(rng.integers(1, 200)) | (abi.KSW_XBYTE if rng.random() < 0.5 else 0)
+            elif u < 0.4:
+                xtra = abi.KSW_XSUBO | abi.KSW_XSTART | int(rng.integers(0, 120))
+            elif u < 0.5:
+                xtra = abi.KSW_XSUBO | abi.KSW_XSTART | abi.KSW_XBYTE | int(rng.integers(0, 120))
+        tasks[k] = (qo, to, ql, tl, xtra, 0)
+        qs.append(q)
+        ts.append(t)
+        qo += ql
+        to += tl
+    cat = lambda v: np.concatenate(v).astype(np.uint8) if v else np.zeros(0, np.uint8)  # noqa: E731
+    return tasks, cat(qs), cat(ts)

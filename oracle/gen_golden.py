@@ -137,7 +137,49 @@ def edge_tasks(rng, n, allow_t5):
     return tasks, np.concatenate(qs).astype(np.uint8), np.concatenate(ts).astype(np.uint8)
 
 
+ALIGN2_OPTS = {
+    "default": None,  # abi.default_opt()
+    "scoring": dict(a=2, b=5, o_del=7, e_del=2, o_ins=5, e_ins=3, pen_clip5=3, pen_clip3=9, w=30, zdrop=40),
+    # cheap gaps: an insertion next to a deletion beats a mismatch, so the
+    # striped first pass (E from segment-local F) and the lazy-F early exit
+    # of ksw_u8/ksw_i16 (o_ins == 0: equality case) decide the results
+    "cheapgap": dict(a=5, b=12, o_del=1, e_del=1, o_ins=0, e_ins=1, pen_clip5=0, pen_clip3=0, w=50, zdrop=60),
+    "cheapdel": dict(a=2, b=9, o_del=0, e_del=2, o_ins=1, e_ins=1, pen_clip5=0, pen_clip3=0, w=50, zdrop=60),
+}
+A2_SHORT = (1, 2, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129, 150, 200, 249, 250, 251, 255, 256, 300)
+
+
+def gen_align2(rng):
+    """ksw_align2 (mate rescue, bwamem_pair.c:150) through the reference's own code"""
+    from bwagpu import synth
+    for name, o in ALIGN2_OPTS.items():
+        opt = abi.default_opt() if o is None else dict(o, mat=abi.fill_scmat(o["a"], o["b"]))
+        parts = [synth.mate_rescue_tasks(rng, 250, a=opt["a"], qlens=(100, 150, 250), xtra_mode="matesw"),
+                 synth.mate_rescue_tasks(rng, 250, a=opt["a"], qlens=A2_SHORT, win=(0, 400), xtra_mode="mix"),
+                 synth.mate_rescue_tasks(rng, 40, a=opt["a"], qlens=(400, 700, 1023), win=(0, 900),
+                                         xtra_mode="mix")]
+        ts, qs, tps, qo, to = [], [], [], 0, 0
+        for t, q, tp in parts:
+            t = t.copy()
+            t["qoff"] += qo
+            t["toff"] += to
+            ts.append(t); qs.append(q); tps.append(tp)
+            qo += len(q); to += len(tp)
+        tasks, qp, tp = np.concatenate(ts), np.concatenate(qs), np.concatenate(tps)
+        res, _ = oracle.align2("ref", opt, tasks, qp, tp)
+        np.savez_compressed(os.path.join(GOLD, "align2_" + name + ".npz"),
+                            opt_int=np.array([opt[k] for k in ("a", "b", "o_del", "e_del", "o_ins", "e_ins",
+                                                               "pen_clip5", "pen_clip3", "w", "zdrop")], np.int32),
+                            opt_mat=np.asarray(opt["mat"], np.int8), tasks=tasks, task_res=res, qpool=qp, tpool=tp)
+        print(f"[gen_golden] align2_{name}: tasks={len(tasks)} q={len(qp)} t={len(tp)} "
+              f"tb>=0:{int((res['tb'] >= 0).sum())} score2>=0:{int((res['score2'] >= 0).sum())} "
+              f"sat255:{int((res['score'] == 255).sum())}")
+
+
 def main():
+    if "--only-align2" in sys.argv:
+        gen_align2(np.random.default_rng(2025))
+        return
     if oracle.ref_lib() is None or not os.path.exists(os.path.join(HERE, "_ref", "gen_golden")):
         sys.exit("build the reference first: make -C oracle")
     os.makedirs(GOLD, exist_ok=True)
@@ -164,6 +206,7 @@ def main():
                                                                "pen_clip5", "pen_clip3", "w", "zdrop")], np.int32),
                             opt_mat=np.asarray(opt["mat"], np.int8), tasks=tasks, task_res=res, qpool=qp, tpool=tp)
         print(f"[gen_golden] {name}: tasks={len(tasks)} q={len(qp)} t={len(tp)}")
+    gen_align2(np.random.default_rng(2025))
 
 
 if __name__ == "__main__":

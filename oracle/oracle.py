@@ -43,6 +43,8 @@ def oracle_lib():
     lib.oracle_chain2aln_batch.restype = C.c_int
     lib.oracle_extend_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
     lib.oracle_extend_batch.restype = C.c_int
+    lib.oracle_align2_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
+    lib.oracle_align2_batch.restype = C.c_int
     return lib
 
 
@@ -57,6 +59,9 @@ def ref_lib():
     lib.ref_extend_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP]
     lib.ref_extend_batch.restype = C.c_int
     lib.ref_abi_check.restype = C.c_int
+    if hasattr(lib, "ref_align2_batch"):
+        lib.ref_align2_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP]
+        lib.ref_align2_batch.restype = C.c_int
     return lib
 
 
@@ -110,4 +115,23 @@ def extend(which: str, opt: dict, tasks, qpool, tpool):
     if lib is None:
         raise RuntimeError("oracle/_ref/libbwaref.so not available")
     lib.ref_extend_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool), _ptr(res))
+    return res[:len(tasks)], None
+
+
+def align2(which: str, opt: dict, tasks, qpool, tpool):
+    """ksw_align2 over a task batch -> (kswr records, cells[cells, rows] or None)"""
+    o = abi.opt_from_dict(opt)
+    tasks = np.ascontiguousarray(tasks, abi.ALIGN2_TASK_DTYPE)
+    qpool = np.ascontiguousarray(qpool, np.uint8)
+    tpool = np.ascontiguousarray(tpool, np.uint8)
+    res = np.zeros(max(len(tasks), 1), abi.KSWR_DTYPE)
+    if which == "oracle":
+        cells = np.zeros(2, np.int64)
+        oracle_lib().oracle_align2_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool),
+                                         _ptr(res), _ptr(cells))
+        return res[:len(tasks)], cells
+    lib = ref_lib()
+    if lib is None or not hasattr(lib, "ref_align2_batch"):
+        raise RuntimeError("oracle/_ref/libbwaref.so (with ref_align2_batch) not available")
+    lib.ref_align2_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool), _ptr(res))
     return res[:len(tasks)], None

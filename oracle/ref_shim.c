@@ -140,3 +140,24 @@ int ref_extend_batch(const bwagpu_opt_t *o, int32_t n_tasks, const bwagpu_ext_ta
   }
   return 0;
 }
+
+/* mate-rescue local SW: the reference ksw_align2 per task (m = 5, opt->mat,
+   qry = 0 as mem_matesw passes, bwamem_pair.c:151).  ksw_align2 reverses the
+   query/target prefixes in place for XSTART, so work on copies. */
+int ref_align2_batch(const bwagpu_opt_t *o, int32_t n_tasks, const bwagpu_align2_task_t *tasks,
+                     const uint8_t *qpool, const uint8_t *tpool, bwagpu_kswr_t *results)
+{
+  for (int32_t k = 0; k < n_tasks; ++k) {
+    const bwagpu_align2_task_t *t = &tasks[k];
+    uint8_t *q = (uint8_t *)malloc((size_t)t->qlen + 1), *r = (uint8_t *)malloc((size_t)t->tlen + 1);
+    kswr_t a;
+    memcpy(q, qpool + t->qoff, (size_t)t->qlen);
+    memcpy(r, tpool + t->toff, (size_t)t->tlen);
+    a = ksw_align2(t->qlen, q, t->tlen, r, 5, o->mat, o->o_del, o->e_del, o->o_ins, o->e_ins, t->xtra, 0);
+    results[k].score = a.score; results[k].te = a.te; results[k].qe = a.qe;
+    results[k].score2 = a.score2; results[k].te2 = a.te2; results[k].tb = a.tb; results[k].qb = a.qb;
+    free(q);
+    free(r);
+  }
+  return 0;
+}

@@ -12,6 +12,7 @@ from bwagpu.engine import Batch
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CHAIN_SETS = ["c1_default", "c5_mixed", "opt1_scoring", "opt2_band"]
 KSW_SETS = ["ksw_edge_default", "ksw_edge_scoring", "ksw_edge_matrix"]
+ALIGN2_SETS = ["align2_default", "align2_scoring", "align2_cheapgap", "align2_cheapdel"]
 OPT_KEYS = ("a", "b", "o_del", "e_del", "o_ins", "e_ins", "pen_clip5", "pen_clip3", "w", "zdrop")
 
 
@@ -43,6 +44,22 @@ def load_tasks(name):
     z = _npz(name)
     return opt_of(z), z["tasks"].astype(abi.EXT_TASK_DTYPE), z["task_res"].astype(abi.EXT_RES_DTYPE), \
         z["qpool"], z["tpool"]
+
+
+def load_align2(name):
+    """ksw_align2 set -> opt, tasks, expected kswr_t records, qpool, tpool"""
+    z = _npz(name)
+    return opt_of(z), z["tasks"].astype(abi.ALIGN2_TASK_DTYPE), z["task_res"].astype(abi.KSWR_DTYPE), \
+        z["qpool"], z["tpool"]
+
+
+def kswr_mismatch(tasks, got, want) -> str | None:
+    g, w = got.view(np.int32).reshape(-1, 7), want.view(np.int32).reshape(-1, 7)
+    bad = np.nonzero((g != w).any(axis=1))[0]
+    if len(bad) == 0:
+        return None
+    i = int(bad[0])
+    return f"{len(bad)}/{len(tasks)} tasks differ; first #{i} {tasks[i]}: got {got[i]} want {want[i]}"
 
 
 def region_mismatch(got: np.ndarray, want: np.ndarray) -> str | None:

@@ -3,7 +3,8 @@
 The fixtures were produced by the reference's own C compiled from
 /root/reference/bwa (oracle/gen_golden.py): chains from its seeding, regions
 from its mem_chain2aln (bwa/bwamem.c:641-795), ksw_extend2 (bwa/ksw.c:380-479)
-outputs for recorded and randomised edge-case calls."""
+outputs for recorded and randomised edge-case calls, ksw_align2
+(bwa/ksw.c:337-357) outputs for mate-rescue-shaped and edge-case calls."""
 import numpy as np
 import pytest
 
@@ -35,6 +36,37 @@ def test_oracle_ksw_extend2_matches_reference(name):
     got, cells = oracle.extend("oracle", opt, tasks, qp, tp)
     bad = np.nonzero(got.view(np.int32).reshape(-1, 6) != want.view(np.int32).reshape(-1, 6))[0]
     assert len(bad) == 0, f"{len(set(bad))} tasks differ, first {tasks[bad[0]]}: {got[bad[0]]} vs {want[bad[0]]}"
+
+
+@pytest.mark.parametrize("name", G.ALIGN2_SETS)
+def test_oracle_ksw_align2_matches_reference(name):
+    opt, tasks, want, qp, tp = G.load_align2(name)
+    got, cells = oracle.align2("oracle", opt, tasks, qp, tp)
+    assert G.kswr_mismatch(tasks, got, want) is None
+    assert cells[0] > 0
+
+
+def test_align2_fixture_coverage():
+    """the ksw_align2 sets reach u8 and i16, the 255 saturation, XSTOP, the
+    2nd-best score, the start pass, scores below minsc and o_ins == 0"""
+    seen = dict(u8=0, i16=0, sat255=0, xstop=0, score2=0, start=0, below_minsc=0, o_ins0=0, qlen_gt_256=0,
+                tlen_le_qlen=0)
+    for name in G.ALIGN2_SETS:
+        opt, t, r, _, _ = G.load_align2(name)
+        u8 = (t["xtra"] & abi.KSW_XBYTE) != 0
+        seen["u8"] += int(u8.sum())
+        seen["i16"] += int((~u8).sum())
+        seen["sat255"] += int((u8 & (r["score"] == 255)).sum())
+        seen["xstop"] += int(((t["xtra"] & abi.KSW_XSTOP) != 0).sum())
+        seen["score2"] += int((r["score2"] >= 0).sum())
+        seen["start"] += int((r["tb"] >= 0).sum())
+        sub = (t["xtra"] & abi.KSW_XSUBO) != 0
+        seen["below_minsc"] += int((sub & (r["score"] < (t["xtra"] & 0xffff))).sum())
+        seen["o_ins0"] += len(t) if opt["o_ins"] == 0 else 0
+        seen["qlen_gt_256"] += int((t["qlen"] > 256).sum())
+        seen["tlen_le_qlen"] += int((t["tlen"] <= t["qlen"]).sum())
+    for k, v in seen.items():
+        assert v > 0, f"ksw_align2 golden vectors never exercise {k}"
 
 
 def test_fixture_coverage():
@@ -75,3 +107,19 @@ def test_oracle_vs_reference_fresh_random_tasks():
         a, _ = oracle.extend("oracle", opt, tasks, qp, tp)
         b, _ = oracle.extend("ref", opt, tasks, qp, tp)
         assert np.array_equal(a.view(np.int32), b.view(np.int32))
+
+
+def test_oracle_align2_vs_reference_fresh_random_tasks():
+    """fresh random ksw_align2 calls, oracle vs the compiled reference"""
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    import gen_golden
+    from bwagpu import synth
+    rng = np.random.default_rng(123)
+    for o in gen_golden.ALIGN2_OPTS.values():
+        opt = abi.default_opt() if o is None else dict(o, mat=abi.fill_scmat(o["a"], o["b"]))
+        tasks, qp, tp = synth.mate_rescue_tasks(rng, 150, a=opt["a"], qlens=gen_golden.A2_SHORT, win=(0, 300),
+                                                xtra_mode="mix")
+        a, _ = oracle.align2("oracle", opt, tasks, qp, tp)
+        b, _ = oracle.align2("ref", opt, tasks, qp, tp)
+        assert G.kswr_mismatch(tasks, a, b) is None
