@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "align2.h"
 #include "engine.h"
 
 using namespace bwagpu;
@@ -112,6 +113,8 @@ struct bwagpu_ctx {
   int32_t* d_ann_len = nullptr;
   int watchdog_ms = 10000;
   Slot slot[BWAGPU_NUM_SLOTS];
+  // ksw_align2 batches (bwagpu_align2_*): grow-only, reused across calls
+  DevBuf a2_tasks, a2_q, a2_t, a2_out, a2_scratch, a2_lists, a2_counts, a2_boff;
   std::string err;
 };
 
@@ -161,6 +164,41 @@ bool make_opt(const bwagpu_opt_t* o, DevOpt* d, std::string* why) {
     d->qprof4[q] = o->mat[20 + q];
   }
   return true;
+}
+
+// ksw_qinit's profile (ksw.c:69-108) as v_perm byte pools, see A2Prof
+A2Prof make_a2prof(const DevOpt& o, bool u8) {
+  A2Prof P{};
+  int mn = 127, mx = 0;
+  for (int i = 0; i < 25; ++i) {
+    mn = std::min<int>(mn, o.mat[i]);
+    mx = std::max<int>(mx, o.mat[i]);
+  }
+  const int shift = (256 - (mn & 0xff)) & 0xff;
+  const int bias = u8 ? shift : 128;
+  for (int t = 0; t < 5; ++t) {
+    uint32_t lo = 0;
+    for (int q = 0; q < 4; ++q) lo |= (uint32_t)(uint8_t)(o.mat[t * 5 + q] + bias) << (8 * q);
+    P.lo[t] = lo;
+    P.hi[t] = (uint32_t)(uint8_t)(o.mat[t * 5 + 4] + bias) | (uint32_t)(uint8_t)bias << 8;
+  }
+  P.shift = shift;
+  P.qmax = mx;
+  P.e_del = o.e_del;
+  P.oe_del = o.oe_del;
+  P.e_ins = o.e_ins;
+  P.oe_ins = o.oe_ins;
+  return P;
+}
+
+// scoring limits of the align2 kernels (reasons are the E_UNSUPPORTED text)
+const char* align2_opt_unsupported(const DevOpt& o) {
+  if (o.o_ins <= 0)
+    return "ksw_align2 with o_ins == 0: the reference's lazy-F early exit (ksw.c:180) then depends on "
+           "its SIMD lane order; run it on the CPU";
+  if (o.max_mat <= 0) return "ksw_align2 needs a positive match score (ksw.c:216 divides by it)";
+  if (o.o_ins > 65535 || o.e_ins > 65535 || o.o_del > 65535 || o.e_del > 65535) return "gap penalty > 65535";
+  return nullptr;
 }
 
 int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, bwagpu_ctx_t** out,
@@ -215,6 +253,8 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     if (s.ev3) (void)hipEventDestroy(s.ev3);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+  ctx->a2_tasks.release(); ctx->a2_q.release(); ctx->a2_t.release(); ctx->a2_out.release();
+  ctx->a2_scratch.release(); ctx->a2_lists.release(); ctx->a2_counts.release(); ctx->a2_boff.release();
   if (ctx->own_pac && ctx->d_pac) (void)hipFree(ctx->d_pac);
   if (ctx->d_ann_off) (void)hipFree(ctx->d_ann_off);
   if (ctx->d_ann_len) (void)hipFree(ctx->d_ann_len);
@@ -631,6 +671,120 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   s.last.rows = hs[ST_ROWS];
   s.last.ext_calls = hs[ST_CALLS];
   cleanup();
+  return BWAGPU_OK;
+}
+
+int bwagpu_align2_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_t* tasks, const uint8_t* qpool,
+                        int64_t qpool_len, const uint8_t* tpool, int64_t tpool_len, bwagpu_kswr_t* results) {
+  if (!ctx || n < 0 || (n && (!tasks || !results)) || qpool_len < 0 || tpool_len < 0 ||
+      (qpool_len && !qpool) || (tpool_len && !tpool))
+    return BWAGPU_E_INVAL;
+  if (n == 0) return BWAGPU_OK;
+  if (const char* why = align2_opt_unsupported(ctx->opt)) return fail(ctx, BWAGPU_E_UNSUPPORTED, why);
+  // validate and bin on the host
+  std::vector<int32_t> lists[kA2Bins];
+  std::vector<int64_t> boff((size_t)n);
+  int64_t scratch = 0;
+  for (int32_t k = 0; k < n; ++k) {
+    const bwagpu_align2_task_t& t = tasks[k];
+    if (t.qlen < 0 || t.tlen < 0 || t.qoff < 0 || t.toff < 0 || t.qoff + t.qlen > qpool_len ||
+        t.toff + t.tlen > tpool_len)
+      return fail(ctx, BWAGPU_E_INVAL, "task outside its pools");
+    if (t.qlen > BWAGPU_MAX_READ_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "qlen > BWAGPU_MAX_READ_LEN");
+    const bool u8 = (t.xtra & BWAGPU_KSW_XBYTE) != 0;
+    if (!u8 && (int64_t)t.qlen * ctx->opt.max_mat > 32767)
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, "i16 scores could saturate (qlen * max score > 32767)");
+    lists[a2_bin_of(t.qlen, u8)].push_back(k);
+    boff[(size_t)k] = scratch;
+    scratch += (int64_t)t.tlen + 1;
+  }
+  for (int64_t i = 0; i < qpool_len; ++i)
+    if (qpool[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "query base > 4");
+  for (int64_t i = 0; i < tpool_len; ++i)
+    if (tpool[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "target base > 4");
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  Slot& s = ctx->slot[0];
+  hipStream_t st = s.stream;
+  HIPC(ctx->a2_tasks.ensure(sizeof(bwagpu_align2_task_t) * n), "hipMalloc");
+  HIPC(ctx->a2_q.ensure((size_t)qpool_len + 1), "hipMalloc");
+  HIPC(ctx->a2_t.ensure((size_t)tpool_len + 1), "hipMalloc");
+  HIPC(ctx->a2_out.ensure(sizeof(bwagpu_kswr_t) * n), "hipMalloc");
+  HIPC(ctx->a2_scratch.ensure(sizeof(int2) * (size_t)scratch), "hipMalloc");
+  HIPC(ctx->a2_lists.ensure(sizeof(int32_t) * n), "hipMalloc");
+  HIPC(ctx->a2_counts.ensure(sizeof(int32_t) * kA2Bins + sizeof(int64_t) * ST_N), "hipMalloc");
+  HIPC(ctx->a2_boff.ensure(sizeof(int64_t) * n), "hipMalloc");
+  std::vector<int32_t> all;
+  all.reserve((size_t)n);
+  int32_t counts[kA2Bins];
+  for (int b = 0; b < kA2Bins; ++b) {
+    counts[b] = (int32_t)lists[b].size();
+    all.insert(all.end(), lists[b].begin(), lists[b].end());
+  }
+  int32_t* d_counts = ctx->a2_counts.as<int32_t>();
+  int64_t* d_stats = (int64_t*)(d_counts + kA2Bins);
+  HIPC(hipMemcpyAsync(ctx->a2_tasks.p, tasks, sizeof(bwagpu_align2_task_t) * n, hipMemcpyHostToDevice, st), "H2D");
+  if (qpool_len) HIPC(hipMemcpyAsync(ctx->a2_q.p, qpool, (size_t)qpool_len, hipMemcpyHostToDevice, st), "H2D");
+  if (tpool_len) HIPC(hipMemcpyAsync(ctx->a2_t.p, tpool, (size_t)tpool_len, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemcpyAsync(ctx->a2_lists.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemcpyAsync(d_counts, counts, sizeof(counts), hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemsetAsync(d_stats, 0, sizeof(int64_t) * ST_N, st), "memset");
+  HIPC(hipMemcpyAsync(ctx->a2_boff.p, boff.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st), "H2D");
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // own events: slot 0's may time an in-flight chain2aln batch
+  HIPC(hipEventCreate(&e0), "event");
+  HIPC(hipEventCreate(&e1), "event");
+  HIPC(hipEventRecord(e0, st), "event");
+  int32_t off = 0;
+  for (int b = 0; b < kA2Bins; ++b) {
+    if (counts[b]) {
+      A2Args a{ctx->a2_tasks.as<bwagpu_align2_task_t>(), ctx->a2_q.as<uint8_t>(), ctx->a2_t.as<uint8_t>(),
+               ctx->a2_out.as<bwagpu_kswr_t>(), ctx->a2_scratch.as<int2>(), ctx->a2_boff.as<int64_t>(),
+               ctx->a2_lists.as<int32_t>() + off, d_counts + b, d_stats};
+      HIPC(launch_align2(b, a, make_a2prof(ctx->opt, b >= kA2Buckets), counts[b], st), "align2 launch");
+    }
+    off += counts[b];
+  }
+  HIPC(hipEventRecord(e1, st), "event");
+  int64_t hs[ST_N];
+  HIPC(hipMemcpyAsync(results, ctx->a2_out.p, sizeof(bwagpu_kswr_t) * n, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipMemcpyAsync(hs, d_stats, sizeof(hs), hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "align2 batch");
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  s.last = bwagpu_stats_t{};
+  s.last.kernel_ms = ms;
+  s.last.cells = hs[ST_CELLS];
+  s.last.rows = hs[ST_ROWS];
+  s.last.ext_calls = hs[ST_CALLS];
+  return BWAGPU_OK;
+}
+
+int bwagpu_align2_device(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_t* dev_tasks,
+                         const uint8_t* dev_qpool, const uint8_t* dev_tpool, bwagpu_kswr_t* dev_results,
+                         void* dev_scratch, void* stream) {
+  if (!ctx || n < 0 || (n && (!dev_tasks || !dev_results || !dev_scratch))) return BWAGPU_E_INVAL;
+  if (n == 0) return BWAGPU_OK;
+  if (const char* why = align2_opt_unsupported(ctx->opt)) return fail(ctx, BWAGPU_E_UNSUPPORTED, why);
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  HIPC(ctx->a2_lists.ensure(sizeof(int32_t) * (size_t)kA2Bins * n), "hipMalloc");
+  HIPC(ctx->a2_boff.ensure(sizeof(int64_t) * n), "hipMalloc");
+  // counts[kA2Bins] | pad | cursor (u64) | stats[ST_N]
+  const size_t cbytes = sizeof(int32_t) * kA2Bins + sizeof(int64_t) * (1 + ST_N);
+  HIPC(ctx->a2_counts.ensure(cbytes), "hipMalloc");
+  int32_t* d_counts = ctx->a2_counts.as<int32_t>();
+  unsigned long long* cursor = (unsigned long long*)(d_counts + kA2Bins);
+  int64_t* d_stats = (int64_t*)(cursor + 1);
+  HIPC(hipMemsetAsync(d_counts, 0, cbytes, st), "memset");
+  HIPC(launch_align2_bins(dev_tasks, n, ctx->a2_lists.as<int32_t>(), d_counts, ctx->a2_boff.as<int64_t>(), cursor,
+                          dev_results, d_stats, st),
+       "align2 bin launch");
+  for (int b = 0; b < kA2Bins; ++b) {
+    A2Args a{dev_tasks, dev_qpool, dev_tpool, dev_results, (int2*)dev_scratch, ctx->a2_boff.as<int64_t>(),
+             ctx->a2_lists.as<int32_t>() + (size_t)b * n, d_counts + b, d_stats};
+    HIPC(launch_align2(b, a, make_a2prof(ctx->opt, b >= kA2Buckets), 0, st), "align2 launch");
+  }
   return BWAGPU_OK;
 }
 

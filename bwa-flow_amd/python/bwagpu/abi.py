@@ -36,7 +36,13 @@ EXT_TASK_DTYPE = np.dtype([("qoff", "<i8"), ("toff", "<i8"), ("qlen", "<i4"), ("
                            ("w", "<i4"), ("end_bonus", "<i4"), ("zdrop", "<i4"), ("h0", "<i4")])
 EXT_RES_DTYPE = np.dtype([("score", "<i4"), ("qle", "<i4"), ("tle", "<i4"), ("gtle", "<i4"),
                           ("gscore", "<i4"), ("max_off", "<i4")])
+ALIGN2_TASK_DTYPE = np.dtype([("qoff", "<i8"), ("toff", "<i8"), ("qlen", "<i4"), ("tlen", "<i4"),
+                              ("xtra", "<i4"), ("pad", "<i4")])
+KSWR_DTYPE = np.dtype([("score", "<i4"), ("te", "<i4"), ("qe", "<i4"), ("score2", "<i4"), ("te2", "<i4"),
+                       ("tb", "<i4"), ("qb", "<i4")])
+KSW_XBYTE, KSW_XSTOP, KSW_XSUBO, KSW_XSTART = 0x10000, 0x20000, 0x40000, 0x80000
 assert SEED_DTYPE.itemsize == 24 and ALNREG_DTYPE.itemsize == 88
+assert ALIGN2_TASK_DTYPE.itemsize == 32 and KSWR_DTYPE.itemsize == 28
 assert EXT_TASK_DTYPE.itemsize == 40 and EXT_RES_DTYPE.itemsize == 24
 
 
@@ -81,6 +87,8 @@ PROTOS = {
     "bwagpu_chain2aln": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP]),
     "bwagpu_chain2aln_device": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP, _VP, _VP]),
     "bwagpu_extend_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),
+    "bwagpu_align2_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),
+    "bwagpu_align2_device": (C.c_int, [_VP, C.c_int32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "bwagpu_last_stats": (C.c_int, [_VP, C.c_int, C.POINTER(Stats)]),
     "bwagpu_debug_set_trace": (C.c_int, [_VP, _VP]),
 }

@@ -178,6 +178,22 @@ class Engine:
                                                  _ptr(tpool), len(tpool), _ptr(res)), "extend_batch")
         return res[:len(tasks)]
 
+    def align2_batch(self, tasks: np.ndarray, qpool: np.ndarray, tpool: np.ndarray) -> np.ndarray:
+        """ksw_align2 (bwa/ksw.c:337-357) per task -> kswr_t records (abi.KSWR_DTYPE)"""
+        tasks = np.ascontiguousarray(tasks, abi.ALIGN2_TASK_DTYPE)
+        qpool = np.ascontiguousarray(qpool, np.uint8)
+        tpool = np.ascontiguousarray(tpool, np.uint8)
+        res = np.zeros(max(len(tasks), 1), abi.KSWR_DTYPE)
+        self._check(self.lib.bwagpu_align2_batch(self.ctx, len(tasks), _ptr(tasks), _ptr(qpool), len(qpool),
+                                                 _ptr(tpool), len(tpool), _ptr(res)), "align2_batch")
+        return res[:len(tasks)]
+
+    def align2_device(self, n: int, dev_tasks: int, dev_q: int, dev_t: int, dev_out: int, dev_scratch: int,
+                      stream: int | None = None):
+        """asynchronous launch on device buffers (pointers as ints, e.g. torch data_ptr())"""
+        self._check(self.lib.bwagpu_align2_device(self.ctx, n, dev_tasks, dev_q, dev_t, dev_out, dev_scratch,
+                                                  stream), "align2_device")
+
     def last_stats(self, slot: int = 0) -> dict:
         s = abi.Stats()
         self._check(self.lib.bwagpu_last_stats(self.ctx, slot, C.byref(s)), "last_stats")

@@ -37,6 +37,13 @@
  *       task-level granularity of the FPGA kernel's seed_proc
  *       (src/fpga/kernel/smithwaterman.cpp:318-445) but with ksw_extend2's
  *       exact semantics (z-drop, band trimming, runtime scoring).
+ *   bwagpu_align2_batch
+ *       a batch of independent ksw_align2 calls (bwa/ksw.c:337-357: ksw_u8 /
+ *       ksw_i16 local SW, 2nd-best score, start by the reverse pass) as made
+ *       by mate rescue, mem_matesw (bwa/bwamem_pair.c:150-151), for every
+ *       read pair of a batch (mem_sam_pe, bwamem_pair.c:290-300).  Results
+ *       equal ksw_align2's kswr_t field for field, including the quirks of
+ *       its striped first pass (see oracle/ksw_align.c).
  *   bwagpu_last_error
  *       the what() of fpgaHangError / fpgaResultsError / std::runtime_error
  *       (src/util.h:16-32, OpenCLEnv.h:21-31).
@@ -155,6 +162,26 @@ typedef struct {
   int32_t score, qle, tle, gtle, gscore, max_off;
 } bwagpu_ext_result_t;
 
+/* ksw_align2 xtra flags (bwa/ksw.h:6-9); the low 16 bits carry minsc/endsc */
+#define BWAGPU_KSW_XBYTE 0x10000
+#define BWAGPU_KSW_XSTOP 0x20000
+#define BWAGPU_KSW_XSUBO 0x40000
+#define BWAGPU_KSW_XSTART 0x80000
+
+/* One ksw_align2(qlen, query, tlen, target, 5, opt->mat, opt->o_del, opt->e_del,
+   opt->o_ins, opt->e_ins, xtra, 0) call: query = qpool[qoff..qoff+qlen),
+   target = tpool[toff..toff+tlen).  qlen <= BWAGPU_MAX_READ_LEN. */
+typedef struct {
+  int64_t qoff, toff;
+  int32_t qlen, tlen;
+  int32_t xtra, pad_;
+} bwagpu_align2_task_t;
+
+/* == kswr_t (bwa/ksw.h:17-21); unset fields are -1 */
+typedef struct {
+  int32_t score, te, qe, score2, te2, tb, qb;
+} bwagpu_kswr_t;
+
 /* per-launch statistics of the last finished launch on a slot */
 typedef struct {
   double kernel_ms;      /* HIP-event time of the extension kernel(s)            */
@@ -195,6 +222,16 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t *ctx, const bwagpu_batch_t *dev_batch,
 int bwagpu_extend_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_ext_task_t *tasks,
                         const uint8_t *qpool, int64_t qpool_len, const uint8_t *tpool,
                         int64_t tpool_len, bwagpu_ext_result_t *results);
+
+int bwagpu_align2_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_align2_task_t *tasks,
+                        const uint8_t *qpool, int64_t qpool_len, const uint8_t *tpool, int64_t tpool_len,
+                        bwagpu_kswr_t *results);
+/* the same with tasks/pools/results in device memory; asynchronous on stream
+   (hipStream_t, NULL = slot-0 stream).  dev_scratch: 8 x (sum of tlen + n_tasks)
+   bytes of device memory for the row-maxima lists (ksw.c:191-198) */
+int bwagpu_align2_device(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_align2_task_t *dev_tasks,
+                         const uint8_t *dev_qpool, const uint8_t *dev_tpool, bwagpu_kswr_t *dev_results,
+                         void *dev_scratch, void *stream);
 
 int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
 
