@@ -44,6 +44,7 @@ struct A2Args {
   const int64_t* boff;  // [n_tasks]
   const int32_t* list;  // task ids of this bin
   const int32_t* count; // device count of this bin
+  int32_t* cursor;      // next unclaimed list index of this bin (zeroed before the launch)
   int64_t* stats;       // ST_* words, may be NULL
 };
 

@@ -221,12 +221,16 @@ __device__ __forceinline__ PassOut a2_pass(const A2Prof& P, const uint8_t* __res
 
 template <int CD, bool U8>
 __global__ __launch_bounds__(256) void align2_kernel(A2Args a, A2Prof P) {
-  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  // tasks are claimed one at a time from the bin's cursor (the host orders
+  // each list longest first): no static deal, no tail of unequal rounds
   const int n = __builtin_amdgcn_readfirstlane(*a.count);
   long long rows = 0, cells = 0;
   int calls = 0;
-  for (int k = wave; k < n; k += nw) {
+  for (;;) {
+    int k = 0;
+    if ((threadIdx.x & 63) == 0) k = atomicAdd(a.cursor, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= n) break;
     const int id = __builtin_amdgcn_readfirstlane(a.list[k]);
     const bwagpu_align2_task_t tk = a.tasks[id];
     const int64_t qoff = tk.qoff, toff = tk.toff;

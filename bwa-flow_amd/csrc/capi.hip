@@ -115,6 +115,10 @@ struct bwagpu_ctx {
   Slot slot[BWAGPU_NUM_SLOTS];
   // ksw_align2 batches (bwagpu_align2_*): grow-only, reused across calls
   DevBuf a2_tasks, a2_q, a2_t, a2_out, a2_scratch, a2_lists, a2_counts, a2_boff;
+  // bins run concurrently on these (fork/join with events from the caller's stream)
+  static constexpr int kA2Streams = 4;
+  hipStream_t a2_st[kA2Streams] = {};
+  hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
   std::string err;
 };
 
@@ -201,6 +205,13 @@ const char* align2_opt_unsupported(const DevOpt& o) {
   return nullptr;
 }
 
+// Launch the given bins concurrently: fork the align2 streams off `st`,
+// deal the bins (in the given order) round-robin over them, join back.
+// counts_host: task count per bin when known (0 = unknown -> grid = capacity).
+int launch_align2_concurrent(bwagpu_ctx_t* ctx, hipStream_t st, const std::vector<int>& bins, const A2Args& base,
+                             const int32_t* list_off, const int32_t* counts_host, int32_t* d_counts,
+                             int32_t* d_cursors, size_t list_stride);
+
 int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, bwagpu_ctx_t** out,
                   bwagpu_ctx_t** made) {
   if (!out || !bns || bns->l_pac <= 0 || bns->n_seqs <= 0 || !bns->ann_offset || !bns->ann_len)
@@ -253,6 +264,12 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     if (s.ev3) (void)hipEventDestroy(s.ev3);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+  for (int i = 0; i < bwagpu_ctx::kA2Streams; ++i) {
+    if (ctx->a2_st[i]) (void)hipStreamSynchronize(ctx->a2_st[i]);
+    if (ctx->a2_st[i]) (void)hipStreamDestroy(ctx->a2_st[i]);
+    if (ctx->a2_join[i]) (void)hipEventDestroy(ctx->a2_join[i]);
+  }
+  if (ctx->a2_fork) (void)hipEventDestroy(ctx->a2_fork);
   ctx->a2_tasks.release(); ctx->a2_q.release(); ctx->a2_t.release(); ctx->a2_out.release();
   ctx->a2_scratch.release(); ctx->a2_lists.release(); ctx->a2_counts.release(); ctx->a2_boff.release();
   if (ctx->own_pac && ctx->d_pac) (void)hipFree(ctx->d_pac);
@@ -674,6 +691,41 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   return BWAGPU_OK;
 }
 
+}  // extern "C"
+
+namespace {
+int launch_align2_concurrent(bwagpu_ctx_t* ctx, hipStream_t st, const std::vector<int>& bins, const A2Args& base,
+                             const int32_t* list_off, const int32_t* counts_host, int32_t* d_counts,
+                             int32_t* d_cursors, size_t list_stride) {
+  constexpr int NS = bwagpu_ctx::kA2Streams;
+  for (int i = 0; i < NS; ++i) {
+    if (!ctx->a2_st[i]) HIPC(hipStreamCreateWithFlags(&ctx->a2_st[i], hipStreamNonBlocking), "stream");
+    if (!ctx->a2_join[i]) HIPC(hipEventCreateWithFlags(&ctx->a2_join[i], hipEventDisableTiming), "event");
+  }
+  if (!ctx->a2_fork) HIPC(hipEventCreateWithFlags(&ctx->a2_fork, hipEventDisableTiming), "event");
+  const int used = std::min<int>(NS, (int)bins.size());
+  HIPC(hipEventRecord(ctx->a2_fork, st), "event");
+  for (int i = 0; i < used; ++i) HIPC(hipStreamWaitEvent(ctx->a2_st[i], ctx->a2_fork, 0), "stream wait");
+  for (size_t k = 0; k < bins.size(); ++k) {
+    const int b = bins[k];
+    A2Args a = base;
+    a.list = base.list + (list_off ? list_off[b] : (size_t)b * list_stride);
+    a.count = d_counts + b;
+    a.cursor = d_cursors + b;
+    HIPC(launch_align2(b, a, make_a2prof(ctx->opt, b >= kA2Buckets), counts_host ? counts_host[b] : 0,
+                       ctx->a2_st[k % used]),
+         "align2 launch");
+  }
+  for (int i = 0; i < used; ++i) {
+    HIPC(hipEventRecord(ctx->a2_join[i], ctx->a2_st[i]), "event");
+    HIPC(hipStreamWaitEvent(st, ctx->a2_join[i], 0), "stream wait");
+  }
+  return BWAGPU_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int bwagpu_align2_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_t* tasks, const uint8_t* qpool,
                         int64_t qpool_len, const uint8_t* tpool, int64_t tpool_len, bwagpu_kswr_t* results) {
   if (!ctx || n < 0 || (n && (!tasks || !results)) || qpool_len < 0 || tpool_len < 0 ||
@@ -711,37 +763,48 @@ int bwagpu_align2_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_t
   HIPC(ctx->a2_out.ensure(sizeof(bwagpu_kswr_t) * n), "hipMalloc");
   HIPC(ctx->a2_scratch.ensure(sizeof(int2) * (size_t)scratch), "hipMalloc");
   HIPC(ctx->a2_lists.ensure(sizeof(int32_t) * n), "hipMalloc");
-  HIPC(ctx->a2_counts.ensure(sizeof(int32_t) * kA2Bins + sizeof(int64_t) * ST_N), "hipMalloc");
+  // counts[kA2Bins] | cursors[kA2Bins] | stats[ST_N]
+  HIPC(ctx->a2_counts.ensure(sizeof(int32_t) * 2 * kA2Bins + sizeof(int64_t) * ST_N), "hipMalloc");
   HIPC(ctx->a2_boff.ensure(sizeof(int64_t) * n), "hipMalloc");
   std::vector<int32_t> all;
   all.reserve((size_t)n);
-  int32_t counts[kA2Bins];
+  int32_t counts[2 * kA2Bins] = {}, list_off[kA2Bins];
+  std::vector<std::pair<int64_t, int>> order;  // bins by total rows, largest first
   for (int b = 0; b < kA2Bins; ++b) {
+    // longest target first inside a bin (rows ~ tlen): the last claims are the short tasks
+    std::stable_sort(lists[b].begin(), lists[b].end(),
+                     [&](int32_t x, int32_t y) { return tasks[x].tlen > tasks[y].tlen; });
     counts[b] = (int32_t)lists[b].size();
+    list_off[b] = (int32_t)all.size();
     all.insert(all.end(), lists[b].begin(), lists[b].end());
+    int64_t rows = 0;
+    for (int32_t k : lists[b]) rows += tasks[k].tlen;
+    if (counts[b]) order.push_back({rows * kA2CD[b % kA2Buckets], b});
   }
+  std::sort(order.begin(), order.end(), [](const std::pair<int64_t, int>& x, const std::pair<int64_t, int>& y) {
+    return x.first > y.first;
+  });
+  std::vector<int> bins;
+  for (auto& o : order) bins.push_back(o.second);
   int32_t* d_counts = ctx->a2_counts.as<int32_t>();
-  int64_t* d_stats = (int64_t*)(d_counts + kA2Bins);
+  int64_t* d_stats = (int64_t*)(d_counts + 2 * kA2Bins);
   HIPC(hipMemcpyAsync(ctx->a2_tasks.p, tasks, sizeof(bwagpu_align2_task_t) * n, hipMemcpyHostToDevice, st), "H2D");
   if (qpool_len) HIPC(hipMemcpyAsync(ctx->a2_q.p, qpool, (size_t)qpool_len, hipMemcpyHostToDevice, st), "H2D");
   if (tpool_len) HIPC(hipMemcpyAsync(ctx->a2_t.p, tpool, (size_t)tpool_len, hipMemcpyHostToDevice, st), "H2D");
   HIPC(hipMemcpyAsync(ctx->a2_lists.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D");
-  HIPC(hipMemcpyAsync(d_counts, counts, sizeof(counts), hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemcpyAsync(d_counts, counts, sizeof(counts), hipMemcpyHostToDevice, st), "H2D");  // + zero cursors
   HIPC(hipMemsetAsync(d_stats, 0, sizeof(int64_t) * ST_N, st), "memset");
   HIPC(hipMemcpyAsync(ctx->a2_boff.p, boff.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st), "H2D");
   hipEvent_t e0 = nullptr, e1 = nullptr;  // own events: slot 0's may time an in-flight chain2aln batch
   HIPC(hipEventCreate(&e0), "event");
   HIPC(hipEventCreate(&e1), "event");
   HIPC(hipEventRecord(e0, st), "event");
-  int32_t off = 0;
-  for (int b = 0; b < kA2Bins; ++b) {
-    if (counts[b]) {
-      A2Args a{ctx->a2_tasks.as<bwagpu_align2_task_t>(), ctx->a2_q.as<uint8_t>(), ctx->a2_t.as<uint8_t>(),
-               ctx->a2_out.as<bwagpu_kswr_t>(), ctx->a2_scratch.as<int2>(), ctx->a2_boff.as<int64_t>(),
-               ctx->a2_lists.as<int32_t>() + off, d_counts + b, d_stats};
-      HIPC(launch_align2(b, a, make_a2prof(ctx->opt, b >= kA2Buckets), counts[b], st), "align2 launch");
-    }
-    off += counts[b];
+  {
+    A2Args base{ctx->a2_tasks.as<bwagpu_align2_task_t>(), ctx->a2_q.as<uint8_t>(), ctx->a2_t.as<uint8_t>(),
+                ctx->a2_out.as<bwagpu_kswr_t>(), ctx->a2_scratch.as<int2>(), ctx->a2_boff.as<int64_t>(),
+                ctx->a2_lists.as<int32_t>(), nullptr, nullptr, d_stats};
+    const int rc = launch_align2_concurrent(ctx, st, bins, base, list_off, counts, d_counts, d_counts + kA2Bins, 0);
+    if (rc) return rc;
   }
   HIPC(hipEventRecord(e1, st), "event");
   int64_t hs[ST_N];
@@ -770,22 +833,23 @@ int bwagpu_align2_device(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_
   hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
   HIPC(ctx->a2_lists.ensure(sizeof(int32_t) * (size_t)kA2Bins * n), "hipMalloc");
   HIPC(ctx->a2_boff.ensure(sizeof(int64_t) * n), "hipMalloc");
-  // counts[kA2Bins] | pad | cursor (u64) | stats[ST_N]
-  const size_t cbytes = sizeof(int32_t) * kA2Bins + sizeof(int64_t) * (1 + ST_N);
+  // counts[kA2Bins] | cursors[kA2Bins] | scratch cursor (u64) | stats[ST_N]
+  const size_t cbytes = sizeof(int32_t) * 2 * kA2Bins + sizeof(int64_t) * (1 + ST_N);
   HIPC(ctx->a2_counts.ensure(cbytes), "hipMalloc");
   int32_t* d_counts = ctx->a2_counts.as<int32_t>();
-  unsigned long long* cursor = (unsigned long long*)(d_counts + kA2Bins);
+  unsigned long long* cursor = (unsigned long long*)(d_counts + 2 * kA2Bins);
   int64_t* d_stats = (int64_t*)(cursor + 1);
   HIPC(hipMemsetAsync(d_counts, 0, cbytes, st), "memset");
   HIPC(launch_align2_bins(dev_tasks, n, ctx->a2_lists.as<int32_t>(), d_counts, ctx->a2_boff.as<int64_t>(), cursor,
                           dev_results, d_stats, st),
        "align2 bin launch");
-  for (int b = 0; b < kA2Bins; ++b) {
-    A2Args a{dev_tasks, dev_qpool, dev_tpool, dev_results, (int2*)dev_scratch, ctx->a2_boff.as<int64_t>(),
-             ctx->a2_lists.as<int32_t>() + (size_t)b * n, d_counts + b, d_stats};
-    HIPC(launch_align2(b, a, make_a2prof(ctx->opt, b >= kA2Buckets), 0, st), "align2 launch");
-  }
-  return BWAGPU_OK;
+  // counts are on the device only: every bin's kernel is launched with a
+  // resident-capacity grid; an empty bin's waves exit on their first claim
+  std::vector<int> bins;
+  for (int b : {2, 3, 10, 11, 1, 9, 0, 8, 4, 12, 5, 13, 6, 14, 7, 15}) bins.push_back(b);
+  A2Args base{dev_tasks, dev_qpool, dev_tpool, dev_results, (int2*)dev_scratch, ctx->a2_boff.as<int64_t>(),
+              ctx->a2_lists.as<int32_t>(), nullptr, nullptr, d_stats};
+  return launch_align2_concurrent(ctx, st, bins, base, nullptr, nullptr, d_counts, d_counts + kA2Bins, (size_t)n);
 }
 
 int bwagpu_debug_set_trace(bwagpu_ctx_t* ctx, void* dev_ptr) {
