@@ -5,9 +5,8 @@
 // (234-328), called by mem_matesw (bwa/bwamem_pair.c:150-151) once per
 // (read, orientation) whose mate was not found in a consistent pair.
 //
-// One task per wave.  Columns are strided over the wave like the extension
-// kernel (lane r holds query columns 64c + r, c < CD); the target is walked
-// row by row.  The reference's results depend on its striped SIMD layout
+// One task per wave.  Columns are blocked over the wave (lane r holds query
+// columns r*CD .. r*CD+CD-1); the target is walked row by row.  The reference's results depend on its striped SIMD layout
 // (p = 16 lanes in u8, 8 in i16; lane k covers the column SEGMENT
 // [k*slen, (k+1)*slen), slen = ceil(qlen/p), columns qlen..p*slen-1 are
 // padding scoring 0), so the kernel computes exactly what that layout does:
@@ -30,13 +29,15 @@
 // The start (XSTART) is the reference's reverse pass: the same kernel body
 // run again with reversed index maps, no copies.
 //
-// Integer VALU work throughout (no MFMA); per row and column ~32 VALU.
+// Integer VALU work throughout (no MFMA); per row ~17 VALU per column register
+// plus ~25 for the row (three 64-lane scans, shifts, profile words).
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
 #include <algorithm>
 
 #include "align2.h"
+#include "scan_asm.h"
 #include "wave_ops.h"
 
 namespace bwagpu {
@@ -57,18 +58,33 @@ __device__ __forceinline__ int wave_min(int v) {
   v = min_bc31(min_bc15(min_ror1(min_ror2(min_ror4(min_ror8(v))))));
   return __builtin_amdgcn_readlane(v, 63);
 }
-// inclusive max-scan over the 64 lanes
-__device__ __forceinline__ int wave_scan_max(int v) {
-  return max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(v))))));
-}
 
 struct PassOut {
   int score, te, qe, score2, te2;
 };
 
+__device__ __forceinline__ int med3_i32(int a, int hi) {  // clamp(a, 0, hi), hi >= 0
+  int d;
+  asm("v_med3_i32 %0, %1, 0, %2" : "=v"(d) : "v"(a), "v"(hi));
+  return d;
+}
+
 // One striped pass (ksw_u8 when U8, ksw_i16 otherwise) over target rows
 // [0, tlen).  Query column j is q[j] (qrev < 0) or q[qrev - j]; target row i
 // is t[i], or t[trev - i] for i <= trev (the XSTART reverse pass, ksw.c:345-348).
+//
+// Columns are BLOCKED over the wave: lane r holds j = r*CD + c, c < CD.  Per
+// row and column:
+//   M = H(i-1, j-1) + S        (u8: clamp to [0, 255-shift] = adds/subs_epu8)
+//   T = max(M, E)              X = T + j*e_ins        W = X + BIG*seg(j)
+//   exclusive prefix maxima of X and W = in-lane running max + one 64-lane
+//   scan of the lane totals (the row maximum rides along: rowmax_j h(j) =
+//   rowmax_j T(j), since Fseg(j) < max_{j'<j} T(j') when o_ins > 0)
+//   h = max(T, Fseg), Fseg = Wprefix - BIG*seg - oe_ins - (j-1)*e_ins, >= 0
+//   E' = max(E - e_del, h - oe_del, 0)     H = max(h, Ffull), Ffull likewise from X
+// H(i-1, j-1) is the lane's own previous register, or for c = 0 lane r-1's
+// last one: one DPP shift per row.  Columns past p*slen are pinned to 0 by
+// their constants (M <= 0, both F offsets "infinite"): nothing is masked.
 template <int CD, bool U8>
 __device__ __forceinline__ PassOut a2_pass(const A2Prof& P, const uint8_t* __restrict__ q, int qlen, int qrev,
                                            const uint8_t* __restrict__ t, int tlen, int trev, int minsc,
@@ -77,25 +93,26 @@ __device__ __forceinline__ PassOut a2_pass(const A2Prof& P, const uint8_t* __res
   const int r = (int)(threadIdx.x & 63);
   constexpr int p = U8 ? 16 : 8;
   constexpr int BIG = 1 << 26;  // > any T + j*e_ins (host checks), 16*BIG < 2^31
+  constexpr int KINF = 0x7fffffff;
   const int slen = (qlen + p - 1) / p, ncol = slen * p;
   const int e_del = P.e_del, oe_del = P.oe_del, e_ins = P.e_ins, oe_ins = P.oe_ins;
   const int shift = P.shift;
   uint32_t sel[CD];
-  int Wk[CD], Xk[CD], Ks[CD], Kf[CD];
+  int Xk[CD], Wk[CD], Ks[CD], Kf[CD], Mk[CD];
   int H[CD], E[CD], Hm[CD];
-  bool valid[CD];
 #pragma unroll
   for (int c = 0; c < CD; ++c) {
-    const int j = 64 * c + r;
-    // v_perm selector: profile byte 0..4 = query base, 5 = padding, 12 = constant 0
-    const int code = j < qlen ? q[qrev < 0 ? j : qrev - j] : (j < ncol ? 5 : 12);
+    const int j = r * CD + c;
+    const bool valid = j < ncol;
+    // v_perm selector: profile byte 0..4 = query base, 5 = padding (scores 0)
+    const int code = j < qlen ? q[qrev < 0 ? j : qrev - j] : 5;
     sel[c] = 0x0c0c0c00u | (uint32_t)code;
     const int seg = slen ? min(j / slen, p) : 0;
     Xk[c] = j * e_ins;
-    Wk[c] = BIG * seg + j * e_ins;
-    Kf[c] = oe_ins + (j - 1) * e_ins;  // F(j) = max(0, Pfull(j) - Kf), o_ins > 0 keeps it >= 0
-    Ks[c] = BIG * seg + Kf[c];
-    valid[c] = j < ncol;
+    Wk[c] = BIG * seg;
+    Kf[c] = valid ? oe_ins + (j - 1) * e_ins : KINF;  // o_ins > 0 keeps it >= 0
+    Ks[c] = valid ? BIG * seg + oe_ins + (j - 1) * e_ins : KINF;
+    Mk[c] = U8 ? (valid ? 255 - shift : 0) : (valid ? -128 : -BIG);
     H[c] = 0;
     E[c] = 0;
     Hm[c] = 0;
@@ -103,75 +120,80 @@ __device__ __forceinline__ PassOut a2_pass(const A2Prof& P, const uint8_t* __res
   int gmax = 0, te = -1, nb = 0, bsc = 0, brow = 0;
   int rows = 0;
   auto tidx = [&](int i) { return i <= trev ? trev - i : i; };
-  int tv = 0, tvn = r < tlen ? t[tidx(r)] : 0;
-  for (int i = 0; i < tlen; ++i) {
-    if ((i & 63) == 0) {  // next 64 target bases, one per lane, fetched a window ahead
-      tv = tvn;
-      const int k = i + 64 + r;
+  // target rows in windows of 64, one base per lane; the next window is
+  // fetched while this one is processed and consumed only at the window
+  // boundary, so no row waits on memory.  Per window each lane turns its base
+  // into the row's two profile words; a row reads them with v_readlane.
+  int tvn = r < tlen ? t[tidx(r)] : 0;
+  for (int i0 = 0; i0 < tlen; i0 += 64) {
+    const int tv = tvn;
+    {
+      const int k = i0 + 64 + r;
       tvn = k < tlen ? t[tidx(k)] : 0;
     }
-    const int tb = __builtin_amdgcn_readlane(tv, i & 63);
-    uint32_t lo = P.lo[0], hi = P.hi[0];
-    lo = tb == 1 ? P.lo[1] : lo;
-    hi = tb == 1 ? P.hi[1] : hi;
-    lo = tb == 2 ? P.lo[2] : lo;
-    hi = tb == 2 ? P.hi[2] : hi;
-    lo = tb == 3 ? P.lo[3] : lo;
-    hi = tb == 3 ? P.hi[3] : hi;
-    lo = tb == 4 ? P.lo[4] : lo;
-    hi = tb == 4 ? P.hi[4] : hi;
-
-    // M, T = max(M, E) and the two scanned sequences
-    int T[CD], X[CD], W[CD];
-    int carry = 0;
+    uint32_t lov = P.lo[0], hiv = P.hi[0];
 #pragma unroll
-    for (int c = 0; c < CD; ++c) {
-      const int hd = dpp<DPP_WAVE_SHR1>(carry, H[c]);  // H(i-1, j-1); lane 0 <- previous segment's lane 63
-      if (c + 1 < CD) carry = __builtin_amdgcn_readlane(H[c], 63);
-      const int pv = (int)__builtin_amdgcn_perm(hi, lo, sel[c]);
-      int m;
-      if (U8) m = usat(min(hd + pv, 255), shift);  // adds_epu8 then subs_epu8 (ksw.c:153-154)
-      else m = hd + pv - 128;                      // adds_epi16 (ksw.c:270), no saturation (host bound)
-      T[c] = max(m, E[c]);
-      X[c] = wave_scan_max(T[c] + Xk[c]);
-      W[c] = wave_scan_max(T[c] + Wk[c]);
+    for (int b = 1; b < 5; ++b) {
+      lov = tv == b ? P.lo[b] : lov;
+      hiv = tv == b ? P.hi[b] : hiv;
     }
-    // exclusive prefixes with the carries of the earlier segments; h, E, H
-    int cx = 0, cw = 0, rm = 0;
+    const int iend = min(tlen - i0, 64);
+    for (int ii = 0; ii < iend; ++ii) {
+      const int i = i0 + ii;
+      const uint32_t lo = __builtin_amdgcn_readlane(lov, ii), hi = __builtin_amdgcn_readlane(hiv, ii);
+      int T[CD], Xl[CD], Wl[CD];
+      // H(i-1, j-1) of c = 0: lane r-1's last column; lane 0 reads 0 (bound_ctrl)
+      const int hd0 = __builtin_amdgcn_update_dpp(0, H[CD - 1], DPP_WAVE_SHR1, 0xF, 0xF, true);
+      int R = 0;
 #pragma unroll
-    for (int c = 0; c < CD; ++c) {
-      const int px = max(dpp<DPP_WAVE_SHR1>(0, X[c]), cx);
-      const int pw = max(dpp<DPP_WAVE_SHR1>(0, W[c]), cw);
-      if (c + 1 < CD) {
-        cx = max(cx, __builtin_amdgcn_readlane(X[c], 63));
-        cw = max(cw, __builtin_amdgcn_readlane(W[c], 63));
+      for (int c = 0; c < CD; ++c) {
+        const int hd = c ? H[c - 1] : hd0;
+        const int pv = (int)__builtin_amdgcn_perm(hi, lo, sel[c]);
+        int m;
+        if (U8) m = med3_i32(hd + pv - shift, Mk[c]);  // adds_epu8 + subs_epu8 (ksw.c:153-154)
+        else m = hd + pv + Mk[c];                      // adds_epi16 (ksw.c:270); host bounds the scores
+        T[c] = max(m, E[c]);
+        const int x = T[c] + Xk[c], w = x + Wk[c];
+        Xl[c] = c ? max(Xl[c - 1], x) : x;  // in-lane inclusive prefix maxima
+        Wl[c] = c ? max(Wl[c - 1], w) : w;
+        R = max(R, T[c]);
       }
-      const int h = max(T[c], usat(pw, Ks[c]));  // first-pass H (segment-local F)
-      rm = max(rm, valid[c] ? h : 0);
-      E[c] = max(usat(E[c], e_del), usat(h, oe_del));
-      H[c] = max(h, usat(px, Kf[c]));            // after the lazy-F loop
-    }
-    rm = wave_max(rm);
-    ++rows;
-    if (rm >= minsc) {  // b[] of row maxima (ksw.c:191-198)
-      if (nb == 0 || brow + 1 != i) {
-        if (nb && r == 0) bs[nb - 1] = make_int2(bsc, brow);
-        ++nb;
-        bsc = rm;
-        brow = i;
-      } else if (bsc < rm) {
-        bsc = rm;
-        brow = i;
-      }
-    }
-    if (rm > gmax) {  // ksw.c:199-204
-      gmax = rm;
-      te = i;
+      int sX = Xl[CD - 1], sW = Wl[CD - 1];
+      scan_max3(sX, sW, R);
+      const int rm = __builtin_amdgcn_readlane(R, 63);
+      // maxima over the lanes before this one (lane 0: none -> 0, the identity)
+      const int Xin = __builtin_amdgcn_update_dpp(0, sX, DPP_WAVE_SHR1, 0xF, 0xF, true);
+      const int Win = __builtin_amdgcn_update_dpp(0, sW, DPP_WAVE_SHR1, 0xF, 0xF, true);
 #pragma unroll
-      for (int c = 0; c < CD; ++c) Hm[c] = H[c];
-      if ((U8 && gmax + shift >= 255) || gmax >= endsc) break;
+      for (int c = 0; c < CD; ++c) {
+        const int px = c ? max(Xin, Xl[c - 1]) : Xin;
+        const int pw = c ? max(Win, Wl[c - 1]) : Win;
+        const int h = max(T[c], usat(pw, Ks[c]));  // first-pass H (segment-local F)
+        E[c] = max(usat(E[c], e_del), usat(h, oe_del));
+        H[c] = max(h, usat(px, Kf[c]));            // after the lazy-F loop
+      }
+      ++rows;
+      if (rm >= minsc) {  // b[] of row maxima (ksw.c:191-198)
+        if (nb == 0 || brow + 1 != i) {
+          if (nb && r == 0) bs[nb - 1] = make_int2(bsc, brow);
+          ++nb;
+          bsc = rm;
+          brow = i;
+        } else if (bsc < rm) {
+          bsc = rm;
+          brow = i;
+        }
+      }
+      if (rm > gmax) {  // ksw.c:199-204
+        gmax = rm;
+        te = i;
+#pragma unroll
+        for (int c = 0; c < CD; ++c) Hm[c] = H[c];
+        if ((U8 && gmax + shift >= 255) || gmax >= endsc) goto rows_done_;
+      }
     }
   }
+rows_done_:
   rows_done += rows;
   cells_done += (long long)rows * qlen;
   PassOut o{};
@@ -183,13 +205,14 @@ __device__ __forceinline__ PassOut a2_pass(const A2Prof& P, const uint8_t* __res
   o.te2 = -1;
   if (sat) return o;
   if (ncol > 0) {  // qe: the smallest column holding the row's maximum (ksw.c:210-213)
-    int mx = -1;
+    // columns past p*slen hold 0 and come after every real one: no masking
+    int mx = 0;
 #pragma unroll
-    for (int c = 0; c < CD; ++c) mx = max(mx, valid[c] ? Hm[c] : -1);
+    for (int c = 0; c < CD; ++c) mx = max(mx, Hm[c]);
     mx = wave_max(mx);
     int jm = INT_MAX;
 #pragma unroll
-    for (int c = CD - 1; c >= 0; --c) jm = (valid[c] && Hm[c] == mx) ? 64 * c + r : jm;
+    for (int c = CD - 1; c >= 0; --c) jm = Hm[c] == mx ? r * CD + c : jm;
     o.qe = wave_min(jm);
   }
   if (nb) {  // 2nd best outside [te-k, te+k] (ksw.c:215-225)
