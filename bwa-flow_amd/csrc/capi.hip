@@ -145,6 +145,14 @@ bool make_opt(const bwagpu_opt_t* o, DevOpt* d, std::string* why) {
   if (!o) { *why = "opt is NULL"; return false; }
   if (o->e_del <= 0 || o->e_ins <= 0) { *why = "gap extension penalties must be > 0"; return false; }
   if (o->w < 0 || o->a < 0) { *why = "negative band width or match score"; return false; }
+  // bounds under which the kernels' integer forms of the reference's double
+  // expressions (cal_max_gap, the ksw_extend2 band clamp) are exact
+  if (o->a > 127 || o->e_del > 65535 || o->e_ins > 65535 || o->o_del < 0 || o->o_del > 65535 || o->o_ins < 0 ||
+      o->o_ins > 65535 || o->pen_clip5 < 0 || o->pen_clip5 >= (1 << 20) || o->pen_clip3 < 0 ||
+      o->pen_clip3 >= (1 << 20) || o->w > (1 << 20)) {
+    *why = "scoring option out of range";
+    return false;
+  }
   memset(d, 0, sizeof(*d));
   d->a = o->a;
   d->o_del = o->o_del;

@@ -67,31 +67,56 @@ __device__ __forceinline__ int pac_base2(const uint8_t* __restrict__ pac, int64_
   return 3 - ((pac[f >> 2] >> ((~f & 3) << 1)) & 3);
 }
 
+// (int)((double)x / e + 1.) exactly, for e >= 1 and |x| < 2^21 (make_opt
+// bounds every input): the real value is (x+e)/e, so it is C's truncating
+// quotient.  A float reciprocal gives it to within one; one remainder check
+// fixes it — instead of the f64 division the reference's expression compiles to.
+__device__ __forceinline__ int trunc_div1(int x, int e) {
+  const int n = x + e;
+  const int an = n < 0 ? -n : n;
+  int q = (int)((float)an * __builtin_amdgcn_rcpf((float)e));
+  const int r = an - q * e;
+  q = r >= e ? q + 1 : (r < 0 ? q - 1 : q);
+  return n < 0 ? -q : q;
+}
+
 // cal_max_gap, bwamem.c:630-637
 __device__ __forceinline__ int max_gap_len(const DevOpt& o, int qlen) {
-  int ld = (int)((double)(qlen * o.a - o.o_del) / o.e_del + 1.);
-  int li = (int)((double)(qlen * o.a - o.o_ins) / o.e_ins + 1.);
+  int ld = trunc_div1(qlen * o.a - o.o_del, o.e_del);
+  int li = trunc_div1(qlen * o.a - o.o_ins, o.e_ins);
   int l = ld > li ? ld : li;
   l = l > 1 ? l : 1;
   return l < (o.w << 1) ? l : (o.w << 1);
 }
 
+// band clamp of ksw_extend2 (ksw.c:399-407), device form of band_cap
+__device__ __forceinline__ int band_cap_dev(int qlen, int max_mat, int end_bonus, int o, int e) {
+  const int l = trunc_div1(qlen * max_mat + end_bonus - o, e);
+  return l > 1 ? l : 1;
+}
+
 // query profile of base q (0..4): byte t = mat[t*5 + q]; selects over kernel
-// arguments (SGPRs), no memory traffic
+// arguments (SGPRs).  The empty asm makes the five words opaque so that the
+// select chain is not turned back into an indexed load from the kernarg
+// segment (a global load per extension whose wait also drained the table DMA).
 __device__ __forceinline__ uint32_t qprof_word(const DevOpt& o, int q) {
-  uint32_t v = o.qprof[0];
-  v = q == 1 ? o.qprof[1] : v;
-  v = q == 2 ? o.qprof[2] : v;
-  v = q == 3 ? o.qprof[3] : v;
-  v = q == 4 ? o.qprof[4] : v;
+  uint32_t p0 = o.qprof[0], p1 = o.qprof[1], p2 = o.qprof[2], p3 = o.qprof[3], p4 = o.qprof[4];
+  asm volatile("" : "+s"(p0), "+s"(p1), "+s"(p2), "+s"(p3), "+s"(p4));
+  uint32_t v = p0;
+  v = q == 1 ? p1 : v;
+  v = q == 2 ? p2 : v;
+  v = q == 3 ? p3 : v;
+  v = q == 4 ? p4 : v;
   return v;
 }
 __device__ __forceinline__ int qprof4_val(const DevOpt& o, int q) {
-  int v = o.qprof4[0];
-  v = q == 1 ? o.qprof4[1] : v;
-  v = q == 2 ? o.qprof4[2] : v;
-  v = q == 3 ? o.qprof4[3] : v;
-  v = q == 4 ? o.qprof4[4] : v;
+  int p0 = o.qprof4[0], p1 = o.qprof4[1], p2 = o.qprof4[2], p3 = o.qprof4[3], p4 = o.qprof4[4];
+  asm volatile("" : "+s"(p0), "+s"(p1), "+s"(p2), "+s"(p3), "+s"(p4));
+  int v = p0;
+  v = q == 1 ? p1 : v;
+  v = q == 2 ? p2 : v;
+  v = q == 3 ? p3 : v;
+  v = q == 4 ? p4 : v;
   return v;
 }
 
@@ -149,8 +174,8 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     Fc[c] = e_ins - j * e_ins;     // F_j = EX_j + Fc
   }
   {  // band clamp (ksw.c:399-407)
-    const int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
-    const int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, e_del);
+    const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
+    const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, e_del);
     w = __builtin_amdgcn_readfirstlane(min(w, min(mi, md)));
   }
   int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0, lo = 0, hi = qlen;
@@ -288,8 +313,8 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
 
 // rows that extend_group can read for (qlen, w, end_bonus)
 __device__ __forceinline__ int rows_needed(const DevOpt& o, int qlen, int tlen, int w, int end_bonus) {
-  int mi = band_cap(qlen, o.max_mat, end_bonus, o.o_ins, o.e_ins);
-  int md = band_cap(qlen, o.max_mat, end_bonus, o.o_del, o.e_del);
+  int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, o.e_ins);
+  int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, o.e_del);
   int we = min(w, min(mi, md));
   return min(tlen, qlen + we + 1);
 }
