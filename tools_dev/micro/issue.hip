@@ -1,0 +1,88 @@
+// Issue-cost microbenchmark (gfx950): cycles per SIMD per instruction for
+// VALU / SALU / DPP / s_nop / mixed streams at W waves per SIMD.
+// W blocks of 4 waves per CU (one wave per SIMD per block): W waves per SIMD.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define REP8(x) x x x x x x x x
+constexpr int ITERS = 4096;
+
+template <int MODE>
+__global__ void k(int* out, int seed) {
+  int v0 = threadIdx.x + seed, v1 = v0 * 3, v2 = v0 * 5, v3 = v0 * 7;
+  int s0 = seed, s1 = seed * 3, s2 = seed * 5, s3 = seed * 7;
+  for (int it = 0; it < ITERS; ++it) {
+    if (MODE == 0) {  // 32 independent VALU
+      REP8(asm volatile("v_add_u32 %0, %0, %1\n v_add_u32 %2, %2, %3\n v_xor_b32 %1, %1, %0\n v_xor_b32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 1) {  // 32 SALU
+      REP8(asm volatile("s_mul_i32 %0, %0, %1\n s_mul_i32 %2, %2, %3\n s_mul_hi_u32 %1, %1, %0\n s_mul_hi_u32 %3, %3, %2" : "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3));)
+    } else if (MODE == 2) {  // 16 VALU + 16 SALU interleaved
+      REP8(asm volatile("v_add_u32 %0, %0, %1\n s_mul_i32 %4, %4, %5\n v_xor_b32 %2, %2, %3\n s_mul_i32 %6, %6, %7" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3));)
+    } else if (MODE == 3) {  // 32 DPP max on 4 independent chains, no nops needed (4 chains)
+      REP8(asm volatile("v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n v_max_i32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf\n v_max_i32_dpp %3, %3, %3 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 4) {  // 16 DPP single chain, s_nop 1 before each (the extension kernel's form)
+      REP8(asm volatile("s_nop 1\n v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf" : "+v"(v0));)
+    } else if (MODE == 5) {  // 32 dependent VALU (one chain)
+      REP8(asm volatile("v_add_u32 %0, %0, %1\n v_xor_b32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_xor_b32 %0, %0, %1" : "+v"(v0) : "v"(v1));)
+    } else if (MODE == 6) {  // 32 dependent SALU
+      REP8(asm volatile("s_mul_i32 %0, %0, %1\n s_mul_hi_u32 %0, %0, %1\n s_mul_i32 %0, %0, %1\n s_mul_hi_u32 %0, %0, %1" : "+s"(s0) : "s"(s1));)
+    } else if (MODE == 7) {  // 8 x (v_readlane -> s_mul -> v_add) round trips
+      REP8(asm volatile("v_readlane_b32 %4, %0, 63\n s_mul_i32 %4, %4, %5\n v_add_u32 %1, %1, %4\n v_xor_b32 %0, %0, %1" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+s"(s0), "+s"(s1));)
+    } else if (MODE == 8) {  // 32 s_nop 0
+      REP8(asm volatile("s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0");)
+    } else if (MODE == 9) {  // 16 VALU + 16 SALU, SALU dependent chain (like band bookkeeping)
+      REP8(asm volatile("v_add_u32 %0, %0, %1\n s_mul_i32 %4, %4, %5\n v_xor_b32 %2, %2, %3\n s_mul_hi_u32 %4, %4, %5" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+s"(s0), "+s"(s1));)
+    }
+  }
+  if ((v0 ^ v1 ^ v2 ^ v3 ^ s0 ^ s1 ^ s2 ^ s3) == 0x12345) out[threadIdx.x] = 1;
+}
+
+int main() {
+  int dev = 0, ncu = 0, clk = 0;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, dev);  // kHz
+  setvbuf(stdout, nullptr, _IONBF, 0);
+  int* out;
+  hipMalloc(&out, 4096 * 4);
+  const char* names[] = {"VALU indep", "SALU indep", "VALU+SALU mix", "DPP 4 chains", "DPP+s_nop1 1 chain",
+                         "VALU dep chain", "SALU dep chain", "readlane rt", "s_nop 0", "VALU + SALU chain"};
+  printf("{\"cus\": %d, \"clock_khz\": %d, \"results\": [\n", ncu, clk);
+  for (int mode = 0; mode < 10; ++mode) {
+    for (int W : {1, 2, 4, 5, 8}) {
+      hipEvent_t a, b;
+      hipEventCreate(&a);
+      hipEventCreate(&b);
+      auto launch = [&]() {
+        dim3 g(ncu * W), blk(256);
+        switch (mode) {
+          case 0: hipLaunchKernelGGL(k<0>, g, blk, 0, 0, out, 1); break;
+          case 1: hipLaunchKernelGGL(k<1>, g, blk, 0, 0, out, 1); break;
+          case 2: hipLaunchKernelGGL(k<2>, g, blk, 0, 0, out, 1); break;
+          case 3: hipLaunchKernelGGL(k<3>, g, blk, 0, 0, out, 1); break;
+          case 4: hipLaunchKernelGGL(k<4>, g, blk, 0, 0, out, 1); break;
+          case 5: hipLaunchKernelGGL(k<5>, g, blk, 0, 0, out, 1); break;
+          case 6: hipLaunchKernelGGL(k<6>, g, blk, 0, 0, out, 1); break;
+          case 7: hipLaunchKernelGGL(k<7>, g, blk, 0, 0, out, 1); break;
+          case 8: hipLaunchKernelGGL(k<8>, g, blk, 0, 0, out, 1); break;
+          case 9: hipLaunchKernelGGL(k<9>, g, blk, 0, 0, out, 1); break;
+        }
+      };
+      launch();
+      hipDeviceSynchronize();
+      hipEventRecord(a);
+      for (int r = 0; r < 5; ++r) launch();
+      hipEventRecord(b);
+      hipEventSynchronize(b);
+      float ms = 0;
+      hipEventElapsedTime(&ms, a, b);
+      const double cycles = ms / 5 * 1e-3 * clk * 1e3;
+      const int per_iter = (mode == 4) ? 16 : (mode == 7 ? 32 : 32);
+      const double per_instr_simd = cycles / ((double)ITERS * per_iter * W);  // SIMD cycles per wave-instruction
+      printf("  {\"mode\": \"%s\", \"waves_per_simd\": %d, \"us\": %.1f, \"simd_cycles_per_instr\": %.3f}%s\n", names[mode],
+             W, ms / 5 * 1e3, per_instr_simd, (mode == 9 && W == 8) ? "" : ",");
+    }
+  }
+  printf("]}\n");
+  return 0;
+}
