@@ -67,6 +67,16 @@ __device__ __forceinline__ int pac_base2(const uint8_t* __restrict__ pac, int64_
   return 3 - ((pac[f >> 2] >> ((~f & 3) << 1)) & 3);
 }
 
+// a wave-uniform value kept in a VGPR: arithmetic on it issues on the VALU
+__device__ __forceinline__ int vgpr(int x) {
+  int y;
+  asm("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+__device__ __forceinline__ int usat32(int a, int b) {  // max(a - b, 0) for a, b >= 0
+  return (int)__builtin_elementwise_sub_sat((unsigned)a, (unsigned)b);
+}
+
 // (int)((double)x / e + 1.) exactly, for e >= 1 and |x| < 2^21 (make_opt
 // bounds every input): the real value is (x+e)/e, so it is C's truncating
 // quotient.  A float reciprocal gives it to within one; one remainder check
@@ -178,16 +188,28 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, e_del);
     w = __builtin_amdgcn_readfirstlane(min(w, min(mi, md)));
   }
-  int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0, lo = 0, hi = qlen;
-  int cells = 0, rows = 0;
+  // Row bookkeeping (band, left column, z-drop, maxima) is wave-uniform but
+  // lives in VGPRs: a VALU op issues at ~2.5 SIMD cycles, an SALU op at ~4.3
+  // (profiles/r01e_issue_costs.json), and VALU work of one wave overlaps the
+  // SALU of another.  Only the two exits branch on scalars.
+  int best = vgpr(h0), bi = vgpr(-1), bj = vgpr(-1), ei = vgpr(-1), esc = vgpr(-1), off = vgpr(0);
+  int lo = vgpr(0), hi = vgpr(qlen);
+  int iw = vgpr(-w), iw1 = vgpr(w + 1);  // i - w, i + w + 1
+  int gl = vgpr(h0 - o.o_del - e_del);   // h0 - (o_del + e_del*(i+1))
+  int vi = vgpr(0);                      // i
+  int cells = vgpr(0);
+  int rows = tlen;
   int tnext = tlen > 0 ? tb[0] : 0;
   for (int i = 0; i < tlen; ++i) {
     const int t = __builtin_amdgcn_readfirstlane(tnext);
     tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
-    lo = __builtin_amdgcn_readfirstlane(max(lo, i - w));
-    hi = __builtin_amdgcn_readfirstlane(min(min(hi, i + w + 1), qlen));
-    const int wd = hi > lo ? hi - lo : 0;  // in band: (unsigned)(j - lo) < wd
-    const int left0 = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
+    lo = max(lo, iw);
+    hi = min(min(hi, iw1), qlen);
+    iw += 1;
+    iw1 += 1;
+    const int wd = usat32(hi, lo);  // hi > lo ? hi - lo : 0; in band: (unsigned)(j - lo) < wd
+    const int left0 = lo == 0 ? max(gl, 0) : 0;
+    gl -= e_del;
     const int sh = (t & 3) << 3;
 
     // pass 1 + segmented exclusive max-scan of u
@@ -208,9 +230,9 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       EX[c] = dpp<DPP_WAVE_SHR1>(carry, x);  // lane 0 takes the carry from the segments before
       if (c + 1 < CD) carry = __builtin_amdgcn_readlane(x, 63);
     }
-    // pass 2: H, E, row-max key, next-row state
-    int rk = 0, prev63 = 0;
-    int h1c[CD];
+    // pass 2: H, E, row-max key, next-row state; hsel = the register holding
+    // column hi (H(i, hi-1) after the shift)
+    int rk = 0, prev63 = 0, hsel = 0;
 #pragma unroll
     for (int c = 0; c < CD; ++c) {
       const int f = EX[c] + Fc[c];
@@ -219,74 +241,93 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       rk = max(rk, inb[c] ? (h << 10 | jc[c]) : 0);
       const int hs = dpp<DPP_WAVE_SHR1>(prev63, h);  // H(i, j-1)
       if (c + 1 < CD) prev63 = __builtin_amdgcn_readlane(h, 63);
-      h1c[c] = __builtin_amdgcn_readlane(hs, (hi - 64 * c) & 63);  // H(i, hi-1) if hi is in segment c
+      hsel = (c == 0 || (hi >> 6) == c) ? hs : hsel;
       hh[c] = inb[c] ? hs : hh[c];
       ee[c] = inb[c] ? en : ee[c];
     }
+    const int hi_s = __builtin_amdgcn_readfirstlane(hi);
     // h1 = H(i, hi-1), or the first-column value when the band is empty
-    int h1 = h1c[0];
-#pragma unroll
-    for (int c = 1; c < CD; ++c) h1 = (hi >> 6) == c ? h1c[c] : h1;
-    h1 = hi > lo ? h1 : left0;
+    const int h1r = __builtin_amdgcn_readlane(hsel, hi_s & 63);
+    const int h1 = hi > lo ? h1r : left0;
     // eh[lo].h = first-column value (only when lo < hi), eh[hi] = {h1, 0}:
-    // single-lane writes at uniform targets; a target outside [0,64) hits no lane
+    // single-lane writes at uniform targets
     const int tlo = hi > lo ? lo : -1;
 #pragma unroll
     for (int c = 0; c < CD; ++c) {
-      hh[c] = r == tlo - 64 * c ? left0 : hh[c];
-      const bool at_hi = r == hi - 64 * c;
+      hh[c] = jc[c] == tlo ? left0 : hh[c];
+      const bool at_hi = jc[c] == hi;
       hh[c] = at_hi ? h1 : hh[c];
       ee[c] = at_hi ? 0 : ee[c];
     }
     // zero-trim of the band for the next row (ksw.c:466-469), computed ahead of
     // the row-max reduction (independent of it; applied only if no break):
     // first non-zero column in [lo,hi), last non-zero column in [lo,hi]
-    int nlo = hi, jl = -1;
+    int nlo, nhi;
+    if constexpr (CD == 1) {
+      // qlen < 64, so hi < 64: one mask per row, no segment loop
+      const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[0] | ee[0]) != 0);
+      const uint64_t f = nz & __builtin_amdgcn_ballot_w64(inb[0]);
+      const uint64_t l = f | (nz & (1ull << hi_s));
+      nlo = f ? __builtin_ctzll(f) : hi_s;
+      const int jl = l ? 63 - __builtin_clzll(l) : nlo - 1;
+      nhi = min(jl + 2, qlen);
+    } else {
+      int jl = -1;
+      nlo = hi_s;
 #pragma unroll
-    for (int c = CD - 1; c >= 0; --c) {
-      const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[c] | ee[c]) != 0);
-      const uint64_t f = nz & __builtin_amdgcn_ballot_w64(inb[c]);
-      const int hc = hi - 64 * c;
-      const uint64_t l = f | (nz & ((unsigned)hc < 64u ? 1ull << hc : 0ull));
-      nlo = f ? 64 * c + __builtin_ctzll(f) : nlo;  // descending c: the lowest segment wins
-      jl = (jl < 0 && l) ? 64 * c + 63 - __builtin_clzll(l) : jl;
+      for (int c = CD - 1; c >= 0; --c) {
+        const uint64_t nz = __builtin_amdgcn_ballot_w64((hh[c] | ee[c]) != 0);
+        const uint64_t f = nz & __builtin_amdgcn_ballot_w64(inb[c]);
+        const int hc = hi_s - 64 * c;
+        const uint64_t l = f | (nz & ((unsigned)hc < 64u ? 1ull << hc : 0ull));
+        nlo = f ? 64 * c + __builtin_ctzll(f) : nlo;  // descending c: the lowest segment wins
+        jl = (jl < 0 && l) ? 64 * c + 63 - __builtin_clzll(l) : jl;
+      }
+      if (jl < 0) jl = nlo - 1;
+      nhi = min(jl + 2, qlen);
     }
-    if (jl < 0) jl = nlo - 1;
-    const int nhi = min(jl + 2, qlen);
     rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
     rk = __builtin_amdgcn_readlane(rk, 63);
-    rows += 1;
     cells += wd;
-    if (max(lo, hi) == qlen) {  // ksw.c:450-453
-      ei = esc > h1 ? ei : i;
-      esc = max(esc, h1);
+    {  // ksw.c:450-453
+      const bool atend = max(lo, hi) == qlen;
+      ei = (atend && !(esc > h1)) ? vi : ei;
+      esc = atend ? max(esc, h1) : esc;
     }
+    // ksw.c:454-465, all lanes alike.  The row's updates come before the one
+    // exit test: on an exit row they are no-ops (a z-drop exit has m <= max,
+    // and m == 0 cannot beat max >= h0 >= 0), and the trimmed band is unused.
+    // drop: exactly one of (di-dj)*e_del, (dj-di)*e_ins is positive (both are
+    // 0 when di == dj), which is the branch ksw.c:461-463 takes.
     const int mrow = rk >> 10, mj = rk & 1023;
-    if (mrow == 0) break;
-    if (mrow > best) {
-      best = mrow;
-      bi = i;
-      bj = mj;
-      off = max(off, abs(mj - i));
-    } else if (zdrop > 0) {
-      const int di = i - bi, dj = mj - bj;
-      const int drop = di > dj ? best - mrow - (di - dj) * e_del : best - mrow - (dj - di) * e_ins;
-      if (drop > zdrop) break;
-    }
+    const bool up = mrow > best;
+    const int di = vi - bi, dj = mj - bj;
+    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
+    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
+    off = up ? max(off, abs(mj - vi)) : off;
+    best = up ? mrow : best;
+    bi = up ? vi : bi;
+    bj = up ? mj : bj;
+    vi += 1;
     lo = nlo;
     hi = nhi;
+    if (__builtin_amdgcn_ballot_w64(brk)) {
+      rows = i + 1;
+      break;
+    }
   }
-  tl.cells += cells;
+  tl.cells += __builtin_amdgcn_readfirstlane(cells);
   tl.rows += rows;
   tl.calls += 1;
 #ifdef BWAGPU_CD_STATS
   if (g_trace && r == 0) {  // diagnostics: rows / cells / calls per segment count
     atomicAdd(&g_trace[4 * CD + 0], (uint32_t)rows);
-    atomicAdd(&g_trace[4 * CD + 1], (uint32_t)cells);
+    atomicAdd(&g_trace[4 * CD + 1], (uint32_t)__builtin_amdgcn_readfirstlane(cells));
     atomicAdd(&g_trace[4 * CD + 2], 1u);
   }
 #endif
-  return ExtOut{best, bj + 1, bi + 1, ei + 1, esc, off};
+  auto u = [](int x) { return __builtin_amdgcn_readfirstlane(x); };
+  return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
 }
 
 // CD is uniform per call (qlen is): one compiled body per segment count
