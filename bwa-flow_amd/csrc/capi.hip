@@ -604,7 +604,12 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   if (n == 0) return BWAGPU_OK;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   // validate and bin on the host
-  std::vector<int32_t> lists[kNumVariants];
+  // bins: [0, kNumVariants) wave kernels, then the 16-lane-group kernels
+  // (CPL 4, 8); BWAGPU_EXT_WAVE=1 keeps every task on the wave kernels (A/B)
+  constexpr int kGrpBins = 2;
+  std::vector<int32_t> lists[kNumVariants + kGrpBins];
+  const char* ew = getenv("BWAGPU_EXT_WAVE");
+  const bool grp = !(ew && ew[0] == '1');
   bool t5 = false;
   int lq_max = 1;
   for (int32_t k = 0; k < n; ++k) {
@@ -616,6 +621,8 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
     int v = kNumVariants - 1;
     for (int i = kNumVariants - 1; i >= 0; --i)
       if (t.qlen + 1 <= kVariants[i].max_len()) v = i;
+    if (grp && t.qlen + 1 <= 64) v = kNumVariants;
+    else if (grp && t.qlen + 1 <= 128) v = kNumVariants + 1;
     lists[v].push_back(k);
     lq_max = std::max(lq_max, t.qlen + 1);
   }
@@ -655,9 +662,9 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   (void)hipEventRecord(e0, st);
   int32_t off = 0;
   std::vector<int32_t> all;
-  for (int v = 0; v < kNumVariants; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
+  for (int v = 0; v < kNumVariants + kGrpBins; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
   if ((rc = ck(hipMemcpyAsync(d_list.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D"))) return rc;
-  for (int v = 0; v < kNumVariants; ++v) {
+  for (int v = 0; v < kNumVariants + kGrpBins; ++v) {
     const int32_t nv = (int32_t)lists[v].size();
     if (nv) {
       int rows = 16;
@@ -669,14 +676,19 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
         rows = std::max(rows, std::min(t.tlen, t.qlen + we + 1));
       }
       const int tb = (rows + 2 + 15) & ~15;
-      const int gpb = kBlock / kVariants[v].G;
+      const int gpb = v < kNumVariants ? kBlock / kVariants[v].G : kBlock / 16;
       if ((size_t)tb * gpb > 64 * 1024) {
         cleanup();
         return fail(ctx, BWAGPU_E_UNSUPPORTED, "task needs too many LDS rows");
       }
-      hipError_t e = launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off,
-                                   nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
-                                   d_stats.as<int64_t>(), st);
+      hipError_t e =
+          v < kNumVariants
+              ? launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off, nv,
+                              d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
+                              d_stats.as<int64_t>(), st)
+              : launch_extend_grp(v == kNumVariants ? 4 : 8, t5, ctx->opt, d_tasks.as<bwagpu_ext_task_t>(),
+                                  d_list.as<int32_t>() + off, nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb,
+                                  d_res.as<bwagpu_ext_result_t>(), d_stats.as<int64_t>(), st);
       if ((rc = ck(e, "extend launch"))) return rc;
     }
     off += nv;

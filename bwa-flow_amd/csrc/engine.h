@@ -110,6 +110,11 @@ hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,
                          bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
 
+// 16-lane-group ksw_extend2 over a task list: cpl = 4 (qlen + 1 <= 64) or 8 (<= 128)
+hipError_t launch_extend_grp(int cpl, bool t5, const DevOpt& o, const bwagpu_ext_task_t* tasks,
+                             const int32_t* task_list, int32_t n_list, const uint8_t* qpool, const uint8_t* tpool,
+                             int tb_bytes, bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
+
 // diagnostics: per-read trace buffer (device pointer, 8 x u32 per read; NULL = off)
 hipError_t set_trace(void* dev_ptr);
 

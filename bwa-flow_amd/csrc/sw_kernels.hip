@@ -352,6 +352,186 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
   return ExtOut{-1, 0, 0, 0, -1, 0};  // unreachable: cd <= C by construction
 }
 
+// ------------------------------------------------ ksw_extend2, 16-lane groups
+// One extension per 16-lane group (one DPP row), FOUR extensions per wave that
+// share every instruction of a DP row.  Columns are BLOCKED: lane r of the
+// group holds columns j = r*CPL + c, c < CPL (qlen + 1 <= 16*CPL).  Every
+// group-uniform quantity (band, maxima, break state) is a per-lane VGPR value
+// identical over the group's lanes, so the four groups of a wave run their rows
+// in lock step, each with its own band, and leave the row loop independently.
+//
+// Per row (ksw.c:415-470):
+//  * M_j = H(i-1,j-1) ? H(i-1,j-1) + S(t_i, q_j) : 0, masked to NEG outside
+//    the band [lo, hi);
+//  * F: F(i,j) = max_{k<j}(t_k - (j-1-k)e_ins) over t_k = max(M_k - oe_ins, 0).
+//    With v_k = M_k + k*e_ins - oe_ins and P_c = max(0, v_0..v_c) (in-lane
+//    prefix), F at the lane's first column comes from ONE exclusive group
+//    scan of U = P_{CPL-1} + e_ins*(r*CPL - CPL + 1); inside the lane
+//    F_c = sat(max(F_in - e_ins, P_{c-1}) - (c-1)e_ins) for c >= 1;
+//  * H = max(M, E, F); the H value stored for column j is H(i, j-1) (the lane's
+//    own previous column, or the DPP-shifted last column of the lane below;
+//    lane 0 of the group injects the first-column value left0, ksw.c:420-423);
+//    the reference's eh[hi] = {h1, 0} write (ksw.c:449) is the same update
+//    applied to column hi with E cleared, so [lo, hi] is updated in one rule;
+//  * row max + LAST argmax: group max of (H << 10 | j), in-lane as H*8 + c;
+//  * band trim (ksw.c:466-469): per-lane bitmask of non-zero columns, first
+//    column in [lo, hi) by a group min, last in [lo, hi] by a group max.
+template <int CPL, bool T5>
+struct GrpExt {
+  int hh[CPL], ee[CPL];
+  uint32_t pf[CPL];
+  uint32_t pf4[T5 ? CPL : 1];
+  int lo, hi, iw, iw1, gl, vi, best, bi, bj, ei, esc, off, cells, tlen, zdrop, qlen;
+  uint32_t tb;  // LDS byte offset of target row 0
+  int tnext;
+};
+
+__device__ __forceinline__ int g16_max(int v) { return max_ror1(max_ror2(max_ror4(max_ror8(v)))); }
+__device__ __forceinline__ int g16_min(int v) { return min_ror1(min_ror2(min_ror4(min_ror8(v)))); }
+
+// Q(j) = query base of column j (j < qlen); tb/lds: target rows in LDS
+template <int CPL, bool T5, typename Q>
+__device__ __forceinline__ void gext_init(GrpExt<CPL, T5>& s, const DevOpt& o, int r, int qlen, Q qbase, int tlen,
+                                          uint32_t tb, const uint8_t* lds, int w, int end_bonus, int zdrop, int h0) {
+  const int e_ins = o.e_ins, oe_ins = o.oe_ins;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j = r * CPL + c;
+    const int qb = j < qlen ? qbase(j) : 0;
+    s.pf[c] = qprof_word(o, qb);
+    if (T5) s.pf4[c] = (uint32_t)(uint8_t)qprof4_val(o, qb);
+    // row -1 of eh[] (ksw.c:392-395)
+    const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
+    s.hh[c] = j <= qlen ? v : 0;
+    s.ee[c] = 0;
+  }
+  const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
+  const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, o.e_del);
+  w = min(w, min(mi, md));
+  s.best = h0;
+  s.bi = s.bj = s.ei = s.esc = -1;
+  s.off = 0;
+  s.lo = 0;
+  s.hi = qlen;
+  s.iw = -w;
+  s.iw1 = w + 1;
+  s.gl = h0 - o.o_del - o.e_del;
+  s.vi = 0;
+  s.cells = 0;
+  s.tlen = tlen;
+  s.zdrop = zdrop;
+  s.qlen = qlen;
+  s.tb = tb;
+  s.tnext = tlen > 0 ? lds[tb] : 0;
+}
+
+// one DP row of every active group; returns true (group-uniform) when the
+// extension is finished (break or last row)
+template <int CPL, bool T5>
+__device__ __forceinline__ bool gext_row(GrpExt<CPL, T5>& s, const DevOpt& o, int r, const uint8_t* lds) {
+  const int e_del = o.e_del, e_ins = o.e_ins, o_del = o.o_del, oe_ins = o.oe_ins;
+  const int j0 = r * CPL;
+  const int t = s.tnext;
+  s.tnext = lds[s.tb + s.vi + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
+  s.lo = max(s.lo, s.iw);
+  s.hi = min(min(s.hi, s.iw1), s.qlen);
+  s.iw += 1;
+  s.iw1 += 1;
+  const int lo = s.lo, hi = s.hi;
+  const int wd = usat32(hi, lo);
+  const int left0 = lo == 0 ? max(s.gl, 0) : 0;
+  s.gl -= e_del;
+  const int sh = (t & 3) << 3;
+  const int x = j0 - lo;
+  int M[CPL], A[CPL];
+  int T = 0;  // F carried to the next column from this lane's columns alone (clamped at the end)
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const bool ib = (unsigned)(x + c) < (unsigned)wd;
+    int sc;
+    if (T5 && t == 4) sc = (int)(int8_t)(s.pf4[c] & 0xff);
+    else sc = __builtin_amdgcn_sbfe((int)s.pf[c], sh, 8);
+    const int m = s.hh[c] ? s.hh[c] + sc : 0;
+    M[c] = m;
+    A[c] = (ib ? m : NEG) - oe_ins;  // t_c before the clamp at 0
+    T = max(T - e_ins, A[c]);
+  }
+  // exclusive group scan: F entering the lane's first column is
+  // max(0, max_{r'<r} T_{r'} - (r-1-r')*CPL*e_ins)
+  const int U = T + e_ins * CPL * r;
+  // the band tests are recomputed below rather than kept as 2*CPL live SGPR
+  // masks across the scan (which spilled)
+  int xb = x;
+  asm volatile("" : "+v"(xb));
+  const int inc = max_shr8(max_shr4(max_shr2(max_shr1(U))));
+  const int EX = dpp<DPP_ROW_SHR(1)>(NEG, inc);
+  int f = max(EX - e_ins * CPL * (r - 1), 0);
+  int hm[CPL];
+  int lk = 0;
+  const int hix = hi - j0;
+  int h1c = 0;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const unsigned d = (unsigned)(xb + c);
+    const bool ib = d < (unsigned)wd, ib2 = d <= (unsigned)wd;
+    if (c > 0) f = max(max(f - e_ins, A[c - 1]), 0);
+    const int h = max(max(M[c], s.ee[c]), f);
+    hm[c] = ib ? h : 0;
+    const int en = usat32(max(s.ee[c], M[c] - o_del), e_del);
+    lk = max(lk, hm[c] * 8 + c);
+    s.ee[c] = ib ? en : (ib2 ? 0 : s.ee[c]);
+    if (c > 0) {
+      s.hh[c] = ib2 ? hm[c - 1] : s.hh[c];
+      h1c = hix == c ? hm[c - 1] : h1c;
+    }
+  }
+  const int hs0 = dpp<DPP_ROW_SHR(1)>(left0, hm[CPL - 1]);  // H(i, j0-1); group lane 0: left0
+  s.hh[0] = (unsigned)xb <= (unsigned)wd ? hs0 : s.hh[0];
+  h1c = hix == 0 ? hs0 : h1c;
+  // band trim for the next row: non-zero columns of the updated state
+  uint32_t nzm = 0;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) nzm |= (uint32_t)min((uint32_t)(s.hh[c] | s.ee[c]), 1u) << c;
+  const int lo_l = min(max(lo - j0, 0), 31), hi_l = min(max(hi - j0, 0), 31);
+  const uint32_t below_lo = (1u << lo_l) - 1u, below_hi = (1u << hi_l) - 1u;
+  const uint32_t at_hi = (hi_l == hi - j0) ? (1u << hi_l) : 0u;
+  const uint32_t mf = nzm & below_hi & ~below_lo;   // [lo, hi)
+  const uint32_t ml = mf | (nzm & at_hi);            // [lo, hi]
+  const int fcand = mf ? j0 + __builtin_ctz(mf) : 1 << 20;
+  const int lcand = ml ? j0 + 31 - __builtin_clz(ml) : -1;
+  const int key = ((lk >> 3) << 10) | (j0 + (lk & 7));
+  const int rk = g16_max(key);
+  const int h1 = g16_max(h1c);
+  const int nlo = min(g16_min(fcand), hi);
+  const int jl = max(g16_max(lcand), nlo - 1);
+  const int nhi = min(jl + 2, s.qlen);
+  s.cells += wd;
+  {  // ksw.c:450-453
+    const bool atend = max(lo, hi) == s.qlen;
+    s.ei = (atend && !(s.esc > h1)) ? s.vi : s.ei;
+    s.esc = atend ? max(s.esc, h1) : s.esc;
+  }
+  // ksw.c:454-465 (see extend_wave: updates before the single exit test)
+  const int mrow = rk >> 10, mj = rk & 1023;
+  const bool up = mrow > s.best;
+  const int di = s.vi - s.bi, dj = mj - s.bj;
+  const int drop = s.best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
+  const bool brk = mrow == 0 || (!up && s.zdrop > 0 && drop > s.zdrop);
+  s.off = up ? max(s.off, abs(mj - s.vi)) : s.off;
+  s.best = up ? mrow : s.best;
+  s.bi = up ? s.vi : s.bi;
+  s.bj = up ? mj : s.bj;
+  s.vi += 1;
+  s.lo = nlo;
+  s.hi = nhi;
+  return brk || s.vi >= s.tlen;
+}
+
+template <int CPL, bool T5>
+__device__ __forceinline__ ExtOut gext_out(const GrpExt<CPL, T5>& s) {
+  return ExtOut{s.best, s.bj + 1, s.bi + 1, s.ei + 1, s.esc, s.off};
+}
+
 // rows that extend_group can read for (qlen, w, end_bonus)
 __device__ __forceinline__ int rows_needed(const DevOpt& o, int qlen, int tlen, int w, int end_bonus) {
   int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, o.e_ins);
@@ -1232,6 +1412,72 @@ __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_e
   block_stats<G>(tl, stats);
 }
 
+// bare task list, 16-lane groups: each group takes tasks li, li + NG, ... and
+// the wave runs the rows of its four groups together until one of them
+// finishes; a finished group stores its result and starts its next task while
+// the others wait (the only divergent section).
+template <int CPL, bool T5>
+__global__ void __launch_bounds__(kBlock) extend_grp_kernel(DevOpt o, const bwagpu_ext_task_t* __restrict__ tasks,
+                                                            const int32_t* __restrict__ task_list, int32_t n_list,
+                                                            const uint8_t* __restrict__ qpool,
+                                                            const uint8_t* __restrict__ tpool, int tb_bytes,
+                                                            bwagpu_ext_result_t* res, int64_t* stats) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int GPB = kBlock / 16;
+  const int gib = (int)(threadIdx.x >> 4);
+  const int r = (int)(threadIdx.x & 15);
+  const int NG = (int)gridDim.x * GPB;
+  const uint32_t tb = (uint32_t)(gib * tb_bytes);
+  int li = (int)blockIdx.x * GPB + gib;
+  long long cells = 0, rows = 0, calls = 0;
+  GrpExt<CPL, T5> s;
+  int k = -1;
+  bool act = false;
+  for (;;) {
+    // groups without a task take the next one (tasks with nothing to do are
+    // answered right here)
+    while (!act && li < n_list) {
+      k = task_list[li];
+      const bwagpu_ext_task_t t = tasks[k];
+      if (t.h0 <= 0 || t.tlen == 0) {
+        // h0 <= 0: the reference asserts (ksw.c:385); tlen == 0: no rows
+        const bwagpu_ext_result_t z = t.h0 <= 0 ? bwagpu_ext_result_t{-1, 0, 0, 0, -1, 0}
+                                                : bwagpu_ext_result_t{t.h0, 0, 0, 0, -1, 0};
+        if (r == 0) res[k] = z;
+        calls += t.h0 > 0;
+        li += NG;
+        continue;
+      }
+      const int nr = rows_needed(o, t.qlen, t.tlen, t.w, t.end_bonus);
+      const uint8_t* tp = tpool + t.toff;
+      for (int base = 0; base < nr; base += 16) lds[tb + min(base + r, nr - 1)] = tp[min(base + r, nr - 1)];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint8_t* q = qpool + t.qoff;
+      gext_init(s, o, r, t.qlen, [&](int j) { return (int)q[j]; }, t.tlen, tb, lds, t.w, t.end_bonus, t.zdrop,
+                t.h0);
+      act = true;
+    }
+    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+    bool fin = false;
+    do {
+      if (act) fin = gext_row(s, o, r, lds);
+    } while (__builtin_amdgcn_ballot_w64(act && fin) == 0);
+    if (act && fin) {
+      const ExtOut x = gext_out(s);
+      if (r == 0) res[k] = bwagpu_ext_result_t{x.score, x.qle, x.tle, x.gtle, x.gscore, x.max_off};
+      cells += s.cells;
+      rows += s.vi;
+      calls += 1;
+      act = false;
+      li += NG;
+    }
+  }
+  Tally tl{r == 0 ? cells : 0, r == 0 ? rows : 0, r == 0 ? calls : 0};
+  block_stats<64>(tl, stats);
+}
+
 // ------------------------------------------------------------ launchers
 hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, ChainWin* win, uint64_t* srt,
                              bwagpu_seed_t* prog, int64_t* stats, hipStream_t st) {
@@ -1295,6 +1541,32 @@ static hipError_t launch_ext_t(const DevOpt& o, const bwagpu_ext_task_t* tasks, 
   hipLaunchKernelGGL((extend_kernel<G, C, T5>), dim3(nb), dim3(kBlock), (size_t)GPB * tb, st, o, tasks, list, n,
                      qp, tp, tb, res, stats);
   return hipGetLastError();
+}
+
+template <int CPL, bool T5>
+static hipError_t launch_ext_grp_t(const DevOpt& o, const bwagpu_ext_task_t* tasks, const int32_t* list, int32_t n,
+                                   const uint8_t* qp, const uint8_t* tp, int tb, bwagpu_ext_result_t* res,
+                                   int64_t* stats, hipStream_t st) {
+  constexpr int GPB = kBlock / 16;
+  const size_t lds = (size_t)GPB * tb;
+  const int cap = resident_blocks(extend_grp_kernel<CPL, T5>, lds);
+  const int nb = std::min((n + GPB - 1) / GPB, cap);
+  hipLaunchKernelGGL((extend_grp_kernel<CPL, T5>), dim3(nb), dim3(kBlock), lds, st, o, tasks, list, n, qp, tp, tb,
+                     res, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_extend_grp(int cpl, bool t5, const DevOpt& o, const bwagpu_ext_task_t* tasks,
+                             const int32_t* task_list, int32_t n_list, const uint8_t* qpool, const uint8_t* tpool,
+                             int tb_bytes, bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st) {
+  if (n_list == 0) return hipSuccess;
+  if (cpl == 4)
+    return t5 ? launch_ext_grp_t<4, true>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st)
+              : launch_ext_grp_t<4, false>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st);
+  if (cpl == 8)
+    return t5 ? launch_ext_grp_t<8, true>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st)
+              : launch_ext_grp_t<8, false>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t, const bwagpu_ext_task_t* tasks,
