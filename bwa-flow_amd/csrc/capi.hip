@@ -353,17 +353,18 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   HIPC(s.d_lists.ensure(2 * sizeof(int32_t) * nr), "hipMalloc(lists)");
   int32_t* bins = s.d_lists.as<int32_t>();
   int32_t* read_list = bins + nr;
-  // [0..15] per-variant read counts, [16 + 8v + xcc] queue heads (generic
-  // kernel), [64 .. 64 + 3*256) read-order histogram
-  constexpr size_t kCountWords = 64 + 3 * 256;
   HIPC(s.d_counts.ensure(sizeof(int32_t) * kCountWords), "hipMalloc(counts)");
   HIPC(hipMemsetAsync(s.d_counts.p, 0, sizeof(int32_t) * kCountWords, st), "memset counts");
   if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
   HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(),
                          s.d_prog.as<bwagpu_seed_t>(), d_stats, st),
        "chain_prep launch");
-  HIPC(launch_read_order(db, bins, s.d_counts.as<int32_t>() + 64, s.d_counts.as<int32_t>(), s.d_desc.as<ReadDesc>(),
-                         read_list, d_stats, st),
+  // BWAGPU_C2A_GRP=1: the 16-lane group kernels for reads <= 256 bp instead of
+  // the wave-per-read kernels (bit-identical; slower on C2 — DESIGN.md §3)
+  const char* eg = getenv("BWAGPU_C2A_GRP");
+  const bool grp = eg && eg[0] == '1';
+  HIPC(launch_read_order(db, bins, s.d_counts.as<int32_t>() + kHistOff, s.d_counts.as<int32_t>(),
+                         s.d_desc.as<ReadDesc>(), read_list, d_stats, grp, st),
        "read order launch");
   C2AArgs a;
   a.read_list = read_list;
@@ -376,10 +377,13 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   a.out_n = d_n;
   a.stats = d_stats;
   for (int v = 0; v < kNumVariants; ++v) {
-    const int lqv = std::min(lq_max, kVariants[v].max_len());
+    const Variant& vk = kVariants[v];
+    if ((vk.kind == VK_GRP) != grp && vk.kind != VK_GENERIC) continue;  // gets no reads
+    const int lqv = std::min(lq_max, vk.kind == VK_GRP ? 256 : vk.max_len());
     const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
-    const size_t lds = kVariants[v].fast ? (size_t)(kBlock / 64) * fast_wave_lds(tb)
-                                         : (size_t)tb * (kBlock / kVariants[v].G);
+    const size_t lds = vk.kind == VK_FAST  ? (size_t)(kBlock / 64) * fast_wave_lds(tb)
+                       : vk.kind == VK_GRP ? (size_t)(kBlock / 16) * grp_group_lds(tb)
+                                           : (size_t)tb * (kBlock / vk.G);
     if (lds > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
     HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, db.n_reads, tb, a, st), "chain2aln launch");
   }
@@ -604,10 +608,10 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   if (n == 0) return BWAGPU_OK;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   // validate and bin on the host
-  // bins: [0, kNumVariants) wave kernels, then the 16-lane-group kernels
+  // bins: [0, kNumExtVariants) wave kernels, then the 16-lane-group kernels
   // (CPL 4, 8); BWAGPU_EXT_WAVE=1 keeps every task on the wave kernels (A/B)
   constexpr int kGrpBins = 2;
-  std::vector<int32_t> lists[kNumVariants + kGrpBins];
+  std::vector<int32_t> lists[kNumExtVariants + kGrpBins];
   const char* ew = getenv("BWAGPU_EXT_WAVE");
   const bool grp = !(ew && ew[0] == '1');
   bool t5 = false;
@@ -617,12 +621,12 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
     if (t.qlen < 0 || t.tlen < 0 || t.qoff < 0 || t.toff < 0 || t.qoff + t.qlen > qpool_len ||
         t.toff + t.tlen > tpool_len || t.w < 0)
       return fail(ctx, BWAGPU_E_INVAL, "task outside its pools");
-    if (t.qlen + 1 > kVariants[kNumVariants - 1].max_len()) return fail(ctx, BWAGPU_E_UNSUPPORTED, "qlen too long");
-    int v = kNumVariants - 1;
-    for (int i = kNumVariants - 1; i >= 0; --i)
-      if (t.qlen + 1 <= kVariants[i].max_len()) v = i;
-    if (grp && t.qlen + 1 <= 64) v = kNumVariants;
-    else if (grp && t.qlen + 1 <= 128) v = kNumVariants + 1;
+    if (t.qlen + 1 > kExtVariants[kNumExtVariants - 1].max_len()) return fail(ctx, BWAGPU_E_UNSUPPORTED, "qlen too long");
+    int v = kNumExtVariants - 1;
+    for (int i = kNumExtVariants - 1; i >= 0; --i)
+      if (t.qlen + 1 <= kExtVariants[i].max_len()) v = i;
+    if (grp && t.qlen + 1 <= 64) v = kNumExtVariants;
+    else if (grp && t.qlen + 1 <= 128) v = kNumExtVariants + 1;
     lists[v].push_back(k);
     lq_max = std::max(lq_max, t.qlen + 1);
   }
@@ -662,9 +666,9 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   (void)hipEventRecord(e0, st);
   int32_t off = 0;
   std::vector<int32_t> all;
-  for (int v = 0; v < kNumVariants + kGrpBins; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
+  for (int v = 0; v < kNumExtVariants + kGrpBins; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
   if ((rc = ck(hipMemcpyAsync(d_list.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D"))) return rc;
-  for (int v = 0; v < kNumVariants + kGrpBins; ++v) {
+  for (int v = 0; v < kNumExtVariants + kGrpBins; ++v) {
     const int32_t nv = (int32_t)lists[v].size();
     if (nv) {
       int rows = 16;
@@ -676,17 +680,17 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
         rows = std::max(rows, std::min(t.tlen, t.qlen + we + 1));
       }
       const int tb = (rows + 2 + 15) & ~15;
-      const int gpb = v < kNumVariants ? kBlock / kVariants[v].G : kBlock / 16;
+      const int gpb = v < kNumExtVariants ? kBlock / kExtVariants[v].G : kBlock / 16;
       if ((size_t)tb * gpb > 64 * 1024) {
         cleanup();
         return fail(ctx, BWAGPU_E_UNSUPPORTED, "task needs too many LDS rows");
       }
       hipError_t e =
-          v < kNumVariants
+          v < kNumExtVariants
               ? launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off, nv,
                               d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
                               d_stats.as<int64_t>(), st)
-              : launch_extend_grp(v == kNumVariants ? 4 : 8, t5, ctx->opt, d_tasks.as<bwagpu_ext_task_t>(),
+              : launch_extend_grp(v == kNumExtVariants ? 4 : 8, t5, ctx->opt, d_tasks.as<bwagpu_ext_task_t>(),
                                   d_list.as<int32_t>() + off, nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb,
                                   d_res.as<bwagpu_ext_result_t>(), d_stats.as<int64_t>(), st);
       if ((rc = ck(e, "extend launch"))) return rc;

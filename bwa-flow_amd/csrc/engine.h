@@ -64,17 +64,26 @@ enum { ERR_RID = 1, ERR_LEN = 2 };
 
 // Kernel variants: G lanes per read ("group"), C = max DP columns per lane.
 // A read of length l needs G*C >= l (+1 column for eh[qlen], qlen <= l-1).
+enum { VK_FAST = 0, VK_GENERIC = 1, VK_GRP = 2 };
 struct Variant {
   int G, C;
-  bool fast;  // chain2aln_fast_kernel (register-resident read) vs the generic kernel
-  int max_len() const { return G * C; }
+  int kind;  // VK_GRP: chain2aln_grp_kernel (16-lane groups, columns = longest extension)
+             // VK_FAST: chain2aln_fast_kernel (wave per read), VK_GENERIC: chain2aln_kernel
+  __host__ __device__ int max_len() const { return G * C; }
 };
-// limits of the fast kernel: one lane per seed / chain / region of a read
+// limits of the fast and group kernels: one lane (slot) per seed / chain / region of a read
 constexpr int kFastMaxSeeds = 32;
 constexpr int kFastMaxChains = 32;
 constexpr int kSeqLds = 256;  // LDS bytes for the read's bases (fast variants: lq <= 256)
-constexpr int kNumVariants = 3;
+constexpr int kNumVariants = 7;
 extern const Variant kVariants[kNumVariants];
+// bare ksw_extend2 task lists (bwagpu_extend_batch): wave kernels by columns
+constexpr int kNumExtVariants = 3;
+extern const Variant kExtVariants[kNumExtVariants];
+// read-order counters: [0..15] per-variant counts, [16 + 8v + xcc] queue heads
+// (generic kernel), [kHistOff ..) the read-order histogram
+constexpr int kHistOff = 128;
+constexpr int kCountWords = kHistOff + kNumVariants * 256;
 constexpr int kBlock = 256;  // threads per workgroup (4 waves)
 
 // host-side launchers (sw_kernels.hip)
@@ -84,7 +93,7 @@ hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch&
 // writes read_list[pos] and desc[pos] (bins: n_reads scratch, hist: 3*256
 // zeroed counters, counts: per-variant read counts)
 hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, int32_t* counts, ReadDesc* desc,
-                             int32_t* list, int64_t* stats, hipStream_t st);
+                             int32_t* list, int64_t* stats, bool grp, hipStream_t st);
 // read_list: reads sorted by key; d_count: per-variant counts (device); the
 // variant's reads start at the sum of the lower variants' counts; max_list
 // bounds the grid
@@ -104,6 +113,8 @@ hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, con
                             int tb_bytes, const C2AArgs& a, hipStream_t st);
 // LDS bytes per wave of chain2aln_fast_kernel for target row buffers of tb bytes
 size_t fast_wave_lds(int tb);
+// LDS bytes per 16-lane group of chain2aln_grp_kernel
+size_t grp_group_lds(int tb);
 
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,

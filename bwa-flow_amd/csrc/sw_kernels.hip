@@ -38,7 +38,9 @@
 
 namespace bwagpu {
 
-const Variant kVariants[kNumVariants] = {{64, 3, true}, {64, 4, true}, {64, 16, false}};
+const Variant kVariants[kNumVariants] = {{16, 4, VK_GRP},  {16, 8, VK_GRP},  {16, 10, VK_GRP},   {16, 16, VK_GRP},
+                                         {64, 3, VK_FAST}, {64, 4, VK_FAST}, {64, 16, VK_GENERIC}};
+const Variant kExtVariants[kNumExtVariants] = {{64, 3, VK_FAST}, {64, 4, VK_FAST}, {64, 16, VK_GENERIC}};
 
 // wave-uniform max of a group-uniform value over the wave's ACTIVE groups (for
 // loop bounds every active group of the wave can share: a scalar branch
@@ -373,7 +375,7 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
 //    lane 0 of the group injects the first-column value left0, ksw.c:420-423);
 //    the reference's eh[hi] = {h1, 0} write (ksw.c:449) is the same update
 //    applied to column hi with E cleared, so [lo, hi] is updated in one rule;
-//  * row max + LAST argmax: group max of (H << 10 | j), in-lane as H*8 + c;
+//  * row max + LAST argmax: group max of (H << 10 | j), in-lane as H << KS | c;
 //  * band trim (ksw.c:466-469): per-lane bitmask of non-zero columns, first
 //    column in [lo, hi) by a group min, last in [lo, hi] by a group max.
 template <int CPL, bool T5>
@@ -430,6 +432,7 @@ __device__ __forceinline__ void gext_init(GrpExt<CPL, T5>& s, const DevOpt& o, i
 template <int CPL, bool T5>
 __device__ __forceinline__ bool gext_row(GrpExt<CPL, T5>& s, const DevOpt& o, int r, const uint8_t* lds) {
   const int e_del = o.e_del, e_ins = o.e_ins, o_del = o.o_del, oe_ins = o.oe_ins;
+  constexpr int KS = CPL > 8 ? 4 : 3;  // bits of the in-lane column in the row-max key
   const int j0 = r * CPL;
   const int t = s.tnext;
   s.tnext = lds[s.tb + s.vi + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
@@ -478,7 +481,7 @@ __device__ __forceinline__ bool gext_row(GrpExt<CPL, T5>& s, const DevOpt& o, in
     const int h = max(max(M[c], s.ee[c]), f);
     hm[c] = ib ? h : 0;
     const int en = usat32(max(s.ee[c], M[c] - o_del), e_del);
-    lk = max(lk, hm[c] * 8 + c);
+    lk = max(lk, (hm[c] << KS) + c);
     s.ee[c] = ib ? en : (ib2 ? 0 : s.ee[c]);
     if (c > 0) {
       s.hh[c] = ib2 ? hm[c - 1] : s.hh[c];
@@ -499,7 +502,7 @@ __device__ __forceinline__ bool gext_row(GrpExt<CPL, T5>& s, const DevOpt& o, in
   const uint32_t ml = mf | (nzm & at_hi);            // [lo, hi]
   const int fcand = mf ? j0 + __builtin_ctz(mf) : 1 << 20;
   const int lcand = ml ? j0 + 31 - __builtin_clz(ml) : -1;
-  const int key = ((lk >> 3) << 10) | (j0 + (lk & 7));
+  const int key = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
   const int rk = g16_max(key);
   const int h1 = g16_max(h1c);
   const int nlo = min(g16_min(fcand), hi);
@@ -699,18 +702,32 @@ __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, D
 constexpr int kCostBins = 256;
 constexpr int kBins = kNumVariants * kCostBins;
 
-__device__ __forceinline__ int read_variant(const DevBatch& b, int rd, int lq) {
+// grp: the 16-lane group kernel, sized by the read's longest possible
+// extension (max over its seeds of qbeg, lq - qbeg - len; + 1 column)
+__device__ __forceinline__ int read_variant(const DevBatch& b, int rd, int lq, bool grp) {
   const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
-  const int nseeds = b.chain_seed_off[c1] - b.chain_seed_off[c0];
-  const bool small = nseeds <= kFastMaxSeeds && c1 - c0 <= kFastMaxChains;
-  int v = -1;
-  for (int k = kNumVariants - 1; k >= 0; --k)
-    if (lq <= kVariants[k].G * kVariants[k].C && (small || !kVariants[k].fast)) v = k;
-  return v;
+  const int s0 = b.chain_seed_off[c0], s1 = b.chain_seed_off[c1];
+  const bool small = s1 - s0 <= kFastMaxSeeds && c1 - c0 <= kFastMaxChains;
+  if (grp && small && lq <= 256) {
+    int need = 1;
+    bool ok = true;
+    for (int k = s0; k < s1; ++k) {
+      const bwagpu_seed_t t = b.seeds[k];
+      ok = ok && t.qbeg >= 0 && t.len > 0 && t.qbeg + t.len <= lq;
+      need = max(need, max(t.qbeg, lq - t.qbeg - t.len) + 1);
+    }
+    if (ok)
+      for (int k = 0; k < kNumVariants; ++k)
+        if (kVariants[k].kind == VK_GRP && need <= kVariants[k].max_len()) return k;
+  }
+  for (int k = 0; k < kNumVariants; ++k)
+    if (kVariants[k].kind != VK_GRP && lq <= kVariants[k].max_len() && (small || kVariants[k].kind != VK_FAST))
+      return k;
+  return -1;
 }
 
 __global__ void __launch_bounds__(256) read_bins_kernel(DevBatch b, int32_t* bins, int32_t* hist, int32_t* counts,
-                                                        int64_t* stats) {
+                                                        int64_t* stats, int grp) {
   __shared__ int h[kBins];
   for (int k = threadIdx.x; k < kBins; k += blockDim.x) h[k] = 0;
   __syncthreads();
@@ -718,7 +735,7 @@ __global__ void __launch_bounds__(256) read_bins_kernel(DevBatch b, int32_t* bin
   int v = -1;
   if (rd < b.n_reads) {
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
-    v = read_variant(b, rd, lq);
+    v = read_variant(b, rd, lq, grp != 0);
     const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
     uint32_t cost = 0;
     int nseed = 0;
@@ -812,10 +829,10 @@ __global__ void __launch_bounds__(256) read_scatter_kernel(DevBatch b, const int
 }
 
 hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, int32_t* counts, ReadDesc* desc,
-                             int32_t* list, int64_t* stats, hipStream_t st) {
+                             int32_t* list, int64_t* stats, bool grp, hipStream_t st) {
   if (b.n_reads == 0) return hipSuccess;
   const int nb = (b.n_reads + 255) / 256;
-  hipLaunchKernelGGL(read_bins_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, counts, stats);
+  hipLaunchKernelGGL(read_bins_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, counts, stats, grp ? 1 : 0);
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(256), 0, st, hist);
   hipLaunchKernelGGL(read_scatter_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, desc, list);
   return hipGetLastError();
@@ -1372,6 +1389,417 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
   block_stats<64>(tl, a.stats);
 }
 
+// ------------------------------------------------------------ chain2aln, 16-lane groups
+// mem_chain2aln (bwamem.c:641-795) with FOUR reads per wave, one per 16-lane
+// group (one DPP row).  Each group walks its reads, chains and seeds with its
+// own control state (a small state machine, all values group-uniform VGPRs);
+// whenever a group reaches a ksw_extend2 it parks in the DP, and the wave runs
+// the DP rows of every parked group together (gext_row: blocked columns, 16
+// lanes x CPL).  When one group's extension ends, the wave leaves the row loop,
+// that group runs its control code up to its next extension (the only
+// divergent section) and the row loop resumes.
+//
+// Per-read data lives in registers, two items per lane (lane r holds seeds /
+// chains / regions r and r + 16; a read has at most 32 of each) and is read
+// group-uniformly with ds_bpermute; only the read's bases and the two target
+// row buffers of the current seed sit in LDS (kGrpSeq + 2 * tb bytes per
+// group), so occupancy is set by VGPRs.
+constexpr int kGrpSeq = 272;  // a read's bases (<= 256) from its first aligned dword
+
+__device__ __forceinline__ int gperm(int v0, int v1, int idx, int gbase) {
+  const int v = idx < 16 ? v0 : v1;
+  return __builtin_amdgcn_ds_bpermute((gbase + (idx & 15)) << 2, v);
+}
+__device__ __forceinline__ int64_t gperm64(const int64_t* v, int idx, int gbase) {
+  const int lo = gperm((int)(uint32_t)v[0], (int)(uint32_t)v[1], idx, gbase);
+  const int hi = gperm((int)(uint32_t)((uint64_t)v[0] >> 32), (int)(uint32_t)((uint64_t)v[1] >> 32), idx, gbase);
+  return (int64_t)((uint64_t)(uint32_t)hi << 32 | (uint32_t)lo);
+}
+// any / sum over the 16 lanes of the group
+__device__ __forceinline__ bool gany(bool p, int gbase) {
+  return ((__builtin_amdgcn_ballot_w64(p) >> gbase) & 0xffffull) != 0;
+}
+__device__ __forceinline__ int gsum16(int v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+  return v;
+}
+
+// target rows of the current seed, both sides in one round trip: left rows
+// x0l - k (k < nl) into tbl, right rows x0r + k (k < nr) into tbr.  Lane r
+// takes rows [16r, 16r + 16) of each side per pass: they are 16 consecutive
+// positions of the forward pac (ascending or descending), so two aligned
+// dwords hold them all (bases [16D, 16D + 32), MSB-first per byte as
+// _get_pac, bntseq.c:225); the 16 bytes go to LDS as one 128-bit write.
+// Rows past n are garbage (the buffer is n rounded up to 16 long).
+// A lane whose dword pair would pass the end of the pac buffer (l_pac/4 + 1
+// bytes) reads its rows byte by byte instead.
+__device__ __forceinline__ void fill_side16(uint8_t* tb, int64_t x0, int dir, int n, const DevRef& ref, int r,
+                                            int base) {
+  const int k0 = base + 16 * r;
+  if (k0 >= n) return;
+  const bool rev = x0 >= ref.l_pac;  // a window never spans both strands
+  const int64_t fb = rev ? (ref.l_pac << 1) - 1 - x0 : x0;
+  const int sg = rev ? -dir : dir;
+  const int64_t f0 = sg > 0 ? fb + k0 : fb - k0;  // row k0
+  const int64_t flo = max(sg > 0 ? f0 : f0 - 15, (int64_t)0);
+  const int64_t D = flo >> 4;
+  const int64_t dmax = ((ref.l_pac >> 2) + 1) / 4 - 2;
+  const uint32_t cmask = rev ? 0x03030303u : 0u;  // complement of the reverse strand
+  if (D <= dmax) {
+    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(ref.pac) + D;
+    const uint64_t win64 = (uint64_t)p32[0] | (uint64_t)p32[1] << 32;
+    const int pb = (int)(f0 - 16 * D);
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = (pb + sg * (4 * q + i)) & 31;
+        v |= ((uint32_t)(win64 >> ((p & ~3) * 2 + 6 - 2 * (p & 3))) & 3u) << (8 * i);
+      }
+      w[q] = v ^ cmask;
+    }
+    *reinterpret_cast<uint4*>(tb + k0) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {  // the last bytes of the pac: row by row
+#pragma nounroll
+    for (int j = 0; j < 16; ++j) {
+      int64_t f = f0 + sg * j;
+      f = f < 0 ? 0 : (f >= ref.l_pac ? ref.l_pac - 1 : f);
+      const uint32_t bse = ((uint32_t)ref.pac[f >> 2] >> ((~f & 3) << 1)) & 3u;
+      tb[k0 + j] = (uint8_t)(rev ? 3u - bse : bse);
+    }
+  }
+}
+
+__device__ __forceinline__ void fill_two16(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
+                                           const DevRef& ref, int r) {
+  const int n = max(nl, nr);
+  for (int base = 0; base < n; base += 256) {
+    fill_side16(tbl, x0l, -1, nl, ref, r, base);
+    fill_side16(tbr, x0r, 1, nr, ref, r, base);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+enum { GM_READ = 0, GM_SEED, GM_SIDE, GM_DP, GM_EXTDONE, GM_DONE };
+
+template <int CPL>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) chain2aln_grp_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
+                                                               int variant, int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int GPB = kBlock / 16;
+  const int r = (int)(threadIdx.x & 15);
+  const int gbase = (int)(threadIdx.x & 48);
+  const int gib = (int)(threadIdx.x >> 4);
+  const uint32_t sq_off = (uint32_t)(gib * (kGrpSeq + 2 * tb_bytes));
+  const uint32_t tbl_off = sq_off + kGrpSeq, tbr_off = tbl_off + tb_bytes;
+  int base = 0;
+  for (int v = 0; v < variant; ++v) base += a.counts[v];
+  const int n_list = a.counts[variant];
+  // static zig-zag deal over the resident groups (cost-sorted list: LPT-like)
+  const int NG = (int)gridDim.x * GPB, G = (int)blockIdx.x * GPB + gib;
+  auto pos = [&](int round) { return round * NG + ((round & 1) ? NG - 1 - G : G); };
+  long long t_cells = 0, t_rows = 0, t_calls = 0;
+  // scalars picked by side are read into locals first: a select between two
+  // fields of `o` would make the compiler copy the struct to scratch
+  const int pc5 = o.pen_clip5, pc3 = o.pen_clip3, ow = o.w, oa = o.a;
+
+  // ---- group state (group-uniform)
+  int mode = GM_READ, round = 0;
+  int rd = 0, lq = 0, nch = 0, s0 = 0, qa0 = 0;  // qa0: LDS offset of base 0 of the read
+  // the read's seeds (processing order) / chains / regions, two per lane
+  int64_t Srb[2] = {0, 0}, Clo[2] = {0, 0}, Chi[2] = {0, 0}, Rrb[2] = {0, 0}, Rre[2] = {0, 0};
+  int Sx[2] = {0, 0}, Ccs[2] = {0, 0}, Crid[2] = {0, 0}, Cfr[2] = {0, 0}, Rq[2] = {0, 0}, Rw[2] = {0, 0};
+  int c = 0, cs0 = 0, cs1 = 0, e = 0, nreg = 0, rid = 0, frac = 0;
+  uint32_t skipped = 0;
+  int64_t clo = 0, chi = 0, srb = 0, rb = 0, re = 0;
+  int sqb = 0, slen = 0, side = 0, t = 0, score = 0, truesc = 0, qb = 0, qe = 0, sc0 = 0, prev = 0, aw0 = 0, aw1 = 0;
+  GrpExt<CPL, false> s;
+
+  // start the extension of the current side (try t); tlen == 0 ends at once
+  auto start_ext = [&]() {
+    const bool left = side == 0;
+    const int qlen = left ? sqb : lq - sqb - slen;
+    const int64_t x0 = left ? srb - 1 : srb + slen;
+    const int tlen = (int)(left ? srb - clo : chi - x0);
+    const int qa = qa0 + (left ? sqb - 1 : sqb + slen);
+    const int dir = left ? -1 : 1;
+    const int h0 = left ? slen * oa : sc0;  // sc0: the score before this side (a retry keeps h0)
+    const int w = ow << t;
+    aw0 = left ? w : aw0;  // value selects: a conditional lvalue would keep these in scratch
+    aw1 = left ? aw1 : w;
+    gext_init(s, o, r, qlen, [&](int j) { return (int)lds[qa + dir * j]; }, tlen, left ? tbl_off : tbr_off, lds, w,
+              left ? pc5 : pc3, o.zdrop, h0);
+    mode = tlen > 0 ? GM_DP : GM_EXTDONE;
+  };
+
+#ifdef BWAGPU_GRP_STATS
+  // diagnostics: wave time in control vs DP rows, row iterations, group-rows
+  uint64_t st_ctrl = 0, st_dp = 0, st_it = 0, st_gr = 0;
+#endif
+  for (;;) {
+#ifdef BWAGPU_GRP_STATS
+    const uint64_t tc0 = __builtin_amdgcn_s_memtime();
+#endif
+    // ---- control: every group that is not in the DP runs to its next extension
+    while (mode != GM_DP && mode != GM_DONE) {
+      if (mode == GM_READ) {
+        const int p = pos(round);
+        if (p >= n_list) {
+          mode = GM_DONE;
+          break;
+        }
+        ++round;
+        const ReadDesc d = a.desc[base + p];
+        rd = d.rd;
+        lq = d.lq;
+        nch = d.nch;
+        s0 = d.s0;
+        const int ns = d.ns;
+        nreg = 0;
+        skipped = 0;
+        if (ns == 0) {
+          if (r == 0) a.out_n[rd] = 0;
+          continue;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int i = r + 16 * k;
+          const bwagpu_seed_t sd = a.prog[s0 + min(i, ns - 1)];
+          Srb[k] = sd.rbeg;
+          Sx[k] = sd.qbeg | sd.len << 9 | (sd.pad_ ? 1 << 18 : 0);
+          const int cc = d.c0 + min(i, nch - 1);
+          Ccs[k] = (b.chain_seed_off[cc] - s0) | (b.chain_seed_off[cc + 1] - s0) << 8;
+          const ChainWin wn = a.win[cc];
+          Clo[k] = wn.lo;
+          Chi[k] = wn.hi;
+          Crid[k] = b.chain_rid[cc];
+          Cfr[k] = __float_as_int(b.chain_frac_rep[cc]);
+        }
+        {  // the read's bases, by aligned dwords
+          const uint32_t* q = reinterpret_cast<const uint32_t*>(b.seq) + (d.qoff >> 2);
+          const int ndw = (int)(((d.qoff & 3) + lq + 3) >> 2);
+          uint32_t* sq = reinterpret_cast<uint32_t*>(lds + sq_off);
+          for (int k = r; k < ndw; k += 16) sq[k] = q[k];
+          qa0 = (int)sq_off + (int)(d.qoff & 3);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        c = -1;
+        e = cs1 = 0;
+        mode = GM_SEED;
+      } else if (mode == GM_SEED) {
+        if (e >= cs1) {  // next chain
+          ++c;
+          if (c >= nch) {
+            if (r == 0) a.out_n[rd] = nreg;
+            mode = GM_READ;
+            continue;
+          }
+          const int cs = gperm(Ccs[0], Ccs[1], c, gbase);
+          cs0 = cs & 0xff;
+          cs1 = cs >> 8;
+          e = cs0;
+          clo = gperm64(Clo, c, gbase);
+          chi = gperm64(Chi, c, gbase);
+          if (chi < clo) e = cs1;  // flagged by prep (the reference would assert)
+          rid = gperm(Crid[0], Crid[1], c, gbase);
+          frac = gperm(Cfr[0], Cfr[1], c, gbase);
+          continue;
+        }
+        srb = gperm64(Srb, e, gbase);
+        {
+          const int x = gperm(Sx[0], Sx[1], e, gbase);
+          sqb = x & 511;
+          slen = (x >> 9) & 511;
+        }
+        if (nreg > 0) {
+          // containment in an existing region (bwamem.c:678-697), regions r, r + 16
+          bool hit = false;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int R_qb = Rq[k] & 511, R_qe = (Rq[k] >> 9) & 511, R_sl = (Rq[k] >> 18) & 511, R_w = Rw[k];
+            const int64_t R_rb = Rrb[k], R_re = Rre[k];
+            const bool inside = !(srb < R_rb || srb + slen > R_re || sqb < R_qb || sqb + slen > R_qe) &&
+                                !(slen - R_sl > .1 * lq);
+            const int qd1 = sqb - R_qb;
+            const int64_t rd1 = srb - R_rb;
+            const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
+            const int bw1 = g1 < R_w ? g1 : R_w;
+            const int qd2 = R_qe - (sqb + slen);
+            const int64_t rd2 = R_re - (srb + slen);
+            const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
+            const int bw2 = g2 < R_w ? g2 : R_w;
+            const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+            hit = hit || (r + 16 * k < nreg && inside && near);
+          }
+          if (gany(hit, gbase)) {
+            // an overlapping seed among those already visited (bwamem.c:698-707), seeds r, r + 16
+            bool ov = false;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const int i = r + 16 * k;
+              const int p_qb = Sx[k] & 511, p_len = (Sx[k] >> 9) & 511, p_flag = Sx[k] >> 18;
+              const int64_t p_rb = Srb[k];
+              const bool a1 = sqb <= p_qb && sqb + slen - p_qb >= slen >> 2 && (int64_t)(p_qb - sqb) != p_rb - srb;
+              const bool b1 = p_qb <= sqb && p_qb + p_len - sqb >= slen >> 2 && (int64_t)(sqb - p_qb) != srb - p_rb;
+              const bool live = i >= cs0 && i < e && !((skipped >> i) & 1u) && p_flag == 0;
+              ov = ov || (live && !(p_len < slen * .95) && (a1 || b1));
+            }
+            if (!gany(ov, gbase)) {
+              skipped |= 1u << e;
+              ++e;
+              continue;
+            }
+          }
+        }
+        // ---- extend (bwamem.c:717-792); both target windows in one round trip
+        {
+          const int qlenL = sqb, qlenR = lq - (sqb + slen);
+          const int64_t x0L = srb - 1, x0R = srb + slen;
+          const int tlenL = (int)(srb - clo), tlenR = (int)(chi - x0R);
+          fill_two16(lds + tbl_off, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0,
+                     lds + tbr_off, x0R, qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref, r);
+        }
+        score = truesc = -1;
+        qb = 0;
+        qe = lq;
+        sc0 = 0;
+        aw0 = aw1 = o.w;
+        rb = srb;
+        re = srb + slen;
+        side = 0;
+        mode = GM_SIDE;
+      } else if (mode == GM_SIDE) {
+        if (side == 0 && sqb == 0) {  // bwamem.c:753
+          score = truesc = slen * o.a;
+          side = 1;
+          continue;
+        }
+        if (side == 1 && lq - sqb - slen == 0) side = 2;  // bwamem.c:781
+        if (side == 2) {
+          // seedcov over the chain's seeds (bwamem.c:784-788), seeds r, r + 16
+          int cov = 0;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int i = r + 16 * k;
+            const int p_qb = Sx[k] & 511, p_len = (Sx[k] >> 9) & 511;
+            const int64_t p_rb = Srb[k];
+            const bool in =
+                i >= cs0 && i < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
+            cov += in ? p_len : 0;
+          }
+          cov = gsum16(cov);
+          // the region as its 88-byte record (rest zero: bwamem.c:718), lane r: dwords r, r + 16
+          const int wmax = aw0 > aw1 ? aw0 : aw1;
+          uint32_t* const dst = reinterpret_cast<uint32_t*>(a.out + s0 + nreg);
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int dw = r + 16 * k;
+            uint32_t v = 0;
+            v = dw == 0 ? (uint32_t)rb : v;
+            v = dw == 1 ? (uint32_t)((uint64_t)rb >> 32) : v;
+            v = dw == 2 ? (uint32_t)re : v;
+            v = dw == 3 ? (uint32_t)((uint64_t)re >> 32) : v;
+            v = dw == 4 ? (uint32_t)qb : v;
+            v = dw == 5 ? (uint32_t)qe : v;
+            v = dw == 6 ? (uint32_t)rid : v;
+            v = dw == 7 ? (uint32_t)score : v;
+            v = dw == 8 ? (uint32_t)truesc : v;
+            v = dw == 13 ? (uint32_t)wmax : v;
+            v = dw == 14 ? (uint32_t)cov : v;
+            v = dw == 17 ? (uint32_t)slen : v;
+            v = dw == 19 ? (uint32_t)frac : v;
+            if (dw < 22) dst[dw] = v;
+          }
+          // the containment fields of region nreg, kept by lane nreg & 15
+          if (r == (nreg & 15)) {
+            const int k = nreg >> 4;
+            const int q = qb | qe << 9 | slen << 18;
+            Rrb[0] = k == 0 ? rb : Rrb[0];
+            Rrb[1] = k == 1 ? rb : Rrb[1];
+            Rre[0] = k == 0 ? re : Rre[0];
+            Rre[1] = k == 1 ? re : Rre[1];
+            Rq[0] = k == 0 ? q : Rq[0];
+            Rq[1] = k == 1 ? q : Rq[1];
+            Rw[0] = k == 0 ? wmax : Rw[0];
+            Rw[1] = k == 1 ? wmax : Rw[1];
+          }
+          ++nreg;
+          ++e;
+          mode = GM_SEED;
+          continue;
+        }
+        sc0 = score;
+        t = 0;
+        prev = score;
+        start_ext();
+      } else {  // GM_EXTDONE
+        const ExtOut x = gext_out(s);
+        t_cells += s.cells;
+        t_rows += s.vi;
+        t_calls += 1;
+        score = x.score;
+        const int aw = side == 0 ? aw0 : aw1;
+        if (t == 0 && !(score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {  // MAX_BAND_TRY (bwamem.c:639)
+          t = 1;
+          prev = score;
+          start_ext();
+          continue;
+        }
+        const bool left = side == 0;
+        const int eb = left ? pc5 : pc3;
+        const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+        if (left) {
+          qb = local ? sqb - x.qle : 0;
+          rb = srb - (local ? x.tle : x.gtle);
+          truesc = local ? score : x.gscore;
+        } else {
+          qe = local ? sqb + slen + x.qle : lq;
+          re = srb + slen + (local ? x.tle : x.gtle);
+          truesc += (local ? score : x.gscore) - sc0;
+        }
+        ++side;
+        mode = GM_SIDE;
+      }
+    }
+    // ---- the DP rows of every parked group, together
+#ifdef BWAGPU_GRP_STATS
+    const uint64_t tc1 = __builtin_amdgcn_s_memtime();
+    st_ctrl += tc1 - tc0;
+#endif
+    if (__builtin_amdgcn_ballot_w64(mode == GM_DP) == 0) break;
+    bool fin = false;
+    do {
+#ifdef BWAGPU_GRP_STATS
+      st_it += 1;
+      st_gr += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == GM_DP)) >> 4;
+#endif
+      if (mode == GM_DP) fin = gext_row(s, o, r, lds);
+    } while (__builtin_amdgcn_ballot_w64(mode == GM_DP && fin) == 0);
+    if (mode == GM_DP && fin) mode = GM_EXTDONE;
+#ifdef BWAGPU_GRP_STATS
+    st_dp += __builtin_amdgcn_s_memtime() - tc1;
+#endif
+  }
+#ifdef BWAGPU_GRP_STATS
+  if (g_trace && (threadIdx.x & 63) == 0) {
+    atomicAdd(&g_trace[8 * CPL + 0], (uint32_t)(st_ctrl >> 8));
+    atomicAdd(&g_trace[8 * CPL + 1], (uint32_t)(st_dp >> 8));
+    atomicAdd(&g_trace[8 * CPL + 2], (uint32_t)st_it);
+    atomicAdd(&g_trace[8 * CPL + 3], (uint32_t)st_gr);
+    atomicAdd(&g_trace[8 * CPL + 4], 1u);
+  }
+#endif
+  Tally tl{r == 0 ? t_cells : 0, r == 0 ? t_rows : 0, r == 0 ? t_calls : 0};
+  block_stats<64>(tl, a.stats);
+}
+
 // ------------------------------------------------------------ extend batch
 template <int G, int C, bool T5>
 __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_ext_task_t* __restrict__ tasks,
@@ -1521,13 +1949,30 @@ static hipError_t launch_c2a_t(const DevOpt& o, const DevRef& ref, const DevBatc
   return hipGetLastError();
 }
 
+size_t grp_group_lds(int tb) { return (size_t)(kGrpSeq + 2 * tb); }
+
+template <int CPL>
+static hipError_t launch_c2a_grp(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n,
+                                 int tb, const C2AArgs& a, hipStream_t st) {
+  constexpr int GPB = kBlock / 16;
+  const size_t lds = (size_t)GPB * grp_group_lds(tb);
+  const int cap = resident_blocks(chain2aln_grp_kernel<CPL>, lds);
+  const int nb = std::min((n + GPB - 1) / GPB, cap);
+  hipLaunchKernelGGL((chain2aln_grp_kernel<CPL>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, variant, tb);
+  return hipGetLastError();
+}
+
 hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b, int32_t max_list,
                             int tb_bytes, const C2AArgs& a, hipStream_t st) {
   if (max_list == 0) return hipSuccess;
   switch (variant) {
-    case 0: return launch_c2a_fast<3>(o, ref, b, 0, max_list, tb_bytes, a, st);
-    case 1: return launch_c2a_fast<4>(o, ref, b, 1, max_list, tb_bytes, a, st);
-    case 2: return launch_c2a_t<64, 16>(o, ref, b, 2, max_list, tb_bytes, a, st);
+    case 0: return launch_c2a_grp<4>(o, ref, b, 0, max_list, tb_bytes, a, st);
+    case 1: return launch_c2a_grp<8>(o, ref, b, 1, max_list, tb_bytes, a, st);
+    case 2: return launch_c2a_grp<10>(o, ref, b, 2, max_list, tb_bytes, a, st);
+    case 3: return launch_c2a_grp<16>(o, ref, b, 3, max_list, tb_bytes, a, st);
+    case 4: return launch_c2a_fast<3>(o, ref, b, 4, max_list, tb_bytes, a, st);
+    case 5: return launch_c2a_fast<4>(o, ref, b, 5, max_list, tb_bytes, a, st);
+    case 6: return launch_c2a_t<64, 16>(o, ref, b, 6, max_list, tb_bytes, a, st);
   }
   return hipErrorInvalidValue;
 }

@@ -26,12 +26,27 @@ def refd():
     return G.load_ref()
 
 
+@pytest.fixture(params=["wave", "grp"])
+def c2a_path(request, monkeypatch):
+    """mem_chain2aln kernels for reads <= 256 bp: wave per read (default) or
+    16-lane groups, four reads per wave (BWAGPU_C2A_GRP=1)"""
+    monkeypatch.setenv("BWAGPU_C2A_GRP", "1" if request.param == "grp" else "0")
+    return request.param
+
+
+@pytest.fixture(params=["grp", "wave"])
+def ext_path(request, monkeypatch):
+    """bare ksw_extend2 lists: 16-lane groups for qlen < 128 (default) or wave kernels only"""
+    monkeypatch.setenv("BWAGPU_EXT_WAVE", "1" if request.param == "wave" else "0")
+    return request.param
+
+
 def make_engine(refd, opt):
     return Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
 
 
 @pytest.mark.parametrize("name", G.CHAIN_SETS)
-def test_chain_sets_bit_exact(refd, name):
+def test_chain_sets_bit_exact(refd, name, c2a_path):
     opt, batch, want, want_n = G.load_chain_set(name)
     eng = make_engine(refd, opt)
     regs, n = eng.chain2aln(batch)
@@ -43,7 +58,7 @@ def test_chain_sets_bit_exact(refd, name):
 
 
 @pytest.mark.parametrize("name", G.CHAIN_SETS + G.KSW_SETS)
-def test_ksw_extend2_tasks_bit_exact(refd, name):
+def test_ksw_extend2_tasks_bit_exact(refd, name, ext_path):
     opt, tasks, want, qp, tp = G.load_tasks(name)
     eng = make_engine(refd, opt)
     got = eng.extend_batch(tasks, qp, tp)
@@ -57,7 +72,7 @@ def test_ksw_extend2_tasks_bit_exact(refd, name):
     eng.close()
 
 
-def test_cell_and_call_counts_match_oracle(refd):
+def test_cell_and_call_counts_match_oracle(refd, c2a_path):
     opt, batch, _, _ = G.load_chain_set("c1_default")
     eng = make_engine(refd, opt)
     eng.chain2aln(batch)
@@ -84,7 +99,7 @@ def test_slots_double_buffered(refd):
     eng.close()
 
 
-def test_reordered_and_ragged_batches(refd):
+def test_reordered_and_ragged_batches(refd, c2a_path):
     opt, batch, want, want_n = G.load_chain_set("c5_mixed")
     eng = make_engine(refd, opt)
     rng = np.random.default_rng(5)
@@ -163,7 +178,7 @@ def test_device_entry_point_with_torch_buffers(refd):
 
 @pytest.mark.parametrize("len_mode,min_seed,pairs", [(150, 19, 800), (0, 19, 600), (250, 12, 400), (400, 12, 300),
                                                      (700, 8, 150), (1000, 8, 60)])
-def test_synthetic_batches_vs_oracle(len_mode, min_seed, pairs):
+def test_synthetic_batches_vs_oracle(len_mode, min_seed, pairs, c2a_path):
     """seeded synthetic reads of every kernel variant's shape — 100-256 bp on
     the fast kernel, > 32 seeds (short min seed length) and 257-1023 bp on the
     generic kernel — against the oracle on the same inputs, bit for bit"""
@@ -197,7 +212,7 @@ def split_seeds(b: Batch, piece: int) -> Batch:
 
 
 @pytest.mark.parametrize("len_mode,piece", [(150, 6), (250, 9), (400, 14)])
-def test_many_seed_reads_vs_oracle(len_mode, piece):
+def test_many_seed_reads_vs_oracle(len_mode, piece, c2a_path):
     """reads with more seeds or chains than the fast kernel keeps per wave
     (> 32) go to the generic kernel; both against the oracle"""
     from bwagpu.synth import SynthRef, synth_batch
