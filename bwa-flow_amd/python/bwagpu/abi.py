@@ -41,6 +41,12 @@ ALIGN2_TASK_DTYPE = np.dtype([("qoff", "<i8"), ("toff", "<i8"), ("qlen", "<i4"),
 KSWR_DTYPE = np.dtype([("score", "<i4"), ("te", "<i4"), ("qe", "<i4"), ("score2", "<i4"), ("te2", "<i4"),
                        ("tb", "<i4"), ("qb", "<i4")])
 KSW_XBYTE, KSW_XSTOP, KSW_XSUBO, KSW_XSTART = 0x10000, 0x20000, 0x40000, 0x80000
+REG2ALN_TASK_DTYPE = np.dtype([("rb", "<i8"), ("re", "<i8"), ("qoff", "<i8"), ("l_seq", "<i4"), ("qb", "<i4"),
+                               ("qe", "<i4"), ("truesc", "<i4"), ("w", "<i4"), ("pad", "<i4")])
+ALN_DTYPE = np.dtype([("pos", "<i8"), ("rid", "<i4"), ("is_rev", "<i4"), ("n_cigar", "<i4"), ("NM", "<i4"),
+                      ("md_len", "<i4"), ("score", "<i4"), ("w", "<i4"), ("status", "<i4")])
+ALN_OK, ALN_NO_CIGAR, ALN_OVERFLOW, ALN_UNMAPPED = 0, 1, 2, 3
+assert REG2ALN_TASK_DTYPE.itemsize == 48 and ALN_DTYPE.itemsize == 40
 assert SEED_DTYPE.itemsize == 24 and ALNREG_DTYPE.itemsize == 88
 assert ALIGN2_TASK_DTYPE.itemsize == 32 and KSWR_DTYPE.itemsize == 28
 assert EXT_TASK_DTYPE.itemsize == 40 and EXT_RES_DTYPE.itemsize == 24

@@ -182,6 +182,38 @@ typedef struct {
   int32_t score, te, qe, score2, te2, tb, qb;
 } bwagpu_kswr_t;
 
+/* One mem_reg2aln CIGAR job (bwa/bwamem.c:1104-1174, as called per output
+   region from src/bwa_wrapper.cpp:611/728/736/774): the region's
+   rb/re/qb/qe/truesc/w (mem_alnreg_t) and its read, l_seq nt4 bases at
+   qpool[qoff..qoff+l_seq).  rb < 0 or re < 0 asks for the unmapped record. */
+typedef struct {
+  int64_t rb, re;
+  int64_t qoff;
+  int32_t l_seq, qb, qe;
+  int32_t truesc, w;
+  int32_t pad_;
+} bwagpu_reg2aln_task_t;
+
+#define BWAGPU_ALN_OK 0
+#define BWAGPU_ALN_NO_CIGAR 1 /* bwa_gen_cigar2 returned no CIGAR (bwa.c:133/135): the
+                                 reference's mem_reg2aln would dereference NULL here */
+#define BWAGPU_ALN_OVERFLOW 2 /* more than max_ops CIGAR ops or max_md MD bytes */
+#define BWAGPU_ALN_UNMAPPED 3 /* rb < 0 || re < 0: rid = -1, pos = -1 (bwamem.c:1112-1115) */
+
+/* The alignment fields mem_reg2aln fills in mem_aln_t (bwa/bwamem.h:81-92)
+   besides mapq/flag/sub/alt_sc (which need the other regions): CIGAR with
+   soft clips (ops at cigar[k * max_ops], BAM encoding len << 4 | op), the MD
+   string after it in the reference layout (here at md[k * max_md],
+   NUL-terminated, md_len = strlen), NM, strand, contig and 0-based position.
+   score / w: the global score and band of the last bwa_gen_cigar2 call. */
+typedef struct {
+  int64_t pos;
+  int32_t rid, is_rev;
+  int32_t n_cigar, NM;
+  int32_t md_len, score;
+  int32_t w, status;
+} bwagpu_aln_t;
+
 /* per-launch statistics of the last finished launch on a slot */
 typedef struct {
   double kernel_ms;      /* HIP-event time of the extension kernel(s)            */
@@ -232,6 +264,16 @@ int bwagpu_align2_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_align2_
 int bwagpu_align2_device(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_align2_task_t *dev_tasks,
                          const uint8_t *dev_qpool, const uint8_t *dev_tpool, bwagpu_kswr_t *dev_results,
                          void *dev_scratch, void *stream);
+
+/* mem_reg2aln's CIGAR/NM/MD/position for n regions (host buffers; blocking).
+   cigar: n * max_ops uint32, md: n * max_md bytes. */
+int bwagpu_reg2aln_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_reg2aln_task_t *tasks,
+                         const uint8_t *qpool, int64_t qpool_len, int32_t max_ops, int32_t max_md,
+                         bwagpu_aln_t *out, uint32_t *cigar, char *md);
+/* the same on device buffers, asynchronous on stream (NULL = slot-0 stream) */
+int bwagpu_reg2aln_device(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_reg2aln_task_t *dev_tasks,
+                          const uint8_t *dev_qpool, int32_t max_ops, int32_t max_md, bwagpu_aln_t *dev_out,
+                          uint32_t *dev_cigar, char *dev_md, void *stream);
 
 int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
 

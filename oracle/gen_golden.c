@@ -100,6 +100,35 @@ int __wrap_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
   return r;
 }
 
+/* ---------------- mem_reg2aln / bwa_gen_cigar2 recorder ---------------- */
+typedef struct { int64_t rb, re, qoff; int32_t l_seq, qb, qe, truesc, w, read; } ctask_t;
+typedef struct { int64_t pos; int32_t rid, is_rev, n_cigar, NM, cig_off, md_off, md_len, pad; } cres_t;
+typedef struct { int32_t task, w, l_query, score, n_cigar, NM, cig_off, md_off; int64_t rb, re; } ccall_t;
+static kvec_t(ctask_t) g_ctasks;
+static kvec_t(cres_t) g_cres;
+static kvec_t(ccall_t) g_ccalls;
+static kvec_t(uint32_t) g_cig;
+static kvec_t(char) g_md;
+uint32_t *__real_bwa_gen_cigar2(const int8_t mat[25], int o_del, int e_del, int o_ins, int e_ins, int w_,
+                                int64_t l_pac, const uint8_t *pac, int l_query, uint8_t *query, int64_t rb,
+                                int64_t re, int *score, int *n_cigar, int *NM);
+uint32_t *__wrap_bwa_gen_cigar2(const int8_t mat[25], int o_del, int e_del, int o_ins, int e_ins, int w_,
+                                int64_t l_pac, const uint8_t *pac, int l_query, uint8_t *query, int64_t rb,
+                                int64_t re, int *score, int *n_cigar, int *NM)
+{
+  uint32_t *c = __real_bwa_gen_cigar2(mat, o_del, e_del, o_ins, e_ins, w_, l_pac, pac, l_query, query, rb, re,
+                                      score, n_cigar, NM);
+  ccall_t k = {(int32_t)g_ctasks.n - 1, w_, l_query, *score, *n_cigar, *NM, (int32_t)g_cig.n, (int32_t)g_md.n, rb,
+               re};
+  if (c) {
+    for (int i = 0; i < *n_cigar; ++i) kv_push(uint32_t, g_cig, c[i]);
+    const char *md = (const char *)(c + *n_cigar);
+    for (size_t i = 0; i <= strlen(md); ++i) kv_push(char, g_md, md[i]);
+  }
+  kv_push(ccall_t, g_ccalls, k);
+  return c;
+}
+
 /* ---------------- reference genome ---------------- */
 static const char ACGT[] = "ACGT";
 
@@ -296,6 +325,21 @@ int main(int argc, char *argv[])
         free(ch->seeds);
       }
       free(chn.a);
+      /* the SAM stage's CIGAR step on every region (bwa_wrapper.cpp:611) */
+      for (size_t k = 0; k < av.n; ++k) {
+        const mem_alnreg_t *ar = &av.a[k];
+        ctask_t t = {ar->rb, ar->re, (int64_t)(seq.n - n), n, ar->qb, ar->qe, ar->truesc, ar->w,
+                     (int32_t)(seq_off.n - 2)};
+        kv_push(ctask_t, g_ctasks, t);
+        mem_aln_t a = mem_reg2aln(opt, idx->bns, idx->pac, n, (const char *)q, ar);
+        cres_t o = {a.pos, a.rid, a.is_rev, a.n_cigar, a.NM, (int32_t)g_cig.n, (int32_t)g_md.n, 0, 0};
+        for (int i = 0; i < a.n_cigar; ++i) kv_push(uint32_t, g_cig, a.cigar[i]);
+        const char *md = (const char *)(a.cigar + a.n_cigar);
+        o.md_len = (int32_t)strlen(md);
+        for (int i = 0; i <= o.md_len; ++i) kv_push(char, g_md, md[i]);
+        kv_push(cres_t, g_cres, o);
+        free(a.cigar);
+      }
       kv_push(int32_t, rco, (int32_t)crid.n);
       kv_push(int32_t, nreg, (int32_t)av.n);
       for (size_t k = 0; k < av.n; ++k) kv_push(mem_alnreg_t, regs, av.a[k]);
@@ -329,6 +373,12 @@ int main(int argc, char *argv[])
   wr(dir, "task_res", g_res.a, sizeof(rres_t) * g_res.n);
   wr(dir, "qpool", g_qpool.a, g_qpool.n);
   wr(dir, "tpool", g_tpool.a, g_tpool.n);
+  wr(dir, "cig_tasks", g_ctasks.a, sizeof(ctask_t) * g_ctasks.n);
+  wr(dir, "cig_res", g_cres.a, sizeof(cres_t) * g_cres.n);
+  wr(dir, "cig_calls", g_ccalls.a, sizeof(ccall_t) * g_ccalls.n);
+  wr(dir, "cig_ops", g_cig.a, 4 * g_cig.n);
+  wr(dir, "cig_md", g_md.a, g_md.n);
+  fprintf(stderr, "[gen_golden] cigar jobs=%zu gen_cigar2 calls=%zu\n", g_ctasks.n, g_ccalls.n);
   fprintf(stderr, "[gen_golden] reads=%zu chains=%zu seeds=%zu regions=%zu ksw_calls=%zu sizeof(alnreg)=%zu\n",
           seq_off.n - 1, crid.n, seeds.n, regs.n, g_tasks.n, sizeof(mem_alnreg_t));
   bwa_idx_destroy(idx);

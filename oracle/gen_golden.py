@@ -176,9 +176,52 @@ def gen_align2(rng):
               f"sat255:{int((res['score'] == 255).sum())}")
 
 
+CTASK = np.dtype([("rb", "<i8"), ("re", "<i8"), ("qoff", "<i8"), ("l_seq", "<i4"), ("qb", "<i4"), ("qe", "<i4"),
+                  ("truesc", "<i4"), ("w", "<i4"), ("read", "<i4")])
+CRES = np.dtype([("pos", "<i8"), ("rid", "<i4"), ("is_rev", "<i4"), ("n_cigar", "<i4"), ("NM", "<i4"),
+                 ("cig_off", "<i4"), ("md_off", "<i4"), ("md_len", "<i4"), ("pad", "<i4")])
+CCALL = np.dtype([("task", "<i4"), ("w", "<i4"), ("l_query", "<i4"), ("score", "<i4"), ("n_cigar", "<i4"),
+                  ("NM", "<i4"), ("cig_off", "<i4"), ("md_off", "<i4"), ("rb", "<i8"), ("re", "<i8")])
+
+
+def gen_cigar(tmp):
+    """mem_reg2aln (bwamem.c:1104-1174) on every region of each chain set, through
+    the reference's own code (gen_golden records its outputs and every
+    bwa_gen_cigar2 call) -> tests/golden/cigar_<set>.npz"""
+    for name, (seed, pairs, lm, om) in CHAIN_SETS.items():
+        d = os.path.join(tmp, "cig_" + name)
+        os.makedirs(d, exist_ok=True)
+        subprocess.run([os.path.join(HERE, "_ref", "gen_golden"), d, str(seed), str(pairs), lm, str(om)], check=True)
+        ct, cr, cc = rd(d, "cig_tasks", CTASK), rd(d, "cig_res", CRES), rd(d, "cig_calls", CCALL)
+        ops, md = rd(d, "cig_ops", np.uint32), rd(d, "cig_md", np.uint8)
+        tasks = np.zeros(len(ct), abi.REG2ALN_TASK_DTYPE)
+        for f in ("rb", "re", "qoff", "l_seq", "qb", "qe", "truesc", "w"):
+            tasks[f] = ct[f]
+        exp = np.zeros(len(ct), abi.ALN_DTYPE)
+        for f in ("pos", "rid", "is_rev", "n_cigar", "NM", "md_len"):
+            exp[f] = cr[f]
+        last = np.full(len(ct), -1, np.int64)  # each job's last bwa_gen_cigar2 call: its score and band
+        last[cc["task"]] = np.arange(len(cc))
+        assert (last >= 0).all()
+        exp["score"] = cc["score"][last]
+        exp["w"] = cc["w"][last]
+        np.savez_compressed(
+            os.path.join(GOLD, "cigar_" + name + ".npz"),
+            opt_int=rd(d, "opt_int", np.int32), opt_mat=rd(d, "opt_mat", np.int8),
+            seq_off=rd(d, "seq_off", np.int64), seq=rd(d, "seq", np.uint8),
+            tasks=tasks, exp=exp, cig_off=cr["cig_off"], md_off=cr["md_off"], cig_ops=ops, md=md,
+            calls=cc)
+        print(f"[gen_golden] cigar_{name}: jobs={len(ct)} gen_cigar2 calls={len(cc)} "
+              f"multi-try jobs={int((np.bincount(cc['task'], minlength=len(ct)) > 1).sum())}")
+
+
 def main():
     if "--only-align2" in sys.argv:
         gen_align2(np.random.default_rng(2025))
+        return
+    if "--only-cigar" in sys.argv:
+        with tempfile.TemporaryDirectory() as tmp:
+            gen_cigar(tmp)
         return
     if oracle.ref_lib() is None or not os.path.exists(os.path.join(HERE, "_ref", "gen_golden")):
         sys.exit("build the reference first: make -C oracle")
@@ -189,6 +232,7 @@ def main():
         for name, (seed, pairs, lm, om) in CHAIN_SETS.items():
             _, _, ref = gen_chain_set(name, seed, pairs, lm, om, tmp, rng)
         np.savez_compressed(os.path.join(GOLD, "ref.npz"), **ref)
+        gen_cigar(tmp)
     # ksw_extend2 edge cases through the reference's own ksw_extend2
     opts = {
         "ksw_edge_default": abi.default_opt(),

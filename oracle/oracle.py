@@ -45,6 +45,9 @@ def oracle_lib():
     lib.oracle_extend_batch.restype = C.c_int
     lib.oracle_align2_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
     lib.oracle_align2_batch.restype = C.c_int
+    lib.oracle_reg2aln_batch.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, C.c_int32, _VP, _VP,
+                                         C.c_int, C.c_int, _VP, _VP, _VP]
+    lib.oracle_reg2aln_batch.restype = C.c_int
     return lib
 
 
@@ -59,6 +62,10 @@ def ref_lib():
     lib.ref_extend_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP]
     lib.ref_extend_batch.restype = C.c_int
     lib.ref_abi_check.restype = C.c_int
+    if hasattr(lib, "ref_reg2aln_batch"):
+        lib.ref_reg2aln_batch.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, C.c_int32, _VP, _VP,
+                                          C.c_int, C.c_int, _VP, _VP, _VP]
+        lib.ref_reg2aln_batch.restype = C.c_int
     if hasattr(lib, "ref_align2_batch"):
         lib.ref_align2_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP]
         lib.ref_align2_batch.restype = C.c_int
@@ -135,3 +142,24 @@ def align2(which: str, opt: dict, tasks, qpool, tpool):
         raise RuntimeError("oracle/_ref/libbwaref.so (with ref_align2_batch) not available")
     lib.ref_align2_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool), _ptr(res))
     return res[:len(tasks)], None
+
+
+def reg2aln(which: str, opt: dict, ref: Ref, tasks, qpool, max_ops: int = 64, max_md: int = 512):
+    """mem_reg2aln's CIGAR part per job -> (aln records, cigar [n, max_ops] u32, md [n, max_md] bytes)"""
+    o = abi.opt_from_dict(opt)
+    tasks = np.ascontiguousarray(tasks, abi.REG2ALN_TASK_DTYPE)
+    qpool = np.ascontiguousarray(qpool, np.uint8)
+    n = len(tasks)
+    out = np.zeros(max(n, 1), abi.ALN_DTYPE)
+    cig = np.zeros((max(n, 1), max_ops), np.uint32)
+    md = np.zeros((max(n, 1), max_md), np.uint8)
+    if which == "oracle":
+        f = oracle_lib().oracle_reg2aln_batch
+    else:
+        lib = ref_lib()
+        if lib is None or not hasattr(lib, "ref_reg2aln_batch"):
+            raise RuntimeError("oracle/_ref/libbwaref.so (with ref_reg2aln_batch) not available")
+        f = lib.ref_reg2aln_batch
+    f(C.byref(o), C.byref(ref.bns), _ptr(ref.pac), n, _ptr(tasks), _ptr(qpool), max_ops, max_md, _ptr(out),
+      _ptr(cig), _ptr(md))
+    return out[:n], cig[:n], md[:n]

@@ -161,3 +161,55 @@ int ref_align2_batch(const bwagpu_opt_t *o, int32_t n_tasks, const bwagpu_align2
   }
   return 0;
 }
+
+/* the reference mem_reg2aln per job (bwa/bwamem.c:1104-1174) — its CIGAR (with
+   clips), MD, NM, strand, contig and position; ar->rid is set to the contig
+   of the region's first base so that mem_reg2aln's assert(a.rid == ar->rid)
+   holds for jobs inside one contig */
+int ref_reg2aln_batch(const bwagpu_opt_t *o, const bwagpu_bns_t *gb, const uint8_t *pac, int32_t n,
+                      const bwagpu_reg2aln_task_t *tasks, const uint8_t *qpool, int max_ops, int max_md,
+                      bwagpu_aln_t *out, uint32_t *cigar, char *md)
+{
+  mem_opt_t opt;
+  bntseq_t bns;
+  fill_opt(o, &opt);
+  memset(&bns, 0, sizeof(bns));
+  bns.l_pac = gb->l_pac;
+  bns.n_seqs = gb->n_seqs;
+  bns.anns = (bntann1_t *)calloc((size_t)gb->n_seqs, sizeof(bntann1_t));
+  for (int i = 0; i < gb->n_seqs; ++i) {
+    bns.anns[i].offset = gb->ann_offset[i];
+    bns.anns[i].len = gb->ann_len[i];
+    bns.anns[i].name = (char *)"ref";
+  }
+  for (int32_t k = 0; k < n; ++k) {
+    const bwagpu_reg2aln_task_t *t = &tasks[k];
+    mem_alnreg_t ar;
+    int is_rev;
+    memset(&ar, 0, sizeof(ar));
+    ar.rb = t->rb; ar.re = t->re; ar.qb = t->qb; ar.qe = t->qe;
+    ar.truesc = ar.score = t->truesc; ar.w = t->w;
+    ar.rid = t->rb >= 0 ? bns_pos2rid(&bns, bns_depos(&bns, t->rb < bns.l_pac ? t->rb : t->re - 1, &is_rev)) : -1;
+    mem_aln_t a = mem_reg2aln(&opt, &bns, pac, t->l_seq, (const char *)(qpool + t->qoff), &ar);
+    bwagpu_aln_t *r = &out[k];
+    memset(r, 0, sizeof(*r));
+    r->pos = a.pos; r->rid = a.rid; r->is_rev = a.is_rev; r->NM = a.NM;
+    if (a.rid < 0) {
+      r->status = BWAGPU_ALN_UNMAPPED;
+      continue;
+    }
+    const char *m = (const char *)(a.cigar + a.n_cigar);
+    const int ml = (int)strlen(m);
+    if (a.n_cigar > max_ops || ml + 1 > max_md) {
+      r->status = BWAGPU_ALN_OVERFLOW;
+    } else {
+      r->n_cigar = a.n_cigar;
+      r->md_len = ml;
+      memcpy(cigar + (size_t)k * max_ops, a.cigar, 4 * (size_t)a.n_cigar);
+      memcpy(md + (size_t)k * max_md, m, (size_t)ml + 1);
+    }
+    free(a.cigar);
+  }
+  free(bns.anns);
+  return 0;
+}

@@ -75,3 +75,95 @@ def region_mismatch(got: np.ndarray, want: np.ndarray) -> str | None:
     fields = [f for f in abi.ALNREG_DTYPE.names if got[i][f] != want[i][f]]
     return (f"{len(bad)} regions differ; first #{i}: fields {fields}: "
             f"got {[got[i][f] for f in fields]} want {[want[i][f] for f in fields]}")
+
+
+CIGAR_SETS = ["cigar_" + n for n in CHAIN_SETS]
+
+
+def load_cigar_set(name):
+    """mem_reg2aln jobs of one chain set -> opt, tasks, qpool (the reads), expected
+    records, expected CIGAR ops per job, expected MD bytes per job"""
+    z = _npz(name)
+    exp = z["exp"].astype(abi.ALN_DTYPE)
+    ops = [z["cig_ops"][o:o + n] for o, n in zip(z["cig_off"], exp["n_cigar"])]
+    mds = [bytes(z["md"][o:o + n]) for o, n in zip(z["md_off"], exp["md_len"])]
+    return opt_of(z), z["tasks"].astype(abi.REG2ALN_TASK_DTYPE), z["seq"], exp, ops, mds
+
+
+def aln_mismatch(tasks, got, cig, md, exp, ops, mds, fields=("pos", "rid", "is_rev", "n_cigar", "NM", "md_len",
+                                                                "score", "w", "status")) -> str | None:
+    """bit-exact comparison of reg2aln outputs (records + CIGAR + MD) with expected ones"""
+    bad = []
+    for k in range(len(tasks)):
+        why = [f for f in fields if got[f][k] != exp[f][k]]
+        if not why and got["status"][k] == abi.ALN_OK:
+            n = int(exp["n_cigar"][k])
+            if not np.array_equal(cig[k, :n], ops[k]):
+                why.append("cigar")
+            if bytes(md[k, :int(exp["md_len"][k])]) != mds[k]:
+                why.append("MD")
+        if why:
+            bad.append((k, why))
+    if not bad:
+        return None
+    k, why = bad[0]
+    return f"{len(bad)}/{len(tasks)} jobs differ; first #{k} {tasks[k]} in {why}: got {got[k]} want {exp[k]}"
+
+
+def aln_expected_from(out, cig, md):
+    """(records, ops list, md list) in the form aln_mismatch takes as expected"""
+    ops = [cig[k, :int(out["n_cigar"][k])] for k in range(len(out))]
+    mds = [bytes(md[k, :int(out["md_len"][k])]) for k in range(len(out))]
+    return out, ops, mds
+
+
+def synth_reg2aln_jobs(rng, ref_pac, l_pac, ann_offset, ann_len, n, lens=(100, 150, 250), mat=None):
+    """mem_reg2aln jobs around real alignments of a synthetic reference: each
+    read is a mutated copy (substitutions, 1-6 bp indels, N bases) of a window
+    on either strand inside one contig; the region is the true window with
+    jittered ends, a clipped query range, a local score that sometimes
+    exceeds the global one (band doubling) and a random region band w"""
+    def base(x):
+        return (int(ref_pac[x >> 2]) >> ((~x & 3) << 1)) & 3
+
+    tasks = np.zeros(n, abi.REG2ALN_TASK_DTYPE)
+    qs, qo = [], 0
+    for k in range(n):
+        L = int(rng.choice(lens))
+        c = int(rng.integers(0, len(ann_offset)))
+        span = L + 40
+        p0 = int(ann_offset[c]) + int(rng.integers(0, int(ann_len[c]) - span))
+        win = [base(p0 + i) for i in range(span)]
+        rev = bool(rng.random() < 0.5)
+        read = []
+        i = 20
+        while len(read) < L and i < span:
+            u = rng.random()
+            if u < 0.01:
+                i += int(rng.integers(1, 7))  # deletion in the read
+                continue
+            if u < 0.02:
+                read.extend(rng.integers(0, 4, int(rng.integers(1, 7))).tolist())  # insertion
+            b = win[i]
+            read.append(4 if rng.random() < 0.003 else (int(rng.integers(0, 4)) if rng.random() < 0.02 else b))
+            i += 1
+        read = read[:L]
+        L = len(read)
+        ref_end = i
+        qb = int(rng.integers(0, 6)) if rng.random() < 0.3 else 0
+        qe = L - (int(rng.integers(0, 6)) if rng.random() < 0.3 else 0)
+        rb = p0 + 20 + int(rng.integers(-3, 4)) + qb
+        re = p0 + ref_end + int(rng.integers(-3, 4)) - (L - qe)
+        if re <= rb:
+            re = rb + 1
+        if rev:  # the read is the reverse complement; the region lives on the reverse strand
+            read = [3 - b if b < 4 else 4 for b in read[::-1]]
+            qb, qe = L - qe, L - qb
+            rb, re = 2 * l_pac - re, 2 * l_pac - rb
+        a = 1 if mat is None else int(mat[0])
+        truesc = int((qe - qb) * a * rng.choice([0.6, 0.9, 1.0, 1.3]))
+        w = int(rng.choice([1, 5, 20, 100, 200]))
+        tasks[k] = (rb, re, qo, L, qb, qe, truesc, w, 0)
+        qs.append(np.array(read, np.uint8))
+        qo += L
+    return tasks, np.concatenate(qs)
