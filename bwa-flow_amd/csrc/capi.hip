@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "align2.h"
+#include "reg2aln.h"
 #include "engine.h"
 
 using namespace bwagpu;
@@ -115,6 +116,8 @@ struct bwagpu_ctx {
   Slot slot[BWAGPU_NUM_SLOTS];
   // ksw_align2 batches (bwagpu_align2_*): grow-only, reused across calls
   DevBuf a2_tasks, a2_q, a2_t, a2_out, a2_scratch, a2_lists, a2_counts, a2_boff;
+  // mem_reg2aln batches (bwagpu_reg2aln_batch)
+  DevBuf r2_tasks, r2_q, r2_out, r2_cig, r2_md, r2_lists, r2_z, r2_stats;
   // bins run concurrently on these (fork/join with events from the caller's stream)
   static constexpr int kA2Streams = 4;
   hipStream_t a2_st[kA2Streams] = {};
@@ -749,6 +752,151 @@ int launch_align2_concurrent(bwagpu_ctx_t* ctx, hipStream_t st, const std::vecto
 }  // namespace
 
 extern "C" {
+
+// mem_reg2aln's CIGAR part (bwa/bwamem.c:1104-1174) per job.  Jobs are binned on
+// the host by query segments (kernel template) and by the size of their
+// direction matrix (ksw_global2's z, ncol x tlen bytes, ksw.c:511-512): the
+// matrix sits in LDS for jobs up to kR2ZSmall / kR2ZLarge bytes and in a
+// per-wave HBM slice beyond.
+namespace {
+constexpr int kR2ZSmall = 8 * 1024, kR2ZLarge = 24 * 1024;
+constexpr int kR2MaxRef = 8192;  // reference window bytes per job (LDS)
+}  // namespace
+
+int bwagpu_reg2aln_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_reg2aln_task_t* tasks, const uint8_t* qpool,
+                         int64_t qpool_len, int32_t max_ops, int32_t max_md, bwagpu_aln_t* out, uint32_t* cigar,
+                         char* md) {
+  if (!ctx || n < 0 || (n && (!tasks || !out || !cigar || !md)) || qpool_len < 0 || (qpool_len && !qpool) ||
+      max_ops < 1 || max_md < 1)
+    return BWAGPU_E_INVAL;
+  if (n == 0) return BWAGPU_OK;
+  const DevOpt& o = ctx->opt;
+  const int64_t l_pac = ctx->ref.l_pac, two = l_pac << 1;
+  const int wmax = o.w << 2;
+  // validate; bin by [query bucket][matrix class 0 LDS small, 1 LDS large, 2 HBM]
+  struct Bin {
+    std::vector<int32_t> ids;
+    int qmax = 0, rmax = 0;
+    int64_t zmax = 0;
+  };
+  Bin bins[kR2Buckets][3];
+  std::vector<int64_t> cost((size_t)n, 0);
+  for (int32_t k = 0; k < n; ++k) {
+    const bwagpu_reg2aln_task_t& t = tasks[k];
+    if (t.l_seq < 0 || t.qoff < 0 || t.qoff + t.l_seq > qpool_len)
+      return fail(ctx, BWAGPU_E_INVAL, "job's read outside the query pool");
+    int lq = 0, rl = 0, cls = 0;
+    int64_t zb = 0;
+    if (t.rb >= 0 && t.re >= 0) {
+      const int64_t beg = t.rb, end = t.re > two ? two : t.re;
+      const bool ok = t.qe - t.qb > 0 && t.rb < t.re && !(t.rb < l_pac && t.re > l_pac) &&
+                      (beg >= l_pac || end <= l_pac) && end - beg == t.re - t.rb;
+      if (ok) {
+        if (t.qb < 0 || t.qe > t.l_seq) return fail(ctx, BWAGPU_E_INVAL, "job's qb/qe outside its read");
+        lq = t.qe - t.qb;
+        if (lq > BWAGPU_MAX_READ_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "qe - qb > BWAGPU_MAX_READ_LEN");
+        if (t.re - t.rb > kR2MaxRef) return fail(ctx, BWAGPU_E_UNSUPPORTED, "re - rb > 8192");
+        rl = (int)(t.re - t.rb);
+        // the widest band any try can use (bwa.c:152-159 with w_ <= opt->w << 2)
+        const int half = (lq + 1) >> 1;
+        const int mi = (int)((double)(half * o.mat[0] - o.o_ins) / o.e_ins + 1.);
+        const int mdl = (int)((double)(half * o.mat[0] - o.o_del) / o.e_del + 1.);
+        const int mg = std::max(std::max(mi, mdl), 1), dl = std::abs(rl - lq);
+        const int wb = std::max(std::min((mg + dl + 1) >> 1, wmax), dl + 3);
+        zb = (int64_t)std::min(lq, 2 * wb + 1) * rl;
+        cls = zb <= kR2ZSmall ? 0 : (zb <= kR2ZLarge ? 1 : 2);
+      }
+    }
+    Bin& b = bins[r2_bucket_of(lq)][cls];
+    b.ids.push_back(k);
+    b.qmax = std::max(b.qmax, lq);
+    b.rmax = std::max(b.rmax, rl);
+    b.zmax = std::max(b.zmax, zb);
+    cost[(size_t)k] = zb + lq + rl;
+  }
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->slot[0].stream;
+  HIPC(ctx->r2_tasks.ensure(sizeof(bwagpu_reg2aln_task_t) * n), "hipMalloc");
+  HIPC(ctx->r2_q.ensure((size_t)qpool_len + 1), "hipMalloc");
+  HIPC(ctx->r2_out.ensure(sizeof(bwagpu_aln_t) * n), "hipMalloc");
+  HIPC(ctx->r2_cig.ensure(sizeof(uint32_t) * (size_t)n * max_ops), "hipMalloc");
+  HIPC(ctx->r2_md.ensure((size_t)n * max_md), "hipMalloc");
+  HIPC(ctx->r2_lists.ensure(sizeof(int32_t) * n), "hipMalloc");
+  HIPC(ctx->r2_stats.ensure(sizeof(int64_t) * ST_N), "hipMalloc");
+  std::vector<int32_t> all;
+  all.reserve((size_t)n);
+  for (auto& row : bins)
+    for (auto& b : row) {
+      // largest matrices first: the last claims are the small jobs
+      std::stable_sort(b.ids.begin(), b.ids.end(), [&](int32_t x, int32_t y) { return cost[x] > cost[y]; });
+      all.insert(all.end(), b.ids.begin(), b.ids.end());
+    }
+  HIPC(hipMemcpyAsync(ctx->r2_tasks.p, tasks, sizeof(bwagpu_reg2aln_task_t) * n, hipMemcpyHostToDevice, st), "H2D");
+  if (qpool_len) HIPC(hipMemcpyAsync(ctx->r2_q.p, qpool, (size_t)qpool_len, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemcpyAsync(ctx->r2_lists.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemsetAsync(ctx->r2_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset");
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPC(hipEventCreate(&e0), "event");
+  HIPC(hipEventCreate(&e1), "event");
+  HIPC(hipEventRecord(e0, st), "event");
+  int32_t off = 0;
+  for (int bk = 0; bk < kR2Buckets; ++bk)
+    for (int cls = 0; cls < 3; ++cls) {
+      const Bin& b = bins[bk][cls];
+      const int nb = (int)b.ids.size();
+      if (!nb) continue;
+      R2AArgs a{};
+      a.tasks = ctx->r2_tasks.as<bwagpu_reg2aln_task_t>();
+      a.qpool = ctx->r2_q.as<uint8_t>();
+      a.list = ctx->r2_lists.as<int32_t>() + off;
+      a.n = nb;
+      a.max_ops = max_ops;
+      a.max_md = max_md;
+      a.out = ctx->r2_out.as<bwagpu_aln_t>();
+      a.cigar = ctx->r2_cig.as<uint32_t>();
+      a.md = ctx->r2_md.as<char>();
+      a.stats = ctx->r2_stats.as<int64_t>();
+      a.qcap = (b.qmax + 16) & ~15;
+      a.rcap = (b.rmax + 16) & ~15;
+      a.ocap = a.qcap + a.rcap + 4;
+      int lpw = a.qcap + a.rcap + 4 * a.ocap;
+      if (cls < 2) lpw += cls == 0 ? kR2ZSmall : kR2ZLarge;
+      a.lds_per_wave = (lpw + 15) & ~15;
+      if ((size_t)4 * a.lds_per_wave > 160 * 1024) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        return fail(ctx, BWAGPU_E_UNSUPPORTED, "reg2aln job needs more LDS than a workgroup has");
+      }
+      int waves = r2_resident_waves(kR2CD[bk], (size_t)4 * a.lds_per_wave);
+      if (cls == 2) {  // HBM matrices: one slice per resident wave, at most 1 GiB
+        a.zstride = (b.zmax + 255) & ~(int64_t)255;
+        waves = (int)std::min<int64_t>(waves, std::max<int64_t>(4, ((int64_t)1 << 30) / a.zstride));
+        HIPC(ctx->r2_z.ensure((size_t)a.zstride * waves), "hipMalloc(reg2aln matrices)");
+        a.zglob = ctx->r2_z.as<uint8_t>();
+      }
+      const int blocks = std::max(1, std::min((nb + 3) / 4, waves / 4));
+      HIPC(launch_reg2aln(kR2CD[bk], o, ctx->ref, a, blocks, st), "reg2aln launch");
+      off += nb;
+    }
+  HIPC(hipEventRecord(e1, st), "event");
+  HIPC(hipMemcpyAsync(out, ctx->r2_out.p, sizeof(bwagpu_aln_t) * n, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipMemcpyAsync(cigar, ctx->r2_cig.p, sizeof(uint32_t) * (size_t)n * max_ops, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipMemcpyAsync(md, ctx->r2_md.p, (size_t)n * max_md, hipMemcpyDeviceToHost, st), "D2H");
+  int64_t hst[ST_N];
+  HIPC(hipMemcpyAsync(hst, ctx->r2_stats.p, sizeof(hst), hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "reg2aln execution");
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  Slot& s0 = ctx->slot[0];
+  s0.last = bwagpu_stats_t{};
+  s0.last.kernel_ms = ms;
+  s0.last.cells = hst[ST_CELLS];
+  s0.last.rows = hst[ST_ROWS];
+  s0.last.ext_calls = hst[ST_CALLS];
+  return BWAGPU_OK;
+}
 
 int bwagpu_align2_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_t* tasks, const uint8_t* qpool,
                         int64_t qpool_len, const uint8_t* tpool, int64_t tpool_len, bwagpu_kswr_t* results) {

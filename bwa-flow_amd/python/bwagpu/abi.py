@@ -95,6 +95,7 @@ PROTOS = {
     "bwagpu_extend_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),
     "bwagpu_align2_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),
     "bwagpu_align2_device": (C.c_int, [_VP, C.c_int32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "bwagpu_reg2aln_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, C.c_int32, C.c_int32, _VP, _VP, _VP]),
     "bwagpu_last_stats": (C.c_int, [_VP, C.c_int, C.POINTER(Stats)]),
     "bwagpu_debug_set_trace": (C.c_int, [_VP, _VP]),
 }

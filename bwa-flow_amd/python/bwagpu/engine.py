@@ -194,6 +194,19 @@ class Engine:
         self._check(self.lib.bwagpu_align2_device(self.ctx, n, dev_tasks, dev_q, dev_t, dev_out, dev_scratch,
                                                   stream), "align2_device")
 
+    def reg2aln_batch(self, tasks: np.ndarray, qpool: np.ndarray, max_ops: int = 64, max_md: int = 512):
+        """mem_reg2aln's CIGAR part (bwa/bwamem.c:1104-1174) per job -> (abi.ALN_DTYPE records,
+        CIGAR ops [n, max_ops] uint32, MD strings [n, max_md] bytes)"""
+        tasks = np.ascontiguousarray(tasks, abi.REG2ALN_TASK_DTYPE)
+        qpool = np.ascontiguousarray(qpool, np.uint8)
+        n = len(tasks)
+        out = np.zeros(max(n, 1), abi.ALN_DTYPE)
+        cig = np.zeros((max(n, 1), max_ops), np.uint32)
+        md = np.zeros((max(n, 1), max_md), np.uint8)
+        self._check(self.lib.bwagpu_reg2aln_batch(self.ctx, n, _ptr(tasks), _ptr(qpool), len(qpool), max_ops, max_md,
+                                                  _ptr(out), _ptr(cig), _ptr(md)), "reg2aln_batch")
+        return out[:n], cig[:n], md[:n]
+
     def last_stats(self, slot: int = 0) -> dict:
         s = abi.Stats()
         self._check(self.lib.bwagpu_last_stats(self.ctx, slot, C.byref(s)), "last_stats")

@@ -270,10 +270,6 @@ int bwagpu_align2_device(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_align2
 int bwagpu_reg2aln_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_reg2aln_task_t *tasks,
                          const uint8_t *qpool, int64_t qpool_len, int32_t max_ops, int32_t max_md,
                          bwagpu_aln_t *out, uint32_t *cigar, char *md);
-/* the same on device buffers, asynchronous on stream (NULL = slot-0 stream) */
-int bwagpu_reg2aln_device(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_reg2aln_task_t *dev_tasks,
-                          const uint8_t *dev_qpool, int32_t max_ops, int32_t max_md, bwagpu_aln_t *dev_out,
-                          uint32_t *dev_cigar, char *dev_md, void *stream);
 
 int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
 
