@@ -797,12 +797,23 @@ int bwagpu_reg2aln_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_reg2aln_task
         if (lq > BWAGPU_MAX_READ_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "qe - qb > BWAGPU_MAX_READ_LEN");
         if (t.re - t.rb > kR2MaxRef) return fail(ctx, BWAGPU_E_UNSUPPORTED, "re - rb > 8192");
         rl = (int)(t.re - t.rb);
-        // the widest band any try can use (bwa.c:152-159 with w_ <= opt->w << 2)
+        // the widest band any try can use: the first try's w2 (infer_bw,
+        // bwamem.c:1123-1126) doubled at most twice (1132), capped at
+        // opt->w << 2, then bwa.c:152-159
+        auto infer = [&](int q_, int r_) {
+          if (lq == rl && lq * o.a - t.truesc < (q_ + r_ - o.a) << 1) return 0;
+          const int w = (int)((double)(std::min(lq, rl) * o.a - t.truesc - q_) / r_ + 2.);
+          return std::max(w, std::abs(lq - rl));
+        };
+        int w2 = std::max(infer(o.o_del, o.e_del), infer(o.o_ins, o.e_ins));
+        if (w2 > o.w) w2 = std::min(w2, t.w);
+        w2 = std::min(w2, wmax);
+        const int w2max = (int)std::min<int64_t>((int64_t)w2 << 2, wmax);
         const int half = (lq + 1) >> 1;
         const int mi = (int)((double)(half * o.mat[0] - o.o_ins) / o.e_ins + 1.);
         const int mdl = (int)((double)(half * o.mat[0] - o.o_del) / o.e_del + 1.);
         const int mg = std::max(std::max(mi, mdl), 1), dl = std::abs(rl - lq);
-        const int wb = std::max(std::min((mg + dl + 1) >> 1, wmax), dl + 3);
+        const int wb = std::max(std::min((mg + dl + 1) >> 1, w2max), dl + 3);
         zb = (int64_t)std::min(lq, 2 * wb + 1) * rl;
         cls = zb <= kR2ZSmall ? 0 : (zb <= kR2ZLarge ? 1 : 2);
       }

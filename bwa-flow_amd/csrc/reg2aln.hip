@@ -144,6 +144,95 @@ __device__ int global_dp(const DevOpt& o, int ql, const uint8_t* q, int tl, cons
   return __builtin_amdgcn_readlane(s, ql & 63);
 }
 
+// The same DP in the BAND frame, for bands of 2w+1 <= 64 CDB columns: lane
+// position p (segment c, p = 64c + lane) holds column j = i - w + p of row
+// i, so the band never moves relative to the lanes.  Per row:
+//  * M(i,j) needs H(i-1, j-1), which sits at the same position p of the
+//    previous row: no shift; the query base of a position changes every row
+//    (one LDS byte per lane);
+//  * E(i,j) is the E written at column j by row i-1, one position up (p+1):
+//    a one-lane shift down of the new E values, NEG entering at the top
+//    (eh[end].e = MINUS_INF, ksw.c:569);
+//  * eh[j+1].h for the next row is H(i, j) at the same position, except the
+//    row's first slot, which takes h1 (ksw.c:533-534);
+//  * eh[qlen].h, the score, is followed as a uniform value.
+template <int CDB>
+__device__ int band_dp(const DevOpt& o, int ql, const uint8_t* q, int tl, const uint8_t* r, int w, int ncol,
+                       uint8_t* z, int64_t& cells) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
+  int EH[CDB], EE[CDB];
+#pragma unroll
+  for (int c = 0; c < CDB; ++c) {
+    const int j = 64 * c + lane - w;  // row 0
+    EH[c] = j == 0 ? 0 : (j >= 1 && j <= ql && j <= w ? -(o.o_ins + e_ins * j) : R2_NEG);
+    EE[c] = R2_NEG;
+  }
+  int sc = ql == 0 ? 0 : (ql <= w ? -(o.o_ins + e_ins * ql) : R2_NEG);  // eh[qlen].h
+  int64_t ncells = 0;
+  for (int i = 0; i < tl; ++i) {
+    const int lo = i > w ? i - w : 0, hi = i + w + 1 < ql ? i + w + 1 : ql;
+    const int sh = (r[i] & 3) << 3;
+    const int h1init = lo == 0 ? -(o.o_del + e_del * (i + 1)) : R2_NEG;
+    const int fdecay = R2_NEG + lo * e_ins;
+    uint8_t* zi = z + (size_t)i * ncol - lo;
+    int M[CDB], EX[CDB], J[CDB];
+    bool inb[CDB];
+    int carry = R2_SENT;
+#pragma unroll
+    for (int c = 0; c < CDB; ++c) {
+      const int j = i - w + 64 * c + lane;
+      J[c] = j;
+      inb[c] = j >= lo && j < hi;
+      const int qb = inb[c] ? q[j] : 0;
+      M[c] = EH[c] + __builtin_amdgcn_sbfe((int)prof_word(o, qb), sh, 8);
+      const int u = inb[c] ? M[c] - oe_ins + j * e_ins : R2_SENT;
+      int x = c == 0 ? u : max(u, carry);
+      x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
+      EX[c] = dpp<DPP_WAVE_SHR1>(carry, x);
+      if (c + 1 < CDB) carry = __builtin_amdgcn_readlane(x, 63);
+    }
+    int En[CDB], Hn[CDB];
+#pragma unroll
+    for (int c = 0; c < CDB; ++c) {
+      const int j = J[c];
+      const int m = M[c], e = EE[c];
+      const int f = max(fdecay - j * e_ins, EX[c] - (j - 1) * e_ins);
+      uint32_t d = m >= e ? 0u : 1u;
+      int h = m >= e ? m : e;
+      d = h >= f ? d : 2u;
+      h = h >= f ? h : f;
+      const int te = m - oe_del, ed = e - e_del;
+      d |= ed > te ? 4u : 0u;
+      const int tf = m - oe_ins, fd = f - e_ins;
+      d |= fd > tf ? 32u : 0u;
+      if (inb[c]) zi[j] = (uint8_t)d;
+      Hn[c] = h;
+      En[c] = inb[c] ? (ed > te ? ed : te) : R2_NEG;
+    }
+    // eh[qlen].h after this row (ksw.c:568): H(i, ql-1), or h1 when the band is empty
+    if (hi == ql) {
+      const int pq = ql - 1 - i + w;  // position of column ql-1
+      int v = 0;
+#pragma unroll
+      for (int c = 0; c < CDB; ++c) v = (pq >> 6) == c ? Hn[c] : v;
+      sc = lo < hi ? __builtin_amdgcn_readlane(v, pq & 63) : h1init;
+    }
+    // next row's frame: EH at the same position (h1 at column lo-1), EE one position down
+    int nxt = R2_NEG;
+#pragma unroll
+    for (int c = CDB - 1; c >= 0; --c) {
+      EH[c] = J[c] == lo - 1 ? h1init : Hn[c];
+      const int dn = __builtin_amdgcn_mov_dpp(En[c], 0x130, 0xF, 0xF, false);  // wave_shl:1 (lane l <- l+1)
+      EE[c] = lane == 63 ? nxt : dn;
+      if (c > 0) nxt = __builtin_amdgcn_readlane(En[c], 0);
+    }
+    ncells += hi > lo ? hi - lo : 0;
+  }
+  cells += ncells;
+  return sc;
+}
+
 __device__ __forceinline__ void put_md_int(char* md, int& ml, int cap, int v, bool& ovf) {
   char b[12];
   int n = 0;
@@ -247,7 +336,12 @@ __global__ void __launch_bounds__(256) reg2aln_kernel(DevOpt o, DevRef ref, R2AA
         wdp = w;
         ncol = lq < 2 * w + 1 ? lq : 2 * w + 1;
         ungapped = false;
-        score = uni(global_dp<CD>(o, lq, q, rl, r, w, ncol, z, t_cells));
+        if (2 * w + 1 <= 64)
+          score = uni(band_dp<1>(o, lq, q, rl, r, w, ncol, z, t_cells));
+        else if (2 * w + 1 <= 128 && CD >= 2)
+          score = uni(band_dp<(CD >= 2 ? 2 : 1)>(o, lq, q, rl, r, w, ncol, z, t_cells));
+        else
+          score = uni(global_dp<CD>(o, lq, q, rl, r, w, ncol, z, t_cells));
         t_rows += rl;
       }
       if (score == last || w2 == wmax) break;
@@ -264,25 +358,14 @@ __global__ void __launch_bounds__(256) reg2aln_kernel(DevOpt o, DevRef ref, R2AA
       nops = 1;
     } else {
       wave_sync_lds();  // direction bytes of every lane visible
+      // Runs of one state are taken 64 cells at a time: in state s the walk
+      // moves diagonally (s = 0, M), up (1, D) or left (2, I) and stays in s
+      // while the cell's bits for s (>> 2s) read s again; lane l looks at the
+      // l-th cell of the run, a ballot finds where it ends.  Cells outside the
+      // row's band end a run (the serial step then reads what the reference
+      // reads).
       int i = rl - 1, kk = min(i + wdp + 1, lq) - 1, st = 0, cop = -1, clen = 0;
-      while (i >= 0 && kk >= 0) {
-        const int lo_i = i > wdp ? i - wdp : 0;
-        const int d = uni((int)z[(size_t)i * ncol + (kk - lo_i)]);
-        st = (d >> (st << 1)) & 3;
-        const int op = st == 0 ? 0 : (st == 1 ? 2 : 1);
-        if (op == cop) {
-          ++clen;
-        } else {
-          if (clen && lane == 0) ops[nops] = (uint32_t)clen << 4 | (uint32_t)cop;
-          nops += clen ? 1 : 0;
-          cop = op;
-          clen = 1;
-        }
-        i -= st != 2;
-        kk -= st != 1;
-      }
-      // the ends (ksw.c:591-592), then the last run
-      auto push = [&](int op, int len) {
+      auto emit = [&](int op, int len) {
         if (op == cop) {
           clen += len;
         } else {
@@ -292,6 +375,31 @@ __global__ void __launch_bounds__(256) reg2aln_kernel(DevOpt o, DevRef ref, R2AA
           clen = len;
         }
       };
+      while (i >= 0 && kk >= 0) {
+        const int di = st != 2, dk = st != 1;
+        const int il = i - lane * di, kl = kk - lane * dk;
+        const int lol = il > wdp ? il - wdp : 0, hil = min(il + wdp + 1, lq);
+        const bool valid = il >= 0 && kl >= lol && kl < hil;
+        const int d = valid ? (int)z[(size_t)il * ncol + (kl - lol)] : 0;
+        const bool stop = !valid || ((d >> (st << 1)) & 3) != st;
+        const uint64_t sb = __builtin_amdgcn_ballot_w64(stop);
+        const int f = sb ? __builtin_ctzll(sb) : 64;
+        if (f) {
+          emit(st == 0 ? 0 : (st == 1 ? 2 : 1), f);
+          i -= f * di;
+          kk -= f * dk;
+        }
+        if (f < 64 && i >= 0 && kk >= 0) {  // one serial step at the run's end (reference addressing)
+          const int lo_i = i > wdp ? i - wdp : 0;
+          const int dd = uni((int)z[(size_t)i * ncol + (kk - lo_i)]);
+          st = (dd >> (st << 1)) & 3;
+          emit(st == 0 ? 0 : (st == 1 ? 2 : 1), 1);
+          i -= st != 2;
+          kk -= st != 1;
+        }
+      }
+      auto push = emit;
+      // the ends (ksw.c:591-592), then the last run
       if (i >= 0) push(2, i + 1);
       if (kk >= 0) push(1, kk + 1);
       if (clen && lane == 0) ops[nops] = (uint32_t)clen << 4 | (uint32_t)cop;
