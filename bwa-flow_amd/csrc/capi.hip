@@ -846,49 +846,97 @@ int bwagpu_reg2aln_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_reg2aln_task
   if (qpool_len) HIPC(hipMemcpyAsync(ctx->r2_q.p, qpool, (size_t)qpool_len, hipMemcpyHostToDevice, st), "H2D");
   HIPC(hipMemcpyAsync(ctx->r2_lists.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D");
   HIPC(hipMemsetAsync(ctx->r2_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset");
+  // bins run concurrently on the context's side streams, largest first
+  constexpr int NS = bwagpu_ctx::kA2Streams;
+  for (int i = 0; i < NS; ++i) {
+    if (!ctx->a2_st[i]) HIPC(hipStreamCreateWithFlags(&ctx->a2_st[i], hipStreamNonBlocking), "stream");
+    if (!ctx->a2_join[i]) HIPC(hipEventCreateWithFlags(&ctx->a2_join[i], hipEventDisableTiming), "event");
+  }
+  if (!ctx->a2_fork) HIPC(hipEventCreateWithFlags(&ctx->a2_fork, hipEventDisableTiming), "event");
+  struct Launch {
+    int bk, cls;
+    int32_t off;
+    int64_t work;
+  };
+  std::vector<Launch> launches;
+  {
+    int32_t off = 0;
+    for (int bk = 0; bk < kR2Buckets; ++bk)
+      for (int cls = 0; cls < 3; ++cls) {
+        const Bin& b = bins[bk][cls];
+        if (b.ids.empty()) continue;
+        int64_t w = 0;
+        for (int32_t k : b.ids) w += cost[(size_t)k];
+        launches.push_back({bk, cls, off, w});
+        off += (int32_t)b.ids.size();
+      }
+  }
+  std::sort(launches.begin(), launches.end(), [](const Launch& x, const Launch& y) { return x.work > y.work; });
+  const int used = std::min<int>(NS, (int)launches.size());
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIPC(hipEventCreate(&e0), "event");
   HIPC(hipEventCreate(&e1), "event");
   HIPC(hipEventRecord(e0, st), "event");
-  int32_t off = 0;
-  for (int bk = 0; bk < kR2Buckets; ++bk)
-    for (int cls = 0; cls < 3; ++cls) {
-      const Bin& b = bins[bk][cls];
-      const int nb = (int)b.ids.size();
-      if (!nb) continue;
-      R2AArgs a{};
-      a.tasks = ctx->r2_tasks.as<bwagpu_reg2aln_task_t>();
-      a.qpool = ctx->r2_q.as<uint8_t>();
-      a.list = ctx->r2_lists.as<int32_t>() + off;
-      a.n = nb;
-      a.max_ops = max_ops;
-      a.max_md = max_md;
-      a.out = ctx->r2_out.as<bwagpu_aln_t>();
-      a.cigar = ctx->r2_cig.as<uint32_t>();
-      a.md = ctx->r2_md.as<char>();
-      a.stats = ctx->r2_stats.as<int64_t>();
-      a.qcap = (b.qmax + 16) & ~15;
-      a.rcap = (b.rmax + 16) & ~15;
-      a.ocap = a.qcap + a.rcap + 4;
-      int lpw = a.qcap + a.rcap + 4 * a.ocap;
-      if (cls < 2) lpw += cls == 0 ? kR2ZSmall : kR2ZLarge;
-      a.lds_per_wave = (lpw + 15) & ~15;
-      if ((size_t)4 * a.lds_per_wave > 160 * 1024) {
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        return fail(ctx, BWAGPU_E_UNSUPPORTED, "reg2aln job needs more LDS than a workgroup has");
-      }
-      int waves = r2_resident_waves(kR2CD[bk], (size_t)4 * a.lds_per_wave);
-      if (cls == 2) {  // HBM matrices: one slice per resident wave, at most 1 GiB
-        a.zstride = (b.zmax + 255) & ~(int64_t)255;
-        waves = (int)std::min<int64_t>(waves, std::max<int64_t>(4, ((int64_t)1 << 30) / a.zstride));
-        HIPC(ctx->r2_z.ensure((size_t)a.zstride * waves), "hipMalloc(reg2aln matrices)");
-        a.zglob = ctx->r2_z.as<uint8_t>();
-      }
-      const int blocks = std::max(1, std::min((nb + 3) / 4, waves / 4));
-      HIPC(launch_reg2aln(kR2CD[bk], o, ctx->ref, a, blocks, st), "reg2aln launch");
-      off += nb;
+  HIPC(hipEventRecord(ctx->a2_fork, st), "event");
+  for (int i = 0; i < used; ++i) HIPC(hipStreamWaitEvent(ctx->a2_st[i], ctx->a2_fork, 0), "stream wait");
+  auto make_args = [&](const Launch& L, int& wpb) {
+    const Bin& b = bins[L.bk][L.cls];
+    R2AArgs a{};
+    a.tasks = ctx->r2_tasks.as<bwagpu_reg2aln_task_t>();
+    a.qpool = ctx->r2_q.as<uint8_t>();
+    a.list = ctx->r2_lists.as<int32_t>() + L.off;
+    a.n = (int)b.ids.size();
+    a.max_ops = max_ops;
+    a.max_md = max_md;
+    a.out = ctx->r2_out.as<bwagpu_aln_t>();
+    a.cigar = ctx->r2_cig.as<uint32_t>();
+    a.md = ctx->r2_md.as<char>();
+    a.stats = ctx->r2_stats.as<int64_t>();
+    a.qcap = (b.qmax + 16) & ~15;
+    a.rcap = (b.rmax + 16) & ~15;
+    a.ocap = a.qcap + a.rcap + 4;
+    int lpw = a.qcap + a.rcap + 4 * a.ocap;
+    if (L.cls < 2) lpw += L.cls == 0 ? kR2ZSmall : kR2ZLarge;
+    a.lds_per_wave = (lpw + 15) & ~15;
+    wpb = L.cls == 1 ? 1 : 4;  // LDS-heavy bins: one wave per workgroup packs LDS finer
+    a.zstride = L.cls == 2 ? ((b.zmax + 255) & ~(int64_t)255) : 0;
+    return a;
+  };
+  // grids first (HBM matrix slices: one per launched wave, at most 1 GiB per bin)
+  size_t zoff = 0;
+  for (Launch& L : launches) {
+    int wpb = 4;
+    const R2AArgs a = make_args(L, wpb);
+    if ((size_t)wpb * a.lds_per_wave > 160 * 1024) {
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, "reg2aln job needs more LDS than a workgroup has");
     }
+    int waves = r2_resident_waves(kR2CD[L.bk], (size_t)wpb * a.lds_per_wave, wpb);
+    if (L.cls == 2) {
+      waves = (int)std::min<int64_t>(waves, std::max<int64_t>(4, ((int64_t)1 << 30) / a.zstride));
+      zoff += (size_t)a.zstride * waves;
+    }
+    L.work = waves;
+  }
+  HIPC(ctx->r2_z.ensure(std::max<size_t>(zoff, 256)), "hipMalloc(reg2aln matrices)");
+  zoff = 0;
+  for (size_t li = 0; li < launches.size(); ++li) {
+    const Launch& L = launches[li];
+    int wpb = 4;
+    R2AArgs a = make_args(L, wpb);
+    const int nb = a.n, waves = (int)L.work;
+    if (L.cls == 2) {
+      a.zglob = ctx->r2_z.as<uint8_t>() + zoff;
+      zoff += (size_t)a.zstride * waves;
+    }
+    const int blocks = std::max(1, std::min((nb + wpb - 1) / wpb, waves / wpb));
+    HIPC(launch_reg2aln(kR2CD[L.bk], o, ctx->ref, a, blocks, wpb, ctx->a2_st[li % used]), "reg2aln launch");
+  }
+  for (int i = 0; i < used; ++i) {
+    HIPC(hipEventRecord(ctx->a2_join[i], ctx->a2_st[i]), "event");
+    HIPC(hipStreamWaitEvent(st, ctx->a2_join[i], 0), "stream wait");
+  }
   HIPC(hipEventRecord(e1, st), "event");
   HIPC(hipMemcpyAsync(out, ctx->r2_out.p, sizeof(bwagpu_aln_t) * n, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipMemcpyAsync(cigar, ctx->r2_cig.p, sizeof(uint32_t) * (size_t)n * max_ops, hipMemcpyDeviceToHost, st), "D2H");

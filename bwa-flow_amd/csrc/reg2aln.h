@@ -34,8 +34,9 @@ struct R2AArgs {
   int64_t* stats;        // ST_* words, may be NULL
 };
 
-int r2_resident_waves(int cd, size_t lds_per_block);
-hipError_t launch_reg2aln(int cd, const DevOpt& o, const DevRef& ref, const R2AArgs& a, int n_blocks,
+// wpb: waves per workgroup (1 for LDS-heavy bins: finer LDS packing per CU)
+int r2_resident_waves(int cd, size_t lds_per_block, int wpb);
+hipError_t launch_reg2aln(int cd, const DevOpt& o, const DevRef& ref, const R2AArgs& a, int n_blocks, int wpb,
                           hipStream_t st);
 
 }  // namespace bwagpu

@@ -260,8 +260,8 @@ template <int CD>
 __global__ void __launch_bounds__(256) reg2aln_kernel(DevOpt o, DevRef ref, R2AArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = (int)(threadIdx.x & 63);
-  const int wib = uni((int)(threadIdx.x >> 6));
-  const int wave = (int)blockIdx.x * 4 + wib, nwaves = (int)gridDim.x * 4;
+  const int wib = uni((int)(threadIdx.x >> 6)), wpb = (int)(blockDim.x >> 6);
+  const int wave = (int)blockIdx.x * wpb + wib, nwaves = (int)gridDim.x * wpb;
   uint8_t* const wl = lds + (size_t)wib * a.lds_per_wave;
   uint8_t* const q = wl;                                               // qcap bytes
   uint8_t* const r = wl + a.qcap;                                      // rcap bytes
@@ -535,27 +535,28 @@ __global__ void __launch_bounds__(256) reg2aln_kernel(DevOpt o, DevRef ref, R2AA
 
 const int kR2CD[kR2Buckets] = {1, 2, 3, 4, 8, 16};
 
-int r2_resident_waves(int cd, size_t lds_per_block) {
+int r2_resident_waves(int cd, size_t lds_per_block, int wpb) {
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 4096;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 4096;
   hipError_t e = hipErrorInvalidValue;
   switch (cd) {
 #define R2_OCC(C) \
-  case C: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reg2aln_kernel<C>, 256, lds_per_block); break;
+  case C: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reg2aln_kernel<C>, 64 * wpb, lds_per_block); break;
     R2_OCC(1) R2_OCC(2) R2_OCC(3) R2_OCC(4) R2_OCC(8) R2_OCC(16)
 #undef R2_OCC
   }
   if (e != hipSuccess || per < 1) per = 1;
-  return per * ncu * 4;
+  return per * ncu * wpb;
 }
 
-hipError_t launch_reg2aln(int cd, const DevOpt& o, const DevRef& ref, const R2AArgs& a, int n_blocks, hipStream_t st) {
-  const size_t lds = 4 * (size_t)a.lds_per_wave;
+hipError_t launch_reg2aln(int cd, const DevOpt& o, const DevRef& ref, const R2AArgs& a, int n_blocks, int wpb,
+                          hipStream_t st) {
+  const size_t lds = (size_t)wpb * a.lds_per_wave;
   switch (cd) {
 #define R2_LAUNCH(C)                                                                                   \
   case C:                                                                                              \
-    hipLaunchKernelGGL((reg2aln_kernel<C>), dim3(n_blocks), dim3(256), lds, st, o, ref, a);            \
+    hipLaunchKernelGGL((reg2aln_kernel<C>), dim3(n_blocks), dim3(64 * wpb), lds, st, o, ref, a);            \
     return hipGetLastError();
     R2_LAUNCH(1) R2_LAUNCH(2) R2_LAUNCH(3) R2_LAUNCH(4) R2_LAUNCH(8) R2_LAUNCH(16)
 #undef R2_LAUNCH
