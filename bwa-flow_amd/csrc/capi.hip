@@ -114,6 +114,9 @@ struct bwagpu_ctx {
   int32_t* d_ann_len = nullptr;
   int watchdog_ms = 10000;
   Slot slot[BWAGPU_NUM_SLOTS];
+  // bwagpu_chain2aln_device: the caller's streams, one per slot's scratch (a
+  // stream always reuses the same scratch, so its launches never race)
+  hipStream_t dev_stream[BWAGPU_NUM_SLOTS] = {};
   // ksw_align2 batches (bwagpu_align2_*): grow-only, reused across calls
   DevBuf a2_tasks, a2_q, a2_t, a2_out, a2_scratch, a2_lists, a2_counts, a2_boff;
   // mem_reg2aln batches (bwagpu_reg2aln_batch)
@@ -582,8 +585,12 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwag
                             int32_t* dev_n, int64_t* dev_stats, void* stream) {
   if (!ctx || !db_in || !dev_out || !dev_n) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  Slot& s = ctx->slot[0];
-  hipStream_t st = stream ? (hipStream_t)stream : s.stream;
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  int k = 0;
+  while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] && ctx->dev_stream[k] != st) ++k;
+  if (k == BWAGPU_NUM_SLOTS) return fail(ctx, BWAGPU_E_INVAL, "more than BWAGPU_NUM_SLOTS streams on one context");
+  ctx->dev_stream[k] = st;
+  Slot& s = ctx->slot[k];
   DevBatch db;
   db.n_reads = db_in->n_reads;
   db.n_chains = db_in->n_chains;

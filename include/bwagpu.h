@@ -246,7 +246,9 @@ int bwagpu_chain2aln(bwagpu_ctx_t *ctx, const bwagpu_batch_t *batch, bwagpu_alnr
                      int32_t *out_n);
 /* all pointers in dev_batch / dev_out / dev_n are device pointers; stream is a
    hipStream_t (NULL = the context's slot-0 stream); asynchronous; dev_stats
-   (device, 4 x int64: cells, rows, ext_calls, error flag) may be NULL */
+   (device, 4 x int64: cells, rows, ext_calls, error flag) may be NULL.
+   Up to BWAGPU_NUM_SLOTS distinct streams may be used on one context (each
+   keeps its own scratch), so consecutive batches can overlap. */
 int bwagpu_chain2aln_device(bwagpu_ctx_t *ctx, const bwagpu_batch_t *dev_batch,
                             bwagpu_alnreg_t *dev_out, int32_t *dev_n, int64_t *dev_stats,
                             void *stream);
