@@ -1300,7 +1300,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
               fetched = true;
             }
             int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
-            int aw[2] = {o.w, o.w};
+            int aw0 = o.w, aw1 = o.w;  // the band of each side (scalars: an indexed pair would live in scratch)
             int64_t rb = srb, re = srb + slen;
 #pragma nounroll
             for (int side = 0; side < 2; ++side) {
@@ -1321,11 +1321,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
               ExtOut x{};
               for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY (bwamem.c:639)
                 const int prev = score;
-                aw[side] = o.w << t;
-                x = extend_wave_dispatch<C, false>(o, qlen, sq, qa, left ? -1 : 1, tlen, tb, aw[side], eb, o.zdrop,
-                                                   h0, tl);
+                const int aw = o.w << t;
+                aw0 = left ? aw : aw0;
+                aw1 = left ? aw1 : aw;
+                x = extend_wave_dispatch<C, false>(o, qlen, sq, qa, left ? -1 : 1, tlen, tb, aw, eb, o.zdrop, h0,
+                                                   tl);
                 score = x.score;
-                if (score == prev || x.max_off < (aw[side] >> 1) + (aw[side] >> 2)) break;
+                if (score == prev || x.max_off < (aw >> 1) + (aw >> 2)) break;
               }
               const bool local = x.gscore <= 0 || x.gscore <= score - eb;
               if (left) {
@@ -1362,7 +1364,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
               v = dw == 6 ? (uint32_t)rid : v;
               v = dw == 7 ? (uint32_t)score : v;
               v = dw == 8 ? (uint32_t)truesc : v;
-              v = dw == 13 ? (uint32_t)(aw[0] > aw[1] ? aw[0] : aw[1]) : v;
+              v = dw == 13 ? (uint32_t)(aw0 > aw1 ? aw0 : aw1) : v;
               v = dw == 14 ? (uint32_t)cov : v;
               v = dw == 17 ? (uint32_t)slen : v;
               v = dw == 19 ? __float_as_uint(frac) : v;
