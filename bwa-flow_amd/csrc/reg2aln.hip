@@ -391,7 +391,11 @@ __global__ void __launch_bounds__(256) reg2aln_kernel(DevOpt o, DevRef ref, R2AA
         }
         if (f < 64 && i >= 0 && kk >= 0) {  // one serial step at the run's end (reference addressing)
           const int lo_i = i > wdp ? i - wdp : 0;
-          const int dd = uni((int)z[(size_t)i * ncol + (kk - lo_i)]);
+          // a walk that leaves the band reads outside the row in the reference
+          // (undefined there); here the index stays inside the matrix
+          int64_t zi = (int64_t)i * ncol + (kk - lo_i);
+          zi = zi < 0 ? 0 : (zi >= (int64_t)ncol * rl ? (int64_t)ncol * rl - 1 : zi);
+          const int dd = uni((int)z[zi]);
           st = (dd >> (st << 1)) & 3;
           emit(st == 0 ? 0 : (st == 1 ? 2 : 1), 1);
           i -= st != 2;
