@@ -181,9 +181,6 @@ bool make_opt(const bwagpu_opt_t* o, DevOpt* d, std::string* why) {
     d->qprof[q] = w;
     d->qprof4[q] = o->mat[20 + q];
   }
-  const char* p2 = getenv("BWAGPU_EXT_P2");
-  const char* p4 = getenv("BWAGPU_EXT_P4");
-  d->p2 = (p2 && p2[0] == '1' ? 1 : 0) | (p4 && p4[0] == '1' ? 2 : 0);  // measured slower: opt-in
   return true;
 }
 

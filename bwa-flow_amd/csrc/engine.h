@@ -19,10 +19,6 @@ struct DevOpt {
   // its scores with register selects instead of loads.
   uint32_t qprof[5];
   int32_t qprof4[5];
-  // packed 16-bit extension bodies for calls whose values fit int16: bit 0 for
-  // two segments, bit 1 for three and four (extend_wave_pk<1|2>); opt-in with
-  // BWAGPU_EXT_P2=1 / BWAGPU_EXT_P4=1 (bit-exact, measured 3-4 % slower)
-  int32_t p2;
 };
 
 // One read in processing order (chain2aln_fast_kernel), written after the sort.

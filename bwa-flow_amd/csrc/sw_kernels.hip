@@ -332,217 +332,6 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
 }
 
-// ------------------------------------------------ ksw_extend2, packed 16-bit columns
-// Two to four segments (64 <= qlen < 256; the two-segment calls alone hold
-// 44 % of a C2 batch's DP rows) with half the elementwise VALU work.  Lane r
-// owns CPL = 2*NP ADJACENT columns j0 = CPL*r .. j0+CPL-1 in NP registers per
-// DP quantity (register k: columns j0+2k and j0+2k+1 as its low and high
-// halves), and M, u, F, H and E step through v_pk_* 16-bit ops.  A call takes
-// this body only when every value stays below 16000 (pk_fits: h0 +
-// qlen*max_mat plus the gap terms of 64*CPL columns), so no 16-bit sum wraps
-// and the outputs are extend_wave's.  Differences from extend_wave:
-//  * S(t, q_j) is one v_perm_b32 of two offset-binary profile words (byte t of
-//    each, zero-extended) minus 128 per half;
-//  * M = (H + S) * min(H, 1): the reference's `M ? M + q : 0` without a select;
-//  * the band is a 0xffff / 0 mask per half, applied with v_bfi_b32;
-//  * ONE F scan per row over the lanes' maxima of their CPL u values (the
-//    32-bit body runs one per segment), then the lane's in-register prefix;
-//  * H(i, j-1) is one DPP shift plus one v_alignbit per register;
-//  * the band trim reads ballots of the masked halves (VALU compares) instead
-//    of shifting lane masks on the scalar unit.
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ s16x2 as_s2(int x) { return __builtin_bit_cast(s16x2, x); }
-__device__ __forceinline__ u16x2 as_u2(int x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ int as_i(s16x2 x) { return __builtin_bit_cast(int, x); }
-__device__ __forceinline__ int as_i(u16x2 x) { return __builtin_bit_cast(int, x); }
-// (lo, hi) 16-bit halves in one v_perm_b32; pdup(x) = (x, x) for 0 <= x < 65536
-__device__ __forceinline__ int pk2(int lo, int hi) {
-  return (int)__builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
-}
-__device__ __forceinline__ int pdup(int x) { return x << 16 | x; }
-__device__ __forceinline__ int bfi(int m, int a, int b) { return (a & m) | (b & ~m); }
-
-template <int NP>
-__device__ __forceinline__ bool pk_fits(const DevOpt& o, int qlen, int h0) {
-  return h0 >= 0 && h0 < 16000 &&
-         h0 + qlen * o.max_mat + 128 * NP * (o.e_ins + o.e_del) + o.oe_ins + o.oe_del < 16000;
-}
-
-template <int NP>
-__device__ __forceinline__ ExtOut extend_wave_pk(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
-                                                 int qd, int tlen, const uint8_t* tb, int w, int end_bonus,
-                                                 int zdrop, int h0, Tally& tl) {
-  constexpr int CPL = 2 * NP;  // 2 or 4: lane of column j = j >> NP
-  const int r = (int)(threadIdx.x & 63);
-  const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
-  const int j0 = CPL * r;
-  uint32_t PB[CPL];  // offset-binary profile words: byte t = S(t, q_j) + 128
-  int HH[NP], EE[NP], KC[NP], JE[NP], FC[NP], JP[NP];
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int j = j0 + c;
-    PB[c] = qprof_word(o, j < qlen ? qp[qa + qd * j] : 0) ^ 0x80808080u;
-  }
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const int a = j0 + 2 * k, b = a + 1;
-    // row -1 of eh[] (ksw.c:392-395)
-    const int va = a == 0 ? h0 : max(h0 - oe_ins - (a - 1) * e_ins, 0);
-    const int vb = max(h0 - oe_ins - (b - 1) * e_ins, 0);
-    HH[k] = pk2(a <= qlen ? va : 0, b <= qlen ? vb : 0);
-    EE[k] = 0;
-    KC[k] = pk2(a * e_ins - oe_ins, b * e_ins - oe_ins);  // u = max(M + KC, JE) in band, JE outside
-    JE[k] = pk2(a * e_ins, b * e_ins);
-    FC[k] = pk2(e_ins - a * e_ins, e_ins - b * e_ins);  // F = EX + FC
-    JP[k] = pk2(a, b);
-  }
-  const int EDEL = pdup(e_del), OEDEL = pdup(oe_del);
-  {  // band clamp (ksw.c:399-407)
-    const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
-    const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, e_del);
-    w = __builtin_amdgcn_readfirstlane(min(w, min(mi, md)));
-  }
-  int best = vgpr(h0), bi = vgpr(-1), bj = vgpr(-1), ei = vgpr(-1), esc = vgpr(-1), off = vgpr(0);
-  int lo = vgpr(0), hi = vgpr(qlen);
-  int iw = vgpr(-w), iw1 = vgpr(w + 1);
-  int gl = vgpr(h0 - o.o_del - e_del);
-  int vi = vgpr(0);
-  int cells = vgpr(0);
-  int rows = tlen;
-  int tnext = tlen > 0 ? tb[0] : 0;
-  const s16x2 k128 = {128, 128}, zero2 = {0, 0};
-  const u16x2 one2 = {1, 1}, ffff2 = {0xffff, 0xffff};
-  for (int i = 0; i < tlen; ++i) {
-    const int t = __builtin_amdgcn_readfirstlane(tnext);
-    tnext = tb[i + 1];
-    lo = max(lo, iw);
-    hi = min(min(hi, iw1), qlen);
-    iw += 1;
-    iw1 += 1;
-    const int wd = usat32(hi, lo);
-    const int left0 = lo == 0 ? max(gl, 0) : 0;
-    gl -= e_del;
-    // byte t of PB[2k] -> low half, byte t of PB[2k+1] -> high half
-    const uint32_t sel = 0x0c040c00u + (uint32_t)(t & 3) * 0x10001u;
-    const u16x2 lo2 = as_u2(pdup(lo)), wd2 = as_u2(pdup(wd));
-    s16x2 m[NP];
-    int MASK[NP], uu[CPL];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const s16x2 sc = as_s2((int)__builtin_amdgcn_perm(PB[2 * k + 1], PB[2 * k], sel)) - k128;
-      // M = hh ? hh + S : 0 per half
-      m[k] = (as_s2(HH[k]) + sc) * as_s2(as_i(__builtin_elementwise_min(as_u2(HH[k]), one2)));
-      // in band: (j - lo) < wd per half, as 0xffff / 0
-      MASK[k] = as_i(__builtin_elementwise_min(__builtin_elementwise_sub_sat(wd2, as_u2(JP[k]) - lo2), one2) * ffff2);
-      const int U = bfi(MASK[k], as_i(__builtin_elementwise_max(m[k] + as_s2(KC[k]), as_s2(JE[k]))), JE[k]);
-      uu[2 * k] = (int)(short)(U & 0xffff);
-      uu[2 * k + 1] = U >> 16;
-    }
-    // the exclusive F scan over the lanes' maxima, then the in-lane prefix
-    int T = uu[0];
-#pragma unroll
-    for (int c = 1; c < CPL; ++c) T = max(T, uu[c]);
-    T = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(T))))));
-    int X[CPL];
-    X[0] = dpp<DPP_WAVE_SHR1>(-16384, T);
-#pragma unroll
-    for (int c = 1; c < CPL; ++c) X[c] = max(X[c - 1], uu[c - 1]);
-    int rk = 0, g[NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const s16x2 ee = as_s2(EE[k]);
-      const s16x2 f = as_s2(pk2(X[2 * k], X[2 * k + 1])) + as_s2(FC[k]);
-      const s16x2 h = __builtin_elementwise_max(__builtin_elementwise_max(m[k], ee), f);
-      const s16x2 en = __builtin_elementwise_max(
-          __builtin_elementwise_max(ee - as_s2(EDEL), m[k] - as_s2(OEDEL)), zero2);
-      g[k] = as_i(h);
-      // row max + last argmax over the in-band columns (H >= 0; out-of-band halves read 0)
-      const int HM = g[k] & MASK[k];
-      rk = max(rk, max((HM & 0xffff) << 10 | (j0 + 2 * k), (int)((unsigned)HM >> 16) << 10 | (j0 + 2 * k + 1)));
-      EE[k] = bfi(MASK[k], as_i(en), EE[k]);
-    }
-    // H(i, j-1): one half down; column j0 takes lane r-1's last high half
-    int HS[NP];
-    HS[0] = (int)__builtin_amdgcn_alignbit((uint32_t)g[0], (uint32_t)dpp<DPP_WAVE_SHR1>(0, g[NP - 1]), 16);
-#pragma unroll
-    for (int k = 1; k < NP; ++k) HS[k] = (int)__builtin_amdgcn_alignbit((uint32_t)g[k], (uint32_t)g[k - 1], 16);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) HH[k] = bfi(MASK[k], HS[k], HH[k]);
-    // h1 = H(i, hi-1) = column hi of HS: register (hi >> 1) & (NP-1), lane hi >> NP
-    const int hi_s = __builtin_amdgcn_readfirstlane(hi);
-    const int kh = (hi_s >> 1) & (NP - 1);
-    const int hsv = __builtin_amdgcn_readlane(kh == 0 ? HS[0] : HS[NP - 1], hi_s >> NP);
-    const int h1r = (hi_s & 1) ? (int)((unsigned)hsv >> 16) : (hsv & 0xffff);
-    const int h1 = hi > lo ? h1r : left0;
-    // eh[lo].h = first-column value (only when lo < hi), eh[hi] = {h1, 0}
-    const int tlo = hi > lo ? lo : -1;
-    const int kl = (tlo >> 1) & (NP - 1);
-    const int mlo = (tlo & 1) ? (int)0xffff0000 : 0xffff;
-    const int mhi = (hi_s & 1) ? (int)0xffff0000 : 0xffff;
-    const bool atl = tlo >= 0 && r == (tlo >> NP), ath = r == (hi_s >> NP);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      HH[k] = (atl && kl == k) ? bfi(mlo, pdup(left0), HH[k]) : HH[k];
-      const bool ah = ath && kh == k;
-      HH[k] = ah ? bfi(mhi, pdup(h1), HH[k]) : HH[k];
-      EE[k] = ah ? (EE[k] & ~mhi) : EE[k];
-    }
-    // zero-trim of the band (ksw.c:466-469): the first non-zero column in
-    // [lo, hi) and the last in [lo, hi], from ballots of the masked halves
-    int nlo, nhi;
-    {
-      int c0 = 1 << 20, jl = -1;
-#pragma unroll
-      for (int k = 0; k < NP; ++k) {
-        const int NZ = HH[k] | EE[k];
-        const int NF = NZ & MASK[k], NL = NZ & ((ath && kh == k) ? (MASK[k] | mhi) : MASK[k]);
-        const uint64_t fa = __builtin_amdgcn_ballot_w64((NF & 0xffff) != 0);
-        const uint64_t fb = __builtin_amdgcn_ballot_w64(((unsigned)NF >> 16) != 0);
-        const uint64_t la = __builtin_amdgcn_ballot_w64((NL & 0xffff) != 0);
-        const uint64_t lb = __builtin_amdgcn_ballot_w64(((unsigned)NL >> 16) != 0);
-        c0 = min(c0, fa ? CPL * __builtin_ctzll(fa) + 2 * k : 1 << 20);
-        c0 = min(c0, fb ? CPL * __builtin_ctzll(fb) + 2 * k + 1 : 1 << 20);
-        jl = max(jl, la ? CPL * (63 - __builtin_clzll(la)) + 2 * k : -1);
-        jl = max(jl, lb ? CPL * (63 - __builtin_clzll(lb)) + 2 * k + 1 : -1);
-      }
-      nlo = min(c0, hi_s);
-      if (jl < 0) jl = nlo - 1;
-      nhi = min(jl + 2, qlen);
-    }
-    rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
-    rk = __builtin_amdgcn_readlane(rk, 63);
-    cells += wd;
-    {  // ksw.c:450-453
-      const bool atend = max(lo, hi) == qlen;
-      ei = (atend && !(esc > h1)) ? vi : ei;
-      esc = atend ? max(esc, h1) : esc;
-    }
-    // ksw.c:454-465 (see extend_wave: updates before the single exit test)
-    const int mrow = rk >> 10, mj = rk & 1023;
-    const bool up = mrow > best;
-    const int di = vi - bi, dj = mj - bj;
-    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
-    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
-    off = up ? max(off, abs(mj - vi)) : off;
-    best = up ? mrow : best;
-    bi = up ? vi : bi;
-    bj = up ? mj : bj;
-    vi += 1;
-    lo = nlo;
-    hi = nhi;
-    if (__builtin_amdgcn_ballot_w64(brk)) {
-      rows = i + 1;
-      break;
-    }
-  }
-  tl.cells += __builtin_amdgcn_readfirstlane(cells);
-  tl.rows += rows;
-  tl.calls += 1;
-  auto u = [](int x) { return __builtin_amdgcn_readfirstlane(x); };
-  return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
-}
-
 // CD is uniform per call (qlen is): one compiled body per segment count
 template <int C, bool T5>
 __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp,
@@ -557,12 +346,6 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
   zdrop = __builtin_amdgcn_readfirstlane(zdrop);
   h0 = __builtin_amdgcn_readfirstlane(h0);
   const int cd = (qlen + 64) >> 6;  // ceil((qlen+1)/64)
-  if constexpr (!T5 && C >= 2) {
-    if (cd == 2 && (o.p2 & 1) && pk_fits<1>(o, qlen, h0))
-      return extend_wave_pk<1>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
-    if (cd >= 3 && cd <= 4 && (o.p2 & 2) && pk_fits<2>(o, qlen, h0))
-      return extend_wave_pk<2>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
-  }
 #define EXT_SEG(n) \
   if (n <= C && cd == n) return extend_wave<(n <= C ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
   EXT_SEG(1) EXT_SEG(2) EXT_SEG(3) EXT_SEG(4) EXT_SEG(5) EXT_SEG(6) EXT_SEG(7) EXT_SEG(8)

@@ -228,65 +228,3 @@ def test_many_seed_reads_vs_oracle(len_mode, piece, c2a_path):
     assert np.array_equal(n, on)
     assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
     eng.close()
-
-
-def _packed_tasks(rng, n, qlo, qhi):
-    """ksw_extend2 tasks with qlen in [qlo, qhi): mostly the query itself with
-    substitutions, one short indel and a random tail as the target, every
-    fourth an unrelated target; h0 on both sides of the int16 range tests"""
-    tasks = np.zeros(n, abi.EXT_TASK_DTYPE)
-    qs, ts, qo, to = [], [], 0, 0
-    for k in range(n):
-        ql = int(rng.integers(qlo, qhi))
-        q = rng.integers(0, 4, ql).astype(np.uint8)
-        q[rng.random(ql) < 0.01] = 4
-        if k % 4 == 3:
-            t = rng.integers(0, 4, int(rng.integers(1, 300))).astype(np.uint8)
-        else:
-            t = np.where(rng.random(ql) < 0.04, rng.integers(0, 4, ql), np.minimum(q, 3)).astype(np.uint8)
-            cut, dl = int(rng.integers(0, ql)), int(rng.integers(0, 3))
-            ins = rng.integers(0, 4, int(rng.integers(0, 4))).astype(np.uint8)
-            tail = rng.integers(0, 4, int(rng.integers(0, 40))).astype(np.uint8)
-            t = np.concatenate([t[:cut], ins, t[cut + dl:], tail])
-        h0 = int(rng.choice([1, 30, 150, 12000, 15000, 15950, 16050, 40000]))
-        tasks[k] = (qo, to, ql, len(t), int(rng.choice([2, 10, 50, 100])), int(rng.choice([0, 5])),
-                    int(rng.choice([0, 20, 100])), h0)
-        qs.append(q)
-        ts.append(t)
-        qo += ql
-        to += len(t)
-    return tasks, np.concatenate(qs), np.concatenate(ts)
-
-
-def _packed_vs_oracle(refd, opt_set, packed, monkeypatch, qlo, qhi, seed):
-    monkeypatch.setenv("BWAGPU_EXT_WAVE", "1")
-    for v in ("BWAGPU_EXT_P2", "BWAGPU_EXT_P4"):
-        monkeypatch.setenv(v, "1" if packed == "on" else "0")
-    opt = G.load_tasks(opt_set)[0]
-    tasks, qp, tp = _packed_tasks(np.random.default_rng(seed), 700, qlo, qhi)
-    eng = make_engine(refd, opt)
-    got = eng.extend_batch(tasks, qp, tp)
-    want, cells = oracle.extend("oracle", opt, tasks, qp, tp)
-    g, w = got.view(np.int32).reshape(-1, 6), want.view(np.int32).reshape(-1, 6)
-    bad = np.nonzero((g != w).any(axis=1))[0]
-    assert len(bad) == 0, f"{len(bad)} tasks differ; first {tasks[bad[0]]}: got {got[bad[0]]} want {want[bad[0]]}"
-    st = eng.last_stats()
-    assert st["cells"] == cells[0] and st["rows"] == cells[1]
-    eng.close()
-
-
-@pytest.mark.parametrize("packed", ["on", "off"])
-@pytest.mark.parametrize("opt_set", ["ksw_edge_default", "ksw_edge_scoring"])
-def test_packed_two_segment_vs_oracle(refd, opt_set, packed, monkeypatch):
-    """64 <= qlen < 128 on the wave kernels: the packed 16-bit body
-    (extend_wave_pk<1>, BWAGPU_EXT_P2=1) and the 32-bit one (default) against
-    the oracle; h0 near the int16 limit sends calls to both bodies"""
-    _packed_vs_oracle(refd, opt_set, packed, monkeypatch, 64, 128, 6402)
-
-
-@pytest.mark.parametrize("packed", ["on", "off"])
-@pytest.mark.parametrize("opt_set", ["ksw_edge_default", "ksw_edge_scoring"])
-def test_packed_four_column_vs_oracle(refd, opt_set, packed, monkeypatch):
-    """128 <= qlen < 256 (three and four segments): extend_wave_pk<2>
-    (BWAGPU_EXT_P4=1) and the 32-bit bodies (default) against the oracle"""
-    _packed_vs_oracle(refd, opt_set, packed, monkeypatch, 128, 256, 6404)
