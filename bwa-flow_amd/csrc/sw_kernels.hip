@@ -1209,7 +1209,10 @@ constexpr int kRegBytes = 88 * kFastMaxSeeds;  // LDS region records per wave
 constexpr int kFastWaveLds(int tb) { return 2 * LaneTab::BYTES + kRegBytes + 2 * tb; }
 
 template <int C>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
+#ifndef BWAGPU_FAST_WPE
+#define BWAGPU_FAST_WPE 5  // waves per SIMD the fast kernel is compiled for (A/B builds override)
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWAGPU_FAST_WPE))) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
                                                                 int variant, int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int r = (int)(threadIdx.x & 63);
