@@ -94,6 +94,12 @@ struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
+  DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
+  void release_scratch() {
+    d_win.release(); d_srt.release(); d_prog.release(); d_desc.release(); d_lists.release(); d_counts.release();
+    d_cread.release(); d_ext.release(); d_tasks.release(); d_ctr.release(); d_regpos.release(); d_skipf.release();
+    d_heavy.release(); d_redo.release();
+  }
   HostBuf h_in, h_out, h_n, h_stats;
   bool busy = false;
   int32_t n_reads = 0, n_seeds = 0;
@@ -117,6 +123,10 @@ struct bwagpu_ctx {
   // bwagpu_chain2aln_device: the caller's streams, one per slot's scratch (a
   // stream always reuses the same scratch, so its launches never race)
   hipStream_t dev_stream[BWAGPU_NUM_SLOTS] = {};
+  // ... and its own scratch (only the Dev buffers of these are used): the
+  // submit/wait path's slots never share scratch with the device entry, so the
+  // two entry points may run concurrently on one context
+  Slot dev_scratch[BWAGPU_NUM_SLOTS];
   // ksw_align2 batches (bwagpu_align2_*): grow-only, reused across calls
   DevBuf a2_tasks, a2_q, a2_t, a2_out, a2_scratch, a2_lists, a2_counts, a2_boff;
   // mem_reg2aln batches (bwagpu_reg2aln_batch)
@@ -268,15 +278,20 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   (void)hipSetDevice(ctx->device);
   for (auto& s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
-    s.d_in.release(); s.d_win.release(); s.d_srt.release(); s.d_prog.release(); s.d_desc.release();
-    s.d_out.release(); s.d_n.release();
-    s.d_stats.release(); s.d_lists.release(); s.d_counts.release();
+    s.d_in.release(); s.release_scratch();
+    s.d_out.release(); s.d_n.release(); s.d_stats.release();
     s.h_in.release(); s.h_out.release(); s.h_n.release(); s.h_stats.release();
     if (s.ev0) (void)hipEventDestroy(s.ev0);
     if (s.ev1) (void)hipEventDestroy(s.ev1);
     if (s.ev2) (void)hipEventDestroy(s.ev2);
     if (s.ev3) (void)hipEventDestroy(s.ev3);
     if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  for (int k = 0; k < BWAGPU_NUM_SLOTS; ++k) {
+    if (ctx->dev_stream[k]) (void)hipStreamSynchronize(ctx->dev_stream[k]);
+    Slot& s = ctx->dev_scratch[k];
+    s.release_scratch();
+    s.d_stats.release();
   }
   for (int i = 0; i < bwagpu_ctx::kA2Streams; ++i) {
     if (ctx->a2_st[i]) (void)hipStreamSynchronize(ctx->a2_st[i]);
@@ -346,10 +361,91 @@ int tb_bytes_for(const DevOpt& o, int lq_max) {
   return (n + 15) & ~15;
 }
 
+// BWAGPU_C2A_PATH=fast: the wave-per-read kernels (chain2aln_fast_kernel /
+// chain2aln_kernel, DESIGN.md §3 "per-read kernels"); default: the speculative
+// path (extension tasks + selection passes)
+bool use_read_kernels() {
+  const char* e = getenv("BWAGPU_C2A_PATH");
+  return e && (strcmp(e, "fast") == 0 || strcmp(e, "read") == 0);
+}
+
+bool use_grp_kernels() {
+  // BWAGPU_C2A_GRP=1: the 16-lane group kernels for reads <= 256 bp instead of
+  // the wave-per-read kernels (bit-identical; slower on C2 — DESIGN.md §3)
+  const char* eg = getenv("BWAGPU_C2A_GRP");
+  return eg && eg[0] == '1';
+}
+
+// dynamic LDS bytes of variant v's launch for reads up to lq_max
+size_t variant_lds(const DevOpt& o, int v, int lq_max) {
+  const Variant& vk = kVariants[v];
+  const int lqv = std::min(lq_max, vk.kind == VK_GRP ? 256 : vk.max_len());
+  const int tb = tb_bytes_for(o, std::max(lqv, 1));
+  return vk.kind == VK_FAST  ? (size_t)(kBlock / 64) * fast_wave_lds(tb)
+         : vk.kind == VK_GRP ? (size_t)(kBlock / 16) * grp_group_lds(tb)
+                             : (size_t)tb * (kBlock / vk.G);
+}
+
+// Options that need more LDS per workgroup than a launch may take are refused
+// BEFORE anything is enqueued (a refusal after the H2D would leave a DMA
+// reading the slot's pinned staging buffer while the caller reuses the slot).
+int check_lds(bwagpu_ctx_t* ctx, int lq_max) {
+  if (!use_read_kernels()) {
+    if (spec_select_lds(tb_bytes_for(ctx->opt, std::max(lq_max, 1))) > 64 * 1024)
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
+    return BWAGPU_OK;
+  }
+  const bool grp = use_grp_kernels();
+  for (int v = 0; v < kNumVariants; ++v) {
+    const Variant& vk = kVariants[v];
+    if ((vk.kind == VK_GRP) != grp && vk.kind != VK_GENERIC) continue;
+    if (variant_lds(ctx->opt, v, lq_max) > 64 * 1024)
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
+  }
+  return BWAGPU_OK;
+}
+
+int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwagpu_alnreg_t* d_out, int32_t* d_n,
+                 int64_t* d_stats, hipStream_t st) {
+  const size_t nc = (size_t)std::max(db.n_chains, 1), ns = (size_t)std::max(db.n_seeds, 1),
+               nr = (size_t)std::max(db.n_reads, 1);
+  HIPC(s.d_win.ensure(sizeof(ChainWin) * nc), "hipMalloc(win)");
+  HIPC(s.d_cread.ensure(sizeof(int32_t) * nc), "hipMalloc(chain_read)");
+  HIPC(s.d_prog.ensure(sizeof(bwagpu_seed_t) * ns), "hipMalloc(prog)");
+  HIPC(s.d_ext.ensure(sizeof(SeedExt) * ns), "hipMalloc(ext)");
+  HIPC(s.d_tasks.ensure(sizeof(int2) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(tasks)");
+  HIPC(s.d_ctr.ensure(sizeof(int32_t) * SPC_WORDS), "hipMalloc(ctr)");
+  HIPC(s.d_regpos.ensure(sizeof(int32_t) * ns), "hipMalloc(regpos)");
+  HIPC(s.d_skipf.ensure(sizeof(int32_t) * ns), "hipMalloc(skipf)");
+  HIPC(s.d_heavy.ensure(sizeof(int32_t) * nr), "hipMalloc(heavy)");
+  HIPC(s.d_redo.ensure(sizeof(int32_t) * nr), "hipMalloc(redo)");
+  HIPC(hipMemsetAsync(s.d_ctr.p, 0, sizeof(int32_t) * SPC_WORDS, st), "memset ctr");
+  if (db.n_seeds) HIPC(hipMemsetAsync(s.d_ext.p, 0, sizeof(SeedExt) * (size_t)db.n_seeds, st), "memset ext");
+  if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
+  SpecArgs a;
+  a.win = s.d_win.as<ChainWin>();
+  a.chain_read = s.d_cread.as<int32_t>();
+  a.prog = s.d_prog.as<bwagpu_seed_t>();
+  a.ext = s.d_ext.as<SeedExt>();
+  a.tasks = s.d_tasks.as<int2>();
+  a.ctr = s.d_ctr.as<int32_t>();
+  a.regpos = s.d_regpos.as<int32_t>();
+  a.skipf = s.d_skipf.as<int32_t>();
+  a.heavy = s.d_heavy.as<int32_t>();
+  a.redo = s.d_redo.as<int32_t>();
+  a.out = d_out;
+  a.out_n = d_n;
+  a.stats = d_stats;
+  const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
+  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, st), "spec chain2aln launch");
+  return BWAGPU_OK;
+}
+
 // enqueue prep + binning + the per-variant kernels for a batch whose arrays
-// are already in device memory
+// are already in device memory (check_lds has passed for lq_max)
 int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwagpu_alnreg_t* d_out,
                       int32_t* d_n, int64_t* d_stats, hipStream_t st) {
+  if (!use_read_kernels()) return enqueue_spec(ctx, s, db, lq_max, d_out, d_n, d_stats, st);
   HIPC(s.d_win.ensure(sizeof(ChainWin) * (size_t)std::max(db.n_chains, 1)), "hipMalloc(win)");
   HIPC(s.d_srt.ensure(sizeof(uint64_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(srt)");
   HIPC(s.d_prog.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max(db.n_seeds, 1)), "hipMalloc(prog)");
@@ -365,10 +461,7 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(),
                          s.d_prog.as<bwagpu_seed_t>(), d_stats, st),
        "chain_prep launch");
-  // BWAGPU_C2A_GRP=1: the 16-lane group kernels for reads <= 256 bp instead of
-  // the wave-per-read kernels (bit-identical; slower on C2 — DESIGN.md §3)
-  const char* eg = getenv("BWAGPU_C2A_GRP");
-  const bool grp = eg && eg[0] == '1';
+  const bool grp = use_grp_kernels();
   HIPC(launch_read_order(db, bins, s.d_counts.as<int32_t>() + kHistOff, s.d_counts.as<int32_t>(),
                          s.d_desc.as<ReadDesc>(), read_list, d_stats, grp, st),
        "read order launch");
@@ -387,10 +480,6 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
     if ((vk.kind == VK_GRP) != grp && vk.kind != VK_GENERIC) continue;  // gets no reads
     const int lqv = std::min(lq_max, vk.kind == VK_GRP ? 256 : vk.max_len());
     const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
-    const size_t lds = vk.kind == VK_FAST  ? (size_t)(kBlock / 64) * fast_wave_lds(tb)
-                       : vk.kind == VK_GRP ? (size_t)(kBlock / 16) * grp_group_lds(tb)
-                                           : (size_t)tb * (kBlock / vk.G);
-    if (lds > 64 * 1024) return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large");
     HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, db.n_reads, tb, a, st), "chain2aln launch");
   }
   return BWAGPU_OK;
@@ -469,6 +558,9 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
   int rc = check_batch(ctx, b);
   if (rc) return rc;
+  int lq_max = 0;
+  for (int r = 0; r < b->n_reads; ++r) lq_max = std::max<int>(lq_max, (int)(b->seq_off[r + 1] - b->seq_off[r]));
+  if ((rc = check_lds(ctx, lq_max))) return rc;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   s.t_submit = std::chrono::steady_clock::now();
   s.n_reads = b->n_reads;
@@ -485,11 +577,9 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   HIPC(s.h_stats.ensure(sizeof(int64_t) * ST_N), "hipHostMalloc(stats)");
   // stage into pinned memory so the caller's buffers are free on return
   char* h = s.h_in.as<char>();
-  int lq_max = 0;
   if (b->n_reads) {
     memcpy(h + L.seq_off, b->seq_off, sizeof(int64_t) * (size_t)(b->n_reads + 1));
     memcpy(h + L.rco, b->read_chain_off, sizeof(int32_t) * (size_t)(b->n_reads + 1));
-    for (int r = 0; r < b->n_reads; ++r) lq_max = std::max<int>(lq_max, (int)(b->seq_off[r + 1] - b->seq_off[r]));
   }
   memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
   if (b->n_chains) {
@@ -518,7 +608,12 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   HIPC(hipEventRecord(s.ev1, st), "event");
   rc = enqueue_chain2aln(ctx, s, db, lq_max, s.d_out.as<bwagpu_alnreg_t>(), s.d_n.as<int32_t>(),
                          s.d_stats.as<int64_t>(), st);
-  if (rc) return rc;
+  if (rc) {
+    // work already queued on the slot's stream may still read h_in / d_in:
+    // drain it before the caller may reuse the slot
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
   HIPC(hipEventRecord(s.ev2, st), "event");
   if (b->n_seeds)
     HIPC(hipMemcpyAsync(s.h_out.p, s.d_out.p, sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds, hipMemcpyDeviceToHost, st),
@@ -585,12 +680,15 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwag
                             int32_t* dev_n, int64_t* dev_stats, void* stream) {
   if (!ctx || !db_in || !dev_out || !dev_n) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  // reads are bounded by BWAGPU_MAX_READ_LEN; the LDS row buffer is sized for it
+  int rc = check_lds(ctx, BWAGPU_MAX_READ_LEN);
+  if (rc) return rc;
   hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
   int k = 0;
   while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] && ctx->dev_stream[k] != st) ++k;
   if (k == BWAGPU_NUM_SLOTS) return fail(ctx, BWAGPU_E_INVAL, "more than BWAGPU_NUM_SLOTS streams on one context");
   ctx->dev_stream[k] = st;
-  Slot& s = ctx->slot[k];
+  Slot& s = ctx->dev_scratch[k];
   DevBatch db;
   db.n_reads = db_in->n_reads;
   db.n_chains = db_in->n_chains;
@@ -608,7 +706,6 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwag
     stats = s.d_stats.as<int64_t>();
     HIPC(hipMemsetAsync(stats, 0, sizeof(int64_t) * ST_N, st), "memset stats");
   }
-  // reads are bounded by BWAGPU_MAX_READ_LEN; the LDS row buffer is sized for it
   return enqueue_chain2aln(ctx, s, db, BWAGPU_MAX_READ_LEN, dev_out, dev_n, stats, st);
 }
 

@@ -126,6 +126,64 @@ hipError_t launch_extend_grp(int cpl, bool t5, const DevOpt& o, const bwagpu_ext
                              const int32_t* task_list, int32_t n_list, const uint8_t* qpool, const uint8_t* tpool,
                              int tb_bytes, bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
 
+// ---------------------------------------------------------------- speculative path
+// mem_chain2aln as (1) extension tasks computed ahead of the sequential
+// containment logic and (2) a selection pass that replays that logic with the
+// precomputed results (sw_kernels.hip, "speculative chain2aln").
+// One seed's extension (bwamem.c:717-792) is a pure function of the seed, the
+// read and its chain's window, so it can run before the sequential pass
+// decides whether mem_chain2aln performs it.
+struct SeedExt {
+  int64_t rb, re;
+  int32_t qb, qe, score, truesc, w;  // w = max of both sides' final band
+  int32_t cells, rows, calls;        // the DP work (counted only if the region is used);
+                                     // calls = ksw_extend2 calls + 1, so 0 = not computed
+};  // 48 B; the per-batch memset 0 marks every slot "not computed"
+
+// extension task lists: 3 length classes (kernel columns per lane) x 3 rounds
+constexpr int kSpecBins = 3;                           // lq <= 192 / <= 256 / <= 1023
+constexpr int kSpecBinLen[kSpecBins] = {192, 256, 1023};
+constexpr int kSpecRounds = 3;                         // A, B, C
+constexpr int kSelLight = 64;                          // reads with more seeds go first
+constexpr int kSelRegLds = 256;                        // regions per wave held in LDS
+// counter words (int32) of one batch (zeroed per batch)
+enum {
+  SPC_CNT = 0,        // [round*3 + bin] task counts (rounds 0 = A, 1 = B, 2 = C)
+  SPC_HEAVY_N = 16,   // reads with > kSelLight seeds
+  SPC_SEL_CUR = 17,   // [pass] heavy-read cursors of the emulate / final pass, [2] redo cursor
+  SPC_REDO_N = 20,    // reads the final pass could not finish (a missing extension)
+  SPC_SPEC64 = 24,    // int64 at words 24-25: DP cells of every computed task (diagnostic)
+  SPC_MISS = 26,      // extensions the redo pass computed inline
+  SPC_EXT_Q = 32,     // [list*8 + xcd] sharded task-queue heads, 9 lists
+  SPC_SEL_Q = 104,    // [pass*8 + xcd] sharded read-queue heads of the emulate / final pass
+  SPC_WORDS = 128
+};
+// task list `list` (= round * kSpecBins + bin) starts at this entry of SpecArgs::tasks
+__host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_seeds) {
+  const int round = list / kSpecBins, bin = list % kSpecBins;
+  return round == 0 ? (size_t)bin * n_chains
+                    : (size_t)kSpecBins * n_chains + ((size_t)(round - 1) * kSpecBins + bin) * n_seeds;
+}
+struct SpecArgs {
+  ChainWin* win;              // per chain
+  int32_t* chain_read;        // per chain
+  bwagpu_seed_t* prog;        // per seed, processing order (pad_ = 1: key 0)
+  SeedExt* ext;               // per seed slot
+  int2* tasks;                // (seed slot, chain) per task, lists at spec_list_off
+  int32_t* ctr;               // SPC_* words
+  int32_t* regpos;            // per seed slot: region i of a read -> seed slot (LDS overflow)
+  int32_t* skipf;             // per seed slot: skip flags of chains > 256 seeds
+  int32_t* heavy;             // reads with > kSelLight seeds
+  int32_t* redo;              // reads the final pass left to the redo pass
+  bwagpu_alnreg_t* out;
+  int32_t* out_n;
+  int64_t* stats;
+};
+hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
+                                 int tb_bytes, hipStream_t st);
+// LDS bytes per workgroup of the final selection pass (the largest spec launch)
+size_t spec_select_lds(int tb_bytes);
+
 // diagnostics: per-read trace buffer (device pointer, 8 x u32 per read; NULL = off)
 hipError_t set_trace(void* dev_ptr);
 

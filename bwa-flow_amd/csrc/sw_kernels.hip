@@ -32,6 +32,9 @@
 #include <limits.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "engine.h"
 #include "wave_ops.h"
@@ -1920,14 +1923,34 @@ hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch&
   return hipGetLastError();
 }
 
-// resident workgroups of a kernel over the whole device (persistent grids)
+// resident workgroups of a kernel over the whole device (persistent grids).
+// The answer depends on the kernel, its dynamic LDS bytes (which change per
+// batch with the read lengths and options) and the device, so it is cached
+// under exactly that key; GPU worker threads of several contexts call this
+// concurrently.
 template <typename K>
 static int resident_blocks(K kernel, size_t lds) {
-  int dev = 0, ncu = 0, per = 0;
+  int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  struct Key {
+    const void* k;
+    size_t lds;
+    int dev;
+    bool operator<(const Key& o) const { return std::tie(k, lds, dev) < std::tie(o.k, o.lds, o.dev); }
+  };
+  static std::mutex mu;
+  static std::map<Key, int> cache;
+  const Key key{reinterpret_cast<const void*>(kernel), lds, dev};
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  int ncu = 0, per = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds) != hipSuccess || per < 1) per = 1;
-  return per * ncu;
+  std::lock_guard<std::mutex> g(mu);
+  return cache[key] = per * ncu;
 }
 
 size_t fast_wave_lds(int tb) { return (size_t)kFastWaveLds(tb); }
@@ -1936,8 +1959,7 @@ template <int C>
 static hipError_t launch_c2a_fast(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n,
                                   int tb, const C2AArgs& a, hipStream_t st) {
   const size_t lds = (size_t)(kBlock / 64) * kFastWaveLds(tb);
-  static int cap = 0;  // per instantiation; same device kind everywhere
-  if (!cap) cap = resident_blocks(chain2aln_fast_kernel<C>, lds);
+  const int cap = resident_blocks(chain2aln_fast_kernel<C>, lds);
   const int nb = std::min((n + 3) / 4, cap);
   hipLaunchKernelGGL((chain2aln_fast_kernel<C>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, variant, tb);
   return hipGetLastError();
@@ -2035,5 +2057,639 @@ hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t, const b
 #undef EXT_CASE
   return hipErrorInvalidValue;
 }
+
+// ============================================================ speculative chain2aln
+// mem_chain2aln (bwamem.c:641-795) restructured for load balance on
+// reference-seeded batches, where a few reads (tandem repeats: hundreds of
+// seeds, one region each) carry more DP than thousands of ordinary reads and,
+// run serially by one wave, set the stage's critical path.
+//
+// The one sequential dependency of mem_chain2aln is the decision whether a
+// seed is extended at all: the containment test against the read's regions so
+// far (bwamem.c:678-697) and the overlapping-seed test (698-707).  The
+// extension itself (717-792: left ksw_extend2 with the band retry, right
+// ksw_extend2 from the left score, local vs to-end choice) depends only on the
+// seed, the read and its chain's window.  So:
+//   round A   extend the first seed (processing order) of every chain — it is
+//             almost always extended; one wave per task, dynamic queue;
+//   emulate   replay the sequential logic per read with the round-A regions:
+//             every seed that would be extended and has no result yet becomes
+//             a round-B task (its region unknown, so later seeds of the read
+//             are tested against fewer regions: a superset is predicted);
+//   round B   extend those;
+//   final     replay the sequential logic exactly, with every result it needs
+//             precomputed except rare mispredictions, which it computes inline.
+// Output = the reference's regions, byte for byte; the stats count only the DP
+// of extensions mem_chain2aln performs (spec work is a separate diagnostic).
+
+// wave-aggregated append: returns the slot of each predicated lane (-1 else)
+__device__ __forceinline__ int wave_append(int32_t* cnt, bool p) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(p);
+  if (m == 0) return -1;
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(cnt, (int)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  return p ? base + rank : -1;
+}
+
+// Dynamic queue with one head per XCD (MI355X_MICROARCH.md "dequeue": one head
+// word saturates at ~88 dequeues/us): shard x holds list positions x, x + 8,
+// ...; a wave claims K consecutive entries of a shard with one atomic, starting
+// on its own XCD's shard and moving on when it runs dry.  Every position is
+// taken exactly once by whichever waves exist; placement is never assumed.
+struct ShardQ {
+  int32_t* heads;
+  int n, shard, tried;
+  __device__ void init(int32_t* h, int n_) {
+    heads = h;
+    n = n_;
+    shard = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7;  // HW_REG_XCC_ID
+    tried = 0;
+  }
+  // -> first claimed entry index m0 of `shard` (positions shard + 8m, m < cap)
+  __device__ bool claim(int K, int& m0, int& cap) {
+    while (tried < 8) {
+      cap = n > shard ? (n - shard + 7) >> 3 : 0;
+      int32_t* h = heads + shard;
+      if (__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cap) {
+        int v = 0;
+        if ((threadIdx.x & 63) == 0) v = atomicAdd(h, K);
+        v = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));
+        if (v < cap) {
+          m0 = v;
+          return true;
+        }
+      }
+      shard = (shard + 1) & 7;
+      ++tried;
+    }
+    return false;
+  }
+};
+
+__device__ __forceinline__ int spec_bin(int lq) { return lq <= kSpecBinLen[0] ? 0 : (lq <= kSpecBinLen[1] ? 1 : 2); }
+
+// lane per chain: window (bwamem.c:648-668 + bns_fetch_seq's clipping), the
+// chain's read, and the round-A task (its first seed in processing order)
+__global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  bool task = false;
+  int bin = 0, s0 = 0;
+  if (c < b.n_chains) {
+    int lo_r = 0, hi_r = b.n_reads - 1;  // owner read: binary search over read_chain_off
+    while (lo_r < hi_r) {
+      const int mid = (lo_r + hi_r + 1) >> 1;
+      if (b.read_chain_off[mid] <= c) lo_r = mid;
+      else hi_r = mid - 1;
+    }
+    a.chain_read[c] = lo_r;
+    s0 = b.chain_seed_off[c];
+    const int ns = b.chain_seed_off[c + 1] - s0;
+    const int lq = (int)(b.seq_off[lo_r + 1] - b.seq_off[lo_r]);
+    if (ns <= 0) {
+      a.win[c] = ChainWin{0, 0};
+    } else {
+      const int64_t two = ref.l_pac << 1;
+      int64_t wlo = two, whi = 0;
+      for (int i = 0; i < ns; ++i) {
+        const bwagpu_seed_t t = b.seeds[s0 + i];
+        const int tail = lq - t.qbeg - t.len;
+        wlo = min(wlo, t.rbeg - (int64_t)(t.qbeg + max_gap_len(o, t.qbeg)));
+        whi = max(whi, t.rbeg + t.len + (int64_t)(tail + max_gap_len(o, tail)));
+      }
+      wlo = max(wlo, (int64_t)0);
+      whi = min(whi, two);
+      const int64_t mid = b.seeds[s0].rbeg;
+      if (wlo < ref.l_pac && ref.l_pac < whi) {
+        if (mid < ref.l_pac) whi = ref.l_pac;
+        else wlo = ref.l_pac;
+      }
+      const int rid = b.chain_rid[c];
+      bool ok = rid >= 0 && rid < ref.n_seqs;
+      if (ok) {
+        const int64_t fpos = mid >= ref.l_pac ? two - 1 - mid : mid;
+        int64_t cb = ref.ann_offset[rid], ce = cb + ref.ann_len[rid];
+        ok = fpos >= cb && fpos < ce;
+        if (mid >= ref.l_pac) {
+          const int64_t t0 = cb;
+          cb = two - ce;
+          ce = two - t0;
+        }
+        wlo = max(wlo, cb);
+        whi = min(whi, ce);
+      }
+      if (!ok) {
+        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_RID);
+        a.win[c] = ChainWin{0, -1};
+      } else {
+        a.win[c] = ChainWin{wlo, whi};
+        task = lq <= BWAGPU_MAX_READ_LEN;
+        bin = spec_bin(lq);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSpecBins; ++k) {
+    const int p = wave_append(&a.ctr[SPC_CNT + k], task && bin == k);
+    if (p >= 0) a.tasks[(size_t)k * b.n_chains + p] = make_int2(s0, c);
+  }
+}
+
+// lane per read: length check, and the list of heavy reads (selected first)
+__global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a) {
+  const int rd = blockIdx.x * blockDim.x + threadIdx.x;
+  bool heavy = false;
+  if (rd < b.n_reads) {
+    const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+    if (lq > BWAGPU_MAX_READ_LEN) atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_LEN);
+    const int ns = b.chain_seed_off[b.read_chain_off[rd + 1]] - b.chain_seed_off[b.read_chain_off[rd]];
+    heavy = ns > kSelLight;
+  }
+  const int p = wave_append(&a.ctr[SPC_HEAVY_N], heavy);
+  if (p >= 0) a.heavy[p] = rd;
+}
+
+// 16 lanes per chain: the seeds in processing order (descending key
+// score<<32|i, bwamem.c:671-676) by ranking — keys are unique, so rank = the
+// number of smaller keys; O(ns^2/16) per chain, no serial lane on a long chain.
+// pad_ = 1 flags the key that is 0 from the start (skipped by the overlap test
+// like a marked seed, bwamem.c:700).
+__global__ void __launch_bounds__(256) spec_order_kernel(DevBatch b, SpecArgs a) {
+  const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4), r = (int)(threadIdx.x & 15);
+  if (g >= b.n_chains) return;
+  const int s0 = b.chain_seed_off[g], ns = b.chain_seed_off[g + 1] - s0;
+  for (int i = r; i < ns; i += 16) {
+    bwagpu_seed_t v = b.seeds[s0 + i];
+    const uint64_t ki = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
+    int rank = 0;
+    for (int j = 0; j < ns; ++j) rank += ((uint64_t)(uint32_t)b.seeds[s0 + j].score << 32 | (uint32_t)j) < ki;
+    v.pad_ = ki == 0 ? 1 : 0;
+    a.prog[s0 + ns - 1 - rank] = v;
+  }
+}
+
+// One seed's extension (bwamem.c:717-792) by one wave: both target windows
+// gathered in one round trip, left ksw_extend2 (reversed query prefix and
+// window) with the MAX_BAND_TRY retry, right ksw_extend2 from the left score,
+// the local vs to-end choice of each side.  s, lq, cw are wave-uniform.
+template <int C>
+__device__ __forceinline__ SeedExt extend_seed(const DevOpt& o, const DevRef& ref, const bwagpu_seed_t& s, int lq,
+                               const uint8_t* q, const ChainWin& cw, uint8_t* tbl, uint8_t* tbr) {
+  Tally tl{0, 0, 0};
+  const int qlenL = s.qbeg, qlenR = lq - (s.qbeg + s.len);
+  const int64_t x0L = s.rbeg - 1, x0R = s.rbeg + s.len;
+  const int tlenL = (int)(s.rbeg - cw.lo), tlenR = (int)(cw.hi - x0R);
+  fill_two(tbl, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0, tbr, x0R,
+           qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref);
+  int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
+  int aw0 = o.w, aw1 = o.w;
+  int64_t rb = s.rbeg, re = s.rbeg + s.len;
+#pragma nounroll
+  for (int side = 0; side < 2; ++side) {
+    const bool left = side == 0;
+    if (left && s.qbeg == 0) {  // bwamem.c:753
+      score = truesc = s.len * o.a;
+      continue;
+    }
+    if (!left && qlenR == 0) continue;  // bwamem.c:781
+    const int qlen = left ? qlenL : qlenR;
+    const int64_t x0 = left ? x0L : x0R;
+    const int tlen = left ? tlenL : tlenR;
+    const int qa = left ? s.qbeg - 1 : s.qbeg + s.len;
+    const int eb = left ? o.pen_clip5 : o.pen_clip3;
+    const int h0 = left ? s.len * o.a : score;
+    uint8_t* const tb = left ? tbl : tbr;
+    sc0 = score;
+    ExtOut x{};
+    for (int t = 0; t < 2; ++t) {  // MAX_BAND_TRY (bwamem.c:639)
+      const int prev = score;
+      const int aw = o.w << t;
+      aw0 = left ? aw : aw0;
+      aw1 = left ? aw1 : aw;
+      x = extend_wave_dispatch<C, false>(o, qlen, q, qa, left ? -1 : 1, tlen, tb, aw, eb, o.zdrop, h0, tl);
+      score = x.score;
+      if (score == prev || x.max_off < (aw >> 1) + (aw >> 2)) break;
+    }
+    const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+    if (left) {
+      qb = local ? s.qbeg - x.qle : 0;
+      rb = s.rbeg - (local ? x.tle : x.gtle);
+      truesc = local ? score : x.gscore;
+    } else {
+      qe = local ? qa + x.qle : lq;
+      re = x0 + (local ? x.tle : x.gtle);
+      truesc += (local ? score : x.gscore) - sc0;
+    }
+  }
+  SeedExt e;
+  e.rb = rb;
+  e.re = re;
+  e.qb = qb;
+  e.qe = qe;
+  e.score = score;
+  e.truesc = truesc;
+  e.w = aw0 > aw1 ? aw0 : aw1;
+  e.cells = (int32_t)tl.cells;
+  e.rows = (int32_t)tl.rows;
+  e.calls = (int32_t)tl.calls + 1;  // + 1: a computed slot is never all-zero
+  return e;
+}
+
+__device__ __forceinline__ void store_ext(SeedExt* dst, const SeedExt& e) {
+  const int d = (int)(threadIdx.x & 63);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&e);
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) v = d == k ? w[k] : v;
+  if (d < 12) reinterpret_cast<uint32_t*>(dst)[d] = v;
+}
+
+__device__ __forceinline__ bwagpu_seed_t uni_seed(const bwagpu_seed_t& s) {
+  bwagpu_seed_t u;
+  u.rbeg = uni64(s.rbeg);
+  u.qbeg = uni(s.qbeg);
+  u.len = uni(s.len);
+  u.score = uni(s.score);
+  u.pad_ = uni(s.pad_);
+  return u;
+}
+
+// Extension tasks of one list (round * kSpecBins + bin): one wave per task,
+// claimed two at a time from the sharded queue.
+template <int C>
+__global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                          int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int wib = uni((int)(threadIdx.x >> 6));
+  uint8_t* const tbl = lds + wib * 2 * tb_bytes;
+  uint8_t* const tbr = tbl + tb_bytes;
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  ShardQ qq;
+  qq.init(a.ctr + SPC_EXT_Q + 8 * list, n);
+  long long spec_cells = 0;
+  int m0, cap;
+  while (qq.claim(2, m0, cap)) {
+    for (int m = m0; m < m0 + 2 && m < cap; ++m) {
+      const int2 tk = tl[qq.shard + 8 * m];
+      const int pos = uni(tk.x), c = uni(tk.y);
+      const int rd = uni(a.chain_read[c]);
+      const int64_t qoff = uni64(b.seq_off[rd]);
+      const int lq = uni((int)(b.seq_off[rd + 1] - qoff));
+      const bwagpu_seed_t s = uni_seed(a.prog[pos]);
+      ChainWin cw = a.win[c];
+      cw.lo = uni64(cw.lo);
+      cw.hi = uni64(cw.hi);
+      const SeedExt e = extend_seed<C>(o, ref, s, lq, b.seq + qoff, cw, tbl, tbr);
+      store_ext(a.ext + pos, e);
+      spec_cells += e.cells;
+    }
+  }
+  if ((threadIdx.x & 63) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+// The sequential logic of mem_chain2aln over one read's chains, by one wave.
+// Regions: containment fields in LDS (SoA, kSelRegLds per wave; beyond that
+// the region's seed slot in regpos[] and its SeedExt, re-read with
+// workgroup-scope atomics).  A chain's seeds (<= 256) sit in VGPRs, four per
+// lane, with their skip flags; longer chains read prog[] and keep the flags in
+// skipf[].  A seed that is extended but has no result yet:
+//   SEL_EMULATE  becomes a round-B task (its region stays unknown);
+//   SEL_FINAL    becomes a round-C task and the read goes to the redo list
+//                (its later decisions depend on that region);
+//   SEL_REDO     (the redo list only) is computed inline — the pass that
+//                guarantees every read completes, at low occupancy.
+// SEL_FINAL and SEL_REDO write the read's mem_alnreg_v.
+enum { SEL_EMULATE = 0, SEL_FINAL = 1, SEL_REDO = 2 };
+constexpr int kSelFields = 8;  // rb lo/hi, re lo/hi, qb, qe, w, seedlen0
+__host__ __device__ constexpr int sel_wave_lds(int mode, int tb) {
+  return kSelFields * 4 * kSelRegLds + (mode == SEL_REDO ? 2 * tb : 0);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) spec_select_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
+                                                             int tb_bytes) {
+  constexpr bool WRITE = MODE != SEL_EMULATE;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int r = (int)(threadIdx.x & 63);
+  const int wib = uni((int)(threadIdx.x >> 6));
+  int32_t* const R = reinterpret_cast<int32_t*>(lds + wib * sel_wave_lds(MODE, tb_bytes));
+  uint8_t* const tbl = reinterpret_cast<uint8_t*>(R + kSelFields * kSelRegLds);
+  uint8_t* const tbr = tbl + tb_bytes;
+  // MODE_REDO walks the redo list in place of the heavy list, and nothing else
+  const int nheavy = uni(__hip_atomic_load(&a.ctr[MODE == SEL_REDO ? SPC_REDO_N : SPC_HEAVY_N], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+  const int32_t* const hlist = MODE == SEL_REDO ? a.redo : a.heavy;
+  int32_t* const cur = a.ctr + SPC_SEL_CUR + MODE;
+  Tally tl{0, 0, 0};
+  ShardQ lq_q;
+  lq_q.init(a.ctr + SPC_SEL_Q + (MODE == SEL_FINAL ? 8 : 0), b.n_reads);
+  bool heavy_phase = true;
+  int m0 = 0, cap = 0, mi = 0;
+  for (;;) {
+    int rd;
+    if (heavy_phase) {
+      int t = 0;
+      if (r == 0) t = atomicAdd(&cur[0], 1);
+      t = uni(__shfl(t, 0, 64));
+      if (t < nheavy) {
+        rd = uni(hlist[t]);
+      } else {
+        if (MODE == SEL_REDO) break;
+        heavy_phase = false;
+        continue;
+      }
+    } else {
+      if (mi >= m0 + 8 || mi >= cap) {
+        if (!lq_q.claim(8, m0, cap)) break;
+        mi = m0;
+      }
+      if (mi >= cap) continue;
+      rd = lq_q.shard + 8 * mi++;
+    }
+    const int c0 = uni(b.read_chain_off[rd]), c1 = uni(b.read_chain_off[rd + 1]);
+    const int s0r = uni(b.chain_seed_off[c0]);
+    if (!heavy_phase && uni(b.chain_seed_off[c1]) - s0r > kSelLight) continue;  // done in the heavy phase
+    bool redo = false;
+    Tally rt{0, 0, 0};  // this read's DP, added once the read completes
+    const int64_t qoff = uni64(b.seq_off[rd]);
+    const int lq = uni((int)(b.seq_off[rd + 1] - qoff));
+    if (lq > BWAGPU_MAX_READ_LEN) continue;  // flagged by spec_reads_kernel
+    const uint8_t* const q = b.seq + qoff;
+    int nreg = 0;
+    for (int c = c0; c < c1 && !redo; ++c) {
+      const int s0 = uni(b.chain_seed_off[c]), ns = uni(b.chain_seed_off[c + 1]) - s0;
+      if (ns == 0) continue;
+      ChainWin cw = a.win[c];
+      cw.lo = uni64(cw.lo);
+      cw.hi = uni64(cw.hi);
+      if (cw.hi < cw.lo) continue;  // flagged by spec_chain_kernel (the reference would assert)
+      const int rid = uni(b.chain_rid[c]);
+      const float frac = __int_as_float(uni(__float_as_int(b.chain_frac_rep[c])));
+      const bool big = ns > 256;
+      // the chain's seeds, four slots per lane (slot m, lane r = seed 64m + r)
+      int64_t srb[4];
+      int sqb[4], slen[4];
+      bool sk[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int i = 64 * m + r;
+        const bwagpu_seed_t v = a.prog[s0 + min(i, ns - 1)];
+        srb[m] = v.rbeg;
+        sqb[m] = v.qbeg;
+        slen[m] = v.len;
+        sk[m] = i >= ns || v.pad_ != 0;
+      }
+      if (big)
+        for (int i = r; i < ns; i += 64) __hip_atomic_store(&a.skipf[s0 + i], a.prog[s0 + i].pad_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int k = 0; k < ns; ++k) {
+        bwagpu_seed_t s;
+        if (!big) {
+          const int m = k >> 6, l = k & 63;
+          const int64_t vrb = m == 0 ? srb[0] : m == 1 ? srb[1] : m == 2 ? srb[2] : srb[3];
+          const int vqb = m == 0 ? sqb[0] : m == 1 ? sqb[1] : m == 2 ? sqb[2] : sqb[3];
+          const int vln = m == 0 ? slen[0] : m == 1 ? slen[1] : m == 2 ? slen[2] : slen[3];
+          s.rbeg = readlane64(vrb, l);
+          s.qbeg = __builtin_amdgcn_readlane(vqb, l);
+          s.len = __builtin_amdgcn_readlane(vln, l);
+        } else {
+          s = uni_seed(a.prog[s0 + k]);
+        }
+        // containment in a region so far (bwamem.c:678-697), one region per lane
+        bool hit = false;
+        for (int base = 0; base < nreg && !hit; base += 64) {
+          const int i = min(base + r, nreg - 1);
+          int64_t prb, pre;
+          int pqb, pqe, pw, psl;
+          if (i < kSelRegLds) {
+            prb = (int64_t)((uint64_t)(uint32_t)R[kSelRegLds + i] << 32 | (uint32_t)R[i]);
+            pre = (int64_t)((uint64_t)(uint32_t)R[3 * kSelRegLds + i] << 32 | (uint32_t)R[2 * kSelRegLds + i]);
+            pqb = R[4 * kSelRegLds + i];
+            pqe = R[5 * kSelRegLds + i];
+            pw = R[6 * kSelRegLds + i];
+            psl = R[7 * kSelRegLds + i];
+          } else {
+            const int pp = __hip_atomic_load(&a.regpos[s0r + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const SeedExt* pe = a.ext + pp;
+            prb = __hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pre = __hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pqb = __hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pqe = __hip_atomic_load(&pe->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pw = __hip_atomic_load(&pe->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            psl = a.prog[pp].len;
+          }
+          const bool inside = !(s.rbeg < prb || s.rbeg + s.len > pre || s.qbeg < pqb || s.qbeg + s.len > pqe) &&
+                              !(s.len - psl > .1 * lq);
+          const int qd1 = s.qbeg - pqb;
+          const int64_t rd1 = s.rbeg - prb;
+          const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
+          const int bw1 = g1 < pw ? g1 : pw;
+          const int qd2 = pqe - (s.qbeg + s.len);
+          const int64_t rd2 = pre - (s.rbeg + s.len);
+          const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
+          const int bw2 = g2 < pw ? g2 : pw;
+          const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+          hit = __builtin_amdgcn_ballot_w64(base + r < nreg && inside && near) != 0;
+        }
+        if (hit) {
+          // a long overlapping seed already visited (bwamem.c:698-707): seeds
+          // 0..k-1 in processing order, not skipped and key != 0
+          bool ov = false;
+          for (int base = 0; base < k && !ov; base += 64) {
+            const int i = base + r;
+            int64_t trb;
+            int tqb, tln;
+            bool tsk;
+            if (!big) {
+              const int m = base >> 6;
+              trb = m == 0 ? srb[0] : m == 1 ? srb[1] : m == 2 ? srb[2] : srb[3];
+              tqb = m == 0 ? sqb[0] : m == 1 ? sqb[1] : m == 2 ? sqb[2] : sqb[3];
+              tln = m == 0 ? slen[0] : m == 1 ? slen[1] : m == 2 ? slen[2] : slen[3];
+              tsk = m == 0 ? sk[0] : m == 1 ? sk[1] : m == 2 ? sk[2] : sk[3];
+            } else {
+              const bwagpu_seed_t t = a.prog[s0 + min(i, ns - 1)];
+              trb = t.rbeg;
+              tqb = t.qbeg;
+              tln = t.len;
+              tsk = __hip_atomic_load(&a.skipf[s0 + min(i, ns - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+            }
+            const bool a1 = s.qbeg <= tqb && s.qbeg + s.len - tqb >= s.len >> 2 && (int64_t)(tqb - s.qbeg) != trb - s.rbeg;
+            const bool b1 = tqb <= s.qbeg && tqb + tln - s.qbeg >= s.len >> 2 && (int64_t)(s.qbeg - tqb) != s.rbeg - trb;
+            ov = __builtin_amdgcn_ballot_w64(i < k && !tsk && !(tln < s.len * .95) && (a1 || b1)) != 0;
+          }
+          if (!ov) {  // skipped: srt[k] = 0 (bwamem.c:709)
+            if (!big) {
+              const int m = k >> 6, l = k & 63;
+#pragma unroll
+              for (int mm = 0; mm < 4; ++mm) sk[mm] = (mm == m && r == l) ? true : sk[mm];
+            } else {
+              __hip_atomic_store(&a.skipf[s0 + k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              mem_fence_group();
+            }
+            continue;
+          }
+        }
+        // ---- this seed is extended (bwamem.c:717-792)
+        const int pos = s0 + k;
+        SeedExt e;
+        e.calls = uni(__hip_atomic_load(&a.ext[pos].calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (e.calls == 0) {  // no result yet
+          if constexpr (MODE == SEL_REDO) {
+            e = extend_seed<16>(o, ref, s, lq, q, cw, tbl, tbr);
+            store_ext(a.ext + pos, e);
+            mem_fence_group();
+            if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+          } else {
+            // a task of the next round: B after emulation, C after the final pass
+            const int list = (MODE == SEL_EMULATE ? 1 : 2) * kSpecBins + spec_bin(lq);
+            int p = 0;
+            if (r == 0) p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+            p = uni(__shfl(p, 0, 64));
+            if (r == 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(pos, c);
+            if (MODE == SEL_EMULATE) continue;  // its region stays unknown in this pass
+            if (r == 0) a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+            redo = true;  // the rest of this read waits for the redo pass
+            break;
+          }
+        } else {
+          const SeedExt* pe = a.ext + pos;
+          e.rb = uni64(__hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.re = uni64(__hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.qb = uni(__hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.qe = uni(__hip_atomic_load(&pe->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.score = uni(__hip_atomic_load(&pe->score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.truesc = uni(__hip_atomic_load(&pe->truesc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.w = uni(__hip_atomic_load(&pe->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.cells = uni(__hip_atomic_load(&pe->cells, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.rows = uni(__hip_atomic_load(&pe->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        }
+        if constexpr (WRITE) {
+          // seedcov over the chain's seeds (bwamem.c:784-788)
+          long long cov = 0;
+          for (int base = 0; base < ns; base += 64) {
+            const int i = base + r;
+            int64_t trb;
+            int tqb, tln;
+            if (!big) {
+              const int m = base >> 6;
+              trb = m == 0 ? srb[0] : m == 1 ? srb[1] : m == 2 ? srb[2] : srb[3];
+              tqb = m == 0 ? sqb[0] : m == 1 ? sqb[1] : m == 2 ? sqb[2] : sqb[3];
+              tln = m == 0 ? slen[0] : m == 1 ? slen[1] : m == 2 ? slen[2] : slen[3];
+            } else {
+              const bwagpu_seed_t t = a.prog[s0 + min(i, ns - 1)];
+              trb = t.rbeg;
+              tqb = t.qbeg;
+              tln = t.len;
+            }
+            const bool in = i < ns && tqb >= e.qb && tqb + tln <= e.qe && trb >= e.rb && trb + tln <= e.re;
+            cov += in ? tln : 0;
+          }
+          cov = grp_sum64(cov, 64);
+          // the 88-byte mem_alnreg_t (rest zero: bwamem.c:718), lane d writes dword d
+          const int d = r < 21 ? r : 21;
+          uint32_t v = 0;
+          v = d == 0 ? (uint32_t)e.rb : v;
+          v = d == 1 ? (uint32_t)((uint64_t)e.rb >> 32) : v;
+          v = d == 2 ? (uint32_t)e.re : v;
+          v = d == 3 ? (uint32_t)((uint64_t)e.re >> 32) : v;
+          v = d == 4 ? (uint32_t)e.qb : v;
+          v = d == 5 ? (uint32_t)e.qe : v;
+          v = d == 6 ? (uint32_t)rid : v;
+          v = d == 7 ? (uint32_t)e.score : v;
+          v = d == 8 ? (uint32_t)e.truesc : v;
+          v = d == 13 ? (uint32_t)e.w : v;
+          v = d == 14 ? (uint32_t)cov : v;
+          v = d == 17 ? (uint32_t)s.len : v;
+          v = d == 19 ? __float_as_uint(frac) : v;
+          reinterpret_cast<uint32_t*>(a.out + s0r + nreg)[d] = v;
+          rt.cells += e.cells;
+          rt.rows += e.rows;
+          rt.calls += e.calls - 1;
+        }
+        // the region's containment fields
+        if (nreg < kSelRegLds) {
+          const int f = r < kSelFields ? r : kSelFields - 1;
+          int32_t v = 0;
+          v = f == 0 ? (int32_t)(uint32_t)e.rb : v;
+          v = f == 1 ? (int32_t)((uint64_t)e.rb >> 32) : v;
+          v = f == 2 ? (int32_t)(uint32_t)e.re : v;
+          v = f == 3 ? (int32_t)((uint64_t)e.re >> 32) : v;
+          v = f == 4 ? e.qb : v;
+          v = f == 5 ? e.qe : v;
+          v = f == 6 ? e.w : v;
+          v = f == 7 ? s.len : v;
+          if (r < kSelFields) R[f * kSelRegLds + nreg] = v;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+          if (r == 0) __hip_atomic_store(&a.regpos[s0r + nreg], pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          mem_fence_group();
+        }
+        ++nreg;
+      }
+    }
+    if constexpr (WRITE) {
+      if (!redo) {
+        a.out_n[rd] = nreg;
+        tl.cells += rt.cells;
+        tl.rows += rt.rows;
+        tl.calls += rt.calls;
+      }
+    }
+  }
+  if constexpr (WRITE) {
+    if (r != 0) tl = Tally{0, 0, 0};
+    block_stats<64>(tl, a.stats);
+  }
+}
+
+template <int MODE>
+static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int tb_bytes,
+                          hipStream_t st) {
+  const size_t lds = (size_t)(kBlock / 64) * sel_wave_lds(MODE, tb_bytes);
+  // the redo pass only sees a handful of reads: a small grid
+  const int nb = MODE == SEL_REDO ? 64 : resident_blocks(spec_select_kernel<MODE>, lds);
+  hipLaunchKernelGGL(spec_select_kernel<MODE>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
+}
+
+static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
+                             int tb_bytes, hipStream_t st) {
+  const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
+  const int l = round * kSpecBins;
+  int nb = resident_blocks(spec_ext_kernel<3>, lds);
+  hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
+  nb = resident_blocks(spec_ext_kernel<4>, lds);
+  hipLaunchKernelGGL(spec_ext_kernel<4>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 1, tb_bytes);
+  nb = resident_blocks(spec_ext_kernel<16>, lds);
+  hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 2, tb_bytes);
+}
+
+// prep -> round A -> emulate -> round B -> final -> round C -> redo, one stream
+hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
+                                 int tb_bytes, hipStream_t st) {
+  if (b.n_reads == 0) return hipSuccess;
+  if (b.n_chains) {
+    hipLaunchKernelGGL(spec_chain_kernel, dim3((b.n_chains + 255) / 256), dim3(256), 0, st, o, ref, b, a);
+    hipLaunchKernelGGL(spec_order_kernel, dim3((b.n_chains + 15) / 16), dim3(256), 0, st, b, a);
+  }
+  hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  if (b.n_chains) {
+    launch_ext_round(o, ref, b, a, 0, tb_bytes, st);
+    launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st);
+    launch_ext_round(o, ref, b, a, 1, tb_bytes, st);
+  }
+  launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st);
+  if (b.n_chains) {
+    launch_ext_round(o, ref, b, a, 2, tb_bytes, st);
+    launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st);
+  }
+  return hipGetLastError();
+}
+
+size_t spec_select_lds(int tb_bytes) { return (size_t)(kBlock / 64) * sel_wave_lds(SEL_REDO, tb_bytes); }
 
 }  // namespace bwagpu

@@ -248,7 +248,11 @@ int bwagpu_chain2aln(bwagpu_ctx_t *ctx, const bwagpu_batch_t *batch, bwagpu_alnr
    hipStream_t (NULL = the context's slot-0 stream); asynchronous; dev_stats
    (device, 4 x int64: cells, rows, ext_calls, error flag) may be NULL.
    Up to BWAGPU_NUM_SLOTS distinct streams may be used on one context (each
-   keeps its own scratch), so consecutive batches can overlap. */
+   keeps its own scratch), so consecutive batches can overlap.  Two calls on
+   the SAME stream are ordered by it; the device entry's scratch is separate
+   from the submit/wait slots', so both entry points may be used concurrently
+   on one context.  Options whose LDS need exceeds a launch are refused with
+   BWAGPU_E_UNSUPPORTED before anything is enqueued. */
 int bwagpu_chain2aln_device(bwagpu_ctx_t *ctx, const bwagpu_batch_t *dev_batch,
                             bwagpu_alnreg_t *dev_out, int32_t *dev_n, int64_t *dev_stats,
                             void *stream);

@@ -1,0 +1,67 @@
+"""GPU parity at full ChainsRecord size on chains the REFERENCE seeded.
+
+One C2-sized batch (33,334 2x150 pairs = 66,668 reads, >= 10 Mbases: one
+ChainsRecord, src/Pipeline.cpp:123,146) is seeded and chained by the
+reference's own bwa (mem_chain -> mem_chain_flt -> mem_flt_chained_seeds, run
+by oracle/_ref/gen_golden on the golden genome with repeats, N runs and contig
+junctions), and the reference's own mem_chain2aln gives the expected regions.
+The GPU stage must reproduce every mem_alnreg_t byte, the region order and the
+per-read counts — through the host-buffer entry and through the device entry.
+The mixed-length set (C5: 2x100 / 2x150 / 2x250) runs the same way.
+"""
+import numpy as np
+import pytest
+
+import golden_io as G
+import refseed
+from bwagpu import abi
+from bwagpu.engine import Engine, compact
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not refseed.available(), reason="oracle/_ref/gen_golden not built")]
+
+
+@pytest.fixture(params=["spec", "fast"])
+def c2a_path(request, monkeypatch):
+    if request.param == "spec":
+        monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
+    else:
+        monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
+    return request.param
+
+
+@pytest.mark.parametrize("length,pairs", [("150", 33334), ("mix", 24000)])
+def test_reference_seeded_full_batch(length, pairs, c2a_path):
+    opt, ref, batch, want, want_n = refseed.make(pairs=pairs, seed=7, length=length)
+    assert int(batch.seq_off[-1]) >= 3_000_000 * (2 if length == "150" else 1)
+    eng = Engine(0, opt, ref["l_pac"], ref["ann_offset"], ref["ann_len"], pac=ref["pac"])
+    regs, n = eng.chain2aln(batch)
+    assert np.array_equal(n, want_n), f"{int((n != want_n).sum())} reads with a different region count"
+    assert G.region_mismatch(compact(batch, regs, n), want) is None
+    st = eng.last_stats()
+    assert st["ext_calls"] > batch.n_reads  # reference-seeded chains: > 1 extension per read
+    eng.close()
+
+
+def test_reference_seeded_device_entry():
+    torch = pytest.importorskip("torch")
+    opt, ref, batch, want, want_n = refseed.make(pairs=33334, seed=11, length="150")
+    eng = Engine(0, opt, ref["l_pac"], ref["ann_offset"], ref["ann_len"], pac=ref["pac"])
+    dev = torch.device("cuda:0")
+    fields = ("seq_off", "seq", "read_chain_off", "chain_seed_off", "chain_rid", "chain_frac_rep", "seeds")
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(batch, k)).view(np.uint8).copy()).to(dev) for k in fields}
+    out = torch.zeros(max(batch.n_seeds, 1) * 88, dtype=torch.uint8, device=dev)
+    nn = torch.zeros(max(batch.n_reads, 1), dtype=torch.int32, device=dev)
+    c = abi.BatchC()
+    c.n_reads, c.n_chains, c.n_seeds = batch.n_reads, batch.n_chains, batch.n_seeds
+    c.seq_bytes = int(batch.seq_off[-1])
+    for k in fields:
+        setattr(c, k, t[k].data_ptr())
+    stream = torch.cuda.current_stream()
+    for _ in range(2):  # the second launch reuses the context's scratch
+        eng.chain2aln_device(c, out.data_ptr(), nn.data_ptr(), None, stream.cuda_stream)
+    torch.cuda.synchronize()
+    regs = out.cpu().numpy().view(abi.ALNREG_DTYPE)[:batch.n_seeds]
+    n = nn.cpu().numpy()[:batch.n_reads]
+    assert np.array_equal(n, want_n)
+    assert G.region_mismatch(compact(batch, regs, n), want) is None
+    eng.close()

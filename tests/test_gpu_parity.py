@@ -26,10 +26,15 @@ def refd():
     return G.load_ref()
 
 
-@pytest.fixture(params=["wave", "grp"])
+@pytest.fixture(params=["spec", "wave", "grp"])
 def c2a_path(request, monkeypatch):
-    """mem_chain2aln kernels for reads <= 256 bp: wave per read (default) or
-    16-lane groups, four reads per wave (BWAGPU_C2A_GRP=1)"""
+    """mem_chain2aln paths: speculative extension tasks + selection passes
+    (default), or the per-read kernels (BWAGPU_C2A_PATH=fast): wave per read,
+    or 16-lane groups, four reads per wave (BWAGPU_C2A_GRP=1)"""
+    if request.param == "spec":
+        monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
+    else:
+        monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
     monkeypatch.setenv("BWAGPU_C2A_GRP", "1" if request.param == "grp" else "0")
     return request.param
 
@@ -147,6 +152,56 @@ def test_error_conditions(refd):
     with pytest.raises(BwaGpuError) as e:
         eng.chain2aln(mal)
     assert e.value.code == abi.E_INVAL
+    eng.close()
+
+
+def test_lds_refusal_before_enqueue(refd):
+    """options whose LDS row buffer cannot fit a launch (huge band and clipping
+    bonus) are refused before the H2D is queued: the slot is not left busy, a
+    second submit on the same slot gets the same answer, and the device entry
+    refuses them too"""
+    opt, batch, _, _ = G.load_chain_set("c1_default")
+    big = dict(opt, w=40000, pen_clip5=40000, pen_clip3=40000)
+    eng = make_engine(refd, big)
+    sub = batch.subset(range(50))
+    for _ in range(2):
+        with pytest.raises(BwaGpuError) as e:
+            eng.submit(0, sub)
+        assert e.value.code == abi.E_UNSUPPORTED
+    eng.close()
+    eng = make_engine(refd, opt)  # the ordinary options on a fresh context still run
+    regs, n = eng.chain2aln(sub)
+    assert n.sum() > 0
+    eng.close()
+
+
+def test_device_and_submit_entries_concurrently(refd):
+    """the device entry and the submit/wait slots keep separate scratch: both in
+    flight on one context give the reference's regions"""
+    torch = pytest.importorskip("torch")
+    opt, batch, want, want_n = G.load_chain_set("c1_default")
+    eng = make_engine(refd, opt)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(batch, k)).view(np.uint8).copy()).to(dev)
+         for k in ("seq_off", "seq", "read_chain_off", "chain_seed_off", "chain_rid", "chain_frac_rep", "seeds")}
+    out = torch.zeros(batch.n_seeds * 88, dtype=torch.uint8, device=dev)
+    n = torch.zeros(batch.n_reads, dtype=torch.int32, device=dev)
+    bc = abi.BatchC()
+    bc.n_reads, bc.n_chains, bc.n_seeds = batch.n_reads, batch.n_chains, batch.n_seeds
+    bc.seq_bytes = int(batch.seq_off[-1])
+    for k in t:
+        setattr(bc, k, t[k].data_ptr())
+    s = torch.cuda.Stream()
+    for _ in range(3):
+        eng.chain2aln_device(bc, out.data_ptr(), n.data_ptr(), None, s.cuda_stream)
+        eng.submit(0, batch)
+        r0, n0 = eng.wait(0, batch)
+        assert G.region_mismatch(compact(batch, r0, n0), want) is None
+    torch.cuda.synchronize()
+    regs = out.cpu().numpy().view(abi.ALNREG_DTYPE)
+    nn = n.cpu().numpy()
+    assert np.array_equal(nn, want_n)
+    assert G.region_mismatch(compact(batch, regs, nn), want) is None
     eng.close()
 
 
