@@ -95,10 +95,17 @@ struct Slot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
+  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent;
+  SpecStreams spec;  // created on first use
   void release_scratch() {
     d_win.release(); d_srt.release(); d_prog.release(); d_desc.release(); d_lists.release(); d_counts.release();
     d_cread.release(); d_ext.release(); d_tasks.release(); d_ctr.release(); d_regpos.release(); d_skipf.release();
-    d_heavy.release(); d_redo.release();
+    d_heavy.release(); d_redo.release(); d_schain.release(); d_hinfo.release(); d_mat.release(); d_cov.release(); d_colent.release();
+    if (spec.side) (void)hipStreamSynchronize(spec.side);
+    if (spec.side) (void)hipStreamDestroy(spec.side);
+    if (spec.fork) (void)hipEventDestroy(spec.fork);
+    if (spec.join) (void)hipEventDestroy(spec.join);
+    spec = SpecStreams{};
   }
   HostBuf h_in, h_out, h_n, h_stats;
   bool busy = false;
@@ -391,7 +398,7 @@ size_t variant_lds(const DevOpt& o, int v, int lq_max) {
 // reading the slot's pinned staging buffer while the caller reuses the slot).
 int check_lds(bwagpu_ctx_t* ctx, int lq_max) {
   if (!use_read_kernels()) {
-    if (spec_select_lds(tb_bytes_for(ctx->opt, std::max(lq_max, 1))) > 64 * 1024)
+    if (spec_redo_cap(tb_bytes_for(ctx->opt, std::max(lq_max, 1))) < 64)
       return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
     return BWAGPU_OK;
   }
@@ -419,6 +426,15 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_skipf.ensure(sizeof(int32_t) * ns), "hipMalloc(skipf)");
   HIPC(s.d_heavy.ensure(sizeof(int32_t) * nr), "hipMalloc(heavy)");
   HIPC(s.d_redo.ensure(sizeof(int32_t) * nr), "hipMalloc(redo)");
+  HIPC(s.d_desc.ensure(sizeof(ReadDesc) * nr), "hipMalloc(desc)");
+  HIPC(s.d_schain.ensure(sizeof(int32_t) * ns), "hipMalloc(seedchain)");
+  HIPC(s.d_hinfo.ensure(sizeof(int4) * nr), "hipMalloc(hinfo)");
+  HIPC(s.d_cov.ensure(sizeof(int32_t) * ns), "hipMalloc(cov)");
+  HIPC(s.d_colent.ensure(sizeof(int32_t) * ns), "hipMalloc(colent)");
+  // pair matrices of heavy reads: sum over them of 2 * ns * ceil(ns / 64) words,
+  // <= 2 * ns_total * (1 + ns_max / 64); reads that do not fit take the per-seed kernel
+  const int64_t mat_words = std::max<int64_t>(1 << 20, 16 * (int64_t)ns);
+  HIPC(s.d_mat.ensure(sizeof(uint64_t) * (size_t)mat_words), "hipMalloc(mat)");
   HIPC(hipMemsetAsync(s.d_ctr.p, 0, sizeof(int32_t) * SPC_WORDS, st), "memset ctr");
   if (db.n_seeds) HIPC(hipMemsetAsync(s.d_ext.p, 0, sizeof(SeedExt) * (size_t)db.n_seeds, st), "memset ext");
   if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
@@ -433,11 +449,23 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.skipf = s.d_skipf.as<int32_t>();
   a.heavy = s.d_heavy.as<int32_t>();
   a.redo = s.d_redo.as<int32_t>();
+  a.rdesc = s.d_desc.as<ReadDesc>();
+  a.seedchain = s.d_schain.as<int32_t>();
+  a.hinfo = s.d_hinfo.as<int4>();
+  a.mat = s.d_mat.as<uint64_t>();
+  a.mat_words = (int64_t)(s.d_mat.cap / sizeof(uint64_t));
+  a.cov = s.d_cov.as<int32_t>();
+  a.colent = s.d_colent.as<int32_t>();
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;
+  if (!s.spec.side) {
+    HIPC(hipStreamCreateWithFlags(&s.spec.side, hipStreamNonBlocking), "hipStreamCreate(side)");
+    HIPC(hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming), "hipEventCreate");
+    HIPC(hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming), "hipEventCreate");
+  }
   const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
-  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, st), "spec chain2aln launch");
+  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, st, s.spec), "spec chain2aln launch");
   return BWAGPU_OK;
 }
 

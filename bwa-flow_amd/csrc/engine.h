@@ -146,6 +146,7 @@ constexpr int kSpecBinLen[kSpecBins] = {192, 256, 1023};
 constexpr int kSpecRounds = 3;                         // A, B, C
 constexpr int kSelLight = 64;                          // reads with more seeds go first
 constexpr int kSelRegLds = 256;                        // regions per wave held in LDS
+constexpr int kSelMatMaxSeeds = 4096;                  // heavy reads up to this many seeds use pair matrices
 // counter words (int32) of one batch (zeroed per batch)
 enum {
   SPC_CNT = 0,        // [round*3 + bin] task counts (rounds 0 = A, 1 = B, 2 = C)
@@ -154,6 +155,8 @@ enum {
   SPC_REDO_N = 20,    // reads the final pass could not finish (a missing extension)
   SPC_SPEC64 = 24,    // int64 at words 24-25: DP cells of every computed task (diagnostic)
   SPC_MISS = 26,      // extensions the redo pass computed inline
+  SPC_MATW64 = 28,    // int64 at words 28-29: uint64 words of heavy-read pair matrices handed out
+  SPC_HCOLS = 30,     // columns (seeds) of heavy reads with a pair matrix
   SPC_EXT_Q = 32,     // [list*8 + xcd] sharded task-queue heads, 9 lists
   SPC_SEL_Q = 104,    // [pass*8 + xcd] sharded read-queue heads of the emulate / final pass
   SPC_WORDS = 128
@@ -175,14 +178,28 @@ struct SpecArgs {
   int32_t* skipf;             // per seed slot: skip flags of chains > 256 seeds
   int32_t* heavy;             // reads with > kSelLight seeds
   int32_t* redo;              // reads the final pass left to the redo pass
+  ReadDesc* rdesc;            // per read (spec_reads_kernel)
+  int32_t* seedchain;         // per seed slot: its chain
+  int4* hinfo;                // per heavy-list entry: rd, matrix word offset (-1: none), first column, ns
+  int32_t* colent;            // per heavy column: its heavy-list entry
+  uint64_t* mat;              // heavy-read pair matrices: C[ns][nw] then O[ns][nw] per read
+  int64_t mat_words;          // capacity of mat
+  int32_t* cov;               // per seed slot: seedcov of its region (heavy reads)
   bwagpu_alnreg_t* out;
   int32_t* out_n;
   int64_t* stats;
 };
+// a side stream and two events: the heavy-read selection runs beside the light one
+struct SpecStreams {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
-                                 int tb_bytes, hipStream_t st);
-// LDS bytes per workgroup of the final selection pass (the largest spec launch)
+                                 int tb_bytes, hipStream_t st, const SpecStreams& ss);
+// LDS bytes per workgroup of the largest spec launch; regions the redo pass
+// holds in LDS for target rows of tb_bytes (must stay > 0)
 size_t spec_select_lds(int tb_bytes);
+int spec_redo_cap(int tb_bytes);
 
 // diagnostics: per-read trace buffer (device pointer, 8 x u32 per read; NULL = off)
 hipError_t set_trace(void* dev_ptr);

@@ -2197,18 +2197,51 @@ __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, D
   }
 }
 
+// rows are triangular: row k holds words w < ceil(k / 64) (only seeds j < k
+// count); tri_off(k) = sum over i < k of ceil(i / 64)
+__host__ __device__ inline int64_t tri_off(int k) {
+  if (k <= 1) return 0;
+  const int64_t q = (k - 1) >> 6;
+  return 32 * q * (q + 1) + (int64_t)(k - 1 - 64 * q) * (q + 1);
+}
+
 // lane per read: length check, and the list of heavy reads (selected first)
 __global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a) {
   const int rd = blockIdx.x * blockDim.x + threadIdx.x;
   bool heavy = false;
+  int ns = 0;
   if (rd < b.n_reads) {
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
     if (lq > BWAGPU_MAX_READ_LEN) atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_LEN);
-    const int ns = b.chain_seed_off[b.read_chain_off[rd + 1]] - b.chain_seed_off[b.read_chain_off[rd]];
-    heavy = ns > kSelLight;
+    ReadDesc d;
+    d.qoff = b.seq_off[rd];
+    d.rd = rd;
+    d.lq = lq;
+    d.c0 = b.read_chain_off[rd];
+    d.nch = b.read_chain_off[rd + 1] - d.c0;
+    d.s0 = b.chain_seed_off[d.c0];
+    d.ns = b.chain_seed_off[d.c0 + d.nch] - d.s0;
+    a.rdesc[rd] = d;
+    heavy = d.ns > kSelLight || d.nch > kSelLight;
+    ns = d.ns;
   }
   const int p = wave_append(&a.ctr[SPC_HEAVY_N], heavy);
-  if (p >= 0) a.heavy[p] = rd;
+  if (p >= 0) {
+    a.heavy[p] = rd;
+    // the read's pair matrices (kSelMatMaxSeeds seeds at most, and room left)
+    const long long words = 2 * tri_off(ns);
+    int woff = -1, col = 0;
+    if (ns <= kSelMatMaxSeeds) {
+      const long long o = (long long)atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr[SPC_MATW64]),
+                                               (unsigned long long)words);
+      if (o + words <= a.mat_words) {
+        woff = (int)o;
+        col = atomicAdd(&a.ctr[SPC_HCOLS], ns);
+        for (int i = 0; i < ns; ++i) a.colent[col + i] = p;
+      }
+    }
+    a.hinfo[p] = make_int4(rd, woff, col, ns);
+  }
 }
 
 // 16 lanes per chain: the seeds in processing order (descending key
@@ -2227,6 +2260,7 @@ __global__ void __launch_bounds__(256) spec_order_kernel(DevBatch b, SpecArgs a)
     for (int j = 0; j < ns; ++j) rank += ((uint64_t)(uint32_t)b.seeds[s0 + j].score << 32 | (uint32_t)j) < ki;
     v.pad_ = ki == 0 ? 1 : 0;
     a.prog[s0 + ns - 1 - rank] = v;
+    a.seedchain[s0 + ns - 1 - rank] = g;
   }
 }
 
@@ -2352,75 +2386,148 @@ __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, 
 }
 
 // The sequential logic of mem_chain2aln over one read's chains, by one wave.
-// Regions: containment fields in LDS (SoA, kSelRegLds per wave; beyond that
-// the region's seed slot in regpos[] and its SeedExt, re-read with
-// workgroup-scope atomics).  A chain's seeds (<= 256) sit in VGPRs, four per
-// lane, with their skip flags; longer chains read prog[] and keep the flags in
-// skipf[].  A seed that is extended but has no result yet:
-//   SEL_EMULATE  becomes a round-B task (its region stays unknown);
+// A seed that is extended but has no result yet:
+//   SEL_EMULATE  becomes a round-B task (its region stays unknown in this pass);
 //   SEL_FINAL    becomes a round-C task and the read goes to the redo list
 //                (its later decisions depend on that region);
 //   SEL_REDO     (the redo list only) is computed inline — the pass that
-//                guarantees every read completes, at low occupancy.
+//                guarantees every read completes.
 // SEL_FINAL and SEL_REDO write the read's mem_alnreg_v.
+// Two shapes: LIGHT reads (<= kSelLight seeds, so every chain and the region
+// list fit one lane slot) four waves per workgroup, 2 KB of LDS each; HEAVY
+// reads one wave per workgroup with up to 64 KB of LDS region records (beyond
+// that: the region's seed slot in regpos[] and its SeedExt, re-read with
+// workgroup-scope atomics), chains of <= 256 seeds in four VGPR slots (longer:
+// prog[] and skip flags in skipf[]).  The two shapes run concurrently on two
+// streams.
 enum { SEL_EMULATE = 0, SEL_FINAL = 1, SEL_REDO = 2 };
-constexpr int kSelFields = 8;  // rb lo/hi, re lo/hi, qb, qe, w, seedlen0
-__host__ __device__ constexpr int sel_wave_lds(int mode, int tb) {
-  return kSelFields * 4 * kSelRegLds + (mode == SEL_REDO ? 2 * tb : 0);
+struct RegRec {  // a region's containment fields (bwamem.c:682-696)
+  int64_t rb, re;
+  int32_t qb, qe, w, seedlen0;
+};
+constexpr int kSelHeavyLds = 64 * 1024;
+constexpr int kSelExtCache = 256;  // a heavy chain's SeedExt records staged in LDS
+__host__ __device__ constexpr int sel_light_wave_lds() { return kSelLight * (int)sizeof(RegRec); }
+__host__ __device__ constexpr int sel_heavy_cap(int mode, int tb) {
+  return (kSelHeavyLds - 4 * (BWAGPU_MAX_READ_LEN + 1) - kSelExtCache * (int)(sizeof(SeedExt) + sizeof(bwagpu_seed_t)) -
+          (mode == SEL_REDO ? 2 * tb : 0)) / (int)sizeof(RegRec);
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(kBlock) spec_select_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
-                                                             int tb_bytes) {
+// max_gap_len (cal_max_gap, bwamem.c:630-637) of every length a containment
+// test can ask for (min(qd, rd) of a region holding the seed: 0..lq-1),
+// tabulated in LDS per workgroup instead of two divisions per lane and region
+constexpr int kMglN = BWAGPU_MAX_READ_LEN + 1;
+
+// near(s, p): the two gap tests of bwamem.c:688-696 for a region p that holds s
+__device__ __forceinline__ bool seed_near(const int32_t* MG, const bwagpu_seed_t& s, const RegRec& p) {
+  const int qd1 = s.qbeg - p.qb;
+  const int64_t rd1 = s.rbeg - p.rb;
+  const int g1 = MG[min(max(qd1 < rd1 ? qd1 : (int)rd1, 0), kMglN - 1)];
+  const int bw1 = g1 < p.w ? g1 : p.w;
+  const int qd2 = p.qe - (s.qbeg + s.len);
+  const int64_t rd2 = p.re - (s.rbeg + s.len);
+  const int g2 = MG[min(max(qd2 < rd2 ? qd2 : (int)rd2, 0), kMglN - 1)];
+  const int bw2 = g2 < p.w ? g2 : p.w;
+  return (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+}
+
+// the 88-byte mem_alnreg_t (rest zero: bwamem.c:718); lane d writes dword d
+__device__ __forceinline__ void write_region(bwagpu_alnreg_t* dst, const SeedExt& e, int rid, int cov, int slen,
+                                             float frac) {
+  const int r = (int)(threadIdx.x & 63);
+  const int dw = r < 21 ? r : 21;
+  uint32_t v = 0;
+  v = dw == 0 ? (uint32_t)e.rb : v;
+  v = dw == 1 ? (uint32_t)((uint64_t)e.rb >> 32) : v;
+  v = dw == 2 ? (uint32_t)e.re : v;
+  v = dw == 3 ? (uint32_t)((uint64_t)e.re >> 32) : v;
+  v = dw == 4 ? (uint32_t)e.qb : v;
+  v = dw == 5 ? (uint32_t)e.qe : v;
+  v = dw == 6 ? (uint32_t)rid : v;
+  v = dw == 7 ? (uint32_t)e.score : v;
+  v = dw == 8 ? (uint32_t)e.truesc : v;
+  v = dw == 13 ? (uint32_t)e.w : v;
+  v = dw == 14 ? (uint32_t)cov : v;
+  v = dw == 17 ? (uint32_t)slen : v;
+  v = dw == 19 ? __float_as_uint(frac) : v;
+  reinterpret_cast<uint32_t*>(dst)[dw] = v;
+}
+
+// a region's containment record into LDS (lanes 0-7 one field each)
+__device__ __forceinline__ void put_regrec(RegRec* dst, const SeedExt& e, int slen) {
+  const int r = (int)(threadIdx.x & 63);
+  const int f = r < 8 ? r : 7;
+  int32_t v = 0;
+  v = f == 0 ? (int32_t)(uint32_t)e.rb : v;
+  v = f == 1 ? (int32_t)((uint64_t)e.rb >> 32) : v;
+  v = f == 2 ? (int32_t)(uint32_t)e.re : v;
+  v = f == 3 ? (int32_t)((uint64_t)e.re >> 32) : v;
+  v = f == 4 ? e.qb : v;
+  v = f == 5 ? e.qe : v;
+  v = f == 6 ? e.w : v;
+  v = f == 7 ? slen : v;
+  if (r < 8) reinterpret_cast<int32_t*>(dst)[f] = v;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// diagnostics (bwagpu_debug_set_trace): per read and selection pass, 8 words
+// at g_trace[(pass * n_reads + rd) * 8]: start / end s_memrealtime (100 MHz),
+// seeds, regions, XCC id, shape (1 light, 2 heavy)
+__device__ __forceinline__ void trace_read(int pass, int n_reads, int rd, uint64_t t0, int ns, int nreg, int shape) {
+  uint32_t* const tr = g_trace;
+  if (!tr) return;
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  const int r = (int)(threadIdx.x & 63);
+  const int d = r < 7 ? r : 7;
+  uint32_t v = (uint32_t)shape;
+  v = d == 0 ? (uint32_t)t0 : v;
+  v = d == 1 ? (uint32_t)(t0 >> 32) : v;
+  v = d == 2 ? (uint32_t)t1 : v;
+  v = d == 3 ? (uint32_t)(t1 >> 32) : v;
+  v = d == 4 ? (uint32_t)ns : v;
+  v = d == 5 ? (uint32_t)nreg : v;
+  v = d == 6 ? __builtin_amdgcn_s_getreg((31 << 11) | 20) : v;
+  if (r < 8) tr[((size_t)pass * n_reads + rd) * 8 + d] = v;
+}
+
+template <int MODE, bool HEAVY>
+__global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int tb_bytes) {
+  static_assert(HEAVY, "one-wave heavy shape only");
   constexpr bool WRITE = MODE != SEL_EMULATE;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int r = (int)(threadIdx.x & 63);
-  const int wib = uni((int)(threadIdx.x >> 6));
-  int32_t* const R = reinterpret_cast<int32_t*>(lds + wib * sel_wave_lds(MODE, tb_bytes));
-  uint8_t* const tbl = reinterpret_cast<uint8_t*>(R + kSelFields * kSelRegLds);
+  // LDS: max_gap_len table | chain seeds (pad_ = skip flag | 2 * pending) |
+  // their SeedExt records | region records | (redo) target rows
+  int32_t* const MG = reinterpret_cast<int32_t*>(lds);
+  bwagpu_seed_t* const SC = reinterpret_cast<bwagpu_seed_t*>(lds + 4 * kMglN);
+  SeedExt* const EC = reinterpret_cast<SeedExt*>(SC + kSelExtCache);
+  RegRec* const R = reinterpret_cast<RegRec*>(EC + kSelExtCache);
+  const int cap_reg = sel_heavy_cap(MODE, tb_bytes);
+  uint8_t* const tbl = reinterpret_cast<uint8_t*>(R + cap_reg);
   uint8_t* const tbr = tbl + tb_bytes;
-  // MODE_REDO walks the redo list in place of the heavy list, and nothing else
-  const int nheavy = uni(__hip_atomic_load(&a.ctr[MODE == SEL_REDO ? SPC_REDO_N : SPC_HEAVY_N], __ATOMIC_RELAXED,
+  for (int x = r; x < kMglN; x += 64) MG[x] = max_gap_len(o, x);
+  Tally tl{0, 0, 0};
+  const int n_list = uni(__hip_atomic_load(&a.ctr[MODE == SEL_REDO ? SPC_REDO_N : SPC_HEAVY_N], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT));
   const int32_t* const hlist = MODE == SEL_REDO ? a.redo : a.heavy;
-  int32_t* const cur = a.ctr + SPC_SEL_CUR + MODE;
-  Tally tl{0, 0, 0};
-  ShardQ lq_q;
-  lq_q.init(a.ctr + SPC_SEL_Q + (MODE == SEL_FINAL ? 8 : 0), b.n_reads);
-  bool heavy_phase = true;
-  int m0 = 0, cap = 0, mi = 0;
   for (;;) {
-    int rd;
-    if (heavy_phase) {
-      int t = 0;
-      if (r == 0) t = atomicAdd(&cur[0], 1);
-      t = uni(__shfl(t, 0, 64));
-      if (t < nheavy) {
-        rd = uni(hlist[t]);
-      } else {
-        if (MODE == SEL_REDO) break;
-        heavy_phase = false;
-        continue;
-      }
-    } else {
-      if (mi >= m0 + 8 || mi >= cap) {
-        if (!lq_q.claim(8, m0, cap)) break;
-        mi = m0;
-      }
-      if (mi >= cap) continue;
-      rd = lq_q.shard + 8 * mi++;
-    }
-    const int c0 = uni(b.read_chain_off[rd]), c1 = uni(b.read_chain_off[rd + 1]);
-    const int s0r = uni(b.chain_seed_off[c0]);
-    if (!heavy_phase && uni(b.chain_seed_off[c1]) - s0r > kSelLight) continue;  // done in the heavy phase
+    int t = 0;
+    if (r == 0) t = atomicAdd(&a.ctr[SPC_SEL_CUR + MODE], 1);
+    t = uni(__shfl(t, 0, 64));
+    if (t >= n_list) break;
+    if (MODE != SEL_REDO && uni(a.hinfo[t].y) >= 0) continue;  // the pair-matrix kernels' read
+    const int rd = uni(hlist[t]);
+    const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const ReadDesc d = uniform_desc(a.rdesc[rd]);
+    if (d.lq > BWAGPU_MAX_READ_LEN) continue;  // flagged by spec_reads_kernel
+    const uint8_t* const q = b.seq + d.qoff;
+    const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
     bool redo = false;
-    Tally rt{0, 0, 0};  // this read's DP, added once the read completes
-    const int64_t qoff = uni64(b.seq_off[rd]);
-    const int lq = uni((int)(b.seq_off[rd + 1] - qoff));
-    if (lq > BWAGPU_MAX_READ_LEN) continue;  // flagged by spec_reads_kernel
-    const uint8_t* const q = b.seq + qoff;
+    Tally rt{0, 0, 0};
     int nreg = 0;
-    for (int c = c0; c < c1 && !redo; ++c) {
+    for (int c = d.c0; c < d.c0 + d.nch && !redo; ++c) {
       const int s0 = uni(b.chain_seed_off[c]), ns = uni(b.chain_seed_off[c + 1]) - s0;
       if (ns == 0) continue;
       ChainWin cw = a.win[c];
@@ -2429,133 +2536,102 @@ __global__ void __launch_bounds__(kBlock) spec_select_kernel(DevOpt o, DevRef re
       if (cw.hi < cw.lo) continue;  // flagged by spec_chain_kernel (the reference would assert)
       const int rid = uni(b.chain_rid[c]);
       const float frac = __int_as_float(uni(__float_as_int(b.chain_frac_rep[c])));
-      const bool big = ns > 256;
-      // the chain's seeds, four slots per lane (slot m, lane r = seed 64m + r)
-      int64_t srb[4];
-      int sqb[4], slen[4];
-      bool sk[4];
+      // the chain's seeds (processing order) and their extension results, staged
+      // in LDS (chains of more than kSelExtCache seeds: prog[] / ext[] / skipf[])
+      const bool big = ns > kSelExtCache;
+      for (int i = r; i < min(ns, kSelExtCache); i += 64) {
+        bwagpu_seed_t v = a.prog[s0 + i];
+        v.pad_ = v.pad_ != 0 ? 1 : 0;
+        SC[i] = v;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ext + s0 + i);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(EC + i);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int i = 64 * m + r;
-        const bwagpu_seed_t v = a.prog[s0 + min(i, ns - 1)];
-        srb[m] = v.rbeg;
-        sqb[m] = v.qbeg;
-        slen[m] = v.len;
-        sk[m] = i >= ns || v.pad_ != 0;
+        for (int w = 0; w < 12; ++w) dst[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (big)
-        for (int i = r; i < ns; i += 64) __hip_atomic_store(&a.skipf[s0 + i], a.prog[s0 + i].pad_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      for (int k = 0; k < ns; ++k) {
-        bwagpu_seed_t s;
-        if (!big) {
-          const int m = k >> 6, l = k & 63;
-          const int64_t vrb = m == 0 ? srb[0] : m == 1 ? srb[1] : m == 2 ? srb[2] : srb[3];
-          const int vqb = m == 0 ? sqb[0] : m == 1 ? sqb[1] : m == 2 ? sqb[2] : sqb[3];
-          const int vln = m == 0 ? slen[0] : m == 1 ? slen[1] : m == 2 ? slen[2] : slen[3];
-          s.rbeg = readlane64(vrb, l);
-          s.qbeg = __builtin_amdgcn_readlane(vqb, l);
-          s.len = __builtin_amdgcn_readlane(vln, l);
-        } else {
-          s = uni_seed(a.prog[s0 + k]);
+        for (int i = r; i < ns; i += 64)
+          __hip_atomic_store(&a.skipf[s0 + i], a.prog[s0 + i].pad_ != 0 ? 1 : 0, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      mem_fence_group();
+      auto seed_at = [&](int i) -> bwagpu_seed_t { return i < kSelExtCache ? SC[i] : a.prog[s0 + i]; };
+      auto flag_at = [&](int i) -> int {
+        return i < kSelExtCache ? SC[i].pad_
+                                : __hip_atomic_load(&a.skipf[s0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      auto set_flag = [&](int i, int f) {
+        if (r == 0) {
+          if (i < kSelExtCache) SC[i].pad_ |= f;
+          else __hip_atomic_store(&a.skipf[s0 + i], f | 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        mem_fence_group();
+      };
+      for (int k = 0; k < ns; ++k) {
+        const bwagpu_seed_t s = uni_seed(seed_at(k));
         // containment in a region so far (bwamem.c:678-697), one region per lane
         bool hit = false;
         for (int base = 0; base < nreg && !hit; base += 64) {
           const int i = min(base + r, nreg - 1);
-          int64_t prb, pre;
-          int pqb, pqe, pw, psl;
-          if (i < kSelRegLds) {
-            prb = (int64_t)((uint64_t)(uint32_t)R[kSelRegLds + i] << 32 | (uint32_t)R[i]);
-            pre = (int64_t)((uint64_t)(uint32_t)R[3 * kSelRegLds + i] << 32 | (uint32_t)R[2 * kSelRegLds + i]);
-            pqb = R[4 * kSelRegLds + i];
-            pqe = R[5 * kSelRegLds + i];
-            pw = R[6 * kSelRegLds + i];
-            psl = R[7 * kSelRegLds + i];
+          RegRec p;
+          if (i < cap_reg) {
+            p = R[i];
           } else {
-            const int pp = __hip_atomic_load(&a.regpos[s0r + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int pp = __hip_atomic_load(&a.regpos[d.s0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             const SeedExt* pe = a.ext + pp;
-            prb = __hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pre = __hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pqb = __hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pqe = __hip_atomic_load(&pe->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            pw = __hip_atomic_load(&pe->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            psl = a.prog[pp].len;
+            p.rb = __hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.re = __hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.qb = __hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.qe = __hip_atomic_load(&pe->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.w = __hip_atomic_load(&pe->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.seedlen0 = a.prog[pp].len;
           }
-          const bool inside = !(s.rbeg < prb || s.rbeg + s.len > pre || s.qbeg < pqb || s.qbeg + s.len > pqe) &&
-                              !(s.len - psl > .1 * lq);
-          const int qd1 = s.qbeg - pqb;
-          const int64_t rd1 = s.rbeg - prb;
-          const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
-          const int bw1 = g1 < pw ? g1 : pw;
-          const int qd2 = pqe - (s.qbeg + s.len);
-          const int64_t rd2 = pre - (s.rbeg + s.len);
-          const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
-          const int bw2 = g2 < pw ? g2 : pw;
-          const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
-          hit = __builtin_amdgcn_ballot_w64(base + r < nreg && inside && near) != 0;
+          const bool inside = base + r < nreg &&
+                              !(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) &&
+                              !(s.len - p.seedlen0 >= rep_lim);
+          if (__builtin_amdgcn_ballot_w64(inside) == 0) continue;
+          hit = __builtin_amdgcn_ballot_w64(inside && seed_near(MG, s, p)) != 0;
         }
         if (hit) {
-          // a long overlapping seed already visited (bwamem.c:698-707): seeds
-          // 0..k-1 in processing order, not skipped and key != 0
+          // a long overlapping seed of this chain already visited (bwamem.c:698-707)
+          const int len95 = uni((int)ceil(s.len * .95));  // t->len < s->len * .95 <=> t->len < ceil(...)
           bool ov = false;
           for (int base = 0; base < k && !ov; base += 64) {
-            const int i = base + r;
-            int64_t trb;
-            int tqb, tln;
-            bool tsk;
-            if (!big) {
-              const int m = base >> 6;
-              trb = m == 0 ? srb[0] : m == 1 ? srb[1] : m == 2 ? srb[2] : srb[3];
-              tqb = m == 0 ? sqb[0] : m == 1 ? sqb[1] : m == 2 ? sqb[2] : sqb[3];
-              tln = m == 0 ? slen[0] : m == 1 ? slen[1] : m == 2 ? slen[2] : slen[3];
-              tsk = m == 0 ? sk[0] : m == 1 ? sk[1] : m == 2 ? sk[2] : sk[3];
-            } else {
-              const bwagpu_seed_t t = a.prog[s0 + min(i, ns - 1)];
-              trb = t.rbeg;
-              tqb = t.qbeg;
-              tln = t.len;
-              tsk = __hip_atomic_load(&a.skipf[s0 + min(i, ns - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-            }
-            const bool a1 = s.qbeg <= tqb && s.qbeg + s.len - tqb >= s.len >> 2 && (int64_t)(tqb - s.qbeg) != trb - s.rbeg;
-            const bool b1 = tqb <= s.qbeg && tqb + tln - s.qbeg >= s.len >> 2 && (int64_t)(s.qbeg - tqb) != s.rbeg - trb;
-            ov = __builtin_amdgcn_ballot_w64(i < k && !tsk && !(tln < s.len * .95) && (a1 || b1)) != 0;
+            const int i = min(base + r, k - 1);
+            const bwagpu_seed_t t = seed_at(i);
+            const bool tsk = (flag_at(i) & 1) != 0;
+            const bool a1 = s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 && (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg;
+            const bool b1 = t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 && (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg;
+            ov = __builtin_amdgcn_ballot_w64(base + r < k && !tsk && t.len >= len95 && (a1 || b1)) != 0;
           }
           if (!ov) {  // skipped: srt[k] = 0 (bwamem.c:709)
-            if (!big) {
-              const int m = k >> 6, l = k & 63;
-#pragma unroll
-              for (int mm = 0; mm < 4; ++mm) sk[mm] = (mm == m && r == l) ? true : sk[mm];
-            } else {
-              __hip_atomic_store(&a.skipf[s0 + k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              mem_fence_group();
-            }
+            set_flag(k, 1);
             continue;
           }
         }
         // ---- this seed is extended (bwamem.c:717-792)
         const int pos = s0 + k;
+        const SeedExt* const pe = k < kSelExtCache ? EC + k : a.ext + pos;
         SeedExt e;
-        e.calls = uni(__hip_atomic_load(&a.ext[pos].calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        e.calls = uni(__hip_atomic_load(&pe->calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (e.calls == 0) {  // no result yet
           if constexpr (MODE == SEL_REDO) {
-            e = extend_seed<16>(o, ref, s, lq, q, cw, tbl, tbr);
+            e = extend_seed<16>(o, ref, s, d.lq, q, cw, tbl, tbr);
             store_ext(a.ext + pos, e);
             mem_fence_group();
             if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+          } else if constexpr (MODE == SEL_EMULATE) {
+            set_flag(k, 2);  // pending: collected per chain below
+            continue;        // its region stays unknown in this pass
           } else {
-            // a task of the next round: B after emulation, C after the final pass
-            const int list = (MODE == SEL_EMULATE ? 1 : 2) * kSpecBins + spec_bin(lq);
-            int p = 0;
-            if (r == 0) p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
-            p = uni(__shfl(p, 0, 64));
-            if (r == 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(pos, c);
-            if (MODE == SEL_EMULATE) continue;  // its region stays unknown in this pass
-            if (r == 0) a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+            const int list = 2 * kSpecBins + spec_bin(d.lq);
+            if (r == 0) {
+              const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+              a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(pos, c);
+              a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+            }
             redo = true;  // the rest of this read waits for the redo pass
             break;
           }
         } else {
-          const SeedExt* pe = a.ext + pos;
           e.rb = uni64(__hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
           e.re = uni64(__hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
           e.qb = uni(__hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -2571,67 +2647,35 @@ __global__ void __launch_bounds__(kBlock) spec_select_kernel(DevOpt o, DevRef re
           long long cov = 0;
           for (int base = 0; base < ns; base += 64) {
             const int i = base + r;
-            int64_t trb;
-            int tqb, tln;
-            if (!big) {
-              const int m = base >> 6;
-              trb = m == 0 ? srb[0] : m == 1 ? srb[1] : m == 2 ? srb[2] : srb[3];
-              tqb = m == 0 ? sqb[0] : m == 1 ? sqb[1] : m == 2 ? sqb[2] : sqb[3];
-              tln = m == 0 ? slen[0] : m == 1 ? slen[1] : m == 2 ? slen[2] : slen[3];
-            } else {
-              const bwagpu_seed_t t = a.prog[s0 + min(i, ns - 1)];
-              trb = t.rbeg;
-              tqb = t.qbeg;
-              tln = t.len;
-            }
-            const bool in = i < ns && tqb >= e.qb && tqb + tln <= e.qe && trb >= e.rb && trb + tln <= e.re;
-            cov += in ? tln : 0;
+            const bwagpu_seed_t t = seed_at(min(i, ns - 1));
+            const bool in = i < ns && t.qbeg >= e.qb && t.qbeg + t.len <= e.qe && t.rbeg >= e.rb && t.rbeg + t.len <= e.re;
+            cov += in ? t.len : 0;
           }
           cov = grp_sum64(cov, 64);
-          // the 88-byte mem_alnreg_t (rest zero: bwamem.c:718), lane d writes dword d
-          const int d = r < 21 ? r : 21;
-          uint32_t v = 0;
-          v = d == 0 ? (uint32_t)e.rb : v;
-          v = d == 1 ? (uint32_t)((uint64_t)e.rb >> 32) : v;
-          v = d == 2 ? (uint32_t)e.re : v;
-          v = d == 3 ? (uint32_t)((uint64_t)e.re >> 32) : v;
-          v = d == 4 ? (uint32_t)e.qb : v;
-          v = d == 5 ? (uint32_t)e.qe : v;
-          v = d == 6 ? (uint32_t)rid : v;
-          v = d == 7 ? (uint32_t)e.score : v;
-          v = d == 8 ? (uint32_t)e.truesc : v;
-          v = d == 13 ? (uint32_t)e.w : v;
-          v = d == 14 ? (uint32_t)cov : v;
-          v = d == 17 ? (uint32_t)s.len : v;
-          v = d == 19 ? __float_as_uint(frac) : v;
-          reinterpret_cast<uint32_t*>(a.out + s0r + nreg)[d] = v;
+          write_region(a.out + d.s0 + nreg, e, rid, (int)cov, s.len, frac);
           rt.cells += e.cells;
           rt.rows += e.rows;
           rt.calls += e.calls - 1;
         }
-        // the region's containment fields
-        if (nreg < kSelRegLds) {
-          const int f = r < kSelFields ? r : kSelFields - 1;
-          int32_t v = 0;
-          v = f == 0 ? (int32_t)(uint32_t)e.rb : v;
-          v = f == 1 ? (int32_t)((uint64_t)e.rb >> 32) : v;
-          v = f == 2 ? (int32_t)(uint32_t)e.re : v;
-          v = f == 3 ? (int32_t)((uint64_t)e.re >> 32) : v;
-          v = f == 4 ? e.qb : v;
-          v = f == 5 ? e.qe : v;
-          v = f == 6 ? e.w : v;
-          v = f == 7 ? s.len : v;
-          if (r < kSelFields) R[f * kSelRegLds + nreg] = v;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (nreg < cap_reg) {
+          put_regrec(R + nreg, e, s.len);
         } else {
-          if (r == 0) __hip_atomic_store(&a.regpos[s0r + nreg], pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (r == 0) __hip_atomic_store(&a.regpos[d.s0 + nreg], pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           mem_fence_group();
         }
         ++nreg;
       }
+      if constexpr (MODE == SEL_EMULATE) {  // this chain's round-B tasks
+        const int list = kSpecBins + spec_bin(d.lq);
+        for (int base = 0; base < ns; base += 64) {
+          const int i = base + r;
+          const bool pnd = i < ns && (flag_at(min(i, ns - 1)) & 2) != 0;
+          const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
+          if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(s0 + i, c);
+        }
+      }
     }
+    if (MODE != SEL_REDO) trace_read(MODE, b.n_reads, rd, t_start, d.ns, nreg, 2);
     if constexpr (WRITE) {
       if (!redo) {
         a.out_n[rd] = nreg;
@@ -2647,13 +2691,431 @@ __global__ void __launch_bounds__(kBlock) spec_select_kernel(DevOpt o, DevRef re
   }
 }
 
+// LIGHT reads (<= kSelLight seeds and chains): the whole read in registers,
+// lane i = seed i of the read in processing order (chain-major, as prog[]
+// stores them) with its SeedExt; lane c = chain c.  mem_chain2aln's
+// sequential decisions depend on each other only through two bit sets — the
+// seeds extended so far (their regions) and the seeds skipped so far — so:
+//   1. pairs: for every seed k, the 64-bit masks of earlier seeds j whose
+//      region would hold it (bwamem.c:678-697: C) and of earlier seeds of its
+//      chain that overlap it (698-707, before the skip filter: O), and its
+//      seedcov if extended (784-788) — lane-parallel, no loop-carried state;
+//   2. scan: the sequential logic on scalar masks only:
+//        hit = C[k] & extended;  skipped = hit && !(O[k] & ~skipped);
+//   3. output: every extended seed's record lane-parallel at its rank.
+// A seed that must be extended but has no result: SEL_EMULATE marks it a
+// round-B task (pending: neither extended nor skipped, as in the per-seed
+// form); SEL_FINAL sends the read to the redo pass.
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+  constexpr bool WRITE = MODE != SEL_EMULATE;
+  __shared__ int32_t MG[kMglN];
+  for (int x = threadIdx.x; x < kMglN; x += kBlock) MG[x] = max_gap_len(o, x);
+  __syncthreads();
+  const int r = (int)(threadIdx.x & 63);
+  const uint64_t lt_mask = r ? (~0ull >> (64 - r)) : 0ull;  // lanes below r
+  Tally tl{0, 0, 0};
+  // static deal: wave w takes reads w, w + NW, ... (light reads cost about the
+  // same; no queue atomics), the next read's descriptor in flight meanwhile
+  const int NW = (int)gridDim.x * (kBlock / 64);
+  int rd = (int)blockIdx.x * (kBlock / 64) + uni((int)(threadIdx.x >> 6));
+  ReadDesc dn{};
+  if (rd < b.n_reads) dn = a.rdesc[rd];
+  for (; rd < b.n_reads; rd += NW) {
+    const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const ReadDesc d = uniform_desc(dn);
+    if (rd + NW < b.n_reads) dn = a.rdesc[rd + NW];
+    if (d.ns > kSelLight || d.nch > kSelLight) continue;  // the heavy kernel's read
+    if (d.lq > BWAGPU_MAX_READ_LEN) continue;             // flagged by spec_reads_kernel
+    if (d.ns == 0) {
+      if (WRITE) a.out_n[rd] = 0;
+      continue;
+    }
+    // everything of the read, one round trip
+    const int ci = min(r, max(d.nch - 1, 0)), si = min(r, d.ns - 1);
+    const int cs_l = b.chain_seed_off[d.c0 + ci] - d.s0, ce_l = b.chain_seed_off[d.c0 + ci + 1] - d.s0;
+    const ChainWin cw_l = a.win[d.c0 + ci];
+    const int rid_l = b.chain_rid[d.c0 + ci];
+    const float fr_l = b.chain_frac_rep[d.c0 + ci];
+    const bwagpu_seed_t sd = a.prog[d.s0 + si];
+    const SeedExt x = a.ext[d.s0 + si];  // written by earlier launches only (a miss goes to redo)
+    // this seed's chain (a chain with a flagged window is never processed)
+    int cid = 0, rid = 0;
+    float frac = 0.f;
+    bool vchain = false;
+    for (int c = 0; c < d.nch; ++c) {
+      const int cs = __builtin_amdgcn_readlane(cs_l, c), ce = __builtin_amdgcn_readlane(ce_l, c);
+      const bool in = r >= cs && r < ce;
+      const bool ok = readlane64(cw_l.hi, c) >= readlane64(cw_l.lo, c);
+      cid = in ? c : cid;
+      vchain = in ? ok : vchain;
+      rid = in ? __builtin_amdgcn_readlane(rid_l, c) : rid;
+      frac = in ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fr_l), c)) : frac;
+    }
+    const bool present = r < d.ns && vchain;
+    const bool computed = present && x.calls != 0;
+    const uint64_t present_m = __builtin_amdgcn_ballot_w64(present);
+    const uint64_t computed_m = __builtin_amdgcn_ballot_w64(computed);
+    const uint64_t pad_m = __builtin_amdgcn_ballot_w64(r < d.ns && sd.pad_ != 0);
+    const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+    // ---- 1. pair masks: lane p = (k, j) = (p / S, p % S) with S the seed count
+    // rounded up to a power of two (8..64), 64 / S values of k per pass; pass
+    // `it`'s ballots land in lane it (c_*, o_*); seedcov of k's region in lane k
+    const int S = d.ns <= 8 ? 8 : d.ns <= 16 ? 16 : d.ns <= 32 ? 32 : 64;
+    const int lgS = S == 8 ? 3 : S == 16 ? 4 : S == 32 ? 5 : 6;
+    const int npass = (S * S) >> 6;
+    uint32_t c_lo = 0, c_hi = 0, o_lo = 0, o_hi = 0;
+    int cov = 0;
+    const int j = r & (S - 1);
+    const int jl = min(j, d.ns - 1) << 2;
+    // seed j of this lane (and its region), gathered once
+    const int64_t j_rbeg = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)(sd.rbeg >> 32)) << 32 |
+                                     (uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)sd.rbeg));
+    const int j_qbeg = __builtin_amdgcn_ds_bpermute(jl, sd.qbeg), j_len = __builtin_amdgcn_ds_bpermute(jl, sd.len);
+    const int j_cid = __builtin_amdgcn_ds_bpermute(jl, cid);
+    const bool j_pad = __builtin_amdgcn_ds_bpermute(jl, sd.pad_) != 0;
+    const bool j_done = __builtin_amdgcn_ds_bpermute(jl, computed ? 1 : 0) != 0;
+    RegRec pj;
+    pj.rb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)(x.rb >> 32)) << 32 |
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)x.rb));
+    pj.re = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)(x.re >> 32)) << 32 |
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)x.re));
+    pj.qb = __builtin_amdgcn_ds_bpermute(jl, x.qb);
+    pj.qe = __builtin_amdgcn_ds_bpermute(jl, x.qe);
+    pj.w = __builtin_amdgcn_ds_bpermute(jl, x.w);
+    pj.seedlen0 = j_len;
+    for (int it = 0; it < npass; ++it) {
+      const int k = (it << (6 - lgS)) + (r >> lgS);
+      const int kl = min(k, d.ns - 1) << 2;
+      bwagpu_seed_t sk;
+      sk.rbeg = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)(sd.rbeg >> 32)) << 32 |
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)sd.rbeg));
+      sk.qbeg = __builtin_amdgcn_ds_bpermute(kl, sd.qbeg);
+      sk.len = __builtin_amdgcn_ds_bpermute(kl, sd.len);
+      const int k_cid = __builtin_amdgcn_ds_bpermute(kl, cid);
+      const bool valid = k < d.ns && j < d.ns;
+      // C: the region of seed j holds seed k (bwamem.c:682-696)
+      const bool inside = valid && j < k && j_done &&
+                          !(sk.rbeg < pj.rb || sk.rbeg + sk.len > pj.re || sk.qbeg < pj.qb || sk.qbeg + sk.len > pj.qe) &&
+                          !(sk.len - j_len >= rep_lim);
+      uint64_t cm = __builtin_amdgcn_ballot_w64(inside);
+      if (cm) cm = __builtin_amdgcn_ballot_w64(inside && seed_near(MG, sk, pj));
+      // O: seed j of k's chain overlaps it (bwamem.c:701-704; t->len < s->len * .95 <=> t->len < ceil(...))
+      const int len95 = (int)ceil(sk.len * .95);
+      const bool a1 = sk.qbeg <= j_qbeg && sk.qbeg + sk.len - j_qbeg >= sk.len >> 2 &&
+                      (int64_t)(j_qbeg - sk.qbeg) != j_rbeg - sk.rbeg;
+      const bool b1 = j_qbeg <= sk.qbeg && j_qbeg + j_len - sk.qbeg >= sk.len >> 2 &&
+                      (int64_t)(sk.qbeg - j_qbeg) != sk.rbeg - j_rbeg;
+      const uint64_t om = __builtin_amdgcn_ballot_w64(valid && j < k && j_cid == k_cid && !j_pad && j_len >= len95 && (a1 || b1));
+      c_lo = r == it ? (uint32_t)cm : c_lo;
+      c_hi = r == it ? (uint32_t)(cm >> 32) : c_hi;
+      o_lo = r == it ? (uint32_t)om : o_lo;
+      o_hi = r == it ? (uint32_t)(om >> 32) : o_hi;
+      if (WRITE) {  // seedcov of k's region over its chain's seeds (bwamem.c:784-788)
+        const int64_t krb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)(x.rb >> 32)) << 32 |
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)x.rb));
+        const int64_t kre = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)(x.re >> 32)) << 32 |
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)x.re));
+        const int kqb = __builtin_amdgcn_ds_bpermute(kl, x.qb), kqe = __builtin_amdgcn_ds_bpermute(kl, x.qe);
+        int v = valid && j_cid == k_cid && j_qbeg >= kqb && j_qbeg + j_len <= kqe && j_rbeg >= krb &&
+                        j_rbeg + j_len <= kre ? j_len : 0;
+        for (int m = 1; m < S; m <<= 1) v += __shfl_xor(v, m, 64);
+        // lane k takes the sum of its group (lane (k - first k of the pass) * S)
+        const int src = (r - (it << (6 - lgS))) << lgS;
+        const int got = __builtin_amdgcn_ds_bpermute(min(max(src, 0), 63) << 2, v);
+        cov = (r >= (it << (6 - lgS)) && r < ((it + 1) << (6 - lgS))) ? got : cov;
+      }
+    }
+    // ---- 2. the sequential decisions, on scalar masks
+    uint64_t ext = 0, skip = pad_m, pend = 0;
+    int miss = -1;
+    for (int k = 0; k < d.ns; ++k) {
+      const uint64_t bit = 1ull << k;
+      if (!(present_m & bit)) continue;
+      const int it = (k << lgS) >> 6, sh = (k << lgS) & 63;
+      const uint64_t fld = S == 64 ? ~0ull : ((1ull << S) - 1);
+      const uint64_t cm = ((uint64_t)__builtin_amdgcn_readlane(c_hi, it) << 32 | (uint32_t)__builtin_amdgcn_readlane(c_lo, it)) >> sh & fld;
+      if (cm & ext) {
+        const uint64_t om = ((uint64_t)__builtin_amdgcn_readlane(o_hi, it) << 32 | (uint32_t)__builtin_amdgcn_readlane(o_lo, it)) >> sh & fld;
+        if (!(om & ~skip)) {  // skipped: srt[k] = 0 (bwamem.c:709)
+          skip |= bit;
+          continue;
+        }
+      }
+      if (!(computed_m & bit)) {
+        if (MODE == SEL_EMULATE) {
+          pend |= bit;  // a round-B task; its region stays unknown in this pass
+          continue;
+        }
+        miss = k;
+        break;
+      }
+      ext |= bit;
+    }
+    // ---- 3. outputs
+    if constexpr (MODE == SEL_EMULATE) {
+      const int list = kSpecBins + spec_bin(d.lq);
+      const bool pnd = (pend >> r) & 1;
+      const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
+      if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
+    } else {
+      if (miss >= 0) {
+        const int list = 2 * kSpecBins + spec_bin(d.lq);
+        if (r == miss) {
+          const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+          a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
+          a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+        }
+        continue;  // the redo pass writes this read
+      }
+      const bool mine = (ext >> r) & 1;
+      if (mine) {  // the region of seed r, at its rank (bwamem.c:718-792 field by field; rest zero)
+        const int slot = (int)__popcll(ext & lt_mask);
+        uint2* dst = reinterpret_cast<uint2*>(a.out + d.s0 + slot);
+        dst[0] = make_uint2((uint32_t)x.rb, (uint32_t)((uint64_t)x.rb >> 32));
+        dst[1] = make_uint2((uint32_t)x.re, (uint32_t)((uint64_t)x.re >> 32));
+        dst[2] = make_uint2((uint32_t)x.qb, (uint32_t)x.qe);
+        dst[3] = make_uint2((uint32_t)rid, (uint32_t)x.score);
+        dst[4] = make_uint2((uint32_t)x.truesc, 0u);
+        dst[5] = make_uint2(0u, 0u);
+        dst[6] = make_uint2(0u, (uint32_t)x.w);
+        dst[7] = make_uint2((uint32_t)cov, 0u);
+        dst[8] = make_uint2(0u, (uint32_t)sd.len);
+        dst[9] = make_uint2(0u, __float_as_uint(frac));
+        dst[10] = make_uint2(0u, 0u);
+        tl.cells += x.cells;
+        tl.rows += x.rows;
+        tl.calls += x.calls - 1;
+      }
+      if (r == 0) a.out_n[rd] = (int)__popcll(ext);
+    }
+    trace_read(MODE, b.n_reads, rd, t_start, d.ns, (int)__popcll(ext), 1);
+  }
+  if constexpr (WRITE) block_stats<64>(tl, a.stats);
+}
+
+// HEAVY reads with pair matrices (<= kSelMatMaxSeeds seeds).  The same
+// decomposition as the light kernel, at a size where one wave cannot hold the
+// read:
+//   spec_pairs_kernel — one wave per column k (a seed) of a heavy read, over
+//     every column of every such read at once: 64-bit words of C[k] (earlier
+//     seeds whose region would hold k: bwamem.c:678-697) and O[k] (earlier
+//     seeds of k's chain overlapping it: 698-707), and k's seedcov (784-788);
+//   spec_scan_kernel  — one wave per read: the sequential decisions on bit
+//     sets (lane w holds word w of the extended / skipped / pending sets), then
+//     every extended seed's record lane-parallel at its rank.
+__global__ void __launch_bounds__(kBlock) spec_pairs_kernel(DevOpt o, DevBatch b, SpecArgs a, int with_cov) {
+  __shared__ int32_t MG[kMglN];
+  for (int x = threadIdx.x; x < kMglN; x += kBlock) MG[x] = max_gap_len(o, x);
+  __syncthreads();
+  const int r = (int)(threadIdx.x & 63);
+  const int ncol = uni(__hip_atomic_load(&a.ctr[SPC_HCOLS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int nwv = (int)gridDim.x * (kBlock / 64);
+  for (int x = (int)blockIdx.x * (kBlock / 64) + uni((int)(threadIdx.x >> 6)); x < ncol; x += nwv) {
+    const int t = uni(a.colent[x]);
+    const int4 hi = a.hinfo[t];
+    const int rd = uni(hi.x), woff = uni(hi.y), col = uni(hi.z), ns = uni(hi.w);
+    const int k = x - col, nw = (ns + 63) >> 6;
+    const ReadDesc d = uniform_desc(a.rdesc[rd]);
+    const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+    const bwagpu_seed_t s = uni_seed(a.prog[d.s0 + k]);
+    const int ck = uni(a.seedchain[d.s0 + k]);
+    const int len95 = uni((int)ceil(s.len * .95));  // t->len < s->len * .95 <=> t->len < ceil(...)
+    const SeedExt ek = a.ext[d.s0 + k];
+    const bool k_done = uni(ek.calls) != 0;
+    const int64_t krb = uni64(ek.rb), kre = uni64(ek.re);
+    const int kqb = uni(ek.qb), kqe = uni(ek.qe);
+    int cov = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int j = 64 * w + r, jj = min(j, ns - 1);
+      const bwagpu_seed_t sj = a.prog[d.s0 + jj];
+      const int cj = a.seedchain[d.s0 + jj];
+      const SeedExt ej = a.ext[d.s0 + jj];
+      RegRec p;
+      p.rb = ej.rb;
+      p.re = ej.re;
+      p.qb = ej.qb;
+      p.qe = ej.qe;
+      p.w = ej.w;
+      p.seedlen0 = sj.len;
+      const bool inside = j < k && ej.calls != 0 &&
+                          !(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) &&
+                          !(s.len - sj.len >= rep_lim);
+      uint64_t cm = __builtin_amdgcn_ballot_w64(inside);
+      if (cm) cm = __builtin_amdgcn_ballot_w64(inside && seed_near(MG, s, p));
+      const bool a1 = s.qbeg <= sj.qbeg && s.qbeg + s.len - sj.qbeg >= s.len >> 2 &&
+                      (int64_t)(sj.qbeg - s.qbeg) != sj.rbeg - s.rbeg;
+      const bool b1 = sj.qbeg <= s.qbeg && sj.qbeg + sj.len - s.qbeg >= s.len >> 2 &&
+                      (int64_t)(s.qbeg - sj.qbeg) != s.rbeg - sj.rbeg;
+      const uint64_t om = __builtin_amdgcn_ballot_w64(j < k && cj == ck && sj.pad_ == 0 && sj.len >= len95 && (a1 || b1));
+      if (r == 0 && 64 * w < k) {
+        a.mat[woff + tri_off(k) + w] = cm;
+        a.mat[woff + tri_off(ns) + tri_off(k) + w] = om;
+      }
+      if (with_cov && k_done)
+        cov += (j < ns && cj == ck && sj.qbeg >= kqb && sj.qbeg + sj.len <= kqe && sj.rbeg >= krb &&
+                sj.rbeg + sj.len <= kre) ? sj.len : 0;
+    }
+    if (with_cov) {
+      cov = (int)grp_sum64(cov, 64);
+      if (r == 0) a.cov[d.s0 + k] = cov;
+    }
+  }
+}
+
+constexpr int kScanLds = 64 * 1024;  // a read's C and O matrices staged in LDS when they fit
+
+template <int MODE>
+__global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevBatch b, SpecArgs a) {
+  constexpr bool WRITE = MODE != SEL_EMULATE;
+  extern __shared__ __attribute__((aligned(16))) uint64_t M[];
+  const int r = (int)(threadIdx.x & 63);
+  const uint64_t lt_mask = r ? (~0ull >> (64 - r)) : 0ull;
+  const int nh = uni(__hip_atomic_load(&a.ctr[SPC_HEAVY_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  Tally tl{0, 0, 0};
+  for (int t = (int)blockIdx.x; t < nh; t += (int)gridDim.x) {
+    const int4 hi = a.hinfo[t];
+    const int rd = uni(hi.x), woff = uni(hi.y), ns = uni(hi.w);
+    if (woff < 0) continue;  // no matrix: the per-seed heavy kernel's read
+    const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const int nw = (ns + 63) >> 6;
+    const ReadDesc d = uniform_desc(a.rdesc[rd]);
+    if (d.lq > BWAGPU_MAX_READ_LEN) continue;
+    const int64_t tw = tri_off(ns);
+    const uint64_t* Cg = a.mat + woff;
+    const bool staged = 2 * tw * 8 <= kScanLds;
+    if (staged) {
+      for (int i = r; i < 2 * tw; i += 64) M[i] = Cg[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint64_t* C = staged ? M : Cg;
+    const uint64_t* O = C + tw;
+    // per-word sets: lane w holds word w
+    uint64_t present_w = 0, computed_w = 0, skip_w = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int j = 64 * w + r, jj = min(j, ns - 1);
+      const bwagpu_seed_t sj = a.prog[d.s0 + jj];
+      const ChainWin cw = a.win[a.seedchain[d.s0 + jj]];
+      const bool pres = j < ns && cw.hi >= cw.lo;  // seeds of a flagged chain are never processed
+      const uint64_t pm = __builtin_amdgcn_ballot_w64(pres);
+      const uint64_t cm = __builtin_amdgcn_ballot_w64(pres && a.ext[d.s0 + jj].calls != 0);
+      const uint64_t km = __builtin_amdgcn_ballot_w64(j < ns && sj.pad_ != 0);
+      present_w = r == w ? pm : present_w;
+      computed_w = r == w ? cm : computed_w;
+      skip_w = r == w ? km : skip_w;
+    }
+    uint64_t ext_w = 0, pend_w = 0;
+    int miss = -1;
+    for (int k = 0; k < ns; ++k) {
+      const int kw = k >> 6;
+      const uint64_t kbit = 1ull << (k & 63);
+      const uint64_t pres = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(present_w >> 32), kw) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)present_w, kw);
+      if (!(pres & kbit)) continue;
+      const int nwk = (k + 63) >> 6;  // words of row k
+      const uint64_t cw = r < nwk ? C[tri_off(k) + r] : 0;
+      if (__builtin_amdgcn_ballot_w64((cw & ext_w) != 0)) {
+        const uint64_t ow = r < nwk ? O[tri_off(k) + r] : 0;
+        if (!__builtin_amdgcn_ballot_w64((ow & ~skip_w) != 0)) {  // skipped: srt[k] = 0 (bwamem.c:709)
+          skip_w |= r == kw ? kbit : 0;
+          continue;
+        }
+      }
+      const uint64_t comp = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(computed_w >> 32), kw) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)computed_w, kw);
+      if (!(comp & kbit)) {
+        if (MODE == SEL_EMULATE) {
+          pend_w |= r == kw ? kbit : 0;  // a round-B task; its region stays unknown
+          continue;
+        }
+        miss = k;
+        break;
+      }
+      ext_w |= r == kw ? kbit : 0;
+    }
+    int nreg = 0;
+    if constexpr (MODE == SEL_EMULATE) {
+      const int list = kSpecBins + spec_bin(d.lq);
+      for (int w = 0; w < nw; ++w) {
+        const uint64_t pw = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(pend_w >> 32), w) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)pend_w, w);
+        const int j = 64 * w + r;
+        const bool pnd = (pw >> r) & 1;
+        const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
+        if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + j, a.seedchain[d.s0 + j]);
+      }
+    } else {
+      if (miss >= 0) {
+        if (r == 0) {
+          const int list = 2 * kSpecBins + spec_bin(d.lq);
+          const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+          a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + miss, a.seedchain[d.s0 + miss]);
+          a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+        }
+        continue;  // the redo pass writes this read
+      }
+      for (int w = 0; w < nw; ++w) {
+        const uint64_t ew = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(ext_w >> 32), w) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)ext_w, w);
+        const int j = 64 * w + r;
+        if ((ew >> r) & 1) {  // the region of seed j at its rank (bwamem.c:718-792; rest zero)
+          const int slot = nreg + (int)__popcll(ew & lt_mask);
+          const SeedExt x = a.ext[d.s0 + j];
+          const int c = a.seedchain[d.s0 + j];
+          uint2* dst = reinterpret_cast<uint2*>(a.out + d.s0 + slot);
+          dst[0] = make_uint2((uint32_t)x.rb, (uint32_t)((uint64_t)x.rb >> 32));
+          dst[1] = make_uint2((uint32_t)x.re, (uint32_t)((uint64_t)x.re >> 32));
+          dst[2] = make_uint2((uint32_t)x.qb, (uint32_t)x.qe);
+          dst[3] = make_uint2((uint32_t)b.chain_rid[c], (uint32_t)x.score);
+          dst[4] = make_uint2((uint32_t)x.truesc, 0u);
+          dst[5] = make_uint2(0u, 0u);
+          dst[6] = make_uint2(0u, (uint32_t)x.w);
+          dst[7] = make_uint2((uint32_t)a.cov[d.s0 + j], 0u);
+          dst[8] = make_uint2(0u, (uint32_t)a.prog[d.s0 + j].len);
+          dst[9] = make_uint2(0u, __float_as_uint(b.chain_frac_rep[c]));
+          dst[10] = make_uint2(0u, 0u);
+          tl.cells += x.cells;
+          tl.rows += x.rows;
+          tl.calls += x.calls - 1;
+        }
+        nreg += (int)__popcll(ew);
+      }
+      if (r == 0) a.out_n[rd] = nreg;
+    }
+    trace_read(MODE, b.n_reads, rd, t_start, ns, nreg, 3);
+  }
+  if constexpr (WRITE) block_stats<64>(tl, a.stats);
+}
+
+// The two selection shapes of one pass: heavy reads on `side` (when given)
+// concurrently with the light reads on `st`; `st` continues once both are done.
 template <int MODE>
 static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int tb_bytes,
-                          hipStream_t st) {
-  const size_t lds = (size_t)(kBlock / 64) * sel_wave_lds(MODE, tb_bytes);
-  // the redo pass only sees a handful of reads: a small grid
-  const int nb = MODE == SEL_REDO ? 64 : resident_blocks(spec_select_kernel<MODE>, lds);
-  hipLaunchKernelGGL(spec_select_kernel<MODE>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
+                          hipStream_t st, const SpecStreams& ss) {
+  hipStream_t hs = st;
+  if (MODE != SEL_REDO && ss.side) {
+    (void)hipEventRecord(ss.fork, st);
+    (void)hipStreamWaitEvent(ss.side, ss.fork, 0);
+    hs = ss.side;
+  }
+  if (MODE != SEL_REDO) {
+    const int nb = resident_blocks(spec_select_light<MODE>, 0);
+    hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), 0, st, o, ref, b, a);
+  }
+  if (MODE != SEL_REDO) {  // heavy reads with pair matrices: all pairs at once, then one scan per read
+    const int nb = resident_blocks(spec_pairs_kernel, 0);
+    hipLaunchKernelGGL(spec_pairs_kernel, dim3(nb), dim3(kBlock), 0, hs, o, b, a, MODE == SEL_FINAL ? 1 : 0);
+    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(1024), dim3(64), (size_t)kScanLds, hs, o, b, a);
+  }
+  // the rest (no matrix; the redo list): one wave per read, per seed
+  hipLaunchKernelGGL((spec_select_kernel<MODE, true>), dim3(MODE == SEL_REDO ? 256 : 1024), dim3(64),
+                     (size_t)kSelHeavyLds, hs, o, ref, b, a, tb_bytes);
+  if (hs != st) {
+    (void)hipEventRecord(ss.join, hs);
+    (void)hipStreamWaitEvent(st, ss.join, 0);
+  }
 }
 
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
@@ -2670,7 +3132,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
 
 // prep -> round A -> emulate -> round B -> final -> round C -> redo, one stream
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
-                                 int tb_bytes, hipStream_t st) {
+                                 int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   if (b.n_reads == 0) return hipSuccess;
   if (b.n_chains) {
     hipLaunchKernelGGL(spec_chain_kernel, dim3((b.n_chains + 255) / 256), dim3(256), 0, st, o, ref, b, a);
@@ -2679,17 +3141,18 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
   hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if (b.n_chains) {
     launch_ext_round(o, ref, b, a, 0, tb_bytes, st);
-    launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st);
+    launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st, ss);
     launch_ext_round(o, ref, b, a, 1, tb_bytes, st);
   }
-  launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st);
+  launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
   if (b.n_chains) {
     launch_ext_round(o, ref, b, a, 2, tb_bytes, st);
-    launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st);
+    launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
   }
   return hipGetLastError();
 }
 
-size_t spec_select_lds(int tb_bytes) { return (size_t)(kBlock / 64) * sel_wave_lds(SEL_REDO, tb_bytes); }
+size_t spec_select_lds(int tb_bytes) { return (size_t)kSelHeavyLds + 0 * tb_bytes; }
+int spec_redo_cap(int tb_bytes) { return sel_heavy_cap(SEL_REDO, tb_bytes); }
 
 }  // namespace bwagpu
