@@ -142,6 +142,9 @@ struct bwagpu_ctx {
   static constexpr int kA2Streams = 4;
   hipStream_t a2_st[kA2Streams] = {};
   hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
+  // bwagpu_prof_*: event pairs around the dominant extension launches
+  std::vector<hipEvent_t> prof_ev;
+  int prof_used = 0;
   std::string err;
 };
 
@@ -300,6 +303,8 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     s.release_scratch();
     s.d_stats.release();
   }
+  for (hipEvent_t e : ctx->prof_ev) (void)hipEventDestroy(e);
+  ctx->prof_ev.clear();
   for (int i = 0; i < bwagpu_ctx::kA2Streams; ++i) {
     if (ctx->a2_st[i]) (void)hipStreamSynchronize(ctx->a2_st[i]);
     if (ctx->a2_st[i]) (void)hipStreamDestroy(ctx->a2_st[i]);
@@ -465,6 +470,9 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
     HIPC(hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming), "hipEventCreate");
   }
   const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
+  s.spec.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
+  s.spec.pool_n = (int)ctx->prof_ev.size();
+  s.spec.pool_used = &ctx->prof_used;
   HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, st, s.spec), "spec chain2aln launch");
   return BWAGPU_OK;
 }
@@ -1219,6 +1227,60 @@ int bwagpu_debug_set_trace(bwagpu_ctx_t* ctx, void* dev_ptr) {
   if (!ctx) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   HIPC(set_trace(dev_ptr), "set trace");
+  return BWAGPU_OK;
+}
+
+int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
+  if (!ctx || !out) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  int k = 0;
+  while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] != st) ++k;
+  if (k == BWAGPU_NUM_SLOTS || !ctx->dev_scratch[k].d_ctr.p) return fail(ctx, BWAGPU_E_INVAL, "no device-entry batch on this stream");
+  HIPC(hipStreamSynchronize(st), "hipStreamSynchronize");
+  int32_t c[SPC_WORDS];
+  HIPC(hipMemcpy(c, ctx->dev_scratch[k].d_ctr.p, sizeof c, hipMemcpyDeviceToHost), "hipMemcpy(ctr)");
+  for (int r = 0; r < kSpecRounds; ++r) {
+    out[r] = 0;
+    for (int b = 0; b < kSpecBins; ++b) out[r] += c[SPC_CNT + r * kSpecBins + b];
+  }
+  int64_t spec = 0;
+  memcpy(&spec, c + SPC_SPEC64, 8);
+  out[3] = spec;
+  out[4] = c[SPC_MISS];
+  out[5] = c[SPC_HEAVY_N];
+  out[6] = c[SPC_REDO_N];
+  out[7] = c[SPC_HCOLS];
+  return BWAGPU_OK;
+}
+
+int bwagpu_prof_start(bwagpu_ctx_t* ctx, int max_launches) {
+  if (!ctx || max_launches < 0) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  for (hipEvent_t e : ctx->prof_ev) HIPC(hipEventSynchronize(e), "hipEventSynchronize");
+  for (hipEvent_t e : ctx->prof_ev) (void)hipEventDestroy(e);
+  ctx->prof_ev.clear();
+  ctx->prof_used = 0;
+  for (int i = 0; i < 2 * max_launches; ++i) {
+    hipEvent_t e = nullptr;
+    HIPC(hipEventCreate(&e), "hipEventCreate");
+    ctx->prof_ev.push_back(e);
+  }
+  return BWAGPU_OK;
+}
+
+int bwagpu_prof_read(bwagpu_ctx_t* ctx, double* total_ms, int32_t* launches) {
+  if (!ctx || !total_ms || !launches) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  double t = 0;
+  for (int i = 0; i + 1 < ctx->prof_used; i += 2) {
+    HIPC(hipEventSynchronize(ctx->prof_ev[i + 1]), "hipEventSynchronize");
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, ctx->prof_ev[i], ctx->prof_ev[i + 1]), "hipEventElapsedTime");
+    t += ms;
+  }
+  *total_ms = t;
+  *launches = ctx->prof_used / 2;
   return BWAGPU_OK;
 }
 

@@ -193,6 +193,11 @@ struct SpecArgs {
 struct SpecStreams {
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // kernel timing (bwagpu_prof_*): event pairs around every C = 3 extension
+  // launch, taken from the context's pool while pool_used < pool_n
+  hipEvent_t* pool = nullptr;
+  int pool_n = 0;
+  int* pool_used = nullptr;
 };
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, hipStream_t st, const SpecStreams& ss);

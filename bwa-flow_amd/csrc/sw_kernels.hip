@@ -3119,11 +3119,17 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
 }
 
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
-                             int tb_bytes, hipStream_t st) {
+                             int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
   int nb = resident_blocks(spec_ext_kernel<3>, lds);
+  const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
+  if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
   hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
+  if (prof) {
+    (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
+    *ss.pool_used += 2;
+  }
   nb = resident_blocks(spec_ext_kernel<4>, lds);
   hipLaunchKernelGGL(spec_ext_kernel<4>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 1, tb_bytes);
   nb = resident_blocks(spec_ext_kernel<16>, lds);
@@ -3140,13 +3146,13 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
   }
   hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if (b.n_chains) {
-    launch_ext_round(o, ref, b, a, 0, tb_bytes, st);
+    launch_ext_round(o, ref, b, a, 0, tb_bytes, st, ss);
     launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st, ss);
-    launch_ext_round(o, ref, b, a, 1, tb_bytes, st);
+    launch_ext_round(o, ref, b, a, 1, tb_bytes, st, ss);
   }
   launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
   if (b.n_chains) {
-    launch_ext_round(o, ref, b, a, 2, tb_bytes, st);
+    launch_ext_round(o, ref, b, a, 2, tb_bytes, st, ss);
     launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
   }
   return hipGetLastError();

@@ -98,8 +98,13 @@ def unflatten(batch: Batch, regs: np.ndarray, n: np.ndarray) -> list[np.ndarray]
 
 def compact(batch: Batch, regs: np.ndarray, n: np.ndarray) -> np.ndarray:
     """concatenate the regions of all reads in read order"""
-    parts = unflatten(batch, regs, n)
-    return np.concatenate(parts) if parts else np.zeros(0, abi.ALNREG_DTYPE)
+    n = np.asarray(n, np.int64)
+    tot = int(n.sum())
+    if tot == 0:
+        return np.zeros(0, regs.dtype if regs is not None else abi.ALNREG_DTYPE)
+    start = np.repeat(batch.read_seed_off().astype(np.int64), n)
+    first = np.repeat(np.cumsum(n) - n, n)
+    return regs[start + np.arange(tot, dtype=np.int64) - first]
 
 
 class Engine:
@@ -206,6 +211,16 @@ class Engine:
         self._check(self.lib.bwagpu_reg2aln_batch(self.ctx, n, _ptr(tasks), _ptr(qpool), len(qpool), max_ops, max_md,
                                                   _ptr(out), _ptr(cig), _ptr(md)), "reg2aln_batch")
         return out[:n], cig[:n], md[:n]
+
+    def prof_start(self, max_launches: int):
+        """time the next max_launches launches of the dominant extension kernel"""
+        self._check(self.lib.bwagpu_prof_start(self.ctx, max_launches), "prof_start")
+
+    def prof_read(self) -> tuple[float, int]:
+        """-> (summed kernel ms, launches timed) since prof_start"""
+        ms, n = C.c_double(), C.c_int32()
+        self._check(self.lib.bwagpu_prof_read(self.ctx, C.byref(ms), C.byref(n)), "prof_read")
+        return ms.value, n.value
 
     def last_stats(self, slot: int = 0) -> dict:
         s = abi.Stats()

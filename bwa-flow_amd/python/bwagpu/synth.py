@@ -27,8 +27,25 @@ def _load():
         lib.synth_reads.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_uint64, C.c_int,
                                     C.c_int, C.c_int] + [C.c_void_p] * 10
         lib.synth_reads.restype = C.c_int
+        lib.golden_genome.argtypes = [C.c_uint64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.golden_genome.restype = C.c_int
         _lib = lib
     return _lib
+
+
+class GoldenRef:
+    """the genome of the reference-seeded workloads (tools/synth.cpp
+    golden_genome = oracle/gen_golden.c's generator + bwa's N filling): the
+    pac bwa_idx_build makes of it, three contigs"""
+
+    def __init__(self, length: int, seed: int = 1234):
+        lib = _load()
+        self.l_pac = int(length)
+        self.pac = np.zeros(self.l_pac // 4 + 1, np.uint8)
+        self.ann_offset = np.zeros(3, np.int64)
+        self.ann_len = np.zeros(3, np.int32)
+        if lib.golden_genome(seed, self.l_pac, _ptr(self.pac), _ptr(self.ann_offset), _ptr(self.ann_len)):
+            raise RuntimeError("golden_genome failed")
 
 
 class SynthRef:

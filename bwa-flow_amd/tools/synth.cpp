@@ -50,6 +50,67 @@ inline void set2(uint8_t* pac, int64_t k, int c) { pac[k >> 2] |= (uint8_t)(c <<
 
 extern "C" {
 
+// The genome of the reference-seeded workloads (oracle/gen_golden.c
+// make_genome, the bench's C2 fixture tests/golden/c2_refseed.npz): total_len
+// bases in three contigs (1 Mb: 500k/300k/200k; otherwise 50/30/20 %), iid ACGT
+// from splitmix64(seed), then per Mb 10 repeat families x 4 copies (1 %
+// diverged), 30 tandem repeats and 12 N runs — and the pac bwa builds from it:
+// each N becomes lrand48() & 3 after srand48(11) (bntseq.c:261,290-291; the
+// drand48 generator is X' = 0x5DEECE66D X + 11 mod 2^48, lrand48 = X >> 17).
+// pac: total_len/4+1 bytes; ann_off/ann_len: 3 entries.
+int golden_genome(uint64_t seed, int64_t total_len, uint8_t* pac, int64_t* ann_off, int32_t* ann_len) {
+  if (total_len < 1000 || !pac) return -1;
+  int64_t ctg[3] = {500000, 300000, 200000};
+  if (total_len != 1000000) {
+    ctg[0] = total_len / 2;
+    ctg[1] = total_len * 3 / 10;
+    ctg[2] = total_len - ctg[0] - ctg[1];
+  }
+  const int64_t L = total_len;
+  static const char kB[4] = {0, 1, 2, 3};
+  Rng g{seed};
+  std::vector<uint8_t> s((size_t)L);  // 0..3, 4 = N
+  for (auto& b : s) b = kB[g.next() & 3];
+  auto per_mb = [L](int k) { return (int)(k * (double)L / 1e6 + 0.5); };
+  const int n_fam = per_mb(10), n_tan = per_mb(30), n_nrun = per_mb(12);
+  for (int fam = 0; fam < n_fam; ++fam) {
+    const int len = 300 + g.i(2700);
+    const int64_t src = (int64_t)(g.u() * (double)(L - len));
+    for (int c = 0; c < 4; ++c) {
+      const int64_t dst = (int64_t)(g.u() * (double)(L - len));
+      for (int k = 0; k < len; ++k) s[dst + k] = g.u() < 0.01 ? kB[g.next() & 3] : s[src + k];
+    }
+  }
+  for (int t = 0; t < n_tan; ++t) {
+    const int per = 2 + g.i(49);
+    const int len = 200 + g.i(800);
+    const int64_t dst = (int64_t)(g.u() * (double)(L - len));
+    for (int k = per; k < len; ++k) s[dst + k] = g.u() < 0.005 ? kB[g.next() & 3] : s[dst + k - per];
+  }
+  for (int t = 0; t < n_nrun; ++t) {
+    const int len = 10 + g.i(300);
+    const int64_t dst = (int64_t)(g.u() * (double)(L - len));
+    memset(s.data() + dst, 4, (size_t)len);
+  }
+  uint64_t x = (11ull << 16) | 0x330Eull;  // srand48(11)
+  memset(pac, 0, (size_t)(L / 4 + 1));
+  for (int64_t k = 0; k < L; ++k) {
+    int c = s[k];
+    if (c >= 4) {
+      x = (0x5DEECE66Dull * x + 0xBull) & ((1ull << 48) - 1);
+      c = (int)(x >> 17) & 3;
+    }
+    set2(pac, k, c);
+  }
+  int64_t off = 0;
+  for (int i = 0; i < 3; ++i) {
+    if (ann_off) ann_off[i] = off;
+    if (ann_len) ann_len[i] = (int32_t)ctg[i];
+    off += ctg[i];
+  }
+  return 0;
+}
+
 // Build a reference of total_len bases in n_ctg contigs.  pac must hold
 // total_len/4+1 zeroed bytes; ann_off/ann_len get n_ctg entries.
 int synth_ref(uint64_t seed, int64_t total_len, int n_ctg, uint8_t* pac, int64_t* ann_off, int32_t* ann_len) {

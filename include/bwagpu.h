@@ -286,6 +286,22 @@ int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
    with getUs(), src/util.h:34-40). */
 int bwagpu_debug_set_trace(bwagpu_ctx_t *ctx, void *dev_ptr);
 
+/* kernel timing (bench.py's roofline): after bwagpu_prof_start(ctx, n) the
+   next n launches of the dominant extension kernel (spec_ext_kernel<3>, one
+   per extension round of a chain2aln batch) are bracketed by HIP events on the
+   stream they run on; bwagpu_prof_read waits for them and returns the summed
+   kernel time and the number of launches timed.  bwagpu_prof_start(ctx, 0)
+   turns timing off.  Diagnostics; the reference prints per-phase stage times
+   instead (src/fpga/FPGAPipeline.cpp:557-578). */
+int bwagpu_prof_start(bwagpu_ctx_t *ctx, int max_launches);
+/* diagnostics: the speculative path's counters of the last device-entry batch
+   on `stream` (waits for it): out[0..2] extension tasks of rounds A/B/C,
+   out[3] DP cells of every computed task (used or not), out[4] extensions the
+   redo pass computed inline, out[5] reads with > 64 seeds, out[6] reads left
+   to the redo pass, out[7] seeds of heavy reads with pair matrices */
+int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
+int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,14 @@
  *   5. dumps everything as raw little-endian arrays into <outdir>/ for
  *      gen_golden.py to pack into tests/golden/*.npz.
  *
- * usage: gen_golden <outdir> <seed> <n_pairs> <len_mode:150|100|250|mix> <opt_mode:0|1>
+ * usage: gen_golden <outdir> <seed> <n_pairs> <len_mode:150|100|250|mix> <opt_mode:0|1|2>
+ *                   [genome_len [record]]
+ *   genome_len  default 1,000,000 (contigs 500k/300k/200k); any other length
+ *               keeps the 50/30/20 % contig split and scales the repeat
+ *               families, tandem repeats and N runs per Mb (the bench's
+ *               chr21-sized C2 genome: oracle/gen_c2_fixture.py)
+ *   record      1 (default) records every ksw_extend2 / bwa_gen_cigar2 call
+ *               and runs mem_reg2aln on every region; 0 skips both
  */
 #include <math.h>
 #include <stdio.h>
@@ -132,14 +139,20 @@ uint32_t *__wrap_bwa_gen_cigar2(const int8_t mat[25], int o_del, int e_del, int 
 /* ---------------- reference genome ---------------- */
 static const char ACGT[] = "ACGT";
 
+/* per Mb: 10 repeat families (4 copies each), 30 tandem repeats, 12 N runs
+   (the counts of the 1 Mb golden genome; bwa-flow_amd/tools/synth.cpp
+   golden_genome() restates this generator for the bench) */
+static int per_mb(int k, int64_t L) { return (int)(k * (double)L / 1e6 + 0.5); }
+
 static char *make_genome(int n_ctg, const int *ctg_len, int64_t *total)
 {
   int64_t L = 0;
   for (int i = 0; i < n_ctg; ++i) L += ctg_len[i];
   char *g = (char *)malloc(L + 1);
   for (int64_t i = 0; i < L; ++i) g[i] = ACGT[rnd() & 3];
-  /* interspersed repeats: 40 copies of 10 families, 1% diverged */
-  for (int fam = 0; fam < 10; ++fam) {
+  const int n_fam = per_mb(10, L), n_tan = per_mb(30, L), n_nrun = per_mb(12, L);
+  /* interspersed repeats: 4 copies per family, 1% diverged */
+  for (int fam = 0; fam < n_fam; ++fam) {
     int len = 300 + irand(2700);
     int64_t src = (int64_t)(urand() * (L - len));
     for (int c = 0; c < 4; ++c) {
@@ -148,13 +161,13 @@ static char *make_genome(int n_ctg, const int *ctg_len, int64_t *total)
     }
   }
   /* tandem repeats */
-  for (int t = 0; t < 30; ++t) {
+  for (int t = 0; t < n_tan; ++t) {
     int per = 2 + irand(49), len = 200 + irand(800);
     int64_t dst = (int64_t)(urand() * (L - len));
     for (int k = per; k < len; ++k) g[dst + k] = urand() < 0.005 ? ACGT[rnd() & 3] : g[dst + k - per];
   }
   /* N runs (bwa turns them into random bases + holes, bntseq.c:261) */
-  for (int t = 0; t < 12; ++t) {
+  for (int t = 0; t < n_nrun; ++t) {
     int len = 10 + irand(300);
     int64_t dst = (int64_t)(urand() * (L - len));
     memset(g + dst, 'N', len);
@@ -222,6 +235,13 @@ int main(int argc, char *argv[])
   char fa[4096];
   int ctg_len[3] = {500000, 300000, 200000};
   int64_t G;
+  if (argc > 6) {
+    const int64_t gl = strtoll(argv[6], 0, 10);
+    ctg_len[0] = (int)(gl / 2);
+    ctg_len[1] = (int)(gl * 3 / 10);
+    ctg_len[2] = (int)(gl - ctg_len[0] - ctg_len[1]);
+  }
+  const int record = argc > 7 ? atoi(argv[7]) : 1;
 
   bwa_verbose = 1;
   uint64_t read_seed = rng_s;
@@ -312,7 +332,7 @@ int main(int argc, char *argv[])
       chain_v chn = mem_chain(opt, idx->bwt, idx->bns, n, q, 0);
       chn.n = mem_chain_flt(opt, (int)chn.n, chn.a);
       mem_flt_chained_seeds(opt, idx->bns, idx->pac, n, q, (int)chn.n, chn.a);
-      g_rec = 1;
+      g_rec = record;
       mem_alnreg_v av;
       kv_init(av);
       for (size_t c = 0; c < chn.n; ++c) {
@@ -326,7 +346,7 @@ int main(int argc, char *argv[])
       }
       free(chn.a);
       /* the SAM stage's CIGAR step on every region (bwa_wrapper.cpp:611) */
-      for (size_t k = 0; k < av.n; ++k) {
+      for (size_t k = 0; record && k < av.n; ++k) {
         const mem_alnreg_t *ar = &av.a[k];
         ctask_t t = {ar->rb, ar->re, (int64_t)(seq.n - n), n, ar->qb, ar->qe, ar->truesc, ar->w,
                      (int32_t)(seq_off.n - 2)};

@@ -1,38 +1,47 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools_dev/gpu_official.sh) into
-profiles/<tag>_traffic.json: HBM-side bytes per SW-stage launch sequence.
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py
+(tools_dev/gpu_round.sh) into profiles/<tag>_<workload>_traffic.json:
+HBM-side bytes per launch of every engine kernel, and per step (one batch's
+launch sequence).  bench.py reads the dominant kernel's entry as
+roofline.traffic.
 
 FETCH_SIZE/WRITE_SIZE are in KiB per dispatch (TCC_EA0_RDREQ/WRREQ based).
 Per MI355X_MICROARCH.md §HBM, gfx950 FETCH_SIZE reads 1/2 of the bytes of a
 wide (16 B/lane) streaming read; our loads are narrow (1-8 B/lane, gathers),
 a width the guide lists as uncalibrated, so both the raw and the x2 figure are
-recorded and the raw one is reported (a lower bound)."""
-import csv
+recorded and the raw one is reported (a lower bound).
+
+    python tools_dev/pmc_traffic.py <dir with pmc_fetch/ pmc_write/> <tag> <workload> <steps per run>"""
 import collections
+import csv
+import glob
 import json
 import sys
 
-d, tag = sys.argv[1], sys.argv[2]
-ours = ("bwagpu::", "rocprim::")
-out = {"tag": tag, "kernels": {}}
-for f, c in ((f"{d}/pmc_fetch/f_counter_collection.csv", "FETCH_SIZE"),
-             (f"{d}/pmc_write/w_counter_collection.csv", "WRITE_SIZE")):
+d, tag, wl, steps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+ours = ("bwagpu::",)
+out = {"tag": tag, "workload": wl, "per_launch": {}}
+tot = collections.defaultdict(float)
+for sub, c in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
     per = collections.defaultdict(list)
-    for r in csv.DictReader(open(f)):
-        if r["Counter_Name"] == c and any(k in r["Kernel_Name"] for k in ours):
-            per[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024)
+    for f in glob.glob(f"{d}/{sub}/*counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == c and any(k in r["Kernel_Name"] for k in ours):
+                per[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("bwagpu::", "")].append(
+                    float(r["Counter_Value"]) * 1024)
     for k, v in per.items():
-        out["kernels"].setdefault(k, {})[c] = {"dispatches": len(v), "bytes_mean": sum(v) / len(v)}
-seq_f = seq_w = 0.0
-launches = max(v["FETCH_SIZE"]["dispatches"] for k, v in out["kernels"].items() if "chain2aln_kernel" in k)
-for k, v in out["kernels"].items():
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        if c in v:
-            tot = v[c]["bytes_mean"] * v[c]["dispatches"] / launches
-            if c == "FETCH_SIZE":
-                seq_f += tot
-            else:
-                seq_w += tot
-out["per_launch_sequence"] = {"fetch_bytes": seq_f, "write_bytes": seq_w, "traffic_bytes": seq_f + seq_w,
-                              "traffic_bytes_fetch_x2": 2 * seq_f + seq_w, "launches": launches}
-json.dump(out, open(f"profiles/{tag}_traffic.json", "w"), indent=1)
-print(json.dumps(out["per_launch_sequence"]))
+        e = out["per_launch"].setdefault(k, {"dispatches": len(v)})
+        e["fetch_bytes" if c == "FETCH_SIZE" else "write_bytes"] = sum(v) / len(v)
+        tot[c] += sum(v)
+for k, e in out["per_launch"].items():
+    e["traffic_bytes"] = e.get("fetch_bytes", 0.0) + e.get("write_bytes", 0.0)
+    e["traffic_bytes_fetch_x2"] = 2 * e.get("fetch_bytes", 0.0) + e.get("write_bytes", 0.0)
+# the bench runs warmup + timed steps + the launch-sequence timing pass; the
+# per-step figure divides the chain2aln kernels' totals by the launches of the
+# first kernel of a sequence (spec_chain_kernel: one per batch)
+n_seq = out["per_launch"].get("spec_chain_kernel", {}).get("dispatches", steps)
+out["per_step"] = {"fetch_bytes": tot["FETCH_SIZE"] / n_seq, "write_bytes": tot["WRITE_SIZE"] / n_seq,
+                   "traffic_bytes": (tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) / n_seq, "sequences": n_seq,
+                   "note": "all engine kernels of the run / chain2aln launch sequences (includes the CIGAR and "
+                           "host-path legs' kernels if they ran)"}
+json.dump(out, open(f"profiles/{tag}_{wl}_traffic.json", "w"), indent=1)
+print(json.dumps({k: round(v["traffic_bytes"]) for k, v in out["per_launch"].items()}))

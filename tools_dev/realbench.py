@@ -10,6 +10,7 @@ evaluated cells / rows / extension calls per batch.
     python tools_dev/realbench.py [--batches 2] [--reps 10] [--length 150|mix]
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -67,6 +68,7 @@ def main():
     # warm-up + parity on every batch
     parity = True
     stats = []
+    spec = []
     for (b, t, c, out, nn, st, want, want_n) in dbs:
         st.zero_()
         eng.chain2aln_device(c, out.data_ptr(), nn.data_ptr(), st.data_ptr(), stream.cuda_stream)
@@ -76,6 +78,10 @@ def main():
         ok = np.array_equal(n, want_n) and G.region_mismatch(compact(b, regs, n), want) is None
         parity &= ok
         stats.append(st.cpu().numpy().tolist())
+        sc = np.zeros(8, np.int64)
+        if a.path == "spec":
+            eng.lib.bwagpu_debug_spec_counters(eng.ctx, C.c_void_p(stream.cuda_stream), sc.ctypes.data_as(C.c_void_p))
+        spec.append(sc.tolist())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     torch.cuda.set_stream(stream)
@@ -93,7 +99,10 @@ def main():
     print(json.dumps(dict(ms_per_batch=round(ms, 4), mreads_s=round(reads / ms / 1e3, 3), gcups=round(cells / ms / 1e6, 2),
                           reads=reads, chains=sum(d[0].n_chains for d in dbs) / len(dbs),
                           seeds=sum(d[0].n_seeds for d in dbs) / len(dbs), cells=cells, rows=rows, ext_calls=calls,
-                          parity_all_batches=bool(parity), length=a.length, path=a.path, gen_s=round(t_gen, 1))), flush=True)
+                          parity_all_batches=bool(parity), length=a.length, path=a.path, gen_s=round(t_gen, 1),
+                          spec_tasks_abc=[s[:3] for s in spec], spec_cells=[s[3] for s in spec],
+                          redo_inline=[s[4] for s in spec], heavy_reads=[s[5] for s in spec],
+                          redo_reads=[s[6] for s in spec])), flush=True)
     eng.close()
 
 
