@@ -95,12 +95,13 @@ struct Slot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
-  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent;
+  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh;
   SpecStreams spec;  // created on first use
   void release_scratch() {
     d_win.release(); d_srt.release(); d_prog.release(); d_desc.release(); d_lists.release(); d_counts.release();
     d_cread.release(); d_ext.release(); d_tasks.release(); d_ctr.release(); d_regpos.release(); d_skipf.release();
     d_heavy.release(); d_redo.release(); d_schain.release(); d_hinfo.release(); d_mat.release(); d_cov.release(); d_colent.release();
+    d_qh.release();
     if (spec.side) (void)hipStreamSynchronize(spec.side);
     if (spec.side) (void)hipStreamDestroy(spec.side);
     if (spec.fork) (void)hipEventDestroy(spec.fork);
@@ -436,6 +437,8 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_hinfo.ensure(sizeof(int4) * nr), "hipMalloc(hinfo)");
   HIPC(s.d_cov.ensure(sizeof(int32_t) * ns), "hipMalloc(cov)");
   HIPC(s.d_colent.ensure(sizeof(int32_t) * ns), "hipMalloc(colent)");
+  HIPC(s.d_qh.ensure(sizeof(int32_t) * kQHWords), "hipMalloc(qh)");
+  HIPC(hipMemsetAsync(s.d_qh.p, 0, sizeof(int32_t) * kQHWords, st), "memset qh");
   // pair matrices of heavy reads: sum over them of 2 * ns * ceil(ns / 64) words,
   // <= 2 * ns_total * (1 + ns_max / 64); reads that do not fit take the per-seed kernel
   const int64_t mat_words = std::max<int64_t>(1 << 20, 16 * (int64_t)ns);
@@ -461,6 +464,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.mat_words = (int64_t)(s.d_mat.cap / sizeof(uint64_t));
   a.cov = s.d_cov.as<int32_t>();
   a.colent = s.d_colent.as<int32_t>();
+  a.qh = s.d_qh.as<int32_t>();
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;
@@ -1251,6 +1255,20 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   out[5] = c[SPC_HEAVY_N];
   out[6] = c[SPC_REDO_N];
   out[7] = c[SPC_HCOLS];
+  return BWAGPU_OK;
+}
+
+int bwagpu_debug_spec_ext(bwagpu_ctx_t* ctx, void* stream, void* host_out, int32_t n) {
+  if (!ctx || !host_out || n < 0) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  int k = 0;
+  while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] != st) ++k;
+  if (k == BWAGPU_NUM_SLOTS || !ctx->dev_scratch[k].d_ext.p || ctx->dev_scratch[k].d_ext.cap < sizeof(SeedExt) * (size_t)n)
+    return fail(ctx, BWAGPU_E_INVAL, "no device-entry batch of that size on this stream");
+  HIPC(hipStreamSynchronize(st), "hipStreamSynchronize");
+  HIPC(hipMemcpy(host_out, ctx->dev_scratch[k].d_ext.p, sizeof(SeedExt) * (size_t)n, hipMemcpyDeviceToHost),
+       "hipMemcpy(ext)");
   return BWAGPU_OK;
 }
 

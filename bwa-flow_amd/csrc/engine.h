@@ -157,10 +157,16 @@ enum {
   SPC_MISS = 26,      // extensions the redo pass computed inline
   SPC_MATW64 = 28,    // int64 at words 28-29: uint64 words of heavy-read pair matrices handed out
   SPC_HCOLS = 30,     // columns (seeds) of heavy reads with a pair matrix
-  SPC_EXT_Q = 32,     // [list*8 + xcd] sharded task-queue heads, 9 lists
-  SPC_SEL_Q = 104,    // [pass*8 + xcd] sharded read-queue heads of the emulate / final pass
   SPC_WORDS = 128
 };
+// sharded queue heads of the extension task lists (SpecArgs::qh, zeroed per
+// batch): head of (list, xcd) at word (list * 8 + xcd) * kQHStride — one
+// 128-byte line each, so claims from different XCDs never meet on a line
+// (device-scope atomics on one line serialize at ~88 per microsecond,
+// MI355X_MICROARCH.md "dequeue"; measured here: 7.9 -> 6.6 ms per C2 batch
+// when the nine lists' heads moved off the two shared lines)
+constexpr int kQHStride = 32;
+constexpr int kQHWords = kSpecRounds * kSpecBins * 8 * kQHStride;
 // task list `list` (= round * kSpecBins + bin) starts at this entry of SpecArgs::tasks
 __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_seeds) {
   const int round = list / kSpecBins, bin = list % kSpecBins;
@@ -185,6 +191,7 @@ struct SpecArgs {
   uint64_t* mat;              // heavy-read pair matrices: C[ns][nw] then O[ns][nw] per read
   int64_t mat_words;          // capacity of mat
   int32_t* cov;               // per seed slot: seedcov of its region (heavy reads)
+  int32_t* qh;                // kQHWords: sharded queue heads of the extension task lists
   bwagpu_alnreg_t* out;
   int32_t* out_n;
   int64_t* stats;

@@ -2094,8 +2094,9 @@ __device__ __forceinline__ int wave_append(int32_t* cnt, bool p) {
   return p ? base + rank : -1;
 }
 
-// Dynamic queue with one head per XCD (MI355X_MICROARCH.md "dequeue": one head
-// word saturates at ~88 dequeues/us): shard x holds list positions x, x + 8,
+// Dynamic queue with one head per XCD, each on its own 128-byte line
+// (MI355X_MICROARCH.md "dequeue": one head word saturates at ~88 dequeues/us,
+// and so do heads sharing a line): shard x holds list positions x, x + 8,
 // ...; a wave claims K consecutive entries of a shard with one atomic, starting
 // on its own XCD's shard and moving on when it runs dry.  Every position is
 // taken exactly once by whichever waves exist; placement is never assumed.
@@ -2112,7 +2113,7 @@ struct ShardQ {
   __device__ bool claim(int K, int& m0, int& cap) {
     while (tried < 8) {
       cap = n > shard ? (n - shard + 7) >> 3 : 0;
-      int32_t* h = heads + shard;
+      int32_t* h = heads + shard * kQHStride;
       if (__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cap) {
         int v = 0;
         if ((threadIdx.x & 63) == 0) v = atomicAdd(h, K);
@@ -2362,7 +2363,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, 
   const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
   ShardQ qq;
-  qq.init(a.ctr + SPC_EXT_Q + 8 * list, n);
+  qq.init(a.qh + 8 * kQHStride * list, n);
   long long spec_cells = 0;
   int m0, cap;
   while (qq.claim(2, m0, cap)) {

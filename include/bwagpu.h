@@ -300,6 +300,10 @@ int bwagpu_prof_start(bwagpu_ctx_t *ctx, int max_launches);
    redo pass computed inline, out[5] reads with > 64 seeds, out[6] reads left
    to the redo pass, out[7] seeds of heavy reads with pair matrices */
 int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
+/* diagnostics: the per-seed extension records (48 B each: rb, re, qb, qe,
+   score, truesc, w, cells, rows, calls + 1; calls == 0: not computed) of the
+   last device-entry batch on `stream`, n = its seed count */
+int bwagpu_debug_spec_ext(bwagpu_ctx_t *ctx, void *stream, void *host_out, int32_t n);
 int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
 
 #ifdef __cplusplus

@@ -1,0 +1,379 @@
+/*
+ * sam_harness.c — TEST INFRASTRUCTURE ONLY: SAM-level parity of the GPU stage.
+ *
+ * Linked (oracle/Makefile -> _ref/sam_harness) against the REFERENCE's bwa
+ * objects compiled from /root/reference/bwa.  It builds a bwa index of a
+ * synthetic genome (sim.h), simulates read pairs, and aligns them batch by
+ * batch (batches of >= K bases, as `bwa mem -K` and bwa-flow's getKseqBatch,
+ * src/Pipeline.cpp:123,146) in one of three modes:
+ *
+ *   ref    the reference's own mem_process_seqs (bwa/bwamem.c:1220-1249):
+ *          worker1 -> mem_pestat -> worker2, exactly what `bwa mem` runs;
+ *   split  the same pipeline restated stage by stage the way bwa-flow splits
+ *          it (SeqsToChains -> ChainsToRegions -> RegionsToSam,
+ *          src/Pipeline.cpp:110-113, 503-544, 546-648): mem_chain ->
+ *          mem_chain_flt -> mem_flt_chained_seeds per read, then the
+ *          reference mem_chain2aln per chain, then mem_sort_dedup_patch +
+ *          is_alt (bwamem.c:1088-1100), mem_pestat, mem_sam_pe — must print
+ *          the same SAM as `ref` (checks the harness itself, no GPU);
+ *   gpu    `split` with the mem_chain2aln loop replaced by ONE
+ *          bwagpu_chain2aln call per batch (bwa-flow_amd/lib/libbwagpu.so,
+ *          dlopen'ed) — the drop-in this repository builds.
+ *
+ * Every mode prints the SAM records (header: bwa_print_sam_hdr) to <out.sam>
+ * and one JSON line of per-phase wall times to stderr.  The -m gpu test
+ * (tests/test_gpu_sam.py) diffs `ref` against `gpu` byte for byte.
+ *
+ * usage: sam_harness <mode> <workdir> <out.sam> <seed> <n_pairs> <len:150|100|250|mix>
+ *                    [batch_bases=10000000] [threads=8] [genome_len=1000000]
+ */
+#include <dlfcn.h>
+#include <stdio.h>
+#include <unistd.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bntseq.h"
+#include "bwa.h"
+#include "bwamem.h"
+#include "bwt.h"
+#include "kvec.h"
+#include "utils.h"
+#include "sim.h"
+#include "bwagpu.h"
+
+typedef struct {
+  int64_t rbeg;
+  int32_t qbeg, len;
+  int score;
+} seed_t; /* == mem_seed_t, bwamem.c:174-178 */
+typedef struct {
+  int n, m, first, rid;
+  uint32_t w : 29, kept : 2, is_alt : 1;
+  float frac_rep;
+  int64_t pos;
+  seed_t *seeds;
+} chain_t; /* == mem_chain_t, bwamem.c:180-186 */
+typedef struct { size_t n, m; chain_t *a; } chain_v;
+
+chain_v mem_chain(const mem_opt_t *opt, const bwt_t *bwt, const bntseq_t *bns, int len, const uint8_t *seq,
+                  void *buf);
+int mem_chain_flt(const mem_opt_t *opt, int n_chn, chain_t *a);
+void mem_flt_chained_seeds(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, int l_query,
+                           const uint8_t *query, int n_chn, chain_t *a);
+void mem_chain2aln(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, int l_query,
+                   const uint8_t *query, const chain_t *c, mem_alnreg_v *av);
+int mem_sort_dedup_patch(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, uint8_t *query, int n,
+                         mem_alnreg_t *a);
+int mem_sam_pe(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, const mem_pestat_t pes[4],
+               uint64_t id, bseq1_t s[2], mem_alnreg_v a[2]);
+void kt_for(int n_threads, void (*func)(void *, int, int), void *data, int n);
+int bwa_idx_build(const char *fa, const char *prefix, int algo_type, int block_size);
+extern unsigned char nst_nt4_table[256];
+
+/* ---------------- the GPU library (dlopen: CPU modes run without it) ---------------- */
+static struct {
+  void *h;
+  int (*create)(int, const bwagpu_opt_t *, const bwagpu_bns_t *, const uint8_t *, bwagpu_ctx_t **);
+  int (*destroy)(bwagpu_ctx_t *);
+  int (*chain2aln)(bwagpu_ctx_t *, const bwagpu_batch_t *, bwagpu_alnreg_t *, int32_t *);
+  const char *(*last_error)(const bwagpu_ctx_t *);
+} G;
+
+static void gpu_load(void)
+{
+  const char *p = getenv("BWAGPU_LIB");
+  G.h = dlopen(p ? p : "bwa-flow_amd/lib/libbwagpu.so", RTLD_NOW);
+  if (!G.h) { fprintf(stderr, "dlopen: %s\n", dlerror()); exit(2); }
+  G.create = (int (*)(int, const bwagpu_opt_t *, const bwagpu_bns_t *, const uint8_t *, bwagpu_ctx_t **))dlsym(G.h, "bwagpu_create");
+  G.destroy = (int (*)(bwagpu_ctx_t *))dlsym(G.h, "bwagpu_destroy");
+  G.chain2aln = (int (*)(bwagpu_ctx_t *, const bwagpu_batch_t *, bwagpu_alnreg_t *, int32_t *))dlsym(G.h, "bwagpu_chain2aln");
+  G.last_error = (const char *(*)(const bwagpu_ctx_t *))dlsym(G.h, "bwagpu_last_error");
+  if (!G.create || !G.destroy || !G.chain2aln || !G.last_error) { fprintf(stderr, "libbwagpu: missing symbol\n"); exit(2); }
+}
+
+/* ---------------- reads ---------------- */
+static bseq1_t *simulate(const char *g, int64_t G_len, const int *ctg_len, int n_pairs, const char *lm, int *n_out)
+{
+  bseq1_t *s = (bseq1_t *)calloc(2 * (size_t)n_pairs, sizeof(bseq1_t));
+  char frag[8192], buf[4096], tmp[4096], name[64];
+  for (int p = 0; p < n_pairs; ++p) {
+    const int L = !strcmp(lm, "mix") ? (int[]){100, 150, 250}[p % 3] : atoi(lm);
+    int fl = (int)(400 + 40 * nrand());
+    if (fl < L + 10) fl = L + 10;
+    if (fl > 4000) fl = 4000;
+    int64_t pos;
+    if (urand() < 0.02) { /* straddle a contig junction */
+      const int c = irand(2);
+      int64_t j = 0;
+      for (int k = 0; k <= c; ++k) j += ctg_len[k];
+      pos = j - irand(fl);
+    } else pos = (int64_t)(urand() * (G_len - fl));
+    if (pos < 0) pos = 0;
+    if (pos + fl > G_len) pos = G_len - fl;
+    memcpy(frag, g + pos, fl);
+    const int strand = rnd() & 1;
+    snprintf(name, sizeof name, "r%d", p);
+    for (int e = 0; e < 2; ++e) {
+      int n;
+      const double kind = urand();
+      if (kind < 0.005) { /* junk */
+        n = L;
+        for (int i = 0; i < n; ++i) buf[i] = ACGT[rnd() & 3];
+      } else {
+        const int fwd = (e == 0) ^ strand;
+        if (fwd) memcpy(tmp, frag, L);
+        else for (int i = 0; i < L; ++i) tmp[i] = comp(frag[fl - 1 - i]);
+        if (kind < 0.015) memcpy(tmp + L / 2, g + (int64_t)(urand() * (G_len - L)), L - L / 2); /* chimera */
+        n = mutate(tmp, L, buf, L + 16);
+        if (n > L) n = L;
+      }
+      bseq1_t *q = &s[2 * p + e];
+      q->name = strdup(name);
+      q->l_seq = n;
+      q->seq = (char *)malloc(n + 1);
+      q->qual = (char *)malloc(n + 1);
+      memcpy(q->seq, buf, n);
+      memset(q->qual, 'I', n);
+      q->seq[n] = q->qual[n] = 0;
+    }
+  }
+  *n_out = 2 * n_pairs;
+  return s;
+}
+
+/* ---------------- the split pipeline ---------------- */
+typedef struct {
+  const mem_opt_t *opt;
+  const bwaidx_t *idx;
+  bseq1_t *seqs;
+  chain_v *chn;
+  mem_alnreg_v *regs;
+  const mem_pestat_t *pes;
+  int64_t n_processed;
+} hw_t;
+
+static void w_seed(void *data, int i, int tid) /* SeqsToChains (bwa_wrapper.cpp:110-113, bwamem.c:1072-1077) */
+{
+  hw_t *w = (hw_t *)data;
+  bseq1_t *s = &w->seqs[i];
+  for (int k = 0; k < s->l_seq; ++k) s->seq[k] = s->seq[k] < 4 ? s->seq[k] : nst_nt4_table[(int)s->seq[k]];
+  chain_v c = mem_chain(w->opt, w->idx->bwt, w->idx->bns, s->l_seq, (uint8_t *)s->seq, 0);
+  c.n = mem_chain_flt(w->opt, (int)c.n, c.a);
+  mem_flt_chained_seeds(w->opt, w->idx->bns, w->idx->pac, s->l_seq, (uint8_t *)s->seq, (int)c.n, c.a);
+  w->chn[i] = c;
+}
+static void w_ext_cpu(void *data, int i, int tid) /* ChainsToRegions::compute (Pipeline.cpp:514-529) */
+{
+  hw_t *w = (hw_t *)data;
+  kv_init(w->regs[i]);
+  for (size_t c = 0; c < w->chn[i].n; ++c)
+    mem_chain2aln(w->opt, w->idx->bns, w->idx->pac, w->seqs[i].l_seq, (uint8_t *)w->seqs[i].seq, &w->chn[i].a[c],
+                  &w->regs[i]);
+}
+static void w_post(void *data, int i, int tid) /* mem_align1_core's tail (bwamem.c:1088-1100) */
+{
+  hw_t *w = (hw_t *)data;
+  mem_alnreg_v *r = &w->regs[i];
+  r->n = mem_sort_dedup_patch(w->opt, w->idx->bns, w->idx->pac, (uint8_t *)w->seqs[i].seq, (int)r->n, r->a);
+  for (size_t k = 0; k < r->n; ++k)
+    if (r->a[k].rid >= 0 && w->idx->bns->anns[r->a[k].rid].is_alt) r->a[k].is_alt = 1;
+}
+static void w_sam(void *data, int i, int tid) /* worker2 (bwamem.c:1214-1216) */
+{
+  hw_t *w = (hw_t *)data;
+  mem_sam_pe(w->opt, w->idx->bns, w->idx->pac, w->pes, (w->n_processed >> 1) + i, &w->seqs[i << 1], &w->regs[i << 1]);
+  free(w->regs[i << 1 | 0].a);
+  free(w->regs[i << 1 | 1].a);
+}
+
+/* one bwagpu_chain2aln call for the whole batch: flatten, run, unflatten into
+   malloc'd mem_alnreg_v (the ownership rule of ChainsToRegions, bwa_wrapper.cpp:824-830) */
+static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n)
+{
+  int64_t nc = 0, ns = 0, nb = 0;
+  for (int i = 0; i < n; ++i) {
+    nc += w->chn[i].n;
+    for (size_t c = 0; c < w->chn[i].n; ++c) ns += w->chn[i].a[c].n;
+    nb += w->seqs[i].l_seq;
+  }
+  int64_t *seq_off = (int64_t *)malloc(8 * (n + 1));
+  uint8_t *seq = (uint8_t *)malloc(nb + 1);
+  int32_t *rco = (int32_t *)malloc(4 * (n + 1)), *cso = (int32_t *)malloc(4 * (nc + 1)), *rid = (int32_t *)malloc(4 * (nc + 1));
+  float *fr = (float *)malloc(4 * (nc + 1));
+  bwagpu_seed_t *sd = (bwagpu_seed_t *)malloc(sizeof(bwagpu_seed_t) * (ns + 1));
+  int64_t q = 0;
+  int32_t c0 = 0, s0 = 0;
+  seq_off[0] = 0;
+  rco[0] = 0;
+  cso[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    memcpy(seq + q, w->seqs[i].seq, w->seqs[i].l_seq);
+    q += w->seqs[i].l_seq;
+    seq_off[i + 1] = q;
+    for (size_t c = 0; c < w->chn[i].n; ++c) {
+      const chain_t *ch = &w->chn[i].a[c];
+      for (int k = 0; k < ch->n; ++k) {
+        bwagpu_seed_t t = {ch->seeds[k].rbeg, ch->seeds[k].qbeg, ch->seeds[k].len, ch->seeds[k].score, 0};
+        sd[s0++] = t;
+      }
+      rid[c0] = ch->rid;
+      fr[c0] = ch->frac_rep;
+      cso[++c0] = s0;
+    }
+    rco[i + 1] = c0;
+  }
+  bwagpu_batch_t b = {n, (int32_t)nc, (int32_t)ns, 0, nb, seq_off, seq, rco, cso, rid, fr, sd};
+  bwagpu_alnreg_t *out = (bwagpu_alnreg_t *)malloc(sizeof(bwagpu_alnreg_t) * (ns + 1));
+  int32_t *on = (int32_t *)malloc(4 * (n + 1));
+  const int rc = G.chain2aln(ctx, &b, out, on);
+  if (rc) { fprintf(stderr, "bwagpu_chain2aln: rc=%d %s\n", rc, G.last_error(ctx)); exit(3); }
+  for (int i = 0; i < n; ++i) {
+    mem_alnreg_v *r = &w->regs[i];
+    r->n = r->m = on[i];
+    r->a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (on[i] ? on[i] : 1));
+    memcpy(r->a, out + cso[rco[i]], sizeof(mem_alnreg_t) * on[i]);
+  }
+  free(seq_off); free(seq); free(rco); free(cso); free(rid); free(fr); free(sd); free(out); free(on);
+}
+
+int main(int argc, char *argv[])
+{
+  if (argc < 7) {
+    fprintf(stderr, "usage: sam_harness <ref|split|gpu> <workdir> <out.sam> <seed> <n_pairs> <150|100|250|mix> "
+                    "[batch_bases] [threads] [genome_len]\n");
+    return 1;
+  }
+  const char *mode = argv[1], *dir = argv[2], *outp = argv[3];
+  const uint64_t seed = strtoull(argv[4], 0, 10);
+  const int n_pairs = atoi(argv[5]);
+  const char *lm = argv[6];
+  const int64_t K = argc > 7 ? strtoll(argv[7], 0, 10) : 10000000;
+  const int T = argc > 8 ? atoi(argv[8]) : 8;
+  const int64_t GL = argc > 9 ? strtoll(argv[9], 0, 10) : 1000000;
+  const int is_gpu = !strcmp(mode, "gpu"), is_ref = !strcmp(mode, "ref");
+  if (!is_gpu && !is_ref && strcmp(mode, "split")) { fprintf(stderr, "unknown mode %s\n", mode); return 1; }
+  if (is_gpu) gpu_load();
+
+  /* genome (the golden genome's generator and seed) + bwa index */
+  int ctg_len[3] = {500000, 300000, 200000};
+  if (GL != 1000000) {
+    ctg_len[0] = (int)(GL / 2);
+    ctg_len[1] = (int)(GL * 3 / 10);
+    ctg_len[2] = (int)(GL - ctg_len[0] - ctg_len[1]);
+  }
+  int64_t G_len;
+  bwa_verbose = 1;
+  rng_s = 1234;
+  char *g = make_genome(3, ctg_len, &G_len);
+  char fa[4096];
+  snprintf(fa, sizeof fa, "%s/ref.fa", dir);
+  FILE *f = fopen(fa, "w");
+  if (!f) { perror(fa); return 1; }
+  for (int c = 0, off = 0; c < 3; off += ctg_len[c], ++c) {
+    fprintf(f, ">chr%d\n", c + 1);
+    for (int64_t i = 0; i < ctg_len[c]; i += 60) {
+      const int64_t k = ctg_len[c] - i < 60 ? ctg_len[c] - i : 60;
+      fwrite(g + off + i, 1, k, f);
+      fputc('\n', f);
+    }
+  }
+  fclose(f);
+  bwa_idx_build(fa, fa, BWTALGO_AUTO, 10000000);
+  bwaidx_t *idx = bwa_idx_load(fa, BWA_IDX_ALL);
+  if (!idx) { fprintf(stderr, "index load failed\n"); return 1; }
+
+  rng_s = seed;
+  int n_all;
+  bseq1_t *all = simulate(g, G_len, ctg_len, n_pairs, lm, &n_all);
+  free(g);
+
+  mem_opt_t *opt = mem_opt_init();
+  opt->flag |= MEM_F_PE;
+  opt->n_threads = T;
+
+  bwagpu_ctx_t *ctx = 0;
+  if (is_gpu) {
+    bwagpu_opt_t go;
+    memset(&go, 0, sizeof go);
+    go.a = opt->a; go.b = opt->b; go.o_del = opt->o_del; go.e_del = opt->e_del; go.o_ins = opt->o_ins;
+    go.e_ins = opt->e_ins; go.pen_clip5 = opt->pen_clip5; go.pen_clip3 = opt->pen_clip3; go.w = opt->w;
+    go.zdrop = opt->zdrop;
+    memcpy(go.mat, opt->mat, 25);
+    const bntseq_t *bns = idx->bns;
+    int64_t *ao = (int64_t *)malloc(8 * bns->n_seqs);
+    int32_t *al = (int32_t *)malloc(4 * bns->n_seqs);
+    for (int i = 0; i < bns->n_seqs; ++i) { ao[i] = bns->anns[i].offset; al[i] = bns->anns[i].len; }
+    bwagpu_bns_t gb = {bns->l_pac, bns->n_seqs, 0, ao, al};
+    const int rc = G.create(0, &go, &gb, idx->pac, &ctx);
+    if (rc) { fprintf(stderr, "bwagpu_create: rc=%d\n", rc); return 3; }
+  }
+
+  FILE *out = fopen(outp, "w");
+  if (!out) { perror(outp); return 1; }
+  {
+    int fd_save = dup(fileno(stdout));
+    fflush(stdout);
+    dup2(fileno(out), fileno(stdout));
+    bwa_print_sam_hdr(idx->bns, 0);
+    fflush(stdout);
+    dup2(fd_save, fileno(stdout));
+    close(fd_save);
+  }
+  double t_seed = 0, t_ext = 0, t_sam = 0, t0, t_all = realtime();
+  int64_t n_processed = 0;
+  for (int r0 = 0; r0 < n_all;) {
+    /* a batch: reads until >= K bases, an even count (getKseqBatch / bseq_read) */
+    int r1 = r0;
+    int64_t bases = 0;
+    while (r1 < n_all && bases < K) bases += all[r1++].l_seq;
+    if ((r1 - r0) & 1) ++r1;
+    const int n = r1 - r0;
+    bseq1_t *seqs = all + r0;
+    if (is_ref) {
+      t0 = realtime();
+      mem_process_seqs(opt, idx->bwt, idx->bns, idx->pac, n_processed, n, seqs, 0);
+      t_ext += realtime() - t0;
+    } else {
+      hw_t w = {opt, idx, seqs, (chain_v *)calloc(n, sizeof(chain_v)), (mem_alnreg_v *)calloc(n, sizeof(mem_alnreg_v)),
+                0, n_processed};
+      t0 = realtime();
+      kt_for(T, w_seed, &w, n);
+      t_seed += realtime() - t0;
+      t0 = realtime();
+      if (is_gpu) ext_gpu(ctx, &w, n);
+      else kt_for(T, w_ext_cpu, &w, n);
+      t_ext += realtime() - t0;
+      t0 = realtime();
+      for (int i = 0; i < n; ++i) {
+        for (size_t c = 0; c < w.chn[i].n; ++c) free(w.chn[i].a[c].seeds);
+        free(w.chn[i].a);
+      }
+      kt_for(T, w_post, &w, n);
+      mem_pestat_t pes[4];
+      mem_pestat(opt, idx->bns->l_pac, n, w.regs, pes);
+      w.pes = pes;
+      kt_for(T, w_sam, &w, n >> 1);
+      t_sam += realtime() - t0;
+      free(w.chn);
+      free(w.regs);
+    }
+    for (int i = 0; i < n; ++i) {
+      fputs(seqs[i].sam, out);
+      free(seqs[i].sam);
+      free(seqs[i].name); free(seqs[i].seq); free(seqs[i].qual);
+    }
+    n_processed += n;
+    r0 = r1;
+  }
+  fclose(out);
+  t_all = realtime() - t_all;
+  fprintf(stderr, "{\"mode\": \"%s\", \"reads\": %ld, \"threads\": %d, \"seed_s\": %.4f, \"ext_s\": %.4f, "
+                  "\"sam_s\": %.4f, \"total_s\": %.4f}\n",
+          mode, (long)n_processed, T, t_seed, t_ext, t_sam, t_all);
+  if (ctx) G.destroy(ctx);
+  free(all);
+  free(opt);
+  bwa_idx_destroy(idx);
+  return 0;
+}

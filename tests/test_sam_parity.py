@@ -1,0 +1,64 @@
+"""SAM-level parity (north_star; the C3 mechanism at C1 / C5 scale).
+
+oracle/_ref/sam_harness (oracle/sam_harness.c, linked against the REFERENCE's
+bwa objects compiled from /root/reference) aligns simulated pairs on the
+golden genome batch by batch, either with the reference's own
+mem_process_seqs (`ref`, i.e. `bwa mem -K`), with the same pipeline split into
+bwa-flow's stages (`split`: seeding -> mem_chain2aln -> sort/dedup, pestat,
+mem_sam_pe), or with the mem_chain2aln loop replaced by one bwagpu_chain2aln
+call per batch (`gpu`).  The SAM outputs must be byte-identical.
+
+Test infrastructure only: nothing of the reference enters bwa-flow_amd/."""
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(REPO, "oracle", "_ref", "sam_harness")
+
+CASES = [  # name, seed, pairs, read lengths, ChainsRecord bases
+    ("c1", 7, 10000, "150", 10_000_000),        # C1: 10k 2x150 pairs, one batch
+    ("c1_batches", 11, 10000, "150", 1_000_000),  # the same size cut into 4 batches (per-batch pestat)
+    ("c5", 5, 9000, "mix", 10_000_000),          # C5: equal thirds of 2x100 / 2x150 / 2x250
+]
+
+
+def _run(mode, tmp, name, seed, pairs, lm, k):
+    d = os.path.join(tmp, f"{name}_{mode}")
+    os.makedirs(d, exist_ok=True)
+    out = os.path.join(d, "out.sam")
+    r = subprocess.run([HARNESS, mode, d, out, str(seed), str(pairs), lm, str(k), "8"], cwd=REPO,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return open(out, "rb").read()
+
+
+def _first_diff(a: bytes, b: bytes) -> str:
+    la, lb = a.split(b"\n"), b.split(b"\n")
+    for i, (x, y) in enumerate(zip(la, lb)):
+        if x != y:
+            return f"line {i}:\n  ref: {x[:300]!r}\n  got: {y[:300]!r}"
+    return f"line counts {len(la)} vs {len(lb)}"
+
+
+needs_harness = pytest.mark.skipif(not os.access(HARNESS, os.X_OK), reason="oracle/_ref/sam_harness not built")
+
+
+@needs_harness
+@pytest.mark.parametrize("name,seed,pairs,lm,k", CASES[:2])
+def test_split_pipeline_is_bwa_mem(tmp_path, name, seed, pairs, lm, k):
+    """the stage-split harness itself prints bwa mem's SAM (no GPU involved)"""
+    a = _run("ref", str(tmp_path), name, seed, pairs, lm, k)
+    b = _run("split", str(tmp_path), name, seed, pairs, lm, k)
+    assert a == b, _first_diff(a, b)
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,pairs,lm,k", CASES)
+def test_gpu_sam_identical_to_bwa_mem(tmp_path, name, seed, pairs, lm, k):
+    a = _run("ref", str(tmp_path), name, seed, pairs, lm, k)
+    b = _run("gpu", str(tmp_path), name, seed, pairs, lm, k)
+    assert a.count(b"\n") > 2 * pairs
+    assert a == b, _first_diff(a, b)
