@@ -4,6 +4,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <deque>
 #include <stdexcept>
@@ -43,42 +45,83 @@ GPUEnv::~GPUEnv() {
 }
 
 // --------------------------------------------------------------- FlatBatch
+// Host-side packing and unpacking run over read ranges on a few threads: at
+// C2 batch size (66.7k reads, 300k seeds) one thread needs ~10 ms for each
+// direction, twice the batch's GPU time (bench.py end_to_end phases).
+int host_threads() {
+  static const int n = [] {
+    const char* e = getenv("BWAGPU_HOST_THREADS");
+    int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(v, 8));
+  }();
+  return n;
+}
+
+template <typename F>
+static void parallel_ranges(int n, F f) {  // f(begin, end) over [0, n) in host_threads() pieces
+  const int t = std::min(host_threads(), std::max(1, n / 2048));
+  if (t <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 1; k < t; ++k) th.emplace_back(f, (int)((int64_t)n * k / t), (int)((int64_t)n * (k + 1) / t));
+  f(0, (int)((int64_t)n / t));
+  for (auto& x : th) x.join();
+}
+
 void FlatBatch::pack(const ChainsRecord& rec) {
   const int nr = rec.batch_num;
-  seq_off.assign(1, 0);
-  read_chain_off.assign(1, 0);
-  chain_seed_off.assign(1, 0);
-  seq.clear();
-  chain_rid.clear();
-  chain_frac_rep.clear();
-  seeds.clear();
+  // pass 1: per-read counts -> offsets
+  seq_off.assign((size_t)nr + 1, 0);
+  read_chain_off.assign((size_t)nr + 1, 0);
+  std::vector<int64_t> seed_base((size_t)nr + 1, 0);
   for (int i = 0; i < nr; ++i) {
-    const bseq1_t& s = rec.seqs[i];
-    seq.insert(seq.end(), (const uint8_t*)s.seq, (const uint8_t*)s.seq + s.l_seq);
-    seq_off.push_back((int64_t)seq.size());
     const mem_chain_v& cv = rec.chains[i];
-    for (size_t j = 0; j < cv.n; ++j) {
-      const mem_chain_t& c = cv.a[j];
-      chain_rid.push_back(c.rid);
-      chain_frac_rep.push_back(c.frac_rep);
-      for (int k = 0; k < c.n; ++k) {
-        bwagpu_seed_t t{};
-        t.rbeg = c.seeds[k].rbeg;
-        t.qbeg = c.seeds[k].qbeg;
-        t.len = c.seeds[k].len;
-        t.score = c.seeds[k].score;
-        seeds.push_back(t);
-      }
-      chain_seed_off.push_back((int32_t)seeds.size());
-    }
-    read_chain_off.push_back((int32_t)chain_rid.size());
+    int64_t ns = 0;
+    for (size_t j = 0; j < cv.n; ++j) ns += cv.a[j].n;
+    seq_off[i + 1] = seq_off[i] + rec.seqs[i].l_seq;
+    read_chain_off[i + 1] = read_chain_off[i] + (int32_t)cv.n;
+    seed_base[i + 1] = seed_base[i] + ns;
   }
-  regs.assign(seeds.size() ? seeds.size() : 1, bwagpu_alnreg_t{});
+  const size_t nc = (size_t)read_chain_off[nr], ns = (size_t)seed_base[nr];
+  seq.resize((size_t)seq_off[nr]);
+  chain_rid.resize(nc);
+  chain_frac_rep.resize(nc);
+  chain_seed_off.resize(nc + 1);
+  seeds.resize(ns);
+  chain_seed_off[0] = 0;
+  // pass 2: every read's bases, chains and seeds in place
+  parallel_ranges(nr, [&](int r0, int r1) {
+    for (int i = r0; i < r1; ++i) {
+      const bseq1_t& s = rec.seqs[i];
+      memcpy(seq.data() + seq_off[i], s.seq, (size_t)s.l_seq);
+      const mem_chain_v& cv = rec.chains[i];
+      int64_t so = seed_base[i];
+      for (size_t j = 0; j < cv.n; ++j) {
+        const mem_chain_t& c = cv.a[j];
+        const size_t ci = (size_t)read_chain_off[i] + j;
+        chain_rid[ci] = c.rid;
+        chain_frac_rep[ci] = c.frac_rep;
+        for (int k = 0; k < c.n; ++k) {
+          bwagpu_seed_t& t = seeds[(size_t)so + k];
+          t.rbeg = c.seeds[k].rbeg;
+          t.qbeg = c.seeds[k].qbeg;
+          t.len = c.seeds[k].len;
+          t.score = c.seeds[k].score;
+          t.pad_ = 0;
+        }
+        so += c.n;
+        chain_seed_off[ci + 1] = (int32_t)so;
+      }
+    }
+  });
+  regs.resize(ns ? ns : 1);
   n.assign(nr ? nr : 1, 0);
   c = bwagpu_batch_t{};
   c.n_reads = nr;
-  c.n_chains = (int32_t)chain_rid.size();
-  c.n_seeds = (int32_t)seeds.size();
+  c.n_chains = (int32_t)nc;
+  c.n_seeds = (int32_t)ns;
   c.seq_bytes = seq_off.back();
   c.seq_off = seq_off.data();
   c.seq = seq.data();
@@ -92,19 +135,29 @@ void FlatBatch::pack(const ChainsRecord& rec) {
 mem_alnreg_v* FlatBatch::unpack(int batch_num) const {
   mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
   if (!av) throw std::runtime_error("Memory allocation failed");
-  for (int i = 0; i < batch_num; ++i) {
-    const size_t k = (size_t)n[i];
-    av[i].n = av[i].m = k;
-    av[i].a = nullptr;
-    if (k) {
-      av[i].a = (mem_alnreg_t*)malloc(sizeof(mem_alnreg_t) * k);
-      if (!av[i].a) throw std::runtime_error("Memory allocation failed");
-      memcpy(av[i].a, &regs[chain_seed_off[read_chain_off[i]]], sizeof(mem_alnreg_t) * k);
+  std::atomic<bool> oom{false};
+  parallel_ranges(batch_num, [&](int r0, int r1) {
+    for (int i = r0; i < r1; ++i) {
+      const size_t k = (size_t)n[i];
+      av[i].n = av[i].m = k;
+      av[i].a = nullptr;
+      if (k) {
+        av[i].a = (mem_alnreg_t*)malloc(sizeof(mem_alnreg_t) * k);
+        if (!av[i].a) {
+          oom = true;
+          continue;
+        }
+        memcpy(av[i].a, &regs[chain_seed_off[read_chain_off[i]]], sizeof(mem_alnreg_t) * k);
+      }
     }
-  }
+  });
+  if (oom) throw std::runtime_error("Memory allocation failed");
   return av;
 }
 
+// serial: the chains were malloc'd by the upstream stage's threads, and frees
+// from several threads into one glibc arena contend for its lock (measured:
+// 2x slower on 8 threads than on one)
 void freeChainsRecordChains(mem_chain_v* chains, int batch_num) {
   if (!chains) return;
   for (int i = 0; i < batch_num; ++i) {
@@ -171,8 +224,12 @@ void ChainsToRegionsGPU::compute(int wid) {
       if (ready) {
         inflight.push_back(Job{rec, FlatBatch{}, (int)(submitted & 1)});
         Job& j = inflight.back();
+        auto t0 = std::chrono::steady_clock::now();
         j.flat.pack(j.rec);
+        auto t1 = std::chrono::steady_clock::now();
         const int rc = bwagpu_chain2aln_submit(ctx, j.slot, &j.flat.c);
+        ns_[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+        ns_[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
         if (rc == BWAGPU_E_UNSUPPORTED || rc == BWAGPU_E_INVAL) {
           // this record only (e.g. a read longer than BWAGPU_MAX_READ_LEN):
           // CPU path for it, the device stays in service
@@ -194,7 +251,10 @@ void ChainsToRegionsGPU::compute(int wid) {
       continue;
     }
     Job& j = inflight.front();
+    auto t0 = std::chrono::steady_clock::now();
     const int rc = bwagpu_chain2aln_wait(ctx, j.slot, j.flat.regs.data(), j.flat.n.data());
+    auto t1 = std::chrono::steady_clock::now();
+    ns_[2] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     if (rc != BWAGPU_OK) {
       fail_all("wait", rc);
       return;
@@ -206,6 +266,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     out.alnreg = j.flat.unpack(j.rec.batch_num);
     freeChainsRecordChains(j.rec.chains, j.rec.batch_num);
     out.chains = nullptr;
+    ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     n_gpu_.fetch_add(1);
     inflight.pop_front();
     pushOutput(out);

@@ -83,6 +83,14 @@ class ChainsToRegionsGPU
   // counters (tests / logging)
   int records_on_gpu() const { return n_gpu_.load(); }
   int records_on_cpu() const { return n_cpu_.load(); }
+  // host-side phase totals over all workers, seconds (the per-phase prep /
+  // enqueue / dequeue / post totals FPGAPipeline.cpp:557-578 prints):
+  // [0] pack (ChainsRecord -> flat arrays), [1] submit (pinned staging + H2D +
+  // launches), [2] wait (device time not hidden + D2H), [3] post (malloc'd
+  // mem_alnreg_v + freeing the chains)
+  void phase_seconds(double out[4]) const {
+    for (int i = 0; i < 4; ++i) out[i] = (double)ns_[i].load() * 1e-9;
+  }
 
  private:
   RegionsRecord on_cpu(const ChainsRecord& rec);
@@ -92,4 +100,5 @@ class ChainsToRegionsGPU
   ChainsToRegions* cpu_stage_;
   GPUEnv* env_;
   std::atomic<int> n_gpu_{0}, n_cpu_{0};
+  std::atomic<long long> ns_[4] = {};
 };

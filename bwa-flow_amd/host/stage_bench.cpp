@@ -1,0 +1,127 @@
+// stage_bench.cpp — the drop-in SW stage end to end (lib/libgpustage.so, used
+// by bench.py's `end_to_end` leg and tests/test_host_stage.py).
+//
+// Host ChainsRecords — malloc'd mem_chain_v / mem_chain_t / seeds per read, as
+// bwa-flow's SeqsToChains hands them over (src/Pipeline.cpp:110-121) — go
+// through a kflow pipeline whose stage 4 is ChainsToRegionsGPU alone
+// (--disable_sw_cpu, main.cpp:320-329): FlatBatch::pack -> bwagpu submit (pinned
+// staging, H2D, kernels) -> wait (D2H) -> malloc'd mem_alnreg_v per read, chains
+// freed; a consumer thread plays RegionsToSam and frees the regions.  The
+// records are built before the clock starts (that is SeqsToChains' work).
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <thread>
+#include <vector>
+
+#include "GPUPipeline.h"
+
+namespace {
+
+ChainsRecord make_record(const bwagpu_batch_t& b, bseq1_t* seqs, uint64_t start_idx) {
+  ChainsRecord rec{};
+  rec.start_idx = start_idx;
+  rec.batch_num = b.n_reads;
+  rec.seqs = seqs;
+  rec.chains = (mem_chain_v*)malloc(sizeof(mem_chain_v) * (size_t)(b.n_reads > 0 ? b.n_reads : 1));
+  for (int r = 0; r < b.n_reads; ++r) {
+    mem_chain_v& cv = rec.chains[r];
+    const int c0 = b.read_chain_off[r], c1 = b.read_chain_off[r + 1];
+    cv.n = cv.m = (size_t)(c1 - c0);
+    cv.a = (mem_chain_t*)calloc(cv.n ? cv.n : 1, sizeof(mem_chain_t));
+    for (int c = c0; c < c1; ++c) {
+      mem_chain_t& ch = cv.a[c - c0];
+      const int s0 = b.chain_seed_off[c], s1 = b.chain_seed_off[c + 1];
+      ch.n = ch.m = s1 - s0;
+      ch.rid = b.chain_rid[c];
+      ch.frac_rep = b.chain_frac_rep[c];
+      ch.seeds = (mem_seed_t*)malloc(sizeof(mem_seed_t) * (size_t)(ch.n ? ch.n : 1));
+      for (int k = 0; k < ch.n; ++k) {
+        ch.seeds[k].rbeg = b.seeds[s0 + k].rbeg;
+        ch.seeds[k].qbeg = b.seeds[s0 + k].qbeg;
+        ch.seeds[k].len = b.seeds[s0 + k].len;
+        ch.seeds[k].score = b.seeds[s0 + k].score;
+      }
+    }
+  }
+  return rec;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Runs reps x n_batches records through the stage on up to max_devices
+// devices.  times[0] = wall seconds from the first record in to the last
+// record out, times[1..4] = the stage's phase totals (pack, submit, wait,
+// post; summed over workers), times[5] = records on the GPU, times[6] =
+// records the CPU fallback took, times[7] = devices used.  The regions of the
+// LAST rep of batch k go to out_n[k][r] / out_regs[k] (compact, read order).
+// Returns 0, or the number of records whose chains were not freed.
+int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t* pac, int n_batches,
+                 const bwagpu_batch_t* batches, int reps, int max_devices, double* times, int32_t** out_n,
+                 bwagpu_alnreg_t** out_regs) {
+  if (!opt || !bns || !pac || n_batches <= 0 || !batches || reps <= 0 || !times) return -1;
+  GPUEnv env(*opt, *bns, pac, max_devices);
+  const int n_dev = env.num_devices();
+  if (n_dev == 0) return -2;
+  // the reads of every batch (shared by its reps: the stage never frees seqs)
+  std::vector<std::vector<bseq1_t>> seqs((size_t)n_batches);
+  for (int k = 0; k < n_batches; ++k) {
+    const bwagpu_batch_t& b = batches[k];
+    seqs[k].assign((size_t)(b.n_reads > 0 ? b.n_reads : 1), bseq1_t{});
+    for (int r = 0; r < b.n_reads; ++r) {
+      seqs[k][r].l_seq = (int)(b.seq_off[r + 1] - b.seq_off[r]);
+      seqs[k][r].id = r;
+      seqs[k][r].seq = (char*)b.seq + b.seq_off[r];
+    }
+  }
+  std::vector<ChainsRecord> recs;
+  for (int rep = 0; rep < reps; ++rep)
+    for (int k = 0; k < n_batches; ++k)
+      recs.push_back(make_record(batches[k], seqs[k].data(), (uint64_t)(rep * n_batches + k)));
+
+  ChainsToRegionsGPU stage(n_dev, nullptr, &env);
+  kestrelFlow::Pipeline pipe(1);
+  pipe.addStage(0, &stage);
+  pipe.start();
+  int bad = 0;
+  std::chrono::steady_clock::time_point t_end;
+  std::thread consumer([&] {  // RegionsToSam's side: take the records, free the regions
+    auto* q = pipe.output<RegionsRecord>();
+    for (size_t got = 0; got < recs.size(); ++got) {
+      RegionsRecord o;
+      q->pop(o);
+      if (o.chains != nullptr) ++bad;
+      const int k = (int)(o.start_idx % (uint64_t)n_batches);
+      const bool keep = o.start_idx / (uint64_t)n_batches == (uint64_t)(reps - 1) && out_n && out_regs;
+      size_t at = 0;
+      for (int r = 0; r < o.batch_num; ++r) {
+        const size_t m = o.alnreg[r].n;
+        if (keep) {
+          out_n[k][r] = (int32_t)m;
+          if (m) memcpy(out_regs[k] + at, o.alnreg[r].a, sizeof(bwagpu_alnreg_t) * m);
+          at += m;
+        }
+        free(o.alnreg[r].a);
+      }
+      free(o.alnreg);
+    }
+    t_end = std::chrono::steady_clock::now();
+  });
+  const auto t0 = std::chrono::steady_clock::now();
+  auto* in = pipe.input<ChainsRecord>();
+  for (auto& r : recs) in->push(r);
+  pipe.closeInput();
+  consumer.join();
+  pipe.wait();
+  times[0] = std::chrono::duration<double>(t_end - t0).count();
+  stage.phase_seconds(times + 1);
+  times[5] = stage.records_on_gpu();
+  times[6] = stage.records_on_cpu();
+  times[7] = n_dev;
+  return bad;
+}
+
+}  // extern "C"

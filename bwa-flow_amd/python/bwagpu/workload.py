@@ -29,10 +29,17 @@ class RefBatch:
         self.batch, self.reg_n, self.regs_sha256 = batch, reg_n, regs_sha256
 
     def check(self, regs: np.ndarray, n: np.ndarray) -> bool:
-        """bit-exact: per-read counts and every byte of every region (read order)"""
+        """bit-exact: per-read counts and every byte of every region; regs in
+        the ABI's slot layout (read r's regions from chain_seed_off[read_chain_off[r]])"""
         if not np.array_equal(np.asarray(n, np.int64), self.reg_n.astype(np.int64)):
             return False
-        c = np.ascontiguousarray(compact(self.batch, regs, n))
+        return self.check_compact(compact(self.batch, regs, n), n)
+
+    def check_compact(self, regs: np.ndarray, n: np.ndarray) -> bool:
+        """the same for regions already concatenated in read order"""
+        if not np.array_equal(np.asarray(n, np.int64), self.reg_n.astype(np.int64)):
+            return False
+        c = np.ascontiguousarray(regs[:int(np.asarray(n, np.int64).sum())])
         return hashlib.sha256(c.view(np.uint8).tobytes()).digest() == self.regs_sha256
 
 

@@ -10,5 +10,5 @@ timeout -k 10 400 python -u -m pytest tests/test_sam_parity.py tests/test_gpu_pa
 tail -3 $OUT/tests.log
 timeout -k 10 200 python -u tools_dev/realbench.py --batches 2 --reps 10 > $OUT/real150.json 2> $OUT/real150.err || { tail $OUT/real150.err; exit 2; }
 cat $OUT/real150.json
-timeout -k 10 300 python bench.py --no-cpu --no-cigar --no-host-path > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 3; }
+timeout -k 10 300 python bench.py --no-cpu --no-cigar > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 3; }
 cat $OUT/bench.json
