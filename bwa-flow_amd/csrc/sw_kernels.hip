@@ -162,6 +162,36 @@ constexpr int NEG = -(1 << 29);
 //    columns past qlen sit after every real column and need no masking;
 //  * the reference's special eh[] writes (eh[lo].h = first-column value,
 //    eh[hi] = {h1, 0}, ksw.c:420-429,449) are single-lane selects.
+#ifndef BWAGPU_DEFER_RK
+#define BWAGPU_DEFER_RK 1
+#endif
+// x <- inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
+// and r <- wave max in lane 63 (row_ror 8/4/2/1, row_bcast 15/31), the two
+// dependency chains interleaved: every DPP read is 2 wait states after the
+// write of its source (the other chain's op + s_nop 0).
+__device__ __forceinline__ void scan_reduce(int& x, int& r) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+      : "+v"(x), "+v"(r));
+}
+
 template <int CD, bool T5>
 __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
                                               int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
@@ -205,6 +235,25 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   int cells = vgpr(0);
   int rows = tlen;
   int tnext = tlen > 0 ? tb[0] : 0;
+#if BWAGPU_DEFER_RK
+  // The row maximum of row i-1 is reduced while row i's F scan runs: the two
+  // 6-step DPP chains interleave in one asm block (scan_reduce), and row i-1's
+  // exit test moves to row i, whose results are dropped if row i-1 exits.
+  int rkp = 0;  // row i-1's per-lane key (H << 10 | j)
+  // row k's bookkeeping (ksw.c:454-465) from its reduced key; true = exit
+  auto row_end = [&](int rkr, int vk) -> bool {
+    const int mrow = rkr >> 10, mj = rkr & 1023;
+    const bool up = mrow > best;
+    const int di = vk - bi, dj = mj - bj;
+    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
+    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
+    off = up ? max(off, abs(mj - vk)) : off;
+    best = up ? mrow : best;
+    bi = up ? vk : bi;
+    bj = up ? mj : bj;
+    return __builtin_amdgcn_ballot_w64(brk) != 0;
+  };
+#endif
   for (int i = 0; i < tlen; ++i) {
     const int t = __builtin_amdgcn_readfirstlane(tnext);
     tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
@@ -231,7 +280,12 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       M[c] = m;
       const int u = inb[c] ? max(m + Kc[c], jEc[c]) : jEc[c];
       int x = c == 0 ? u : max(u, carry);
+#if BWAGPU_DEFER_RK
+      if (c == 0) scan_reduce(x, rkp);
+      else x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
+#else
       x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
+#endif
       EX[c] = dpp<DPP_WAVE_SHR1>(carry, x);  // lane 0 takes the carry from the segments before
       if (c + 1 < CD) carry = __builtin_amdgcn_readlane(x, 63);
     }
@@ -291,6 +345,27 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       if (jl < 0) jl = nlo - 1;
       nhi = min(jl + 2, qlen);
     }
+#if BWAGPU_DEFER_RK
+    if (i > 0 && row_end(__builtin_amdgcn_readlane(rkp, 63), vi - 1)) {
+      rows = i;  // row i-1 was the last row: row i never ran
+      break;
+    }
+    rkp = rk;
+    cells += wd;
+    {  // ksw.c:450-453
+      const bool atend = max(lo, hi) == qlen;
+      ei = (atend && !(esc > h1)) ? vi : ei;
+      esc = atend ? max(esc, h1) : esc;
+    }
+    vi += 1;
+    lo = nlo;
+    hi = nhi;
+  }
+  if (rows == tlen && tlen > 0) {  // the last row's bookkeeping (its exit test is moot)
+    int rkr = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rkp))))));
+    (void)row_end(__builtin_amdgcn_readlane(rkr, 63), vi - 1);
+  }
+#else
     rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
     rk = __builtin_amdgcn_readlane(rk, 63);
     cells += wd;
@@ -321,6 +396,7 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       break;
     }
   }
+#endif
   tl.cells += __builtin_amdgcn_readfirstlane(cells);
   tl.rows += rows;
   tl.calls += 1;

@@ -188,8 +188,11 @@ void ChainsToRegionsGPU::compute(int wid) {
     retire();
     return;
   }
-  // two records in flight (the SWTask ping-pong, FPGAPipeline.cpp:374-386):
-  // record k uses slot k&1; waits are FIFO, so that slot is free again
+  // up to BWAGPU_NUM_SLOTS records in flight (the SWTask ping-pong,
+  // FPGAPipeline.cpp:374-386, widened: a batch's serial tail — the last
+  // extension round and the redo pass — overlaps the next batches' kernels):
+  // record k uses slot k % BWAGPU_NUM_SLOTS; waits are FIFO, so that slot is
+  // free again
   struct Job {
     ChainsRecord rec;
     FlatBatch flat;
@@ -222,7 +225,7 @@ void ChainsToRegionsGPU::compute(int wid) {
         if (!ready) more = false;
       }
       if (ready) {
-        inflight.push_back(Job{rec, FlatBatch{}, (int)(submitted & 1)});
+        inflight.push_back(Job{rec, FlatBatch{}, (int)(submitted % BWAGPU_NUM_SLOTS)});
         Job& j = inflight.back();
         auto t0 = std::chrono::steady_clock::now();
         j.flat.pack(j.rec);

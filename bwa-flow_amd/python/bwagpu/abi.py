@@ -23,7 +23,7 @@ ERR_NAMES = {
     E_RESULTS: "E_RESULTS", E_UNSUPPORTED: "E_UNSUPPORTED", E_NODEVICE: "E_NODEVICE",
 }
 MAX_READ_LEN = 1023
-NUM_SLOTS = 2
+NUM_SLOTS = 4
 
 SEED_DTYPE = np.dtype([("rbeg", "<i8"), ("qbeg", "<i4"), ("len", "<i4"), ("score", "<i4"),
                        ("pad", "<i4")])

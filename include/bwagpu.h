@@ -83,7 +83,7 @@ enum {
 /* longest read (bp) the device kernels accept; longer reads -> E_UNSUPPORTED */
 #define BWAGPU_MAX_READ_LEN 1023
 /* number of independent in-flight slots per context (ping-pong, FPGAPipeline.cpp:373-386) */
-#define BWAGPU_NUM_SLOTS 2
+#define BWAGPU_NUM_SLOTS 4
 
 /* The fields of mem_opt_t (bwa/bwamem.h:26-58) that mem_chain2aln/ksw_extend2 read. */
 typedef struct {
