@@ -2784,9 +2784,16 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
 // round-B task (pending: neither extended nor skipped, as in the per-seed
 // form); SEL_FINAL sends the read to the redo pass.
 template <int MODE>
-__global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+#ifndef BWAGPU_LIGHT_WPE
+#define BWAGPU_LIGHT_WPE 1  // no occupancy cap: 6 waves/SIMD (80 VGPRs, spills) measured 5% slower per batch
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWAGPU_LIGHT_WPE))) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
+                                                            int tb_bytes) {
   constexpr bool WRITE = MODE != SEL_EMULATE;
   __shared__ int32_t MG[kMglN];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lrows[];  // per wave: target rows of an inline extension
+  uint8_t* const tbl = lrows + (threadIdx.x >> 6) * 2 * tb_bytes;
+  uint8_t* const tbr = tbl + tb_bytes;
   for (int x = threadIdx.x; x < kMglN; x += kBlock) MG[x] = max_gap_len(o, x);
   __syncthreads();
   const int r = (int)(threadIdx.x & 63);
@@ -2808,6 +2815,9 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
       if (WRITE) a.out_n[rd] = 0;
       continue;
     }
+    // a miss of the final pass is computed inline and the read starts over
+    // with it (a region changes only later decisions; light reads are cheap)
+    for (;;) {
     // everything of the read, one round trip
     const int ci = min(r, max(d.nch - 1, 0)), si = min(r, d.ns - 1);
     const int cs_l = b.chain_seed_off[d.c0 + ci] - d.s0, ce_l = b.chain_seed_off[d.c0 + ci + 1] - d.s0;
@@ -2815,7 +2825,7 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
     const int rid_l = b.chain_rid[d.c0 + ci];
     const float fr_l = b.chain_frac_rep[d.c0 + ci];
     const bwagpu_seed_t sd = a.prog[d.s0 + si];
-    const SeedExt x = a.ext[d.s0 + si];  // written by earlier launches only (a miss goes to redo)
+    const SeedExt x = a.ext[d.s0 + si];  // earlier launches, or this wave's inline extension
     // this seed's chain (a chain with a flagged window is never processed)
     int cid = 0, rid = 0;
     float frac = 0.f;
@@ -2936,14 +2946,27 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
       const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
       if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
     } else {
-      if (miss >= 0) {
+      if (miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
+        const bwagpu_seed_t sm = uni_seed(a.prog[d.s0 + miss]);
+        const int cm_id = uni(__shfl(cid, miss, 64));
+        ChainWin cw = a.win[d.c0 + cm_id];
+        cw.lo = uni64(cw.lo);
+        cw.hi = uni64(cw.hi);
+        const SeedExt e = extend_seed<3>(o, ref, sm, d.lq, b.seq + d.qoff, cw, tbl, tbr);
+        store_ext(a.ext + d.s0 + miss, e);
+        if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+        mem_fence_group();
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
+      if (miss >= 0) {  // longer reads: round C + the redo pass (the C = 3 body holds reads <= 192 bp)
         const int list = 2 * kSpecBins + spec_bin(d.lq);
         if (r == miss) {
           const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
           a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
           a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
         }
-        continue;  // the redo pass writes this read
+        break;  // the redo pass writes this read
       }
       const bool mine = (ext >> r) & 1;
       if (mine) {  // the region of seed r, at its rank (bwamem.c:718-792 field by field; rest zero)
@@ -2967,6 +2990,8 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
       if (r == 0) a.out_n[rd] = (int)__popcll(ext);
     }
     trace_read(MODE, b.n_reads, rd, t_start, d.ns, (int)__popcll(ext), 1);
+    break;
+    }  // the read's attempts
   }
   if constexpr (WRITE) block_stats<64>(tl, a.stats);
 }
@@ -3042,10 +3067,70 @@ __global__ void __launch_bounds__(kBlock) spec_pairs_kernel(DevOpt o, DevBatch b
 
 constexpr int kScanLds = 64 * 1024;  // a read's C and O matrices staged in LDS when they fit
 
+// The final pass over a heavy read computes a missing extension INLINE (the
+// read's wave runs extend_seed, then sets the new region's containment bits in
+// column k of C for every later seed, and k's seedcov) and carries on: a
+// region only changes the decisions of the seeds after it, so the scan state
+// up to k stays valid.  (Deferring such a read to round C + the serial redo
+// pass cost 2.4-2.6 ms on one read of 1,167 seeds and 749 regions.)
+__device__ __forceinline__ void heavy_fill_missing(const DevOpt& o, const DevRef& ref, const DevBatch& b,
+                                                   const SpecArgs& a, const ReadDesc& d, int k, int ns,
+                                                   uint64_t* C, uint8_t* tbl, uint8_t* tbr) {
+  const int r = (int)(threadIdx.x & 63);
+  const bwagpu_seed_t sk = uni_seed(a.prog[d.s0 + k]);
+  const int ck = uni(a.seedchain[d.s0 + k]);
+  ChainWin cw = a.win[ck];
+  cw.lo = uni64(cw.lo);
+  cw.hi = uni64(cw.hi);
+  const SeedExt e = extend_seed<3>(o, ref, sk, d.lq, b.seq + d.qoff, cw, tbl, tbr);  // reads <= 192 bp
+  store_ext(a.ext + d.s0 + k, e);
+  if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+  // region k as the containment tests see it (bwamem.c:682-696)
+  RegRec p;
+  p.rb = e.rb;
+  p.re = e.re;
+  p.qb = e.qb;
+  p.qe = e.qe;
+  p.w = e.w;
+  p.seedlen0 = sk.len;
+  const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+  int cov = 0;
+  for (int base = 0; base < ns; base += 64) {
+    const int j = base + r, jj = min(j, ns - 1);
+    const bwagpu_seed_t sj = a.prog[d.s0 + jj];
+    // column k of C for the later seeds j > k (the pairs kernel's predicate)
+    bool in = j > k && j < ns && !(sj.rbeg < p.rb || sj.rbeg + sj.len > p.re || sj.qbeg < p.qb || sj.qbeg + sj.len > p.qe) &&
+              !(sj.len - sk.len >= rep_lim);
+    if (in) {
+      const int qd1 = sj.qbeg - p.qb;
+      const int64_t rd1 = sj.rbeg - p.rb;
+      const int g1 = max_gap_len(o, max(qd1 < rd1 ? qd1 : (int)rd1, 0));
+      const int bw1 = g1 < p.w ? g1 : p.w;
+      const int qd2 = p.qe - (sj.qbeg + sj.len);
+      const int64_t rd2 = p.re - (sj.rbeg + sj.len);
+      const int g2 = max_gap_len(o, max(qd2 < rd2 ? qd2 : (int)rd2, 0));
+      const int bw2 = g2 < p.w ? g2 : p.w;
+      in = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+    }
+    if (in) C[tri_off(j) + (k >> 6)] |= 1ull << (k & 63);  // word k>>6 of row j: this lane's alone
+    // seedcov of k (bwamem.c:784-788): its chain's seeds inside region k
+    const int cj = a.seedchain[d.s0 + jj];
+    cov += (j < ns && cj == ck && sj.qbeg >= p.qb && sj.qbeg + sj.len <= p.qe && sj.rbeg >= p.rb &&
+            sj.rbeg + sj.len <= p.re) ? sj.len : 0;
+  }
+  cov = (int)grp_sum64(cov, 64);
+  if (r == 0) a.cov[d.s0 + k] = cov;
+  // the wave re-reads C (LDS or its own global writes) and ext/cov next
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int MODE>
-__global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevBatch b, SpecArgs a) {
+__global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int tb_bytes) {
   constexpr bool WRITE = MODE != SEL_EMULATE;
   extern __shared__ __attribute__((aligned(16))) uint64_t M[];
+  uint8_t* const tbl = reinterpret_cast<uint8_t*>(M) + kScanLds;
+  uint8_t* const tbr = tbl + tb_bytes;
   const int r = (int)(threadIdx.x & 63);
   const uint64_t lt_mask = r ? (~0ull >> (64 - r)) : 0ull;
   const int nh = uni(__hip_atomic_load(&a.ctr[SPC_HEAVY_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -3067,7 +3152,7 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevBatch b, Spe
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const uint64_t* C = staged ? M : Cg;
+    uint64_t* C = staged ? M : a.mat + woff;
     const uint64_t* O = C + tw;
     // per-word sets: lane w holds word w
     uint64_t present_w = 0, computed_w = 0, skip_w = 0;
@@ -3107,8 +3192,12 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevBatch b, Spe
           pend_w |= r == kw ? kbit : 0;  // a round-B task; its region stays unknown
           continue;
         }
-        miss = k;
-        break;
+        if (d.lq > kSpecBinLen[0]) {  // longer reads: round C + the redo pass
+          miss = k;
+          break;
+        }
+        heavy_fill_missing(o, ref, b, a, d, k, ns, C, tbl, tbr);
+        computed_w |= r == kw ? kbit : 0;
       }
       ext_w |= r == kw ? kbit : 0;
     }
@@ -3178,13 +3267,15 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
     hs = ss.side;
   }
   if (MODE != SEL_REDO) {
-    const int nb = resident_blocks(spec_select_light<MODE>, 0);
-    hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), 0, st, o, ref, b, a);
+    const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
+    const int nb = resident_blocks(spec_select_light<MODE>, lds);
+    hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
   }
   if (MODE != SEL_REDO) {  // heavy reads with pair matrices: all pairs at once, then one scan per read
     const int nb = resident_blocks(spec_pairs_kernel, 0);
     hipLaunchKernelGGL(spec_pairs_kernel, dim3(nb), dim3(kBlock), 0, hs, o, b, a, MODE == SEL_FINAL ? 1 : 0);
-    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(1024), dim3(64), (size_t)kScanLds, hs, o, b, a);
+    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(1024), dim3(64), (size_t)kScanLds + 2 * (size_t)tb_bytes, hs, o,
+                       ref, b, a, tb_bytes);
   }
   // the rest (no matrix; the redo list): one wave per read, per seed
   hipLaunchKernelGGL((spec_select_kernel<MODE, true>), dim3(MODE == SEL_REDO ? 256 : 1024), dim3(64),
