@@ -143,6 +143,9 @@ struct bwagpu_ctx {
   static constexpr int kA2Streams = 4;
   hipStream_t a2_st[kA2Streams] = {};
   hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
+  // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
+  // returns fail_code once (tests of the stage's recovery path)
+  int fail_after = -1, fail_code = 0;
   // bwagpu_prof_*: event pairs around the dominant extension launches
   std::vector<hipEvent_t> prof_ev;
   int prof_used = 0;
@@ -673,6 +676,11 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (!s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot has no batch in flight");
+  if (ctx->fail_after == 0) {  // injected failure: the batch stays in flight, as after a real watchdog expiry
+    ctx->fail_after = -1;
+    return fail(ctx, ctx->fail_code, "injected failure (bwagpu_debug_fail_wait)");
+  }
+  if (ctx->fail_after > 0) --ctx->fail_after;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   // watchdog (SWTask::finish, SWTask.cpp:162-169): poll the completion event
   const auto t0 = std::chrono::steady_clock::now();
@@ -702,11 +710,13 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
   s.last.ext_calls = st[ST_CALLS];
   s.last.h2d_bytes = s.h2d;
   s.last.d2h_bytes = s.d2h;
-  if (st[ST_ERR] & ERR_RID)
-    return fail(ctx, BWAGPU_E_RESULTS, "a chain's first seed is not inside contig chain_rid (bwamem.c:669 assert)");
   if (st[ST_ERR] & ERR_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_READ_LEN");
+  // on a flagged chain the results are still copied: every other chain's
+  // regions are valid, the flagged ones were skipped (the caller's error path)
   if (out_n && s.n_reads) memcpy(out_n, s.h_n.p, sizeof(int32_t) * (size_t)s.n_reads);
   if (out_regs && s.n_seeds) memcpy(out_regs, s.h_out.p, sizeof(bwagpu_alnreg_t) * (size_t)s.n_seeds);
+  if (st[ST_ERR] & ERR_RID)
+    return fail(ctx, BWAGPU_E_RESULTS, "a chain's first seed is not inside contig chain_rid (bwamem.c:669 assert)");
   return BWAGPU_OK;
 }
 
@@ -1231,6 +1241,13 @@ int bwagpu_debug_set_trace(bwagpu_ctx_t* ctx, void* dev_ptr) {
   if (!ctx) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   HIPC(set_trace(dev_ptr), "set trace");
+  return BWAGPU_OK;
+}
+
+int bwagpu_debug_fail_wait(bwagpu_ctx_t* ctx, int after_n_waits, int code) {
+  if (!ctx || code <= 0) return BWAGPU_E_INVAL;
+  ctx->fail_after = after_n_waits;
+  ctx->fail_code = code;
   return BWAGPU_OK;
 }
 

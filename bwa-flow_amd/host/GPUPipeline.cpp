@@ -1,6 +1,10 @@
 // GPUPipeline.cpp — see GPUPipeline.h.
 #include "GPUPipeline.h"
 
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -18,30 +22,120 @@
 #endif
 
 // ------------------------------------------------------------------ GPUEnv
+namespace {
+
+// the few RCCL entry points GPUEnv needs, resolved at run time
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*bcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  bool load() {
+    const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+    for (const char* n : names)
+      if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) return false;
+    init_all = (decltype(init_all))dlsym(h, "ncclCommInitAll");
+    bcast = (decltype(bcast))dlsym(h, "ncclBroadcast");
+    group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
+    group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
+    destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+    return init_all && bcast && group_start && group_end && destroy;
+  }
+};
+
+}  // namespace
+
 GPUEnv::GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* pac, int max_devices,
-               int watchdog_ms) {
+               int watchdog_ms, int per_device) {
   int n = 0;
   const int rc = bwagpu_device_count(&n);
   if (rc != BWAGPU_OK) {
     status_ = "no GPU device (bwagpu_device_count rc=" + std::to_string(rc) + ")";
     return;
   }
-  for (int d = 0; d < n && d < max_devices; ++d) {
-    bwagpu_ctx_t* c = nullptr;
-    const int r = bwagpu_create(d, &opt, &bns, pac, &c);
-    if (r != BWAGPU_OK) {
-      status_ += "device " + std::to_string(d) + ": " + (c ? bwagpu_last_error(c) : "create failed") + "; ";
-      if (c) bwagpu_destroy(c);
+  n = std::min(n, max_devices);
+  const size_t pac_bytes = (size_t)(bns.l_pac / 4 + 1);
+  // the reference on every device: H2D to the first, RCCL broadcast to the rest
+  for (int d = 0; d < n; ++d) {
+    void* p = nullptr;
+    if (hipSetDevice(d) != hipSuccess || hipMalloc(&p, pac_bytes) != hipSuccess) {
+      status_ += "device " + std::to_string(d) + ": no memory for the reference; ";
       continue;
     }
-    bwagpu_set_watchdog_ms(c, watchdog_ms);  // fpgaHangError's 10 s watchdog (SWTask.cpp:116-122)
-    ctx_.push_back(c);
+    pac_dev_.push_back(p);
+    pac_devid_.push_back(d);
   }
-  if (status_.empty()) status_ = std::to_string(ctx_.size()) + " device(s)";
+  if (pac_dev_.empty()) return;
+  (void)hipSetDevice(pac_devid_[0]);
+  if (hipMemcpy(pac_dev_[0], pac, pac_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    status_ += "H2D of the reference failed; ";
+    for (size_t i = 0; i < pac_dev_.size(); ++i) {
+      (void)hipSetDevice(pac_devid_[i]);
+      (void)hipFree(pac_dev_[i]);
+    }
+    pac_dev_.clear();
+    pac_devid_.clear();
+    return;
+  }
+  if (pac_dev_.size() > 1) {
+    Rccl r;
+    bool ok = r.load();
+    const int nd = (int)pac_dev_.size();
+    std::vector<ncclComm_t> comms((size_t)nd, nullptr);
+    std::vector<hipStream_t> st((size_t)nd, nullptr);
+    if (ok) ok = r.init_all(comms.data(), nd, pac_devid_.data()) == ncclSuccess;
+    if (ok) {
+      for (int i = 0; i < nd; ++i) {
+        (void)hipSetDevice(pac_devid_[i]);
+        (void)hipStreamCreate(&st[i]);
+      }
+      ok = r.group_start() == ncclSuccess;
+      for (int i = 0; ok && i < nd; ++i)
+        ok = r.bcast(pac_dev_[0], pac_dev_[i], pac_bytes, ncclUint8, 0, comms[i], st[i]) == ncclSuccess;
+      ok = (r.group_end() == ncclSuccess) && ok;
+      for (int i = 0; i < nd; ++i) {
+        (void)hipSetDevice(pac_devid_[i]);
+        ok = (hipStreamSynchronize(st[i]) == hipSuccess) && ok;
+        (void)hipStreamDestroy(st[i]);
+      }
+    }
+    for (auto c : comms)
+      if (c) r.destroy(c);
+    rccl_ = ok;
+    if (!ok) {  // per-device host copies instead
+      for (size_t i = 1; i < pac_dev_.size(); ++i) {
+        (void)hipSetDevice(pac_devid_[i]);
+        (void)hipMemcpy(pac_dev_[i], pac, pac_bytes, hipMemcpyHostToDevice);
+      }
+      status_ += "RCCL unavailable: host copies; ";
+    }
+  }
+  for (size_t i = 0; i < pac_dev_.size(); ++i) {
+    for (int k = 0; k < per_device; ++k) {
+      bwagpu_ctx_t* c = nullptr;
+      const int r = bwagpu_create_resident(pac_devid_[i], &opt, &bns, pac_dev_[i], &c);
+      if (r != BWAGPU_OK) {
+        status_ += "device " + std::to_string(pac_devid_[i]) + ": " + (c ? bwagpu_last_error(c) : "create failed") + "; ";
+        if (c) bwagpu_destroy(c);
+        continue;
+      }
+      bwagpu_set_watchdog_ms(c, watchdog_ms);  // fpgaHangError's 10 s watchdog (SWTask.cpp:116-122)
+      ctx_.push_back(c);
+    }
+  }
+  status_ += std::to_string(ctx_.size()) + " context(s) on " + std::to_string(pac_dev_.size()) + " device(s)" +
+             (rccl_ ? ", reference broadcast over RCCL" : "");
 }
 
 GPUEnv::~GPUEnv() {
-  for (auto* c : ctx_) bwagpu_destroy(c);
+  for (auto* c : ctx_) bwagpu_destroy(c);  // synchronizes each context's streams
+  for (size_t i = 0; i < pac_dev_.size(); ++i) {
+    (void)hipSetDevice(pac_devid_[i]);
+    (void)hipFree(pac_dev_[i]);
+  }
 }
 
 // --------------------------------------------------------------- FlatBatch
@@ -258,7 +352,14 @@ void ChainsToRegionsGPU::compute(int wid) {
     const int rc = bwagpu_chain2aln_wait(ctx, j.slot, j.flat.regs.data(), j.flat.n.data());
     auto t1 = std::chrono::steady_clock::now();
     ns_[2] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-    if (rc != BWAGPU_OK) {
+    if (rc == BWAGPU_E_RESULTS) {
+      // a malformed record (a chain outside its contig: bwa would assert,
+      // bwamem.c:669): the error path — reported, emitted with that chain
+      // skipped; the CPU stage never sees it and the device stays in service
+      n_failed_.fetch_add(1);
+      fprintf(stderr, "[ChainsToRegionsGPU] record %llu: %s; its flagged chains are skipped\n",
+              (unsigned long long)j.rec.start_idx, bwagpu_last_error(ctx));
+    } else if (rc != BWAGPU_OK) {
       fail_all("wait", rc);
       return;
     }
@@ -271,6 +372,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     out.chains = nullptr;
     ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     n_gpu_.fetch_add(1);
+    if (wid < kMaxWorkers) per_worker_[wid].fetch_add(1);
     inflight.pop_front();
     pushOutput(out);
   }

@@ -31,22 +31,34 @@
 
 class ChainsToRegions;  // the CPU stage (src/Pipeline.h:162-171 / cpu_stage.h)
 
-// One bwagpu context per usable device.  Devices that fail to initialise are
-// skipped (their workers retire at once, like an FPGA env with fewer PEs).
+// The GPU environment (BWAOCLEnv, src/fpga/BWAOCLEnv.h:41-114): the packed
+// reference resident ONCE per device — copied host->device to the first
+// device and broadcast from there to the others over xGMI with RCCL
+// (ncclBroadcast on an ncclCommInitAll communicator; librccl is dlopen'ed, and
+// without it every device gets its own host copy) — and `per_device`
+// bwagpu contexts per device sharing that copy (bwagpu_create_resident), one
+// per stage worker.  Devices that fail to initialise are skipped (their
+// workers retire at once, like an FPGA env with fewer PEs).
 class GPUEnv {
  public:
   GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* pac, int max_devices = 8,
-         int watchdog_ms = 10000);
+         int watchdog_ms = 10000, int per_device = 1);
   ~GPUEnv();
   GPUEnv(const GPUEnv&) = delete;
   GPUEnv& operator=(const GPUEnv&) = delete;
 
+  // contexts (= stage workers), devices they are on
   int num_devices() const { return (int)ctx_.size(); }
+  int num_physical_devices() const { return (int)pac_dev_.size(); }
   bwagpu_ctx_t* ctx(int i) const { return i >= 0 && i < (int)ctx_.size() ? ctx_[i] : nullptr; }
   const std::string& status() const { return status_; }
+  bool used_rccl() const { return rccl_; }
 
  private:
   std::vector<bwagpu_ctx_t*> ctx_;
+  std::vector<void*> pac_dev_;  // the resident reference of each device (owned)
+  std::vector<int> pac_devid_;
+  bool rccl_ = false;
   std::string status_;
 };
 
@@ -83,6 +95,12 @@ class ChainsToRegionsGPU
   // counters (tests / logging)
   int records_on_gpu() const { return n_gpu_.load(); }
   int records_on_cpu() const { return n_cpu_.load(); }
+  // records the device flagged (BWAGPU_E_RESULTS: a chain outside its contig,
+  // where bwa asserts): emitted with that chain skipped, never handed to the CPU stage
+  int records_failed() const { return n_failed_.load(); }
+  // records each worker took (workers = env contexts)
+  int records_of_worker(int wid) const { return wid >= 0 && wid < kMaxWorkers ? per_worker_[wid].load() : 0; }
+  static constexpr int kMaxWorkers = 64;
   // host-side phase totals over all workers, seconds (the per-phase prep /
   // enqueue / dequeue / post totals FPGAPipeline.cpp:557-578 prints):
   // [0] pack (ChainsRecord -> flat arrays), [1] submit (pinned staging + H2D +
@@ -99,6 +117,7 @@ class ChainsToRegionsGPU
   std::atomic<int> n_active_;
   ChainsToRegions* cpu_stage_;
   GPUEnv* env_;
-  std::atomic<int> n_gpu_{0}, n_cpu_{0};
+  std::atomic<int> n_gpu_{0}, n_cpu_{0}, n_failed_{0};
+  std::atomic<int> per_worker_[kMaxWorkers] = {};
   std::atomic<long long> ns_[4] = {};
 };

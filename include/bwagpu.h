@@ -240,6 +240,9 @@ const char *bwagpu_last_error(const bwagpu_ctx_t *ctx);
 /* watchdog for _wait in milliseconds (default 10000, SWTask.cpp:116-122); 0 = none */
 int bwagpu_set_watchdog_ms(bwagpu_ctx_t *ctx, int ms);
 
+/* _wait returns BWAGPU_E_RESULTS when a chain's first seed lies outside its
+   contig (where bwa asserts, bwamem.c:669); the outputs are still written:
+   that chain is skipped, every other chain's regions are valid. */
 int bwagpu_chain2aln_submit(bwagpu_ctx_t *ctx, int slot, const bwagpu_batch_t *batch);
 int bwagpu_chain2aln_wait(bwagpu_ctx_t *ctx, int slot, bwagpu_alnreg_t *out_regs, int32_t *out_n);
 int bwagpu_chain2aln(bwagpu_ctx_t *ctx, const bwagpu_batch_t *batch, bwagpu_alnreg_t *out_regs,
@@ -285,6 +288,10 @@ int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
    Not part of the reference interface (the reference logs stage wall times
    with getUs(), src/util.h:34-40). */
 int bwagpu_debug_set_trace(bwagpu_ctx_t *ctx, void *dev_ptr);
+/* tests of the caller's recovery path: after `after_n_waits` more successful
+   bwagpu_chain2aln_wait calls, the next one returns `code` (e.g.
+   BWAGPU_E_HANG, as a watchdog expiry does) with its batch left in flight */
+int bwagpu_debug_fail_wait(bwagpu_ctx_t *ctx, int after_n_waits, int code);
 
 /* kernel timing (bench.py's roofline): after bwagpu_prof_start(ctx, n) the
    next n launches of the dominant extension kernel (spec_ext_kernel<3>, one

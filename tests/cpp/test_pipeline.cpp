@@ -11,6 +11,14 @@
 //                   retire at once and every record must come back to the CPU
 //   mode gpu        CPU stage + GPU back end (addAccxBckStage, priority 10)
 //   mode gpu_only   GPU stage as the sole stage (--disable_sw_cpu)
+//   mode gpu_2ctx   the sole stage with TWO contexts on each device (two
+//                   workers per GPU sharing one resident reference)
+//   mode gpu_hang   CPU stage + GPU back end whose 3rd wait fails as a
+//                   watchdog expiry does: in-flight records go to the CPU,
+//                   the worker retires, accx dispatch is switched off
+//   mode gpu_badrid the sole stage, record 1 holding a chain outside its
+//                   contig: the error path (reported, chain skipped), the
+//                   device stays in service
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -137,17 +145,29 @@ int main(int argc, char** argv) {
   ChainsToRegions cpu_stage(cpu_workers, read_fn);
   GPUEnv* env = nullptr;
   int n_dev = 0;
-  if (mode == "gpu" || mode == "gpu_only") {
-    env = new GPUEnv(opt, bns, pac.data());
+  const bool sole = mode == "gpu_only" || mode == "gpu_2ctx" || mode == "gpu_badrid";
+  if (mode == "gpu" || sole || mode == "gpu_hang") {
+    env = new GPUEnv(opt, bns, pac.data(), 8, 10000, mode == "gpu_2ctx" ? 2 : 1);
     n_dev = env->num_devices();
     if (n_dev == 0) {
       fprintf(stderr, "no device: %s\n", env->status().c_str());
       return 5;
     }
+    if (mode == "gpu_hang") bwagpu_debug_fail_wait(env->ctx(0), 2, BWAGPU_E_HANG);
+  }
+  int bad_rid_read = -1;
+  if (mode == "gpu_badrid" && recs.size() > 1) {  // the first chain of record 1 that has one
+    ChainsRecord& rr = recs[1];
+    for (int i = 0; i < rr.batch_num && bad_rid_read < 0; ++i)
+      if (rr.chains[i].n) {
+        mem_chain_t& ch = rr.chains[i].a[0];
+        ch.rid = (ch.rid + 1) % bns.n_seqs;
+        bad_rid_read = (int)rr.start_idx + i;
+      }
   }
   ChainsToRegionsGPU gpu_stage(mode == "accx_none" ? 2 : std::max(n_dev, 1), &cpu_stage, env);
   kestrelFlow::Pipeline pipe(1);
-  if (mode == "gpu_only") {
+  if (sole) {
     pipe.addStage(0, &gpu_stage);
   } else {
     pipe.addStage(0, &cpu_stage);
@@ -187,8 +207,11 @@ int main(int argc, char** argv) {
   fclose(fr);
   fclose(fn);
   printf("{\"records\": %zu, \"outputs\": %zu, \"on_gpu\": %d, \"gpu_fallback_cpu\": %d, \"devices\": %d, "
-         "\"bad_ownership\": %d}\n",
-         recs.size(), outs.size(), gpu_stage.records_on_gpu(), gpu_stage.records_on_cpu(), n_dev, bad);
+         "\"bad_ownership\": %d, \"failed\": %d, \"bad_rid_read\": %d, \"w0\": %d, \"w1\": %d, "
+         "\"accx_on_at_end\": %d, \"rccl\": %d, \"env\": \"%s\"}\n",
+         recs.size(), outs.size(), gpu_stage.records_on_gpu(), gpu_stage.records_on_cpu(), n_dev, bad,
+         gpu_stage.records_failed(), bad_rid_read, gpu_stage.records_of_worker(0), gpu_stage.records_of_worker(1),
+         cpu_stage.useAccx() ? 1 : 0, env && env->used_rccl() ? 1 : 0, env ? env->status().c_str() : "");
   delete env;
   return 0;
 }

@@ -80,3 +80,51 @@ def test_pipeline_gpu_stage(exe, tmp_path, name, mode):
         assert info["on_gpu"] == info["records"]
     assert info["bad_ownership"] == 0
     check(regs, n, want_regs, want_n)
+
+
+@pytest.mark.gpu
+def test_two_workers_per_device(exe, tmp_path):
+    """two contexts on each device share one resident reference (GPUEnv
+    per_device = 2): both workers pull records, outputs equal the golden regions"""
+    d = str(tmp_path)
+    b, want_regs, want_n = write_inputs(d, "c1_default")
+    info, regs, n = run(exe, d, "gpu_2ctx", 40, 2)
+    assert info["devices"] >= 2 and info["on_gpu"] == info["records"]
+    assert info["w0"] > 0 and info["w1"] > 0, info
+    check(regs, n, want_regs, want_n)
+
+
+@pytest.mark.gpu
+def test_midstream_device_failure_recovers_on_cpu(exe, tmp_path):
+    """the third wait fails as a watchdog expiry does (fpgaHangError path,
+    FPGAPipeline.cpp:526-551): the records in flight are recomputed by the CPU
+    stage, the worker retires and switches accx dispatch off, every output
+    still equals the golden regions"""
+    d = str(tmp_path)
+    b, want_regs, want_n = write_inputs(d, "c1_default")
+    info, regs, n = run(exe, d, "gpu_hang", 50, 2)
+    assert info["on_gpu"] >= 1 and info["gpu_fallback_cpu"] >= 1
+    assert info["accx_on_at_end"] == 0
+    assert info["outputs"] == info["records"] and info["bad_ownership"] == 0
+    check(regs, n, want_regs, want_n)
+
+
+@pytest.mark.gpu
+def test_malformed_record_takes_the_error_path(exe, tmp_path):
+    """a chain outside its contig (bwa asserts, bwamem.c:669) in record 1: the
+    stage reports it, emits the record with that chain skipped, never hands
+    it to the CPU stage, and keeps the device in service"""
+    d = str(tmp_path)
+    b, want_regs, want_n = write_inputs(d, "c1_default")
+    per = 50
+    info, regs, n = run(exe, d, "gpu_badrid", per, 2)
+    assert info["failed"] == 1 and info["gpu_fallback_cpu"] == 0
+    assert info["on_gpu"] == info["records"]
+    bad = info["bad_rid_read"]
+    assert bad >= per
+    off = np.concatenate([[0], np.cumsum(want_n)])
+    got_off = np.concatenate([[0], np.cumsum(n)])
+    keep = [r for r in range(b.n_reads) if r != bad]
+    assert np.array_equal(n[keep], want_n[keep])
+    for r in keep[::7] + keep[-3:]:
+        assert G.region_mismatch(regs[got_off[r]:got_off[r + 1]], want_regs[off[r]:off[r + 1]]) is None
