@@ -1,0 +1,286 @@
+// SamCache.cpp — the SAM-stage call cache of include/bwagpu_sam.h
+// (lib/libgpusam.so): ksw_align2 calls of mate rescue (bwa/bwamem_pair.c:154)
+// and mem_reg2aln CIGAR jobs (bwa/bwamem.c:1104-1174), keyed by content,
+// queued on a miss and computed in one device batch per kind on flush
+// (bwagpu_align2_batch / bwagpu_reg2aln_batch).
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "bwagpu.h"
+#include "bwagpu_sam.h"
+
+namespace {
+
+// 64-bit content hash (multiply-xorshift over 8-byte words); collisions are
+// resolved by comparing the stored bytes, so the hash only has to spread keys
+inline uint64_t mix(uint64_t h, uint64_t v) {
+  h ^= v + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
+  h *= 0xbf58476d1ce4e5b9ULL;
+  return h ^ (h >> 31);
+}
+uint64_t hash_bytes(uint64_t h, const uint8_t* p, int64_t n) {
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v;
+    memcpy(&v, p + i, 8);
+    h = mix(h, v);
+  }
+  uint64_t t = 0;
+  for (int k = 0; i < n; ++i, ++k) t |= (uint64_t)p[i] << (8 * k);
+  return mix(h, t ^ (uint64_t)n);
+}
+
+struct A2Entry {
+  int64_t qoff, toff;
+  int32_t qlen, tlen, xtra;
+  bool ready;
+  bwagpu_kswr_t r;
+};
+
+struct R2Entry {
+  int64_t rb, re, qoff;
+  int32_t l_seq, qb, qe, truesc, w;
+  bool ready;
+  bwagpu_aln_t a;
+  int64_t cig_off, md_off;  // into the result pools once ready
+};
+
+}  // namespace
+
+struct bwagpu_samcache {
+  bwagpu_ctx_t* ctx;
+  int32_t max_ops, max_md;
+  std::mutex mu;
+  std::vector<uint8_t> a2q, a2t, r2q;  // bases of the calls (nt4)
+  std::vector<A2Entry> a2;
+  std::vector<R2Entry> r2;
+  std::unordered_multimap<uint64_t, int32_t> a2map, r2map;
+  std::vector<int32_t> a2pend, r2pend;
+  std::vector<uint32_t> cig;  // CIGAR ops of the ready reg2aln jobs
+  std::vector<char> md;       // their MD strings, NUL-terminated
+  int64_t st[8] = {};
+};
+
+namespace {
+
+uint32_t* empty_block() { return (uint32_t*)calloc(1, sizeof(uint32_t)); }
+
+int flush_align2(bwagpu_samcache_t* c) {
+  const int32_t n = (int32_t)c->a2pend.size();
+  if (n == 0) return 0;
+  std::vector<bwagpu_align2_task_t> tasks((size_t)n);
+  for (int32_t k = 0; k < n; ++k) {
+    const A2Entry& e = c->a2[(size_t)c->a2pend[(size_t)k]];
+    tasks[(size_t)k] = bwagpu_align2_task_t{e.qoff, e.toff, e.qlen, e.tlen, e.xtra, 0};
+  }
+  std::vector<bwagpu_kswr_t> res((size_t)n);
+  const int rc = bwagpu_align2_batch(c->ctx, n, tasks.data(), c->a2q.data(), (int64_t)c->a2q.size(), c->a2t.data(),
+                                     (int64_t)c->a2t.size(), res.data());
+  if (rc) return rc;
+  for (int32_t k = 0; k < n; ++k) {
+    A2Entry& e = c->a2[(size_t)c->a2pend[(size_t)k]];
+    e.r = res[(size_t)k];
+    e.ready = true;
+  }
+  c->st[4] += n;
+  c->a2pend.clear();
+  return 0;
+}
+
+// one bwagpu_reg2aln_batch over `ids`; jobs whose CIGAR or MD overflowed the
+// launch's capacity are returned in `over`
+int run_reg2aln(bwagpu_samcache_t* c, const std::vector<int32_t>& ids, int32_t max_ops, int32_t max_md,
+                std::vector<int32_t>& over) {
+  const int32_t n = (int32_t)ids.size();
+  if (n == 0) return 0;
+  std::vector<bwagpu_reg2aln_task_t> tasks((size_t)n);
+  for (int32_t k = 0; k < n; ++k) {
+    const R2Entry& e = c->r2[(size_t)ids[(size_t)k]];
+    tasks[(size_t)k] = bwagpu_reg2aln_task_t{e.rb, e.re, e.qoff, e.l_seq, e.qb, e.qe, e.truesc, e.w, 0};
+  }
+  std::vector<bwagpu_aln_t> out((size_t)n);
+  std::vector<uint32_t> cg((size_t)n * (size_t)max_ops);
+  std::vector<char> mdb((size_t)n * (size_t)max_md);
+  const int rc = bwagpu_reg2aln_batch(c->ctx, n, tasks.data(), c->r2q.data(), (int64_t)c->r2q.size(), max_ops, max_md,
+                                      out.data(), cg.data(), mdb.data());
+  if (rc) return rc;
+  for (int32_t k = 0; k < n; ++k) {
+    R2Entry& e = c->r2[(size_t)ids[(size_t)k]];
+    const bwagpu_aln_t& a = out[(size_t)k];
+    if (a.status == BWAGPU_ALN_OVERFLOW) {
+      over.push_back(ids[(size_t)k]);
+      continue;
+    }
+    e.a = a;
+    e.cig_off = (int64_t)c->cig.size();
+    e.md_off = (int64_t)c->md.size();
+    if (a.status == BWAGPU_ALN_OK) {
+      const uint32_t* src = cg.data() + (size_t)k * max_ops;
+      c->cig.insert(c->cig.end(), src, src + a.n_cigar);
+      const char* m = mdb.data() + (size_t)k * max_md;
+      c->md.insert(c->md.end(), m, m + a.md_len);
+    }
+    c->md.push_back(0);
+    e.ready = true;
+  }
+  c->st[5] += n - (int64_t)over.size();
+  return 0;
+}
+
+int flush_reg2aln(bwagpu_samcache_t* c) {
+  if (c->r2pend.empty()) return 0;
+  std::vector<int32_t> over, over2;
+  int rc = run_reg2aln(c, c->r2pend, c->max_ops, c->max_md, over);
+  if (rc) return rc;
+  if (!over.empty()) {
+    // room for any alignment of the longest read among them: one op per base
+    // and indel run, MD at most a few bytes per base
+    int32_t lmax = 0;
+    for (int32_t id : over) lmax = std::max(lmax, c->r2[(size_t)id].l_seq);
+    rc = run_reg2aln(c, over, 2 * lmax + 8, 8 * lmax + 64, over2);
+    if (rc) return rc;
+    if (!over2.empty()) return BWAGPU_E_RESULTS;
+  }
+  c->r2pend.clear();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bwagpu_samcache_create(bwagpu_ctx_t* ctx, int32_t max_ops, int32_t max_md, bwagpu_samcache_t** out) {
+  if (!ctx || !out || max_ops < 1 || max_md < 1) return BWAGPU_E_INVAL;
+  auto* c = new bwagpu_samcache;
+  c->ctx = ctx;
+  c->max_ops = max_ops;
+  c->max_md = max_md;
+  *out = c;
+  return BWAGPU_OK;
+}
+
+int bwagpu_samcache_destroy(bwagpu_samcache_t* c) {
+  delete c;
+  return BWAGPU_OK;
+}
+
+int bwagpu_samcache_clear(bwagpu_samcache_t* c) {
+  if (!c) return BWAGPU_E_INVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->a2q.clear();
+  c->a2t.clear();
+  c->r2q.clear();
+  c->a2.clear();
+  c->r2.clear();
+  c->a2map.clear();
+  c->r2map.clear();
+  c->a2pend.clear();
+  c->r2pend.clear();
+  c->cig.clear();
+  c->md.clear();
+  return BWAGPU_OK;
+}
+
+int bwagpu_samcache_align2(bwagpu_samcache_t* c, int32_t qlen, const uint8_t* query, int32_t tlen,
+                           const uint8_t* target, int32_t xtra, bwagpu_kswr_t* out) {
+  if (!c || !out || qlen < 0 || tlen < 0 || (qlen && !query) || (tlen && !target)) return -BWAGPU_E_INVAL;
+  uint64_t h = mix(mix(0x243f6a8885a308d3ULL, (uint64_t)(uint32_t)qlen << 32 | (uint32_t)tlen), (uint64_t)(uint32_t)xtra);
+  h = hash_bytes(hash_bytes(h, query, qlen), target, tlen);
+  std::lock_guard<std::mutex> g(c->mu);
+  auto range = c->a2map.equal_range(h);
+  for (auto it = range.first; it != range.second; ++it) {
+    const A2Entry& e = c->a2[(size_t)it->second];
+    if (e.qlen != qlen || e.tlen != tlen || e.xtra != xtra || memcmp(c->a2q.data() + e.qoff, query, (size_t)qlen) ||
+        memcmp(c->a2t.data() + e.toff, target, (size_t)tlen))
+      continue;
+    if (e.ready) {
+      *out = e.r;
+      ++c->st[0];
+      return 0;
+    }
+    *out = bwagpu_kswr_t{0, -1, -1, -1, -1, -1, -1};
+    ++c->st[1];
+    return 1;  // queued by an earlier miss of this pass
+  }
+  A2Entry e{(int64_t)c->a2q.size(), (int64_t)c->a2t.size(), qlen, tlen, xtra, false, {}};
+  c->a2q.insert(c->a2q.end(), query, query + qlen);
+  c->a2t.insert(c->a2t.end(), target, target + tlen);
+  c->a2map.emplace(h, (int32_t)c->a2.size());
+  c->a2pend.push_back((int32_t)c->a2.size());
+  c->a2.push_back(e);
+  *out = bwagpu_kswr_t{0, -1, -1, -1, -1, -1, -1};
+  ++c->st[1];
+  return 1;
+}
+
+int bwagpu_samcache_reg2aln(bwagpu_samcache_t* c, int32_t l_seq, const uint8_t* read, int64_t rb, int64_t re,
+                            int32_t qb, int32_t qe, int32_t truesc, int32_t w, bwagpu_aln_t* out, uint32_t** cigar) {
+  if (!c || !out || !cigar || l_seq < 0 || (l_seq && !read) || rb < 0 || re < 0) return -BWAGPU_E_INVAL;
+  uint64_t h = mix(mix(mix(0x13198a2e03707344ULL, (uint64_t)rb), (uint64_t)re),
+                   (uint64_t)(uint32_t)qb << 32 | (uint32_t)qe);
+  h = mix(mix(h, (uint64_t)(uint32_t)truesc << 32 | (uint32_t)w), (uint64_t)(uint32_t)l_seq);
+  h = hash_bytes(h, read, l_seq);
+  std::lock_guard<std::mutex> g(c->mu);
+  auto range = c->r2map.equal_range(h);
+  for (auto it = range.first; it != range.second; ++it) {
+    const R2Entry& e = c->r2[(size_t)it->second];
+    if (e.rb != rb || e.re != re || e.qb != qb || e.qe != qe || e.truesc != truesc || e.w != w || e.l_seq != l_seq ||
+        memcmp(c->r2q.data() + e.qoff, read, (size_t)l_seq))
+      continue;
+    if (!e.ready) break;
+    *out = e.a;
+    const int32_t nc = e.a.status == BWAGPU_ALN_OK ? e.a.n_cigar : 0;
+    const int32_t ml = e.a.status == BWAGPU_ALN_OK ? e.a.md_len : 0;
+    uint32_t* blk = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)nc + (size_t)ml + 1);
+    if (!blk) return -BWAGPU_E_NOMEM;
+    memcpy(blk, c->cig.data() + e.cig_off, sizeof(uint32_t) * (size_t)nc);
+    memcpy((char*)(blk + nc), c->md.data() + e.md_off, (size_t)ml + 1);
+    *cigar = blk;
+    ++c->st[2];
+    return 0;
+  }
+  bool queued = false;
+  for (auto it = range.first; it != range.second && !queued; ++it) {
+    const R2Entry& e = c->r2[(size_t)it->second];
+    queued = e.rb == rb && e.re == re && e.qb == qb && e.qe == qe && e.truesc == truesc && e.w == w &&
+             e.l_seq == l_seq && !memcmp(c->r2q.data() + e.qoff, read, (size_t)l_seq);
+  }
+  if (!queued) {
+    R2Entry e{rb, re, (int64_t)c->r2q.size(), l_seq, qb, qe, truesc, w, false, {}, 0, 0};
+    c->r2q.insert(c->r2q.end(), read, read + l_seq);
+    c->r2map.emplace(h, (int32_t)c->r2.size());
+    c->r2pend.push_back((int32_t)c->r2.size());
+    c->r2.push_back(e);
+  }
+  memset(out, 0, sizeof *out);
+  out->status = -1;
+  *cigar = empty_block();
+  ++c->st[3];
+  return *cigar ? 1 : -BWAGPU_E_NOMEM;
+}
+
+int64_t bwagpu_samcache_flush(bwagpu_samcache_t* c) {
+  if (!c) return -BWAGPU_E_INVAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t n = (int64_t)c->a2pend.size() + (int64_t)c->r2pend.size();
+  if (n == 0) return 0;
+  int rc = flush_align2(c);
+  if (!rc) rc = flush_reg2aln(c);
+  ++c->st[6];
+  c->st[7] += (int64_t)std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  return rc ? -(int64_t)rc : n;
+}
+
+int bwagpu_samcache_stats(const bwagpu_samcache_t* c, int64_t out[8]) {
+  if (!c || !out) return BWAGPU_E_INVAL;
+  for (int i = 0; i < 8; ++i) out[i] = c->st[i];
+  return BWAGPU_OK;
+}
+
+}  // extern "C"

@@ -18,13 +18,23 @@
  *          the same SAM as `ref` (checks the harness itself, no GPU);
  *   gpu    `split` with the mem_chain2aln loop replaced by ONE
  *          bwagpu_chain2aln call per batch (bwa-flow_amd/lib/libbwagpu.so,
- *          dlopen'ed) — the drop-in this repository builds.
+ *          dlopen'ed) — the drop-in this repository builds;
+ *   gpusam `gpu` plus the SAM stage's Smith-Waterman on the device: mate
+ *          rescue (ksw_align2 in mem_matesw) and CIGAR generation
+ *          (mem_reg2aln) answered from the call cache of
+ *          bwa-flow_amd/lib/libgpusam.so through the interposers of
+ *          bwa-flow_amd/host/sam_hooks.c, the mem_sam_pe loop run as
+ *          collect -> flush -> replay passes (include/bwagpu_sam.h).
+ *
+ * The reference's objects are linked as a shared object (_ref/libbwaref.so,
+ * -fPIC), so sam_hooks.c's ksw_align2 / mem_reg2aln interpose on every call
+ * bwa makes; without a cache attached they forward to bwa's own.
  *
  * Every mode prints the SAM records (header: bwa_print_sam_hdr) to <out.sam>
  * and one JSON line of per-phase wall times to stderr.  The -m gpu test
  * (tests/test_gpu_sam.py) diffs `ref` against `gpu` byte for byte.
  *
- * usage: sam_harness <mode> <workdir> <out.sam> <seed> <n_pairs> <len:150|100|250|mix>
+ * usage: sam_harness <ref|split|gpu|gpusam> <workdir> <out.sam> <seed> <n_pairs> <len:150|100|250|mix>
  *                    [batch_bases=10000000] [threads=8] [genome_len=1000000]
  */
 #include <dlfcn.h>
@@ -41,6 +51,10 @@
 #include "utils.h"
 #include "sim.h"
 #include "bwagpu.h"
+#include "bwagpu_sam.h"
+
+int bwagpu_sam_hooks_attach(bwagpu_samcache_t *c); /* bwa-flow_amd/host/sam_hooks.c */
+int bwagpu_sam_hooks_errors(void);
 
 typedef struct {
   int64_t rbeg;
@@ -78,7 +92,29 @@ static struct {
   int (*destroy)(bwagpu_ctx_t *);
   int (*chain2aln)(bwagpu_ctx_t *, const bwagpu_batch_t *, bwagpu_alnreg_t *, int32_t *);
   const char *(*last_error)(const bwagpu_ctx_t *);
+  /* libgpusam.so (gpusam mode) */
+  int (*sc_create)(bwagpu_ctx_t *, int32_t, int32_t, bwagpu_samcache_t **);
+  int (*sc_destroy)(bwagpu_samcache_t *);
+  int (*sc_clear)(bwagpu_samcache_t *);
+  int64_t (*sc_flush)(bwagpu_samcache_t *);
+  int (*sc_stats)(const bwagpu_samcache_t *, int64_t *);
 } G;
+
+static void gpusam_load(void)
+{
+  const char *p = getenv("BWAGPU_SAM_LIB");
+  void *h = dlopen(p ? p : "bwa-flow_amd/lib/libgpusam.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) { fprintf(stderr, "dlopen: %s\n", dlerror()); exit(2); }
+  G.sc_create = (int (*)(bwagpu_ctx_t *, int32_t, int32_t, bwagpu_samcache_t **))dlsym(h, "bwagpu_samcache_create");
+  G.sc_destroy = (int (*)(bwagpu_samcache_t *))dlsym(h, "bwagpu_samcache_destroy");
+  G.sc_clear = (int (*)(bwagpu_samcache_t *))dlsym(h, "bwagpu_samcache_clear");
+  G.sc_flush = (int64_t (*)(bwagpu_samcache_t *))dlsym(h, "bwagpu_samcache_flush");
+  G.sc_stats = (int (*)(const bwagpu_samcache_t *, int64_t *))dlsym(h, "bwagpu_samcache_stats");
+  if (!G.sc_create || !G.sc_destroy || !G.sc_clear || !G.sc_flush || !G.sc_stats) {
+    fprintf(stderr, "libgpusam: missing symbol\n");
+    exit(2);
+  }
+}
 
 static void gpu_load(void)
 {
@@ -237,6 +273,42 @@ static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n)
   free(seq_off); free(seq); free(rco); free(cso); free(rid); free(fr); free(sd); free(out); free(on);
 }
 
+/* the SAM stage with its Smith-Waterman on the device (include/bwagpu_sam.h):
+   mem_sam_pe over a copy of the regions with the cache attached; a pass with
+   misses is discarded and its queued calls flushed to the device; the first
+   pass without a miss is the output */
+static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t *n_passes, double *t_flush)
+{
+  mem_alnreg_v *keep = w->regs, *cp = (mem_alnreg_v *)calloc(n, sizeof(mem_alnreg_v));
+  int64_t st[8];
+  bwagpu_sam_hooks_attach(cache);
+  for (;;) {
+    G.sc_stats(cache, st);
+    const int64_t miss0 = st[1] + st[3];
+    for (int i = 0; i < n; ++i) {
+      cp[i] = keep[i];
+      cp[i].a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (keep[i].m ? keep[i].m : 1));
+      memcpy(cp[i].a, keep[i].a, sizeof(mem_alnreg_t) * keep[i].n);
+    }
+    w->regs = cp;
+    kt_for(T, w_sam, w, n >> 1); /* frees cp[i].a */
+    ++*n_passes;
+    G.sc_stats(cache, st);
+    if (bwagpu_sam_hooks_errors()) { fprintf(stderr, "sam_hooks: the device flagged a CIGAR job\n"); exit(4); }
+    if (st[1] + st[3] == miss0) break;
+    for (int i = 0; i < n; ++i) { free(w->seqs[i].sam); w->seqs[i].sam = 0; }
+    const double t0 = realtime();
+    const int64_t rc = G.sc_flush(cache);
+    *t_flush += realtime() - t0;
+    if (rc <= 0) { fprintf(stderr, "bwagpu_samcache_flush: %ld\n", (long)rc); exit(3); }
+  }
+  bwagpu_sam_hooks_attach(0);
+  G.sc_clear(cache);
+  for (int i = 0; i < n; ++i) free(keep[i].a);
+  free(cp);
+  w->regs = keep;
+}
+
 int main(int argc, char *argv[])
 {
   if (argc < 7) {
@@ -251,9 +323,10 @@ int main(int argc, char *argv[])
   const int64_t K = argc > 7 ? strtoll(argv[7], 0, 10) : 10000000;
   const int T = argc > 8 ? atoi(argv[8]) : 8;
   const int64_t GL = argc > 9 ? strtoll(argv[9], 0, 10) : 1000000;
-  const int is_gpu = !strcmp(mode, "gpu"), is_ref = !strcmp(mode, "ref");
+  const int is_sam = !strcmp(mode, "gpusam"), is_gpu = is_sam || !strcmp(mode, "gpu"), is_ref = !strcmp(mode, "ref");
   if (!is_gpu && !is_ref && strcmp(mode, "split")) { fprintf(stderr, "unknown mode %s\n", mode); return 1; }
   if (is_gpu) gpu_load();
+  if (is_sam) gpusam_load();
 
   /* genome (the golden genome's generator and seed) + bwa index */
   int ctg_len[3] = {500000, 300000, 200000};
@@ -308,6 +381,9 @@ int main(int argc, char *argv[])
     const int rc = G.create(0, &go, &gb, idx->pac, &ctx);
     if (rc) { fprintf(stderr, "bwagpu_create: rc=%d\n", rc); return 3; }
   }
+  bwagpu_samcache_t *cache = 0;
+  if (is_sam && G.sc_create(ctx, 64, 512, &cache)) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
+  int64_t n_passes = 0;
 
   FILE *out = fopen(outp, "w");
   if (!out) { perror(outp); return 1; }
@@ -320,7 +396,7 @@ int main(int argc, char *argv[])
     dup2(fd_save, fileno(stdout));
     close(fd_save);
   }
-  double t_seed = 0, t_ext = 0, t_sam = 0, t0, t_all = realtime();
+  double t_seed = 0, t_ext = 0, t_sam = 0, t_flush = 0, t0, t_all = realtime();
   int64_t n_processed = 0;
   for (int r0 = 0; r0 < n_all;) {
     /* a batch: reads until >= K bases, an even count (getKseqBatch / bseq_read) */
@@ -353,7 +429,8 @@ int main(int argc, char *argv[])
       mem_pestat_t pes[4];
       mem_pestat(opt, idx->bns->l_pac, n, w.regs, pes);
       w.pes = pes;
-      kt_for(T, w_sam, &w, n >> 1);
+      if (is_sam) sam_passes(cache, &w, n, T, &n_passes, &t_flush);
+      else kt_for(T, w_sam, &w, n >> 1);
       t_sam += realtime() - t0;
       free(w.chn);
       free(w.regs);
@@ -368,9 +445,13 @@ int main(int argc, char *argv[])
   }
   fclose(out);
   t_all = realtime() - t_all;
+  int64_t st[8] = {0};
+  if (cache) G.sc_stats(cache, st);
   fprintf(stderr, "{\"mode\": \"%s\", \"reads\": %ld, \"threads\": %d, \"seed_s\": %.4f, \"ext_s\": %.4f, "
-                  "\"sam_s\": %.4f, \"total_s\": %.4f}\n",
-          mode, (long)n_processed, T, t_seed, t_ext, t_sam, t_all);
+                  "\"sam_s\": %.4f, \"flush_s\": %.4f, \"sam_passes\": %ld, \"align2_calls\": %ld, "
+                  "\"reg2aln_calls\": %ld, \"total_s\": %.4f}\n",
+          mode, (long)n_processed, T, t_seed, t_ext, t_sam, t_flush, (long)n_passes, (long)st[4], (long)st[5], t_all);
+  if (cache) G.sc_destroy(cache);
   if (ctx) G.destroy(ctx);
   free(all);
   free(opt);

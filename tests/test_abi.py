@@ -117,3 +117,51 @@ def test_reference_struct_offsets():
                 frac_rep=76, hash=80)
     for k, v in want.items():
         assert abi.ALNREG_DTYPE.fields[k][1] == v
+
+
+SAM_HDR = os.path.join(REPO, "include", "bwagpu_sam.h")
+SAM_LIB = os.path.join(REPO, "bwa-flow_amd", "lib", "libgpusam.so")
+
+
+def test_sam_cache_library_exports_its_header():
+    """lib/libgpusam.so (the SAM-stage call cache) exports exactly what
+    include/bwagpu_sam.h declares"""
+    txt = open(SAM_HDR).read()
+    declared = set(re.findall(r"^\s*(?:int|int64_t)\s*(bwagpu_samcache_\w+)\s*\(", txt, re.M))
+    assert len(declared) == 7
+    out = subprocess.run(["nm", "-D", "--defined-only", SAM_LIB], capture_output=True, text=True).stdout
+    assert set(re.findall(r"\bT (bwagpu_\w+)", out)) == declared
+
+
+def test_sam_cache_queues_misses_without_a_device():
+    """host logic only (no flush): a miss answers with the placeholders the
+    hooks rely on, a repeated call is not queued twice, bad arguments are
+    negative codes distinct from hit (0) / miss (1)"""
+    lib = C.CDLL(SAM_LIB)
+    lib.bwagpu_samcache_create.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.bwagpu_samcache_align2.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32, C.c_char_p, C.c_int32,
+                                           C.c_void_p]
+    lib.bwagpu_samcache_reg2aln.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_int64, C.c_int64, C.c_int32,
+                                            C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]
+    lib.bwagpu_samcache_stats.argtypes = [C.c_void_p, C.c_void_p]
+    lib.bwagpu_samcache_clear.argtypes = [C.c_void_p]
+    lib.bwagpu_samcache_destroy.argtypes = [C.c_void_p]
+    c = C.c_void_p()
+    # the cache keeps the context for flushes only; none happens here
+    assert lib.bwagpu_samcache_create(C.c_void_p(1), 64, 512, C.byref(c)) == 0
+    r = (C.c_int32 * 7)()
+    q, t = bytes([0, 1, 2, 3] * 10), bytes([3, 2, 1, 0] * 50)
+    for _ in range(2):
+        assert lib.bwagpu_samcache_align2(c, len(q), q, len(t), t, 0x40000 | 30, r) == 1
+        assert list(r) == [0, -1, -1, -1, -1, -1, -1]
+    assert lib.bwagpu_samcache_align2(c, -1, q, len(t), t, 0, r) < 0
+    aln = (C.c_int32 * 12)()
+    cig = C.c_void_p()
+    assert lib.bwagpu_samcache_reg2aln(c, len(q), q, 100, 140, 0, 40, 40, 5, aln, C.byref(cig)) == 1
+    assert aln[9] == -1 and cig.value  # status, empty malloc'd block
+    C.CDLL(None).free(cig)
+    assert lib.bwagpu_samcache_reg2aln(c, len(q), q, -1, 140, 0, 40, 40, 5, aln, C.byref(cig)) < 0
+    st = (C.c_int64 * 8)()
+    assert lib.bwagpu_samcache_stats(c, st) == 0
+    assert list(st) == [0, 2, 0, 1, 0, 0, 0, 0]
+    assert lib.bwagpu_samcache_clear(c) == 0 and lib.bwagpu_samcache_destroy(c) == 0

@@ -6,9 +6,14 @@ golden genome batch by batch, either with the reference's own
 mem_process_seqs (`ref`, i.e. `bwa mem -K`), with the same pipeline split into
 bwa-flow's stages (`split`: seeding -> mem_chain2aln -> sort/dedup, pestat,
 mem_sam_pe), or with the mem_chain2aln loop replaced by one bwagpu_chain2aln
-call per batch (`gpu`).  The SAM outputs must be byte-identical.
+call per batch (`gpu`), or with the SAM stage's Smith-Waterman on the device
+too (`gpusam`: mate rescue via bwagpu_align2_batch and CIGAR/MD/NM via
+bwagpu_reg2aln_batch, through the call cache of include/bwagpu_sam.h and the
+interposers of bwa-flow_amd/host/sam_hooks.c).  The SAM outputs must be
+byte-identical.
 
 Test infrastructure only: nothing of the reference enters bwa-flow_amd/."""
+import json
 import os
 import subprocess
 
@@ -31,6 +36,7 @@ def _run(mode, tmp, name, seed, pairs, lm, k):
     r = subprocess.run([HARNESS, mode, d, out, str(seed), str(pairs), lm, str(k), "8"], cwd=REPO,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
+    _run.info = json.loads(r.stderr.strip().splitlines()[-1])
     return open(out, "rb").read()
 
 
@@ -62,3 +68,18 @@ def test_gpu_sam_identical_to_bwa_mem(tmp_path, name, seed, pairs, lm, k):
     b = _run("gpu", str(tmp_path), name, seed, pairs, lm, k)
     assert a.count(b"\n") > 2 * pairs
     assert a == b, _first_diff(a, b)
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,pairs,lm,k", CASES)
+def test_gpu_sam_stage_identical_to_bwa_mem(tmp_path, name, seed, pairs, lm, k):
+    """chain2aln, mate rescue and CIGAR generation all on the device: the SAM
+    text is bwa mem's byte for byte; the device really did the rescue and
+    CIGAR work (calls computed, more than one pass per batch)"""
+    a = _run("ref", str(tmp_path), name, seed, pairs, lm, k)
+    b = _run("gpusam", str(tmp_path), name, seed, pairs, lm, k)
+    info = _run.info
+    assert a == b, _first_diff(a, b)
+    assert info["align2_calls"] > 0 and info["reg2aln_calls"] >= 2 * pairs * 0.9, info
+    assert info["sam_passes"] >= 2, info
