@@ -411,7 +411,174 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
 }
 
+// ------------------------------------------------ ksw_extend2, blocked columns
+// The same extension with the query's columns BLOCKED over the wave: lane r
+// holds columns j = r*CPL + c, c < CPL (CPL = ceil((qlen+1)/64)).  The row's
+// cross-lane work no longer grows with the segment count: ONE exclusive
+// max-plus scan (the in-lane part of F runs sequentially, as in gext_row), ONE
+// shift of H(i, j-1) into the next lane, ONE row-max reduction (interleaved
+// with the next row's scan), and the band trim by two ballots + readlanes.
+// Per row (ksw.c:415-470), as gext_row on 16-lane groups:
+//  * M_j = H(i-1,j-1) ? H(i-1,j-1) + S(t_i, q_j) : 0;
+//  * F: with A_c = (in band ? M_c : NEG) - oe_ins and T the lane's running
+//    max(T - e_ins, A_c), F entering the lane is max(0, max_{r'<r} T_r' -
+//    (r-1-r')*CPL*e_ins): one exclusive wave scan of T + r*CPL*e_ins;
+//  * the stored H of column j is H(i, j-1); column lo takes left0 (lane 0 via
+//    the shift's old value, other lanes from an out-of-band column = 0), and
+//    eh[hi] = {h1, 0} (ksw.c:449) is the same update applied to column hi with
+//    E cleared: [lo, hi] updates under one rule;
+//  * h1 = H(i, hi-1) is one readlane of the lane holding column hi.
+template <int CPL, bool T5>
+__device__ __forceinline__ ExtOut extend_wave_blk(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
+                                                  int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
+                                                  int h0, Tally& tl) {
+  const int r = (int)(threadIdx.x & 63);
+  const int e_del = o.e_del, e_ins = o.e_ins, o_del = o.o_del, oe_ins = o.oe_ins;
+  constexpr int KS = 2;  // bits of the in-lane column in the row-max key (CPL <= 4)
+  static_assert(CPL >= 1 && CPL <= 4, "blocked columns: CPL <= 4");
+  const int j0 = r * CPL;
+  int hh[CPL], ee[CPL];
+  uint32_t pf[CPL];
+  uint32_t pf4[T5 ? CPL : 1];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j = j0 + c;
+    const int qb = j < qlen ? qp[qa + qd * j] : 0;
+    pf[c] = qprof_word(o, qb);
+    if (T5) pf4[c] = (uint32_t)(uint8_t)qprof4_val(o, qb);
+    const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);  // ksw.c:392-395
+    hh[c] = j <= qlen ? v : 0;
+    ee[c] = 0;
+  }
+  {  // band clamp (ksw.c:399-407)
+    const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
+    const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, e_del);
+    w = __builtin_amdgcn_readfirstlane(min(w, min(mi, md)));
+  }
+  const int rE = e_ins * CPL * r;  // the lane's offset in the scan
+  int best = vgpr(h0), bi = vgpr(-1), bj = vgpr(-1), ei = vgpr(-1), esc = vgpr(-1), off = vgpr(0);
+  int lo = vgpr(0), hi = vgpr(qlen);
+  int iw = vgpr(-w), iw1 = vgpr(w + 1);
+  int gl = vgpr(h0 - o.o_del - e_del);
+  int vi = vgpr(0);
+  int cells = vgpr(0);
+  int rows = tlen;
+  int tnext = tlen > 0 ? tb[0] : 0;
+  int rkp = 0;  // row i-1's per-lane key, reduced during row i's scan
+  auto row_end = [&](int rkr, int vk) -> bool {  // ksw.c:454-465 of row vk
+    const int mrow = rkr >> 10, mj = rkr & 1023;
+    const bool up = mrow > best;
+    const int di = vk - bi, dj = mj - bj;
+    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
+    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
+    off = up ? max(off, abs(mj - vk)) : off;
+    best = up ? mrow : best;
+    bi = up ? vk : bi;
+    bj = up ? mj : bj;
+    return __builtin_amdgcn_ballot_w64(brk) != 0;
+  };
+  for (int i = 0; i < tlen; ++i) {
+    const int t = __builtin_amdgcn_readfirstlane(tnext);
+    tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
+    lo = max(lo, iw);
+    hi = min(min(hi, iw1), qlen);
+    iw += 1;
+    iw1 += 1;
+    const int wd = usat32(hi, lo);
+    const int left0 = lo == 0 ? max(gl, 0) : 0;
+    gl -= e_del;
+    const int sh = (t & 3) << 3;
+    const int x = j0 - lo;
+    int M[CPL], A[CPL];
+    int T = 0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const bool ib = (unsigned)(x + c) < (unsigned)wd;
+      int sc;
+      if (T5 && t == 4) sc = (int)(int8_t)(pf4[c] & 0xff);
+      else sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
+      const int m = hh[c] ? hh[c] + sc : 0;
+      M[c] = m;
+      A[c] = (ib ? m : NEG) - oe_ins;
+      T = max(T - e_ins, A[c]);
+    }
+    int sx = T + rE;
+    scan_reduce(sx, rkp);  // inclusive scan of this row + row i-1's max
+    const int EX = dpp<DPP_WAVE_SHR1>(NEG, sx);
+    int f = max(EX - rE + e_ins * CPL, 0);
+    int hm[CPL];
+    int lk = 0, h1c = 0;
+    const int hix = hi - j0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const unsigned d = (unsigned)(x + c);
+      const bool ib = d < (unsigned)wd, ib2 = d <= (unsigned)wd;
+      if (c > 0) f = max(max(f - e_ins, A[c - 1]), 0);
+      const int h = max(max(M[c], ee[c]), f);
+      hm[c] = ib ? h : 0;
+      const int en = usat32(max(ee[c], M[c] - o_del), e_del);
+      lk = max(lk, (hm[c] << KS) + c);
+      ee[c] = ib ? en : (ib2 ? 0 : ee[c]);
+      if (c > 0) {
+        hh[c] = ib2 ? hm[c - 1] : hh[c];
+        h1c = hix == c ? hm[c - 1] : h1c;
+      }
+    }
+    const int hs0 = dpp<DPP_WAVE_SHR1>(left0, hm[CPL - 1]);  // H(i, j0-1); lane 0: left0
+    hh[0] = (unsigned)x <= (unsigned)wd ? hs0 : hh[0];
+    h1c = hix == 0 ? hs0 : h1c;
+    const int hi_s = __builtin_amdgcn_readfirstlane(hi);
+    const int h1 = __builtin_amdgcn_readlane(h1c, hi_s / CPL);
+    // band trim for the next row (ksw.c:466-469)
+    uint32_t nzm = 0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) nzm |= (uint32_t)((hh[c] | ee[c]) != 0) << c;
+    const int lo_l = min(max(lo - j0, 0), 7), hi_l = min(max(hix, 0), 7);
+    const uint32_t mf = nzm & ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);  // [lo, hi)
+    const uint32_t ml = mf | (nzm & (hi_l == hix ? 1u << hi_l : 0u));     // [lo, hi]
+    const uint64_t bf = __builtin_amdgcn_ballot_w64(mf != 0), bl = __builtin_amdgcn_ballot_w64(ml != 0);
+    int nlo = hi_s, jl = -1;
+    if (bf) {
+      const int ln = (int)__builtin_ctzll(bf);
+      nlo = min(ln * CPL + (int)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)mf, ln)), hi_s);
+    }
+    if (bl) {
+      const int ln = 63 - (int)__builtin_clzll(bl);
+      jl = ln * CPL + 31 - (int)__builtin_clz((uint32_t)__builtin_amdgcn_readlane((int)ml, ln));
+    }
+    jl = max(jl, nlo - 1);
+    const int nhi = min(jl + 2, qlen);
+    if (i > 0 && row_end(__builtin_amdgcn_readlane(rkp, 63), vi - 1)) {
+      rows = i;  // row i-1 was the last row: row i never ran
+      break;
+    }
+    rkp = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
+    cells += wd;
+    {  // ksw.c:450-453
+      const bool atend = max(lo, hi) == qlen;
+      ei = (atend && !(esc > h1)) ? vi : ei;
+      esc = atend ? max(esc, h1) : esc;
+    }
+    vi += 1;
+    lo = nlo;
+    hi = nhi;
+  }
+  if (rows == tlen && tlen > 0) {  // the last row's bookkeeping (its exit test is moot)
+    int rkr = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rkp))))));
+    (void)row_end(__builtin_amdgcn_readlane(rkr, 63), vi - 1);
+  }
+  tl.cells += __builtin_amdgcn_readfirstlane(cells);
+  tl.rows += rows;
+  tl.calls += 1;
+  auto u = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+  return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
+}
+
 // CD is uniform per call (qlen is): one compiled body per segment count
+// (CD 2..4 on blocked columns with -DBWAGPU_BLK=1: bit-exact, measured slower)
+#ifndef BWAGPU_BLK
+#define BWAGPU_BLK 0
+#endif
 template <int C, bool T5>
 __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp,
                                                     int qa, int qd, int tlen, const uint8_t* tb, int w,
@@ -425,8 +592,13 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
   zdrop = __builtin_amdgcn_readfirstlane(zdrop);
   h0 = __builtin_amdgcn_readfirstlane(h0);
   const int cd = (qlen + 64) >> 6;  // ceil((qlen+1)/64)
-#define EXT_SEG(n) \
-  if (n <= C && cd == n) return extend_wave<(n <= C ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
+#define EXT_SEG(n)                                                                                          \
+  if (n <= C && cd == n) {                                                                                  \
+    if (BWAGPU_BLK && n >= 2 && n <= 4)                                                                     \
+      return extend_wave_blk<(n <= C && n <= 4 ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, \
+                                                           h0, tl);                                         \
+    return extend_wave<(n <= C ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);    \
+  }
   EXT_SEG(1) EXT_SEG(2) EXT_SEG(3) EXT_SEG(4) EXT_SEG(5) EXT_SEG(6) EXT_SEG(7) EXT_SEG(8)
   EXT_SEG(9) EXT_SEG(10) EXT_SEG(11) EXT_SEG(12) EXT_SEG(13) EXT_SEG(14) EXT_SEG(15) EXT_SEG(16)
 #undef EXT_SEG
