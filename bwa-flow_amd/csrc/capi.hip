@@ -19,6 +19,7 @@
 
 #include "align2.h"
 #include "reg2aln.h"
+#include "seed.h"
 #include "engine.h"
 
 using namespace bwagpu;
@@ -143,6 +144,12 @@ struct bwagpu_ctx {
   static constexpr int kA2Streams = 4;
   hipStream_t a2_st[kA2Streams] = {};
   hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
+  // seeding (bwagpu_set_bwt / bwagpu_collect_intv): the resident FM-index and
+  // the batch buffers
+  DevBuf bwt_words;
+  DevBwt bwt{};
+  bool has_bwt = false;
+  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch;
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
@@ -1326,3 +1333,70 @@ int bwagpu_last_stats(const bwagpu_ctx_t* ctx, int slot, bwagpu_stats_t* out) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ seeding
+extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
+  if (!ctx || !bwt || !bwt->bwt || bwt->bwt_size == 0) return BWAGPU_E_INVAL;
+  // the occurrence array covers every position: 16 words per 128 positions
+  if (bwt->bwt_size < ((bwt->seq_len + 127) >> 7) * 16 || bwt->L2[4] != bwt->seq_len || bwt->primary > bwt->seq_len)
+    return fail(ctx, BWAGPU_E_INVAL, "bwt header inconsistent with its occurrence array");
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  HIPC(ctx->bwt_words.ensure(sizeof(uint32_t) * bwt->bwt_size + 64), "hipMalloc");
+  HIPC(hipMemcpy(ctx->bwt_words.p, bwt->bwt, sizeof(uint32_t) * bwt->bwt_size, hipMemcpyHostToDevice), "H2D");
+  ctx->bwt.primary = bwt->primary;
+  for (int i = 0; i < 5; ++i) ctx->bwt.L2[i] = bwt->L2[i];
+  ctx->bwt.seq_len = bwt->seq_len;
+  ctx->bwt.bwt = ctx->bwt_words.as<uint32_t>();
+  ctx->has_bwt = true;
+  return BWAGPU_OK;
+}
+
+extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads,
+                                   const int64_t* seq_off, const uint8_t* seq, int32_t max_per_read,
+                                   bwagpu_intv_t* out, int32_t* out_n) {
+  if (!ctx || !opt || n_reads < 0 || max_per_read < 1 || (n_reads && (!seq_off || !out || !out_n)))
+    return BWAGPU_E_INVAL;
+  if (!ctx->has_bwt) return fail(ctx, BWAGPU_E_INVAL, "no FM-index: call bwagpu_set_bwt first");
+  if (opt->min_seed_len < 1 || opt->split_width < 0) return fail(ctx, BWAGPU_E_INVAL, "bad seeding options");
+  if (n_reads == 0) return BWAGPU_OK;
+  const int64_t bases = seq_off[n_reads] - seq_off[0];
+  if (seq_off[0] != 0 || bases < 0 || (bases && !seq)) return fail(ctx, BWAGPU_E_INVAL, "seq_off must start at 0");
+  for (int32_t r = 0; r < n_reads; ++r) {
+    const int64_t l = seq_off[r + 1] - seq_off[r];
+    if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
+    if (l > BWAGPU_MAX_SEED_READ) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_SEED_READ");
+  }
+  for (int64_t i = 0; i < bases; ++i)
+    if (seq[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->slot[0].stream;
+  HIPC(ctx->sd_off.ensure(sizeof(int64_t) * ((size_t)n_reads + 1)), "hipMalloc");
+  HIPC(ctx->sd_seq.ensure((size_t)bases + 1), "hipMalloc");
+  HIPC(ctx->sd_out.ensure(sizeof(bwagpu_intv_t) * (size_t)n_reads * (size_t)max_per_read), "hipMalloc");
+  HIPC(ctx->sd_n.ensure(sizeof(int32_t) * (size_t)n_reads), "hipMalloc");
+  HIPC(ctx->sd_scratch.ensure(sizeof(bwagpu_intv_t) * (size_t)seed_scratch_entries(bases, n_reads)), "hipMalloc");
+  HIPC(hipMemcpyAsync(ctx->sd_off.p, seq_off, sizeof(int64_t) * ((size_t)n_reads + 1), hipMemcpyHostToDevice, st),
+       "H2D");
+  if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, seq, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
+  SeedArgs a;
+  a.n_reads = n_reads;
+  a.seq_off = ctx->sd_off.as<int64_t>();
+  a.seq = ctx->sd_seq.as<uint8_t>();
+  a.max_per_read = max_per_read;
+  a.out = ctx->sd_out.as<bwagpu_intv_t>();
+  a.out_n = ctx->sd_n.as<int32_t>();
+  a.scratch = ctx->sd_scratch.as<bwagpu_intv_t>();
+  a.min_seed_len = opt->min_seed_len;
+  a.split_width = opt->split_width;
+  a.max_mem_intv = opt->max_mem_intv;
+  a.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);  // bwamem.c:124
+  HIPC(launch_collect_intv(ctx->bwt, a, st), "collect_intv launch");
+  HIPC(hipMemcpyAsync(out, ctx->sd_out.p, sizeof(bwagpu_intv_t) * (size_t)n_reads * (size_t)max_per_read,
+                      hipMemcpyDeviceToHost, st),
+       "D2H");
+  HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
+  for (int32_t r = 0; r < n_reads; ++r)
+    if (out_n[r] < 0) return fail(ctx, BWAGPU_E_UNSUPPORTED, "a read has more than max_per_read intervals");
+  return BWAGPU_OK;
+}

@@ -1,0 +1,35 @@
+// seed.h — internal declarations of the seeding kernels (seed.hip) shared
+// with the C ABI (capi.hip).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bwagpu.h"
+
+namespace bwagpu {
+
+// the resident FM-index (bwt_t, bwa/bwt.h:46-57)
+struct DevBwt {
+  uint64_t primary;
+  uint64_t L2[5];
+  uint64_t seq_len;
+  const uint32_t* bwt;  // 128-base blocks: 4 uint64 counts + 8 words of 2-bit bases
+};
+
+struct SeedArgs {
+  int32_t n_reads;
+  const int64_t* seq_off;
+  const uint8_t* seq;
+  int32_t max_per_read;
+  bwagpu_intv_t* out;       // n_reads * max_per_read
+  int32_t* out_n;           // n_reads
+  bwagpu_intv_t* scratch;   // read r: 3 lists of len_r + 2 at 3 * (seq_off[r] + 2r)
+  int32_t min_seed_len, split_width, max_mem_intv, split_len;
+};
+
+// lists a read needs in the scratch buffer: 3 * (bases + 2 * reads) entries
+inline int64_t seed_scratch_entries(int64_t bases, int32_t n_reads) { return 3 * (bases + 2 * (int64_t)n_reads); }
+
+hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st);
+
+}  // namespace bwagpu

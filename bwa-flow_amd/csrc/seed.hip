@@ -1,0 +1,324 @@
+// seed.hip — seeding's interval collection on the device: mem_collect_intv
+// (bwa/bwamem.c:120-167) for every read of a batch.
+//
+// One lane per read.  The work is a chain of dependent FM-index lookups — each
+// bwt_extend is two occurrence-block reads of 64 bytes at data-dependent
+// positions — so the kernel is bound by memory latency, not by ALU or HBM
+// bandwidth: it keeps as many reads in flight as the device holds lanes, and
+// each lookup is one 64-byte block fetched with four 16-byte loads issued
+// together.  The occurrence counts are computed in registers (three
+// equality-popcounts per 2-bit base word; A from the position count) instead
+// of bwa's 256-entry byte table.  The intermediate interval lists live in a
+// per-read scratch region of global memory (L1/L2 resident while a read works
+// on them); the read's own intervals are built in its output slots and sorted
+// there with klib's introsort restated step for step (the order of intervals
+// with equal info is the algorithm's).
+#include <hip/hip_runtime.h>
+
+#include "seed.h"
+
+namespace bwagpu {
+namespace {
+
+struct Ivl {
+  uint64_t x[3], info;
+};
+static_assert(sizeof(Ivl) == sizeof(bwagpu_intv_t), "interval layout");
+
+// bwt_occ4 (bwt.c:169-187): occurrences of A/C/G/T in bwt[0..k], $ removed
+__device__ __forceinline__ void occ4(const DevBwt& b, uint64_t k, uint64_t cnt[4]) {
+  if (k == ~0ull) {
+    cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
+    return;
+  }
+  k -= (k >= b.primary);
+  const uint4* p = reinterpret_cast<const uint4*>(b.bwt + (k >> 7 << 4));
+  const uint4 c01 = p[0], c23 = p[1], w0 = p[2], w1 = p[3];
+  const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  const int nfull = (int)((k & 127) >> 4);
+  const uint32_t tail = ~((1u << ((~(uint32_t)k & 15) << 1)) - 1);  // fields 0..(k & 15) of word nfull
+  uint32_t c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t m = (i < nfull ? 0xffffffffu : i == nfull ? tail : 0u) & 0x55555555u;
+    const uint32_t x1 = w[i] ^ 0x55555555u, x2 = w[i] ^ 0xaaaaaaaau, x3 = ~w[i];
+    c1 += __popc(~(x1 | x1 >> 1) & m);
+    c2 += __popc(~(x2 | x2 >> 1) & m);
+    c3 += __popc(~(x3 | x3 >> 1) & m);
+  }
+  const uint32_t c0 = (uint32_t)(k & 127) + 1 - c1 - c2 - c3;
+  cnt[0] = ((uint64_t)c01.y << 32 | c01.x) + c0;
+  cnt[1] = ((uint64_t)c01.w << 32 | c01.z) + c1;
+  cnt[2] = ((uint64_t)c23.y << 32 | c23.x) + c2;
+  cnt[3] = ((uint64_t)c23.w << 32 | c23.z) + c3;
+}
+
+// bwt_extend (bwt.c:262-276)
+__device__ __forceinline__ void extend(const DevBwt& b, const Ivl& ik, Ivl ok[4], int is_back) {
+  uint64_t tk[4], tl[4];
+  const int nb = !is_back;
+  occ4(b, ik.x[nb] - 1, tk);
+  occ4(b, ik.x[nb] - 1 + ik.x[2], tl);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ok[i].x[nb] = b.L2[i] + 1 + tk[i];
+    ok[i].x[2] = tl[i] - tk[i];
+    ok[i].info = 0;
+  }
+  ok[3].x[is_back] = ik.x[is_back] + (ik.x[nb] <= b.primary && ik.x[nb] + ik.x[2] - 1 >= b.primary);
+  ok[2].x[is_back] = ok[3].x[is_back] + ok[3].x[2];
+  ok[1].x[is_back] = ok[2].x[is_back] + ok[2].x[2];
+  ok[0].x[is_back] = ok[1].x[is_back] + ok[1].x[2];
+}
+
+__device__ __forceinline__ Ivl set_intv(const DevBwt& b, int c) {  // bwt.h:80
+  Ivl ik;
+  ik.x[0] = b.L2[c] + 1;
+  ik.x[2] = b.L2[c + 1] - b.L2[c];
+  ik.x[1] = b.L2[3 - c] + 1;
+  ik.info = 0;
+  return ik;
+}
+
+struct List {
+  Ivl* a;
+  int n, cap;
+  __device__ void push(const Ivl& v) {
+    if (n < cap) a[n] = v;
+    ++n;
+  }
+};
+
+__device__ __forceinline__ void reverse(List& v) {
+  for (int j = 0; j < v.n >> 1; ++j) {
+    const Ivl t = v.a[v.n - 1 - j];
+    v.a[v.n - 1 - j] = v.a[j];
+    v.a[j] = t;
+  }
+}
+
+// bwt_smem1a with max_intv = 0 (bwt.c:289-356)
+__device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, List& mem, List* prev,
+                     List* curr) {
+  Ivl ok[4];
+  int i;
+  mem.n = 0;
+  if (q[x] > 3) return x + 1;
+  if (min_intv < 1) min_intv = 1;
+  Ivl ik = set_intv(b, q[x]);
+  ik.info = (uint64_t)(x + 1);
+  curr->n = 0;
+  for (i = x + 1; i < len; ++i) {  // forward
+    const int qi = q[i];
+    if (qi < 4) {
+      const int c = 3 - qi;
+      extend(b, ik, ok, 0);
+      if (ok[c].x[2] != ik.x[2]) {
+        curr->push(ik);
+        if (ok[c].x[2] < (uint64_t)min_intv) break;
+      }
+      ik = ok[c];
+      ik.info = (uint64_t)(i + 1);
+    } else {
+      curr->push(ik);
+      break;
+    }
+  }
+  if (i == len) curr->push(ik);
+  reverse(*curr);  // longest matches first
+  const int ret = (int)curr->a[0].info;
+  List* t = curr;
+  curr = prev;
+  prev = t;
+  for (i = x - 1; i >= -1; --i) {  // backward
+    const int c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
+    curr->n = 0;
+    for (int j = 0; j < prev->n; ++j) {
+      const Ivl p = prev->a[j];
+      if (c >= 0) extend(b, p, ok, 1);
+      if (c < 0 || ok[c].x[2] < (uint64_t)min_intv) {
+        if (curr->n == 0 && (mem.n == 0 || (uint64_t)(i + 1) < mem.a[mem.n - 1].info >> 32)) {
+          Ivl h = p;
+          h.info |= (uint64_t)(i + 1) << 32;
+          mem.push(h);
+        }
+      } else if (curr->n == 0 || ok[c].x[2] != curr->a[curr->n - 1].x[2]) {
+        ok[c].info = p.info;
+        curr->push(ok[c]);
+      }
+    }
+    if (curr->n == 0) break;
+    t = curr;
+    curr = prev;
+    prev = t;
+  }
+  reverse(mem);  // by start
+  return ret;
+}
+
+// bwt_seed_strategy1 (bwt.c:358-378)
+__device__ int seed_strategy1(const DevBwt& b, int len, const uint8_t* q, int x, int min_len, int max_intv, Ivl& m) {
+  Ivl ok[4];
+  m.x[0] = m.x[1] = m.x[2] = m.info = 0;
+  if (q[x] > 3) return x + 1;
+  Ivl ik = set_intv(b, q[x]);
+  for (int i = x + 1; i < len; ++i) {
+    const int qi = q[i];
+    if (qi < 4) {
+      const int c = 3 - qi;
+      extend(b, ik, ok, 0);
+      if (ok[c].x[2] < (uint64_t)max_intv && i - x >= min_len) {
+        m = ok[c];
+        m.info = (uint64_t)x << 32 | (uint64_t)(i + 1);
+        return i + 1;
+      }
+      ik = ok[c];
+    } else {
+      return i + 1;
+    }
+  }
+  return len;
+}
+
+// klib's introsort by info (ksort.h:146-226, bwamem.c:90-91), step for step
+__device__ __forceinline__ bool lt(const Ivl& a, const Ivl& b) { return a.info < b.info; }
+__device__ __forceinline__ void swp(Ivl* a, int i, int j) {
+  const Ivl t = a[i];
+  a[i] = a[j];
+  a[j] = t;
+}
+__device__ void insert_sort(Ivl* a, int s, int t) {  // [s, t)
+  for (int i = s + 1; i < t; ++i)
+    for (int j = i; j > s && lt(a[j], a[j - 1]); --j) swp(a, j, j - 1);
+}
+__device__ void comb_sort(Ivl* a, int n) {
+  const double shrink = 1.2473309501039786540366528676643;
+  int gap = n;
+  bool swapped;
+  do {
+    if (gap > 2) {
+      gap = (int)(gap / shrink);
+      if (gap == 9 || gap == 10) gap = 11;
+    }
+    swapped = false;
+    for (int i = 0; i < n - gap; ++i)
+      if (lt(a[i + gap], a[i])) {
+        swp(a, i, i + gap);
+        swapped = true;
+      }
+  } while (swapped || gap > 2);
+  if (gap != 1) insert_sort(a, 0, n);
+}
+__device__ void intro_sort(Ivl* a, int n) {
+  if (n < 1) return;
+  if (n == 2) {
+    if (lt(a[1], a[0])) swp(a, 0, 1);
+    return;
+  }
+  int d = 2;
+  while ((1 << d) < n) ++d;
+  struct Frame {
+    int l, r, d;
+  } stack[40];
+  int top = 0, s = 0, t = n - 1;
+  d <<= 1;
+  for (;;) {
+    if (s < t) {
+      if (--d == 0) {
+        comb_sort(a + s, t - s + 1);
+        t = s;
+        continue;
+      }
+      int i = s, j = t, k = i + ((j - i) >> 1) + 1;
+      if (lt(a[k], a[i])) {
+        if (lt(a[k], a[j])) k = j;
+      } else {
+        k = lt(a[j], a[i]) ? i : j;
+      }
+      const Ivl rp = a[k];
+      if (k != t) swp(a, k, t);
+      for (;;) {
+        do ++i; while (lt(a[i], rp));
+        do --j; while (i <= j && lt(rp, a[j]));
+        if (j <= i) break;
+        swp(a, i, j);
+      }
+      swp(a, i, t);
+      if (i - s > t - i) {
+        if (i - s > 16) stack[top++] = Frame{s, i - 1, d};
+        s = t - i > 16 ? i + 1 : t;
+      } else {
+        if (t - i > 16) stack[top++] = Frame{i + 1, t, d};
+        t = i - s > 16 ? i - 1 : s;
+      }
+    } else {
+      if (top == 0) {
+        insert_sort(a, 0, n);
+        return;
+      }
+      --top;
+      s = stack[top].l;
+      t = stack[top].r;
+      d = stack[top].d;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a) {
+  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r >= a.n_reads) return;
+  const int64_t q0 = a.seq_off[r];
+  const int len = (int)(a.seq_off[r + 1] - q0);
+  const uint8_t* q = a.seq + q0;
+  Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 3 * (q0 + 2 * (int64_t)r);
+  List la{base, 0, len + 2}, lb{base + (len + 2), 0, len + 2}, mem1{base + 2 * (len + 2), 0, len + 2};
+  List mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, 0, a.max_per_read};
+  int x = 0;
+  while (x < len) {  // SMEMs
+    if (q[x] < 4) {
+      x = smem1(b, len, q, x, 1, mem1, &la, &lb);
+      for (int i = 0; i < mem1.n; ++i)
+        if ((int)((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32)) >= a.min_seed_len) mem.push(mem1.a[i]);
+    } else {
+      ++x;
+    }
+  }
+  const int old_n = min(mem.n, mem.cap);
+  for (int k = 0; k < old_n; ++k) {  // re-seeding inside long SMEMs
+    const Ivl p = mem.a[k];
+    const int start = (int)(p.info >> 32), end = (int)(int32_t)p.info;
+    if (end - start < a.split_len || p.x[2] > (uint64_t)a.split_width) continue;
+    smem1(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, &la, &lb);
+    for (int i = 0; i < mem1.n; ++i)
+      if ((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32) >= (uint32_t)a.min_seed_len) mem.push(mem1.a[i]);
+  }
+  if (a.max_mem_intv > 0) {  // LAST-like
+    x = 0;
+    while (x < len) {
+      if (q[x] < 4) {
+        Ivl m;
+        x = seed_strategy1(b, len, q, x, a.min_seed_len, a.max_mem_intv, m);
+        if (m.x[2] > 0) mem.push(m);
+      } else {
+        ++x;
+      }
+    }
+  }
+  if (mem.n <= mem.cap) {
+    intro_sort(mem.a, mem.n);
+    a.out_n[r] = mem.n;
+  } else {
+    a.out_n[r] = -mem.n;  // does not fit: flagged, left unsorted
+  }
+}
+
+}  // namespace
+
+hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st) {
+  if (a.n_reads <= 0) return hipSuccess;
+  const int blocks = (a.n_reads + 255) / 256;
+  hipLaunchKernelGGL(collect_intv_kernel, dim3(blocks), dim3(256), 0, st, b, a);
+  return hipGetLastError();
+}
+
+}  // namespace bwagpu

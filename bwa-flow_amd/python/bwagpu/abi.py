@@ -78,6 +78,21 @@ class Stats(C.Structure):
                 ("d2h_bytes", C.c_int64)]
 
 
+class BwtC(C.Structure):
+    """bwagpu_bwt_t == bwt_t's header + occurrence words (bwa/bwt.h:46-57)"""
+    _fields_ = [("primary", C.c_uint64), ("L2", C.c_uint64 * 5), ("seq_len", C.c_uint64),
+                ("bwt_size", C.c_uint64), ("bwt", C.c_void_p)]
+
+
+class SeedOpt(C.Structure):
+    """bwagpu_seedopt_t: mem_opt_t's seeding fields (bwamem.c:62-72)"""
+    _fields_ = [("min_seed_len", C.c_int32), ("split_width", C.c_int32), ("max_mem_intv", C.c_int32),
+                ("split_factor", C.c_float)]
+
+
+INTV_DTYPE = np.dtype([("x", "<u8", (3,)), ("info", "<u8")])  # bwagpu_intv_t == bwtintv_t
+assert INTV_DTYPE.itemsize == 32
+
 # every entry point declared in include/bwagpu.h: name -> (restype, argtypes)
 _VP = C.c_void_p
 PROTOS = {
@@ -103,6 +118,8 @@ PROTOS = {
     "bwagpu_debug_spec_counters": (C.c_int, [_VP, _VP, _VP]),
     "bwagpu_debug_spec_ext": (C.c_int, [_VP, _VP, _VP, C.c_int32]),
     "bwagpu_prof_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
+    "bwagpu_set_bwt": (C.c_int, [_VP, C.POINTER(BwtC)]),
+    "bwagpu_collect_intv": (C.c_int, [_VP, C.POINTER(SeedOpt), C.c_int32, _VP, _VP, C.c_int32, _VP, _VP]),
 }
 
 _lib = None

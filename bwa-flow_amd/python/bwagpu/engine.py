@@ -212,6 +212,35 @@ class Engine:
                                                   _ptr(out), _ptr(cig), _ptr(md)), "reg2aln_batch")
         return out[:n], cig[:n], md[:n]
 
+    def set_bwt(self, hdr, words):
+        """make the FM-index resident (hdr = primary, L2[0..4], seq_len as bwa's bwt_t)"""
+        hdr = np.asarray(hdr, np.int64)
+        self._bwt_words = np.ascontiguousarray(words, np.uint32)
+        b = abi.BwtC()
+        b.primary = int(hdr[0])
+        for i in range(5):
+            b.L2[i] = int(hdr[1 + i])
+        b.seq_len = int(hdr[6])
+        b.bwt_size = len(self._bwt_words)
+        b.bwt = self._bwt_words.ctypes.data
+        self._check(self.lib.bwagpu_set_bwt(self.ctx, C.byref(b)), "set_bwt")
+
+    def collect_intv(self, seq_off: np.ndarray, seq: np.ndarray, min_seed_len: int = 19, split_width: int = 10,
+                     max_mem_intv: int = 20, split_factor: float = 1.5, max_per_read: int = 256):
+        """mem_collect_intv (bwa/bwamem.c:120-167) per read -> (counts int32[n], intervals INTV_DTYPE[sum])"""
+        seq_off = np.ascontiguousarray(seq_off, np.int64)
+        seq = np.ascontiguousarray(seq, np.uint8)
+        n = len(seq_off) - 1
+        o = abi.SeedOpt(min_seed_len, split_width, max_mem_intv, split_factor)
+        out = np.zeros(max(n, 1) * max_per_read, abi.INTV_DTYPE)
+        cnt = np.zeros(max(n, 1), np.int32)
+        self._check(self.lib.bwagpu_collect_intv(self.ctx, C.byref(o), n, _ptr(seq_off), _ptr(seq), max_per_read,
+                                                 _ptr(out), _ptr(cnt)), "collect_intv")
+        cnt = cnt[:n]
+        rows = np.repeat(np.arange(n) * max_per_read, cnt) + (np.arange(int(cnt.sum())) -
+                                                               np.repeat(np.cumsum(cnt) - cnt, cnt))
+        return cnt, out[rows]
+
     def prof_start(self, max_launches: int):
         """time the next max_launches launches of the dominant extension kernel"""
         self._check(self.lib.bwagpu_prof_start(self.ctx, max_launches), "prof_start")

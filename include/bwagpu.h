@@ -214,6 +214,37 @@ typedef struct {
   int32_t w, status;
 } bwagpu_aln_t;
 
+/* ---- seeding: mem_collect_intv on the device ---- */
+
+/* The FM-index of the reference as bwa holds it (bwt_t, bwa/bwt.h:46-57):
+   primary, the cumulative counts L2[5], seq_len, and the bwt_size uint32
+   words of the interleaved occurrence array (per 128 BWT positions: 4 uint64
+   counts, then 8 words of 2-bit bases, first base in the highest bits). */
+typedef struct {
+  uint64_t primary;
+  uint64_t L2[5];
+  uint64_t seq_len;
+  uint64_t bwt_size;
+  const uint32_t *bwt;
+} bwagpu_bwt_t;
+
+/* == bwtintv_t (bwa/bwt.h:60-62): x[0] / x[1] the SA intervals of the match
+   and of its reverse complement, x[2] their size, info = start << 32 | end */
+typedef struct {
+  uint64_t x[3];
+  uint64_t info;
+} bwagpu_intv_t;
+
+/* mem_opt_t's seeding fields (bwa/bwamem.h:34-46, defaults bwamem.c:62-72) */
+typedef struct {
+  int32_t min_seed_len; /* -k, 19 */
+  int32_t split_width;  /* 10 */
+  int32_t max_mem_intv; /* 20: the LAST-like third pass runs when > 0 */
+  float split_factor;   /* -r, 1.5 */
+} bwagpu_seedopt_t;
+
+#define BWAGPU_MAX_SEED_READ 4096 /* longest read bwagpu_collect_intv takes */
+
 /* per-launch statistics of the last finished launch on a slot */
 typedef struct {
   double kernel_ms;      /* HIP-event time of the extension kernel(s)            */
@@ -281,6 +312,24 @@ int bwagpu_reg2aln_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_reg2al
                          bwagpu_aln_t *out, uint32_t *cigar, char *md);
 
 int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
+
+/* Makes bwt the context's resident FM-index (copied to the device; a later
+   call replaces it).  Replaces bwa's in-memory bwt_t for the seeding stage
+   (bwa_idx_load_bwt, bwa/bwa.c:244-260; bwa-flow's SeqsToChains reads it through
+   aux->idx->bwt, src/Pipeline.cpp:110-121). */
+int bwagpu_set_bwt(bwagpu_ctx_t *ctx, const bwagpu_bwt_t *bwt);
+
+/* mem_collect_intv (bwa/bwamem.c:120-167) for every read of a batch: the
+   SMEMs (bwt_smem1, bwt.c:289-356), the re-seeding inside long SMEMs, the
+   LAST-like pass (bwt_seed_strategy1, bwt.c:358-378), sorted by info as
+   ks_introsort leaves them (bwamem.c:90-91, 166).  Reads: nt4 bases (0..4) at
+   seq[seq_off[r]..seq_off[r+1]), host buffers, at most BWAGPU_MAX_SEED_READ
+   bases.  Read r's intervals go to out[r * max_per_read ...], their number to
+   out_n[r].  A read with more than max_per_read intervals gets out_n[r] =
+   -(its count) and the call returns BWAGPU_E_UNSUPPORTED after writing every
+   other read.  Blocking. */
+int bwagpu_collect_intv(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *opt, int32_t n_reads, const int64_t *seq_off,
+                        const uint8_t *seq, int32_t max_per_read, bwagpu_intv_t *out, int32_t *out_n);
 
 /* diagnostics: while dev_ptr != NULL every chain2aln launch on this device
    writes 8 x uint32 per read index r at dev_ptr[8r..8r+7]: start and end

@@ -48,6 +48,8 @@ def oracle_lib():
     lib.oracle_reg2aln_batch.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, C.c_int32, _VP, _VP,
                                          C.c_int, C.c_int, _VP, _VP, _VP]
     lib.oracle_reg2aln_batch.restype = C.c_int
+    lib.oracle_collect_intv.argtypes = [_VP, _VP, _VP, C.c_float, C.c_int, _VP, _VP, C.c_int]
+    lib.oracle_collect_intv.restype = C.c_int
     return lib
 
 
@@ -163,3 +165,27 @@ def reg2aln(which: str, opt: dict, ref: Ref, tasks, qpool, max_ops: int = 64, ma
     f(C.byref(o), C.byref(ref.bns), _ptr(ref.pac), n, _ptr(tasks), _ptr(qpool), max_ops, max_md, _ptr(out),
       _ptr(cig), _ptr(md))
     return out[:n], cig[:n], md[:n]
+
+
+def collect_intv(bwt_hdr, bwt_words, opt_i32, split_factor, seq_off, seq, cap: int = 512):
+    """mem_collect_intv per read with the restatement (oracle/seed.c) ->
+    (counts int32[n], intervals uint64[sum, 4] in the reference's order)"""
+    hdr = np.ascontiguousarray(np.asarray(bwt_hdr, np.int64)[:7])
+    words = np.ascontiguousarray(bwt_words, np.uint32)
+    ov = np.ascontiguousarray(opt_i32, np.int32)
+    seq = np.ascontiguousarray(seq, np.uint8)
+    lib = oracle_lib()
+    buf = np.zeros((cap, 4), np.uint64)
+    counts, out = [], []
+    for r in range(len(seq_off) - 1):
+        q = seq[seq_off[r]:seq_off[r + 1]]
+        q = np.ascontiguousarray(q)
+        n = lib.oracle_collect_intv(_ptr(hdr), _ptr(words), _ptr(ov), float(split_factor), len(q), _ptr(q),
+                                    _ptr(buf), len(buf))
+        if n > len(buf):  # a repetitive read: again with room for all of them
+            buf = np.zeros((n, 4), np.uint64)
+            n = lib.oracle_collect_intv(_ptr(hdr), _ptr(words), _ptr(ov), float(split_factor), len(q), _ptr(q),
+                                        _ptr(buf), len(buf))
+        counts.append(n)
+        out.append(buf[:n].copy())
+    return np.array(counts, np.int32), (np.concatenate(out) if out else np.zeros((0, 4), np.uint64))

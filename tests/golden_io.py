@@ -167,3 +167,19 @@ def synth_reg2aln_jobs(rng, ref_pac, l_pac, ann_offset, ann_len, n, lens=(100, 1
         qs.append(np.array(read, np.uint8))
         qo += L
     return tasks, np.concatenate(qs)
+
+
+SEED_SETS = ["c1", "mix"]
+
+
+def load_seed_bwt():
+    """-> (hdr int64[8]: primary, L2[0..4], seq_len, bwt_size; occurrence words uint32)"""
+    z = _npz("seed_bwt")
+    return z["hdr"], z["words"]
+
+
+def load_seed_set(name):
+    """-> (opt int32[3]: min_seed_len, split_width, max_mem_intv; split_factor; seq_off; seq;
+    expected counts per read; expected intervals uint64[sum, 4] = x0, x1, x2, info)"""
+    z = _npz("seed_" + name)
+    return z["opt"], float(z["split_factor"][0]), z["seq_off"], z["seq"], z["intv_n"], z["intv"]
