@@ -149,7 +149,7 @@ struct bwagpu_ctx {
   DevBuf bwt_words;
   DevBwt bwt{};
   bool has_bwt = false;
-  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch;
+  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack;
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
@@ -1353,8 +1353,9 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
 
 extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads,
                                    const int64_t* seq_off, const uint8_t* seq, int32_t max_per_read,
-                                   bwagpu_intv_t* out, int32_t* out_n) {
-  if (!ctx || !opt || n_reads < 0 || max_per_read < 1 || (n_reads && (!seq_off || !out || !out_n)))
+                                   bwagpu_intv_t* out, int64_t out_cap, int32_t* out_n) {
+  if (!ctx || !opt || n_reads < 0 || max_per_read < 1 || out_cap < 0 || (n_reads && (!seq_off || !out_n)) ||
+      (out_cap && !out))
     return BWAGPU_E_INVAL;
   if (!ctx->has_bwt) return fail(ctx, BWAGPU_E_INVAL, "no FM-index: call bwagpu_set_bwt first");
   if (opt->min_seed_len < 1 || opt->split_width < 0) return fail(ctx, BWAGPU_E_INVAL, "bad seeding options");
@@ -1391,12 +1392,22 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   a.max_mem_intv = opt->max_mem_intv;
   a.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);  // bwamem.c:124
   HIPC(launch_collect_intv(ctx->bwt, a, st), "collect_intv launch");
-  HIPC(hipMemcpyAsync(out, ctx->sd_out.p, sizeof(bwagpu_intv_t) * (size_t)n_reads * (size_t)max_per_read,
-                      hipMemcpyDeviceToHost, st),
-       "D2H");
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");
-  for (int32_t r = 0; r < n_reads; ++r)
+  // pack the per-read slots back to back (read order) and copy only those
+  std::vector<int64_t> off((size_t)n_reads + 1, 0);
+  for (int32_t r = 0; r < n_reads; ++r) {
     if (out_n[r] < 0) return fail(ctx, BWAGPU_E_UNSUPPORTED, "a read has more than max_per_read intervals");
+    off[(size_t)r + 1] = off[(size_t)r] + out_n[r];
+  }
+  const int64_t total = off[(size_t)n_reads];
+  if (total > out_cap) return fail(ctx, BWAGPU_E_UNSUPPORTED, "the batch has more than out_cap intervals");
+  if (total == 0) return BWAGPU_OK;
+  HIPC(ctx->sd_poff.ensure(sizeof(int64_t) * off.size()), "hipMalloc");
+  HIPC(ctx->sd_pack.ensure(sizeof(bwagpu_intv_t) * (size_t)total), "hipMalloc");
+  HIPC(hipMemcpyAsync(ctx->sd_poff.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, st), "H2D");
+  HIPC(launch_pack_intv(a, ctx->sd_poff.as<int64_t>(), ctx->sd_pack.as<bwagpu_intv_t>(), st), "pack launch");
+  HIPC(hipMemcpyAsync(out, ctx->sd_pack.p, sizeof(bwagpu_intv_t) * (size_t)total, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
   return BWAGPU_OK;
 }

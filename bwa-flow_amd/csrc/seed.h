@@ -31,5 +31,7 @@ struct SeedArgs {
 inline int64_t seed_scratch_entries(int64_t bases, int32_t n_reads) { return 3 * (bases + 2 * (int64_t)n_reads); }
 
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st);
+// packs the per-read slots: read r's out_n[r] intervals to dst + off[r]
+hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t* dst, hipStream_t st);
 
 }  // namespace bwagpu

@@ -312,7 +312,26 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
   }
 }
 
+// one wave per read: its intervals (32 B each) copied lane-parallel
+__global__ void __launch_bounds__(256) pack_intv_kernel(SeedArgs a, const int64_t* __restrict__ off,
+                                                        bwagpu_intv_t* __restrict__ dst) {
+  const int r = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int lane = (int)(threadIdx.x & 63);
+  if (r >= a.n_reads) return;
+  const int n = a.out_n[r];
+  const ulonglong4* src = reinterpret_cast<const ulonglong4*>(a.out) + (int64_t)r * a.max_per_read;
+  ulonglong4* d = reinterpret_cast<ulonglong4*>(dst) + off[r];
+  for (int i = lane; i < n; i += 64) d[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t* dst, hipStream_t st) {
+  if (a.n_reads <= 0) return hipSuccess;
+  const int blocks = (a.n_reads + 3) / 4;
+  hipLaunchKernelGGL(pack_intv_kernel, dim3(blocks), dim3(256), 0, st, a, off, dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st) {
   if (a.n_reads <= 0) return hipSuccess;

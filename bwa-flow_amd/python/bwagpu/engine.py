@@ -226,20 +226,20 @@ class Engine:
         self._check(self.lib.bwagpu_set_bwt(self.ctx, C.byref(b)), "set_bwt")
 
     def collect_intv(self, seq_off: np.ndarray, seq: np.ndarray, min_seed_len: int = 19, split_width: int = 10,
-                     max_mem_intv: int = 20, split_factor: float = 1.5, max_per_read: int = 256):
+                     max_mem_intv: int = 20, split_factor: float = 1.5, max_per_read: int = 256,
+                     out_cap: int | None = None):
         """mem_collect_intv (bwa/bwamem.c:120-167) per read -> (counts int32[n], intervals INTV_DTYPE[sum])"""
         seq_off = np.ascontiguousarray(seq_off, np.int64)
         seq = np.ascontiguousarray(seq, np.uint8)
         n = len(seq_off) - 1
         o = abi.SeedOpt(min_seed_len, split_width, max_mem_intv, split_factor)
-        out = np.zeros(max(n, 1) * max_per_read, abi.INTV_DTYPE)
+        cap = max(n, 1) * max_per_read if out_cap is None else out_cap
+        out = np.zeros(max(cap, 1), abi.INTV_DTYPE)
         cnt = np.zeros(max(n, 1), np.int32)
         self._check(self.lib.bwagpu_collect_intv(self.ctx, C.byref(o), n, _ptr(seq_off), _ptr(seq), max_per_read,
-                                                 _ptr(out), _ptr(cnt)), "collect_intv")
+                                                 _ptr(out), cap, _ptr(cnt)), "collect_intv")
         cnt = cnt[:n]
-        rows = np.repeat(np.arange(n) * max_per_read, cnt) + (np.arange(int(cnt.sum())) -
-                                                               np.repeat(np.cumsum(cnt) - cnt, cnt))
-        return cnt, out[rows]
+        return cnt, out[:int(cnt.sum())]
 
     def prof_start(self, max_launches: int):
         """time the next max_launches launches of the dominant extension kernel"""

@@ -324,12 +324,15 @@ int bwagpu_set_bwt(bwagpu_ctx_t *ctx, const bwagpu_bwt_t *bwt);
    LAST-like pass (bwt_seed_strategy1, bwt.c:358-378), sorted by info as
    ks_introsort leaves them (bwamem.c:90-91, 166).  Reads: nt4 bases (0..4) at
    seq[seq_off[r]..seq_off[r+1]), host buffers, at most BWAGPU_MAX_SEED_READ
-   bases.  Read r's intervals go to out[r * max_per_read ...], their number to
-   out_n[r].  A read with more than max_per_read intervals gets out_n[r] =
-   -(its count) and the call returns BWAGPU_E_UNSUPPORTED after writing every
-   other read.  Blocking. */
+   bases.  out_n[r] = read r's interval count; the intervals of all reads go
+   to out back to back in read order (read r's at sum(out_n[0..r))), at most
+   out_cap of them.  max_per_read bounds one read's list on the device: a read
+   with more gets out_n[r] = -(its count) and the call returns
+   BWAGPU_E_UNSUPPORTED (out_n is still written); so does a batch whose total
+   exceeds out_cap.  Blocking. */
 int bwagpu_collect_intv(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *opt, int32_t n_reads, const int64_t *seq_off,
-                        const uint8_t *seq, int32_t max_per_read, bwagpu_intv_t *out, int32_t *out_n);
+                        const uint8_t *seq, int32_t max_per_read, bwagpu_intv_t *out, int64_t out_cap,
+                        int32_t *out_n);
 
 /* diagnostics: while dev_ptr != NULL every chain2aln launch on this device
    writes 8 x uint32 per read index r at dev_ptr[8r..8r+7]: start and end
