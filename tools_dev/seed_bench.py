@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--check", type=int, default=2000)
     ap.add_argument("--cpu-reads", type=int, default=4000)
+    ap.add_argument("--mult", type=str, default="", help="comma list: also time k copies of the batch in one call")
     a = ap.parse_args()
     hdr = np.load(os.path.join(ROOT, "bench_data", "c2_bwt_hdr.npy"))
     words = np.load(os.path.join(ROOT, "bench_data", "c2_bwt_words.npy"))
@@ -55,6 +56,15 @@ def main():
     t0 = time.perf_counter()
     oracle.collect_intv(hdr, words, np.array([19, 10, 20], np.int32), 1.5, b.seq_off[:c + 1], b.seq[:b.seq_off[c]])
     cpu_s = time.perf_counter() - t0
+    scaling = {}
+    for k in [int(x) for x in a.mult.split(",") if x]:
+        so = np.concatenate([[0], np.cumsum(np.tile(np.diff(b.seq_off), k))]).astype(np.int64)
+        sq = np.tile(b.seq, k)
+        eng.collect_intv(so, sq, out_cap=int(n.sum()) * k)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            eng.collect_intv(so, sq, out_cap=int(n.sum()) * k)
+        scaling[k] = round((time.perf_counter() - t0) * 1e3 / 3, 2)
     slen = (iv["info"] & 0xffffffff).astype(np.int64) - (iv["info"] >> 32).astype(np.int64)
     print(json.dumps({
         "metric": "seeding_reads_per_s", "reads": int(b.n_reads), "ms_per_batch": round(ms, 3),
@@ -62,6 +72,7 @@ def main():
         "intervals_per_read": round(float(n.mean()), 2), "mean_interval_len": round(float(slen.mean()), 1),
         "parity_sample_reads": k, "parity": parity,
         "cpu_baseline": {"kind": "port", "threads": 1, "reads": c, "reads_per_s": round(c / cpu_s)},
+        "ms_for_k_batches_in_one_call": scaling,
         "scope": "host API wall incl. H2D of reads, D2H of packed intervals; BWT resident"}))
 
 
