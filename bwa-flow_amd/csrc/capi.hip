@@ -149,7 +149,10 @@ struct bwagpu_ctx {
   DevBuf bwt_words;
   DevBwt bwt{};
   bool has_bwt = false;
-  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack;
+  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy;
+  // bwt_extend calls tier 1 spends on a read before tier 2 (one wave per read)
+  // takes it: ~p90 of the C2 batch's per-read counts (mean 666, p90 975)
+  int seed_budget = 1024;
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
@@ -1391,6 +1394,10 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   a.split_width = opt->split_width;
   a.max_mem_intv = opt->max_mem_intv;
   a.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);  // bwamem.c:124
+  HIPC(ctx->sd_heavy.ensure(sizeof(int32_t) * ((size_t)n_reads + 1)), "hipMalloc");
+  a.budget = ctx->seed_budget;
+  a.heavy = ctx->sd_heavy.as<int32_t>() + 1;
+  a.n_heavy = ctx->sd_heavy.as<int32_t>();
   HIPC(launch_collect_intv(ctx->bwt, a, st), "collect_intv launch");
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");
@@ -1409,5 +1416,11 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   HIPC(launch_pack_intv(a, ctx->sd_poff.as<int64_t>(), ctx->sd_pack.as<bwagpu_intv_t>(), st), "pack launch");
   HIPC(hipMemcpyAsync(out, ctx->sd_pack.p, sizeof(bwagpu_intv_t) * (size_t)total, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");
+  return BWAGPU_OK;
+}
+
+extern "C" int bwagpu_debug_seed_budget(bwagpu_ctx_t* ctx, int32_t budget) {
+  if (!ctx || budget < 0) return BWAGPU_E_INVAL;
+  ctx->seed_budget = budget;
   return BWAGPU_OK;
 }

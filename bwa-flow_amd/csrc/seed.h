@@ -25,6 +25,9 @@ struct SeedArgs {
   int32_t* out_n;           // n_reads
   bwagpu_intv_t* scratch;   // read r: 3 lists of len_r + 2 at 3 * (seq_off[r] + 2r)
   int32_t min_seed_len, split_width, max_mem_intv, split_len;
+  int32_t budget;     // bwt_extend calls tier 1 spends on one read before handing it to tier 2
+  int32_t* heavy;     // n_reads: the reads handed over
+  int32_t* n_heavy;   // their number
 };
 
 // lists a read needs in the scratch buffer: 3 * (bases + 2 * reads) entries

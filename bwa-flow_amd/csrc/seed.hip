@@ -89,6 +89,13 @@ struct List {
   }
 };
 
+// tier 1 gives up on a read after this many bwt_extend calls (its wave would
+// otherwise wait for the slowest lane); tier 2 redoes it wave-parallel
+struct Budget {
+  int left;
+  __device__ bool spend() { return --left < 0; }
+};
+
 __device__ __forceinline__ void reverse(List& v) {
   for (int j = 0; j < v.n >> 1; ++j) {
     const Ivl t = v.a[v.n - 1 - j];
@@ -99,7 +106,7 @@ __device__ __forceinline__ void reverse(List& v) {
 
 // bwt_smem1a with max_intv = 0 (bwt.c:289-356)
 __device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, List& mem, List* prev,
-                     List* curr) {
+                     List* curr, Budget& bg) {
   Ivl ok[4];
   int i;
   mem.n = 0;
@@ -112,6 +119,7 @@ __device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_
     const int qi = q[i];
     if (qi < 4) {
       const int c = 3 - qi;
+      if (bg.spend()) return -1;
       extend(b, ik, ok, 0);
       if (ok[c].x[2] != ik.x[2]) {
         curr->push(ik);
@@ -135,7 +143,10 @@ __device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_
     curr->n = 0;
     for (int j = 0; j < prev->n; ++j) {
       const Ivl p = prev->a[j];
-      if (c >= 0) extend(b, p, ok, 1);
+      if (c >= 0) {
+        if (bg.spend()) return -1;
+        extend(b, p, ok, 1);
+      }
       if (c < 0 || ok[c].x[2] < (uint64_t)min_intv) {
         if (curr->n == 0 && (mem.n == 0 || (uint64_t)(i + 1) < mem.a[mem.n - 1].info >> 32)) {
           Ivl h = p;
@@ -157,7 +168,9 @@ __device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_
 }
 
 // bwt_seed_strategy1 (bwt.c:358-378)
-__device__ int seed_strategy1(const DevBwt& b, int len, const uint8_t* q, int x, int min_len, int max_intv, Ivl& m) {
+template <class B>
+__device__ int seed_strategy1(const DevBwt& b, int len, const uint8_t* q, int x, int min_len, int max_intv, Ivl& m,
+                              B& bg) {
   Ivl ok[4];
   m.x[0] = m.x[1] = m.x[2] = m.info = 0;
   if (q[x] > 3) return x + 1;
@@ -166,6 +179,7 @@ __device__ int seed_strategy1(const DevBwt& b, int len, const uint8_t* q, int x,
     const int qi = q[i];
     if (qi < 4) {
       const int c = 3 - qi;
+      if (bg.spend()) return -1;
       extend(b, ik, ok, 0);
       if (ok[c].x[2] < (uint64_t)max_intv && i - x >= min_len) {
         m = ok[c];
@@ -264,6 +278,7 @@ __device__ void intro_sort(Ivl* a, int n) {
   }
 }
 
+// ---- tier 1: one lane per read, within an extension budget
 __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a) {
   const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (r >= a.n_reads) return;
@@ -273,10 +288,16 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
   Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 3 * (q0 + 2 * (int64_t)r);
   List la{base, 0, len + 2}, lb{base + (len + 2), 0, len + 2}, mem1{base + 2 * (len + 2), 0, len + 2};
   List mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, 0, a.max_per_read};
+  Budget bg{a.budget};
+  auto give_up = [&]() {  // tier 2 takes the read
+    a.out_n[r] = 0;
+    a.heavy[atomicAdd(a.n_heavy, 1)] = r;
+  };
   int x = 0;
   while (x < len) {  // SMEMs
     if (q[x] < 4) {
-      x = smem1(b, len, q, x, 1, mem1, &la, &lb);
+      x = smem1(b, len, q, x, 1, mem1, &la, &lb, bg);
+      if (x < 0) return give_up();
       for (int i = 0; i < mem1.n; ++i)
         if ((int)((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32)) >= a.min_seed_len) mem.push(mem1.a[i]);
     } else {
@@ -288,7 +309,7 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
     const Ivl p = mem.a[k];
     const int start = (int)(p.info >> 32), end = (int)(int32_t)p.info;
     if (end - start < a.split_len || p.x[2] > (uint64_t)a.split_width) continue;
-    smem1(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, &la, &lb);
+    if (smem1(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, &la, &lb, bg) < 0) return give_up();
     for (int i = 0; i < mem1.n; ++i)
       if ((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32) >= (uint32_t)a.min_seed_len) mem.push(mem1.a[i]);
   }
@@ -297,7 +318,8 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
     while (x < len) {
       if (q[x] < 4) {
         Ivl m;
-        x = seed_strategy1(b, len, q, x, a.min_seed_len, a.max_mem_intv, m);
+        x = seed_strategy1(b, len, q, x, a.min_seed_len, a.max_mem_intv, m, bg);
+        if (x < 0) return give_up();
         if (m.x[2] > 0) mem.push(m);
       } else {
         ++x;
@@ -309,6 +331,210 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
     a.out_n[r] = mem.n;
   } else {
     a.out_n[r] = -mem.n;  // does not fit: flagged, left unsorted
+  }
+}
+
+// ---- tier 2: one wave per read, the backward search lane-parallel
+// Every scalar (interval under forward extension, list lengths, positions) is
+// wave-uniform; list entries written by lane 0 (or by their owner lane) are
+// published with a workgroup fence before other lanes read them.
+struct NoBudget {
+  __device__ bool spend() { return false; }
+};
+
+struct WList {
+  Ivl* a;
+  int n, cap;
+  __device__ void push(const Ivl& v, bool lane0) {
+    if (n < cap && lane0) a[n] = v;
+    ++n;
+  }
+};
+
+__device__ __forceinline__ void publish() { __threadfence_block(); }
+
+__device__ __forceinline__ void wreverse(WList& v, int lane) {
+  for (int j0 = 0; j0 < v.n >> 1; j0 += 64) {
+    const int j = j0 + lane;
+    const bool on = j < v.n >> 1;
+    Ivl lo, hi;
+    if (on) {
+      lo = v.a[j];
+      hi = v.a[v.n - 1 - j];
+    }
+    publish();
+    if (on) {
+      v.a[j] = hi;
+      v.a[v.n - 1 - j] = lo;
+    }
+    publish();
+  }
+}
+
+__device__ __forceinline__ uint64_t bperm64(int src_lane, uint64_t v) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)v);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(v >> 32));
+  return (uint64_t)(uint32_t)hi << 32 | (uint32_t)lo;
+}
+
+// bwt_smem1a with max_intv = 0 (bwt.c:289-356), one wave
+__device__ int smem1_wave(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, WList& mem, WList* prev,
+                          WList* curr, int lane) {
+  const bool l0 = lane == 0;
+  Ivl ok[4];
+  int i;
+  mem.n = 0;
+  if (q[x] > 3) return x + 1;
+  if (min_intv < 1) min_intv = 1;
+  Ivl ik = set_intv(b, q[x]);
+  ik.info = (uint64_t)(x + 1);
+  curr->n = 0;
+  for (i = x + 1; i < len; ++i) {  // forward: one interval, every lane alike
+    const int qi = q[i];
+    if (qi < 4) {
+      const int c = 3 - qi;
+      extend(b, ik, ok, 0);
+      if (ok[c].x[2] != ik.x[2]) {
+        curr->push(ik, l0);
+        if (ok[c].x[2] < (uint64_t)min_intv) break;
+      }
+      ik = ok[c];
+      ik.info = (uint64_t)(i + 1);
+    } else {
+      curr->push(ik, l0);
+      break;
+    }
+  }
+  if (i == len) curr->push(ik, l0);
+  publish();
+  wreverse(*curr, lane);
+  const int ret = (int)curr->a[0].info;
+  WList* t = curr;
+  curr = prev;
+  prev = t;
+  const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
+  for (i = x - 1; i >= -1; --i) {  // backward: lane j extends prev[j]
+    const int c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
+    curr->n = 0;
+    bool have_last = false;  // a kept (pushed) entry exists in curr
+    uint64_t last_sz = 0;
+    for (int j0 = 0; j0 < prev->n; j0 += 64) {
+      const int j = j0 + lane;
+      const bool valid = j < prev->n;
+      Ivl p{};
+      if (valid) p = prev->a[j];
+      Ivl okc{};
+      if (valid && c >= 0) {
+        extend(b, p, ok, 1);
+        okc = ok[c];
+      }
+      const bool A = valid && (c < 0 || okc.x[2] < (uint64_t)min_intv);
+      const bool nA = valid && !A;
+      // bwt.c:333-338: only entry 0 can reach mem (curr is empty before the
+      // first non-A entry; after a push the containment test fails)
+      if (j0 == 0) {
+        const bool a0 = __builtin_amdgcn_readfirstlane((int)A) != 0;
+        if (a0) {
+          const Ivl p0 = prev->a[0];
+          if (mem.n == 0 || (uint64_t)(i + 1) < mem.a[mem.n - 1].info >> 32) {
+            Ivl h = p0;
+            h.info |= (uint64_t)(i + 1) << 32;
+            mem.push(h, l0);
+            publish();
+          }
+        }
+      }
+      // bwt.c:339-342: a non-A entry is pushed unless its size equals the last
+      // pushed one, i.e. that of the previous non-A entry
+      const uint64_t nA_m = __builtin_amdgcn_ballot_w64(nA);
+      const uint64_t prev_m = nA_m & below;
+      const int pl = prev_m ? 63 - (int)__builtin_clzll(prev_m) : 0;
+      const uint64_t psz = bperm64(pl, okc.x[2]);
+      const bool keep = nA && (prev_m ? okc.x[2] != psz : (!have_last || okc.x[2] != last_sz));
+      const uint64_t keep_m = __builtin_amdgcn_ballot_w64(keep);
+      if (keep) {
+        Ivl v = okc;
+        v.info = p.info;
+        curr->a[curr->n + (int)__builtin_popcountll(keep_m & below)] = v;
+      }
+      curr->n += (int)__builtin_popcountll(keep_m);
+      if (nA_m) {
+        const int hl = 63 - (int)__builtin_clzll(nA_m);
+        last_sz = bperm64(hl, okc.x[2]);
+        have_last = true;
+      }
+      publish();
+    }
+    if (curr->n == 0) break;
+    t = curr;
+    curr = prev;
+    prev = t;
+  }
+  wreverse(mem, lane);
+  return ret;
+}
+
+__global__ void __launch_bounds__(256) collect_intv_wave_kernel(DevBwt b, SeedArgs a) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool l0 = lane == 0;
+  const int nw = (int)(gridDim.x * (blockDim.x >> 6));
+  const int n_heavy = *a.n_heavy;
+  NoBudget nb;
+  for (int h = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); h < n_heavy; h += nw) {
+    const int r = __builtin_amdgcn_readfirstlane(a.heavy[h]);
+    const int64_t q0 = a.seq_off[r];
+    const int len = (int)(a.seq_off[r + 1] - q0);
+    const uint8_t* q = a.seq + q0;
+    Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 3 * (q0 + 2 * (int64_t)r);
+    WList la{base, 0, len + 2}, lb{base + (len + 2), 0, len + 2}, mem1{base + 2 * (len + 2), 0, len + 2};
+    WList mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, 0, a.max_per_read};
+    int x = 0;
+    while (x < len) {  // SMEMs
+      if (q[x] < 4) {
+        x = smem1_wave(b, len, q, x, 1, mem1, &la, &lb, lane);
+        for (int i = 0; i < mem1.n; ++i) {
+          const Ivl v = mem1.a[i];
+          if ((int)((uint32_t)v.info - (uint32_t)(v.info >> 32)) >= a.min_seed_len) mem.push(v, l0);
+        }
+        publish();
+      } else {
+        ++x;
+      }
+    }
+    const int old_n = min(mem.n, mem.cap);
+    for (int k = 0; k < old_n; ++k) {  // re-seeding inside long SMEMs
+      const Ivl p = mem.a[k];
+      const int start = (int)(p.info >> 32), end = (int)(int32_t)p.info;
+      if (end - start < a.split_len || p.x[2] > (uint64_t)a.split_width) continue;
+      smem1_wave(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, &la, &lb, lane);
+      for (int i = 0; i < mem1.n; ++i) {
+        const Ivl v = mem1.a[i];
+        if ((uint32_t)v.info - (uint32_t)(v.info >> 32) >= (uint32_t)a.min_seed_len) mem.push(v, l0);
+      }
+      publish();
+    }
+    if (a.max_mem_intv > 0) {  // LAST-like
+      x = 0;
+      while (x < len) {
+        if (q[x] < 4) {
+          Ivl m;
+          x = seed_strategy1(b, len, q, x, a.min_seed_len, a.max_mem_intv, m, nb);
+          if (m.x[2] > 0) mem.push(m, l0);
+        } else {
+          ++x;
+        }
+      }
+      publish();
+    }
+    if (l0) {
+      if (mem.n <= mem.cap) {
+        intro_sort(mem.a, mem.n);
+        a.out_n[r] = mem.n;
+      } else {
+        a.out_n[r] = -mem.n;
+      }
+    }
+    publish();
   }
 }
 
@@ -335,8 +561,13 @@ hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t
 
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st) {
   if (a.n_reads <= 0) return hipSuccess;
-  const int blocks = (a.n_reads + 255) / 256;
-  hipLaunchKernelGGL(collect_intv_kernel, dim3(blocks), dim3(256), 0, st, b, a);
+  hipError_t e = hipMemsetAsync(a.n_heavy, 0, sizeof(int32_t), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(collect_intv_kernel, dim3((a.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // the reads tier 1 gave up on, one wave each (the count is read on the device)
+  const int waves = a.n_reads < 4096 ? a.n_reads : 4096;
+  hipLaunchKernelGGL(collect_intv_wave_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, b, a);
   return hipGetLastError();
 }
 

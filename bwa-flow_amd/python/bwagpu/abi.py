@@ -119,6 +119,7 @@ PROTOS = {
     "bwagpu_debug_spec_ext": (C.c_int, [_VP, _VP, _VP, C.c_int32]),
     "bwagpu_prof_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "bwagpu_set_bwt": (C.c_int, [_VP, C.POINTER(BwtC)]),
+    "bwagpu_debug_seed_budget": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_collect_intv": (C.c_int, [_VP, C.POINTER(SeedOpt), C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int64,
                                        _VP]),
 }

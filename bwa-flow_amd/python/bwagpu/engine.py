@@ -225,6 +225,10 @@ class Engine:
         b.bwt = self._bwt_words.ctypes.data
         self._check(self.lib.bwagpu_set_bwt(self.ctx, C.byref(b)), "set_bwt")
 
+    def seed_budget(self, budget: int):
+        """bwt_extend calls a read gets on one lane before the wave kernel takes it (0: all on waves)"""
+        self._check(self.lib.bwagpu_debug_seed_budget(self.ctx, budget), "seed_budget")
+
     def collect_intv(self, seq_off: np.ndarray, seq: np.ndarray, min_seed_len: int = 19, split_width: int = 10,
                      max_mem_intv: int = 20, split_factor: float = 1.5, max_per_read: int = 256,
                      out_cap: int | None = None):

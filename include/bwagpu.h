@@ -334,6 +334,13 @@ int bwagpu_collect_intv(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *opt, int32_t 
                         const uint8_t *seq, int32_t max_per_read, bwagpu_intv_t *out, int64_t out_cap,
                         int32_t *out_n);
 
+/* Tuning / tests: bwagpu_collect_intv runs each read on one lane until it has
+   made `budget` bwt_extend calls (default 1024, about the 90th percentile of a
+   150 bp read on a chr21-sized index), then hands it to a second kernel that
+   runs it on a whole wave (backward search lane-parallel).  0 sends every
+   read to the wave kernel.  Results do not depend on it. */
+int bwagpu_debug_seed_budget(bwagpu_ctx_t *ctx, int32_t budget);
+
 /* diagnostics: while dev_ptr != NULL every chain2aln launch on this device
    writes 8 x uint32 per read index r at dev_ptr[8r..8r+7]: start and end
    s_memrealtime (100 MHz, lo/hi), DP rows, DP cells, HW_ID, XCC_ID.

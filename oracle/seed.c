@@ -51,10 +51,14 @@ static void occ4(const obwt_t *b, uint64_t k, uint64_t cnt[4])
   for (int v = 0; v < 4; ++v) cnt[v] += c[v];
 }
 
+static uint64_t n_extend; /* bwt_extend calls (work statistics for the device kernel's tiers) */
+uint64_t oracle_seed_extends(void) { return n_extend; }
+
 /* bwt.c:262-276 */
 static void extend(const obwt_t *b, const ivl_t *ik, ivl_t ok[4], int is_back)
 {
   uint64_t tk[4], tl[4];
+  ++n_extend;
   occ4(b, ik->x[!is_back] - 1, tk);
   occ4(b, ik->x[!is_back] - 1 + ik->x[2], tl);
   for (int i = 0; i < 4; ++i) {

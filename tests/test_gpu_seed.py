@@ -34,10 +34,16 @@ def as_u64(iv):
     return np.column_stack([iv["x"], iv["info"]]).astype(np.uint64) if len(iv) else np.zeros((0, 4), np.uint64)
 
 
+@pytest.mark.parametrize("budget", [1024, 0, 200])
 @pytest.mark.parametrize("name", G.SEED_SETS)
-def test_collect_intv_golden(eng, name):
+def test_collect_intv_golden(eng, name, budget):
+    """budget 0: every read on the wave kernel; 200: a mix of both tiers"""
     opt, sf, seq_off, seq, want_n, want = G.load_seed_set(name)
-    n, iv = eng.collect_intv(seq_off, seq, int(opt[0]), int(opt[1]), int(opt[2]), sf)
+    eng.seed_budget(budget)
+    try:
+        n, iv = eng.collect_intv(seq_off, seq, int(opt[0]), int(opt[1]), int(opt[2]), sf)
+    finally:
+        eng.seed_budget(1024)
     assert np.array_equal(n, want_n)
     assert np.array_equal(as_u64(iv), want)
 
@@ -82,9 +88,12 @@ def test_collect_intv_edge_reads(eng):
     seq = np.concatenate(reads)
     hdr, words = G.load_seed_bwt()
     want_n, want = oracle.collect_intv(hdr, words, np.array([19, 10, 20], np.int32), 1.5, seq_off, seq)
-    n, iv = eng.collect_intv(seq_off, seq, max_per_read=8192)  # the homopolymer has thousands
-    assert n[0] == 0 and n[1] == 0 and n[2] == 0 and n[3] > 1000
-    assert np.array_equal(n, want_n) and np.array_equal(as_u64(iv), want)
+    for budget in (1024, 0):
+        eng.seed_budget(budget)
+        n, iv = eng.collect_intv(seq_off, seq, max_per_read=8192)  # the homopolymer has thousands
+        assert n[0] == 0 and n[1] == 0 and n[2] == 0 and n[3] > 1000
+        assert np.array_equal(n, want_n) and np.array_equal(as_u64(iv), want)
+    eng.seed_budget(1024)
 
 
 def test_collect_intv_overflow_and_missing_index(eng):

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--check", type=int, default=2000)
     ap.add_argument("--cpu-reads", type=int, default=4000)
+    ap.add_argument("--budget", type=int, default=-1, help="bwt_extend calls per read on one lane (-1: library default)")
     ap.add_argument("--mult", type=str, default="", help="comma list: also time k copies of the batch in one call")
     a = ap.parse_args()
     hdr = np.load(os.path.join(ROOT, "bench_data", "c2_bwt_hdr.npy"))
@@ -41,6 +42,8 @@ def main():
     opt, *_ = G.load_chain_set("c1_default")
     eng = Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
     eng.set_bwt(hdr, words)
+    if a.budget >= 0:
+        eng.seed_budget(a.budget)
     n, iv = eng.collect_intv(b.seq_off, b.seq)  # warm-up
     t0 = time.perf_counter()
     for _ in range(a.reps):
