@@ -128,3 +128,29 @@ def test_malformed_record_takes_the_error_path(exe, tmp_path):
     assert np.array_equal(n[keep], want_n[keep])
     for r in keep[::7] + keep[-3:]:
         assert G.region_mismatch(regs[got_off[r]:got_off[r + 1]], want_regs[off[r]:off[r + 1]]) is None
+
+
+@pytest.mark.gpu
+def test_record_with_overlong_read_falls_back_to_cpu(exe, tmp_path):
+    """a read longer than BWAGPU_MAX_READ_LEN makes its record unsupported on
+    the device (E_UNSUPPORTED before anything is enqueued): that record goes to
+    the CPU stage (FPGAPipeline.cpp's per-record fallback), the others stay on
+    the GPU, and every output equals the CPU stage's on the same input"""
+    d_cpu, d_gpu = str(tmp_path / "cpu"), str(tmp_path / "gpu")
+    os.makedirs(d_cpu)
+    os.makedirs(d_gpu)
+    per = 50
+    for d in (d_cpu, d_gpu):
+        b, _, _ = write_inputs(d, "c1_default")
+        r = per + 3  # a read of record 1
+        seq_off = b.seq_off.copy()
+        ext = np.full(abi.MAX_READ_LEN + 10 - int(seq_off[r + 1] - seq_off[r]), 2, np.uint8)
+        seq = np.concatenate([b.seq[:seq_off[r + 1]], ext, b.seq[seq_off[r + 1]:]])
+        seq_off[r + 1:] += len(ext)
+        seq_off.astype(np.int64).tofile(os.path.join(d, "seq_off.bin"))
+        seq.astype(np.uint8).tofile(os.path.join(d, "seq.bin"))
+    want_info, want_regs, want_n = run(exe, d_cpu, "cpu", per, 2)
+    info, regs, n = run(exe, d_gpu, "gpu_only", per, 2)
+    assert info["gpu_fallback_cpu"] == 1 and info["on_gpu"] >= info["records"] - 1, info
+    assert info["outputs"] == info["records"] and info["bad_ownership"] == 0
+    check(regs, n, want_regs, want_n)
