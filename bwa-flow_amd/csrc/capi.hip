@@ -146,7 +146,7 @@ struct bwagpu_ctx {
   hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
   // seeding (bwagpu_set_bwt / bwagpu_collect_intv): the resident FM-index and
   // the batch buffers
-  DevBuf bwt_words;
+  DevBuf bwt_words, sa_d, sa_in, sa_out;
   DevBwt bwt{};
   bool has_bwt = false;
   DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy;
@@ -1350,7 +1350,37 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
   for (int i = 0; i < 5; ++i) ctx->bwt.L2[i] = bwt->L2[i];
   ctx->bwt.seq_len = bwt->seq_len;
   ctx->bwt.bwt = ctx->bwt_words.as<uint32_t>();
+  ctx->bwt.sa = nullptr;
+  ctx->bwt.sa_mask = 0;
+  ctx->bwt.sa_shift = 0;
+  if (bwt->sa) {
+    const int iv = bwt->sa_intv;
+    if (iv < 1 || (iv & (iv - 1)) || bwt->n_sa < bwt->seq_len / (uint64_t)iv + 1)
+      return fail(ctx, BWAGPU_E_INVAL, "suffix array sample interval / size inconsistent");
+    HIPC(ctx->sa_d.ensure(sizeof(uint64_t) * bwt->n_sa), "hipMalloc");
+    HIPC(hipMemcpy(ctx->sa_d.p, bwt->sa, sizeof(uint64_t) * bwt->n_sa, hipMemcpyHostToDevice), "H2D");
+    ctx->bwt.sa = ctx->sa_d.as<uint64_t>();
+    ctx->bwt.sa_mask = (uint64_t)iv - 1;
+    while ((1 << ctx->bwt.sa_shift) < iv) ++ctx->bwt.sa_shift;
+  }
   ctx->has_bwt = true;
+  return BWAGPU_OK;
+}
+
+extern "C" int bwagpu_bwt_sa(bwagpu_ctx_t* ctx, int64_t n, const uint64_t* k, uint64_t* out) {
+  if (!ctx || n < 0 || (n && (!k || !out))) return BWAGPU_E_INVAL;
+  if (!ctx->has_bwt || !ctx->bwt.sa) return fail(ctx, BWAGPU_E_INVAL, "no suffix array: pass it to bwagpu_set_bwt");
+  for (int64_t i = 0; i < n; ++i)
+    if (k[i] > ctx->bwt.seq_len) return fail(ctx, BWAGPU_E_INVAL, "BWT position past seq_len");
+  if (n == 0) return BWAGPU_OK;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->slot[0].stream;
+  HIPC(ctx->sa_in.ensure(sizeof(uint64_t) * (size_t)n), "hipMalloc");
+  HIPC(ctx->sa_out.ensure(sizeof(uint64_t) * (size_t)n), "hipMalloc");
+  HIPC(hipMemcpyAsync(ctx->sa_in.p, k, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(launch_bwt_sa(ctx->bwt, n, ctx->sa_in.as<uint64_t>(), ctx->sa_out.as<uint64_t>(), st), "bwt_sa launch");
+  HIPC(hipMemcpyAsync(out, ctx->sa_out.p, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
   return BWAGPU_OK;
 }
 

@@ -14,6 +14,9 @@ struct DevBwt {
   uint64_t L2[5];
   uint64_t seq_len;
   const uint32_t* bwt;  // 128-base blocks: 4 uint64 counts + 8 words of 2-bit bases
+  const uint64_t* sa;    // sampled suffix array (NULL if not uploaded)
+  uint64_t sa_mask;      // sa_intv - 1
+  int sa_shift;          // log2(sa_intv)
 };
 
 struct SeedArgs {
@@ -34,6 +37,8 @@ struct SeedArgs {
 inline int64_t seed_scratch_entries(int64_t bases, int32_t n_reads) { return 3 * (bases + 2 * (int64_t)n_reads); }
 
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st);
+// bwt_sa for n positions
+hipError_t launch_bwt_sa(const DevBwt& b, int64_t n, const uint64_t* k, uint64_t* out, hipStream_t st);
 // packs the per-read slots: read r's out_n[r] intervals to dst + off[r]
 hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t* dst, hipStream_t st);
 

@@ -550,7 +550,36 @@ __global__ void __launch_bounds__(256) pack_intv_kernel(SeedArgs a, const int64_
   for (int i = lane; i < n; i += 64) d[i] = src[i];
 }
 
+// bwt_sa (bwt.c:86-96): one lane per position; every LF step reads one
+// 64-byte occurrence block (bwt_B0 and bwt_occ of a step fall in the same one)
+__global__ void __launch_bounds__(256) bwt_sa_kernel(DevBwt b, int64_t n, const uint64_t* __restrict__ kin,
+                                                     uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = kin[i], steps = 0;
+  while (k & b.sa_mask) {
+    ++steps;
+    if (k == b.primary) {  // bwt_invPsi (bwt.c:53-59)
+      k = 0;
+      continue;
+    }
+    const uint64_t x = k - (k > b.primary);
+    const uint32_t w = b.bwt[(x >> 7 << 4) + 8 + ((x & 127) >> 4)];
+    const int c = (int)(w >> ((~(uint32_t)x & 15) << 1) & 3);  // bwt_B0
+    uint64_t cnt[4];
+    occ4(b, k, cnt);  // bwt_occ(k, c); k == seq_len gives the column total
+    k = b.L2[c] + cnt[c];
+  }
+  out[i] = steps + b.sa[k >> b.sa_shift];
+}
+
 }  // namespace
+
+hipError_t launch_bwt_sa(const DevBwt& b, int64_t n, const uint64_t* k, uint64_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bwt_sa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, b, n, k, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t* dst, hipStream_t st) {
   if (a.n_reads <= 0) return hipSuccess;

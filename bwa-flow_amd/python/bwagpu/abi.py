@@ -81,7 +81,8 @@ class Stats(C.Structure):
 class BwtC(C.Structure):
     """bwagpu_bwt_t == bwt_t's header + occurrence words (bwa/bwt.h:46-57)"""
     _fields_ = [("primary", C.c_uint64), ("L2", C.c_uint64 * 5), ("seq_len", C.c_uint64),
-                ("bwt_size", C.c_uint64), ("bwt", C.c_void_p)]
+                ("bwt_size", C.c_uint64), ("bwt", C.c_void_p), ("sa_intv", C.c_int32), ("pad_", C.c_int32),
+                ("n_sa", C.c_uint64), ("sa", C.c_void_p)]
 
 
 class SeedOpt(C.Structure):
@@ -120,6 +121,7 @@ PROTOS = {
     "bwagpu_prof_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "bwagpu_set_bwt": (C.c_int, [_VP, C.POINTER(BwtC)]),
     "bwagpu_debug_seed_budget": (C.c_int, [_VP, C.c_int32]),
+    "bwagpu_bwt_sa": (C.c_int, [_VP, C.c_int64, _VP, _VP]),
     "bwagpu_collect_intv": (C.c_int, [_VP, C.POINTER(SeedOpt), C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int64,
                                        _VP]),
 }

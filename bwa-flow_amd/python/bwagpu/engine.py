@@ -212,10 +212,12 @@ class Engine:
                                                   _ptr(out), _ptr(cig), _ptr(md)), "reg2aln_batch")
         return out[:n], cig[:n], md[:n]
 
-    def set_bwt(self, hdr, words):
-        """make the FM-index resident (hdr = primary, L2[0..4], seq_len as bwa's bwt_t)"""
+    def set_bwt(self, hdr, words, sa=None, sa_intv: int = 32):
+        """make the FM-index resident (hdr = primary, L2[0..4], seq_len as bwa's bwt_t;
+        sa = the sampled suffix array, for bwt_sa)"""
         hdr = np.asarray(hdr, np.int64)
         self._bwt_words = np.ascontiguousarray(words, np.uint32)
+        self._bwt_sa = None if sa is None else np.ascontiguousarray(sa, np.uint64)
         b = abi.BwtC()
         b.primary = int(hdr[0])
         for i in range(5):
@@ -223,7 +225,18 @@ class Engine:
         b.seq_len = int(hdr[6])
         b.bwt_size = len(self._bwt_words)
         b.bwt = self._bwt_words.ctypes.data
+        if self._bwt_sa is not None:
+            b.sa_intv = sa_intv
+            b.n_sa = len(self._bwt_sa)
+            b.sa = self._bwt_sa.ctypes.data
         self._check(self.lib.bwagpu_set_bwt(self.ctx, C.byref(b)), "set_bwt")
+
+    def bwt_sa(self, ks) -> np.ndarray:
+        """bwt_sa (bwa/bwt.c:86-96) per BWT position"""
+        ks = np.ascontiguousarray(ks, np.uint64)
+        out = np.zeros(max(len(ks), 1), np.uint64)
+        self._check(self.lib.bwagpu_bwt_sa(self.ctx, len(ks), _ptr(ks), _ptr(out)), "bwt_sa")
+        return out[:len(ks)]
 
     def seed_budget(self, budget: int):
         """bwt_extend calls a read gets on one lane before the wave kernel takes it (0: all on waves)"""

@@ -226,6 +226,12 @@ typedef struct {
   uint64_t seq_len;
   uint64_t bwt_size;
   const uint32_t *bwt;
+  /* the sampled suffix array (bwt.h:55-57): sa[i] = SA[i * sa_intv], n_sa
+     entries; sa may be NULL when bwagpu_bwt_sa is not used */
+  int32_t sa_intv;
+  int32_t pad_;
+  uint64_t n_sa;
+  const uint64_t *sa;
 } bwagpu_bwt_t;
 
 /* == bwtintv_t (bwa/bwt.h:60-62): x[0] / x[1] the SA intervals of the match
@@ -333,6 +339,11 @@ int bwagpu_set_bwt(bwagpu_ctx_t *ctx, const bwagpu_bwt_t *bwt);
 int bwagpu_collect_intv(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *opt, int32_t n_reads, const int64_t *seq_off,
                         const uint8_t *seq, int32_t max_per_read, bwagpu_intv_t *out, int64_t out_cap,
                         int32_t *out_n);
+
+/* bwt_sa (bwa/bwt.c:86-96) for n BWT positions k[i] in [0, seq_len]: out[i]
+   = the forward-reverse coordinate mem_chain takes as a seed's rbeg
+   (bwamem.c:288).  Needs the suffix array in bwagpu_set_bwt.  Blocking. */
+int bwagpu_bwt_sa(bwagpu_ctx_t *ctx, int64_t n, const uint64_t *k, uint64_t *out);
 
 /* Tuning / tests: bwagpu_collect_intv runs each read on one lane until it has
    made `budget` bwt_extend calls (default 1024, about the 90th percentile of a

@@ -17,6 +17,8 @@
  *   seq_off   int64 [n+1], seq uint8 (0..4)
  *   intv_n    int32 [n], intv uint64 [sum intv_n][4] = bwtintv_t {x0, x1, x2, info}
  *   opt       int32 [min_seed_len, split_width, max_mem_intv], float split_factor
+ *   sa_hdr    int64 [sa_intv, n_sa], sa uint64 [n_sa]  (the sampled suffix array)
+ *   sa_q/sa_v uint64: BWT positions and the reference bwt_sa of each
  *
  * usage: gen_seed <outdir> <seed> <n_reads> <len:150|100|250|mix> [genome_len] [n_frac]
  */
@@ -114,13 +116,35 @@ int main(int argc, char *argv[])
   }
   fclose(f);
   bwa_idx_build(fa, fa, BWTALGO_AUTO, 10000000);
-  bwaidx_t *idx = bwa_idx_load(fa, BWA_IDX_BWT);
+  bwaidx_t *idx = bwa_idx_load(fa, BWA_IDX_BWT); /* bwa_idx_load_bwt also restores the SA (bwa.c:244-260) */
   if (!idx) { fprintf(stderr, "index load failed\n"); return 1; }
   const bwt_t *bwt = idx->bwt;
   int64_t hdr[8] = {(int64_t)bwt->primary, (int64_t)bwt->L2[0], (int64_t)bwt->L2[1], (int64_t)bwt->L2[2],
                     (int64_t)bwt->L2[3],   (int64_t)bwt->L2[4], (int64_t)bwt->seq_len, (int64_t)bwt->bwt_size};
   wr(dir, "bwt_hdr", hdr, sizeof hdr);
   wr(dir, "bwt", bwt->bwt, 4 * (size_t)bwt->bwt_size);
+  /* the sampled suffix array and bwt_sa (bwt.c:86-96) on a spread of BWT
+     positions: every sa_intv-th one, its neighbours, primary, the ends */
+  int64_t sah[2] = {bwt->sa_intv, (int64_t)bwt->n_sa};
+  wr(dir, "sa_hdr", sah, sizeof sah);
+  wr(dir, "sa", bwt->sa, 8 * (size_t)bwt->n_sa);
+  {
+    kvec_t(uint64_t) qk, qv;
+    kv_init(qk); kv_init(qv);
+    const uint64_t n = bwt->seq_len + 1;
+    uint64_t s = 0x9e3779b97f4a7c15ULL;
+    for (int i = 0; i < 20000; ++i) {
+      s = s * 6364136223846793005ULL + 1442695040888963407ULL;
+      kv_push(uint64_t, qk, (s >> 11) % n);
+    }
+    const uint64_t fixed[] = {0, 1, 31, 32, 33, bwt->primary - 1, bwt->primary, bwt->primary + 1, n - 2, n - 1};
+    for (size_t i = 0; i < sizeof fixed / sizeof fixed[0]; ++i)
+      if (fixed[i] < n) kv_push(uint64_t, qk, fixed[i]);
+    for (size_t i = 0; i < qk.n; ++i) kv_push(uint64_t, qv, bwt_sa(bwt, qk.a[i]));
+    wr(dir, "sa_q", qk.a, 8 * qk.n);
+    wr(dir, "sa_v", qv.a, 8 * qv.n);
+    free(qk.a); free(qv.a);
+  }
 
   mem_opt_t *opt = mem_opt_init();
   int32_t ov[3] = {opt->min_seed_len, opt->split_width, opt->max_mem_intv};

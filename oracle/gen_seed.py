@@ -5,7 +5,9 @@ mem_collect_intv's control flow, gen_seed.c) into tests/golden/seed_*.npz.
     make -C oracle ref && python oracle/gen_seed.py
 
 seed_bwt.npz     the golden genome's BWT (bwa index of oracle/sim.h's genome,
-                 1 Mbp, seed 1234): header + interleaved occurrence words
+                 1 Mbp, seed 1234): header + interleaved occurrence words,
+                 the sampled suffix array, and the reference's bwt_sa on
+                 20 010 BWT positions
 seed_<set>.npz   reads (nt4, with N runs) and their intervals per read, in
                  the order mem_collect_intv leaves them (sorted by info)
 """
@@ -35,7 +37,9 @@ def main():
             subprocess.run([exe, d, str(seed), str(n), lm, "1000000", str(nf)], check=True)
             if not bwt_done:
                 np.savez_compressed(os.path.join(GOLD, "seed_bwt.npz"), hdr=rd(d, "bwt_hdr", np.int64),
-                                    words=rd(d, "bwt", np.uint32))
+                                    words=rd(d, "bwt", np.uint32), sa_hdr=rd(d, "sa_hdr", np.int64),
+                                    sa=rd(d, "sa", np.uint64), sa_q=rd(d, "sa_q", np.uint64),
+                                    sa_v=rd(d, "sa_v", np.uint64))
                 bwt_done = True
             np.savez_compressed(os.path.join(GOLD, f"seed_{name}.npz"), opt=rd(d, "opt", np.int32),
                                 split_factor=rd(d, "split_factor", np.float32), seq_off=rd(d, "seq_off", np.int64),

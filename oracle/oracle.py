@@ -50,6 +50,8 @@ def oracle_lib():
     lib.oracle_reg2aln_batch.restype = C.c_int
     lib.oracle_collect_intv.argtypes = [_VP, _VP, _VP, C.c_float, C.c_int, _VP, _VP, C.c_int]
     lib.oracle_collect_intv.restype = C.c_int
+    lib.oracle_bwt_sa.argtypes = [_VP, _VP, _VP, C.c_int, C.c_uint64]
+    lib.oracle_bwt_sa.restype = C.c_uint64
     return lib
 
 
@@ -189,3 +191,12 @@ def collect_intv(bwt_hdr, bwt_words, opt_i32, split_factor, seq_off, seq, cap: i
         counts.append(n)
         out.append(buf[:n].copy())
     return np.array(counts, np.int32), (np.concatenate(out) if out else np.zeros((0, 4), np.uint64))
+
+
+def bwt_sa(bwt_hdr, bwt_words, sa, sa_intv, ks):
+    """bwt_sa per BWT position with the restatement (oracle/seed.c)"""
+    hdr = np.ascontiguousarray(np.asarray(bwt_hdr, np.int64)[:7])
+    words = np.ascontiguousarray(bwt_words, np.uint32)
+    sa = np.ascontiguousarray(sa, np.uint64)
+    lib = oracle_lib()
+    return np.array([lib.oracle_bwt_sa(_ptr(hdr), _ptr(words), _ptr(sa), int(sa_intv), int(k)) for k in ks], np.uint64)

@@ -305,3 +305,29 @@ int oracle_collect_intv(const int64_t *hdr, const uint32_t *bwt_words, const int
   free(mem.a); free(mem1.a); free(va.a); free(vb.a);
   return n;
 }
+
+/* bwt_sa (bwt.c:86-96) with bwt_invPsi (bwt.c:53-59): walk the LF mapping
+   until a sampled row, counting steps.  hdr as for oracle_collect_intv. */
+uint64_t oracle_bwt_sa(const int64_t *hdr, const uint32_t *bwt_words, const uint64_t *sa, int sa_intv, uint64_t k)
+{
+  obwt_t b;
+  b.primary = (uint64_t)hdr[0];
+  for (int i = 0; i < 5; ++i) b.L2[i] = (uint64_t)hdr[1 + i];
+  b.seq_len = (uint64_t)hdr[6];
+  b.bwt = bwt_words;
+  uint64_t steps = 0;
+  const uint64_t mask = (uint64_t)sa_intv - 1;
+  while (k & mask) {
+    ++steps;
+    if (k == b.primary) {
+      k = 0;
+      continue;
+    }
+    const uint64_t x = k - (k > b.primary);
+    const int c = (int)(b.bwt[(x >> 7 << 4) + 8 + ((x & 127) >> 4)] >> ((~x & 15) << 1) & 3); /* bwt_B0 */
+    uint64_t cnt[4];
+    occ4(&b, k, cnt); /* bwt_occ(k, c), bwt.c:107-128; k == seq_len gives the column total */
+    k = b.L2[c] + cnt[c];
+  }
+  return steps + sa[k / (uint64_t)sa_intv];
+}

@@ -183,3 +183,9 @@ def load_seed_set(name):
     expected counts per read; expected intervals uint64[sum, 4] = x0, x1, x2, info)"""
     z = _npz("seed_" + name)
     return z["opt"], float(z["split_factor"][0]), z["seq_off"], z["seq"], z["intv_n"], z["intv"]
+
+
+def load_seed_sa():
+    """-> (sa_intv, sampled suffix array uint64, query BWT positions, the reference's bwt_sa of each)"""
+    z = _npz("seed_bwt")
+    return int(z["sa_hdr"][0]), z["sa"], z["sa_q"], z["sa_v"]

@@ -26,7 +26,8 @@ def eng():
     opt, *_ = G.load_chain_set("c1_default")
     e = Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
     hdr, words = G.load_seed_bwt()
-    e.set_bwt(hdr, words)
+    intv, sa, _, _ = G.load_seed_sa()
+    e.set_bwt(hdr, words, sa, intv)
     return e
 
 
@@ -109,3 +110,28 @@ def test_collect_intv_overflow_and_missing_index(eng):
                 refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
     with pytest.raises(BwaGpuError):
         e2.collect_intv(sub_off, sub)
+
+
+def test_bwt_sa_golden(eng):
+    """bwt_sa on the device equals the reference's at 20 010 BWT positions
+    (random, sample boundaries, primary and neighbours, seq_len)"""
+    intv, sa, q, want = G.load_seed_sa()
+    assert np.array_equal(eng.bwt_sa(q), want)
+    hdr, words = G.load_seed_bwt()
+    with pytest.raises(BwaGpuError):
+        eng.bwt_sa(np.array([hdr[6] + 1], np.uint64))  # past seq_len
+
+
+def test_bwt_sa_of_collected_intervals(eng):
+    """the seeds mem_chain would take from the golden intervals
+    (bwamem.c:282-288: up to max_occ positions per interval, stepped): the
+    device's rbeg values equal the oracle's"""
+    opt, sf, seq_off, seq, want_n, want = G.load_seed_set("c1")
+    ks = []
+    for x0, _, x2, _ in want[:4000]:
+        step = x2 // 500 if x2 > 500 else 1
+        ks.extend(int(x0) + k for k in range(0, int(min(x2, 500 * step)), int(step)))
+    ks = np.array(ks[:20000], np.uint64)
+    hdr, words = G.load_seed_bwt()
+    intv, sa, _, _ = G.load_seed_sa()
+    assert np.array_equal(eng.bwt_sa(ks), oracle.bwt_sa(hdr, words, sa, intv, ks))

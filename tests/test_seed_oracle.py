@@ -36,3 +36,12 @@ def test_oracle_collect_intv_matches_reference(name):
     ties = sum(len(want[off[r]:off[r + 1], 3]) - len(np.unique(want[off[r]:off[r + 1], 3])) for r in range(len(want_n)))
     assert ties > 0
     assert (seq == 4).any()
+
+
+def test_oracle_bwt_sa_matches_reference():
+    """bwt_sa (bwt.c:86-96) restated: 20 000 random BWT positions plus 0, the
+    sample boundaries, primary and its neighbours, seq_len"""
+    hdr, words = G.load_seed_bwt()
+    intv, sa, q, want = G.load_seed_sa()
+    assert intv == 32 and hdr[0] in q
+    assert np.array_equal(oracle.bwt_sa(hdr, words, sa, intv, q), want)
