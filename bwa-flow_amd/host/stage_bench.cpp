@@ -53,17 +53,17 @@ ChainsRecord make_record(const bwagpu_batch_t& b, bseq1_t* seqs, uint64_t start_
 extern "C" {
 
 // Runs reps x n_batches records through the stage on up to max_devices
-// devices.  times[0] = wall seconds from the first record in to the last
+// devices with per_device stage workers (bwagpu contexts) on each.  times[0] = wall seconds from the first record in to the last
 // record out, times[1..4] = the stage's phase totals (pack, submit, wait,
 // post; summed over workers), times[5] = records on the GPU, times[6] =
-// records the CPU fallback took, times[7] = devices used.  The regions of the
+// records the CPU fallback took, times[7] = stage workers (contexts) used.  The regions of the
 // LAST rep of batch k go to out_n[k][r] / out_regs[k] (compact, read order).
 // Returns 0, or the number of records whose chains were not freed.
 int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t* pac, int n_batches,
-                 const bwagpu_batch_t* batches, int reps, int max_devices, double* times, int32_t** out_n,
-                 bwagpu_alnreg_t** out_regs) {
-  if (!opt || !bns || !pac || n_batches <= 0 || !batches || reps <= 0 || !times) return -1;
-  GPUEnv env(*opt, *bns, pac, max_devices);
+                 const bwagpu_batch_t* batches, int reps, int max_devices, int per_device, double* times,
+                 int32_t** out_n, bwagpu_alnreg_t** out_regs) {
+  if (!opt || !bns || !pac || n_batches <= 0 || !batches || reps <= 0 || !times || per_device < 1) return -1;
+  GPUEnv env(*opt, *bns, pac, max_devices, 10000, per_device);
   const int n_dev = env.num_devices();
   if (n_dev == 0) return -2;
   // the reads of every batch (shared by its reps: the stage never frees seqs)
