@@ -83,3 +83,16 @@ def test_gpu_sam_stage_identical_to_bwa_mem(tmp_path, name, seed, pairs, lm, k):
     assert a == b, _first_diff(a, b)
     assert info["align2_calls"] > 0 and info["reg2aln_calls"] >= 2 * pairs * 0.9, info
     assert info["sam_passes"] >= 2, info
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,pairs,lm,k", CASES)
+def test_gpu_seeding_and_sam_stage_identical_to_bwa_mem(tmp_path, name, seed, pairs, lm, k):
+    """seeding's interval collection and SA lookups on the device as well
+    (bwagpu_collect_intv + bwagpu_bwt_sa, the chaining around them on the
+    host): chain2aln, rescue and CIGARs on the device, SAM byte-identical"""
+    a = _run("ref", str(tmp_path), name, seed, pairs, lm, k)
+    b = _run("gpuseed", str(tmp_path), name, seed, pairs, lm, k)
+    assert a == b, _first_diff(a, b)
+    assert _run.info["seed_device_s"] > 0 and _run.info["reg2aln_calls"] > 0

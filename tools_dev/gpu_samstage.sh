@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT/w
-timeout -k 10 120 oracle/_ref/sam_harness gpusam $OUT/w $OUT/w/gpusam.sam 7 10000 150 10000000 8 > $OUT/direct.log 2>&1 || { echo "direct run failed: $?" >> $OUT/direct.log; tail -20 $OUT/direct.log; exit 1; }
+timeout -k 10 120 oracle/_ref/sam_harness ${MODE:-gpusam} $OUT/w $OUT/w/gpusam.sam 7 10000 150 10000000 8 > $OUT/direct.log 2>&1 || { echo "direct run failed: $?" >> $OUT/direct.log; tail -20 $OUT/direct.log; exit 1; }
 tail -2 $OUT/direct.log
 timeout -k 10 120 oracle/_ref/sam_harness ref $OUT/w $OUT/w/ref.sam 7 10000 150 10000000 8 > $OUT/ref.log 2>&1 || { tail -5 $OUT/ref.log; exit 2; }
 tail -1 $OUT/ref.log
