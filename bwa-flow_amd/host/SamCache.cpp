@@ -51,11 +51,11 @@ struct R2Entry {
   int64_t cig_off, md_off;  // into the result pools once ready
 };
 
-}  // namespace
+// Calls are spread over kShards shards by hash, each with its own lock, so the
+// stage's worker threads (16 on the reference's pipeline) rarely contend.
+constexpr int kShards = 64;
 
-struct bwagpu_samcache {
-  bwagpu_ctx_t* ctx;
-  int32_t max_ops, max_md;
+struct Shard {
   std::mutex mu;
   std::vector<uint8_t> a2q, a2t, r2q;  // bases of the calls (nt4)
   std::vector<A2Entry> a2;
@@ -64,90 +64,121 @@ struct bwagpu_samcache {
   std::vector<int32_t> a2pend, r2pend;
   std::vector<uint32_t> cig;  // CIGAR ops of the ready reg2aln jobs
   std::vector<char> md;       // their MD strings, NUL-terminated
-  int64_t st[8] = {};
+  int64_t st[4] = {};         // align2 hits / misses, reg2aln hits / misses
+  void clear() {
+    a2q.clear(); a2t.clear(); r2q.clear(); a2.clear(); r2.clear(); a2map.clear(); r2map.clear();
+    a2pend.clear(); r2pend.clear(); cig.clear(); md.clear();
+  }
+};
+
+}  // namespace
+
+struct bwagpu_samcache {
+  bwagpu_ctx_t* ctx;
+  int32_t max_ops, max_md;
+  Shard sh[kShards];
+  int64_t st[4] = {};  // align2 computed, reg2aln computed, flushes, flush microseconds
 };
 
 namespace {
 
+inline Shard& shard_of(bwagpu_samcache_t* c, uint64_t h) { return c->sh[h >> 58]; }
+
 uint32_t* empty_block() { return (uint32_t*)calloc(1, sizeof(uint32_t)); }
 
+// every shard's queued ksw_align2 calls in one bwagpu_align2_batch (their
+// bases gathered into one query / target pool)
 int flush_align2(bwagpu_samcache_t* c) {
-  const int32_t n = (int32_t)c->a2pend.size();
+  std::vector<bwagpu_align2_task_t> tasks;
+  std::vector<std::pair<int, int32_t>> who;  // (shard, entry)
+  std::vector<uint8_t> qp, tp;
+  for (int s = 0; s < kShards; ++s)
+    for (int32_t id : c->sh[s].a2pend) {
+      const A2Entry& e = c->sh[s].a2[(size_t)id];
+      tasks.push_back(bwagpu_align2_task_t{(int64_t)qp.size(), (int64_t)tp.size(), e.qlen, e.tlen, e.xtra, 0});
+      qp.insert(qp.end(), c->sh[s].a2q.begin() + e.qoff, c->sh[s].a2q.begin() + e.qoff + e.qlen);
+      tp.insert(tp.end(), c->sh[s].a2t.begin() + e.toff, c->sh[s].a2t.begin() + e.toff + e.tlen);
+      who.emplace_back(s, id);
+    }
+  const int32_t n = (int32_t)tasks.size();
   if (n == 0) return 0;
-  std::vector<bwagpu_align2_task_t> tasks((size_t)n);
-  for (int32_t k = 0; k < n; ++k) {
-    const A2Entry& e = c->a2[(size_t)c->a2pend[(size_t)k]];
-    tasks[(size_t)k] = bwagpu_align2_task_t{e.qoff, e.toff, e.qlen, e.tlen, e.xtra, 0};
-  }
   std::vector<bwagpu_kswr_t> res((size_t)n);
-  const int rc = bwagpu_align2_batch(c->ctx, n, tasks.data(), c->a2q.data(), (int64_t)c->a2q.size(), c->a2t.data(),
-                                     (int64_t)c->a2t.size(), res.data());
+  const int rc = bwagpu_align2_batch(c->ctx, n, tasks.data(), qp.data(), (int64_t)qp.size(), tp.data(),
+                                     (int64_t)tp.size(), res.data());
   if (rc) return rc;
   for (int32_t k = 0; k < n; ++k) {
-    A2Entry& e = c->a2[(size_t)c->a2pend[(size_t)k]];
+    A2Entry& e = c->sh[who[(size_t)k].first].a2[(size_t)who[(size_t)k].second];
     e.r = res[(size_t)k];
     e.ready = true;
   }
-  c->st[4] += n;
-  c->a2pend.clear();
+  for (auto& sh : c->sh) sh.a2pend.clear();
+  c->st[0] += n;
   return 0;
 }
 
-// one bwagpu_reg2aln_batch over `ids`; jobs whose CIGAR or MD overflowed the
-// launch's capacity are returned in `over`
-int run_reg2aln(bwagpu_samcache_t* c, const std::vector<int32_t>& ids, int32_t max_ops, int32_t max_md,
-                std::vector<int32_t>& over) {
+// one bwagpu_reg2aln_batch over `ids` (shard, entry); jobs whose CIGAR or MD
+// overflowed the launch's capacity are returned in `over`
+int run_reg2aln(bwagpu_samcache_t* c, const std::vector<std::pair<int, int32_t>>& ids, int32_t max_ops,
+                int32_t max_md, std::vector<std::pair<int, int32_t>>& over) {
   const int32_t n = (int32_t)ids.size();
   if (n == 0) return 0;
   std::vector<bwagpu_reg2aln_task_t> tasks((size_t)n);
+  std::vector<uint8_t> qp;
   for (int32_t k = 0; k < n; ++k) {
-    const R2Entry& e = c->r2[(size_t)ids[(size_t)k]];
-    tasks[(size_t)k] = bwagpu_reg2aln_task_t{e.rb, e.re, e.qoff, e.l_seq, e.qb, e.qe, e.truesc, e.w, 0};
+    const Shard& sh = c->sh[ids[(size_t)k].first];
+    const R2Entry& e = sh.r2[(size_t)ids[(size_t)k].second];
+    tasks[(size_t)k] = bwagpu_reg2aln_task_t{e.rb, e.re, (int64_t)qp.size(), e.l_seq, e.qb, e.qe, e.truesc, e.w, 0};
+    qp.insert(qp.end(), sh.r2q.begin() + e.qoff, sh.r2q.begin() + e.qoff + e.l_seq);
   }
   std::vector<bwagpu_aln_t> out((size_t)n);
   std::vector<uint32_t> cg((size_t)n * (size_t)max_ops);
   std::vector<char> mdb((size_t)n * (size_t)max_md);
-  const int rc = bwagpu_reg2aln_batch(c->ctx, n, tasks.data(), c->r2q.data(), (int64_t)c->r2q.size(), max_ops, max_md,
+  const int rc = bwagpu_reg2aln_batch(c->ctx, n, tasks.data(), qp.data(), (int64_t)qp.size(), max_ops, max_md,
                                       out.data(), cg.data(), mdb.data());
   if (rc) return rc;
+  int64_t done = 0;
   for (int32_t k = 0; k < n; ++k) {
-    R2Entry& e = c->r2[(size_t)ids[(size_t)k]];
+    Shard& sh = c->sh[ids[(size_t)k].first];
+    R2Entry& e = sh.r2[(size_t)ids[(size_t)k].second];
     const bwagpu_aln_t& a = out[(size_t)k];
     if (a.status == BWAGPU_ALN_OVERFLOW) {
       over.push_back(ids[(size_t)k]);
       continue;
     }
     e.a = a;
-    e.cig_off = (int64_t)c->cig.size();
-    e.md_off = (int64_t)c->md.size();
+    e.cig_off = (int64_t)sh.cig.size();
+    e.md_off = (int64_t)sh.md.size();
     if (a.status == BWAGPU_ALN_OK) {
       const uint32_t* src = cg.data() + (size_t)k * max_ops;
-      c->cig.insert(c->cig.end(), src, src + a.n_cigar);
+      sh.cig.insert(sh.cig.end(), src, src + a.n_cigar);
       const char* m = mdb.data() + (size_t)k * max_md;
-      c->md.insert(c->md.end(), m, m + a.md_len);
+      sh.md.insert(sh.md.end(), m, m + a.md_len);
     }
-    c->md.push_back(0);
+    sh.md.push_back(0);
     e.ready = true;
+    ++done;
   }
-  c->st[5] += n - (int64_t)over.size();
+  c->st[1] += done;
   return 0;
 }
 
 int flush_reg2aln(bwagpu_samcache_t* c) {
-  if (c->r2pend.empty()) return 0;
-  std::vector<int32_t> over, over2;
-  int rc = run_reg2aln(c, c->r2pend, c->max_ops, c->max_md, over);
+  std::vector<std::pair<int, int32_t>> ids, over, over2;
+  for (int s = 0; s < kShards; ++s)
+    for (int32_t id : c->sh[s].r2pend) ids.emplace_back(s, id);
+  if (ids.empty()) return 0;
+  int rc = run_reg2aln(c, ids, c->max_ops, c->max_md, over);
   if (rc) return rc;
   if (!over.empty()) {
     // room for any alignment of the longest read among them: one op per base
     // and indel run, MD at most a few bytes per base
     int32_t lmax = 0;
-    for (int32_t id : over) lmax = std::max(lmax, c->r2[(size_t)id].l_seq);
+    for (auto& w : over) lmax = std::max(lmax, c->sh[w.first].r2[(size_t)w.second].l_seq);
     rc = run_reg2aln(c, over, 2 * lmax + 8, 8 * lmax + 64, over2);
     if (rc) return rc;
     if (!over2.empty()) return BWAGPU_E_RESULTS;
   }
-  c->r2pend.clear();
+  for (auto& sh : c->sh) sh.r2pend.clear();
   return 0;
 }
 
@@ -172,18 +203,10 @@ int bwagpu_samcache_destroy(bwagpu_samcache_t* c) {
 
 int bwagpu_samcache_clear(bwagpu_samcache_t* c) {
   if (!c) return BWAGPU_E_INVAL;
-  std::lock_guard<std::mutex> g(c->mu);
-  c->a2q.clear();
-  c->a2t.clear();
-  c->r2q.clear();
-  c->a2.clear();
-  c->r2.clear();
-  c->a2map.clear();
-  c->r2map.clear();
-  c->a2pend.clear();
-  c->r2pend.clear();
-  c->cig.clear();
-  c->md.clear();
+  for (auto& sh : c->sh) {
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.clear();
+  }
   return BWAGPU_OK;
 }
 
@@ -192,30 +215,31 @@ int bwagpu_samcache_align2(bwagpu_samcache_t* c, int32_t qlen, const uint8_t* qu
   if (!c || !out || qlen < 0 || tlen < 0 || (qlen && !query) || (tlen && !target)) return -BWAGPU_E_INVAL;
   uint64_t h = mix(mix(0x243f6a8885a308d3ULL, (uint64_t)(uint32_t)qlen << 32 | (uint32_t)tlen), (uint64_t)(uint32_t)xtra);
   h = hash_bytes(hash_bytes(h, query, qlen), target, tlen);
-  std::lock_guard<std::mutex> g(c->mu);
-  auto range = c->a2map.equal_range(h);
+  Shard& sh = shard_of(c, h);
+  std::lock_guard<std::mutex> g(sh.mu);
+  auto range = sh.a2map.equal_range(h);
   for (auto it = range.first; it != range.second; ++it) {
-    const A2Entry& e = c->a2[(size_t)it->second];
-    if (e.qlen != qlen || e.tlen != tlen || e.xtra != xtra || memcmp(c->a2q.data() + e.qoff, query, (size_t)qlen) ||
-        memcmp(c->a2t.data() + e.toff, target, (size_t)tlen))
+    const A2Entry& e = sh.a2[(size_t)it->second];
+    if (e.qlen != qlen || e.tlen != tlen || e.xtra != xtra || memcmp(sh.a2q.data() + e.qoff, query, (size_t)qlen) ||
+        memcmp(sh.a2t.data() + e.toff, target, (size_t)tlen))
       continue;
     if (e.ready) {
       *out = e.r;
-      ++c->st[0];
+      ++sh.st[0];
       return 0;
     }
     *out = bwagpu_kswr_t{0, -1, -1, -1, -1, -1, -1};
-    ++c->st[1];
+    ++sh.st[1];
     return 1;  // queued by an earlier miss of this pass
   }
-  A2Entry e{(int64_t)c->a2q.size(), (int64_t)c->a2t.size(), qlen, tlen, xtra, false, {}};
-  c->a2q.insert(c->a2q.end(), query, query + qlen);
-  c->a2t.insert(c->a2t.end(), target, target + tlen);
-  c->a2map.emplace(h, (int32_t)c->a2.size());
-  c->a2pend.push_back((int32_t)c->a2.size());
-  c->a2.push_back(e);
+  A2Entry e{(int64_t)sh.a2q.size(), (int64_t)sh.a2t.size(), qlen, tlen, xtra, false, {}};
+  sh.a2q.insert(sh.a2q.end(), query, query + qlen);
+  sh.a2t.insert(sh.a2t.end(), target, target + tlen);
+  sh.a2map.emplace(h, (int32_t)sh.a2.size());
+  sh.a2pend.push_back((int32_t)sh.a2.size());
+  sh.a2.push_back(e);
   *out = bwagpu_kswr_t{0, -1, -1, -1, -1, -1, -1};
-  ++c->st[1];
+  ++sh.st[1];
   return 1;
 }
 
@@ -226,60 +250,63 @@ int bwagpu_samcache_reg2aln(bwagpu_samcache_t* c, int32_t l_seq, const uint8_t* 
                    (uint64_t)(uint32_t)qb << 32 | (uint32_t)qe);
   h = mix(mix(h, (uint64_t)(uint32_t)truesc << 32 | (uint32_t)w), (uint64_t)(uint32_t)l_seq);
   h = hash_bytes(h, read, l_seq);
-  std::lock_guard<std::mutex> g(c->mu);
-  auto range = c->r2map.equal_range(h);
+  Shard& sh = shard_of(c, h);
+  std::lock_guard<std::mutex> g(sh.mu);
+  auto range = sh.r2map.equal_range(h);
+  bool queued = false;
   for (auto it = range.first; it != range.second; ++it) {
-    const R2Entry& e = c->r2[(size_t)it->second];
+    const R2Entry& e = sh.r2[(size_t)it->second];
     if (e.rb != rb || e.re != re || e.qb != qb || e.qe != qe || e.truesc != truesc || e.w != w || e.l_seq != l_seq ||
-        memcmp(c->r2q.data() + e.qoff, read, (size_t)l_seq))
+        memcmp(sh.r2q.data() + e.qoff, read, (size_t)l_seq))
       continue;
-    if (!e.ready) break;
+    if (!e.ready) {
+      queued = true;
+      break;
+    }
     *out = e.a;
     const int32_t nc = e.a.status == BWAGPU_ALN_OK ? e.a.n_cigar : 0;
     const int32_t ml = e.a.status == BWAGPU_ALN_OK ? e.a.md_len : 0;
     uint32_t* blk = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)nc + (size_t)ml + 1);
     if (!blk) return -BWAGPU_E_NOMEM;
-    memcpy(blk, c->cig.data() + e.cig_off, sizeof(uint32_t) * (size_t)nc);
-    memcpy((char*)(blk + nc), c->md.data() + e.md_off, (size_t)ml + 1);
+    memcpy(blk, sh.cig.data() + e.cig_off, sizeof(uint32_t) * (size_t)nc);
+    memcpy((char*)(blk + nc), sh.md.data() + e.md_off, (size_t)ml + 1);
     *cigar = blk;
-    ++c->st[2];
+    ++sh.st[2];
     return 0;
   }
-  bool queued = false;
-  for (auto it = range.first; it != range.second && !queued; ++it) {
-    const R2Entry& e = c->r2[(size_t)it->second];
-    queued = e.rb == rb && e.re == re && e.qb == qb && e.qe == qe && e.truesc == truesc && e.w == w &&
-             e.l_seq == l_seq && !memcmp(c->r2q.data() + e.qoff, read, (size_t)l_seq);
-  }
   if (!queued) {
-    R2Entry e{rb, re, (int64_t)c->r2q.size(), l_seq, qb, qe, truesc, w, false, {}, 0, 0};
-    c->r2q.insert(c->r2q.end(), read, read + l_seq);
-    c->r2map.emplace(h, (int32_t)c->r2.size());
-    c->r2pend.push_back((int32_t)c->r2.size());
-    c->r2.push_back(e);
+    R2Entry e{rb, re, (int64_t)sh.r2q.size(), l_seq, qb, qe, truesc, w, false, {}, 0, 0};
+    sh.r2q.insert(sh.r2q.end(), read, read + l_seq);
+    sh.r2map.emplace(h, (int32_t)sh.r2.size());
+    sh.r2pend.push_back((int32_t)sh.r2.size());
+    sh.r2.push_back(e);
   }
   memset(out, 0, sizeof *out);
   out->status = -1;
   *cigar = empty_block();
-  ++c->st[3];
+  ++sh.st[3];
   return *cigar ? 1 : -BWAGPU_E_NOMEM;
 }
 
 int64_t bwagpu_samcache_flush(bwagpu_samcache_t* c) {
   if (!c) return -BWAGPU_E_INVAL;
   const auto t0 = std::chrono::steady_clock::now();
-  const int64_t n = (int64_t)c->a2pend.size() + (int64_t)c->r2pend.size();
+  int64_t n = 0;
+  for (auto& sh : c->sh) n += (int64_t)sh.a2pend.size() + (int64_t)sh.r2pend.size();
   if (n == 0) return 0;
   int rc = flush_align2(c);
   if (!rc) rc = flush_reg2aln(c);
-  ++c->st[6];
-  c->st[7] += (int64_t)std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  ++c->st[2];
+  c->st[3] += (int64_t)std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
   return rc ? -(int64_t)rc : n;
 }
 
 int bwagpu_samcache_stats(const bwagpu_samcache_t* c, int64_t out[8]) {
   if (!c || !out) return BWAGPU_E_INVAL;
-  for (int i = 0; i < 8; ++i) out[i] = c->st[i];
+  for (int i = 0; i < 4; ++i) out[i] = 0;
+  for (const auto& sh : c->sh)
+    for (int i = 0; i < 4; ++i) out[i] += sh.st[i];
+  for (int i = 0; i < 4; ++i) out[4 + i] = c->st[i];
   return BWAGPU_OK;
 }
 

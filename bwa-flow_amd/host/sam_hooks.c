@@ -31,6 +31,7 @@
 
 #include "bntseq.h"
 #include "bwamem.h"
+#include "kstring.h"
 #include "ksw.h"
 #include "bwagpu_sam.h"
 
@@ -75,6 +76,32 @@ int bwagpu_sam_hooks_attach(bwagpu_samcache_t *c)
   }
   g_cache = c;
   return 0;
+}
+
+/* quiet passes: mem_aln2sam (bwamem.c:837-930) writes no SAM text — the
+   collect passes' text is discarded anyway, and formatting is most of a
+   pass's CPU time.  The string is still allocated and terminated, since
+   mem_sam_pe strdup's it (bwamem_pair.c:359). */
+static volatile int g_quiet;
+void bwagpu_sam_hooks_quiet(int quiet) { g_quiet = quiet; }
+
+typedef void (*aln2sam_fn)(const mem_opt_t *, const bntseq_t *, kstring_t *, bseq1_t *, int, const mem_aln_t *, int,
+                           const mem_aln_t *);
+static aln2sam_fn real_aln2sam;
+
+void mem_aln2sam(const mem_opt_t *opt, const bntseq_t *bns, kstring_t *str, bseq1_t *s, int n, const mem_aln_t *list,
+                 int which, const mem_aln_t *m)
+{
+  if (g_quiet && g_cache) {
+    if (!str->s) {
+      str->m = 16;
+      str->s = (char *)malloc(str->m);
+    }
+    str->s[str->l] = 0;
+    return;
+  }
+  if (!real_aln2sam) real_aln2sam = (aln2sam_fn)dlsym(RTLD_NEXT, "mem_aln2sam");
+  real_aln2sam(opt, bns, str, s, n, list, which, m);
 }
 
 /* jobs the device flagged since the last call (BWAGPU_ALN_NO_CIGAR: the

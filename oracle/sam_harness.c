@@ -63,6 +63,7 @@
 
 int bwagpu_sam_hooks_attach(bwagpu_samcache_t *c); /* bwa-flow_amd/host/sam_hooks.c */
 int bwagpu_sam_hooks_errors(void);
+void bwagpu_sam_hooks_quiet(int quiet);
 
 typedef struct {
   int64_t rbeg;
@@ -466,7 +467,11 @@ static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t 
   mem_alnreg_v *keep = w->regs, *cp = (mem_alnreg_v *)calloc(n, sizeof(mem_alnreg_v));
   int64_t st[8];
   bwagpu_sam_hooks_attach(cache);
-  for (;;) {
+  /* the first two passes only collect calls (rescues, then CIGARs of the final
+     regions): no SAM text; a text pass with misses is redone after a flush */
+  for (int pass = 0;; ++pass) {
+    const int quiet = pass < 2;
+    bwagpu_sam_hooks_quiet(quiet);
     G.sc_stats(cache, st);
     const int64_t miss0 = st[1] + st[3];
     for (int i = 0; i < n; ++i) {
@@ -479,13 +484,15 @@ static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t 
     ++*n_passes;
     G.sc_stats(cache, st);
     if (bwagpu_sam_hooks_errors()) { fprintf(stderr, "sam_hooks: the device flagged a CIGAR job\n"); exit(4); }
-    if (st[1] + st[3] == miss0) break;
+    if (st[1] + st[3] == miss0 && !quiet) break;
     for (int i = 0; i < n; ++i) { free(w->seqs[i].sam); w->seqs[i].sam = 0; }
+    if (st[1] + st[3] == miss0) { pass = 1; continue; } /* nothing to flush: straight to a text pass */
     const double t0 = realtime();
     const int64_t rc = G.sc_flush(cache);
     *t_flush += realtime() - t0;
     if (rc <= 0) { fprintf(stderr, "bwagpu_samcache_flush: %ld\n", (long)rc); exit(3); }
   }
+  bwagpu_sam_hooks_quiet(0);
   bwagpu_sam_hooks_attach(0);
   G.sc_clear(cache);
   for (int i = 0; i < n; ++i) free(keep[i].a);
