@@ -1,8 +1,8 @@
 """Seeding benchmark: bwagpu_collect_intv (mem_collect_intv on the device) over
 the reference-seeded C2 batch's reads (tests/golden/c2_refseed.npz, 66,668 x
 150 bp) against the chr21-sized golden genome's FM-index
-(bench_data/c2_bwt_*.npy, built by the reference's bwa_idx_build:
-`oracle/_ref/gen_seed /tmp/x 1 0 150 46709983 0`, then saved as .npy).
+(bench_data/c2_bwt.npz, built by the reference's bwa_idx_build:
+`oracle/_ref/gen_seed /tmp/x 1 0 150 46709983 0`, then saved with np.savez_compressed).
 Parity: a sample of reads checked against the oracle (oracle/seed.c).
 CPU: the oracle restatement, one thread, on a bounded sample.
 Prints one JSON line."""
@@ -34,8 +34,8 @@ def main():
     ap.add_argument("--budget", type=int, default=-1, help="bwt_extend calls per read on one lane (-1: library default)")
     ap.add_argument("--mult", type=str, default="", help="comma list: also time k copies of the batch in one call")
     a = ap.parse_args()
-    hdr = np.load(os.path.join(ROOT, "bench_data", "c2_bwt_hdr.npy"))
-    words = np.load(os.path.join(ROOT, "bench_data", "c2_bwt_words.npy"))
+    z = np.load(os.path.join(ROOT, "bench_data", "c2_bwt.npz"))
+    hdr, words = z["hdr"], z["words"]
     _, _, batches = load_fixture(with_ref=False)
     b = batches[0].batch
     refd = G.load_ref()
