@@ -1400,8 +1400,17 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
     if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
     if (l > BWAGPU_MAX_SEED_READ) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_SEED_READ");
   }
-  for (int64_t i = 0; i < bases; ++i)
-    if (seq[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
+  {  // every base is nt4 (0..4): eight bytes at a time, (b & 0x7f) + 0x7b carries into bit 7 iff b > 4
+    int64_t i = 0;
+    uint64_t bad = 0;
+    for (; i + 8 <= bases; i += 8) {
+      uint64_t w;
+      memcpy(&w, seq + i, 8);
+      bad |= (((w & 0x7f7f7f7f7f7f7f7fULL) + 0x7b7b7b7b7b7b7b7bULL) | w) & 0x8080808080808080ULL;
+    }
+    for (; i < bases; ++i) bad |= seq[i] > 4;
+    if (bad) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
+  }
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   hipStream_t st = ctx->slot[0].stream;
   HIPC(ctx->sd_off.ensure(sizeof(int64_t) * ((size_t)n_reads + 1)), "hipMalloc");

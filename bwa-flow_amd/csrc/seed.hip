@@ -71,11 +71,37 @@ __device__ __forceinline__ void extend(const DevBwt& b, const Ivl& ik, Ivl ok[4]
   ok[0].x[is_back] = ok[1].x[is_back] + ok[1].x[2];
 }
 
+// bwt_extend's interval for one base c only (ok[c] of bwt.c:262-276).  The
+// callers index ok[] with a per-lane base, which would put the 4-entry array
+// in scratch memory; here the entry is picked with selects instead.
+__device__ __forceinline__ Ivl extend1(const DevBwt& b, const Ivl& ik, int c, int is_back) {
+  uint64_t tk[4], tl[4];
+  const int nb = !is_back;
+  occ4(b, ik.x[nb] - 1, tk);
+  occ4(b, ik.x[nb] - 1 + ik.x[2], tl);
+  const uint64_t s0 = tl[0] - tk[0], s1 = tl[1] - tk[1], s2 = tl[2] - tk[2], s3 = tl[3] - tk[3];
+  const uint64_t tkc = c == 0 ? tk[0] : c == 1 ? tk[1] : c == 2 ? tk[2] : tk[3];
+  const uint64_t l2c = c == 0 ? b.L2[0] : c == 1 ? b.L2[1] : c == 2 ? b.L2[2] : b.L2[3];
+  const uint64_t sc = c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3;
+  // ok[c].x[is_back] = ok[3].x[is_back] + sizes of the bases above c (bwt.c:272-275)
+  const uint64_t above = (c < 3 ? s3 : 0) + (c < 2 ? s2 : 0) + (c < 1 ? s1 : 0);
+  Ivl o;
+  o.x[nb] = l2c + 1 + tkc;
+  o.x[2] = sc;
+  o.x[is_back] = ik.x[is_back] + (ik.x[nb] <= b.primary && ik.x[nb] + ik.x[2] - 1 >= b.primary) + above;
+  o.info = 0;
+  return o;
+}
+
+__device__ __forceinline__ uint64_t l2_at(const DevBwt& b, int i) {  // L2[i] by selects, not a scratch copy
+  return i == 0 ? b.L2[0] : i == 1 ? b.L2[1] : i == 2 ? b.L2[2] : i == 3 ? b.L2[3] : b.L2[4];
+}
+
 __device__ __forceinline__ Ivl set_intv(const DevBwt& b, int c) {  // bwt.h:80
   Ivl ik;
-  ik.x[0] = b.L2[c] + 1;
-  ik.x[2] = b.L2[c + 1] - b.L2[c];
-  ik.x[1] = b.L2[3 - c] + 1;
+  ik.x[0] = l2_at(b, c) + 1;
+  ik.x[2] = l2_at(b, c + 1) - l2_at(b, c);
+  ik.x[1] = l2_at(b, 3 - c) + 1;
   ik.info = 0;
   return ik;
 }
@@ -105,63 +131,65 @@ __device__ __forceinline__ void reverse(List& v) {
 }
 
 // bwt_smem1a with max_intv = 0 (bwt.c:289-356)
-__device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, List& mem, List* prev,
-                     List* curr, Budget& bg) {
-  Ivl ok[4];
+__device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, List& mem, List& prev,
+                     List& curr, Budget& bg) {
   int i;
   mem.n = 0;
   if (q[x] > 3) return x + 1;
   if (min_intv < 1) min_intv = 1;
   Ivl ik = set_intv(b, q[x]);
   ik.info = (uint64_t)(x + 1);
-  curr->n = 0;
+  curr.n = 0;
   for (i = x + 1; i < len; ++i) {  // forward
     const int qi = q[i];
     if (qi < 4) {
       const int c = 3 - qi;
       if (bg.spend()) return -1;
-      extend(b, ik, ok, 0);
-      if (ok[c].x[2] != ik.x[2]) {
-        curr->push(ik);
-        if (ok[c].x[2] < (uint64_t)min_intv) break;
+      const Ivl okc = extend1(b, ik, c, 0);
+      if (okc.x[2] != ik.x[2]) {
+        curr.push(ik);
+        if (okc.x[2] < (uint64_t)min_intv) break;
       }
-      ik = ok[c];
+      ik = okc;
       ik.info = (uint64_t)(i + 1);
     } else {
-      curr->push(ik);
+      curr.push(ik);
       break;
     }
   }
-  if (i == len) curr->push(ik);
-  reverse(*curr);  // longest matches first
-  const int ret = (int)curr->a[0].info;
-  List* t = curr;
-  curr = prev;
-  prev = t;
+  if (i == len) curr.push(ik);
+  reverse(curr);  // longest matches first
+  const int ret = (int)curr.a[0].info;
+  {  // the two lists trade places (values, not pointers: no addressable locals)
+    const List t = curr;
+    curr = prev;
+    prev = t;
+  }
   for (i = x - 1; i >= -1; --i) {  // backward
     const int c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
-    curr->n = 0;
-    for (int j = 0; j < prev->n; ++j) {
-      const Ivl p = prev->a[j];
+    curr.n = 0;
+    for (int j = 0; j < prev.n; ++j) {
+      const Ivl p = prev.a[j];
+      Ivl okc{};
       if (c >= 0) {
         if (bg.spend()) return -1;
-        extend(b, p, ok, 1);
+        okc = extend1(b, p, c, 1);
       }
-      if (c < 0 || ok[c].x[2] < (uint64_t)min_intv) {
-        if (curr->n == 0 && (mem.n == 0 || (uint64_t)(i + 1) < mem.a[mem.n - 1].info >> 32)) {
+      if (c < 0 || okc.x[2] < (uint64_t)min_intv) {
+        if (curr.n == 0 && (mem.n == 0 || (uint64_t)(i + 1) < mem.a[mem.n - 1].info >> 32)) {
           Ivl h = p;
           h.info |= (uint64_t)(i + 1) << 32;
           mem.push(h);
         }
-      } else if (curr->n == 0 || ok[c].x[2] != curr->a[curr->n - 1].x[2]) {
-        ok[c].info = p.info;
-        curr->push(ok[c]);
+      } else if (curr.n == 0 || okc.x[2] != curr.a[curr.n - 1].x[2]) {
+        okc.info = p.info;
+        curr.push(okc);
       }
     }
-    if (curr->n == 0) break;
-    t = curr;
+    if (curr.n == 0) break;
+    const List t2 = curr;
     curr = prev;
-    prev = t;
+    prev = t2;
   }
   reverse(mem);  // by start
   return ret;
@@ -171,7 +199,6 @@ __device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_
 template <class B>
 __device__ int seed_strategy1(const DevBwt& b, int len, const uint8_t* q, int x, int min_len, int max_intv, Ivl& m,
                               B& bg) {
-  Ivl ok[4];
   m.x[0] = m.x[1] = m.x[2] = m.info = 0;
   if (q[x] > 3) return x + 1;
   Ivl ik = set_intv(b, q[x]);
@@ -180,13 +207,13 @@ __device__ int seed_strategy1(const DevBwt& b, int len, const uint8_t* q, int x,
     if (qi < 4) {
       const int c = 3 - qi;
       if (bg.spend()) return -1;
-      extend(b, ik, ok, 0);
-      if (ok[c].x[2] < (uint64_t)max_intv && i - x >= min_len) {
-        m = ok[c];
+      const Ivl okc = extend1(b, ik, c, 0);
+      if (okc.x[2] < (uint64_t)max_intv && i - x >= min_len) {
+        m = okc;
         m.info = (uint64_t)x << 32 | (uint64_t)(i + 1);
         return i + 1;
       }
-      ik = ok[c];
+      ik = okc;
     } else {
       return i + 1;
     }
@@ -296,7 +323,7 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
   int x = 0;
   while (x < len) {  // SMEMs
     if (q[x] < 4) {
-      x = smem1(b, len, q, x, 1, mem1, &la, &lb, bg);
+      x = smem1(b, len, q, x, 1, mem1, la, lb, bg);
       if (x < 0) return give_up();
       for (int i = 0; i < mem1.n; ++i)
         if ((int)((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32)) >= a.min_seed_len) mem.push(mem1.a[i]);
@@ -309,7 +336,7 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
     const Ivl p = mem.a[k];
     const int start = (int)(p.info >> 32), end = (int)(int32_t)p.info;
     if (end - start < a.split_len || p.x[2] > (uint64_t)a.split_width) continue;
-    if (smem1(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, &la, &lb, bg) < 0) return give_up();
+    if (smem1(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, la, lb, bg) < 0) return give_up();
     for (int i = 0; i < mem1.n; ++i)
       if ((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32) >= (uint32_t)a.min_seed_len) mem.push(mem1.a[i]);
   }
@@ -378,56 +405,54 @@ __device__ __forceinline__ uint64_t bperm64(int src_lane, uint64_t v) {
 }
 
 // bwt_smem1a with max_intv = 0 (bwt.c:289-356), one wave
-__device__ int smem1_wave(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, WList& mem, WList* prev,
-                          WList* curr, int lane) {
+__device__ int smem1_wave(const DevBwt& b, int len, const uint8_t* q, int x, int min_intv, WList& mem, WList& prev,
+                          WList& curr, int lane) {
   const bool l0 = lane == 0;
-  Ivl ok[4];
   int i;
   mem.n = 0;
   if (q[x] > 3) return x + 1;
   if (min_intv < 1) min_intv = 1;
   Ivl ik = set_intv(b, q[x]);
   ik.info = (uint64_t)(x + 1);
-  curr->n = 0;
+  curr.n = 0;
   for (i = x + 1; i < len; ++i) {  // forward: one interval, every lane alike
     const int qi = q[i];
     if (qi < 4) {
       const int c = 3 - qi;
-      extend(b, ik, ok, 0);
-      if (ok[c].x[2] != ik.x[2]) {
-        curr->push(ik, l0);
-        if (ok[c].x[2] < (uint64_t)min_intv) break;
+      const Ivl okc = extend1(b, ik, c, 0);
+      if (okc.x[2] != ik.x[2]) {
+        curr.push(ik, l0);
+        if (okc.x[2] < (uint64_t)min_intv) break;
       }
-      ik = ok[c];
+      ik = okc;
       ik.info = (uint64_t)(i + 1);
     } else {
-      curr->push(ik, l0);
+      curr.push(ik, l0);
       break;
     }
   }
-  if (i == len) curr->push(ik, l0);
+  if (i == len) curr.push(ik, l0);
   publish();
-  wreverse(*curr, lane);
-  const int ret = (int)curr->a[0].info;
-  WList* t = curr;
-  curr = prev;
-  prev = t;
+  wreverse(curr, lane);
+  const int ret = (int)curr.a[0].info;
+  {
+    const WList t = curr;
+    curr = prev;
+    prev = t;
+  }
   const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
   for (i = x - 1; i >= -1; --i) {  // backward: lane j extends prev[j]
     const int c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
-    curr->n = 0;
+    curr.n = 0;
     bool have_last = false;  // a kept (pushed) entry exists in curr
     uint64_t last_sz = 0;
-    for (int j0 = 0; j0 < prev->n; j0 += 64) {
+    for (int j0 = 0; j0 < prev.n; j0 += 64) {
       const int j = j0 + lane;
-      const bool valid = j < prev->n;
+      const bool valid = j < prev.n;
       Ivl p{};
-      if (valid) p = prev->a[j];
+      if (valid) p = prev.a[j];
       Ivl okc{};
-      if (valid && c >= 0) {
-        extend(b, p, ok, 1);
-        okc = ok[c];
-      }
+      if (valid && c >= 0) okc = extend1(b, p, c, 1);
       const bool A = valid && (c < 0 || okc.x[2] < (uint64_t)min_intv);
       const bool nA = valid && !A;
       // bwt.c:333-338: only entry 0 can reach mem (curr is empty before the
@@ -435,7 +460,7 @@ __device__ int smem1_wave(const DevBwt& b, int len, const uint8_t* q, int x, int
       if (j0 == 0) {
         const bool a0 = __builtin_amdgcn_readfirstlane((int)A) != 0;
         if (a0) {
-          const Ivl p0 = prev->a[0];
+          const Ivl p0 = prev.a[0];
           if (mem.n == 0 || (uint64_t)(i + 1) < mem.a[mem.n - 1].info >> 32) {
             Ivl h = p0;
             h.info |= (uint64_t)(i + 1) << 32;
@@ -455,9 +480,9 @@ __device__ int smem1_wave(const DevBwt& b, int len, const uint8_t* q, int x, int
       if (keep) {
         Ivl v = okc;
         v.info = p.info;
-        curr->a[curr->n + (int)__builtin_popcountll(keep_m & below)] = v;
+        curr.a[curr.n + (int)__builtin_popcountll(keep_m & below)] = v;
       }
-      curr->n += (int)__builtin_popcountll(keep_m);
+      curr.n += (int)__builtin_popcountll(keep_m);
       if (nA_m) {
         const int hl = 63 - (int)__builtin_clzll(nA_m);
         last_sz = bperm64(hl, okc.x[2]);
@@ -465,10 +490,10 @@ __device__ int smem1_wave(const DevBwt& b, int len, const uint8_t* q, int x, int
       }
       publish();
     }
-    if (curr->n == 0) break;
-    t = curr;
+    if (curr.n == 0) break;
+    const WList t2 = curr;
     curr = prev;
-    prev = t;
+    prev = t2;
   }
   wreverse(mem, lane);
   return ret;
@@ -491,7 +516,7 @@ __global__ void __launch_bounds__(256) collect_intv_wave_kernel(DevBwt b, SeedAr
     int x = 0;
     while (x < len) {  // SMEMs
       if (q[x] < 4) {
-        x = smem1_wave(b, len, q, x, 1, mem1, &la, &lb, lane);
+        x = smem1_wave(b, len, q, x, 1, mem1, la, lb, lane);
         for (int i = 0; i < mem1.n; ++i) {
           const Ivl v = mem1.a[i];
           if ((int)((uint32_t)v.info - (uint32_t)(v.info >> 32)) >= a.min_seed_len) mem.push(v, l0);
@@ -506,7 +531,7 @@ __global__ void __launch_bounds__(256) collect_intv_wave_kernel(DevBwt b, SeedAr
       const Ivl p = mem.a[k];
       const int start = (int)(p.info >> 32), end = (int)(int32_t)p.info;
       if (end - start < a.split_len || p.x[2] > (uint64_t)a.split_width) continue;
-      smem1_wave(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, &la, &lb, lane);
+      smem1_wave(b, len, q, (start + end) >> 1, (int)(p.x[2] + 1), mem1, la, lb, lane);
       for (int i = 0; i < mem1.n; ++i) {
         const Ivl v = mem1.a[i];
         if ((uint32_t)v.info - (uint32_t)(v.info >> 32) >= (uint32_t)a.min_seed_len) mem.push(v, l0);

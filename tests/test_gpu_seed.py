@@ -105,6 +105,11 @@ def test_collect_intv_overflow_and_missing_index(eng):
     with pytest.raises(BwaGpuError) as ei:
         eng.collect_intv(sub_off, sub, max_per_read=int(want_n[r]) - 1)
     assert ei.value.code == 6  # BWAGPU_E_UNSUPPORTED
+    bad = sub.copy()
+    bad[len(bad) // 2] = 5  # not an nt4 base
+    with pytest.raises(BwaGpuError) as ei:
+        eng.collect_intv(sub_off, bad)
+    assert ei.value.code == 1  # BWAGPU_E_INVAL
     refd = G.load_ref()
     e2 = Engine(0, {k: v for k, v in G.load_chain_set("c1_default")[0].items()}, refd["l_pac"],
                 refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
