@@ -1433,10 +1433,12 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   a.split_width = opt->split_width;
   a.max_mem_intv = opt->max_mem_intv;
   a.split_len = (int)(opt->min_seed_len * opt->split_factor + .499);  // bwamem.c:124
-  HIPC(ctx->sd_heavy.ensure(sizeof(int32_t) * ((size_t)n_reads + 1)), "hipMalloc");
+  HIPC(ctx->sd_heavy.ensure(sizeof(int32_t) * (3 * (size_t)n_reads + 1)), "hipMalloc");
   a.budget = ctx->seed_budget;
   a.heavy = ctx->sd_heavy.as<int32_t>() + 1;
   a.n_heavy = ctx->sd_heavy.as<int32_t>();
+  a.flags = a.heavy + n_reads;
+  a.p3_n = a.flags + n_reads;
   HIPC(launch_collect_intv(ctx->bwt, a, st), "collect_intv launch");
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");

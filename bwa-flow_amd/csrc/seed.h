@@ -26,15 +26,17 @@ struct SeedArgs {
   int32_t max_per_read;
   bwagpu_intv_t* out;       // n_reads * max_per_read
   int32_t* out_n;           // n_reads
-  bwagpu_intv_t* scratch;   // read r: 3 lists of len_r + 2 at 3 * (seq_off[r] + 2r)
+  bwagpu_intv_t* scratch;   // read r: 4 lists of len_r + 2 at 4 * (seq_off[r] + 2r)
   int32_t min_seed_len, split_width, max_mem_intv, split_len;
   int32_t budget;     // bwt_extend calls tier 1 spends on one read before handing it to tier 2
   int32_t* heavy;     // n_reads: the reads handed over
   int32_t* n_heavy;   // their number
+  int32_t* flags;     // n_reads: 1 = handed to tier 2
+  int32_t* p3_n;      // n_reads: LAST-like intervals in the read's fourth list
 };
 
-// lists a read needs in the scratch buffer: 3 * (bases + 2 * reads) entries
-inline int64_t seed_scratch_entries(int64_t bases, int32_t n_reads) { return 3 * (bases + 2 * (int64_t)n_reads); }
+// lists a read needs in the scratch buffer: 4 * (bases + 2 * reads) entries
+inline int64_t seed_scratch_entries(int64_t bases, int32_t n_reads) { return 4 * (bases + 2 * (int64_t)n_reads); }
 
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st);
 // bwt_sa for n positions

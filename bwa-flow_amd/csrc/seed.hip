@@ -305,21 +305,45 @@ __device__ void intro_sort(Ivl* a, int n) {
   }
 }
 
-// ---- tier 1: one lane per read, within an extension budget
+// ---- tier 1: two lanes per read, within an extension budget each
+// The LAST-like pass does not read the first two passes' results, so it runs
+// on a lane of its own (threads [n, 2n)) beside the SMEM + re-seeding lane
+// (threads [0, n)); tier1_merge_kernel appends its intervals after theirs —
+// mem_collect_intv's push order — and sorts.  A lane out of budget hands the
+// whole read to tier 2 (the first of the two to give up lists it).
 __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a) {
-  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (r >= a.n_reads) return;
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= 2 * a.n_reads) return;
+  const bool last_like = t >= a.n_reads;
+  const int r = last_like ? t - a.n_reads : t;
   const int64_t q0 = a.seq_off[r];
   const int len = (int)(a.seq_off[r + 1] - q0);
   const uint8_t* q = a.seq + q0;
-  Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 3 * (q0 + 2 * (int64_t)r);
-  List la{base, 0, len + 2}, lb{base + (len + 2), 0, len + 2}, mem1{base + 2 * (len + 2), 0, len + 2};
-  List mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, 0, a.max_per_read};
+  Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 4 * (q0 + 2 * (int64_t)r);
   Budget bg{a.budget};
   auto give_up = [&]() {  // tier 2 takes the read
-    a.out_n[r] = 0;
-    a.heavy[atomicAdd(a.n_heavy, 1)] = r;
+    if (atomicCAS(a.flags + r, 0, 1) == 0) a.heavy[atomicAdd(a.n_heavy, 1)] = r;
   };
+  if (last_like) {  // bwamem.c:150-165 into the read's fourth list
+    List p3{base + 3 * (len + 2), 0, len + 2};
+    if (a.max_mem_intv > 0) {
+      int x = 0;
+      while (x < len) {
+        if (q[x] < 4) {
+          Ivl m;
+          x = seed_strategy1(b, len, q, x, a.min_seed_len, a.max_mem_intv, m, bg);
+          if (x < 0) return give_up();
+          if (m.x[2] > 0) p3.push(m);
+        } else {
+          ++x;
+        }
+      }
+    }
+    a.p3_n[r] = p3.n;
+    return;
+  }
+  List la{base, 0, len + 2}, lb{base + (len + 2), 0, len + 2}, mem1{base + 2 * (len + 2), 0, len + 2};
+  List mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, 0, a.max_per_read};
   int x = 0;
   while (x < len) {  // SMEMs
     if (q[x] < 4) {
@@ -340,19 +364,19 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
     for (int i = 0; i < mem1.n; ++i)
       if ((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32) >= (uint32_t)a.min_seed_len) mem.push(mem1.a[i]);
   }
-  if (a.max_mem_intv > 0) {  // LAST-like
-    x = 0;
-    while (x < len) {
-      if (q[x] < 4) {
-        Ivl m;
-        x = seed_strategy1(b, len, q, x, a.min_seed_len, a.max_mem_intv, m, bg);
-        if (x < 0) return give_up();
-        if (m.x[2] > 0) mem.push(m);
-      } else {
-        ++x;
-      }
-    }
-  }
+  a.out_n[r] = mem.n;  // passes 1-2; the merge adds pass 3 and sorts
+}
+
+// tier 1's two halves of a read joined (bwamem.c:166: the sort of all)
+__global__ void __launch_bounds__(256) tier1_merge_kernel(SeedArgs a) {
+  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r >= a.n_reads || a.flags[r]) return;
+  const int64_t q0 = a.seq_off[r];
+  const int len = (int)(a.seq_off[r + 1] - q0);
+  const Ivl* p3 = reinterpret_cast<const Ivl*>(a.scratch) + 4 * (q0 + 2 * (int64_t)r) + 3 * (len + 2);
+  List mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, a.out_n[r], a.max_per_read};
+  const int n3 = a.p3_n[r];
+  for (int i = 0; i < n3; ++i) mem.push(p3[i]);
   if (mem.n <= mem.cap) {
     intro_sort(mem.a, mem.n);
     a.out_n[r] = mem.n;
@@ -510,7 +534,7 @@ __global__ void __launch_bounds__(256) collect_intv_wave_kernel(DevBwt b, SeedAr
     const int64_t q0 = a.seq_off[r];
     const int len = (int)(a.seq_off[r + 1] - q0);
     const uint8_t* q = a.seq + q0;
-    Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 3 * (q0 + 2 * (int64_t)r);
+    Ivl* base = reinterpret_cast<Ivl*>(a.scratch) + 4 * (q0 + 2 * (int64_t)r);
     WList la{base, 0, len + 2}, lb{base + (len + 2), 0, len + 2}, mem1{base + 2 * (len + 2), 0, len + 2};
     WList mem{reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read, 0, a.max_per_read};
     int x = 0;
@@ -616,8 +640,11 @@ hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st) {
   if (a.n_reads <= 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(a.n_heavy, 0, sizeof(int32_t), st);
+  if (e == hipSuccess) e = hipMemsetAsync(a.flags, 0, sizeof(int32_t) * (size_t)a.n_reads, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(collect_intv_kernel, dim3((a.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  hipLaunchKernelGGL(collect_intv_kernel, dim3((2 * a.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(tier1_merge_kernel, dim3((a.n_reads + 255) / 256), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the reads tier 1 gave up on, one wave each (the count is read on the device)
   const int waves = a.n_reads < 4096 ? a.n_reads : 4096;
