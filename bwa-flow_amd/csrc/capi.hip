@@ -150,6 +150,8 @@ struct bwagpu_ctx {
   DevBwt bwt{};
   bool has_bwt = false;
   DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy;
+  // the FPGA wire format (bwagpu_sw_stream)
+  DevBuf st_buf, st_start, st_q, st_tasks, st_lists, st_seen, st_ctr, st_out;
   // bwt_extend calls tier 1 spends on a read before tier 2 (one wave per read)
   // takes it: ~p90 of the C2 batch's per-read counts (mean 666, p90 975)
   int seed_budget = 1024;
@@ -1463,5 +1465,81 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
 extern "C" int bwagpu_debug_seed_budget(bwagpu_ctx_t* ctx, int32_t budget) {
   if (!ctx || budget < 0) return BWAGPU_E_INVAL;
   ctx->seed_budget = budget;
+  return BWAGPU_OK;
+}
+
+// The FPGA back end's own job (sw_top, xlnx/XCLAgent.cpp:89-106) on its wire
+// format: the host walks the record chain (one load per read record — the
+// "end" words of packReadData, FPGAPipeline.cpp:258,336) and checks lengths;
+// the device decodes and checks everything else (stream_decode_kernel) and
+// extends every task (stream_ext_kernel).  Device-found problems come back as
+// BWAGPU_E_RESULTS, the fpgaResultsError of processOutput's checks
+// (FPGAPipeline.cpp:38-74).
+extern "C" int bwagpu_sw_stream(bwagpu_ctx_t* ctx, const int32_t* i_buf, int64_t i_words, int16_t* o_buf,
+                                int32_t o_cap_tasks, int32_t* o_tasks) {
+  if (!ctx || !o_tasks || i_words < 0 || o_cap_tasks < 0 || (i_words && !i_buf) || (o_cap_tasks && !o_buf))
+    return BWAGPU_E_INVAL;
+  *o_tasks = 0;
+  if (i_words == 0) return BWAGPU_OK;
+  std::vector<int64_t> starts;
+  int lq_max = 1;
+  for (int64_t p = 0; p < i_words;) {
+    const int64_t end = i_buf[p];
+    if (end <= p + 2 || end > i_words) return fail(ctx, BWAGPU_E_INVAL, "stream: a record's end word is out of range");
+    const int lq = i_buf[p + 1];
+    if (lq < 0) return fail(ctx, BWAGPU_E_INVAL, "stream: negative read length");
+    if (lq > BWAGPU_MAX_READ_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "stream: read longer than BWAGPU_MAX_READ_LEN");
+    lq_max = std::max(lq_max, lq);
+    starts.push_back(p);
+    p = end;
+  }
+  const int tb = tb_bytes_for(ctx->opt, lq_max);
+  if ((size_t)(kBlock / 64) * 2 * tb > 64 * 1024)
+    return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->slot[0].stream;
+  const size_t cap = (size_t)std::max(o_cap_tasks, 1), nr = starts.size();
+  HIPC(ctx->st_buf.ensure(sizeof(int32_t) * (size_t)i_words), "hipMalloc");
+  HIPC(ctx->st_start.ensure(sizeof(int64_t) * nr), "hipMalloc");
+  HIPC(ctx->st_q.ensure(8 * (size_t)i_words), "hipMalloc");
+  HIPC(ctx->st_tasks.ensure(sizeof(StreamTask) * cap), "hipMalloc");
+  HIPC(ctx->st_lists.ensure(sizeof(int32_t) * kSpecBins * cap), "hipMalloc");
+  HIPC(ctx->st_seen.ensure(sizeof(int32_t) * cap), "hipMalloc");
+  HIPC(ctx->st_ctr.ensure(sizeof(int32_t) * kStrCtrWords), "hipMalloc");
+  HIPC(ctx->st_out.ensure(sizeof(int32_t) * 5 * cap), "hipMalloc");
+  HIPC(hipMemcpyAsync(ctx->st_buf.p, i_buf, sizeof(int32_t) * (size_t)i_words, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemcpyAsync(ctx->st_start.p, starts.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, st), "H2D");
+  HIPC(hipMemsetAsync(ctx->st_seen.p, 0, sizeof(int32_t) * cap, st), "memset");
+  HIPC(hipMemsetAsync(ctx->st_ctr.p, 0, sizeof(int32_t) * kStrCtrWords, st), "memset");
+  StreamArgs a;
+  a.buf = ctx->st_buf.as<int32_t>();
+  a.rstart = ctx->st_start.as<int64_t>();
+  a.n_reads = (int32_t)nr;
+  a.cap = (int32_t)cap;
+  a.l_pac = ctx->ref.l_pac;
+  a.qpool = ctx->st_q.as<uint8_t>();
+  a.tasks = ctx->st_tasks.as<StreamTask>();
+  a.lists = ctx->st_lists.as<int32_t>();
+  a.seen = ctx->st_seen.as<int32_t>();
+  a.ctr = ctx->st_ctr.as<int32_t>();
+  a.out = ctx->st_out.as<int32_t>();
+  if (o_cap_tasks == 0) a.cap = 0;  // every task index is then out of range
+  HIPC(launch_sw_stream(ctx->opt, ctx->ref, a, tb, st), "sw_stream launch");
+  int32_t c[8];
+  HIPC(hipMemcpyAsync(c, ctx->st_ctr.p, sizeof c, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
+  if (c[kStrErr]) {
+    const int e = c[kStrErr];
+    return fail(ctx, BWAGPU_E_RESULTS,
+                std::string("stream: ") + (e & STR_ERR_RECORD ? "a record does not end at its end word; " : "") +
+                    (e & STR_ERR_TASK ? "task index out of range; " : "") +
+                    (e & STR_ERR_DUP ? "task index repeated; " : "") +
+                    (e & STR_ERR_SEED ? "seed outside its read or window; " : "") +
+                    (e & STR_ERR_BASE ? "base > 4; " : ""));
+  }
+  if (c[kStrDecoded] != c[kStrMax]) return fail(ctx, BWAGPU_E_RESULTS, "stream: task indices are not 0..n-1");
+  const int32_t n = c[kStrMax];
+  if (n) HIPC(hipMemcpy(o_buf, ctx->st_out.p, sizeof(int32_t) * 5 * (size_t)n, hipMemcpyDeviceToHost), "D2H");
+  *o_tasks = n;
   return BWAGPU_OK;
 }

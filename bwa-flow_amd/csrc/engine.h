@@ -213,6 +213,35 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
 size_t spec_select_lds(int tb_bytes);
 int spec_redo_cap(int tb_bytes);
 
+// ---------------------------------------------------------------- FPGA wire format
+// bwagpu_sw_stream: packReadData's stream (src/fpga/FPGAPipeline.cpp:252-336)
+// decoded by one lane per read record, every task one extend_seed.
+struct StreamTask {
+  bwagpu_seed_t s;  // rbeg, qbeg, len (score unused)
+  int64_t lo, hi;   // the chain's window rmax
+  int64_t qoff;     // the read's bases in StreamArgs::qpool
+  int32_t lq, pad_;
+};
+// error flags (StreamArgs::ctr[kStrErr])
+enum { STR_ERR_RECORD = 1, STR_ERR_TASK = 2, STR_ERR_DUP = 4, STR_ERR_SEED = 8, STR_ERR_BASE = 16 };
+// counter words: [bin] task counts, kStrDecoded, kStrMax (max index + 1),
+// kStrErr, then the sharded queue heads of the kSpecBins lists
+enum { kStrDecoded = 4, kStrMax = 5, kStrErr = 6, kStrHeads = 64 };
+constexpr int kStrCtrWords = kStrHeads + kSpecBins * 8 * kQHStride;
+struct StreamArgs {
+  const int32_t* buf;     // the stream
+  const int64_t* rstart;  // first word of each read record (host walk)
+  int32_t n_reads, cap;   // records; task capacity
+  int64_t l_pac;
+  uint8_t* qpool;         // 8 bytes per stream word: record at word p -> bases at 8 p
+  StreamTask* tasks;      // [cap]
+  int32_t* lists;         // kSpecBins lists of cap entries
+  int32_t* seen;          // [cap], zeroed: duplicate task indices
+  int32_t* ctr;           // kStrCtrWords, zeroed
+  int32_t* out;           // 5 words per task
+};
+hipError_t launch_sw_stream(const DevOpt& o, const DevRef& ref, const StreamArgs& a, int tb_bytes, hipStream_t st);
+
 // diagnostics: per-read trace buffer (device pointer, 8 x u32 per read; NULL = off)
 hipError_t set_trace(void* dev_ptr);
 

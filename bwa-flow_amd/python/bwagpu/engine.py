@@ -238,6 +238,16 @@ class Engine:
         self._check(self.lib.bwagpu_bwt_sa(self.ctx, len(ks), _ptr(ks), _ptr(out)), "bwt_sa")
         return out[:len(ks)]
 
+    def sw_stream(self, words: np.ndarray, cap_tasks: int) -> np.ndarray:
+        """sw_top on the FPGA wire format (src/fpga/FPGAPipeline.cpp:252-336 in,
+        :91-105 out): one packed task stream -> int16[n_tasks, 10] records"""
+        words = np.ascontiguousarray(words, np.int32)
+        out = np.zeros((max(cap_tasks, 1), 10), np.int16)
+        n = C.c_int32(0)
+        self._check(self.lib.bwagpu_sw_stream(self.ctx, _ptr(words), len(words), _ptr(out), int(cap_tasks),
+                                              C.byref(n)), "sw_stream")
+        return out[:n.value]
+
     def seed_budget(self, budget: int):
         """bwt_extend calls a read gets on one lane before the wave kernel takes it (0: all on waves)"""
         self._check(self.lib.bwagpu_debug_seed_budget(self.ctx, budget), "seed_budget")

@@ -44,6 +44,13 @@
  *       read pair of a batch (mem_sam_pe, bwamem_pair.c:290-300).  Results
  *       equal ksw_align2's kswr_t field for field, including the quirks of
  *       its striped first pass (see oracle/ksw_align.c).
+ *   bwagpu_sw_stream
+ *       the FPGA kernel's own job, sw_top over one packed task stream
+ *       (clEnqueueTask, xlnx/XCLAgent.cpp:89-106): the input stream of
+ *       packReadData (src/fpga/FPGAPipeline.cpp:252-336) in, the 5-int
+ *       per-seed result records processOutput reads (FPGAPipeline.cpp:90-105)
+ *       out, every seed extended as mem_chain2aln extends one seed
+ *       (bwa/bwamem.c:717-792) in its chain's window rmax.
  *   bwagpu_last_error
  *       the what() of fpgaHangError / fpgaResultsError / std::runtime_error
  *       (src/util.h:16-32, OpenCLEnv.h:21-31).
@@ -316,6 +323,27 @@ int bwagpu_align2_device(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_align2
 int bwagpu_reg2aln_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_reg2aln_task_t *tasks,
                          const uint8_t *qpool, int64_t qpool_len, int32_t max_ops, int32_t max_md,
                          bwagpu_aln_t *out, uint32_t *cigar, char *md);
+
+/* The FPGA wire format.  i_buf/i_words: one or more
+   read records exactly as packReadData writes them (FPGAPipeline.cpp:252-336),
+   back to back from word 0 (each record's first word is the word index of its
+   end, relative to i_buf):
+     end, l_seq, ceil(l_seq/8) words of 4-bit bases (first base in the high
+     nibble), n_chains, then per chain: rmax[0], rmax[1] (int64, the window of
+     getChainRef, FPGAPipeline.cpp:143-192), n_tasks, then per task: task index,
+     rbeg (int64), qbeg, len.
+   Every task is one seed extended left and right in its chain's window
+   (bwamem.c:717-792: band retry, z-drop, local vs to-end); the record of task
+   t is o_buf[10 t .. 10 t + 9] (int16): t & 0xffff, t >> 16, qb, qe - (qbeg +
+   len), rb - rbeg, re - (rbeg + len), score, truesc, w, 0 — the fields
+   processOutput applies (FPGAPipeline.cpp:91-105).  Task indices must be
+   0..n-1, each once; *o_tasks = n.  o_cap_tasks bounds n.  A malformed
+   stream returns BWAGPU_E_INVAL before any launch, or BWAGPU_E_RESULTS when
+   the device finds it (a record that does not end at its end word, a task
+   index out of range or repeated, a seed outside its window).  Reads up to
+   BWAGPU_MAX_READ_LEN bp. */
+int bwagpu_sw_stream(bwagpu_ctx_t *ctx, const int32_t *i_buf, int64_t i_words, int16_t *o_buf,
+                     int32_t o_cap_tasks, int32_t *o_tasks);
 
 int bwagpu_last_stats(const bwagpu_ctx_t *ctx, int slot, bwagpu_stats_t *stats);
 

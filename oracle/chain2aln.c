@@ -29,6 +29,8 @@ static int max_gap_len(const bwagpu_opt_t *o, int qlen)
   return l < (o->w << 1) ? l : (o->w << 1);
 }
 
+int oracle_max_gap_len(const bwagpu_opt_t *o, int qlen) { return max_gap_len(o, qlen); }
+
 static inline int pac_base(const uint8_t *pac, int64_t k) { return pac[k >> 2] >> ((~k & 3) << 1) & 3; }
 
 /* materialise [beg,end) of the 2-strand coordinate space (bns_get_seq) */
@@ -39,6 +41,11 @@ static void get_window(int64_t l_pac, const uint8_t *pac, int64_t beg, int64_t e
   } else {
     for (int64_t k = beg; k < end; ++k) out[k - beg] = pac_base(pac, k);
   }
+}
+
+void oracle_get_window(int64_t l_pac, const uint8_t *pac, int64_t beg, int64_t end, uint8_t *out)
+{
+  get_window(l_pac, pac, beg, end, out);
 }
 
 static int cmp_u64(const void *a, const void *b)
@@ -52,6 +59,78 @@ typedef struct {
   int64_t calls;
 } tally_t;
 #define tl_cells(t) ((t)->cells)
+
+/* One seed's extension, bwamem.c:717-792: the left ksw_extend2 over the
+   reversed query prefix and reversed window prefix with the MAX_BAND_TRY
+   retry, the right one from the left score, the local vs to-end choice of each
+   side.  win = the window [lo, hi); qrev/trev = scratch of lq / hi - lo bytes.
+   Fills w, score, truesc, qb, qe, rb, re of *a (nothing else). */
+void oracle_seed_extend(const bwagpu_opt_t *opt, int lq, const uint8_t *q, const bwagpu_seed_t *s, int64_t lo,
+                        int64_t hi, const uint8_t *win, uint8_t *qrev, uint8_t *trev, bwagpu_alnreg_t *a,
+                        int64_t *cells, int64_t *calls)
+{
+  int aw0 = opt->w, aw1 = opt->w, mo, i;
+  a->w = opt->w;
+  a->score = a->truesc = -1;
+
+  if (s->qbeg) { /* leftwards: reversed query prefix against reversed window prefix */
+    int qle = 0, tle = 0, gtle = 0, gsc = 0;
+    int64_t ltl = s->rbeg - lo;
+    for (i = 0; i < s->qbeg; ++i) qrev[i] = q[s->qbeg - 1 - i];
+    for (i = 0; i < ltl; ++i) trev[i] = win[ltl - 1 - i];
+    for (i = 0; i < BAND_TRIES; ++i) {
+      int before = a->score;
+      aw0 = opt->w << i;
+      a->score = oracle_ksw_extend2(s->qbeg, qrev, (int)ltl, trev, 5, opt->mat, opt->o_del, opt->e_del,
+                                    opt->o_ins, opt->e_ins, aw0, opt->pen_clip5, opt->zdrop,
+                                    s->len * opt->a, &qle, &tle, &gtle, &gsc, &mo, cells);
+      ++*calls;
+      if (a->score == before || mo < (aw0 >> 1) + (aw0 >> 2)) break;
+    }
+    if (gsc <= 0 || gsc <= a->score - opt->pen_clip5) {
+      a->qb = s->qbeg - qle;
+      a->rb = s->rbeg - tle;
+      a->truesc = a->score;
+    } else {
+      a->qb = 0;
+      a->rb = s->rbeg - gtle;
+      a->truesc = gsc;
+    }
+  } else {
+    a->score = a->truesc = s->len * opt->a;
+    a->qb = 0;
+    a->rb = s->rbeg;
+  }
+
+  if (s->qbeg + s->len != lq) { /* rightwards from the seed end */
+    int qle = 0, tle = 0, gtle = 0, gsc = 0, sc0 = a->score;
+    int qe = s->qbeg + s->len;
+    int64_t re = s->rbeg + s->len - lo;
+    for (i = 0; i < BAND_TRIES; ++i) {
+      int before = a->score;
+      aw1 = opt->w << i;
+      a->score = oracle_ksw_extend2(lq - qe, q + qe, (int)(hi - lo - re), win + re, 5, opt->mat,
+                                    opt->o_del, opt->e_del, opt->o_ins, opt->e_ins, aw1,
+                                    opt->pen_clip3, opt->zdrop, sc0, &qle, &tle, &gtle, &gsc, &mo,
+                                    cells);
+      ++*calls;
+      if (a->score == before || mo < (aw1 >> 1) + (aw1 >> 2)) break;
+    }
+    if (gsc <= 0 || gsc <= a->score - opt->pen_clip3) {
+      a->qe = qe + qle;
+      a->re = lo + re + tle;
+      a->truesc += a->score - sc0;
+    } else {
+      a->qe = lq;
+      a->re = lo + re + gtle;
+      a->truesc += gsc - sc0;
+    }
+  } else {
+    a->qe = lq;
+    a->re = s->rbeg + s->len;
+  }
+  a->w = aw0 > aw1 ? aw0 : aw1;
+}
 
 /* one chain; regs/nreg is the read's region vector (capacity = read's seeds) */
 static int one_chain(const bwagpu_opt_t *opt, const bwagpu_bns_t *bns, const uint8_t *pac, int lq,
@@ -99,7 +178,6 @@ static int one_chain(const bwagpu_opt_t *opt, const bwagpu_bns_t *bns, const uin
   for (k = ns - 1; k >= 0; --k) {
     const bwagpu_seed_t *s = &sd[(uint32_t)key[k]];
     bwagpu_alnreg_t *a;
-    int aw0 = opt->w, aw1 = opt->w, mo;
 
     /* is the seed (almost) inside a region already found for this read? */
     for (i = 0; i < *nreg; ++i) {
@@ -138,74 +216,14 @@ static int one_chain(const bwagpu_opt_t *opt, const bwagpu_bns_t *bns, const uin
 
     a = &regs[(*nreg)++];
     memset(a, 0, sizeof(*a));
-    a->w = opt->w;
-    a->score = a->truesc = -1;
     a->rid = rid;
-
-    if (s->qbeg) { /* leftwards: reversed query prefix against reversed window prefix */
-      int qle = 0, tle = 0, gtle = 0, gsc = 0;
-      int64_t ltl = s->rbeg - lo;
-      for (i = 0; i < s->qbeg; ++i) qrev[i] = q[s->qbeg - 1 - i];
-      for (i = 0; i < ltl; ++i) trev[i] = win[ltl - 1 - i];
-      for (i = 0; i < BAND_TRIES; ++i) {
-        int before = a->score;
-        aw0 = opt->w << i;
-        a->score = oracle_ksw_extend2(s->qbeg, qrev, (int)ltl, trev, 5, opt->mat, opt->o_del, opt->e_del,
-                                      opt->o_ins, opt->e_ins, aw0, opt->pen_clip5, opt->zdrop,
-                                      s->len * opt->a, &qle, &tle, &gtle, &gsc, &mo, tl_cells(tl));
-        tl->calls++;
-        if (a->score == before || mo < (aw0 >> 1) + (aw0 >> 2)) break;
-      }
-      if (gsc <= 0 || gsc <= a->score - opt->pen_clip5) {
-        a->qb = s->qbeg - qle;
-        a->rb = s->rbeg - tle;
-        a->truesc = a->score;
-      } else {
-        a->qb = 0;
-        a->rb = s->rbeg - gtle;
-        a->truesc = gsc;
-      }
-    } else {
-      a->score = a->truesc = s->len * opt->a;
-      a->qb = 0;
-      a->rb = s->rbeg;
-    }
-
-    if (s->qbeg + s->len != lq) { /* rightwards from the seed end */
-      int qle = 0, tle = 0, gtle = 0, gsc = 0, sc0 = a->score;
-      int qe = s->qbeg + s->len;
-      int64_t re = s->rbeg + s->len - lo;
-      for (i = 0; i < BAND_TRIES; ++i) {
-        int before = a->score;
-        aw1 = opt->w << i;
-        a->score = oracle_ksw_extend2(lq - qe, q + qe, (int)(hi - lo - re), win + re, 5, opt->mat,
-                                      opt->o_del, opt->e_del, opt->o_ins, opt->e_ins, aw1,
-                                      opt->pen_clip3, opt->zdrop, sc0, &qle, &tle, &gtle, &gsc, &mo,
-                                      tl_cells(tl));
-        tl->calls++;
-        if (a->score == before || mo < (aw1 >> 1) + (aw1 >> 2)) break;
-      }
-      if (gsc <= 0 || gsc <= a->score - opt->pen_clip3) {
-        a->qe = qe + qle;
-        a->re = lo + re + tle;
-        a->truesc += a->score - sc0;
-      } else {
-        a->qe = lq;
-        a->re = lo + re + gtle;
-        a->truesc += gsc - sc0;
-      }
-    } else {
-      a->qe = lq;
-      a->re = s->rbeg + s->len;
-    }
-
+    oracle_seed_extend(opt, lq, q, s, lo, hi, win, qrev, trev, a, tl->cells, &tl->calls);
     a->seedcov = 0;
     for (i = 0; i < ns; ++i) {
       const bwagpu_seed_t *t = &sd[i];
       if (t->qbeg >= a->qb && t->qbeg + t->len <= a->qe && t->rbeg >= a->rb && t->rbeg + t->len <= a->re)
         a->seedcov += t->len;
     }
-    a->w = aw0 > aw1 ? aw0 : aw1;
     a->seedlen0 = s->len;
     a->frac_rep = frac_rep;
   }

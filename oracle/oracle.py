@@ -52,6 +52,12 @@ def oracle_lib():
     lib.oracle_collect_intv.restype = C.c_int
     lib.oracle_bwt_sa.argtypes = [_VP, _VP, _VP, C.c_int, C.c_uint64]
     lib.oracle_bwt_sa.restype = C.c_uint64
+    lib.oracle_fpga_pack.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), C.POINTER(abi.BatchC), _VP, C.c_int64,
+                                     C.c_int32, C.POINTER(C.c_int32), _VP, _VP]
+    lib.oracle_fpga_pack.restype = C.c_int64
+    lib.oracle_fpga_sw.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, _VP, C.c_int64, _VP, C.c_int32,
+                                   C.POINTER(C.c_int32)]
+    lib.oracle_fpga_sw.restype = C.c_int
     return lib
 
 
@@ -200,3 +206,31 @@ def bwt_sa(bwt_hdr, bwt_words, sa, sa_intv, ks):
     sa = np.ascontiguousarray(sa, np.uint64)
     lib = oracle_lib()
     return np.array([lib.oracle_bwt_sa(_ptr(hdr), _ptr(words), _ptr(sa), int(sa_intv), int(k)) for k in ks], np.uint64)
+
+
+def fpga_pack(opt: dict, ref: Ref, batch: Batch):
+    """packReadData over a batch (FPGAPipeline.cpp:194-343) -> (words int32, n_tasks, packed[n_reads],
+    task_seed[n_tasks]: the batch seed index of each task)"""
+    o = abi.opt_from_dict(opt)
+    bc = batch.to_c()
+    cap_w = 16 + 4 * batch.n_reads + int(batch.seq_off[-1]) // 8 + 5 * batch.n_chains + 5 * batch.n_seeds
+    words = np.zeros(max(cap_w, 1), np.int32)
+    packed = np.zeros(max(batch.n_reads, 1), np.int32)
+    task_seed = np.zeros(max(batch.n_seeds, 1), np.int32)
+    nt = C.c_int32(0)
+    nw = oracle_lib().oracle_fpga_pack(C.byref(o), C.byref(ref.bns), C.byref(bc), _ptr(words), cap_w,
+                                       max(batch.n_seeds, 1), C.byref(nt), _ptr(packed), _ptr(task_seed))
+    if nw < 0:
+        raise RuntimeError("fpga_pack: buffer too small")
+    return words[:nw], nt.value, packed[:batch.n_reads], task_seed[:nt.value]
+
+
+def fpga_sw(opt: dict, ref: Ref, words, cap_tasks: int):
+    """the records bwagpu_sw_stream must return -> int16[n, 10], or None for a malformed stream"""
+    o = abi.opt_from_dict(opt)
+    words = np.ascontiguousarray(words, np.int32)
+    out = np.zeros((max(cap_tasks, 1), 10), np.int16)
+    nt = C.c_int32(0)
+    rc = oracle_lib().oracle_fpga_sw(C.byref(o), C.byref(ref.bns), _ptr(ref.pac), _ptr(words), len(words),
+                                     _ptr(out), int(cap_tasks), C.byref(nt))
+    return None if rc != 0 else out[:nt.value]
