@@ -144,6 +144,7 @@ struct SeedExt {
 constexpr int kSpecBins = 3;                           // lq <= 192 / <= 256 / <= 1023
 constexpr int kSpecBinLen[kSpecBins] = {192, 256, 1023};
 constexpr int kSpecRounds = 3;                         // A, B, C
+constexpr int kOrderLane = 8;                          // chains up to this many seeds are ordered by their spec_chain lane
 constexpr int kSelLight = 64;                          // reads with more seeds go first
 constexpr int kSelRegLds = 256;                        // regions per wave held in LDS
 constexpr int kSelMatMaxSeeds = 4096;                  // heavy reads up to this many seeds use pair matrices
@@ -157,6 +158,7 @@ enum {
   SPC_MISS = 26,      // extensions the redo pass computed inline
   SPC_MATW64 = 28,    // int64 at words 28-29: uint64 words of heavy-read pair matrices handed out
   SPC_HCOLS = 30,     // columns (seeds) of heavy reads with a pair matrix
+  SPC_LONG_N = 31,    // chains with more than kOrderLane seeds (ordered by spec_order_kernel)
   SPC_WORDS = 128
 };
 // sharded queue heads of the extension task lists (SpecArgs::qh, zeroed per
@@ -188,6 +190,7 @@ struct SpecArgs {
   int32_t* seedchain;         // per seed slot: its chain
   int4* hinfo;                // per heavy-list entry: rd, matrix word offset (-1: none), first column, ns
   int32_t* colent;            // per heavy column: its heavy-list entry
+  int32_t* longc;             // chains with more than kOrderLane seeds
   uint64_t* mat;              // heavy-read pair matrices: C[ns][nw] then O[ns][nw] per read
   int64_t mat_words;          // capacity of mat
   int32_t* cov;               // per seed slot: seedcov of its region (heavy reads)

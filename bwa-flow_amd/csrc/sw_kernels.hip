@@ -2384,7 +2384,7 @@ __device__ __forceinline__ int spec_bin(int lq) { return lq <= kSpecBinLen[0] ? 
 // chain's read, and the round-A task (its first seed in processing order)
 __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  bool task = false;
+  bool task = false, longc = false;
   int bin = 0, s0 = 0;
   if (c < b.n_chains) {
     int lo_r = 0, hi_r = b.n_reads - 1;  // owner read: binary search over read_chain_off
@@ -2429,6 +2429,29 @@ __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, D
         wlo = max(wlo, cb);
         whi = min(whi, ce);
       }
+      // the processing order (descending key score<<32|i, bwamem.c:671-676)
+      // of a short chain, ranked in this lane's registers; longer chains go
+      // to spec_order_kernel
+      if (ns <= kOrderLane) {
+        uint64_t key[kOrderLane];
+#pragma unroll
+        for (int t = 0; t < kOrderLane; ++t)
+          key[t] = t < ns ? (uint64_t)(uint32_t)b.seeds[s0 + t].score << 32 | (uint32_t)t : ~0ull;
+#pragma unroll
+        for (int t = 0; t < kOrderLane; ++t) {
+          if (t < ns) {
+            int rank = 0;
+#pragma unroll
+            for (int u = 0; u < kOrderLane; ++u) rank += key[u] < key[t];
+            bwagpu_seed_t v = b.seeds[s0 + t];
+            v.pad_ = key[t] == 0 ? 1 : 0;
+            a.prog[s0 + ns - 1 - rank] = v;
+            a.seedchain[s0 + ns - 1 - rank] = c;
+          }
+        }
+      } else {
+        longc = true;
+      }
       if (!ok) {
         atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_RID);
         a.win[c] = ChainWin{0, -1};
@@ -2444,6 +2467,8 @@ __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, D
     const int p = wave_append(&a.ctr[SPC_CNT + k], task && bin == k);
     if (p >= 0) a.tasks[(size_t)k * b.n_chains + p] = make_int2(s0, c);
   }
+  const int p = wave_append(&a.ctr[SPC_LONG_N], longc);
+  if (p >= 0) a.longc[p] = c;
 }
 
 // rows are triangular: row k holds words w < ceil(k / 64) (only seeds j < k
@@ -2493,23 +2518,43 @@ __global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a)
   }
 }
 
-// 16 lanes per chain: the seeds in processing order (descending key
-// score<<32|i, bwamem.c:671-676) by ranking — keys are unique, so rank = the
-// number of smaller keys; O(ns^2/16) per chain, no serial lane on a long chain.
-// pad_ = 1 flags the key that is 0 from the start (skipped by the overlap test
-// like a marked seed, bwamem.c:700).
+// The processing order (descending key score<<32|i, bwamem.c:671-676) of
+// the chains spec_chain_kernel listed (more than kOrderLane seeds), by
+// ranking: keys are unique, so rank = the number of smaller keys.  One
+// workgroup per chain with the keys staged in LDS (a lane looping over global
+// keys made the longest chain, ~170 seeds, a 250 us tail).  pad_ = 1 flags
+// the key that is 0 from the start (skipped by the overlap test like a
+// marked seed, bwamem.c:700).
+constexpr int kOrderBlocks = 1024;
+constexpr int kOrderLds = 4096;  // longer chains rank against global memory
+__device__ __forceinline__ uint64_t order_key(const bwagpu_seed_t* sd, int i) {
+  return (uint64_t)(uint32_t)sd[i].score << 32 | (uint32_t)i;
+}
 __global__ void __launch_bounds__(256) spec_order_kernel(DevBatch b, SpecArgs a) {
-  const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4), r = (int)(threadIdx.x & 15);
-  if (g >= b.n_chains) return;
-  const int s0 = b.chain_seed_off[g], ns = b.chain_seed_off[g + 1] - s0;
-  for (int i = r; i < ns; i += 16) {
-    bwagpu_seed_t v = b.seeds[s0 + i];
-    const uint64_t ki = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
-    int rank = 0;
-    for (int j = 0; j < ns; ++j) rank += ((uint64_t)(uint32_t)b.seeds[s0 + j].score << 32 | (uint32_t)j) < ki;
-    v.pad_ = ki == 0 ? 1 : 0;
-    a.prog[s0 + ns - 1 - rank] = v;
-    a.seedchain[s0 + ns - 1 - rank] = g;
+  __shared__ uint64_t keys[kOrderLds];
+  const int tid = (int)threadIdx.x;
+  const int n_long = __hip_atomic_load(&a.ctr[SPC_LONG_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int gi = (int)blockIdx.x; gi < n_long; gi += (int)gridDim.x) {
+    const int g = a.longc[gi];
+    const int s0 = b.chain_seed_off[g], ns = b.chain_seed_off[g + 1] - s0;
+    const bwagpu_seed_t* sd = b.seeds + s0;
+    const bool in_lds = ns <= kOrderLds;
+    if (in_lds)
+      for (int i = tid; i < ns; i += 256) keys[i] = order_key(sd, i);
+    __syncthreads();
+    for (int i = tid; i < ns; i += 256) {
+      bwagpu_seed_t v = sd[i];
+      const uint64_t ki = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
+      int rank = 0;
+      if (in_lds)
+        for (int j = 0; j < ns; ++j) rank += keys[j] < ki;
+      else
+        for (int j = 0; j < ns; ++j) rank += order_key(sd, j) < ki;
+      v.pad_ = ki == 0 ? 1 : 0;
+      a.prog[s0 + ns - 1 - rank] = v;
+      a.seedchain[s0 + ns - 1 - rank] = g;
+    }
+    __syncthreads();
   }
 }
 
@@ -3624,7 +3669,7 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
   if (b.n_reads == 0) return hipSuccess;
   if (b.n_chains) {
     hipLaunchKernelGGL(spec_chain_kernel, dim3((b.n_chains + 255) / 256), dim3(256), 0, st, o, ref, b, a);
-    hipLaunchKernelGGL(spec_order_kernel, dim3((b.n_chains + 15) / 16), dim3(256), 0, st, b, a);
+    hipLaunchKernelGGL(spec_order_kernel, dim3(kOrderBlocks), dim3(256), 0, st, b, a);
   }
   hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if (b.n_chains) {
