@@ -2380,63 +2380,74 @@ struct ShardQ {
 
 __device__ __forceinline__ int spec_bin(int lq) { return lq <= kSpecBinLen[0] ? 0 : (lq <= kSpecBinLen[1] ? 1 : 2); }
 
+// the raw extent of a chain's seeds' reach (bwamem.c:650-657), min / max
+__device__ __forceinline__ void seed_reach(const DevOpt& o, const bwagpu_seed_t& t, int lq, int64_t& wlo,
+                                           int64_t& whi) {
+  const int tail = lq - t.qbeg - t.len;
+  wlo = min(wlo, t.rbeg - (int64_t)(t.qbeg + max_gap_len(o, t.qbeg)));
+  whi = max(whi, t.rbeg + t.len + (int64_t)(tail + max_gap_len(o, tail)));
+}
+
+// the rest of the window (bwamem.c:658-668 + bns_fetch_seq's clipping,
+// bntseq.c:421-446): clamp, one strand, the contig of the first seed; false
+// when that seed is not in contig rid (where bwa asserts, bwamem.c:669)
+__device__ __forceinline__ bool finish_window(const DevRef& ref, int rid, int64_t mid, int64_t& wlo, int64_t& whi) {
+  const int64_t two = ref.l_pac << 1;
+  wlo = max(wlo, (int64_t)0);
+  whi = min(whi, two);
+  if (wlo < ref.l_pac && ref.l_pac < whi) {
+    if (mid < ref.l_pac) whi = ref.l_pac;
+    else wlo = ref.l_pac;
+  }
+  bool ok = rid >= 0 && rid < ref.n_seqs;
+  if (ok) {
+    const int64_t fpos = mid >= ref.l_pac ? two - 1 - mid : mid;
+    int64_t cb = ref.ann_offset[rid], ce = cb + ref.ann_len[rid];
+    ok = fpos >= cb && fpos < ce;
+    if (mid >= ref.l_pac) {
+      const int64_t t0 = cb;
+      cb = two - ce;
+      ce = two - t0;
+    }
+    wlo = max(wlo, cb);
+    whi = min(whi, ce);
+  }
+  return ok;
+}
+
 // lane per chain: window (bwamem.c:648-668 + bns_fetch_seq's clipping), the
-// chain's read, and the round-A task (its first seed in processing order)
+// round-A task (the chain's first seed in processing order) and, for chains
+// of up to kOrderLane seeds, the processing order; longer chains are listed
+// for spec_order_kernel, which does their window and order one workgroup
+// each (a lane looping over ~170 seeds was this kernel's tail).  chain_read
+// comes from spec_reads_kernel.
 __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   bool task = false, longc = false;
   int bin = 0, s0 = 0;
   if (c < b.n_chains) {
-    int lo_r = 0, hi_r = b.n_reads - 1;  // owner read: binary search over read_chain_off
-    while (lo_r < hi_r) {
-      const int mid = (lo_r + hi_r + 1) >> 1;
-      if (b.read_chain_off[mid] <= c) lo_r = mid;
-      else hi_r = mid - 1;
-    }
-    a.chain_read[c] = lo_r;
+    const int rd = a.chain_read[c];
     s0 = b.chain_seed_off[c];
     const int ns = b.chain_seed_off[c + 1] - s0;
-    const int lq = (int)(b.seq_off[lo_r + 1] - b.seq_off[lo_r]);
+    const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
     if (ns <= 0) {
       a.win[c] = ChainWin{0, 0};
     } else {
-      const int64_t two = ref.l_pac << 1;
-      int64_t wlo = two, whi = 0;
-      for (int i = 0; i < ns; ++i) {
-        const bwagpu_seed_t t = b.seeds[s0 + i];
-        const int tail = lq - t.qbeg - t.len;
-        wlo = min(wlo, t.rbeg - (int64_t)(t.qbeg + max_gap_len(o, t.qbeg)));
-        whi = max(whi, t.rbeg + t.len + (int64_t)(tail + max_gap_len(o, tail)));
-      }
-      wlo = max(wlo, (int64_t)0);
-      whi = min(whi, two);
-      const int64_t mid = b.seeds[s0].rbeg;
-      if (wlo < ref.l_pac && ref.l_pac < whi) {
-        if (mid < ref.l_pac) whi = ref.l_pac;
-        else wlo = ref.l_pac;
-      }
-      const int rid = b.chain_rid[c];
-      bool ok = rid >= 0 && rid < ref.n_seqs;
-      if (ok) {
-        const int64_t fpos = mid >= ref.l_pac ? two - 1 - mid : mid;
-        int64_t cb = ref.ann_offset[rid], ce = cb + ref.ann_len[rid];
-        ok = fpos >= cb && fpos < ce;
-        if (mid >= ref.l_pac) {
-          const int64_t t0 = cb;
-          cb = two - ce;
-          ce = two - t0;
-        }
-        wlo = max(wlo, cb);
-        whi = min(whi, ce);
-      }
-      // the processing order (descending key score<<32|i, bwamem.c:671-676)
-      // of a short chain, ranked in this lane's registers; longer chains go
-      // to spec_order_kernel
-      if (ns <= kOrderLane) {
+      int64_t wlo = ref.l_pac << 1, whi = 0;
+      longc = ns > kOrderLane;
+      if (!longc) {
+        // the processing order (descending key score<<32|i, bwamem.c:671-676),
+        // ranked in registers
         uint64_t key[kOrderLane];
 #pragma unroll
-        for (int t = 0; t < kOrderLane; ++t)
-          key[t] = t < ns ? (uint64_t)(uint32_t)b.seeds[s0 + t].score << 32 | (uint32_t)t : ~0ull;
+        for (int t = 0; t < kOrderLane; ++t) {
+          key[t] = ~0ull;
+          if (t < ns) {
+            const bwagpu_seed_t v = b.seeds[s0 + t];
+            key[t] = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)t;
+            seed_reach(o, v, lq, wlo, whi);
+          }
+        }
 #pragma unroll
         for (int t = 0; t < kOrderLane; ++t) {
           if (t < ns) {
@@ -2449,14 +2460,13 @@ __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, D
             a.seedchain[s0 + ns - 1 - rank] = c;
           }
         }
-      } else {
-        longc = true;
       }
+      const bool ok = finish_window(ref, b.chain_rid[c], b.seeds[s0].rbeg, wlo, whi);
       if (!ok) {
         atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_RID);
         a.win[c] = ChainWin{0, -1};
       } else {
-        a.win[c] = ChainWin{wlo, whi};
+        if (!longc) a.win[c] = ChainWin{wlo, whi};
         task = lq <= BWAGPU_MAX_READ_LEN;
         bin = spec_bin(lq);
       }
@@ -2496,6 +2506,7 @@ __global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a)
     d.s0 = b.chain_seed_off[d.c0];
     d.ns = b.chain_seed_off[d.c0 + d.nch] - d.s0;
     a.rdesc[rd] = d;
+    for (int c = d.c0; c < d.c0 + d.nch; ++c) a.chain_read[c] = rd;
     heavy = d.ns > kSelLight || d.nch > kSelLight;
     ns = d.ns;
   }
@@ -2530,8 +2541,9 @@ constexpr int kOrderLds = 4096;  // longer chains rank against global memory
 __device__ __forceinline__ uint64_t order_key(const bwagpu_seed_t* sd, int i) {
   return (uint64_t)(uint32_t)sd[i].score << 32 | (uint32_t)i;
 }
-__global__ void __launch_bounds__(256) spec_order_kernel(DevBatch b, SpecArgs a) {
+__global__ void __launch_bounds__(256) spec_order_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
   __shared__ uint64_t keys[kOrderLds];
+  __shared__ int64_t wred[2][4];
   const int tid = (int)threadIdx.x;
   const int n_long = __hip_atomic_load(&a.ctr[SPC_LONG_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int gi = (int)blockIdx.x; gi < n_long; gi += (int)gridDim.x) {
@@ -2539,9 +2551,29 @@ __global__ void __launch_bounds__(256) spec_order_kernel(DevBatch b, SpecArgs a)
     const int s0 = b.chain_seed_off[g], ns = b.chain_seed_off[g + 1] - s0;
     const bwagpu_seed_t* sd = b.seeds + s0;
     const bool in_lds = ns <= kOrderLds;
-    if (in_lds)
-      for (int i = tid; i < ns; i += 256) keys[i] = order_key(sd, i);
+    const int rd = a.chain_read[g];
+    const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+    int64_t wlo = ref.l_pac << 1, whi = 0;
+    for (int i = tid; i < ns; i += 256) {
+      const bwagpu_seed_t v = sd[i];
+      if (in_lds) keys[i] = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
+      seed_reach(o, v, lq, wlo, whi);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      wlo = min(wlo, (int64_t)__shfl_xor((long long)wlo, m, 64));
+      whi = max(whi, (int64_t)__shfl_xor((long long)whi, m, 64));
+    }
+    if ((tid & 63) == 0) {
+      wred[0][tid >> 6] = wlo;
+      wred[1][tid >> 6] = whi;
+    }
     __syncthreads();
+    if (tid == 0) {
+      wlo = min(min(wred[0][0], wred[0][1]), min(wred[0][2], wred[0][3]));
+      whi = max(max(wred[1][0], wred[1][1]), max(wred[1][2], wred[1][3]));
+      if (finish_window(ref, b.chain_rid[g], sd[0].rbeg, wlo, whi)) a.win[g] = ChainWin{wlo, whi};
+    }
     for (int i = tid; i < ns; i += 256) {
       bwagpu_seed_t v = sd[i];
       const uint64_t ki = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
@@ -3667,11 +3699,11 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   if (b.n_reads == 0) return hipSuccess;
+  hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if (b.n_chains) {
     hipLaunchKernelGGL(spec_chain_kernel, dim3((b.n_chains + 255) / 256), dim3(256), 0, st, o, ref, b, a);
-    hipLaunchKernelGGL(spec_order_kernel, dim3(kOrderBlocks), dim3(256), 0, st, b, a);
+    hipLaunchKernelGGL(spec_order_kernel, dim3(kOrderBlocks), dim3(256), 0, st, o, ref, b, a);
   }
-  hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if (b.n_chains) {
     launch_ext_round(o, ref, b, a, 0, tb_bytes, st, ss);
     launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st, ss);
