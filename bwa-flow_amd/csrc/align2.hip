@@ -351,14 +351,15 @@ __global__ __launch_bounds__(256) void align2_bin_kernel(const bwagpu_align2_tas
 namespace {
 template <int CD, bool U8>
 hipError_t launch_one(const A2Args& a, const A2Prof& P, int n_hint, hipStream_t st) {
-  static int cap = 0;
-  if (!cap) {
+  // no dynamic LDS, so the resident grid depends on the kernel alone; a
+  // function-local static initialiser runs once even with several worker threads
+  static const int cap = [] {
     int per_cu = 0, dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, align2_kernel<CD, U8>, 256, 0);
-    cap = std::max(1, per_cu) * std::max(1, ncu);
-  }
+    return std::max(1, per_cu) * std::max(1, ncu);
+  }();
   const int want = n_hint > 0 ? (n_hint + 3) / 4 : cap;
   const int grid = std::max(1, std::min(want, cap));
   hipLaunchKernelGGL((align2_kernel<CD, U8>), dim3(grid), dim3(256), 0, st, a, P);
