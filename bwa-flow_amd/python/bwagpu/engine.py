@@ -160,9 +160,17 @@ class Engine:
         bc = batch.to_c()
         self._check(self.lib.bwagpu_chain2aln_submit(self.ctx, slot, C.byref(bc)), "submit")
 
-    def wait(self, slot: int, batch: Batch):
-        regs = np.zeros(max(batch.n_seeds, 1), abi.ALNREG_DTYPE)
-        n = np.zeros(max(batch.n_reads, 1), np.int32)
+    def wait(self, slot: int, batch: Batch, out=None):
+        """-> (regs, n) as chain2aln; `out` = (regs, n) arrays of at least
+        max(n_seeds, 1) / max(n_reads, 1) entries to reuse instead of fresh ones"""
+        if out is None:
+            regs = np.zeros(max(batch.n_seeds, 1), abi.ALNREG_DTYPE)
+            n = np.zeros(max(batch.n_reads, 1), np.int32)
+        else:
+            regs, n = out
+            if (regs.dtype != abi.ALNREG_DTYPE or n.dtype != np.int32 or not regs.flags.c_contiguous
+                    or not n.flags.c_contiguous or len(regs) < max(batch.n_seeds, 1) or len(n) < max(batch.n_reads, 1)):
+                raise ValueError("wait: out arrays too small or of the wrong dtype/layout")
         self._check(self.lib.bwagpu_chain2aln_wait(self.ctx, slot, _ptr(regs), _ptr(n)), "wait")
         return regs[:batch.n_seeds], n[:batch.n_reads]
 
