@@ -261,6 +261,62 @@ void freeChainsRecordChains(mem_chain_v* chains, int batch_num) {
   free(chains);
 }
 
+// ------------------------------------------------------------ ChainReaper
+static bool reaper_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("BWAGPU_CHAIN_REAPER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+ChainReaper::~ChainReaper() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();  // run() frees what is left before it returns
+}
+
+void ChainReaper::release(mem_chain_v* chains, int batch_num) {
+  if (!chains) return;
+  if (!reaper_enabled()) {
+    freeChainsRecordChains(chains, batch_num);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!started_) {
+      started_ = true;
+      th_ = std::thread([this] { run(); });
+    }
+    q_.emplace_back(chains, batch_num);
+  }
+  cv_.notify_one();
+}
+
+void ChainReaper::drain() {
+  std::unique_lock<std::mutex> g(mu_);
+  idle_.wait(g, [this] { return q_.empty() && !busy_; });
+}
+
+void ChainReaper::run() {
+  std::unique_lock<std::mutex> g(mu_);
+  for (;;) {
+    cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+    if (q_.empty()) return;  // stop_ and nothing left
+    auto job = q_.front();
+    q_.pop_front();
+    busy_ = true;
+    g.unlock();
+    freeChainsRecordChains(job.first, job.second);
+    g.lock();
+    busy_ = false;
+    if (q_.empty()) idle_.notify_all();
+  }
+}
+
 // ------------------------------------------------------- ChainsToRegionsGPU
 RegionsRecord ChainsToRegionsGPU::on_cpu(const ChainsRecord& rec) {
   // finishUpOnCPU (FPGAPipeline.cpp:526-551): the whole record goes through
@@ -273,7 +329,10 @@ RegionsRecord ChainsToRegionsGPU::on_cpu(const ChainsRecord& rec) {
 void ChainsToRegionsGPU::retire() {
   // the last accelerator worker switches the CPU stage's accx dispatch off
   // (FPGAPipeline.cpp:402-405, 528-529): queued records drain back to the CPU
-  if (--n_active_ == 0 && cpu_stage_) cpu_stage_->setUseAccx(false);
+  if (--n_active_ == 0) {
+    reaper_.drain();  // the stage is done when its chains are freed
+    if (cpu_stage_) cpu_stage_->setUseAccx(false);
+  }
 }
 
 void ChainsToRegionsGPU::compute(int wid) {
@@ -368,7 +427,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     out.batch_num = j.rec.batch_num;
     out.seqs = j.rec.seqs;
     out.alnreg = j.flat.unpack(j.rec.batch_num);
-    freeChainsRecordChains(j.rec.chains, j.rec.batch_num);
+    reaper_.release(j.rec.chains, j.rec.batch_num);
     out.chains = nullptr;
     ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     n_gpu_.fetch_add(1);

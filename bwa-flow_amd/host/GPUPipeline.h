@@ -14,7 +14,12 @@
 // bwa_wrapper.cpp:824-830, can free them).
 #pragma once
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "bwagpu.h"
@@ -81,6 +86,29 @@ struct FlatBatch {
 // frees the chains of a record the way ChainsToRegions::compute does
 void freeChainsRecordChains(mem_chain_v* chains, int batch_num);
 
+// One background thread that frees the records' chains (freeChainsRecordChains)
+// in arrival order, so the stage workers do not: the frees go back into the
+// producing stage's glibc arena, and one thread freeing avoids the workers
+// contending for its lock.  drain() returns once everything queued is freed.
+// BWAGPU_CHAIN_REAPER=0 frees inline on the worker instead.
+class ChainReaper {
+ public:
+  ChainReaper() = default;
+  ~ChainReaper();
+  ChainReaper(const ChainReaper&) = delete;
+  ChainReaper& operator=(const ChainReaper&) = delete;
+  void release(mem_chain_v* chains, int batch_num);
+  void drain();
+
+ private:
+  void run();
+  std::mutex mu_;
+  std::condition_variable cv_, idle_;
+  std::deque<std::pair<mem_chain_v*, int>> q_;
+  bool stop_ = false, busy_ = false, started_ = false;
+  std::thread th_;
+};
+
 class ChainsToRegionsGPU
     : public kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH> {
  public:
@@ -105,7 +133,7 @@ class ChainsToRegionsGPU
   // enqueue / dequeue / post totals FPGAPipeline.cpp:557-578 prints):
   // [0] pack (ChainsRecord -> flat arrays), [1] submit (pinned staging + H2D +
   // launches), [2] wait (device time not hidden + D2H), [3] post (malloc'd
-  // mem_alnreg_v + freeing the chains)
+  // mem_alnreg_v + freeing the chains, or handing them to the reaper)
   void phase_seconds(double out[4]) const {
     for (int i = 0; i < 4; ++i) out[i] = (double)ns_[i].load() * 1e-9;
   }
@@ -120,4 +148,5 @@ class ChainsToRegionsGPU
   std::atomic<int> n_gpu_{0}, n_cpu_{0}, n_failed_{0};
   std::atomic<int> per_worker_[kMaxWorkers] = {};
   std::atomic<long long> ns_[4] = {};
+  ChainReaper reaper_;
 };

@@ -54,7 +54,7 @@ extern "C" {
 
 // Runs reps x n_batches records through the stage on up to max_devices
 // devices with per_device stage workers (bwagpu contexts) on each.  times[0] = wall seconds from the first record in to the last
-// record out, times[1..4] = the stage's phase totals (pack, submit, wait,
+// record out and the stage's last chain freed, times[1..4] = the stage's phase totals (pack, submit, wait,
 // post; summed over workers), times[5] = records on the GPU, times[6] =
 // records the CPU fallback took, times[7] = stage workers (contexts) used.  The regions of the
 // LAST rep of batch k go to out_n[k][r] / out_regs[k] (compact, read order).
@@ -115,7 +115,8 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
   for (auto& r : recs) in->push(r);
   pipe.closeInput();
   consumer.join();
-  pipe.wait();
+  pipe.wait();  // the workers are done, and the last one drained the stage's chain frees
+  t_end = std::max(t_end, std::chrono::steady_clock::now());
   times[0] = std::chrono::duration<double>(t_end - t0).count();
   stage.phase_seconds(times + 1);
   times[5] = stage.records_on_gpu();
