@@ -346,11 +346,15 @@ void ChainsToRegionsGPU::compute(int wid) {
   // extension round and the redo pass — overlaps the next batches' kernels):
   // record k uses slot k % BWAGPU_NUM_SLOTS; waits are FIFO, so that slot is
   // free again
+  // one FlatBatch per slot, reused record after record: its vectors keep their
+  // capacity, so packing and the region copy-back write into pages already
+  // faulted in (a fresh 40-MB set per record cost page faults on every byte)
   struct Job {
     ChainsRecord rec;
-    FlatBatch flat;
+    FlatBatch* flat;
     int slot;
   };
+  std::vector<FlatBatch> flats(BWAGPU_NUM_SLOTS);
   std::deque<Job> inflight;
   long long submitted = 0;
   bool more = true;
@@ -378,12 +382,13 @@ void ChainsToRegionsGPU::compute(int wid) {
         if (!ready) more = false;
       }
       if (ready) {
-        inflight.push_back(Job{rec, FlatBatch{}, (int)(submitted % BWAGPU_NUM_SLOTS)});
+        const int sl = (int)(submitted % BWAGPU_NUM_SLOTS);
+        inflight.push_back(Job{rec, &flats[sl], sl});
         Job& j = inflight.back();
         auto t0 = std::chrono::steady_clock::now();
-        j.flat.pack(j.rec);
+        j.flat->pack(j.rec);
         auto t1 = std::chrono::steady_clock::now();
-        const int rc = bwagpu_chain2aln_submit(ctx, j.slot, &j.flat.c);
+        const int rc = bwagpu_chain2aln_submit(ctx, j.slot, &j.flat->c);
         ns_[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
         ns_[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
         if (rc == BWAGPU_E_UNSUPPORTED || rc == BWAGPU_E_INVAL) {
@@ -408,7 +413,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     }
     Job& j = inflight.front();
     auto t0 = std::chrono::steady_clock::now();
-    const int rc = bwagpu_chain2aln_wait(ctx, j.slot, j.flat.regs.data(), j.flat.n.data());
+    const int rc = bwagpu_chain2aln_wait(ctx, j.slot, j.flat->regs.data(), j.flat->n.data());
     auto t1 = std::chrono::steady_clock::now();
     ns_[2] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     if (rc == BWAGPU_E_RESULTS) {
@@ -426,7 +431,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     out.start_idx = j.rec.start_idx;
     out.batch_num = j.rec.batch_num;
     out.seqs = j.rec.seqs;
-    out.alnreg = j.flat.unpack(j.rec.batch_num);
+    out.alnreg = j.flat->unpack(j.rec.batch_num);
     reaper_.release(j.rec.chains, j.rec.batch_num);
     out.chains = nullptr;
     ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
