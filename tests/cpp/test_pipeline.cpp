@@ -19,6 +19,11 @@
 //   mode gpu_badrid the sole stage, record 1 holding a chain outside its
 //                   contig: the error path (reported, chain skipped), the
 //                   device stays in service
+//   mode reaper     no stage: every record's chains go through a ChainReaper
+//                   (the GPU stage's background frees) from cpu_workers
+//                   threads at once; after drain() the heap must be back to
+//                   its size before the records were built
+#include <malloc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -83,13 +88,15 @@ int main(int argc, char** argv) {
 
   // ChainsRecords with malloc'd chains/seeds (the stages free them)
   std::vector<bseq1_t> seqs(n_reads > 0 ? n_reads : 1);
+  std::vector<ChainsRecord> recs;
+  recs.reserve((size_t)(n_reads / std::max(per_rec, 1) + 1));
+  const size_t heap0 = mallinfo2().uordblks;
   for (int r = 0; r < n_reads; ++r) {
     memset(&seqs[r], 0, sizeof(bseq1_t));
     seqs[r].l_seq = (int)(seq_off[r + 1] - seq_off[r]);
     seqs[r].id = r;
     seqs[r].seq = (char*)seq.data() + seq_off[r];
   }
-  std::vector<ChainsRecord> recs;
   for (int r0 = 0; r0 < n_reads; r0 += per_rec) {
     const int nb = std::min(per_rec, n_reads - r0);
     ChainsRecord rec{};
@@ -119,6 +126,27 @@ int main(int argc, char** argv) {
       }
     }
     recs.push_back(rec);
+  }
+
+  if (mode == "reaper") {
+    const size_t heap1 = mallinfo2().uordblks;
+    size_t released = 0;
+    {
+      ChainReaper reaper;
+      std::vector<std::thread> th;
+      const int t = std::max(cpu_workers, 1);
+      for (int k = 0; k < t; ++k)
+        th.emplace_back([&, k] {
+          for (size_t i = (size_t)k; i < recs.size(); i += (size_t)t) reaper.release(recs[i].chains, recs[i].batch_num);
+        });
+      for (auto& x : th) x.join();
+      reaper.drain();
+      released = recs.size();
+      const size_t heap2 = mallinfo2().uordblks;
+      printf("{\"records\": %zu, \"built_bytes\": %zu, \"left_bytes\": %lld}\n", released, heap1 - heap0,
+             (long long)heap2 - (long long)heap0);
+    }  // ~ChainReaper joins its thread
+    return 0;
   }
 
   // CPU body: the oracle over one read (its chains in order, like the loop

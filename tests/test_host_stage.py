@@ -68,6 +68,26 @@ def test_pipeline_cpu_paths(exe, tmp_path, mode, per_rec, workers):
     check(regs, n, want_regs, want_n)
 
 
+@pytest.mark.parametrize("inline", [False, True])
+def test_chain_reaper_frees_every_record(exe, tmp_path, inline):
+    """ChainReaper (host/GPUPipeline.cpp): the GPU stage's background frees of
+    the records' chains, released from 4 threads at once; after drain() the
+    heap is back to its size before the records were built.  BWAGPU_CHAIN_REAPER=0
+    frees inline in release()."""
+    d = str(tmp_path)
+    b, _, _ = write_inputs(d, "c1_default")
+    env = dict(os.environ, BWAGPU_CHAIN_REAPER="0" if inline else "1")
+    p = subprocess.run([exe, d, "reaper", "37", "4"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr
+    info = json.loads(p.stdout.strip().splitlines()[-1])
+    assert info["records"] == -(-b.n_reads // 37)
+    # what may stay "in use" after the frees: the reaper's queue nodes and the
+    # chunks glibc parks in the freeing thread's tcache (at most 7 per size
+    # class); a leak would leave about all of built_bytes
+    assert info["built_bytes"] > 400_000
+    assert info["left_bytes"] < min(256 * 1024, info["built_bytes"] // 2), info
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_default", "c5_mixed"])
 @pytest.mark.parametrize("mode", ["gpu", "gpu_only"])
