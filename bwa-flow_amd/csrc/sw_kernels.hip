@@ -2677,7 +2677,10 @@ __device__ __forceinline__ bwagpu_seed_t uni_seed(const bwagpu_seed_t& s) {
 }
 
 // Extension tasks of one list (round * kSpecBins + bin): one wave per task,
-// claimed two at a time from the sharded queue.
+// claimed BWAGPU_EXT_CLAIM at a time from the sharded queue.
+#ifndef BWAGPU_EXT_CLAIM
+#define BWAGPU_EXT_CLAIM 1
+#endif
 template <int C>
 __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
                                                           int tb_bytes) {
@@ -2691,8 +2694,8 @@ __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, 
   qq.init(a.qh + 8 * kQHStride * list, n);
   long long spec_cells = 0;
   int m0, cap;
-  while (qq.claim(2, m0, cap)) {
-    for (int m = m0; m < m0 + 2 && m < cap; ++m) {
+  while (qq.claim(BWAGPU_EXT_CLAIM, m0, cap)) {
+    for (int m = m0; m < m0 + BWAGPU_EXT_CLAIM && m < cap; ++m) {
       const int2 tk = tl[qq.shard + 8 * m];
       const int pos = uni(tk.x), c = uni(tk.y);
       const int rd = uni(a.chain_read[c]);
