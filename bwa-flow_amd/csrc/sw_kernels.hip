@@ -2820,8 +2820,8 @@ __global__ void __launch_bounds__(kBlock) stream_ext_kernel(DevOpt o, DevRef ref
   ShardQ qq;
   qq.init(a.ctr + kStrHeads + 8 * kQHStride * bin, n);
   int m0, cap;
-  while (qq.claim(2, m0, cap)) {
-    for (int m = m0; m < m0 + 2 && m < cap; ++m) {
+  while (qq.claim(BWAGPU_EXT_CLAIM, m0, cap)) {
+    for (int m = m0; m < m0 + BWAGPU_EXT_CLAIM && m < cap; ++m) {
       const int t = uni(L[qq.shard + 8 * m]);
       const StreamTask& T = a.tasks[t];
       const bwagpu_seed_t s = uni_seed(T.s);
