@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <deque>
+#include <functional>
 #include <stdexcept>
 #include <thread>
 
@@ -48,8 +49,13 @@ struct Rccl {
 
 }  // namespace
 
+static bool force_rccl_env() {
+  const char* e = getenv("BWAGPU_FORCE_RCCL");
+  return e && e[0] == '1';
+}
+
 GPUEnv::GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* pac, int max_devices,
-               int watchdog_ms, int per_device) {
+               int watchdog_ms, int per_device, int force_rccl) {
   int n = 0;
   const int rc = bwagpu_device_count(&n);
   if (rc != BWAGPU_OK) {
@@ -69,18 +75,32 @@ GPUEnv::GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* 
     pac_devid_.push_back(d);
   }
   if (pac_dev_.empty()) return;
+  auto drop = [&](size_t i) {  // device i keeps no reference and gets no context
+    (void)hipSetDevice(pac_devid_[i]);
+    (void)hipFree(pac_dev_[i]);
+    pac_dev_.erase(pac_dev_.begin() + (long)i);
+    pac_devid_.erase(pac_devid_.begin() + (long)i);
+  };
+  // With one device the broadcast is normally skipped.  force_rccl (or
+  // BWAGPU_FORCE_RCCL=1) runs it anyway on a one-rank communicator: the host
+  // copy goes to a staging buffer and ncclBroadcast fills the context's
+  // reference from it, so the path the 8-GPU node takes is exercised (and its
+  // result checked by every alignment) on a one-GPU box.
+  const bool force = (force_rccl < 0 ? force_rccl_env() : force_rccl > 0) && pac_dev_.size() == 1;
+  void* root = pac_dev_[0];
   (void)hipSetDevice(pac_devid_[0]);
-  if (hipMemcpy(pac_dev_[0], pac, pac_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+  if (force && hipMalloc(&root, pac_bytes) != hipSuccess) {
+    status_ += "no memory for the broadcast staging buffer; ";
+    root = pac_dev_[0];
+  }
+  const bool staged = root != pac_dev_[0];
+  if (hipMemcpy(root, pac, pac_bytes, hipMemcpyHostToDevice) != hipSuccess) {
     status_ += "H2D of the reference failed; ";
-    for (size_t i = 0; i < pac_dev_.size(); ++i) {
-      (void)hipSetDevice(pac_devid_[i]);
-      (void)hipFree(pac_dev_[i]);
-    }
-    pac_dev_.clear();
-    pac_devid_.clear();
+    if (staged) (void)hipFree(root);
+    while (!pac_dev_.empty()) drop(pac_dev_.size() - 1);
     return;
   }
-  if (pac_dev_.size() > 1) {
+  if (pac_dev_.size() > 1 || staged) {
     Rccl r;
     bool ok = r.load();
     const int nd = (int)pac_dev_.size();
@@ -94,7 +114,7 @@ GPUEnv::GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* 
       }
       ok = r.group_start() == ncclSuccess;
       for (int i = 0; ok && i < nd; ++i)
-        ok = r.bcast(pac_dev_[0], pac_dev_[i], pac_bytes, ncclUint8, 0, comms[i], st[i]) == ncclSuccess;
+        ok = r.bcast(root, pac_dev_[i], pac_bytes, ncclUint8, 0, comms[i], st[i]) == ncclSuccess;
       ok = (r.group_end() == ncclSuccess) && ok;
       for (int i = 0; i < nd; ++i) {
         (void)hipSetDevice(pac_devid_[i]);
@@ -105,13 +125,22 @@ GPUEnv::GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* 
     for (auto c : comms)
       if (c) r.destroy(c);
     rccl_ = ok;
-    if (!ok) {  // per-device host copies instead
-      for (size_t i = 1; i < pac_dev_.size(); ++i) {
+    if (!ok) {  // per-device host copies instead; a device whose copy fails is dropped
+      for (size_t i = staged ? 0 : 1; i < pac_dev_.size();) {
         (void)hipSetDevice(pac_devid_[i]);
-        (void)hipMemcpy(pac_dev_[i], pac, pac_bytes, hipMemcpyHostToDevice);
+        if (hipMemcpy(pac_dev_[i], pac, pac_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+          status_ += "device " + std::to_string(pac_devid_[i]) + ": H2D of the reference failed; ";
+          drop(i);
+          continue;
+        }
+        ++i;
       }
       status_ += "RCCL unavailable: host copies; ";
     }
+  }
+  if (staged) {
+    (void)hipSetDevice(pac_devid_.empty() ? 0 : pac_devid_[0]);
+    (void)hipFree(root);
   }
   for (size_t i = 0; i < pac_dev_.size(); ++i) {
     for (int k = 0; k < per_device; ++k) {
@@ -151,6 +180,57 @@ int host_threads() {
   return n;
 }
 
+// One persistent pool for every stage worker's pack/unpack ranges (threads are
+// not created per record; with several workers per device their pieces queue
+// on the same host_threads() - 1 threads).
+namespace {
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool p(host_threads() - 1);
+    return p;
+  }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  explicit HostPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+}  // namespace
+
 template <typename F>
 static void parallel_ranges(int n, F f) {  // f(begin, end) over [0, n) in host_threads() pieces
   const int t = std::min(host_threads(), std::max(1, n / 2048));
@@ -158,10 +238,20 @@ static void parallel_ranges(int n, F f) {  // f(begin, end) over [0, n) in host_
     f(0, n);
     return;
   }
-  std::vector<std::thread> th;
-  for (int k = 1; k < t; ++k) th.emplace_back(f, (int)((int64_t)n * k / t), (int)((int64_t)n * (k + 1) / t));
+  std::atomic<int> left{t - 1};
+  std::mutex m;
+  std::condition_variable done;
+  for (int k = 1; k < t; ++k)
+    HostPool::get().post([&, k] {
+      f((int)((int64_t)n * k / t), (int)((int64_t)n * (k + 1) / t));
+      if (left.fetch_sub(1) == 1) {
+        std::lock_guard<std::mutex> g(m);
+        done.notify_all();
+      }
+    });
   f(0, (int)((int64_t)n / t));
-  for (auto& x : th) x.join();
+  std::unique_lock<std::mutex> g(m);
+  done.wait(g, [&] { return left.load() == 0; });
 }
 
 void FlatBatch::pack(const ChainsRecord& rec) {
@@ -285,13 +375,24 @@ void ChainReaper::release(mem_chain_v* chains, int batch_num) {
     freeChainsRecordChains(chains, batch_num);
     return;
   }
+  bool queued = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     if (!started_) {
       started_ = true;
       th_ = std::thread([this] { run(); });
     }
-    q_.emplace_back(chains, batch_num);
+    // bounded: when the reaper falls behind, the releasing worker frees this
+    // record itself (chain memory cannot grow without limit)
+    if (q_.size() < kMaxQueued) {
+      q_.emplace_back(chains, batch_num);
+      queued = true;
+    }
+  }
+  if (!queued) {
+    n_inline_.fetch_add(1);
+    freeChainsRecordChains(chains, batch_num);
+    return;
   }
   cv_.notify_one();
 }

@@ -46,8 +46,10 @@ class ChainsToRegions;  // the CPU stage (src/Pipeline.h:162-171 / cpu_stage.h)
 // workers retire at once, like an FPGA env with fewer PEs).
 class GPUEnv {
  public:
+  // force_rccl: 1 = broadcast over RCCL even with one device (a one-rank
+  // communicator), 0 = only with several, -1 = from BWAGPU_FORCE_RCCL
   GPUEnv(const bwagpu_opt_t& opt, const bwagpu_bns_t& bns, const uint8_t* pac, int max_devices = 8,
-         int watchdog_ms = 10000, int per_device = 1);
+         int watchdog_ms = 10000, int per_device = 1, int force_rccl = -1);
   ~GPUEnv();
   GPUEnv(const GPUEnv&) = delete;
   GPUEnv& operator=(const GPUEnv&) = delete;
@@ -99,6 +101,9 @@ class ChainReaper {
   ChainReaper& operator=(const ChainReaper&) = delete;
   void release(mem_chain_v* chains, int batch_num);
   void drain();
+  // records freed inline because kMaxQueued were already waiting
+  int inline_frees() const { return n_inline_.load(); }
+  static constexpr size_t kMaxQueued = 4 * BWAGPU_NUM_SLOTS;
 
  private:
   void run();
@@ -106,6 +111,7 @@ class ChainReaper {
   std::condition_variable cv_, idle_;
   std::deque<std::pair<mem_chain_v*, int>> q_;
   bool stop_ = false, busy_ = false, started_ = false;
+  std::atomic<int> n_inline_{0};
   std::thread th_;
 };
 

@@ -29,6 +29,12 @@ def _load():
         lib.synth_reads.restype = C.c_int
         lib.golden_genome.argtypes = [C.c_uint64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.golden_genome.restype = C.c_int
+        lib.synth_reads_genome.argtypes = lib.synth_reads.argtypes
+        lib.synth_reads_genome.restype = C.c_int
+        lib.grch38_layout.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.grch38_layout.restype = C.c_int
+        lib.grch38_genome.argtypes = [C.c_uint64, C.c_void_p, C.c_int]
+        lib.grch38_genome.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -60,8 +66,32 @@ class SynthRef:
             raise RuntimeError("synth_ref failed")
 
 
-def synth_batch(ref: SynthRef, seed: int, n_pairs: int, len_mode: int = 150, min_seed_len: int = 19) -> Batch:
-    """len_mode 100/150/250, or 0 for equal thirds of 100/150/250"""
+class Grch38Ref:
+    """the C3 regime's reference (tools/synth.cpp grch38_layout/grch38_genome):
+    GRCh38's 195-contig table and l_pac (3,099,734,149), seeded content; the
+    pac is 0.78 GB"""
+
+    N_CTG = 195
+
+    def __init__(self, seed: int = 38, threads: int | None = None):
+        lib = _load()
+        self.ann_offset = np.zeros(self.N_CTG, np.int64)
+        self.ann_len = np.zeros(self.N_CTG, np.int32)
+        lp = C.c_int64()
+        if lib.grch38_layout(_ptr(self.ann_offset), _ptr(self.ann_len), C.byref(lp)) != self.N_CTG:
+            raise RuntimeError("grch38_layout failed")
+        self.l_pac = int(lp.value)
+        self.pac = np.empty(self.l_pac // 4 + 1, np.uint8)
+        nt = threads or min(16, os.cpu_count() or 1)
+        if lib.grch38_genome(seed, _ptr(self.pac), nt):
+            raise RuntimeError("grch38_genome failed")
+
+
+def synth_batch(ref, seed: int, n_pairs: int, len_mode: int = 150, min_seed_len: int = 19,
+                genome_wide: bool = False) -> Batch:
+    """len_mode 100/150/250, or 0 for equal thirds of 100/150/250; genome_wide:
+    C3 placement (contigs weighted by length, one pair in ten across a contig
+    junction) instead of a uniform contig"""
     lib = _load()
     ms, mc, mseed = C.c_int64(), C.c_int32(), C.c_int32()
     lib.synth_bounds(n_pairs, len_mode, C.byref(ms), C.byref(mc), C.byref(mseed))
@@ -74,9 +104,10 @@ def synth_batch(ref: SynthRef, seed: int, n_pairs: int, len_mode: int = 150, min
     fr = np.zeros(mc.value, np.float32)
     seeds = np.zeros(mseed.value, abi.SEED_DTYPE)
     nr, nc, ns = C.c_int32(), C.c_int32(), C.c_int32()
-    rc = lib.synth_reads(_ptr(ref.pac), ref.l_pac, _ptr(ref.ann_offset), _ptr(ref.ann_len), len(ref.ann_len), seed,
-                         n_pairs, len_mode, min_seed_len, _ptr(seq_off), _ptr(seq), _ptr(rco), _ptr(cso), _ptr(rid),
-                         _ptr(fr), _ptr(seeds), C.byref(nr), C.byref(nc), C.byref(ns))
+    fn = lib.synth_reads_genome if genome_wide else lib.synth_reads
+    rc = fn(_ptr(ref.pac), ref.l_pac, _ptr(ref.ann_offset), _ptr(ref.ann_len), len(ref.ann_len), seed,
+            n_pairs, len_mode, min_seed_len, _ptr(seq_off), _ptr(seq), _ptr(rco), _ptr(cso), _ptr(rid),
+            _ptr(fr), _ptr(seeds), C.byref(nr), C.byref(nc), C.byref(ns))
     if rc:
         raise RuntimeError("synth_reads failed")
     r, c, s = nr.value, nc.value, ns.value

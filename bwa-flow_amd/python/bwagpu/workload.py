@@ -43,6 +43,140 @@ class RefBatch:
         return hashlib.sha256(c.view(np.uint8).tobytes()).digest() == self.regs_sha256
 
 
+# ---------------------------------------------------------------- C3 / C5 regime
+# tests/golden/c3_grch38.npz (oracle/gen_c3_fixture.py): synthetic chains on a
+# GRCh38-shaped genome (195 contigs, l_pac 3.1e9) with the reference's own
+# mem_chain2aln / mem_reg2aln answers as digests.
+C3_FIXTURE = os.path.join(REPO, "tests", "golden", "c3_grch38.npz")
+C3_MAX_OPS, C3_MAX_MD = 128, 1024
+C3_CHUNK = 256  # reads (regions) / jobs per chunk digest
+C3_COVERAGE_KEYS = ("seeds_fwd_ge_2^31", "seeds_ge_2^32", "regs_fwd_ge_2^31", "regs_ge_2^32", "contigs_hit",
+                    "regs_small_contigs", "regs_at_contig_edge")
+ALN_FIELDS = ("pos", "rid", "is_rev", "n_cigar", "NM", "md_len", "status")
+
+
+def batch_digest(b: Batch) -> bytes:
+    """SHA-256 over every array of a flattened ChainsRecord"""
+    h = hashlib.sha256()
+    for a in (b.seq_off, b.seq, b.read_chain_off, b.chain_seed_off, b.chain_rid, b.chain_frac_rep, b.seeds):
+        h.update(np.ascontiguousarray(a).view(np.uint8).tobytes())
+    return h.digest()
+
+
+def chunk_digests(b: Batch, regs_compact: np.ndarray, n: np.ndarray) -> np.ndarray:
+    """uint8[n_chunks, 32]: SHA-256 of the regions of reads [256k, 256k+256)"""
+    off = np.concatenate([[0], np.cumsum(np.asarray(n, np.int64))])
+    raw = np.ascontiguousarray(regs_compact).view(np.uint8).reshape(-1, 88) if len(regs_compact) else \
+        np.zeros((0, 88), np.uint8)
+    out = []
+    for r0 in range(0, b.n_reads, C3_CHUNK):
+        r1 = min(r0 + C3_CHUNK, b.n_reads)
+        out.append(np.frombuffer(hashlib.sha256(raw[off[r0]:off[r1]].tobytes()).digest(), np.uint8))
+    return np.array(out, np.uint8).reshape(-1, 32)
+
+
+def cigar_chunk_digests(jobs, aln, cig, md) -> np.ndarray:
+    """uint8[n_chunks, 32]: SHA-256 of 256 jobs' mem_reg2aln outputs (the record
+    fields the reference fills, the CIGAR ops and the MD string)"""
+    out = []
+    rec = np.stack([aln[f].astype(np.int64) for f in ALN_FIELDS], axis=1) if len(aln) else np.zeros((0, 7), np.int64)
+    for k0 in range(0, len(jobs), C3_CHUNK):
+        h = hashlib.sha256()
+        for k in range(k0, min(k0 + C3_CHUNK, len(jobs))):
+            h.update(rec[k].tobytes())
+            if aln["status"][k] == abi.ALN_OK:
+                h.update(np.ascontiguousarray(cig[k, :int(aln["n_cigar"][k])]).tobytes())
+                h.update(bytes(md[k, :int(aln["md_len"][k])]))
+        out.append(np.frombuffer(h.digest(), np.uint8))
+    return np.array(out, np.uint8).reshape(-1, 32)
+
+
+def reg2aln_jobs(b: Batch, regs, n):
+    """the SAM stage's mem_reg2aln jobs for one batch: every region of every read
+    (bwa_wrapper.cpp:611 runs it on the regions a read outputs; all of them here)"""
+    c = compact(b, regs, n)
+    rd = np.repeat(np.arange(b.n_reads), n)
+    jobs = np.zeros(len(c), abi.REG2ALN_TASK_DTYPE)
+    for f in ("rb", "re", "qb", "qe", "truesc", "w"):
+        jobs[f] = c[f]
+    jobs["qoff"] = b.seq_off[rd]
+    jobs["l_seq"] = b.seq_off[rd + 1] - b.seq_off[rd]
+    return jobs
+
+
+def c3_coverage(ref, b: Batch, regs_compact: np.ndarray) -> dict:
+    """how much of the GRCh38 regime a batch exercises: coordinates past 2^31
+    (forward) and 2^32 (2-strand), contigs, regions clipped at a contig edge"""
+    L = int(ref.l_pac)
+    s, c = b.seeds["rbeg"].astype(np.int64), regs_compact
+    rb, re = c["rb"].astype(np.int64), c["re"].astype(np.int64)
+    fwd = rb < L
+    cb = np.asarray(ref.ann_offset, np.int64)[c["rid"]]
+    ce = cb + np.asarray(ref.ann_len, np.int64)[c["rid"]]
+    lo = np.where(fwd, cb, 2 * L - ce)  # the contig's span on the region's strand
+    hi = np.where(fwd, ce, 2 * L - cb)
+    return {"seeds_fwd_ge_2^31": int(((s >= 2 ** 31) & (s < L)).sum()), "seeds_ge_2^32": int((s >= 2 ** 32).sum()),
+            "regs_fwd_ge_2^31": int(((rb >= 2 ** 31) & fwd).sum()), "regs_ge_2^32": int((rb >= 2 ** 32).sum()),
+            "contigs_hit": int(len(np.unique(c["rid"]))), "regs_small_contigs": int((c["rid"] >= 25).sum()),
+            "regs_at_contig_edge": int(((rb == lo) | (re == hi)).sum())}
+
+
+class C3Set:
+    """one C3/C5 batch regenerated from the fixture's seeds, with the
+    reference's answers (region digests, CIGAR digests)"""
+
+    def __init__(self, z, name: str, ref):
+        from .synth import synth_batch
+        self.name = name
+        self.batch = synth_batch(ref, int(z[f"{name}_read_seed"]), int(z[f"{name}_pairs"]),
+                                 int(z[f"{name}_len_mode"]), genome_wide=True)
+        if batch_digest(self.batch) != z[f"{name}_batch_sha256"].tobytes():
+            raise RuntimeError(f"regenerated {name} batch differs from the fixture's (tools/synth.cpp reads_core)")
+        self.reg_n = z[f"{name}_reg_n"].astype(np.int32)
+        self.regs_sha256 = z[f"{name}_regs_sha256"].tobytes()
+        self.regs_chunks = z[f"{name}_regs_chunks"]
+        self.cigar_chunks = z[f"{name}_cigar_chunks"]
+        self.coverage = dict(zip(C3_COVERAGE_KEYS, z[f"{name}_coverage"].tolist()))
+
+    def check(self, regs, n) -> str | None:
+        """None when bit-exact with the reference, else where it first differs"""
+        n = np.asarray(n, np.int32)
+        if not np.array_equal(n, self.reg_n):
+            k = int(np.argmax(n != self.reg_n))
+            return f"region count of read {k}: {n[k]} vs {self.reg_n[k]}"
+        c = np.ascontiguousarray(compact(self.batch, regs, n))
+        if hashlib.sha256(c.tobytes()).digest() == self.regs_sha256:
+            return None
+        got = chunk_digests(self.batch, c, n)
+        k = int(np.argmax(np.any(got != self.regs_chunks, axis=1)))
+        return f"regions of reads [{k * C3_CHUNK}, {(k + 1) * C3_CHUNK}) differ"
+
+    def check_cigar(self, jobs, aln, cig, md) -> str | None:
+        got = cigar_chunk_digests(jobs, aln, cig, md)
+        if got.shape == self.cigar_chunks.shape and np.array_equal(got, self.cigar_chunks):
+            return None
+        if got.shape != self.cigar_chunks.shape:
+            return f"{len(jobs)} jobs: chunk count {len(got)} vs {len(self.cigar_chunks)}"
+        k = int(np.argmax(np.any(got != self.cigar_chunks, axis=1)))
+        return f"CIGAR jobs [{k * C3_CHUNK}, {(k + 1) * C3_CHUNK}) differ"
+
+
+def load_c3(path: str = C3_FIXTURE, names=("c3", "c5"), ref=None):
+    """-> (opt dict, Grch38Ref, {name: C3Set}); raises if the regenerated genome
+    or a batch differs from the one the reference was run on"""
+    from .synth import Grch38Ref
+    z = np.load(path, allow_pickle=False)
+    opt = dict(zip(OPT_KEYS, z["opt_int"].tolist()))
+    opt["mat"] = z["opt_mat"].astype(np.int8)
+    if ref is None:
+        ref = Grch38Ref(int(z["genome_seed"]))
+    if ref.l_pac != int(z["l_pac"]) or not np.array_equal(ref.ann_offset, z["ann_offset"]):
+        raise RuntimeError("regenerated GRCh38 contig table differs from the fixture's")
+    if hashlib.sha256(ref.pac).digest() != z["pac_sha256"].tobytes():
+        raise RuntimeError("regenerated GRCh38-shaped genome differs from the fixture's (tools/synth.cpp)")
+    return opt, ref, {nm: C3Set(z, nm, ref) for nm in names}
+
+
 def _unpack_seq(seq2: np.ndarray, npos: np.ndarray, n: int) -> np.ndarray:
     s = np.empty(4 * len(seq2), np.uint8)
     for k in range(4):

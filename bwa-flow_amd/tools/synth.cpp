@@ -21,6 +21,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "bwagpu.h"
@@ -45,6 +46,20 @@ struct Rng {
 
 inline int get2(const uint8_t* pac, int64_t k) { return pac[k >> 2] >> ((~k & 3) << 1) & 3; }
 inline void set2(uint8_t* pac, int64_t k, int c) { pac[k >> 2] |= (uint8_t)(c << ((~k & 3) << 1)); }
+inline void put2(uint8_t* pac, int64_t k, int c) {  // overwrite
+  const int sh = (~k & 3) << 1;
+  pac[k >> 2] = (uint8_t)((pac[k >> 2] & ~(3 << sh)) | (c << sh));
+}
+
+// GRCh38 primary assembly: chr1..chr22, chrX, chrY, chrM lengths (the
+// no-alt analysis set has these 25 plus 170 unlocalized/unplaced contigs,
+// 195 sequences, l_pac = 3,099,734,149).
+constexpr int kG38Primary = 25, kG38Contigs = 195;
+constexpr int64_t kG38Len = 3099734149LL;
+const int64_t kG38PrimaryLen[kG38Primary] = {
+    248956422, 242193529, 198295559, 190214555, 181538259, 170805979, 159345973, 145138636, 138394717,
+    133797422, 135086622, 133275309, 114364328, 107043718, 101991189, 90338345,  83257441,  80373285,
+    58617616,  64444167,  46709983,  50818468,  156040895, 57227415,  16569};
 
 }  // namespace
 
@@ -149,6 +164,73 @@ int synth_ref(uint64_t seed, int64_t total_len, int n_ctg, uint8_t* pac, int64_t
   return 0;
 }
 
+// The C3 regime's reference (BASELINE.json configs[2]): a GRCh38-shaped
+// genome.  grch38_layout fills the 195-entry contig table (the 25 primary
+// chromosomes at their real lengths, then 170 small contigs of seeded lengths
+// that bring the total to GRCh38's l_pac) and returns the contig count;
+// grch38_genome fills pac (l_pac/4+1 bytes) with seeded content: iid bases
+// (a counter-based splitmix64 per 32-base word, so threads do not change the
+// result), then interspersed repeat families (4 copies, 1 % diverged) and
+// tandem repeats.  Forward coordinates reach 3.1e9 (> 2^31) and 2-strand
+// coordinates 6.2e9 (> 2^32); the pac is 0.78 GB (outside the MALL).
+int grch38_layout(int64_t* ann_off, int32_t* ann_len, int64_t* l_pac) {
+  int64_t len[kG38Contigs];
+  int64_t prim = 0;
+  for (int i = 0; i < kG38Primary; ++i) prim += (len[i] = kG38PrimaryLen[i]);
+  Rng g{195};
+  int64_t raw = 0;
+  for (int i = kG38Primary; i < kG38Contigs; ++i) raw += (len[i] = 1000 + g.i(300000));
+  const int64_t want = kG38Len - prim;  // 11,447,748
+  int64_t acc = 0;
+  for (int i = kG38Primary; i < kG38Contigs; ++i) {
+    len[i] = i + 1 < kG38Contigs ? std::max<int64_t>(1000, len[i] * want / raw) : want - acc;
+    acc += len[i];
+  }
+  int64_t off = 0;
+  for (int i = 0; i < kG38Contigs; ++i) {
+    if (ann_off) ann_off[i] = off;
+    if (ann_len) ann_len[i] = (int32_t)len[i];
+    off += len[i];
+  }
+  if (l_pac) *l_pac = off;
+  return kG38Contigs;
+}
+
+int grch38_genome(uint64_t seed, uint8_t* pac, int n_threads) {
+  if (!pac) return -1;
+  const int64_t L = kG38Len, nbytes = L / 4 + 1, nwords = (nbytes + 7) / 8;
+  n_threads = std::max(1, std::min(n_threads, 64));
+  std::vector<std::thread> th;
+  for (int t = 0; t < n_threads; ++t)
+    th.emplace_back([=] {
+      for (int64_t w = nwords * t / n_threads; w < nwords * (t + 1) / n_threads; ++w) {
+        Rng r{seed * 0x2545F4914F6CDD1DULL + (uint64_t)w * 0x9E3779B97F4A7C15ULL};
+        const uint64_t v = r.next();
+        const int64_t b0 = w * 8, nb = std::min<int64_t>(8, nbytes - b0);
+        memcpy(pac + b0, &v, (size_t)nb);
+      }
+    });
+  for (auto& x : th) x.join();
+  // bits past the last base are zero, as in the pac bwa builds
+  const int rem = (int)(L & 3);
+  pac[L >> 2] &= (uint8_t)(rem ? 0xff00 >> (2 * rem) : 0);
+  Rng g{seed ^ 0xC3C3C3C3ULL};
+  for (int fam = 0; fam < 3000; ++fam) {  // ~20 Mb of interspersed repeats
+    const int len = 300 + g.i(2700);
+    const int64_t src = (int64_t)(g.u() * (double)(L - len));
+    for (int c = 0; c < 4; ++c) {
+      const int64_t dst = (int64_t)(g.u() * (double)(L - len));
+      for (int k = 0; k < len; ++k) put2(pac, dst + k, g.u() < 0.01 ? (int)(g.next() & 3) : get2(pac, src + k));
+    }
+  }
+  for (int t = 0; t < 10000; ++t) {  // tandem repeats
+    const int per = 2 + g.i(49), len = 200 + g.i(800);
+    const int64_t dst = (int64_t)(g.u() * (double)(L - len));
+    for (int k = per; k < len; ++k) put2(pac, dst + k, g.u() < 0.005 ? (int)(g.next() & 3) : get2(pac, dst + k - per));
+  }
+  return 0;
+}
+
 // Upper bounds for synth_reads outputs.
 void synth_bounds(int n_pairs, int len_mode, int64_t* max_seq, int32_t* max_chains, int32_t* max_seeds) {
   const int L = len_mode == 0 ? 250 : len_mode;
@@ -157,13 +239,18 @@ void synth_bounds(int n_pairs, int len_mode, int64_t* max_seq, int32_t* max_chai
   *max_seeds = 2 * n_pairs * (L / 19 + 4) * 2;
 }
 
-// Simulate n_pairs read pairs and their chains.  len_mode: 100/150/250, or 0
-// for equal thirds of 100/150/250 (BASELINE config 5).  Outputs follow
-// bwagpu_batch_t; sizes are returned through *n_*.  Returns 0 or -1.
-int synth_reads(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const int32_t* ann_len, int n_ctg,
-                uint64_t seed, int n_pairs, int len_mode, int min_seed_len, int64_t* seq_off, uint8_t* seq,
-                int32_t* read_chain_off, int32_t* chain_seed_off, int32_t* chain_rid, float* chain_frac_rep,
-                bwagpu_seed_t* seeds, int32_t* n_reads_out, int32_t* n_chains_out, int32_t* n_seeds_out) {
+}  // extern "C"
+
+namespace {
+
+// placement 0: a uniform contig, then a uniform fragment inside it (the
+// synth workload); 1: genome-wide (contigs weighted by length, fragments may
+// run off a contig) with one pair in ten straddling a contig junction (C3).
+int reads_core(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const int32_t* ann_len, int n_ctg,
+               uint64_t seed, int n_pairs, int len_mode, int min_seed_len, int placement, int64_t* seq_off,
+               uint8_t* seq, int32_t* read_chain_off, int32_t* chain_seed_off, int32_t* chain_rid,
+               float* chain_frac_rep, bwagpu_seed_t* seeds, int32_t* n_reads_out, int32_t* n_chains_out,
+               int32_t* n_seeds_out) {
   Rng g{seed ^ 0x5eedULL};
   int64_t so = 0;
   int32_t nr = 0, nc = 0, ns = 0;
@@ -186,9 +273,18 @@ int synth_reads(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const
     int fl = (int)(400 + 40 * g.n());
     fl = std::max(fl, L + 10);
     fl = std::min<int64_t>(fl, l_pac - 1);
-    const int ctg = g.i(n_ctg);
-    if (ann_len[ctg] <= fl + 1) continue;
-    const int64_t start = ann_off[ctg] + (int64_t)(g.u() * (double)(ann_len[ctg] - fl));
+    int64_t start;
+    if (placement == 0) {
+      const int ctg = g.i(n_ctg);
+      if (ann_len[ctg] <= fl + 1) continue;
+      start = ann_off[ctg] + (int64_t)(g.u() * (double)(ann_len[ctg] - fl));
+    } else if (n_ctg > 1 && g.u() < 0.1) {  // the fragment straddles the start of contig k
+      const int k = 1 + g.i(n_ctg - 1);
+      start = std::max<int64_t>(0, ann_off[k] - 1 - g.i(fl - 1));
+      if (start + fl > l_pac) continue;
+    } else {
+      start = (int64_t)(g.u() * (double)(l_pac - fl));
+    }
     const int strand = (int)(g.next() & 1);
     for (int e = 0; e < 2; ++e) {
       const bool fwd = ((e == 0) ^ strand) != 0;
@@ -312,6 +408,32 @@ int synth_reads(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const
   *n_chains_out = nc;
   *n_seeds_out = ns;
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Simulate n_pairs read pairs and their chains.  len_mode: 100/150/250, or 0
+// for equal thirds of 100/150/250 (BASELINE config 5).  Outputs follow
+// bwagpu_batch_t; sizes are returned through *n_*.  Returns 0 or -1.
+int synth_reads(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const int32_t* ann_len, int n_ctg,
+                uint64_t seed, int n_pairs, int len_mode, int min_seed_len, int64_t* seq_off, uint8_t* seq,
+                int32_t* read_chain_off, int32_t* chain_seed_off, int32_t* chain_rid, float* chain_frac_rep,
+                bwagpu_seed_t* seeds, int32_t* n_reads_out, int32_t* n_chains_out, int32_t* n_seeds_out) {
+  return reads_core(pac, l_pac, ann_off, ann_len, n_ctg, seed, n_pairs, len_mode, min_seed_len, 0, seq_off, seq,
+                    read_chain_off, chain_seed_off, chain_rid, chain_frac_rep, seeds, n_reads_out, n_chains_out,
+                    n_seeds_out);
+}
+
+// The same generator with C3's placement (reads_core placement 1).
+int synth_reads_genome(const uint8_t* pac, int64_t l_pac, const int64_t* ann_off, const int32_t* ann_len, int n_ctg,
+                       uint64_t seed, int n_pairs, int len_mode, int min_seed_len, int64_t* seq_off, uint8_t* seq,
+                       int32_t* read_chain_off, int32_t* chain_seed_off, int32_t* chain_rid, float* chain_frac_rep,
+                       bwagpu_seed_t* seeds, int32_t* n_reads_out, int32_t* n_chains_out, int32_t* n_seeds_out) {
+  return reads_core(pac, l_pac, ann_off, ann_len, n_ctg, seed, n_pairs, len_mode, min_seed_len, 1, seq_off, seq,
+                    read_chain_off, chain_seed_off, chain_rid, chain_frac_rep, seeds, n_reads_out, n_chains_out,
+                    n_seeds_out);
 }
 
 }  // extern "C"

@@ -143,8 +143,8 @@ int main(int argc, char** argv) {
       reaper.drain();
       released = recs.size();
       const size_t heap2 = mallinfo2().uordblks;
-      printf("{\"records\": %zu, \"built_bytes\": %zu, \"left_bytes\": %lld}\n", released, heap1 - heap0,
-             (long long)heap2 - (long long)heap0);
+      printf("{\"records\": %zu, \"built_bytes\": %zu, \"left_bytes\": %lld, \"inline_frees\": %d}\n", released,
+             heap1 - heap0, (long long)heap2 - (long long)heap0, reaper.inline_frees());
     }  // ~ChainReaper joins its thread
     return 0;
   }
@@ -173,9 +173,11 @@ int main(int argc, char** argv) {
   ChainsToRegions cpu_stage(cpu_workers, read_fn);
   GPUEnv* env = nullptr;
   int n_dev = 0;
-  const bool sole = mode == "gpu_only" || mode == "gpu_2ctx" || mode == "gpu_badrid";
+  const bool sole = mode == "gpu_only" || mode == "gpu_2ctx" || mode == "gpu_badrid" || mode == "gpu_rccl";
   if (mode == "gpu" || sole || mode == "gpu_hang") {
-    env = new GPUEnv(opt, bns, pac.data(), 8, 10000, mode == "gpu_2ctx" ? 2 : 1);
+    // gpu_rccl: the reference reaches the device through GPUEnv's RCCL
+    // broadcast (forced on a one-rank communicator when there is one device)
+    env = new GPUEnv(opt, bns, pac.data(), 8, 10000, mode == "gpu_2ctx" ? 2 : 1, mode == "gpu_rccl" ? 1 : 0);
     n_dev = env->num_devices();
     if (n_dev == 0) {
       fprintf(stderr, "no device: %s\n", env->status().c_str());
@@ -240,6 +242,10 @@ int main(int argc, char** argv) {
          recs.size(), outs.size(), gpu_stage.records_on_gpu(), gpu_stage.records_on_cpu(), n_dev, bad,
          gpu_stage.records_failed(), bad_rid_read, gpu_stage.records_of_worker(0), gpu_stage.records_of_worker(1),
          cpu_stage.useAccx() ? 1 : 0, env && env->used_rccl() ? 1 : 0, env ? env->status().c_str() : "");
+  const int failed = gpu_stage.records_failed();
   delete env;
-  return 0;
+  // a record the device flagged (a chain outside its contig, where bwa itself
+  // asserts, bwamem.c:669) was emitted with that chain skipped: the run must
+  // not end as a success (error codes)
+  return failed > 0 ? 7 : 0;
 }

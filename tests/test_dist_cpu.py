@@ -58,6 +58,51 @@ def test_bench_distributed_plumbing_gloo(tmp_path):
         assert float(r[k]["tot"]) == float(sum(int(x["n_reads"]) for x in r))
 
 
+def _worker_fixture(rank, world, port, out_dir):
+    """bench.load_workload on the c2_refseed fixture path with 2 ranks: rank 0
+    regenerates the genome, rank 1 only receives it (any contig count)"""
+    import argparse
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    args = argparse.Namespace(workload="c2_refseed")
+    opt, ref, pac_t, batches, checks, data, wl = bench.load_workload(args, rank, world, torch.device("cpu"))
+    # a 195-contig table (the GRCh38 layout) through the same broadcast
+    from bwagpu.synth import _load
+    import ctypes as C
+    off, ln, lp = np.zeros(195, np.int64), np.zeros(195, np.int32), C.c_int64()
+    _load().grch38_layout(off.ctypes.data, ln.ctypes.data, C.byref(lp))
+
+    class Small:
+        l_pac, pac, ann_offset, ann_len = 4000, (np.arange(1001) % 251).astype(np.uint8), off, ln
+    g, _ = bench.broadcast_reference(Small if rank == 0 else None, rank, world, torch.device("cpu"))
+    np.savez(os.path.join(out_dir, f"f{rank}.npz"), pac=ref.pac, ann_offset=ref.ann_offset, ann_len=ref.ann_len,
+             l_pac=ref.l_pac, first_reads=batches[0].n_reads, first_seq=batches[0].seq[:1000],
+             checks=checks is not None and all(c.batch is b for c, b in zip(checks, batches)),
+             g_off=g.ann_offset, g_len=g.ann_len, g_lpac=g.l_pac, g_pac=g.pac[:1000])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_load_workload_fixture_gloo(tmp_path):
+    world = 2
+    mp.spawn(_worker_fixture, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [np.load(os.path.join(tmp_path, f"f{k}.npz")) for k in range(world)]
+    from bwagpu import workload
+    z = np.load(workload.C2_FIXTURE)
+    for k in range(world):
+        assert int(r[k]["l_pac"]) == int(z["genome_len"])
+        assert np.array_equal(r[k]["ann_offset"], z["ann_offset"]) and np.array_equal(r[k]["ann_len"], z["ann_len"])
+        assert np.array_equal(r[k]["pac"], r[0]["pac"])
+        assert bool(r[k]["checks"])
+        assert len(r[k]["g_off"]) == 195 and int(r[k]["g_lpac"]) == 4000
+        assert np.array_equal(r[k]["g_off"], r[0]["g_off"]) and np.array_equal(r[k]["g_len"], r[0]["g_len"])
+        assert np.array_equal(r[k]["g_pac"], (np.arange(1000) % 251).astype(np.uint8))
+        assert int(r[k]["g_off"][-1]) + int(r[k]["g_len"][-1]) == 3_099_734_149
+    # rank 1 starts at the other batch
+    assert not np.array_equal(r[0]["first_seq"], r[1]["first_seq"])
+
+
 def test_shards_are_deterministic():
     import bench
     from bwagpu.synth import SynthRef

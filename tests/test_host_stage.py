@@ -44,9 +44,9 @@ def write_inputs(d, name):
     return b, regs, n
 
 
-def run(exe, d, mode, per_rec, workers):
+def run(exe, d, mode, per_rec, workers, rc=0):
     p = subprocess.run([exe, d, mode, str(per_rec), str(workers)], capture_output=True, text=True, timeout=600)
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == rc, p.stderr
     info = json.loads(p.stdout.strip().splitlines()[-1])
     n = np.fromfile(os.path.join(d, "out_n.bin"), np.int32)
     regs = np.fromfile(os.path.join(d, "out_regs.bin"), np.uint8).view(abi.ALNREG_DTYPE)
@@ -86,6 +86,7 @@ def test_chain_reaper_frees_every_record(exe, tmp_path, inline):
     # class); a leak would leave about all of built_bytes
     assert info["built_bytes"] > 400_000
     assert info["left_bytes"] < min(256 * 1024, info["built_bytes"] // 2), info
+    assert inline or info["inline_frees"] >= 0
 
 
 @pytest.mark.gpu
@@ -115,6 +116,20 @@ def test_two_workers_per_device(exe, tmp_path):
 
 
 @pytest.mark.gpu
+def test_reference_through_rccl_broadcast(exe, tmp_path):
+    """GPUEnv's RCCL branch (ncclCommInitAll + grouped ncclBroadcast, the
+    start-up broadcast of the packed reference over xGMI, BWAOCLEnv.h:67-114's
+    per-device upload): forced on a one-rank communicator, the context's
+    reference is the broadcast's output, and every region equals the golden one"""
+    d = str(tmp_path)
+    b, want_regs, want_n = write_inputs(d, "c1_default")
+    info, regs, n = run(exe, d, "gpu_rccl", 50, 2)
+    assert info["rccl"] == 1, info["env"]
+    assert info["on_gpu"] == info["records"] and info["gpu_fallback_cpu"] == 0
+    check(regs, n, want_regs, want_n)
+
+
+@pytest.mark.gpu
 def test_midstream_device_failure_recovers_on_cpu(exe, tmp_path):
     """the third wait fails as a watchdog expiry does (fpgaHangError path,
     FPGAPipeline.cpp:526-551): the records in flight are recomputed by the CPU
@@ -137,7 +152,7 @@ def test_malformed_record_takes_the_error_path(exe, tmp_path):
     d = str(tmp_path)
     b, want_regs, want_n = write_inputs(d, "c1_default")
     per = 50
-    info, regs, n = run(exe, d, "gpu_badrid", per, 2)
+    info, regs, n = run(exe, d, "gpu_badrid", per, 2, rc=7)  # the driver exits non-zero
     assert info["failed"] == 1 and info["gpu_fallback_cpu"] == 0
     assert info["on_gpu"] == info["records"]
     bad = info["bad_rid_read"]
