@@ -96,13 +96,15 @@ struct Slot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
-  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc;
+  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks;
   SpecStreams spec;  // created on first use
   void release_scratch() {
     d_win.release(); d_srt.release(); d_prog.release(); d_desc.release(); d_lists.release(); d_counts.release();
     d_cread.release(); d_ext.release(); d_tasks.release(); d_ctr.release(); d_regpos.release(); d_skipf.release();
     d_heavy.release(); d_redo.release(); d_schain.release(); d_hinfo.release(); d_mat.release(); d_cov.release(); d_colent.release(); d_longc.release();
     d_qh.release();
+    d_sorth.release();
+    d_stasks.release();
     if (spec.side) (void)hipStreamSynchronize(spec.side);
     if (spec.side) (void)hipStreamDestroy(spec.side);
     if (spec.fork) (void)hipEventDestroy(spec.fork);
@@ -455,6 +457,9 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_longc.ensure(sizeof(int32_t) * nc), "hipMalloc(longc)");
   HIPC(s.d_qh.ensure(sizeof(int32_t) * kQHWords), "hipMalloc(qh)");
   HIPC(hipMemsetAsync(s.d_qh.p, 0, sizeof(int32_t) * kQHWords, st), "memset qh");
+  HIPC(s.d_sorth.ensure(sizeof(int32_t) * kSortWords), "hipMalloc(sorth)");
+  HIPC(hipMemsetAsync(s.d_sorth.p, 0, sizeof(int32_t) * kSortWords, st), "memset sorth");
+  HIPC(s.d_stasks.ensure(sizeof(int2) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(stasks)");
   // pair matrices of heavy reads: sum over them of 2 * ns * ceil(ns / 64) words,
   // <= 2 * ns_total * (1 + ns_max / 64); reads that do not fit take the per-seed kernel
   const int64_t mat_words = std::max<int64_t>(1 << 20, 16 * (int64_t)ns);
@@ -482,6 +487,8 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.colent = s.d_colent.as<int32_t>();
   a.longc = s.d_longc.as<int32_t>();
   a.qh = s.d_qh.as<int32_t>();
+  a.sorth = s.d_sorth.as<int32_t>();
+  a.stasks = s.d_stasks.as<int2>();
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;

@@ -141,8 +141,9 @@ struct SeedExt {
 };  // 48 B; the per-batch memset 0 marks every slot "not computed"
 
 // extension task lists: 3 length classes (kernel columns per lane) x 3 rounds
-constexpr int kSpecBins = 3;                           // lq <= 192 / <= 256 / <= 1023
-constexpr int kSpecBinLen[kSpecBins] = {192, 256, 1023};
+constexpr int kSpecBins = 3;                           // lq <= 160 / <= 256 / <= 1023
+// (160: the pair kernel's first bin needs CPL <= 5 = 160 / 32; 2x150 reads all fall in it)
+constexpr int kSpecBinLen[kSpecBins] = {160, 256, 1023};
 constexpr int kSpecRounds = 3;                         // A, B, C
 constexpr int kOrderLane = 8;                          // chains up to this many seeds are ordered by their spec_chain lane
 constexpr int kSelLight = 64;                          // reads with more seeds go first
@@ -169,6 +170,9 @@ enum {
 // when the nine lists' heads moved off the two shared lines)
 constexpr int kQHStride = 32;
 constexpr int kQHWords = kSpecRounds * kSpecBins * 8 * kQHStride;
+// pair-kernel task order (spec_sort_*): 1024 keys = (left qlen / 8, right qlen / 8)
+constexpr int kSortKeys = 1024;
+constexpr int kSortWords = kSpecRounds * 2 * kSortKeys;
 // task list `list` (= round * kSpecBins + bin) starts at this entry of SpecArgs::tasks
 __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_seeds) {
   const int round = list / kSpecBins, bin = list % kSpecBins;
@@ -195,6 +199,8 @@ struct SpecArgs {
   int64_t mat_words;          // capacity of mat
   int32_t* cov;               // per seed slot: seedcov of its region (heavy reads)
   int32_t* qh;                // kQHWords: sharded queue heads of the extension task lists
+  int32_t* sorth;             // kSortWords, zeroed per batch: per (round, bin < 2) key histograms / cursors
+  int2* stasks;               // the C = 3 / 4 lists sorted by key (same offsets as tasks), for the pair kernel
   bwagpu_alnreg_t* out;
   int32_t* out_n;
   int64_t* stats;

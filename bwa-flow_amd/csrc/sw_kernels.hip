@@ -605,6 +605,255 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
   return ExtOut{-1, 0, 0, 0, -1, 0};  // unreachable: cd <= C by construction
 }
 
+// ------------------------------------------------ ksw_extend2, two per wave
+// TWO extensions per wave: lanes 0-31 run one ksw_extend2, lanes 32-63 another
+// (the halves' rows run in lock step; a half whose call has ended is off in
+// EXEC until the other's ends too).  Every per-row instruction of
+// extend_wave_blk — the F scan, the row-max reduction, the band bookkeeping —
+// then serves two extensions, and a 32-lane half covers a short extension
+// (qlen < 32: most left/right extensions of a 150 bp read are below 64) with
+// one column slot per lane.
+//  * columns are BLOCKED over the half: lane r holds j = r*CPL + c, c < CPL;
+//  * every per-call quantity (qlen, band, maxima, break state) is a per-lane
+//    VGPR value that is uniform over the half: no readfirstlane, no ballot;
+//  * the F scan is ONE inclusive max-scan over the half (row_shr 1/2/4/8 +
+//    row_bcast:15 into rows 1/3, which never crosses the half boundary), the
+//    row max a row_ror reduction finished by an exchange of
+//    the half's two rows (v_permlane16_swap); the band trim (ksw.c:466-469)
+//    a min and a max reduction of the same shape;
+//  * the gscore/max_ie tracking (ksw.c:450-453) runs on the lane that owns
+//    column qlen-1 (h1 = H(i, qlen-1) whenever the row ends at qlen) and is
+//    read from it once per call.
+// Half-wave all-reduce from per-row results: v_permlane16_swap (gfx950)
+// exchanges rows 0<->1 and 2<->3 of two registers — a VALU op, so there is no
+// LDS round trip (ds_swizzle) on the row's dependency chain.
+__device__ __forceinline__ int half_max(int v) {  // v: its row's max in every lane -> the half's
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return max((int)r[0], (int)r[1]);
+}
+__device__ __forceinline__ int half_min(int v) {
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return min((int)r[0], (int)r[1]);
+}
+
+// x <- inclusive max-scan over each 32-lane half; r <- its 16-lane row's max in
+// every lane (finish with half_max(r)).  Interleaved like scan_reduce.
+__device__ __forceinline__ void scan_reduce32(int& x, int& r) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf"
+      : "+v"(x), "+v"(r));
+}
+
+// lo <- 16-lane row min, hi <- row max, in every lane (two chains interleaved)
+__device__ __forceinline__ void row_minmax(int& lo, int& hi) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_min_i32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_min_i32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_min_i32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_min_i32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_i32_dpp %1, %1, %1 row_ror:1 row_mask:0xf bank_mask:0xf"
+      : "+v"(lo), "+v"(hi));
+}
+
+__device__ __forceinline__ int row_max32(int x) {
+  return max_ror1(max_ror2(max_ror4(max_ror8(x))));
+}
+
+struct Tally32 {  // per-seed DP work (fits 32 bits: <= 1023 columns x a window's rows)
+  int cells, rows, calls;
+};
+
+template <int CPL>
+__device__ __forceinline__ ExtOut extend_pair(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
+                                              int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
+                                              int h0, Tally32& tl) {
+  // the lane index is re-derived here behind an opaque move: otherwise the
+  // compiler hoists every variant's lane constants (j0 + c, ...) to the kernel
+  // entry, where they stay live across all of it (measured: 167 VGPRs)
+  int r;
+  asm volatile("v_and_b32 %0, 31, %1" : "=v"(r) : "v"((int)threadIdx.x));
+  const int e_del = o.e_del, e_ins = o.e_ins, o_del = o.o_del, oe_ins = o.oe_ins;
+  constexpr int KS = CPL <= 2 ? 1 : (CPL <= 4 ? 2 : (CPL <= 8 ? 3 : 4));  // in-lane column bits of the key
+  static_assert(CPL >= 1 && CPL <= 16, "two extensions per wave: CPL <= 16");
+  const int j0 = r * CPL;
+  int hh[CPL], ee[CPL];
+  uint32_t pf[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j = j0 + c;
+    const int qv = qp[qa + qd * min(j, qlen - 1)];  // unconditional load (qlen >= 1)
+    const int qb = j < qlen ? qv : 0;
+    pf[c] = qprof_word(o, qb);
+    const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);  // ksw.c:392-395
+    hh[c] = j <= qlen ? v : 0;
+    ee[c] = 0;
+  }
+  {  // band clamp (ksw.c:399-407)
+    const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
+    const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, e_del);
+    w = min(w, min(mi, md));
+  }
+  const int rE = e_ins * CPL * r;  // the lane's offset in the scan
+  const int cq = qlen - 1 - j0;    // slot of column qlen-1 on its owner lane
+  int best = h0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0;
+  int lo = 0, hi = qlen;
+  int iw = -w, iw1 = w + 1;
+  int gl = h0 - o.o_del - e_del;
+  int vi = 0, cells = 0;
+  int rows = tlen;
+  int tnext = tlen > 0 ? tb[0] : 0;
+  int rkp = 0;  // row i-1's per-lane key, reduced during row i's scan
+  auto row_end = [&](int rkr, int vk) -> bool {  // ksw.c:454-465 of row vk
+    const int mrow = rkr >> 10, mj = rkr & 1023;
+    const bool up = mrow > best;
+    const int di = vk - bi, dj = mj - bj;
+    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
+    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
+    off = up ? max(off, abs(mj - vk)) : off;
+    best = up ? mrow : best;
+    bi = up ? vk : bi;
+    bj = up ? mj : bj;
+    return brk;
+  };
+  // The halves run their rows in lock step; a half whose call ends leaves the
+  // loop (EXEC) while the other finishes.  (A branch-free form — the ended half
+  // kept in the loop with an empty band and select-guarded bookkeeping — was
+  // measured 7 % slower: 0.97 vs 0.90 ms per spec_ext2_kernel<5> launch.)
+  for (int i = 0; i < tlen; ++i) {
+    const int t = tnext;
+    tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
+    lo = max(lo, iw);
+    hi = min(min(hi, iw1), qlen);
+    iw += 1;
+    iw1 += 1;
+    const int wd = usat32(hi, lo);
+    const int left0 = lo == 0 ? max(gl, 0) : 0;
+    gl -= e_del;
+    const int sh = (t & 3) << 3;
+    const int x = j0 - lo;
+    int M[CPL], A[CPL];
+    int T = 0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const bool ib = (unsigned)(x + c) < (unsigned)wd;
+      const int sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
+      const int m = hh[c] ? hh[c] + sc : 0;
+      M[c] = m;
+      A[c] = (ib ? m : NEG) - oe_ins;
+      T = max(T - e_ins, A[c]);
+    }
+    int sx = T + rE;
+    scan_reduce32(sx, rkp);  // inclusive half scan of this row + row i-1's row maxima
+    int EX = dpp<DPP_WAVE_SHR1>(NEG, sx);
+    EX = r == 0 ? NEG : EX;  // lane 32 took lane 31's value
+    int f = max(EX - rE + e_ins * CPL, 0);
+    int hm[CPL];
+    int lk = 0;
+    const int hix = hi - j0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const unsigned d = (unsigned)(x + c);
+      const bool ib = d < (unsigned)wd, ib2 = d <= (unsigned)wd;
+      if (c > 0) f = max(max(f - e_ins, A[c - 1]), 0);
+      const int h = max(max(M[c], ee[c]), f);
+      hm[c] = ib ? h : 0;
+      const int en = usat32(max(ee[c], M[c] - o_del), e_del);
+      lk = max(lk, (hm[c] << KS) + c);
+      ee[c] = ib ? en : (ib2 ? 0 : ee[c]);
+      if (c > 0) hh[c] = ib2 ? hm[c - 1] : hh[c];
+    }
+    int hs0 = dpp<DPP_WAVE_SHR1>(0, hm[CPL - 1]);  // H(i, j0-1)
+    hs0 = r == 0 ? left0 : hs0;                    // column 0: the first-column value
+    hh[0] = (unsigned)x <= (unsigned)wd ? hs0 : hh[0];
+    // h1 when the row ends at qlen: H(i, qlen-1) (0 when out of band), on its owner
+    int h1q = 0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) h1q = cq == c ? hm[c] : h1q;
+    // band trim for the next row (ksw.c:466-469): first non-zero column in
+    // [lo, hi), last in [lo, hi]
+    uint32_t nzm = 0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) nzm |= (uint32_t)((hh[c] | ee[c]) != 0) << c;
+    const int lo_l = min(max(lo - j0, 0), 31), hi_l = min(max(hix, 0), 31);
+    const uint32_t mf = nzm & ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);   // [lo, hi)
+    const uint32_t ml = mf | (nzm & ((unsigned)hix < (unsigned)CPL ? 1u << hix : 0u));  // + column hi
+    int cl = mf ? j0 + (int)__builtin_ctz(mf) : 0x7fff;
+    int ch = ml ? j0 + 31 - (int)__builtin_clz(ml) : -1;
+    row_minmax(cl, ch);
+    if (i > 0) {
+      const int rkr = half_max(rkp);
+      if (row_end(rkr, vi - 1)) {
+        rows = i;  // row i-1 was the last row: row i never ran
+        break;
+      }
+    }
+    cl = half_min(cl);
+    ch = half_max(ch);
+    const int nlo = min(cl, hi);
+    const int nhi = min(max(ch, nlo - 1) + 2, qlen);
+    rkp = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
+    cells += wd;
+    {  // ksw.c:450-453 (meaningful on the owner of column qlen-1)
+      const bool atend = max(lo, hi) == qlen;
+      ei = (atend && !(esc > h1q)) ? vi : ei;
+      esc = atend ? max(esc, h1q) : esc;
+    }
+    vi += 1;
+    lo = nlo;
+    hi = nhi;
+  }
+  if (rows == tlen && tlen > 0) {  // the last row's bookkeeping (its exit test is moot)
+    const int rkr = half_max(row_max32(rkp));
+    (void)row_end(rkr, vi - 1);
+  }
+  // gscore / max_ie from the owner of column qlen-1 (qlen >= 1 for every call)
+  const int own = (int)(threadIdx.x & 32) + (qlen - 1) / CPL;
+  ei = __shfl(ei, own, 64);
+  esc = __shfl(esc, own, 64);
+  tl.cells += cells;
+  tl.rows += rows;
+  tl.calls += 1;
+  return ExtOut{best, bj + 1, bi + 1, ei + 1, esc, off};
+}
+
+// The column count of the halves' current calls: CPL = ceil((qlen+1)/32) of
+// the larger active half (both halves run one compiled body).
+template <int PMAX>
+__device__ __forceinline__ ExtOut extend_pair_dispatch(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp,
+                                                       int qa, int qd, int tlen, const uint8_t* tb, int w,
+                                                       int end_bonus, int zdrop, int h0, Tally32& tl) {
+  const unsigned long long ex = __builtin_amdgcn_read_exec();
+  int qm = 0;
+  if (ex & 1ull) qm = __builtin_amdgcn_readlane(qlen, 0);
+  if ((ex >> 32) & 1ull) qm = max(qm, __builtin_amdgcn_readlane(qlen, 32));
+  const int cpl = (qm + 32) >> 5;
+#define EXT_PAIR(n) \
+  if (n <= PMAX && cpl == n) return extend_pair<(n <= PMAX ? n : 1)>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
+  EXT_PAIR(1) EXT_PAIR(2) EXT_PAIR(3) EXT_PAIR(4) EXT_PAIR(5) EXT_PAIR(6) EXT_PAIR(7) EXT_PAIR(8)
+#undef EXT_PAIR
+  return ExtOut{-1, 0, 0, 0, -1, 0};  // unreachable: cpl <= PMAX by construction
+}
+
 // ------------------------------------------------ ksw_extend2, 16-lane groups
 // One extension per 16-lane group (one DPP row), FOUR extensions per wave that
 // share every instruction of a DP row.  Columns are BLOCKED: lane r of the
@@ -2714,6 +2963,327 @@ __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, 
     atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
 }
 
+// ---------------------------------------------------- two seeds per wave
+// The same extension tasks with one seed per 32-lane half (extend_pair).
+// Everything below is per lane and uniform over a half; the halves diverge
+// only through EXEC (a half without a left side, a retry or a task waits for
+// the other).
+//
+// Both target windows of the half's seed into its LDS rows (fill_two on 32
+// lanes: 4 loads per side per lane in flight, 128 rows per side per pass).
+__device__ __forceinline__ void fill_two_half(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
+                                              const DevRef& ref) {
+  const int r = (int)(threadIdx.x & 31);
+  const int64_t two1 = (ref.l_pac << 1) - 1;
+  const int n = max(nl, nr);
+  for (int base = 0; base < n; base += 128) {
+    uint32_t raw[8];
+    int sh[8], kk[8];
+    bool rev[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const bool left = m < 4;
+      const int nn = left ? nl : nr;
+      const int k = min(base + (m & 3) * 32 + r, max(nn - 1, 0));
+      kk[m] = k;
+      const int64_t x = left ? x0l - k : x0r + k;
+      rev[m] = x >= ref.l_pac;
+      int64_t f = rev[m] ? two1 - x : x;
+      f = f < 0 ? 0 : (f >= ref.l_pac ? ref.l_pac - 1 : f);  // only for an empty side (nn == 0)
+      raw[m] = ref.pac[f >> 2];
+      sh[m] = (int)((~f & 3) << 1);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int bse = (raw[m] >> sh[m]) & 3;
+      const uint8_t v = (uint8_t)(rev[m] ? 3 - bse : bse);
+      if (m < 4) {
+        if (nl > 0) tbl[kk[m]] = v;
+      } else {
+        if (nr > 0) tbr[kk[m]] = v;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One half's task and the state of its extension, in LDS for the whole task:
+// re-read (volatile, LDS address space) around every call, so that none of it
+// occupies VGPRs across the DP loop.
+struct PairCtx {
+  int64_t rbeg, lo, hi, qoff;  // the seed, its chain's window, its read
+  int32_t qbeg, len, lq, phase;
+  int64_t rb, re;              // the region so far
+  int32_t score, truesc, qb, qe, sc0, aw0, aw1, cells, rows, calls, pad_[2];
+};
+static_assert(sizeof(PairCtx) == 112, "PairCtx layout");
+typedef volatile __attribute__((address_space(3))) PairCtx LdsCtx;
+
+// extend_seed (bwamem.c:717-792) for the half's seed, as a state machine with
+// ONE extend_pair call site: phase 0/1 = left side try 0/1 (MAX_BAND_TRY,
+// bwamem.c:639), 2/3 = right side, 4 = done; a half whose phases are over
+// leaves the loop (EXEC) while the other finishes.
+template <int PMAX>
+__device__ __forceinline__ SeedExt extend_seed2(const DevOpt& o, const DevRef& ref, LdsCtx* cx, const uint8_t* seq,
+                                                uint8_t* tbl, uint8_t* tbr) {
+  {
+    const int64_t rbeg = cx->rbeg, lo = cx->lo, hi = cx->hi;
+    const int qbeg = cx->qbeg, len = cx->len, lq = cx->lq;
+    const int qlenL = qbeg, qlenR = lq - (qbeg + len);
+    const int64_t x0R = rbeg + len;
+    fill_two_half(tbl, rbeg - 1, qlenL ? rows_needed(o, qlenL, (int)(rbeg - lo), o.w << 1, o.pen_clip5) : 0, tbr, x0R,
+                  qlenR ? rows_needed(o, qlenR, (int)(hi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
+    cx->phase = qbeg != 0 ? 0 : (qlenR != 0 ? 2 : 4);
+    const int sc = qbeg != 0 ? -1 : len * o.a;  // bwamem.c:753
+    cx->score = sc;
+    cx->truesc = sc;
+    cx->qb = 0;
+    cx->qe = lq;
+    cx->sc0 = 0;
+    cx->aw0 = o.w;
+    cx->aw1 = o.w;
+    cx->rb = rbeg;
+    cx->re = rbeg + len;
+    cx->cells = 0;
+    cx->rows = 0;
+    cx->calls = 0;
+  }
+  for (;;) {
+    const int phase = cx->phase;
+    if (phase >= 4) break;
+    const int64_t rbeg = cx->rbeg;
+    const int qbeg = cx->qbeg, len = cx->len, lq = cx->lq;
+    const bool left = phase < 2;
+    const int t = phase & 1;
+    const int qlenR = lq - (qbeg + len);
+    const int qlen = left ? qbeg : qlenR;
+    const int64_t x0 = left ? rbeg - 1 : rbeg + len;
+    const int tlen = left ? (int)(rbeg - cx->lo) : (int)(cx->hi - x0);
+    const int qa = left ? qbeg - 1 : qbeg + len;
+    const int eb = left ? o.pen_clip5 : o.pen_clip3;
+    if (t == 0) cx->sc0 = cx->score;
+    const int h0 = left ? len * o.a : cx->sc0;
+    const int aw = o.w << t;
+    if (left) cx->aw0 = aw;
+    else cx->aw1 = aw;
+    Tally32 tl{0, 0, 0};
+    const ExtOut x = extend_pair_dispatch<PMAX>(o, qlen, seq + cx->qoff, qa, left ? -1 : 1, tlen, left ? tbl : tbr, aw,
+                                             eb, o.zdrop, h0, tl);
+    cx->cells = cx->cells + tl.cells;
+    cx->rows = cx->rows + tl.rows;
+    cx->calls = cx->calls + tl.calls;
+    const int prev = cx->score;
+    const int score = x.score;
+    cx->score = score;
+    if (t == 0 && !(score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {
+      cx->phase = phase + 1;  // the band retry
+      continue;
+    }
+    const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+    if (left) {
+      cx->qb = local ? qbeg - x.qle : 0;
+      cx->rb = rbeg - (local ? x.tle : x.gtle);
+      cx->truesc = local ? score : x.gscore;
+      cx->phase = qlenR != 0 ? 2 : 4;
+    } else {
+      cx->qe = local ? qa + x.qle : lq;
+      cx->re = x0 + (local ? x.tle : x.gtle);
+      cx->truesc = cx->truesc + (local ? score : x.gscore) - cx->sc0;
+      cx->phase = 4;
+    }
+  }
+  SeedExt e;
+  e.rb = cx->rb;
+  e.re = cx->re;
+  e.qb = cx->qb;
+  e.qe = cx->qe;
+  e.score = cx->score;
+  e.truesc = cx->truesc;
+  const int aw0 = cx->aw0, aw1 = cx->aw1;
+  e.w = aw0 > aw1 ? aw0 : aw1;
+  e.cells = cx->cells;
+  e.rows = cx->rows;
+  e.calls = cx->calls + 1;  // + 1: a computed slot is never all-zero
+  return e;
+}
+
+__device__ __forceinline__ void store_ext_half(SeedExt* dst, const SeedExt& e) {
+  const int d = (int)(threadIdx.x & 31);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&e);
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) v = d == k ? w[k] : v;
+  if (d < 12) reinterpret_cast<uint32_t*>(dst)[d] = v;
+}
+
+// Extension tasks of one list, two per wave: a wave claims two consecutive
+// entries of a shard (one atomic), lanes 0-31 take the first, 32-63 the second.
+// PMAX = the bin's largest CPL: ceil(read length / 32) (qlen + 1 <= read length)
+template <int PMAX>
+__global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                           int tb_bytes, int sorted) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int hf = (int)(threadIdx.x >> 5) & 1;
+  // per half: left rows, right rows, the task context
+  uint8_t* const tbl = lds + (size_t)(threadIdx.x >> 5) * (2 * tb_bytes + sizeof(PairCtx));
+  uint8_t* const tbr = tbl + tb_bytes;
+  LdsCtx* const cx = (LdsCtx*)(tbr + tb_bytes);
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = (sorted ? a.stasks : a.tasks) + spec_list_off(list, b.n_chains, b.n_seeds);
+  ShardQ qq;
+  qq.init(a.qh + 8 * kQHStride * list, n);
+  long long spec_cells = 0;
+  int m0, cap;
+  while (qq.claim(2, m0, cap)) {
+    const int m = m0 + hf;
+    if (m < cap) {
+      const int2 tk = tl[qq.shard + 8 * m];
+      const int pos = tk.x, c = tk.y;
+      if ((threadIdx.x & 31) == 0) {
+        const int rd = a.chain_read[c];
+        const bwagpu_seed_t s = a.prog[pos];
+        const ChainWin cw = a.win[c];
+        const int64_t qoff = b.seq_off[rd];
+        cx->rbeg = s.rbeg;
+        cx->lo = cw.lo;
+        cx->hi = cw.hi;
+        cx->qoff = qoff;
+        cx->qbeg = s.qbeg;
+        cx->len = s.len;
+        cx->lq = (int)(b.seq_off[rd + 1] - qoff);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const SeedExt e = extend_seed2<PMAX>(o, ref, cx, b.seq, tbl, tbr);
+      store_ext_half(a.ext + pos, e);
+      spec_cells += e.cells;
+    }
+  }
+  if ((threadIdx.x & 31) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+// LDS bytes of a spec_ext2_kernel workgroup
+static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size_t)tb_bytes + sizeof(PairCtx)); }
+
+// Task order for the pair kernel: the two seeds a wave takes should need the
+// same phases for about as long — a half whose seed has no left side, or a
+// much shorter one, idles while the other runs (EXEC).  A counting sort of
+// the C = 3 / 4 lists of a round by key = (left qlen / 8, right qlen / 8):
+// count (per-block LDS histograms, one global atomic per block and key),
+// scan (one block per list), scatter (per-block LDS ranks, one global atomic
+// per block and key to reserve the block's range).  Claims then take entries
+// 8 apart in the sorted list (the sharded queue), which have about the same
+// key.  The order changes nothing but which seeds share a wave.
+__device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, int2 tk) {
+  const bwagpu_seed_t s = a.prog[tk.x];
+  const int rd = a.chain_read[tk.y];
+  const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+  const int ql = min(s.qbeg, 255), qr = min(max(lq - s.qbeg - s.len, 0), 255);
+  return (ql >> 3) << 5 | (qr >> 3);
+}
+
+__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
+  __shared__ int hist[kSortKeys];
+  const int list = round * kSpecBins + (int)blockIdx.y;
+  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  for (int k = threadIdx.x; k < kSortKeys; k += 256) hist[k] = 0;
+  __syncthreads();
+  const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) atomicAdd(&hist[pair_key(b, a, tl[i])], 1);
+  __syncthreads();
+  for (int k = threadIdx.x; k < kSortKeys; k += 256)
+    if (hist[k]) atomicAdd(&gh[k], hist[k]);
+}
+
+__global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
+  __shared__ int part[256];
+  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.x) * kSortKeys;
+  const int t = (int)threadIdx.x;  // 4 keys per thread
+  int v[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = gh[4 * t + k];
+    s += v[k];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the per-thread sums
+    const int x = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int base = part[t] - s;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    gh[4 * t + k] = base;  // the key's first position (a cursor from here on)
+    base += v[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round) {
+  __shared__ int cnt[kSortKeys];
+  const int list = round * kSpecBins + (int)blockIdx.y;
+  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  for (int k = threadIdx.x; k < kSortKeys; k += 256) cnt[k] = 0;
+  __syncthreads();
+  const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const size_t off = spec_list_off(list, b.n_chains, b.n_seeds);
+  const int2* tl = a.tasks + off;
+  int2* out = a.stasks + off;
+  const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  constexpr int kPer = 16;  // entries per thread held across the barrier
+  int keys[kPer], rank[kPer];
+  int2 tk[kPer];
+  for (int base = i0; base < i1; base += 256 * kPer) {
+#pragma unroll
+    for (int m = 0; m < kPer; ++m) {
+      const int i = base + m * 256 + (int)threadIdx.x;
+      keys[m] = -1;
+      if (i < i1) {
+        tk[m] = tl[i];
+        keys[m] = pair_key(b, a, tk[m]);
+        rank[m] = atomicAdd(&cnt[keys[m]], 1);
+      }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kSortKeys; k += 256) {
+      const int c = cnt[k];
+      cnt[k] = c ? atomicAdd(&gh[k], c) : 0;  // this pass's range of key k
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kPer; ++m)
+      if (keys[m] >= 0) out[cnt[keys[m]] + rank[m]] = tk[m];
+    __syncthreads();
+    for (int k = threadIdx.x; k < kSortKeys; k += 256) cnt[k] = 0;
+    __syncthreads();
+  }
+}
+
+// The extension rounds' first two length bins run two seeds per wave
+// (spec_ext2_kernel) on key-sorted lists by default.  BWAGPU_EXT_PAIR: 0 = one
+// seed per wave (spec_ext_kernel), 1 = pairs in list order, 2 (default) =
+// pairs of sorted tasks.  A/B on the C2 bench: 0.89-0.91 vs
+// 0.92-0.94 ms per C = 3 launch, 3.25-3.35 vs 3.47-3.50 ms per step; mode 1
+// 1.07 ms (a third of the lanes idle while the other half's seed runs).
+static int ext_pair_mode() {
+  static const int v = [] {
+    const char* e = getenv("BWAGPU_EXT_PAIR");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+static bool ext_pair_enabled() { return ext_pair_mode() != 0; }
+
 // ============================================================ FPGA wire format
 // bwagpu_sw_stream (include/bwagpu.h).  Lane per read record: the record's
 // bases unpacked to bytes (4-bit words, first base in the high nibble,
@@ -3684,16 +4254,32 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
                              int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
-  int nb = resident_blocks(spec_ext_kernel<3>, lds);
+  const bool pair = ext_pair_enabled();
+  const size_t lds2 = ext2_lds(tb_bytes);
+  const int sorted = ext_pair_mode() == 2 ? 1 : 0;
+  if (pair && sorted) {
+    hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
+    hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
+    hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
+  }
+  int nb = pair ? resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2) : resident_blocks(spec_ext_kernel<3>, lds);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
+  if (pair)
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 0, tb_bytes, sorted);
+  else
+    hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
   if (prof) {
     (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
     *ss.pool_used += 2;
   }
-  nb = resident_blocks(spec_ext_kernel<4>, lds);
-  hipLaunchKernelGGL(spec_ext_kernel<4>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 1, tb_bytes);
+  if (pair) {
+    nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 1, tb_bytes, sorted);
+  } else {
+    nb = resident_blocks(spec_ext_kernel<4>, lds);
+    hipLaunchKernelGGL(spec_ext_kernel<4>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 1, tb_bytes);
+  }
   nb = resident_blocks(spec_ext_kernel<16>, lds);
   hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 2, tb_bytes);
 }
