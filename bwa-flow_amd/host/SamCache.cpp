@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -131,10 +132,14 @@ int run_reg2aln(bwagpu_samcache_t* c, const std::vector<std::pair<int, int32_t>>
     qp.insert(qp.end(), sh.r2q.begin() + e.qoff, sh.r2q.begin() + e.qoff + e.l_seq);
   }
   std::vector<bwagpu_aln_t> out((size_t)n);
-  std::vector<uint32_t> cg((size_t)n * (size_t)max_ops);
-  std::vector<char> mdb((size_t)n * (size_t)max_md);
+  // the device fills every slot it reports; no zero fill of the n x (max_ops,
+  // max_md) blocks (tens of MB per flush at C2 batch size)
+  std::unique_ptr<uint32_t[]> cgp(new uint32_t[(size_t)n * (size_t)max_ops]);
+  std::unique_ptr<char[]> mdp(new char[(size_t)n * (size_t)max_md]);
+  uint32_t* const cg = cgp.get();
+  char* const mdb = mdp.get();
   const int rc = bwagpu_reg2aln_batch(c->ctx, n, tasks.data(), qp.data(), (int64_t)qp.size(), max_ops, max_md,
-                                      out.data(), cg.data(), mdb.data());
+                                      out.data(), cg, mdb);
   if (rc) return rc;
   int64_t done = 0;
   for (int32_t k = 0; k < n; ++k) {
@@ -149,9 +154,9 @@ int run_reg2aln(bwagpu_samcache_t* c, const std::vector<std::pair<int, int32_t>>
     e.cig_off = (int64_t)sh.cig.size();
     e.md_off = (int64_t)sh.md.size();
     if (a.status == BWAGPU_ALN_OK) {
-      const uint32_t* src = cg.data() + (size_t)k * max_ops;
+      const uint32_t* src = cg + (size_t)k * max_ops;
       sh.cig.insert(sh.cig.end(), src, src + a.n_cigar);
-      const char* m = mdb.data() + (size_t)k * max_md;
+      const char* m = mdb + (size_t)k * max_md;
       sh.md.insert(sh.md.end(), m, m + a.md_len);
     }
     sh.md.push_back(0);

@@ -52,6 +52,17 @@ static cache_r2_fn g_r2;
 static align2_fn real_align2;
 static reg2aln_fn real_reg2aln;
 static volatile int g_error; /* a cached job the device could not align */
+static __thread int g_tls_miss; /* misses of the calling thread since the last take */
+
+/* cache misses of the calling thread since the last call, reset to 0: a
+   stage worker brackets one pair's mem_sam_pe with it to learn whether that
+   pair's text must be redone after the next flush */
+int bwagpu_sam_hooks_take_misses(void)
+{
+  const int m = g_tls_miss;
+  g_tls_miss = 0;
+  return m;
+}
 
 static void resolve_real(void)
 {
@@ -121,10 +132,12 @@ kswr_t ksw_align2(int qlen, uint8_t *query, int tlen, uint8_t *target, int m, co
     return real_align2(qlen, query, tlen, target, m, mat, o_del, e_del, o_ins, e_ins, xtra, qry);
   }
   bwagpu_kswr_t r;
-  if (g_a2(g_cache, qlen, query, tlen, target, xtra, &r) < 0) {
+  const int rc = g_a2(g_cache, qlen, query, tlen, target, xtra, &r);
+  if (rc < 0) {
     fprintf(stderr, "sam_hooks: bwagpu_samcache_align2 failed\n");
     abort();
   }
+  g_tls_miss += rc;
   kswr_t x;
   x.score = r.score; x.te = r.te; x.qe = r.qe; x.score2 = r.score2; x.te2 = r.te2; x.tb = r.tb; x.qb = r.qb;
   return x;
@@ -148,6 +161,7 @@ mem_aln_t mem_reg2aln(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *
     fprintf(stderr, "sam_hooks: bwagpu_samcache_reg2aln failed\n");
     abort();
   }
+  g_tls_miss += rc;
   mem_aln_t a;
   memset(&a, 0, sizeof a);
   a.mapq = ar->secondary < 0 ? mem_approx_mapq_se(opt, ar) : 0;

@@ -64,6 +64,7 @@
 int bwagpu_sam_hooks_attach(bwagpu_samcache_t *c); /* bwa-flow_amd/host/sam_hooks.c */
 int bwagpu_sam_hooks_errors(void);
 void bwagpu_sam_hooks_quiet(int quiet);
+int bwagpu_sam_hooks_take_misses(void);
 
 typedef struct {
   int64_t rbeg;
@@ -244,6 +245,36 @@ static void w_sam(void *data, int i, int tid) /* worker2 (bwamem.c:1214-1216) */
   free(w->regs[i << 1 | 1].a);
 }
 
+/* one SAM pass over a list of pairs (gpusam modes): each pair's regions are a
+   fresh copy of the stage's (mem_sam_pe consumes them); miss[k] = 1 when the
+   pair's calls missed the cache, i.e. its text must be redone */
+typedef struct {
+  hw_t *w;
+  const mem_alnreg_v *keep;
+  const int *pairs;
+  char *miss;
+} pass_t;
+static void w_sam_pass(void *data, int k, int tid)
+{
+  pass_t *p = (pass_t *)data;
+  hw_t *w = p->w;
+  const int i = p->pairs[k];
+  mem_alnreg_v r[2];
+  for (int e = 0; e < 2; ++e) {
+    const mem_alnreg_v *s = &p->keep[i << 1 | e];
+    r[e] = *s;
+    r[e].a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (s->m ? s->m : 1));
+    memcpy(r[e].a, s->a, sizeof(mem_alnreg_t) * s->n);
+  }
+  free(w->seqs[i << 1].sam); free(w->seqs[i << 1 | 1].sam);
+  w->seqs[i << 1].sam = w->seqs[i << 1 | 1].sam = 0;
+  (void)bwagpu_sam_hooks_take_misses();
+  mem_sam_pe(w->opt, w->idx->bns, w->idx->pac, w->pes, (w->n_processed >> 1) + i, &w->seqs[i << 1], r);
+  p->miss[k] = bwagpu_sam_hooks_take_misses() > 0;
+  free(r[0].a);
+  free(r[1].a);
+}
+
 /* ---------------- seeding on the device (gpuseed mode) ---------------- */
 /* test_and_merge, bwamem.c:199-221 (static in the reference build) */
 static int merge_seed(const mem_opt_t *opt, int64_t l_pac, chain_t *c, const seed_t *p, int seed_rid)
@@ -409,95 +440,108 @@ static void seed_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T, double *t_dev)
 }
 
 /* one bwagpu_chain2aln call for the whole batch: flatten, run, unflatten into
-   malloc'd mem_alnreg_v (the ownership rule of ChainsToRegions, bwa_wrapper.cpp:824-830) */
-static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n)
+   malloc'd mem_alnreg_v (the ownership rule of ChainsToRegions, bwa_wrapper.cpp:824-830);
+   the per-read copies run on the stage's threads (offsets from one serial pass) */
+typedef struct {
+  hw_t *w;
+  int64_t *seq_off;
+  uint8_t *seq;
+  int32_t *rco, *cso, *rid;
+  float *fr;
+  bwagpu_seed_t *sd;
+  bwagpu_alnreg_t *out;
+  int32_t *on;
+} flat_t;
+static void w_flat(void *data, int i, int tid)
 {
-  int64_t nc = 0, ns = 0, nb = 0;
-  for (int i = 0; i < n; ++i) {
-    nc += w->chn[i].n;
-    for (size_t c = 0; c < w->chn[i].n; ++c) ns += w->chn[i].a[c].n;
-    nb += w->seqs[i].l_seq;
+  flat_t *f = (flat_t *)data;
+  hw_t *w = f->w;
+  memcpy(f->seq + f->seq_off[i], w->seqs[i].seq, w->seqs[i].l_seq);
+  int32_t c0 = f->rco[i], s0 = f->cso[c0];
+  for (size_t c = 0; c < w->chn[i].n; ++c) {
+    const chain_t *ch = &w->chn[i].a[c];
+    for (int k = 0; k < ch->n; ++k) {
+      bwagpu_seed_t t = {ch->seeds[k].rbeg, ch->seeds[k].qbeg, ch->seeds[k].len, ch->seeds[k].score, 0};
+      f->sd[s0++] = t;
+    }
+    f->rid[c0] = ch->rid;
+    f->fr[c0] = ch->frac_rep;
+    f->cso[++c0] = s0;
   }
+}
+static void w_unflat(void *data, int i, int tid)
+{
+  flat_t *f = (flat_t *)data;
+  mem_alnreg_v *r = &f->w->regs[i];
+  r->n = r->m = f->on[i];
+  r->a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (f->on[i] ? f->on[i] : 1));
+  memcpy(r->a, f->out + f->cso[f->rco[i]], sizeof(mem_alnreg_t) * f->on[i]);
+}
+static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T)
+{
   int64_t *seq_off = (int64_t *)malloc(8 * (n + 1));
-  uint8_t *seq = (uint8_t *)malloc(nb + 1);
-  int32_t *rco = (int32_t *)malloc(4 * (n + 1)), *cso = (int32_t *)malloc(4 * (nc + 1)), *rid = (int32_t *)malloc(4 * (nc + 1));
-  float *fr = (float *)malloc(4 * (nc + 1));
-  bwagpu_seed_t *sd = (bwagpu_seed_t *)malloc(sizeof(bwagpu_seed_t) * (ns + 1));
-  int64_t q = 0;
-  int32_t c0 = 0, s0 = 0;
+  int32_t *rco = (int32_t *)malloc(4 * (n + 1));
   seq_off[0] = 0;
   rco[0] = 0;
+  int64_t ns = 0;
+  for (int i = 0; i < n; ++i) {
+    seq_off[i + 1] = seq_off[i] + w->seqs[i].l_seq;
+    rco[i + 1] = rco[i] + (int32_t)w->chn[i].n;
+    for (size_t c = 0; c < w->chn[i].n; ++c) ns += w->chn[i].a[c].n;
+  }
+  const int64_t nc = rco[n], nb = seq_off[n];
+  int32_t *cso = (int32_t *)malloc(4 * (nc + 1)), *rid = (int32_t *)malloc(4 * (nc + 1));
+  /* chain seed offsets: one more serial pass over the chains (cheap) */
   cso[0] = 0;
-  for (int i = 0; i < n; ++i) {
-    memcpy(seq + q, w->seqs[i].seq, w->seqs[i].l_seq);
-    q += w->seqs[i].l_seq;
-    seq_off[i + 1] = q;
-    for (size_t c = 0; c < w->chn[i].n; ++c) {
-      const chain_t *ch = &w->chn[i].a[c];
-      for (int k = 0; k < ch->n; ++k) {
-        bwagpu_seed_t t = {ch->seeds[k].rbeg, ch->seeds[k].qbeg, ch->seeds[k].len, ch->seeds[k].score, 0};
-        sd[s0++] = t;
-      }
-      rid[c0] = ch->rid;
-      fr[c0] = ch->frac_rep;
-      cso[++c0] = s0;
-    }
-    rco[i + 1] = c0;
-  }
-  bwagpu_batch_t b = {n, (int32_t)nc, (int32_t)ns, 0, nb, seq_off, seq, rco, cso, rid, fr, sd};
-  bwagpu_alnreg_t *out = (bwagpu_alnreg_t *)malloc(sizeof(bwagpu_alnreg_t) * (ns + 1));
-  int32_t *on = (int32_t *)malloc(4 * (n + 1));
-  const int rc = G.chain2aln(ctx, &b, out, on);
+  for (int i = 0, c0 = 0; i < n; ++i)
+    for (size_t c = 0; c < w->chn[i].n; ++c, ++c0) cso[c0 + 1] = cso[c0] + w->chn[i].a[c].n;
+  flat_t f = {w, seq_off, (uint8_t *)malloc(nb + 1), rco, cso, rid, (float *)malloc(4 * (nc + 1)),
+              (bwagpu_seed_t *)malloc(sizeof(bwagpu_seed_t) * (ns + 1)),
+              (bwagpu_alnreg_t *)malloc(sizeof(bwagpu_alnreg_t) * (ns + 1)), (int32_t *)malloc(4 * (n + 1))};
+  kt_for(T, w_flat, &f, n);
+  bwagpu_batch_t b = {n, (int32_t)nc, (int32_t)ns, 0, nb, seq_off, f.seq, rco, cso, rid, f.fr, f.sd};
+  const int rc = G.chain2aln(ctx, &b, f.out, f.on);
   if (rc) { fprintf(stderr, "bwagpu_chain2aln: rc=%d %s\n", rc, G.last_error(ctx)); exit(3); }
-  for (int i = 0; i < n; ++i) {
-    mem_alnreg_v *r = &w->regs[i];
-    r->n = r->m = on[i];
-    r->a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (on[i] ? on[i] : 1));
-    memcpy(r->a, out + cso[rco[i]], sizeof(mem_alnreg_t) * on[i]);
-  }
-  free(seq_off); free(seq); free(rco); free(cso); free(rid); free(fr); free(sd); free(out); free(on);
+  kt_for(T, w_unflat, &f, n);
+  free(seq_off); free(f.seq); free(rco); free(cso); free(rid); free(f.fr); free(f.sd); free(f.out); free(f.on);
 }
 
 /* the SAM stage with its Smith-Waterman on the device (include/bwagpu_sam.h):
-   mem_sam_pe over a copy of the regions with the cache attached; a pass with
-   misses is discarded and its queued calls flushed to the device; the first
-   pass without a miss is the output */
+   mem_sam_pe over copies of the regions with the cache attached.  Pass 0
+   (every pair, no SAM text) queues the mate rescues and the CIGARs of the
+   pairs that need no rescue; a flush runs them.  Pass 1 (every pair, with
+   text) is final for every pair without a miss; the pairs that missed (their
+   rescue found a hit, so they print a region pass 0 could not know) are
+   flushed and redone alone until none misses. */
 static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t *n_passes, double *t_flush)
 {
-  mem_alnreg_v *keep = w->regs, *cp = (mem_alnreg_v *)calloc(n, sizeof(mem_alnreg_v));
-  int64_t st[8];
+  const int np = n >> 1;
+  int *pairs = (int *)malloc(sizeof(int) * (np + 1)), m = np;
+  char *miss = (char *)calloc(np + 1, 1);
+  for (int k = 0; k < np; ++k) pairs[k] = k;
+  pass_t p = {w, w->regs, pairs, miss};
   bwagpu_sam_hooks_attach(cache);
-  /* the first two passes only collect calls (rescues, then CIGARs of the final
-     regions): no SAM text; a text pass with misses is redone after a flush */
-  for (int pass = 0;; ++pass) {
-    const int quiet = pass < 2;
-    bwagpu_sam_hooks_quiet(quiet);
-    G.sc_stats(cache, st);
-    const int64_t miss0 = st[1] + st[3];
-    for (int i = 0; i < n; ++i) {
-      cp[i] = keep[i];
-      cp[i].a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (keep[i].m ? keep[i].m : 1));
-      memcpy(cp[i].a, keep[i].a, sizeof(mem_alnreg_t) * keep[i].n);
-    }
-    w->regs = cp;
-    kt_for(T, w_sam, w, n >> 1); /* frees cp[i].a */
+  for (int pass = 0; m > 0; ++pass) {
+    bwagpu_sam_hooks_quiet(pass == 0);
+    kt_for(T, w_sam_pass, &p, m);
     ++*n_passes;
-    G.sc_stats(cache, st);
     if (bwagpu_sam_hooks_errors()) { fprintf(stderr, "sam_hooks: the device flagged a CIGAR job\n"); exit(4); }
-    if (st[1] + st[3] == miss0 && !quiet) break;
-    for (int i = 0; i < n; ++i) { free(w->seqs[i].sam); w->seqs[i].sam = 0; }
-    if (st[1] + st[3] == miss0) { pass = 1; continue; } /* nothing to flush: straight to a text pass */
+    int m2 = 0;
+    for (int k = 0; k < m; ++k)
+      if (pass == 0 || miss[k]) pairs[m2++] = pairs[k];  /* pass 0's text is never final */
+    m = m2;
+    if (m == 0) break;
     const double t0 = realtime();
     const int64_t rc = G.sc_flush(cache);
     *t_flush += realtime() - t0;
-    if (rc <= 0) { fprintf(stderr, "bwagpu_samcache_flush: %ld\n", (long)rc); exit(3); }
+    if (rc < 0 || (rc == 0 && pass > 0)) { fprintf(stderr, "bwagpu_samcache_flush: %ld\n", (long)rc); exit(3); }
   }
   bwagpu_sam_hooks_quiet(0);
   bwagpu_sam_hooks_attach(0);
   G.sc_clear(cache);
-  for (int i = 0; i < n; ++i) free(keep[i].a);
-  free(cp);
-  w->regs = keep;
+  for (int i = 0; i < n; ++i) free(w->regs[i].a);
+  free(pairs);
+  free(miss);
 }
 
 int main(int argc, char *argv[])
@@ -532,20 +576,32 @@ int main(int argc, char *argv[])
   bwa_verbose = 1;
   rng_s = 1234;
   char *g = make_genome(3, ctg_len, &G_len);
-  char fa[4096];
+  char fa[4096], stamp[4200], want[64];
   snprintf(fa, sizeof fa, "%s/ref.fa", dir);
-  FILE *f = fopen(fa, "w");
-  if (!f) { perror(fa); return 1; }
-  for (int c = 0, off = 0; c < 3; off += ctg_len[c], ++c) {
-    fprintf(f, ">chr%d\n", c + 1);
-    for (int64_t i = 0; i < ctg_len[c]; i += 60) {
-      const int64_t k = ctg_len[c] - i < 60 ? ctg_len[c] - i : 60;
-      fwrite(g + off + i, 1, k, f);
-      fputc('\n', f);
+  snprintf(stamp, sizeof stamp, "%s/ref.fa.stamp", dir);
+  snprintf(want, sizeof want, "golden 1234 %ld\n", (long)GL);
+  /* an index built earlier for the same genome (the stamp file) is reused:
+     bwa_idx_build takes ~50 s at chr21 size */
+  char have[64] = {0};
+  FILE *sf = fopen(stamp, "r");
+  if (sf) { if (!fgets(have, sizeof have, sf)) have[0] = 0; fclose(sf); }
+  if (strcmp(have, want) != 0) {
+    FILE *f = fopen(fa, "w");
+    if (!f) { perror(fa); return 1; }
+    for (int c = 0, off = 0; c < 3; off += ctg_len[c], ++c) {
+      fprintf(f, ">chr%d\n", c + 1);
+      for (int64_t i = 0; i < ctg_len[c]; i += 60) {
+        const int64_t k = ctg_len[c] - i < 60 ? ctg_len[c] - i : 60;
+        fwrite(g + off + i, 1, k, f);
+        fputc('\n', f);
+      }
     }
+    fclose(f);
+    bwa_idx_build(fa, fa, BWTALGO_AUTO, 10000000);
+    remove(fa); /* the index files are all bwa_idx_load reads */
+    sf = fopen(stamp, "w");
+    if (sf) { fputs(want, sf); fclose(sf); }
   }
-  fclose(f);
-  bwa_idx_build(fa, fa, BWTALGO_AUTO, 10000000);
   bwaidx_t *idx = bwa_idx_load(fa, BWA_IDX_ALL);
   if (!idx) { fprintf(stderr, "index load failed\n"); return 1; }
 
@@ -581,7 +637,9 @@ int main(int argc, char *argv[])
     if (G.set_bwt(ctx, &gb)) { fprintf(stderr, "bwagpu_set_bwt: %s\n", G.last_error(ctx)); return 3; }
   }
   bwagpu_samcache_t *cache = 0;
-  if (is_sam && G.sc_create(ctx, 64, 512, &cache)) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
+  /* first-launch capacities sized for short reads (2x150: a handful of CIGAR
+     ops, MD well under 128 bytes); the rare longer ones are re-run with room */
+  if (is_sam && G.sc_create(ctx, 16, 128, &cache)) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
   int64_t n_passes = 0;
 
   FILE *out = fopen(outp, "w");
@@ -617,7 +675,7 @@ int main(int argc, char *argv[])
       else kt_for(T, w_seed, &w, n);
       t_seed += realtime() - t0;
       t0 = realtime();
-      if (is_gpu) ext_gpu(ctx, &w, n);
+      if (is_gpu) ext_gpu(ctx, &w, n, T);
       else kt_for(T, w_ext_cpu, &w, n);
       t_ext += realtime() - t0;
       t0 = realtime();
