@@ -10,6 +10,7 @@
 #include <chrono>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -85,6 +86,17 @@ namespace {
 
 inline Shard& shard_of(bwagpu_samcache_t* c, uint64_t h) { return c->sh[h >> 58]; }
 
+// f(t, nt) on nt threads (the flush runs with the stage's workers joined, so
+// their cores are free)
+template <typename F>
+void on_threads(F f) {
+  const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(f, t, nt);
+  f(0, nt);
+  for (auto& x : th) x.join();
+}
+
 uint32_t* empty_block() { return (uint32_t*)calloc(1, sizeof(uint32_t)); }
 
 // every shard's queued ksw_align2 calls in one bwagpu_align2_batch (their
@@ -117,20 +129,28 @@ int flush_align2(bwagpu_samcache_t* c) {
   return 0;
 }
 
-// one bwagpu_reg2aln_batch over `ids` (shard, entry); jobs whose CIGAR or MD
-// overflowed the launch's capacity are returned in `over`
+// one bwagpu_reg2aln_batch over `ids` (shard, entry; in shard order); jobs
+// whose CIGAR or MD overflowed the launch's capacity are returned in `over`.
+// Packing and the result copy-back run on several threads (the result copy
+// split at shard boundaries, so each shard's pools have one writer).
 int run_reg2aln(bwagpu_samcache_t* c, const std::vector<std::pair<int, int32_t>>& ids, int32_t max_ops,
                 int32_t max_md, std::vector<std::pair<int, int32_t>>& over) {
   const int32_t n = (int32_t)ids.size();
   if (n == 0) return 0;
   std::vector<bwagpu_reg2aln_task_t> tasks((size_t)n);
-  std::vector<uint8_t> qp;
-  for (int32_t k = 0; k < n; ++k) {
-    const Shard& sh = c->sh[ids[(size_t)k].first];
-    const R2Entry& e = sh.r2[(size_t)ids[(size_t)k].second];
-    tasks[(size_t)k] = bwagpu_reg2aln_task_t{e.rb, e.re, (int64_t)qp.size(), e.l_seq, e.qb, e.qe, e.truesc, e.w, 0};
-    qp.insert(qp.end(), sh.r2q.begin() + e.qoff, sh.r2q.begin() + e.qoff + e.l_seq);
-  }
+  std::vector<int64_t> qoff((size_t)n + 1, 0);
+  for (int32_t k = 0; k < n; ++k)
+    qoff[(size_t)k + 1] = qoff[(size_t)k] + c->sh[ids[(size_t)k].first].r2[(size_t)ids[(size_t)k].second].l_seq;
+  std::unique_ptr<uint8_t[]> qpp(new uint8_t[(size_t)qoff[(size_t)n] + 1]);
+  uint8_t* const qp = qpp.get();
+  on_threads([&](int t, int nt) {
+    for (int32_t k = (int32_t)((int64_t)n * t / nt); k < (int32_t)((int64_t)n * (t + 1) / nt); ++k) {
+      const Shard& sh = c->sh[ids[(size_t)k].first];
+      const R2Entry& e = sh.r2[(size_t)ids[(size_t)k].second];
+      tasks[(size_t)k] = bwagpu_reg2aln_task_t{e.rb, e.re, qoff[(size_t)k], e.l_seq, e.qb, e.qe, e.truesc, e.w, 0};
+      memcpy(qp + qoff[(size_t)k], sh.r2q.data() + e.qoff, (size_t)e.l_seq);
+    }
+  });
   std::vector<bwagpu_aln_t> out((size_t)n);
   // the device fills every slot it reports; no zero fill of the n x (max_ops,
   // max_md) blocks (tens of MB per flush at C2 batch size)
@@ -138,32 +158,44 @@ int run_reg2aln(bwagpu_samcache_t* c, const std::vector<std::pair<int, int32_t>>
   std::unique_ptr<char[]> mdp(new char[(size_t)n * (size_t)max_md]);
   uint32_t* const cg = cgp.get();
   char* const mdb = mdp.get();
-  const int rc = bwagpu_reg2aln_batch(c->ctx, n, tasks.data(), qp.data(), (int64_t)qp.size(), max_ops, max_md,
-                                      out.data(), cg, mdb);
+  const int rc = bwagpu_reg2aln_batch(c->ctx, n, tasks.data(), qp, qoff[(size_t)n], max_ops, max_md, out.data(), cg,
+                                      mdb);
   if (rc) return rc;
-  int64_t done = 0;
-  for (int32_t k = 0; k < n; ++k) {
-    Shard& sh = c->sh[ids[(size_t)k].first];
-    R2Entry& e = sh.r2[(size_t)ids[(size_t)k].second];
-    const bwagpu_aln_t& a = out[(size_t)k];
-    if (a.status == BWAGPU_ALN_OVERFLOW) {
-      over.push_back(ids[(size_t)k]);
-      continue;
+  // shard boundaries in ids
+  std::vector<int32_t> sb(kShards + 1, n);
+  for (int32_t k = n - 1; k >= 0; --k) sb[(size_t)ids[(size_t)k].first] = k;
+  for (int s = kShards - 1; s >= 0; --s) sb[(size_t)s] = std::min(sb[(size_t)s], sb[(size_t)s + 1]);
+  std::vector<std::vector<std::pair<int, int32_t>>> over_t(16);
+  std::vector<int64_t> done_t(16, 0);
+  on_threads([&](int t, int nt) {
+    for (int s = t; s < kShards; s += nt) {
+      Shard& sh = c->sh[s];
+      for (int32_t k = sb[(size_t)s]; k < sb[(size_t)s + 1]; ++k) {
+        R2Entry& e = sh.r2[(size_t)ids[(size_t)k].second];
+        const bwagpu_aln_t& a = out[(size_t)k];
+        if (a.status == BWAGPU_ALN_OVERFLOW) {
+          over_t[(size_t)t].push_back(ids[(size_t)k]);
+          continue;
+        }
+        e.a = a;
+        e.cig_off = (int64_t)sh.cig.size();
+        e.md_off = (int64_t)sh.md.size();
+        if (a.status == BWAGPU_ALN_OK) {
+          const uint32_t* src = cg + (size_t)k * max_ops;
+          sh.cig.insert(sh.cig.end(), src, src + a.n_cigar);
+          const char* m = mdb + (size_t)k * max_md;
+          sh.md.insert(sh.md.end(), m, m + a.md_len);
+        }
+        sh.md.push_back(0);
+        e.ready = true;
+        ++done_t[(size_t)t];
+      }
     }
-    e.a = a;
-    e.cig_off = (int64_t)sh.cig.size();
-    e.md_off = (int64_t)sh.md.size();
-    if (a.status == BWAGPU_ALN_OK) {
-      const uint32_t* src = cg + (size_t)k * max_ops;
-      sh.cig.insert(sh.cig.end(), src, src + a.n_cigar);
-      const char* m = mdb + (size_t)k * max_md;
-      sh.md.insert(sh.md.end(), m, m + a.md_len);
-    }
-    sh.md.push_back(0);
-    e.ready = true;
-    ++done;
+  });
+  for (int t = 0; t < 16; ++t) {
+    over.insert(over.end(), over_t[(size_t)t].begin(), over_t[(size_t)t].end());
+    c->st[1] += done_t[(size_t)t];
   }
-  c->st[1] += done;
   return 0;
 }
 
@@ -177,6 +209,7 @@ int flush_reg2aln(bwagpu_samcache_t* c) {
   if (!over.empty()) {
     // room for any alignment of the longest read among them: one op per base
     // and indel run, MD at most a few bytes per base
+    std::sort(over.begin(), over.end());  // run_reg2aln wants shard order
     int32_t lmax = 0;
     for (auto& w : over) lmax = std::max(lmax, c->sh[w.first].r2[(size_t)w.second].l_seq);
     rc = run_reg2aln(c, over, 2 * lmax + 8, 8 * lmax + 64, over2);
@@ -208,10 +241,12 @@ int bwagpu_samcache_destroy(bwagpu_samcache_t* c) {
 
 int bwagpu_samcache_clear(bwagpu_samcache_t* c) {
   if (!c) return BWAGPU_E_INVAL;
-  for (auto& sh : c->sh) {
-    std::lock_guard<std::mutex> g(sh.mu);
-    sh.clear();
-  }
+  on_threads([&](int t, int nt) {
+    for (int s = t; s < kShards; s += nt) {
+      std::lock_guard<std::mutex> g(c->sh[s].mu);
+      c->sh[s].clear();
+    }
+  });
   return BWAGPU_OK;
 }
 

@@ -230,6 +230,12 @@ static void w_ext_cpu(void *data, int i, int tid) /* ChainsToRegions::compute (P
     mem_chain2aln(w->opt, w->idx->bns, w->idx->pac, w->seqs[i].l_seq, (uint8_t *)w->seqs[i].seq, &w->chn[i].a[c],
                   &w->regs[i]);
 }
+static void w_free_chains(void *data, int i, int tid)
+{
+  hw_t *w = (hw_t *)data;
+  for (size_t c = 0; c < w->chn[i].n; ++c) free(w->chn[i].a[c].seeds);
+  free(w->chn[i].a);
+}
 static void w_post(void *data, int i, int tid) /* mem_align1_core's tail (bwamem.c:1088-1100) */
 {
   hw_t *w = (hw_t *)data;
@@ -478,8 +484,10 @@ static void w_unflat(void *data, int i, int tid)
   r->a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (f->on[i] ? f->on[i] : 1));
   memcpy(r->a, f->out + f->cso[f->rco[i]], sizeof(mem_alnreg_t) * f->on[i]);
 }
+static double g_t_flat, g_t_call, g_t_unflat, g_t_pass[3], g_t_clear, g_t_pestat;
 static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T)
 {
+  const double t_a = realtime();
   int64_t *seq_off = (int64_t *)malloc(8 * (n + 1));
   int32_t *rco = (int32_t *)malloc(4 * (n + 1));
   seq_off[0] = 0;
@@ -512,10 +520,15 @@ static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T)
   flat_t f = {w, seq_off, k_seq, rco, cso, rid, (float *)malloc(4 * (nc + 1)), k_sd, k_out,
               (int32_t *)malloc(4 * (n + 1))};
   kt_for(T, w_flat, &f, n);
+  const double t_b = realtime();
   bwagpu_batch_t b = {n, (int32_t)nc, (int32_t)ns, 0, nb, seq_off, f.seq, rco, cso, rid, f.fr, f.sd};
   const int rc = G.chain2aln(ctx, &b, f.out, f.on);
   if (rc) { fprintf(stderr, "bwagpu_chain2aln: rc=%d %s\n", rc, G.last_error(ctx)); exit(3); }
+  const double t_c = realtime();
   kt_for(T, w_unflat, &f, n);
+  g_t_flat += t_b - t_a;
+  g_t_call += t_c - t_b;
+  g_t_unflat += realtime() - t_c;
   free(seq_off); free(rco); free(cso); free(rid); free(f.fr); free(f.on);
 }
 
@@ -526,6 +539,7 @@ static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T)
    text) is final for every pair without a miss; the pairs that missed (their
    rescue found a hit, so they print a region pass 0 could not know) are
    flushed and redone alone until none misses. */
+static void w_free_regs(void *data, int i, int tid) { free(((hw_t *)data)->regs[i].a); }
 static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t *n_passes, double *t_flush)
 {
   const int np = n >> 1;
@@ -536,7 +550,9 @@ static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t 
   bwagpu_sam_hooks_attach(cache);
   for (int pass = 0; m > 0; ++pass) {
     bwagpu_sam_hooks_quiet(pass == 0);
+    const double tp = realtime();
     kt_for(T, w_sam_pass, &p, m);
+    g_t_pass[pass < 2 ? pass : 2] += realtime() - tp;
     ++*n_passes;
     if (bwagpu_sam_hooks_errors()) { fprintf(stderr, "sam_hooks: the device flagged a CIGAR job\n"); exit(4); }
     int m2 = 0;
@@ -551,8 +567,10 @@ static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t 
   }
   bwagpu_sam_hooks_quiet(0);
   bwagpu_sam_hooks_attach(0);
+  const double tc = realtime();
   G.sc_clear(cache);
-  for (int i = 0; i < n; ++i) free(w->regs[i].a);
+  kt_for(T, w_free_regs, w, n);
+  g_t_clear += realtime() - tc;
   free(pairs);
   free(miss);
 }
@@ -752,14 +770,13 @@ int main(int argc, char *argv[])
       else kt_for(T, w_ext_cpu, &w, n);
       t_ext += realtime() - t0;
       t0 = realtime();
-      for (int i = 0; i < n; ++i) {
-        for (size_t c = 0; c < w.chn[i].n; ++c) free(w.chn[i].a[c].seeds);
-        free(w.chn[i].a);
-      }
+      kt_for(T, w_free_chains, &w, n);
       kt_for(T, w_post, &w, n);
       t_post += realtime() - t0;
       mem_pestat_t pes[4];
+      const double tq = realtime();
       mem_pestat(opt, idx->bns->l_pac, n, w.regs, pes);
+      g_t_pestat += realtime() - tq;
       w.pes = pes;
       if (is_sam) sam_passes(cache, &w, n, T, &n_passes, &t_flush);
       else kt_for(T, w_sam, &w, n >> 1);
@@ -789,9 +806,11 @@ int main(int argc, char *argv[])
   if (cache) G.sc_stats(cache, st);
   fprintf(stderr, "{\"mode\": \"%s\", \"reads\": %ld, \"threads\": %d, \"seed_s\": %.4f, \"ext_s\": %.4f, "
                   "\"sam_s\": %.4f, \"flush_s\": %.4f, \"sam_passes\": %ld, \"align2_calls\": %ld, "
-                  "\"reg2aln_calls\": %ld, \"seed_device_s\": %.4f, \"post_s\": %.4f, \"out_s\": %.4f, \"total_s\": %.4f}\n",
+                  "\"reg2aln_calls\": %ld, \"seed_device_s\": %.4f, \"post_s\": %.4f, \"out_s\": %.4f, \"ext_flat_s\": %.4f, "
+                  "\"ext_call_s\": %.4f, \"ext_unflat_s\": %.4f, \"pass0_s\": %.4f, \"pass1_s\": %.4f, \"pass2_s\": %.4f, "
+                  "\"clear_s\": %.4f, \"pestat_s\": %.4f, \"total_s\": %.4f}\n",
           mode, (long)n_processed, T, t_seed, t_ext, t_sam, t_flush, (long)n_passes, (long)st[4], (long)st[5],
-          t_seed_dev, t_post, t_out, t_all);
+          t_seed_dev, t_post, t_out, g_t_flat, g_t_call, g_t_unflat, g_t_pass[0], g_t_pass[1], g_t_pass[2], g_t_clear, g_t_pestat, t_all);
   if (cache) G.sc_destroy(cache);
   if (ctx) G.destroy(ctx);
   free(all);
