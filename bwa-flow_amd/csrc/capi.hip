@@ -639,19 +639,27 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipHostMalloc(out)");
   HIPC(s.h_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipHostMalloc(out_n)");
   HIPC(s.h_stats.ensure(sizeof(int64_t) * ST_N), "hipHostMalloc(stats)");
-  // stage into pinned memory so the caller's buffers are free on return
+  // stage into pinned memory so the caller's buffers are free on return —
+  // unless the caller packed into that memory already (bwagpu_chain2aln_stage)
   char* h = s.h_in.as<char>();
-  if (b->n_reads) {
+  const bool staged = b->n_reads > 0 && (const void*)b->seq_off == (const void*)(h + L.seq_off) &&
+                      (const void*)b->seeds == (const void*)(h + L.seeds) &&
+                      (const void*)b->seq == (const void*)(h + L.seq) &&
+                      (const void*)b->chain_seed_off == (const void*)(h + L.cso);
+  if (staged) {
+  } else if (b->n_reads) {
     memcpy(h + L.seq_off, b->seq_off, sizeof(int64_t) * (size_t)(b->n_reads + 1));
     memcpy(h + L.rco, b->read_chain_off, sizeof(int32_t) * (size_t)(b->n_reads + 1));
   }
-  memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
-  if (b->n_chains) {
-    memcpy(h + L.rid, b->chain_rid, sizeof(int32_t) * (size_t)b->n_chains);
-    memcpy(h + L.frac, b->chain_frac_rep, sizeof(float) * (size_t)b->n_chains);
+  if (!staged) {
+    memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
+    if (b->n_chains) {
+      memcpy(h + L.rid, b->chain_rid, sizeof(int32_t) * (size_t)b->n_chains);
+      memcpy(h + L.frac, b->chain_frac_rep, sizeof(float) * (size_t)b->n_chains);
+    }
+    if (b->n_seeds) memcpy(h + L.seeds, b->seeds, sizeof(bwagpu_seed_t) * (size_t)b->n_seeds);
+    if (b->seq_bytes) memcpy(h + L.seq, b->seq, (size_t)b->seq_bytes);
   }
-  if (b->n_seeds) memcpy(h + L.seeds, b->seeds, sizeof(bwagpu_seed_t) * (size_t)b->n_seeds);
-  if (b->seq_bytes) memcpy(h + L.seq, b->seq, (size_t)b->seq_bytes);
 
   hipStream_t st = s.stream;
   HIPC(hipEventRecord(s.ev0, st), "event");
@@ -738,6 +746,43 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
   if (out_regs && s.n_seeds) memcpy(out_regs, s.h_out.p, sizeof(bwagpu_alnreg_t) * (size_t)s.n_seeds);
   if (st[ST_ERR] & ERR_RID)
     return fail(ctx, BWAGPU_E_RESULTS, "a chain's first seed is not inside contig chain_rid (bwamem.c:669 assert)");
+  return BWAGPU_OK;
+}
+
+int bwagpu_chain2aln_stage(bwagpu_ctx_t* ctx, int slot, int32_t n_reads, int32_t n_chains, int32_t n_seeds,
+                           int64_t seq_bytes, bwagpu_batch_t* view) {
+  if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS || !view || n_reads < 0 || n_chains < 0 || n_seeds < 0 ||
+      seq_bytes < 0)
+    return BWAGPU_E_INVAL;
+  Slot& s = ctx->slot[slot];
+  if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
+  bwagpu_batch_t b{};
+  b.n_reads = n_reads;
+  b.n_chains = n_chains;
+  b.n_seeds = n_seeds;
+  b.seq_bytes = seq_bytes;
+  InLayout L;
+  L.make(b);
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
+  char* h = s.h_in.as<char>();
+  b.seq_off = (const int64_t*)(h + L.seq_off);
+  b.seq = (const uint8_t*)(h + L.seq);
+  b.read_chain_off = (const int32_t*)(h + L.rco);
+  b.chain_seed_off = (const int32_t*)(h + L.cso);
+  b.chain_rid = (const int32_t*)(h + L.rid);
+  b.chain_frac_rep = (const float*)(h + L.frac);
+  b.seeds = (const bwagpu_seed_t*)(h + L.seeds);
+  *view = b;
+  return BWAGPU_OK;
+}
+
+int bwagpu_chain2aln_results(bwagpu_ctx_t* ctx, int slot, const bwagpu_alnreg_t** regs, const int32_t** n) {
+  if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS || !regs || !n) return BWAGPU_E_INVAL;
+  Slot& s = ctx->slot[slot];
+  if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot's batch still in flight (wait first)");
+  *regs = s.h_out.as<const bwagpu_alnreg_t>();
+  *n = s.h_n.as<const int32_t>();
   return BWAGPU_OK;
 }
 

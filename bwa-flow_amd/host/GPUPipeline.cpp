@@ -316,6 +316,89 @@ void FlatBatch::pack(const ChainsRecord& rec) {
   c.seeds = seeds.data();
 }
 
+int FlatBatch::pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec) {
+  const int nr = rec.batch_num;
+  // pass 1: per-read counts -> offsets (kept here: unpack needs them)
+  seq_off.assign((size_t)nr + 1, 0);
+  read_chain_off.assign((size_t)nr + 1, 0);
+  std::vector<int64_t> seed_base((size_t)nr + 1, 0);
+  for (int i = 0; i < nr; ++i) {
+    const mem_chain_v& cv = rec.chains[i];
+    int64_t ns = 0;
+    for (size_t j = 0; j < cv.n; ++j) ns += cv.a[j].n;
+    seq_off[i + 1] = seq_off[i] + rec.seqs[i].l_seq;
+    read_chain_off[i + 1] = read_chain_off[i] + (int32_t)cv.n;
+    seed_base[i + 1] = seed_base[i] + ns;
+  }
+  const int32_t nc = read_chain_off[nr];
+  const int64_t ns = seed_base[nr];
+  if (ns > INT32_MAX) return BWAGPU_E_UNSUPPORTED;
+  const int rc = bwagpu_chain2aln_stage(ctx, slot, nr, nc, (int32_t)ns, seq_off[nr], &c);
+  if (rc != BWAGPU_OK) return rc;
+  int64_t* v_so = const_cast<int64_t*>(c.seq_off);
+  uint8_t* v_seq = const_cast<uint8_t*>(c.seq);
+  int32_t* v_rco = const_cast<int32_t*>(c.read_chain_off);
+  int32_t* v_cso = const_cast<int32_t*>(c.chain_seed_off);
+  int32_t* v_rid = const_cast<int32_t*>(c.chain_rid);
+  float* v_fr = const_cast<float*>(c.chain_frac_rep);
+  bwagpu_seed_t* v_sd = const_cast<bwagpu_seed_t*>(c.seeds);
+  memcpy(v_so, seq_off.data(), sizeof(int64_t) * ((size_t)nr + 1));
+  memcpy(v_rco, read_chain_off.data(), sizeof(int32_t) * ((size_t)nr + 1));
+  v_cso[0] = 0;
+  chain_seed_off.resize((size_t)nc + 1);
+  chain_seed_off[0] = 0;
+  // pass 2: every read's bases, chains and seeds, in place in pinned memory
+  parallel_ranges(nr, [&](int r0, int r1) {
+    for (int i = r0; i < r1; ++i) {
+      const bseq1_t& s = rec.seqs[i];
+      memcpy(v_seq + seq_off[i], s.seq, (size_t)s.l_seq);
+      const mem_chain_v& cv = rec.chains[i];
+      int64_t so = seed_base[i];
+      for (size_t j = 0; j < cv.n; ++j) {
+        const mem_chain_t& ch = cv.a[j];
+        const size_t ci = (size_t)read_chain_off[i] + j;
+        v_rid[ci] = ch.rid;
+        v_fr[ci] = ch.frac_rep;
+        for (int k = 0; k < ch.n; ++k) {
+          bwagpu_seed_t& t = v_sd[(size_t)so + k];
+          t.rbeg = ch.seeds[k].rbeg;
+          t.qbeg = ch.seeds[k].qbeg;
+          t.len = ch.seeds[k].len;
+          t.score = ch.seeds[k].score;
+          t.pad_ = 0;
+        }
+        so += ch.n;
+        v_cso[ci + 1] = (int32_t)so;
+        chain_seed_off[ci + 1] = (int32_t)so;
+      }
+    }
+  });
+  return BWAGPU_OK;
+}
+
+mem_alnreg_v* FlatBatch::unpack_from(const bwagpu_alnreg_t* rg, const int32_t* nn, int batch_num) const {
+  mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
+  if (!av) throw std::runtime_error("Memory allocation failed");
+  std::atomic<bool> oom{false};
+  parallel_ranges(batch_num, [&](int r0, int r1) {
+    for (int i = r0; i < r1; ++i) {
+      const size_t k = (size_t)nn[i];
+      av[i].n = av[i].m = k;
+      av[i].a = nullptr;
+      if (k) {
+        av[i].a = (mem_alnreg_t*)malloc(sizeof(mem_alnreg_t) * k);
+        if (!av[i].a) {
+          oom = true;
+          continue;
+        }
+        memcpy(av[i].a, &rg[chain_seed_off[read_chain_off[i]]], sizeof(mem_alnreg_t) * k);
+      }
+    }
+  });
+  if (oom) throw std::runtime_error("Memory allocation failed");
+  return av;
+}
+
 mem_alnreg_v* FlatBatch::unpack(int batch_num) const {
   mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
   if (!av) throw std::runtime_error("Memory allocation failed");
@@ -487,9 +570,9 @@ void ChainsToRegionsGPU::compute(int wid) {
         inflight.push_back(Job{rec, &flats[sl], sl});
         Job& j = inflight.back();
         auto t0 = std::chrono::steady_clock::now();
-        j.flat->pack(j.rec);
+        int rc = j.flat->pack_staged(ctx, j.slot, j.rec);
         auto t1 = std::chrono::steady_clock::now();
-        const int rc = bwagpu_chain2aln_submit(ctx, j.slot, &j.flat->c);
+        if (rc == BWAGPU_OK) rc = bwagpu_chain2aln_submit(ctx, j.slot, &j.flat->c);
         ns_[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
         ns_[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
         if (rc == BWAGPU_E_UNSUPPORTED || rc == BWAGPU_E_INVAL) {
@@ -514,7 +597,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     }
     Job& j = inflight.front();
     auto t0 = std::chrono::steady_clock::now();
-    const int rc = bwagpu_chain2aln_wait(ctx, j.slot, j.flat->regs.data(), j.flat->n.data());
+    const int rc = bwagpu_chain2aln_wait(ctx, j.slot, nullptr, nullptr);  // results stay in pinned memory
     auto t1 = std::chrono::steady_clock::now();
     ns_[2] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     if (rc == BWAGPU_E_RESULTS) {
@@ -532,7 +615,13 @@ void ChainsToRegionsGPU::compute(int wid) {
     out.start_idx = j.rec.start_idx;
     out.batch_num = j.rec.batch_num;
     out.seqs = j.rec.seqs;
-    out.alnreg = j.flat->unpack(j.rec.batch_num);
+    const bwagpu_alnreg_t* rg = nullptr;
+    const int32_t* nn = nullptr;
+    if (bwagpu_chain2aln_results(ctx, j.slot, &rg, &nn) != BWAGPU_OK) {
+      fail_all("results", BWAGPU_E_INVAL);
+      return;
+    }
+    out.alnreg = j.flat->unpack_from(rg, nn, j.rec.batch_num);
     reaper_.release(j.rec.chains, j.rec.batch_num);
     out.chains = nullptr;
     ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();

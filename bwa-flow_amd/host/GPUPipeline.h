@@ -81,8 +81,13 @@ struct FlatBatch {
   bwagpu_batch_t c{};
 
   void pack(const ChainsRecord& rec);  // ~ packReadData (FPGAPipeline.cpp:194-343)
+  // the same, written straight into the slot's pinned DMA buffer
+  // (bwagpu_chain2aln_stage): c then points there and _submit copies nothing
+  int pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec);
   // ~ processOutput (FPGAPipeline.cpp:29-130): regions into malloc'd mem_alnreg_v
   mem_alnreg_v* unpack(int batch_num) const;
+  // the same from a slot's pinned results (bwagpu_chain2aln_results)
+  mem_alnreg_v* unpack_from(const bwagpu_alnreg_t* regs, const int32_t* n, int batch_num) const;
 };
 
 // frees the chains of a record the way ChainsToRegions::compute does

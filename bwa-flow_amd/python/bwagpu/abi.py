@@ -106,6 +106,9 @@ PROTOS = {
     "bwagpu_set_watchdog_ms": (C.c_int, [_VP, C.c_int]),
     "bwagpu_chain2aln_submit": (C.c_int, [_VP, C.c_int, C.POINTER(BatchC)]),
     "bwagpu_chain2aln_wait": (C.c_int, [_VP, C.c_int, _VP, _VP]),
+    "bwagpu_chain2aln_stage": (C.c_int, [_VP, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int64,
+                                         C.POINTER(BatchC)]),
+    "bwagpu_chain2aln_results": (C.c_int, [_VP, C.c_int, C.POINTER(_VP), C.POINTER(_VP)]),
     "bwagpu_chain2aln": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP]),
     "bwagpu_chain2aln_device": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP, _VP, _VP]),
     "bwagpu_extend_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),

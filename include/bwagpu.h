@@ -21,6 +21,7 @@
  *       (src/fpga/SWTask.cpp:106-152, xlnx/XCLAgent.cpp:51,89-106): stage one
  *       packed read batch into a slot's buffers and launch asynchronously.
  *   bwagpu_chain2aln_wait
+ *   bwagpu_chain2aln_stage / _results (zero-copy host path)
  *       SWTask::finish -> XCLAgent::readOutput + processOutput
  *       (SWTask.cpp:154-180, XCLAgent.cpp:64, FPGAPipeline.cpp:29-130): wait
  *       with a watchdog and return finished mem_alnreg_t records.
@@ -291,6 +292,19 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t *ctx, int slot, const bwagpu_batch_t *b
 int bwagpu_chain2aln_wait(bwagpu_ctx_t *ctx, int slot, bwagpu_alnreg_t *out_regs, int32_t *out_n);
 int bwagpu_chain2aln(bwagpu_ctx_t *ctx, const bwagpu_batch_t *batch, bwagpu_alnreg_t *out_regs,
                      int32_t *out_n);
+
+/* Zero-copy host path (packReadData writing straight into the device's DMA
+   buffer instead of a staging copy, FPGAPipeline.cpp:252-336 / SWTask.cpp:
+   writeInput).  _stage sizes the slot's pinned input buffer for a batch of
+   these counts and fills *view with pointers into it (and the counts); the
+   caller writes the batch there and passes *view to _submit, which then skips
+   its copy.  The view stays valid until the slot's next _stage.  After a
+   successful _wait(ctx, slot, NULL, NULL), _results points *regs / *n at the
+   slot's pinned output (same layout as _wait's out_regs / out_n), valid until
+   the slot's next _submit. */
+int bwagpu_chain2aln_stage(bwagpu_ctx_t *ctx, int slot, int32_t n_reads, int32_t n_chains, int32_t n_seeds,
+                           int64_t seq_bytes, bwagpu_batch_t *view);
+int bwagpu_chain2aln_results(bwagpu_ctx_t *ctx, int slot, const bwagpu_alnreg_t **regs, const int32_t **n);
 /* all pointers in dev_batch / dev_out / dev_n are device pointers; stream is a
    hipStream_t (NULL = the context's slot-0 stream); asynchronous; dev_stats
    (device, 4 x int64: cells, rows, ext_calls, error flag) may be NULL.
