@@ -338,8 +338,10 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
 }
 
 // validate the flattened batch on the host (cheap O(n) checks so that a
-// malformed batch is an E_INVAL here, never an out-of-bounds access on device)
-int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b) {
+// malformed batch is an E_INVAL here, never an out-of-bounds access on device);
+// one pass over reads -> chains -> seeds, which also yields the longest read
+int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
+  *lq_max_out = 0;
   if (!b) return fail(ctx, BWAGPU_E_INVAL, "batch is NULL");
   if (b->n_reads < 0 || b->n_chains < 0 || b->n_seeds < 0 || b->seq_bytes < 0)
     return fail(ctx, BWAGPU_E_INVAL, "negative batch dimension");
@@ -352,32 +354,39 @@ int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b) {
     return fail(ctx, BWAGPU_E_INVAL, "read_chain_off does not span n_chains");
   if (b->chain_seed_off[0] != 0 || b->chain_seed_off[b->n_chains] != b->n_seeds)
     return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off does not span n_seeds");
+  if (b->n_chains && (!b->chain_rid || !b->chain_frac_rep)) return fail(ctx, BWAGPU_E_INVAL, "NULL chain array");
+  if (b->n_seeds && !b->seeds) return fail(ctx, BWAGPU_E_INVAL, "NULL seeds");
+  if (b->seq_bytes && !b->seq) return fail(ctx, BWAGPU_E_INVAL, "NULL seq");
+  // seeds must lie inside their read and inside [0, 2*l_pac); offsets monotone
+  const int64_t two = ctx->ref.l_pac << 1;
+  const int64_t* so = b->seq_off;
+  const int32_t* rco = b->read_chain_off;
+  const int32_t* cso = b->chain_seed_off;
+  const bwagpu_seed_t* sd = b->seeds;
+  int64_t lmax = 0;
+  bool bad_seed = false;
   for (int r = 0; r < b->n_reads; ++r) {
-    int64_t l = b->seq_off[r + 1] - b->seq_off[r];
+    const int64_t l = so[r + 1] - so[r];
     if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
     if (l > BWAGPU_MAX_READ_LEN) {
       char m[128];
       snprintf(m, sizeof m, "read %d has length %lld > %d", r, (long long)l, BWAGPU_MAX_READ_LEN);
       return fail(ctx, BWAGPU_E_UNSUPPORTED, m);
     }
-    if (b->read_chain_off[r + 1] < b->read_chain_off[r]) return fail(ctx, BWAGPU_E_INVAL, "read_chain_off not monotone");
-  }
-  if (b->n_chains && (!b->chain_rid || !b->chain_frac_rep)) return fail(ctx, BWAGPU_E_INVAL, "NULL chain array");
-  if (b->n_seeds && !b->seeds) return fail(ctx, BWAGPU_E_INVAL, "NULL seeds");
-  if (b->seq_bytes && !b->seq) return fail(ctx, BWAGPU_E_INVAL, "NULL seq");
-  for (int c = 0; c < b->n_chains; ++c)
-    if (b->chain_seed_off[c + 1] < b->chain_seed_off[c]) return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off not monotone");
-  // seeds must lie inside their read and inside [0, 2*l_pac)
-  const int64_t two = ctx->ref.l_pac << 1;
-  for (int r = 0; r < b->n_reads; ++r) {
-    const int l = (int)(b->seq_off[r + 1] - b->seq_off[r]);
-    for (int c = b->read_chain_off[r]; c < b->read_chain_off[r + 1]; ++c)
-      for (int k = b->chain_seed_off[c]; k < b->chain_seed_off[c + 1]; ++k) {
-        const bwagpu_seed_t& s = b->seeds[k];
-        if (s.qbeg < 0 || s.len <= 0 || s.qbeg + s.len > l || s.rbeg < 0 || s.rbeg + s.len > two)
-          return fail(ctx, BWAGPU_E_INVAL, "seed outside its read or the reference");
+    lmax = std::max(lmax, l);
+    const int c0 = rco[r], c1 = rco[r + 1];
+    if (c1 < c0) return fail(ctx, BWAGPU_E_INVAL, "read_chain_off not monotone");
+    for (int c = c0; c < c1; ++c) {
+      const int k0 = cso[c], k1 = cso[c + 1];
+      if (k1 < k0) return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off not monotone");
+      for (int k = k0; k < k1; ++k) {  // branch-free accumulation: one test per read
+        const bwagpu_seed_t& s = sd[k];
+        bad_seed |= (s.qbeg < 0) | (s.len <= 0) | ((int64_t)s.qbeg + s.len > l) | (s.rbeg < 0) | (s.rbeg + s.len > two);
       }
+    }
+    if (bad_seed) return fail(ctx, BWAGPU_E_INVAL, "seed outside its read or the reference");
   }
+  *lq_max_out = (int)lmax;
   return BWAGPU_OK;
 }
 
@@ -620,10 +629,9 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
-  int rc = check_batch(ctx, b);
-  if (rc) return rc;
   int lq_max = 0;
-  for (int r = 0; r < b->n_reads; ++r) lq_max = std::max<int>(lq_max, (int)(b->seq_off[r + 1] - b->seq_off[r]));
+  int rc = check_batch(ctx, b, &lq_max);
+  if (rc) return rc;
   if ((rc = check_lds(ctx, lq_max))) return rc;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   s.t_submit = std::chrono::steady_clock::now();

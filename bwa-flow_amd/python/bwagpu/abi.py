@@ -94,6 +94,30 @@ class SeedOpt(C.Structure):
 INTV_DTYPE = np.dtype([("x", "<u8", (3,)), ("info", "<u8")])  # bwagpu_intv_t == bwtintv_t
 assert INTV_DTYPE.itemsize == 32
 
+# bwagpu_chain_t: mem_chain_t (bwa/bwamem.c:180-186) without its seed vector
+CHAIN_DTYPE = np.dtype([("pos", "<i8"), ("rid", "<i4"), ("n", "<i4"), ("w", "<i4"), ("kept", "<i4"),
+                        ("first", "<i4"), ("is_alt", "<i4"), ("frac_rep", "<f4"), ("pad_", "<i4")])
+assert CHAIN_DTYPE.itemsize == 40
+
+
+class ChainOpt(C.Structure):
+    """bwagpu_chainopt_t: mem_opt_t's chaining fields (bwamem.c:62-72)"""
+    _fields_ = [("max_occ", C.c_int32), ("max_chain_gap", C.c_int32), ("min_chain_weight", C.c_int32),
+                ("max_chain_extend", C.c_int32), ("mask_level", C.c_float), ("drop_ratio", C.c_float)]
+
+
+class ChainsC(C.Structure):
+    """bwagpu_chains_t: a batch's chains in the bwagpu_batch_t layout"""
+    _fields_ = [("n_reads", C.c_int32), ("n_chains", C.c_int32), ("n_seeds", C.c_int64),
+                ("read_chain_off", C.c_void_p), ("chain_seed_off", C.c_void_p), ("chains", C.c_void_p),
+                ("seeds", C.c_void_p)]
+
+
+def default_chainopt() -> dict:
+    """mem_opt_init's chaining defaults (bwa/bwamem.c:62-72)"""
+    return dict(max_occ=500, max_chain_gap=10000, min_chain_weight=0, max_chain_extend=1 << 30, mask_level=0.5,
+                drop_ratio=0.5)
+
 # every entry point declared in include/bwagpu.h: name -> (restype, argtypes)
 _VP = C.c_void_p
 PROTOS = {
@@ -128,6 +152,11 @@ PROTOS = {
     "bwagpu_sw_stream": (C.c_int, [_VP, _VP, C.c_int64, _VP, C.c_int32, C.POINTER(C.c_int32)]),
     "bwagpu_collect_intv": (C.c_int, [_VP, C.POINTER(SeedOpt), C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int64,
                                        _VP]),
+    "bwagpu_set_alt": (C.c_int, [_VP, _VP]),
+    "bwagpu_seqs2chains": (C.c_int, [_VP, C.POINTER(SeedOpt), C.POINTER(ChainOpt), C.c_int32, _VP, _VP, C.c_int32,
+                                      C.POINTER(ChainsC)]),
+    "bwagpu_seqs2regions": (C.c_int, [_VP, C.POINTER(SeedOpt), C.POINTER(ChainOpt), C.c_int32, _VP, _VP, _VP,
+                                       C.POINTER(_VP), C.POINTER(C.c_int64)]),
 }
 
 _lib = None

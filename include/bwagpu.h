@@ -259,6 +259,32 @@ typedef struct {
 
 #define BWAGPU_MAX_SEED_READ 4096 /* longest read bwagpu_collect_intv takes */
 
+/* mem_opt_t's chaining fields (bwa/bwamem.h:38-52, defaults bwamem.c:62-72);
+   the band (w) and scoring (a, mat, gaps) come from the context's
+   bwagpu_opt_t, min_seed_len from bwagpu_seedopt_t */
+typedef struct {
+  int32_t max_occ;          /* -c, 500: SA positions taken per interval  */
+  int32_t max_chain_gap;    /* 10000                                     */
+  int32_t min_chain_weight; /* 0                                         */
+  int32_t max_chain_extend; /* 1<<30                                     */
+  float mask_level;         /* 0.50                                      */
+  float drop_ratio;         /* -D, 0.50                                  */
+} bwagpu_chainopt_t;
+
+/* one chain: mem_chain_t (bwa/bwamem.c:180-186) without its seed vector —
+   the seeds follow in the batch layout (chain_seed_off / seeds) */
+typedef struct {
+  int64_t pos;      /* the first seed's rbeg: the kbtree key            */
+  int32_t rid;      /* contig                                           */
+  int32_t n;        /* seeds                                            */
+  int32_t w;        /* mem_chain_weight (29-bit field)                  */
+  int32_t kept;     /* mem_chain_flt: 1, 2 or 3 (0 chains are dropped)  */
+  int32_t first;    /* mem_chain_flt's shadowed-chain index, -1 if none */
+  int32_t is_alt;
+  float frac_rep;
+  int32_t pad_;
+} bwagpu_chain_t;
+
 /* per-launch statistics of the last finished launch on a slot */
 typedef struct {
   double kernel_ms;      /* HIP-event time of the extension kernel(s)            */

@@ -52,6 +52,8 @@ def oracle_lib():
     lib.oracle_collect_intv.restype = C.c_int
     lib.oracle_bwt_sa.argtypes = [_VP, _VP, _VP, C.c_int, C.c_uint64]
     lib.oracle_bwt_sa.restype = C.c_uint64
+    lib.oracle_seqs2chains.argtypes = [C.POINTER(ChainEnv), C.c_int32, _VP, _VP, C.c_int, _VP, C.POINTER(ChainsOut)]
+    lib.oracle_seqs2chains.restype = C.c_int
     lib.oracle_fpga_pack.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), C.POINTER(abi.BatchC), _VP, C.c_int64,
                                      C.c_int32, C.POINTER(C.c_int32), _VP, _VP]
     lib.oracle_fpga_pack.restype = C.c_int64
@@ -206,6 +208,56 @@ def bwt_sa(bwt_hdr, bwt_words, sa, sa_intv, ks):
     sa = np.ascontiguousarray(sa, np.uint64)
     lib = oracle_lib()
     return np.array([lib.oracle_bwt_sa(_ptr(hdr), _ptr(words), _ptr(sa), int(sa_intv), int(k)) for k in ks], np.uint64)
+
+
+class ChainOptO(C.Structure):  # oracle_chainopt_t
+    _fields_ = [("max_occ", C.c_int32), ("max_chain_gap", C.c_int32), ("min_chain_weight", C.c_int32),
+                ("max_chain_extend", C.c_int32), ("mask_level", C.c_float), ("drop_ratio", C.c_float),
+                ("min_seed_len", C.c_int32)]
+
+
+class ChainEnv(C.Structure):  # oracle_chain_env_t
+    _fields_ = [("opt", C.POINTER(abi.Opt)), ("copt", C.POINTER(ChainOptO)), ("bns", C.POINTER(abi.Bns)),
+                ("pac", _VP), ("is_alt", _VP), ("bwt_hdr", _VP), ("bwt_words", _VP), ("sa", _VP),
+                ("sa_intv", C.c_int32), ("seedopt", _VP), ("split_factor", C.c_float)]
+
+
+class ChainsOut(C.Structure):  # oracle_chains_t
+    _fields_ = [("chains", _VP), ("seeds", _VP), ("cap_chains", C.c_int64), ("cap_seeds", C.c_int64),
+                ("n_chains", C.c_int64), ("n_seeds", C.c_int64)]
+
+
+def seqs2chains(opt: dict, copt: dict, seedopt, split_factor, ref: Ref, is_alt, bwt_hdr, bwt_words, sa, sa_intv,
+                seq_off, seq, raw: bool = False):
+    """SeqsToChains' chaining per read with the restatement (oracle/chain.c) ->
+    (read_chain_off int32[n+1], chains CHAIN_DTYPE, chain_seed_off int32, seeds SEED_DTYPE)"""
+    o = abi.opt_from_dict(opt)
+    co = ChainOptO(int(copt["max_occ"]), int(copt["max_chain_gap"]), int(copt["min_chain_weight"]),
+                   int(copt["max_chain_extend"]), float(copt["mask_level"]), float(copt["drop_ratio"]),
+                   int(seedopt[0]))
+    keep = dict(hdr=np.ascontiguousarray(np.asarray(bwt_hdr, np.int64)[:7]),
+                words=np.ascontiguousarray(bwt_words, np.uint32), sa=np.ascontiguousarray(sa, np.uint64),
+                so=np.ascontiguousarray(seedopt, np.int32)[:3].copy(),
+                alt=None if is_alt is None else np.ascontiguousarray(is_alt, np.uint8),
+                seq_off=np.ascontiguousarray(seq_off, np.int64), seq=np.ascontiguousarray(seq, np.uint8))
+    env = ChainEnv(C.pointer(o), C.pointer(co), C.pointer(ref.bns), _ptr(ref.pac),
+                   None if keep["alt"] is None else _ptr(keep["alt"]), _ptr(keep["hdr"]), _ptr(keep["words"]),
+                   _ptr(keep["sa"]), int(sa_intv), _ptr(keep["so"]), float(split_factor))
+    n = len(keep["seq_off"]) - 1
+    rco = np.zeros(n + 1, np.int32)
+    cap_c, cap_s = 4 * n + 16, 16 * n + 64
+    while True:
+        ch = np.zeros(cap_c, abi.CHAIN_DTYPE)
+        sd = np.zeros(cap_s, abi.SEED_DTYPE)
+        out = ChainsOut(_ptr(ch), _ptr(sd), cap_c, cap_s, 0, 0)
+        rc = oracle_lib().oracle_seqs2chains(C.byref(env), n, _ptr(keep["seq_off"]), _ptr(keep["seq"]), int(raw),
+                                             _ptr(rco), C.byref(out))
+        if rc == 0:
+            break
+        cap_c, cap_s = int(out.n_chains), int(out.n_seeds)
+    ch = ch[:out.n_chains]
+    cso = np.concatenate([[0], np.cumsum(ch["n"])]).astype(np.int32)
+    return rco, ch, cso, sd[:out.n_seeds]
 
 
 def fpga_pack(opt: dict, ref: Ref, batch: Batch):

@@ -189,3 +189,29 @@ def load_seed_sa():
     """-> (sa_intv, sampled suffix array uint64, query BWT positions, the reference's bwt_sa of each)"""
     z = _npz("seed_bwt")
     return int(z["sa_hdr"][0]), z["sa"], z["sa_q"], z["sa_v"]
+
+
+CHAIN_GOLD_SETS = ["c1", "mix", "long", "opt", "rep", "longopt"]
+
+
+def load_chain_gold(name):
+    """tests/golden/chain_<name>.npz (oracle/gen_chain.py: the reference's own mem_chain ->
+    mem_chain_flt -> mem_flt_chained_seeds) -> dict with opt (bwagpu_opt_t dict), copt
+    (bwagpu_chainopt_t dict), seedopt int32[3], split_factor, is_alt uint8[3], seq_off, seq,
+    raw (rco, chains[pos, rid, n, is_alt], seeds[rbeg, qbeg, len]) and final
+    (rco, chains[pos, rid, n, w, kept, first, is_alt], frac float32, seeds[rbeg, qbeg, len, score])"""
+    z = _npz("chain_" + name)
+    ov, fv = z["opt"], z["optf"]
+    opt = dict(a=int(ov[6]), b=int(ov[7]), o_del=int(ov[8]), e_del=int(ov[9]), o_ins=int(ov[10]),
+               e_ins=int(ov[11]), pen_clip5=5, pen_clip3=5, w=int(ov[0]), zdrop=100)
+    opt["mat"] = abi.fill_scmat(opt["a"], opt["b"])
+    copt = dict(max_occ=int(ov[2]), max_chain_gap=int(ov[1]), min_chain_weight=int(ov[3]),
+                max_chain_extend=int(ov[4]), mask_level=float(fv[0]), drop_ratio=float(fv[1]))
+    seedopt = np.array([ov[5], ov[12], ov[13]], np.int32)
+    alt = np.zeros(3, np.uint8)
+    if int(z["alt_rid"][0]) >= 0:
+        alt[int(z["alt_rid"][0])] = 1
+    return dict(opt=opt, copt=copt, seedopt=seedopt, split_factor=float(fv[2]), is_alt=alt,
+                seq_off=z["seq_off"], seq=z["seq"],
+                raw=(np.concatenate([[0], np.cumsum(z["raw_n"])]), z["raw_chn"], z["raw_seed"]),
+                final=(np.concatenate([[0], np.cumsum(z["chn_n"])]), z["chn"], z["chn_frac"], z["seed"]))
