@@ -20,6 +20,7 @@
 #include "align2.h"
 #include "reg2aln.h"
 #include "seed.h"
+#include "chain.h"
 #include "engine.h"
 
 using namespace bwagpu;
@@ -152,6 +153,16 @@ struct bwagpu_ctx {
   DevBwt bwt{};
   bool has_bwt = false;
   DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy;
+  // seeding's chaining (bwagpu_seqs2chains / bwagpu_seqs2regions): per read,
+  // per SA position, the kbtree arenas, mem_seed_sw tasks, the packed chains
+  DevBuf ch_npos, ch_posoff, ch_frac, ch_nout, ch_noseed, ch_nsw, ch_need, ch_swtab, ch_alt;
+  DevBuf ch_kpos, ch_rbeg, ch_qinfo, ch_label, ch_score, ch_slist, ch_ord, ch_chains, ch_nodes;
+  DevBuf ch_swoff, ch_swtasks, ch_swt, ch_swskip, ch_swres, ch_swscr;
+  DevBuf ch_ocoff, ch_osoff, ch_rco, ch_cso, ch_rid, ch_cfrac, ch_out, ch_seeds;
+  DevBuf ch_regoff, ch_regc;
+  HostBuf chh_tot, chh_rco, chh_cso, chh_chains, chh_seeds, chh_regs, chh_n;
+  Slot ch_slot;  // chain2aln scratch of bwagpu_seqs2regions
+  bool has_alt = false;
   // the FPGA wire format (bwagpu_sw_stream)
   DevBuf st_buf, st_start, st_q, st_tasks, st_lists, st_seen, st_ctr, st_out;
   // bwt_extend calls tier 1 spends on a read before tier 2 (one wave per read)
@@ -331,6 +342,23 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   if (ctx->a2_fork) (void)hipEventDestroy(ctx->a2_fork);
   ctx->a2_tasks.release(); ctx->a2_q.release(); ctx->a2_t.release(); ctx->a2_out.release();
   ctx->a2_scratch.release(); ctx->a2_lists.release(); ctx->a2_counts.release(); ctx->a2_boff.release();
+  ctx->ch_slot.release_scratch();
+  ctx->ch_slot.d_out.release(); ctx->ch_slot.d_n.release(); ctx->ch_slot.d_stats.release();
+  for (DevBuf* b : {&ctx->r2_tasks, &ctx->r2_q, &ctx->r2_out, &ctx->r2_cig, &ctx->r2_md, &ctx->r2_lists, &ctx->r2_z,
+                    &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->sd_off,
+                    &ctx->sd_seq, &ctx->sd_out, &ctx->sd_n, &ctx->sd_scratch, &ctx->sd_poff, &ctx->sd_pack,
+                    &ctx->sd_heavy, &ctx->st_buf, &ctx->st_start, &ctx->st_q, &ctx->st_tasks, &ctx->st_lists,
+                    &ctx->st_seen, &ctx->st_ctr, &ctx->st_out, &ctx->ch_npos, &ctx->ch_posoff, &ctx->ch_frac,
+                    &ctx->ch_nout, &ctx->ch_noseed, &ctx->ch_nsw, &ctx->ch_need, &ctx->ch_swtab, &ctx->ch_alt,
+                    &ctx->ch_kpos, &ctx->ch_rbeg, &ctx->ch_qinfo, &ctx->ch_label, &ctx->ch_score, &ctx->ch_slist,
+                    &ctx->ch_ord, &ctx->ch_chains, &ctx->ch_nodes, &ctx->ch_swoff, &ctx->ch_swtasks, &ctx->ch_swt,
+                    &ctx->ch_swskip, &ctx->ch_swres, &ctx->ch_swscr, &ctx->ch_ocoff, &ctx->ch_osoff, &ctx->ch_rco,
+                    &ctx->ch_cso, &ctx->ch_rid, &ctx->ch_cfrac, &ctx->ch_out, &ctx->ch_seeds, &ctx->ch_regoff,
+                    &ctx->ch_regc})
+    b->release();
+  for (HostBuf* b : {&ctx->chh_tot, &ctx->chh_rco, &ctx->chh_cso, &ctx->chh_chains, &ctx->chh_seeds, &ctx->chh_regs,
+                     &ctx->chh_n})
+    b->release();
   if (ctx->own_pac && ctx->d_pac) (void)hipFree(ctx->d_pac);
   if (ctx->d_ann_off) (void)hipFree(ctx->d_ann_off);
   if (ctx->d_ann_len) (void)hipFree(ctx->d_ann_len);
@@ -1448,17 +1476,17 @@ extern "C" int bwagpu_bwt_sa(bwagpu_ctx_t* ctx, int64_t n, const uint64_t* k, ui
   return BWAGPU_OK;
 }
 
-extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads,
-                                   const int64_t* seq_off, const uint8_t* seq, int32_t max_per_read,
-                                   bwagpu_intv_t* out, int64_t out_cap, int32_t* out_n) {
-  if (!ctx || !opt || n_reads < 0 || max_per_read < 1 || out_cap < 0 || (n_reads && (!seq_off || !out_n)) ||
-      (out_cap && !out))
-    return BWAGPU_E_INVAL;
+namespace {
+
+// the checks of bwagpu_collect_intv's arguments; *bases = the batch's bases
+int seed_validate(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads, const int64_t* seq_off,
+                  const uint8_t* seq, int64_t* bases) {
   if (!ctx->has_bwt) return fail(ctx, BWAGPU_E_INVAL, "no FM-index: call bwagpu_set_bwt first");
   if (opt->min_seed_len < 1 || opt->split_width < 0) return fail(ctx, BWAGPU_E_INVAL, "bad seeding options");
+  *bases = 0;
   if (n_reads == 0) return BWAGPU_OK;
-  const int64_t bases = seq_off[n_reads] - seq_off[0];
-  if (seq_off[0] != 0 || bases < 0 || (bases && !seq)) return fail(ctx, BWAGPU_E_INVAL, "seq_off must start at 0");
+  const int64_t nb = seq_off[n_reads] - seq_off[0];
+  if (seq_off[0] != 0 || nb < 0 || (nb && !seq)) return fail(ctx, BWAGPU_E_INVAL, "seq_off must start at 0");
   for (int32_t r = 0; r < n_reads; ++r) {
     const int64_t l = seq_off[r + 1] - seq_off[r];
     if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
@@ -1467,25 +1495,33 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   {  // every base is nt4 (0..4): eight bytes at a time, (b & 0x7f) + 0x7b carries into bit 7 iff b > 4
     int64_t i = 0;
     uint64_t bad = 0;
-    for (; i + 8 <= bases; i += 8) {
+    for (; i + 8 <= nb; i += 8) {
       uint64_t w;
       memcpy(&w, seq + i, 8);
       bad |= (((w & 0x7f7f7f7f7f7f7f7fULL) + 0x7b7b7b7b7b7b7b7bULL) | w) & 0x8080808080808080ULL;
     }
-    for (; i < bases; ++i) bad |= seq[i] > 4;
+    for (; i < nb; ++i) bad |= seq[i] > 4;
     if (bad) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
   }
-  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = ctx->slot[0].stream;
+  *bases = nb;
+  return BWAGPU_OK;
+}
+
+// H2D of the reads (when upload) and mem_collect_intv into per-read slots of
+// max_per_read intervals (ctx->sd_*), enqueued on st
+int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads, const int64_t* seq_off,
+                 const uint8_t* seq, int64_t bases, int32_t max_per_read, bool upload, hipStream_t st, SeedArgs& a) {
   HIPC(ctx->sd_off.ensure(sizeof(int64_t) * ((size_t)n_reads + 1)), "hipMalloc");
   HIPC(ctx->sd_seq.ensure((size_t)bases + 1), "hipMalloc");
   HIPC(ctx->sd_out.ensure(sizeof(bwagpu_intv_t) * (size_t)n_reads * (size_t)max_per_read), "hipMalloc");
   HIPC(ctx->sd_n.ensure(sizeof(int32_t) * (size_t)n_reads), "hipMalloc");
   HIPC(ctx->sd_scratch.ensure(sizeof(bwagpu_intv_t) * (size_t)seed_scratch_entries(bases, n_reads)), "hipMalloc");
-  HIPC(hipMemcpyAsync(ctx->sd_off.p, seq_off, sizeof(int64_t) * ((size_t)n_reads + 1), hipMemcpyHostToDevice, st),
-       "H2D");
-  if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, seq, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
-  SeedArgs a;
+  if (upload) {
+    HIPC(hipMemcpyAsync(ctx->sd_off.p, seq_off, sizeof(int64_t) * ((size_t)n_reads + 1), hipMemcpyHostToDevice, st),
+         "H2D");
+    if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, seq, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
+  }
+  a = SeedArgs{};
   a.n_reads = n_reads;
   a.seq_off = ctx->sd_off.as<int64_t>();
   a.seq = ctx->sd_seq.as<uint8_t>();
@@ -1504,6 +1540,25 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   a.flags = a.heavy + n_reads;
   a.p3_n = a.flags + n_reads;
   HIPC(launch_collect_intv(ctx->bwt, a, st), "collect_intv launch");
+  return BWAGPU_OK;
+}
+
+}  // namespace
+
+extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads,
+                                   const int64_t* seq_off, const uint8_t* seq, int32_t max_per_read,
+                                   bwagpu_intv_t* out, int64_t out_cap, int32_t* out_n) {
+  if (!ctx || !opt || n_reads < 0 || max_per_read < 1 || out_cap < 0 || (n_reads && (!seq_off || !out_n)) ||
+      (out_cap && !out))
+    return BWAGPU_E_INVAL;
+  int64_t bases = 0;
+  int rc = seed_validate(ctx, opt, n_reads, seq_off, seq, &bases);
+  if (rc) return rc;
+  if (n_reads == 0) return BWAGPU_OK;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = ctx->slot[0].stream;
+  SeedArgs a;
+  if ((rc = seed_enqueue(ctx, opt, n_reads, seq_off, seq, bases, max_per_read, true, st, a))) return rc;
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");
   // pack the per-read slots back to back (read order) and copy only those
@@ -1603,5 +1658,295 @@ extern "C" int bwagpu_sw_stream(bwagpu_ctx_t* ctx, const int32_t* i_buf, int64_t
   const int32_t n = c[kStrMax];
   if (n) HIPC(hipMemcpy(o_buf, ctx->st_out.p, sizeof(int32_t) * 5 * (size_t)n, hipMemcpyDeviceToHost), "D2H");
   *o_tasks = n;
+  return BWAGPU_OK;
+}
+
+// ------------------------------------------------------------------ chaining
+// SeqsToChains on the device (chain.h): mem_collect_intv, mem_chain's body,
+// mem_chain_flt and mem_flt_chained_seeds, with three host round trips for
+// sizes (positions, mem_seed_sw tasks when a read is long enough for them,
+// chains out).
+namespace {
+
+int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_chainopt_t* copt, int32_t n_reads,
+                 const int64_t* seq_off, const uint8_t* seq, bool raw, hipStream_t st, int64_t* n_chains,
+                 int64_t* n_seeds, int* lq_max_out) {
+  *n_chains = *n_seeds = 0;
+  if (copt->max_occ < 1 || copt->max_chain_gap < 0 || copt->max_chain_extend < 0 || !(copt->mask_level >= 0) ||
+      !(copt->drop_ratio >= 0))
+    return fail(ctx, BWAGPU_E_INVAL, "bad chaining options");
+  if (!ctx->bwt.sa) return fail(ctx, BWAGPU_E_INVAL, "no suffix array: pass it to bwagpu_set_bwt");
+  int64_t bases = 0;
+  int rc = seed_validate(ctx, sopt, n_reads, seq_off, seq, &bases);
+  if (rc) return rc;
+  int lq_max = 0;
+  for (int32_t r = 0; r < n_reads; ++r) lq_max = std::max<int>(lq_max, (int)(seq_off[r + 1] - seq_off[r]));
+  *lq_max_out = lq_max;
+  if (n_reads == 0) return BWAGPU_OK;
+  // mem_flt_chained_seeds' gate and min_HSP_score per read length
+  // (bwamem.c:609-611), in the host's double arithmetic
+  std::vector<int32_t> tab((size_t)lq_max + 1, -1);
+  bool any_sw = false;
+  {
+    std::vector<char> has((size_t)lq_max + 1, 0);
+    for (int32_t r = 0; r < n_reads; ++r) has[(size_t)(seq_off[r + 1] - seq_off[r])] = 1;
+    for (int l = 1; l <= lq_max; ++l) {
+      const double min_l = copt->min_chain_weight ? 1.1f * copt->min_chain_weight : 5.5f * log((double)l);
+      if (min_l > 0.05f * l) continue;
+      tab[(size_t)l] = (int)(ctx->opt.a * min_l + .499);
+      any_sw = any_sw || (has[(size_t)l] && l >= sopt->min_seed_len);
+    }
+  }
+  if (!raw && any_sw)
+    if (const char* why = align2_opt_unsupported(ctx->opt)) return fail(ctx, BWAGPU_E_UNSUPPORTED, why);
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  int32_t mpr = std::max(64, 2 * lq_max + 64);  // interval slots per read (grown on overflow)
+  SeedArgs sa;
+  if ((rc = seed_enqueue(ctx, sopt, n_reads, seq_off, seq, bases, mpr, true, st, sa))) return rc;
+  const size_t nr = (size_t)n_reads;
+  HIPC(ctx->ch_npos.ensure(sizeof(int32_t) * nr), "hipMalloc");
+  HIPC(ctx->ch_posoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
+  HIPC(ctx->ch_frac.ensure(sizeof(float) * nr), "hipMalloc");
+  HIPC(ctx->ch_nout.ensure(sizeof(int32_t) * nr), "hipMalloc");
+  HIPC(ctx->ch_noseed.ensure(sizeof(int32_t) * nr), "hipMalloc");
+  HIPC(ctx->ch_nsw.ensure(sizeof(int32_t) * nr), "hipMalloc");
+  HIPC(ctx->ch_need.ensure(sizeof(int32_t)), "hipMalloc");
+  HIPC(ctx->ch_swtab.ensure(sizeof(int32_t) * tab.size()), "hipMalloc");
+  HIPC(ctx->chh_tot.ensure(sizeof(int64_t) * 8), "hipHostMalloc");
+  HIPC(hipMemcpyAsync(ctx->ch_swtab.p, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice, st), "H2D");
+  int64_t* tot = ctx->chh_tot.as<int64_t>();
+  ChainArgs a{};
+  a.n_reads = n_reads;
+  a.seq_off = sa.seq_off;
+  a.seq = sa.seq;
+  a.max_occ = copt->max_occ;
+  a.max_chain_gap = copt->max_chain_gap;
+  a.min_chain_weight = copt->min_chain_weight;
+  a.max_chain_extend = copt->max_chain_extend;
+  a.mask_level = copt->mask_level;
+  a.drop_ratio = copt->drop_ratio;
+  a.min_seed_len = sopt->min_seed_len;
+  a.w = ctx->opt.w;
+  a.a = ctx->opt.a;
+  a.raw = raw ? 1 : 0;
+  a.l_pac = ctx->ref.l_pac;
+  a.n_seqs = ctx->ref.n_seqs;
+  a.ann_off = ctx->ref.ann_offset;
+  a.ann_len = ctx->ref.ann_len;
+  a.is_alt = ctx->has_alt ? ctx->ch_alt.as<uint8_t>() : nullptr;
+  a.pac = ctx->ref.pac;
+  a.sw_tab = ctx->ch_swtab.as<int32_t>();
+  a.n_pos = ctx->ch_npos.as<int32_t>();
+  a.pos_off = ctx->ch_posoff.as<int64_t>();
+  a.frac_rep = ctx->ch_frac.as<float>();
+  a.n_out = ctx->ch_nout.as<int32_t>();
+  a.n_oseed = ctx->ch_noseed.as<int32_t>();
+  a.n_sw = ctx->ch_nsw.as<int32_t>();
+  a.need = ctx->ch_need.as<int32_t>();
+  for (int pass = 0;; ++pass) {  // positions per read; a read out of interval slots reruns the search
+    a.intv = sa.out;
+    a.intv_n = sa.out_n;
+    a.max_per_read = sa.max_per_read;
+    HIPC(hipMemsetAsync(a.need, 0, sizeof(int32_t), st), "memset");
+    HIPC(launch_chain_count(a, st), "chain_count launch");
+    HIPC(launch_scan_i32(a.n_pos, a.pos_off, n_reads, st), "scan launch");
+    HIPC(hipMemcpyAsync(tot, a.pos_off + n_reads, sizeof(int64_t), hipMemcpyDeviceToHost, st), "D2H");
+    HIPC(hipMemcpyAsync(tot + 1, a.need, sizeof(int32_t), hipMemcpyDeviceToHost, st), "D2H");
+    HIPC(hipStreamSynchronize(st), "sync");
+    const int32_t need = (int32_t)(uint32_t)tot[1];
+    if (need <= 0) break;
+    if (pass) return fail(ctx, BWAGPU_E_DEVICE, "interval slots still overflow");
+    if ((rc = seed_enqueue(ctx, sopt, n_reads, seq_off, seq, bases, need, false, st, sa))) return rc;
+  }
+  const int64_t P = tot[0];
+  const size_t p1 = (size_t)std::max<int64_t>(P, 1);
+  HIPC(ctx->ch_kpos.ensure(sizeof(uint64_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_rbeg.ensure(sizeof(uint64_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_qinfo.ensure(sizeof(int2) * p1), "hipMalloc");
+  HIPC(ctx->ch_label.ensure(sizeof(int32_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_score.ensure(sizeof(int32_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_slist.ensure(sizeof(int32_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_ord.ensure(sizeof(int32_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_chains.ensure(sizeof(DChain) * p1), "hipMalloc");
+  HIPC(ctx->ch_nodes.ensure(sizeof(BNode) * (size_t)node_total(P, n_reads)), "hipMalloc");
+  a.kpos = ctx->ch_kpos.as<uint64_t>();
+  a.rbeg = ctx->ch_rbeg.as<uint64_t>();
+  a.qinfo = ctx->ch_qinfo.as<int2>();
+  a.label = ctx->ch_label.as<int32_t>();
+  a.score = ctx->ch_score.as<int32_t>();
+  a.slist = ctx->ch_slist.as<int32_t>();
+  a.ord = ctx->ch_ord.as<int32_t>();
+  a.chains = ctx->ch_chains.as<DChain>();
+  a.nodes = ctx->ch_nodes.as<BNode>();
+  HIPC(launch_chain_emit(a, st), "chain_emit launch");
+  if (P) HIPC(launch_bwt_sa(ctx->bwt, P, a.kpos, a.rbeg, st), "bwt_sa launch");
+  HIPC(launch_chain_build(a, st), "chain_build launch");
+  if (!raw && any_sw) {  // mem_flt_chained_seeds: every kept seed of a long read realigned
+    HIPC(ctx->ch_swoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
+    HIPC(launch_scan_i32(a.n_sw, ctx->ch_swoff.as<int64_t>(), n_reads, st), "scan launch");
+    HIPC(hipMemcpyAsync(tot + 2, ctx->ch_swoff.as<int64_t>() + n_reads, sizeof(int64_t), hipMemcpyDeviceToHost, st),
+         "D2H");
+    HIPC(hipStreamSynchronize(st), "sync");
+    const int64_t T = tot[2];
+    if (T > INT32_MAX / 2) return fail(ctx, BWAGPU_E_UNSUPPORTED, "too many seeds to realign");
+    if (T) {
+      HIPC(ctx->ch_swtasks.ensure(sizeof(bwagpu_align2_task_t) * (size_t)T), "hipMalloc");
+      HIPC(ctx->ch_swt.ensure((size_t)kSwWin * (size_t)T), "hipMalloc");
+      HIPC(ctx->ch_swskip.ensure(sizeof(int32_t) * (size_t)T), "hipMalloc");
+      HIPC(ctx->ch_swres.ensure(sizeof(bwagpu_kswr_t) * (size_t)T), "hipMalloc");
+      HIPC(ctx->ch_swscr.ensure(8 * ((size_t)kSwWin * (size_t)T + (size_t)T)), "hipMalloc");
+      ChainSw sw{ctx->ch_swoff.as<int64_t>(), ctx->ch_swtasks.as<bwagpu_align2_task_t>(), ctx->ch_swt.as<uint8_t>(),
+                 ctx->ch_swskip.as<int32_t>(), ctx->ch_swres.as<bwagpu_kswr_t>()};
+      HIPC(launch_chain_sw_prep(a, sw, st), "chain_sw_prep launch");
+      if ((rc = bwagpu_align2_device(ctx, (int32_t)T, sw.tasks, sa.seq, sw.tpool, ctx->ch_swres.as<bwagpu_kswr_t>(),
+                                     ctx->ch_swscr.p, st)))
+        return rc;
+      HIPC(launch_chain_sw_apply(a, sw, st), "chain_sw_apply launch");
+    }
+  }
+  HIPC(ctx->ch_ocoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
+  HIPC(ctx->ch_osoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
+  HIPC(launch_scan_i32(a.n_out, ctx->ch_ocoff.as<int64_t>(), n_reads, st), "scan launch");
+  HIPC(launch_scan_i32(a.n_oseed, ctx->ch_osoff.as<int64_t>(), n_reads, st), "scan launch");
+  HIPC(hipMemcpyAsync(tot + 3, ctx->ch_ocoff.as<int64_t>() + n_reads, sizeof(int64_t), hipMemcpyDeviceToHost, st),
+       "D2H");
+  HIPC(hipMemcpyAsync(tot + 4, ctx->ch_osoff.as<int64_t>() + n_reads, sizeof(int64_t), hipMemcpyDeviceToHost, st),
+       "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
+  const int64_t nc = tot[3], ns = tot[4];
+  if (nc > INT32_MAX - 1 || ns > INT32_MAX - 1) return fail(ctx, BWAGPU_E_UNSUPPORTED, "batch has too many chains");
+  HIPC(ctx->ch_rco.ensure(sizeof(int32_t) * (nr + 1)), "hipMalloc");
+  HIPC(ctx->ch_cso.ensure(sizeof(int32_t) * ((size_t)nc + 1)), "hipMalloc");
+  HIPC(ctx->ch_rid.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(nc, 1)), "hipMalloc");
+  HIPC(ctx->ch_cfrac.ensure(sizeof(float) * (size_t)std::max<int64_t>(nc, 1)), "hipMalloc");
+  HIPC(ctx->ch_out.ensure(sizeof(bwagpu_chain_t) * (size_t)std::max<int64_t>(nc, 1)), "hipMalloc");
+  HIPC(ctx->ch_seeds.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max<int64_t>(ns, 1)), "hipMalloc");
+  ChainPack pk{ctx->ch_ocoff.as<int64_t>(), ctx->ch_osoff.as<int64_t>(), ctx->ch_rco.as<int32_t>(),
+               ctx->ch_cso.as<int32_t>(), ctx->ch_rid.as<int32_t>(), ctx->ch_cfrac.as<float>(),
+               ctx->ch_out.as<bwagpu_chain_t>(), ctx->ch_seeds.as<bwagpu_seed_t>()};
+  HIPC(launch_chain_pack(a, pk, st), "chain_pack launch");
+  *n_chains = nc;
+  *n_seeds = ns;
+  return BWAGPU_OK;
+}
+
+}  // namespace
+
+extern "C" int bwagpu_set_alt(bwagpu_ctx_t* ctx, const uint8_t* is_alt) {
+  if (!ctx) return BWAGPU_E_INVAL;
+  if (!is_alt) {
+    ctx->has_alt = false;
+    return BWAGPU_OK;
+  }
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  HIPC(ctx->ch_alt.ensure((size_t)std::max(ctx->ref.n_seqs, 1)), "hipMalloc");
+  HIPC(hipMemcpy(ctx->ch_alt.p, is_alt, (size_t)ctx->ref.n_seqs, hipMemcpyHostToDevice), "H2D");
+  ctx->has_alt = true;
+  return BWAGPU_OK;
+}
+
+extern "C" int bwagpu_seqs2chains(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_chainopt_t* copt,
+                                  int32_t n_reads, const int64_t* seq_off, const uint8_t* seq, int32_t raw,
+                                  bwagpu_chains_t* out) {
+  if (!ctx || !sopt || !copt || !out || n_reads < 0 || (n_reads && !seq_off)) return BWAGPU_E_INVAL;
+  *out = bwagpu_chains_t{};
+  hipStream_t st = ctx->slot[0].stream;
+  int64_t nc = 0, ns = 0;
+  int lq = 0;
+  int rc = run_chaining(ctx, sopt, copt, n_reads, seq_off, seq, raw != 0, st, &nc, &ns, &lq);
+  if (rc) return rc;
+  const size_t nr = (size_t)n_reads;
+  HIPC(ctx->chh_rco.ensure(sizeof(int32_t) * (nr + 1)), "hipHostMalloc");
+  HIPC(ctx->chh_cso.ensure(sizeof(int32_t) * ((size_t)nc + 1)), "hipHostMalloc");
+  HIPC(ctx->chh_chains.ensure(sizeof(bwagpu_chain_t) * (size_t)std::max<int64_t>(nc, 1)), "hipHostMalloc");
+  HIPC(ctx->chh_seeds.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max<int64_t>(ns, 1)), "hipHostMalloc");
+  if (n_reads) {
+    HIPC(hipMemcpyAsync(ctx->chh_rco.p, ctx->ch_rco.p, sizeof(int32_t) * (nr + 1), hipMemcpyDeviceToHost, st), "D2H");
+    HIPC(hipMemcpyAsync(ctx->chh_cso.p, ctx->ch_cso.p, sizeof(int32_t) * ((size_t)nc + 1), hipMemcpyDeviceToHost, st),
+         "D2H");
+    if (nc)
+      HIPC(hipMemcpyAsync(ctx->chh_chains.p, ctx->ch_out.p, sizeof(bwagpu_chain_t) * (size_t)nc, hipMemcpyDeviceToHost,
+                          st),
+           "D2H");
+    if (ns)
+      HIPC(hipMemcpyAsync(ctx->chh_seeds.p, ctx->ch_seeds.p, sizeof(bwagpu_seed_t) * (size_t)ns, hipMemcpyDeviceToHost,
+                          st),
+           "D2H");
+    HIPC(hipStreamSynchronize(st), "sync");
+  } else {
+    ctx->chh_rco.as<int32_t>()[0] = 0;
+    ctx->chh_cso.as<int32_t>()[0] = 0;
+  }
+  out->n_reads = n_reads;
+  out->n_chains = (int32_t)nc;
+  out->n_seeds = ns;
+  out->read_chain_off = ctx->chh_rco.as<int32_t>();
+  out->chain_seed_off = ctx->chh_cso.as<int32_t>();
+  out->chains = ctx->chh_chains.as<bwagpu_chain_t>();
+  out->seeds = ctx->chh_seeds.as<bwagpu_seed_t>();
+  return BWAGPU_OK;
+}
+
+extern "C" int bwagpu_seqs2regions(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_chainopt_t* copt,
+                                   int32_t n_reads, const int64_t* seq_off, const uint8_t* seq, int32_t* out_n,
+                                   const bwagpu_alnreg_t** regs, int64_t* n_regs) {
+  if (!ctx || !sopt || !copt || !regs || !n_regs || n_reads < 0 || (n_reads && (!seq_off || !out_n)))
+    return BWAGPU_E_INVAL;
+  *regs = nullptr;
+  *n_regs = 0;
+  for (int32_t r = 0; r < n_reads; ++r)
+    if (seq_off[r + 1] - seq_off[r] > BWAGPU_MAX_READ_LEN)
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_READ_LEN");
+  hipStream_t st = ctx->slot[0].stream;
+  int64_t nc = 0, ns = 0;
+  int lq = 0;
+  int rc = run_chaining(ctx, sopt, copt, n_reads, seq_off, seq, false, st, &nc, &ns, &lq);
+  if (rc) return rc;
+  if (n_reads == 0) return BWAGPU_OK;
+  if ((rc = check_lds(ctx, lq))) return rc;
+  Slot& s = ctx->ch_slot;
+  const size_t nr = (size_t)n_reads;
+  HIPC(s.d_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max<int64_t>(ns, 1)), "hipMalloc(out)");
+  HIPC(s.d_n.ensure(sizeof(int32_t) * nr), "hipMalloc(out_n)");
+  HIPC(s.d_stats.ensure(sizeof(int64_t) * ST_N), "hipMalloc(stats)");
+  HIPC(hipMemsetAsync(s.d_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset stats");
+  DevBatch db;
+  db.n_reads = n_reads;
+  db.n_chains = (int32_t)nc;
+  db.n_seeds = (int32_t)ns;
+  db.seq_off = ctx->sd_off.as<int64_t>();
+  db.seq = ctx->sd_seq.as<uint8_t>();
+  db.read_chain_off = ctx->ch_rco.as<int32_t>();
+  db.chain_seed_off = ctx->ch_cso.as<int32_t>();
+  db.chain_rid = ctx->ch_rid.as<int32_t>();
+  db.chain_frac_rep = ctx->ch_cfrac.as<float>();
+  db.seeds = ctx->ch_seeds.as<bwagpu_seed_t>();
+  if ((rc = enqueue_chain2aln(ctx, s, db, lq, s.d_out.as<bwagpu_alnreg_t>(), s.d_n.as<int32_t>(),
+                              s.d_stats.as<int64_t>(), st)))
+    return rc;
+  HIPC(ctx->ch_regoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
+  HIPC(launch_scan_i32(s.d_n.as<int32_t>(), ctx->ch_regoff.as<int64_t>(), n_reads, st), "scan launch");
+  int64_t* tot = ctx->chh_tot.as<int64_t>();
+  HIPC(hipMemcpyAsync(tot + 5, ctx->ch_regoff.as<int64_t>() + n_reads, sizeof(int64_t), hipMemcpyDeviceToHost, st),
+       "D2H");
+  HIPC(hipMemcpyAsync(tot + 6, s.d_stats.as<int64_t>() + ST_ERR, sizeof(int64_t), hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipMemcpyAsync(out_n, s.d_n.p, sizeof(int32_t) * nr, hipMemcpyDeviceToHost, st), "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
+  const int64_t nreg = tot[5];
+  HIPC(ctx->ch_regc.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max<int64_t>(nreg, 1)), "hipMalloc");
+  HIPC(ctx->chh_regs.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max<int64_t>(nreg, 1)), "hipHostMalloc");
+  HIPC(launch_reg_compact(n_reads, db.read_chain_off, db.chain_seed_off, s.d_out.as<bwagpu_alnreg_t>(),
+                          ctx->ch_regoff.as<int64_t>(), ctx->ch_regc.as<bwagpu_alnreg_t>(), st),
+       "reg_compact launch");
+  if (nreg)
+    HIPC(hipMemcpyAsync(ctx->chh_regs.p, ctx->ch_regc.p, sizeof(bwagpu_alnreg_t) * (size_t)nreg, hipMemcpyDeviceToHost,
+                        st),
+         "D2H");
+  HIPC(hipStreamSynchronize(st), "sync");
+  *regs = ctx->chh_regs.as<const bwagpu_alnreg_t>();
+  *n_regs = nreg;
+  if (tot[6] & ERR_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_READ_LEN");
+  if (tot[6] & ERR_RID)
+    return fail(ctx, BWAGPU_E_RESULTS, "a chain's first seed is not inside contig chain_rid (bwamem.c:669 assert)");
   return BWAGPU_OK;
 }

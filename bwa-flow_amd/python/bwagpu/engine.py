@@ -276,6 +276,56 @@ class Engine:
         cnt = cnt[:n]
         return cnt, out[:int(cnt.sum())]
 
+    def set_alt(self, is_alt):
+        """per-contig ALT flags for the chaining (None: none)"""
+        self._alt = None if is_alt is None else np.ascontiguousarray(is_alt, np.uint8)
+        self._check(self.lib.bwagpu_set_alt(self.ctx, None if self._alt is None else _ptr(self._alt)), "set_alt")
+
+    @staticmethod
+    def _seed_chain_opts(seedopt, split_factor, chainopt):
+        so = np.asarray(seedopt, np.int32)
+        co = abi.default_chainopt() if chainopt is None else chainopt
+        return (abi.SeedOpt(int(so[0]), int(so[1]), int(so[2]), float(split_factor)),
+                abi.ChainOpt(int(co["max_occ"]), int(co["max_chain_gap"]), int(co["min_chain_weight"]),
+                             int(co["max_chain_extend"]), float(co["mask_level"]), float(co["drop_ratio"])))
+
+    def seqs2chains(self, seq_off, seq, seedopt=(19, 10, 20), split_factor: float = 1.5, chainopt: dict | None = None,
+                    raw: bool = False):
+        """bwa-flow's SeqsToChains on the device (src/bwa_wrapper.cpp:105-115) ->
+        (read_chain_off int32[n+1], chains CHAIN_DTYPE, chain_seed_off int32, seeds SEED_DTYPE)"""
+        seq_off = np.ascontiguousarray(seq_off, np.int64)
+        seq = np.ascontiguousarray(seq, np.uint8)
+        n = len(seq_off) - 1
+        so, co = self._seed_chain_opts(seedopt, split_factor, chainopt)
+        out = abi.ChainsC()
+        self._check(self.lib.bwagpu_seqs2chains(self.ctx, C.byref(so), C.byref(co), n, _ptr(seq_off), _ptr(seq),
+                                                int(raw), C.byref(out)), "seqs2chains")
+        nc, ns = out.n_chains, out.n_seeds
+
+        def view(p, dt, k):
+            if k == 0:
+                return np.zeros(0, dt)
+            return np.frombuffer((C.c_char * (k * np.dtype(dt).itemsize)).from_address(p), dt).copy()
+        return (view(out.read_chain_off, np.int32, n + 1), view(out.chains, abi.CHAIN_DTYPE, nc),
+                view(out.chain_seed_off, np.int32, nc + 1), view(out.seeds, abi.SEED_DTYPE, ns))
+
+    def seqs2regions(self, seq_off, seq, seedopt=(19, 10, 20), split_factor: float = 1.5,
+                     chainopt: dict | None = None):
+        """SeqsToChains + ChainsToRegions fused on the device -> (regions per read int32[n],
+        regions ALNREG_DTYPE back to back in read order)"""
+        seq_off = np.ascontiguousarray(seq_off, np.int64)
+        seq = np.ascontiguousarray(seq, np.uint8)
+        n = len(seq_off) - 1
+        so, co = self._seed_chain_opts(seedopt, split_factor, chainopt)
+        cnt = np.zeros(max(n, 1), np.int32)
+        regs, nreg = C.c_void_p(), C.c_int64()
+        self._check(self.lib.bwagpu_seqs2regions(self.ctx, C.byref(so), C.byref(co), n, _ptr(seq_off), _ptr(seq),
+                                                 _ptr(cnt), C.byref(regs), C.byref(nreg)), "seqs2regions")
+        k = nreg.value
+        out = np.zeros(0, abi.ALNREG_DTYPE) if k == 0 else np.frombuffer(
+            (C.c_char * (k * abi.ALNREG_DTYPE.itemsize)).from_address(regs.value), abi.ALNREG_DTYPE).copy()
+        return cnt[:n], out
+
     def prof_start(self, max_launches: int):
         """time the next max_launches launches of the dominant extension kernel"""
         self._check(self.lib.bwagpu_prof_start(self.ctx, max_launches), "prof_start")

@@ -413,6 +413,51 @@ int bwagpu_collect_intv(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *opt, int32_t 
    (bwamem.c:288).  Needs the suffix array in bwagpu_set_bwt.  Blocking. */
 int bwagpu_bwt_sa(bwagpu_ctx_t *ctx, int64_t n, const uint64_t *k, uint64_t *out);
 
+/* ---- seeding's chaining: SeqsToChains on the device ---- */
+
+/* a batch's chains in the bwagpu_batch_t layout: read r's chains are
+   read_chain_off[r] .. read_chain_off[r+1]-1 (in the order bwa-flow's
+   SeqsToChains leaves them), chain c's seeds chain_seed_off[c] ..
+   chain_seed_off[c+1]-1 (mem_chain_t.seeds, in order) */
+typedef struct {
+  int32_t n_reads, n_chains;
+  int64_t n_seeds;
+  const int32_t *read_chain_off;  /* [n_reads+1]  */
+  const int32_t *chain_seed_off;  /* [n_chains+1] */
+  const bwagpu_chain_t *chains;   /* [n_chains]   */
+  const bwagpu_seed_t *seeds;     /* [n_seeds]    */
+} bwagpu_chains_t;
+
+/* per-contig ALT flags (bntann1_t.is_alt, bwa/bntseq.h:41) that mem_chain
+   copies into its chains and mem_chain_flt reads (bwamem.c:305, 359); n_seqs
+   bytes, NULL = none (the default) */
+int bwagpu_set_alt(bwagpu_ctx_t *ctx, const uint8_t *is_alt);
+
+/* bwa-flow's SeqsToChains (src/bwa_wrapper.cpp:105-115) for every read of a
+   batch: mem_collect_intv, then mem_chain's body (bwamem.c:260-330: bwt_sa of
+   each interval's positions stepped to max_occ, bns_intv2rid, the kbtree of
+   chains with test_and_merge), mem_chain_flt (336-396) and
+   mem_flt_chained_seeds (607-624, mem_seed_sw through ksw_align2).  raw = 1
+   stops after mem_chain (chains in kbtree order; w = kept = 0, first = -1).
+   Reads as for bwagpu_collect_intv (host buffers, nt4, <= BWAGPU_MAX_SEED_READ
+   bases); needs the suffix array in bwagpu_set_bwt.  *out points into
+   context-owned pinned memory, valid until the next call on the context.
+   Blocking. */
+int bwagpu_seqs2chains(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *sopt, const bwagpu_chainopt_t *copt,
+                       int32_t n_reads, const int64_t *seq_off, const uint8_t *seq, int32_t raw,
+                       bwagpu_chains_t *out);
+
+/* SeqsToChains and ChainsToRegions (src/Pipeline.cpp:110-121, 503-544) fused
+   on the device: the chains never leave it.  out_n[r] = read r's regions
+   (mem_chain2aln of each of its chains in order, as bwagpu_chain2aln returns
+   them); *regs = every read's regions back to back in read order, *n_regs in
+   all (context-owned pinned memory, valid until the next call).  Reads <=
+   BWAGPU_MAX_READ_LEN.  BWAGPU_E_RESULTS as for bwagpu_chain2aln_wait.
+   Blocking. */
+int bwagpu_seqs2regions(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *sopt, const bwagpu_chainopt_t *copt,
+                        int32_t n_reads, const int64_t *seq_off, const uint8_t *seq, int32_t *out_n,
+                        const bwagpu_alnreg_t **regs, int64_t *n_regs);
+
 /* Tuning / tests: bwagpu_collect_intv runs each read on one lane until it has
    made `budget` bwt_extend calls (default 1024, about the 90th percentile of a
    150 bp read on a chr21-sized index), then hands it to a second kernel that
