@@ -43,6 +43,29 @@ class RefBatch:
         return hashlib.sha256(c.view(np.uint8).tobytes()).digest() == self.regs_sha256
 
 
+def load_bwa_index(prefix: str):
+    """a bwa index's FM-index and sampled suffix array from its files
+    (bwt_dump_bwt / bwt_dump_sa, bwa/bwt.c:385-407; restored as
+    bwt_restore_bwt / bwt_restore_sa do, 421-462) -> (hdr int64[8]: primary,
+    L2[0..4], seq_len, bwt_size; occurrence words uint32; sa uint64 with
+    sa[0] = -1 as bwa sets it; sa_intv)"""
+    raw = np.fromfile(prefix + ".bwt", np.uint8)
+    head = raw[:40].view(np.uint64)
+    words = raw[40:].view(np.uint32)
+    primary, l2 = int(head[0]), [0] + [int(x) for x in head[1:5]]
+    sraw = np.fromfile(prefix + ".sa", np.uint8)
+    sh = sraw[:56].view(np.uint64)
+    if int(sh[0]) != primary or int(sh[6]) != l2[4]:
+        raise RuntimeError("SA-BWT inconsistency")
+    sa_intv, seq_len = int(sh[5]), int(sh[6])
+    n_sa = (seq_len + sa_intv) // sa_intv
+    sa = np.empty(n_sa, np.uint64)
+    sa[0] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    sa[1:] = sraw[56:56 + 8 * (n_sa - 1)].view(np.uint64)
+    hdr = np.array([primary, *l2, seq_len, len(words)], np.int64)
+    return hdr, words, sa, sa_intv
+
+
 # ---------------------------------------------------------------- C3 / C5 regime
 # tests/golden/c3_grch38.npz (oracle/gen_c3_fixture.py): synthetic chains on a
 # GRCh38-shaped genome (195 contigs, l_pac 3.1e9) with the reference's own

@@ -26,6 +26,10 @@
  *          bwa-flow_amd/host/sam_hooks.c, the mem_sam_pe loop run as
  *          collect -> flush -> replay passes (include/bwagpu_sam.h).
  *
+ *   gpuchain SeqsToChains and ChainsToRegions fused on the device
+ *          (bwagpu_seqs2regions: interval search, SA lookups, the kbtree
+ *          chaining, mem_chain_flt, mem_flt_chained_seeds and mem_chain2aln;
+ *          no chain exists on the host), then the SAM stage as in `gpusam`.
  *   gpuseed `gpusam` with seeding's interval collection and SA lookups on the
  *          device too: bwagpu_collect_intv (mem_collect_intv) and
  *          bwagpu_bwt_sa (bwt_sa) per batch; the chaining around them
@@ -42,7 +46,7 @@
  * and one JSON line of per-phase wall times to stderr.  The -m gpu test
  * (tests/test_gpu_sam.py) diffs `ref` against `gpu` byte for byte.
  *
- * usage: sam_harness <ref|split|gpu|gpusam|gpuseed> <workdir> <out.sam> <seed> <n_pairs> <len:150|100|250|mix>
+ * usage: sam_harness <ref|split|gpu|gpusam|gpuseed|gpuchain> <workdir> <out.sam> <seed> <n_pairs> <len:150|100|250|mix>
  *                    [batch_bases=10000000] [threads=8] [genome_len=1000000]
  */
 #include <dlfcn.h>
@@ -111,6 +115,9 @@ static struct {
   int (*collect_intv)(bwagpu_ctx_t *, const bwagpu_seedopt_t *, int32_t, const int64_t *, const uint8_t *, int32_t,
                       bwagpu_intv_t *, int64_t, int32_t *);
   int (*bwt_sa)(bwagpu_ctx_t *, int64_t, const uint64_t *, uint64_t *);
+  int (*set_alt)(bwagpu_ctx_t *, const uint8_t *);
+  int (*seqs2regions)(bwagpu_ctx_t *, const bwagpu_seedopt_t *, const bwagpu_chainopt_t *, int32_t, const int64_t *,
+                      const uint8_t *, int32_t *, const bwagpu_alnreg_t **, int64_t *);
   /* libgpusam.so (gpusam mode) */
   int (*sc_create)(bwagpu_ctx_t *, int32_t, int32_t, bwagpu_samcache_t **);
   int (*sc_destroy)(bwagpu_samcache_t *);
@@ -148,6 +155,10 @@ static void gpu_load(void)
   G.collect_intv = (int (*)(bwagpu_ctx_t *, const bwagpu_seedopt_t *, int32_t, const int64_t *, const uint8_t *,
                             int32_t, bwagpu_intv_t *, int64_t, int32_t *))dlsym(G.h, "bwagpu_collect_intv");
   G.bwt_sa = (int (*)(bwagpu_ctx_t *, int64_t, const uint64_t *, uint64_t *))dlsym(G.h, "bwagpu_bwt_sa");
+  G.set_alt = (int (*)(bwagpu_ctx_t *, const uint8_t *))dlsym(G.h, "bwagpu_set_alt");
+  G.seqs2regions = (int (*)(bwagpu_ctx_t *, const bwagpu_seedopt_t *, const bwagpu_chainopt_t *, int32_t,
+                            const int64_t *, const uint8_t *, int32_t *, const bwagpu_alnreg_t **,
+                            int64_t *))dlsym(G.h, "bwagpu_seqs2regions");
   if (!G.create || !G.destroy || !G.chain2aln || !G.last_error) { fprintf(stderr, "libbwagpu: missing symbol\n"); exit(2); }
 }
 
@@ -446,6 +457,58 @@ static void seed_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T, double *t_dev)
   free(seq_off); free(seq); free(cnt); free(iv); free(ioff); free(soff); free(ks); free(sa);
 }
 
+/* SeqsToChains + ChainsToRegions in one device call (gpuchain mode): the
+   reads go in, each read's mem_alnreg_v comes back (malloc'd per read, the
+   ownership rule of ChainsToRegions); no chain is built on the host */
+typedef struct {
+  hw_t *w;
+  const int32_t *cnt;
+  const int64_t *off;
+  const bwagpu_alnreg_t *regs;
+} regs_t;
+static void w_regs(void *data, int i, int tid)
+{
+  regs_t *f = (regs_t *)data;
+  mem_alnreg_v *r = &f->w->regs[i];
+  r->n = r->m = f->cnt[i];
+  r->a = (mem_alnreg_t *)malloc(sizeof(mem_alnreg_t) * (f->cnt[i] ? f->cnt[i] : 1));
+  memcpy(r->a, f->regs + f->off[i], sizeof(mem_alnreg_t) * f->cnt[i]);
+}
+static void seqs2regions_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T, double *t_dev)
+{
+  const mem_opt_t *opt = w->opt;
+  kt_for(T, w_nt4, w, n);
+  static int64_t *seq_off, *off, k_n;
+  static int32_t *cnt;
+  static uint8_t *seq;
+  static int64_t k_nb;
+  if (n + 1 > k_n) {
+    free(seq_off); free(off); free(cnt);
+    k_n = 2 * (int64_t)(n + 1);
+    seq_off = (int64_t *)malloc(8 * k_n);
+    off = (int64_t *)malloc(8 * k_n);
+    cnt = (int32_t *)malloc(4 * k_n);
+  }
+  int64_t nb = 0;
+  seq_off[0] = 0;
+  for (int i = 0; i < n; ++i) seq_off[i + 1] = (nb += w->seqs[i].l_seq);
+  if (nb + 1 > k_nb) { free(seq); k_nb = 2 * (nb + 1); seq = (uint8_t *)malloc(k_nb); }
+  for (int i = 0; i < n; ++i) memcpy(seq + seq_off[i], w->seqs[i].seq, w->seqs[i].l_seq);
+  bwagpu_seedopt_t so = {opt->min_seed_len, opt->split_width, (int32_t)opt->max_mem_intv, opt->split_factor};
+  bwagpu_chainopt_t co = {opt->max_occ, opt->max_chain_gap, opt->min_chain_weight, opt->max_chain_extend,
+                          opt->mask_level, opt->drop_ratio};
+  const bwagpu_alnreg_t *regs = 0;
+  int64_t nreg = 0;
+  const double t0 = realtime();
+  const int rc = G.seqs2regions(ctx, &so, &co, n, seq_off, seq, cnt, &regs, &nreg);
+  if (rc) { fprintf(stderr, "bwagpu_seqs2regions: rc=%d %s\n", rc, G.last_error(ctx)); exit(3); }
+  *t_dev += realtime() - t0;
+  off[0] = 0;
+  for (int i = 0; i < n; ++i) off[i + 1] = off[i] + cnt[i];
+  regs_t f = {w, cnt, off, regs};
+  kt_for(T, w_regs, &f, n);
+}
+
 /* one bwagpu_chain2aln call for the whole batch: flatten, run, unflatten into
    malloc'd mem_alnreg_v (the ownership rule of ChainsToRegions, bwa_wrapper.cpp:824-830);
    the per-read copies run on the stage's threads (offsets from one serial pass) */
@@ -638,7 +701,8 @@ int main(int argc, char *argv[])
   const int64_t K = argc > 7 ? strtoll(argv[7], 0, 10) : 10000000;
   const int T = argc > 8 ? atoi(argv[8]) : 8;
   const int64_t GL = argc > 9 ? strtoll(argv[9], 0, 10) : 1000000;
-  const int is_seed = !strcmp(mode, "gpuseed");
+  const int is_chain = !strcmp(mode, "gpuchain");
+  const int is_seed = is_chain || !strcmp(mode, "gpuseed");
   const int is_sam = is_seed || !strcmp(mode, "gpusam"), is_gpu = is_sam || !strcmp(mode, "gpu"),
             is_ref = !strcmp(mode, "ref");
   if (!is_gpu && !is_ref && strcmp(mode, "split")) { fprintf(stderr, "unknown mode %s\n", mode); return 1; }
@@ -723,6 +787,13 @@ int main(int argc, char *argv[])
     bwagpu_bwt_t gb = {bt->primary, {bt->L2[0], bt->L2[1], bt->L2[2], bt->L2[3], bt->L2[4]}, bt->seq_len,
                        bt->bwt_size, bt->bwt, bt->sa_intv, 0, bt->n_sa, bt->sa};
     if (G.set_bwt(ctx, &gb)) { fprintf(stderr, "bwagpu_set_bwt: %s\n", G.last_error(ctx)); return 3; }
+    if (is_chain) {
+      uint8_t *alt = (uint8_t *)calloc(idx->bns->n_seqs, 1);
+      int any = 0;
+      for (int i = 0; i < idx->bns->n_seqs; ++i) any |= alt[i] = (uint8_t)!!idx->bns->anns[i].is_alt;
+      if (G.set_alt(ctx, any ? alt : 0)) { fprintf(stderr, "bwagpu_set_alt: %s\n", G.last_error(ctx)); return 3; }
+      free(alt);
+    }
   }
   bwagpu_samcache_t *cache = 0;
   /* first-launch capacities sized for short reads (2x150: a handful of CIGAR
@@ -762,11 +833,13 @@ int main(int argc, char *argv[])
       hw_t w = {opt, idx, seqs, (chain_v *)calloc(n, sizeof(chain_v)), (mem_alnreg_v *)calloc(n, sizeof(mem_alnreg_v)),
                 0, n_processed};
       t0 = realtime();
-      if (is_seed) seed_gpu(ctx, &w, n, T, &t_seed_dev);
+      if (is_chain) seqs2regions_gpu(ctx, &w, n, T, &t_seed_dev); /* seeding + chain2aln: seed_s */
+      else if (is_seed) seed_gpu(ctx, &w, n, T, &t_seed_dev);
       else kt_for(T, w_seed, &w, n);
       t_seed += realtime() - t0;
       t0 = realtime();
-      if (is_gpu) ext_gpu(ctx, &w, n, T);
+      if (is_chain) {
+      } else if (is_gpu) ext_gpu(ctx, &w, n, T);
       else kt_for(T, w_ext_cpu, &w, n);
       t_ext += realtime() - t0;
       t0 = realtime();

@@ -96,3 +96,17 @@ def test_gpu_seeding_and_sam_stage_identical_to_bwa_mem(tmp_path, name, seed, pa
     b = _run("gpuseed", str(tmp_path), name, seed, pairs, lm, k)
     assert a == b, _first_diff(a, b)
     assert _run.info["seed_device_s"] > 0 and _run.info["reg2aln_calls"] > 0
+
+
+@needs_harness
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,seed,pairs,lm,k", CASES)
+def test_gpu_seqs2regions_and_sam_stage_identical_to_bwa_mem(tmp_path, name, seed, pairs, lm, k):
+    """the whole of SeqsToChains + ChainsToRegions on the device in one call
+    (bwagpu_seqs2regions: interval search, SA lookups, the kbtree chaining,
+    mem_chain_flt, mem_flt_chained_seeds, mem_chain2aln — no host chaining),
+    rescue and CIGARs on the device: SAM byte-identical"""
+    a = _run("ref", str(tmp_path), name, seed, pairs, lm, k)
+    b = _run("gpuchain", str(tmp_path), name, seed, pairs, lm, k)
+    assert a == b, _first_diff(a, b)
+    assert _run.info["seed_device_s"] > 0 and _run.info["reg2aln_calls"] > 0
