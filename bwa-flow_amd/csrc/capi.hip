@@ -157,11 +157,13 @@ struct bwagpu_ctx {
   // per SA position, the kbtree arenas, mem_seed_sw tasks, the packed chains
   DevBuf ch_npos, ch_posoff, ch_frac, ch_nout, ch_noseed, ch_nsw, ch_need, ch_swtab, ch_alt;
   DevBuf ch_kpos, ch_rbeg, ch_qinfo, ch_label, ch_score, ch_slist, ch_ord, ch_chains, ch_nodes;
+  DevBuf ch_ochains, ch_oslist, ch_bins, ch_dbg;
   DevBuf ch_swoff, ch_swtasks, ch_swt, ch_swskip, ch_swres, ch_swscr;
   DevBuf ch_ocoff, ch_osoff, ch_rco, ch_cso, ch_rid, ch_cfrac, ch_out, ch_seeds;
   DevBuf ch_regoff, ch_regc;
   HostBuf chh_tot, chh_rco, chh_cso, chh_chains, chh_seeds, chh_regs, chh_n;
   Slot ch_slot;  // chain2aln scratch of bwagpu_seqs2regions
+  ChainStreams ch_cs{};  // created on first use
   bool has_alt = false;
   // the FPGA wire format (bwagpu_sw_stream)
   DevBuf st_buf, st_start, st_q, st_tasks, st_lists, st_seen, st_ctr, st_out;
@@ -343,6 +345,12 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   ctx->a2_tasks.release(); ctx->a2_q.release(); ctx->a2_t.release(); ctx->a2_out.release();
   ctx->a2_scratch.release(); ctx->a2_lists.release(); ctx->a2_counts.release(); ctx->a2_boff.release();
   ctx->ch_slot.release_scratch();
+  for (int k = 0; k < 2; ++k) {
+    if (ctx->ch_cs.side[k]) (void)hipStreamSynchronize(ctx->ch_cs.side[k]);
+    if (ctx->ch_cs.side[k]) (void)hipStreamDestroy(ctx->ch_cs.side[k]);
+    if (ctx->ch_cs.join[k]) (void)hipEventDestroy(ctx->ch_cs.join[k]);
+  }
+  if (ctx->ch_cs.fork) (void)hipEventDestroy(ctx->ch_cs.fork);
   ctx->ch_slot.d_out.release(); ctx->ch_slot.d_n.release(); ctx->ch_slot.d_stats.release();
   for (DevBuf* b : {&ctx->r2_tasks, &ctx->r2_q, &ctx->r2_out, &ctx->r2_cig, &ctx->r2_md, &ctx->r2_lists, &ctx->r2_z,
                     &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->sd_off,
@@ -351,7 +359,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
                     &ctx->st_seen, &ctx->st_ctr, &ctx->st_out, &ctx->ch_npos, &ctx->ch_posoff, &ctx->ch_frac,
                     &ctx->ch_nout, &ctx->ch_noseed, &ctx->ch_nsw, &ctx->ch_need, &ctx->ch_swtab, &ctx->ch_alt,
                     &ctx->ch_kpos, &ctx->ch_rbeg, &ctx->ch_qinfo, &ctx->ch_label, &ctx->ch_score, &ctx->ch_slist,
-                    &ctx->ch_ord, &ctx->ch_chains, &ctx->ch_nodes, &ctx->ch_swoff, &ctx->ch_swtasks, &ctx->ch_swt,
+                    &ctx->ch_ord, &ctx->ch_chains, &ctx->ch_nodes, &ctx->ch_ochains, &ctx->ch_oslist, &ctx->ch_bins, &ctx->ch_dbg, &ctx->ch_swoff, &ctx->ch_swtasks, &ctx->ch_swt,
                     &ctx->ch_swskip, &ctx->ch_swres, &ctx->ch_swscr, &ctx->ch_ocoff, &ctx->ch_osoff, &ctx->ch_rco,
                     &ctx->ch_cso, &ctx->ch_rid, &ctx->ch_cfrac, &ctx->ch_out, &ctx->ch_seeds, &ctx->ch_regoff,
                     &ctx->ch_regc})
@@ -1767,8 +1775,11 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
   HIPC(ctx->ch_score.ensure(sizeof(int32_t) * p1), "hipMalloc");
   HIPC(ctx->ch_slist.ensure(sizeof(int32_t) * p1), "hipMalloc");
   HIPC(ctx->ch_ord.ensure(sizeof(int32_t) * p1), "hipMalloc");
-  HIPC(ctx->ch_chains.ensure(sizeof(DChain) * p1), "hipMalloc");
-  HIPC(ctx->ch_nodes.ensure(sizeof(BNode) * (size_t)node_total(P, n_reads)), "hipMalloc");
+  HIPC(ctx->ch_chains.ensure(sizeof(LChain) * p1), "hipMalloc");
+  HIPC(ctx->ch_nodes.ensure(sizeof(BNode32) * (size_t)node_total(P, n_reads)), "hipMalloc");
+  HIPC(ctx->ch_ochains.ensure(sizeof(DChain) * p1), "hipMalloc");
+  HIPC(ctx->ch_oslist.ensure(sizeof(int32_t) * p1), "hipMalloc");
+  HIPC(ctx->ch_bins.ensure(sizeof(int32_t) * ((size_t)(kLdsBins + 1) * nr + kLdsBins + 1)), "hipMalloc");
   a.kpos = ctx->ch_kpos.as<uint64_t>();
   a.rbeg = ctx->ch_rbeg.as<uint64_t>();
   a.qinfo = ctx->ch_qinfo.as<int2>();
@@ -1776,11 +1787,47 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
   a.score = ctx->ch_score.as<int32_t>();
   a.slist = ctx->ch_slist.as<int32_t>();
   a.ord = ctx->ch_ord.as<int32_t>();
-  a.chains = ctx->ch_chains.as<DChain>();
-  a.nodes = ctx->ch_nodes.as<BNode>();
+  a.lchains = ctx->ch_chains.as<LChain>();
+  a.lnodes = ctx->ch_nodes.as<BNode32>();
+  a.ochains = ctx->ch_ochains.as<DChain>();
+  a.oslist = ctx->ch_oslist.as<int32_t>();
+  a.bin_count = ctx->ch_bins.as<int32_t>();
+  a.bin_list = a.bin_count + kLdsBins + 1;
   HIPC(launch_chain_emit(a, st), "chain_emit launch");
   if (P) HIPC(launch_bwt_sa(ctx->bwt, P, a.kpos, a.rbeg, st), "bwt_sa launch");
-  HIPC(launch_chain_build(a, st), "chain_build launch");
+  if (!ctx->ch_cs.fork) {
+    for (int k = 0; k < 2; ++k) {
+      HIPC(hipStreamCreateWithFlags(&ctx->ch_cs.side[k], hipStreamNonBlocking), "hipStreamCreate");
+      HIPC(hipEventCreateWithFlags(&ctx->ch_cs.join[k], hipEventDisableTiming), "hipEventCreate");
+    }
+    HIPC(hipEventCreateWithFlags(&ctx->ch_cs.fork, hipEventDisableTiming), "hipEventCreate");
+  }
+  const char* dbg_env = getenv("BWAGPU_CHAIN_PHASES");
+  const bool dbg_on = dbg_env && dbg_env[0] == '1';
+  if (dbg_on) {
+    HIPC(ctx->ch_dbg.ensure(sizeof(uint64_t) * 8 * nr), "hipMalloc");
+    HIPC(hipMemsetAsync(ctx->ch_dbg.p, 0, sizeof(uint64_t) * 8 * nr, st), "memset");
+    a.dbg = ctx->ch_dbg.as<uint64_t>();
+  }
+  HIPC(launch_chain_build(a, st, ctx->ch_cs), "chain_build launch");
+  if (dbg_on) {  // the slowest reads' phase times (100 MHz ticks) to stderr
+    std::vector<uint64_t> d(8 * nr);
+    HIPC(hipMemcpyAsync(d.data(), ctx->ch_dbg.p, sizeof(uint64_t) * 8 * nr, hipMemcpyDeviceToHost, st), "D2H");
+    HIPC(hipStreamSynchronize(st), "sync");
+    std::vector<int> idx;
+    for (int r = 0; r < n_reads; ++r)
+      if (d[8 * (size_t)r + 6]) idx.push_back(r);
+    std::sort(idx.begin(), idx.end(), [&](int x, int y) {
+      return d[8 * (size_t)x + 6] - d[8 * (size_t)x] > d[8 * (size_t)y + 6] - d[8 * (size_t)y];
+    });
+    for (size_t k = 0; k < idx.size() && k < 8; ++k) {
+      const uint64_t* q = &d[8 * (size_t)idx[k]];
+      fprintf(stderr, "[chain phases] read %d pos %u chains %u: loop %.1f trav %.1f prep %.1f sort %.1f flt %.1f out %.1f us\n",
+              idx[k], (unsigned)(q[7] & 0xffffffff), (unsigned)(q[7] >> 32), (q[1] - q[0]) / 100.0,
+              (q[2] - q[1]) / 100.0, (q[3] ? q[3] - q[2] : 0) / 100.0, (q[4] ? q[4] - q[3] : 0) / 100.0,
+              (q[5] - (q[4] ? q[4] : q[2])) / 100.0, (q[6] - q[5]) / 100.0);
+    }
+  }
   if (!raw && any_sw) {  // mem_flt_chained_seeds: every kept seed of a long read realigned
     HIPC(ctx->ch_swoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
     HIPC(launch_scan_i32(a.n_sw, ctx->ch_swoff.as<int64_t>(), n_reads, st), "scan launch");

@@ -23,30 +23,56 @@ namespace bwagpu {
 constexpr int kBT = 5;
 constexpr int kBN = 2 * kBT - 1;  // keys per node
 
-struct BNode {  // one kbtree node: keys are read-local chain ids, pos their chain's key
-  int32_t n, internal;
-  int32_t key[kBN];
-  int32_t child[kBN + 1];
-  int32_t pad_;
-  int64_t pos[kBN];
+// one kbtree node; keys are read-local chain ids (the chain's pos is its first
+// seed's rbeg, read through the id).  16-bit ids in LDS, 32-bit in global memory.
+template <class K>
+struct BNodeT {
+  K n, internal;
+  K key[kBN];
+  K child[kBN + 1];
 };
-static_assert(sizeof(BNode) == 160, "node layout");
+typedef BNodeT<int16_t> BNode16;
+typedef BNodeT<int32_t> BNode32;
+static_assert(sizeof(BNode16) == 42 && sizeof(BNode32) == 84, "node layout");
 
-struct DChain {  // mem_chain_t's state while chaining (seeds live in the seed lists)
-  int64_t pos, s0_rbeg, last_rbeg;
-  int32_t s0_qbeg, last_qbeg, last_len, rid;
-  int32_t n, is_alt, w, kept, first;
-  int32_t soff;  // its seeds' offset in the read's seed list
-  int32_t cur;
-  int32_t pad_;
+// a chain while its read is chained: mem_chain_t's first and last seed,
+// mem_chain_weight's running sums (the weight is built as seeds are appended,
+// bwamem.c:223-244), and mem_chain_flt's fields
+struct LChain {
+  int64_t s0_rbeg, last_rbeg, endr;
+  int32_t rid, n;
+  int32_t first, soff, cur;
+  int16_t s0_qbeg, last_qbeg, last_len, endq;
+  int16_t wq, wr, w;  // wr saturates at 32767 (w = min(wq, wr), wq <= the read's length)
+  int8_t is_alt, kept;
 };
-static_assert(sizeof(DChain) == 72, "chain layout");
+static_assert(sizeof(LChain) == 64, "chain layout");
+
+struct DChain {  // a chain out of mem_chain_flt (its seeds at oslist[soff..soff+n))
+  int64_t pos;
+  int32_t rid, n, w, kept, first, is_alt, soff, pad_;
+};
+static_assert(sizeof(DChain) == 40, "out chain layout");
 
 // the read's node arena: nodes <= keys / (t - 1) + 1 <= n_pos / 4 + 1
 __host__ __device__ inline int64_t node_base(int64_t pos_off_r, int32_t r) { return (pos_off_r >> 2) + 2 * (int64_t)r; }
 __host__ __device__ inline int64_t node_total(int64_t p_total, int32_t n_reads) {
   return (p_total >> 2) + 2 * (int64_t)n_reads + 2;
 }
+
+// reads are binned by their SA position count: a read of bin b (b < kLdsBins)
+// is chained by one wave with its kbtree, chains and lists in LDS sized for
+// kBinCap[b] positions; larger reads use the same code on global memory
+constexpr int kLdsBins = 4;
+constexpr int kBinCap[kLdsBins] = {32, 128, 512, 1536};
+// chains | nodes | the seeds' rbeg (int64) | qbeg/len (int2) | label, slist, ord (int32)
+__host__ __device__ constexpr size_t lds_nodes_bytes(int cap) {
+  return ((size_t)(cap / 4 + 2) * sizeof(BNode16) + 7) & ~(size_t)7;
+}
+__host__ __device__ constexpr size_t lds_arena(int cap) {
+  return (size_t)cap * sizeof(LChain) + lds_nodes_bytes(cap) + (8 + 8 + 3 * 4) * (size_t)cap;
+}
+static_assert(lds_arena(1536) <= 160 * 1024, "the largest bin fits one CU's LDS");
 
 struct ChainArgs {
   int32_t n_reads;
@@ -75,16 +101,22 @@ struct ChainArgs {
   int32_t* n_oseed;     // seeds over the chains out
   int32_t* n_sw;        // mem_seed_sw tasks
   int32_t* need;        // [0]: the largest interval count of an overflowed read
+  int32_t* bin_list;    // [kLdsBins + 1][n_reads]
+  int32_t* bin_count;   // [kLdsBins + 1]
   // per position, in the read's interval order
   uint64_t* kpos;   // BWT row
   uint64_t* rbeg;   // bwt_sa of it
   int2* qinfo;      // qbeg, len
-  int32_t* label;   // chain id (-1: dropped), then scratch of mem_chain_flt
   int32_t* score;   // seed score (len, or mem_seed_sw's)
-  int32_t* slist;   // positions grouped by chain (kbtree order)
-  int32_t* ord;     // chain ids: kbtree order, then mem_chain_flt's output order
-  DChain* chains;
-  BNode* nodes;
+  DChain* ochains;  // the read's chains out, in order
+  int32_t* oslist;  // their seeds (positions), chain after chain
+  // the global-memory arena of reads past the largest bin
+  LChain* lchains;
+  BNode32* lnodes;
+  int32_t* label;
+  int32_t* slist;
+  int32_t* ord;
+  uint64_t* dbg;  // diagnostics (BWAGPU_CHAIN_PHASES=1): per read, s_memrealtime at 8 phase ends
 };
 
 struct ChainPack {  // the chains out, in bwagpu_batch_t's layout
@@ -111,7 +143,11 @@ constexpr int kSwWin = 200;  // MEM_SHORT_LEN: no window reaches it
 hipError_t launch_scan_i32(const int32_t* in, int64_t* out, int32_t n, hipStream_t st);
 hipError_t launch_chain_count(const ChainArgs& a, hipStream_t st);
 hipError_t launch_chain_emit(const ChainArgs& a, hipStream_t st);
-hipError_t launch_chain_build(const ChainArgs& a, hipStream_t st);
+struct ChainStreams {  // the bins' side streams (fork / join with events)
+  hipStream_t side[2];
+  hipEvent_t fork, join[2];
+};
+hipError_t launch_chain_build(const ChainArgs& a, hipStream_t st, const ChainStreams& cs);  // bins, one launch each
 hipError_t launch_chain_sw_prep(const ChainArgs& a, const ChainSw& s, hipStream_t st);
 hipError_t launch_chain_sw_apply(const ChainArgs& a, const ChainSw& s, hipStream_t st);
 hipError_t launch_chain_pack(const ChainArgs& a, const ChainPack& p, hipStream_t st);

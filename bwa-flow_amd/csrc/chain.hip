@@ -6,13 +6,19 @@
 //
 // The work of one read is a strictly sequential walk — every seed either
 // joins the chain kb_intervalp finds for it or opens a new one, and the
-// chain's last seed decides the next merge — so a read runs on one lane,
-// with its kbtree in global memory (a few KB per read, L1/L2 resident while
-// the lane works on it).  The kbtree is restated as a B-tree of chain ids with
+// chain's last seed decides the next merge — so a read runs on one wave that
+// executes the walk wave-uniformly, with its kbtree, chain records and lists
+// in LDS: each step of the walk is a chain of dependent accesses (~25 per
+// seed), which LDS answers in ~100 cycles where L2 takes several hundred.
+// Reads are binned by their SA position count (LDS arenas for 32 / 128 / 512 /
+// 1664 positions, up to 157 KB); the rare larger reads run the same code on a
+// global-memory arena.  The kbtree is restated as a B-tree of chain ids with
 // the reference's node search, split and in-order traversal (t = 5): chains
 // with EQUAL positions exist (tandem repeats), and their order — and which of
-// them kb_intervalp returns — follows the tree's shape.  Positions are
-// expanded by a wave per read and resolved by bwt_sa (seed.hip) in between.
+// them kb_intervalp returns — follows the tree's shape.  mem_chain_weight is
+// accumulated as seeds are appended (its two sweeps run in append order), so
+// mem_chain_flt needs no second pass over the seeds.  Positions are expanded
+// by a wave per read and resolved by bwt_sa (seed.hip) in between.
 #include <hip/hip_runtime.h>
 
 #include "chain.h"
@@ -70,96 +76,122 @@ __global__ void __launch_bounds__(256) chain_emit_kernel(ChainArgs a) {
   }
 }
 
-// ---- the kbtree (kbtree.h:54-197, 336-358) over one read's node arena
+// ---- the kbtree (kbtree.h:54-197, 336-358) of one read.  CH / ND are the
+// chain and node pointer types: LDS (address space 3) or global.  The tree is
+// walked by the whole wave: a node's keys are read one per lane and its
+// search is a ballot (keys are sorted, so the count of keys below pos is the
+// lower bound the reference's binary search finds); insertion shifts and
+// splits move one key per lane.
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l), hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+  return (int64_t)((uint64_t)(uint32_t)hi << 32 | (uint32_t)lo);
+}
+__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+template <class CH, class ND>
 struct Tree {
-  BNode* nd;
+  CH* ch;
+  ND* nd;
   int root, n_nodes, n_keys;
 
   // first key >= pos (r = 0 if equal, else -1 after stepping back to the last
-  // key < pos); past the end the last key with r = 1 (kbtree.h:100-113)
-  __device__ int find(int x, int64_t pos, int& r) const {
+  // key < pos); past the end the last key with r = 1 (kbtree.h:100-113);
+  // *key = the key at the returned index
+  __device__ int find(int x, int64_t pos, int& r, int& key) const {
+    const int lane = (int)(threadIdx.x & 63);
     const int n = nd[x].n;
     if (n == 0) {
       r = -1;
       return -1;
     }
-    int b = 0, e = n;
-    while (b < e) {
-      const int m = (b + e) >> 1;
-      if (nd[x].pos[m] < pos) b = m + 1;
-      else e = m;
+    int k = 0;
+    int64_t kp = 0;
+    if (lane < n) {
+      k = nd[x].key[lane];
+      kp = ch[k].s0_rbeg;
     }
+    const int b = __builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < n && kp < pos));
+    int i;
     if (b == n) {
       r = 1;
-      return n - 1;
+      i = n - 1;
+    } else {
+      r = pcmp(pos, readlane64(kp, b));
+      i = r < 0 ? b - 1 : b;
     }
-    r = pcmp(pos, nd[x].pos[b]);
-    return r < 0 ? b - 1 : b;
+    key = i >= 0 ? __builtin_amdgcn_readlane(k, i) : -1;
+    return i;
   }
 
   __device__ int lower(int64_t pos) const {  // kb_intervalp's lower (kbtree.h:130-147)
-    int lo = -1, r = 0;
+    int lo = -1, r = 0, key;
     for (int x = root;;) {
-      const int i = find(x, pos, r);
-      if (i >= 0 && r == 0) return nd[x].key[i];
-      if (i >= 0) lo = nd[x].key[i];
+      const int i = find(x, pos, r, key);
+      if (i >= 0 && r == 0) return key;
+      if (i >= 0) lo = key;
       if (!nd[x].internal) return lo;
       x = nd[x].child[i + 1];
     }
   }
 
   __device__ void split(int x, int i, int y) {  // __kb_split (kbtree.h:152-167)
+    const int lane = (int)(threadIdx.x & 63);
     const int z = n_nodes++;
-    BNode& Z = nd[z];
-    BNode& Y = nd[y];
-    BNode& X = nd[x];
-    Z.internal = Y.internal;
-    Z.n = kBT - 1;
-    for (int k = 0; k < kBT - 1; ++k) {
-      Z.key[k] = Y.key[kBT + k];
-      Z.pos[k] = Y.pos[kBT + k];
-    }
-    if (Y.internal)
-      for (int k = 0; k < kBT; ++k) Z.child[k] = Y.child[kBT + k];
-    Y.n = kBT - 1;
-    for (int k = X.n; k > i; --k) X.child[k + 1] = X.child[k];
-    X.child[i + 1] = z;
-    for (int k = X.n; k > i; --k) {
-      X.key[k] = X.key[k - 1];
-      X.pos[k] = X.pos[k - 1];
-    }
-    X.key[i] = Y.key[kBT - 1];
-    X.pos[i] = Y.pos[kBT - 1];
-    ++X.n;
+    const int yi = nd[y].internal, xn = nd[x].n;
+    const int med = nd[y].key[kBT - 1];
+    if (lane < kBT - 1) nd[z].key[lane] = nd[y].key[kBT + lane];
+    if (yi && lane < kBT) nd[z].child[lane] = nd[y].child[kBT + lane];
+    // x's children i+1..xn move up one, keys i..xn-1 likewise (read, then write)
+    int cv = 0, kv = 0;
+    const bool mc = lane > i && lane <= xn, mk = lane >= i && lane < xn;
+    if (mc) cv = nd[x].child[lane];
+    if (mk) kv = nd[x].key[lane];
+    wave_sync();
+    if (mc) nd[x].child[lane + 1] = cv;
+    if (mk) nd[x].key[lane + 1] = kv;
+    wave_sync();
+    nd[z].internal = yi;
+    nd[z].n = kBT - 1;
+    nd[y].n = kBT - 1;
+    nd[x].child[i + 1] = z;
+    nd[x].key[i] = med;
+    nd[x].n = xn + 1;
+    wave_sync();
   }
 
   __device__ void put(int k, int64_t pos) {  // kb_putp (kbtree.h:168-197)
-    int r;
+    const int lane = (int)(threadIdx.x & 63);
+    int r, key;
     ++n_keys;
     if (nd[root].n == kBN) {
       const int s = n_nodes++;
       nd[s].internal = 1;
       nd[s].n = 0;
       nd[s].child[0] = root;
+      wave_sync();
       split(s, 0, root);
       root = s;
     }
     for (int x = root;;) {
       if (!nd[x].internal) {
-        const int i = find(x, pos, r);
-        for (int j = nd[x].n - 1; j > i; --j) {
-          nd[x].key[j + 1] = nd[x].key[j];
-          nd[x].pos[j + 1] = nd[x].pos[j];
-        }
+        const int i = find(x, pos, r, key);
+        const int xn = nd[x].n;
+        int kv = 0;
+        const bool mv = lane > i && lane < xn;  // keys i+1..xn-1 move up one
+        if (mv) kv = nd[x].key[lane];
+        wave_sync();
+        if (mv) nd[x].key[lane + 1] = kv;
+        wave_sync();
         nd[x].key[i + 1] = k;
-        nd[x].pos[i + 1] = pos;
-        ++nd[x].n;
+        nd[x].n = xn + 1;
+        wave_sync();
         return;
       }
-      int i = find(x, pos, r) + 1;
-      if (nd[nd[x].child[i]].n == kBN) {
-        split(x, i, nd[x].child[i]);
-        if (pos > nd[x].pos[i]) ++i;
+      int i = find(x, pos, r, key) + 1;
+      const int c = nd[x].child[i];
+      if (nd[c].n == kBN) {
+        split(x, i, c);
+        if (pos > ch[nd[x].key[i]].s0_rbeg) ++i;
       }
       x = nd[x].child[i];
     }
@@ -191,21 +223,24 @@ __device__ int intv2rid(const ChainArgs& a, int64_t rb, int64_t re) {  // bntseq
   return b == e ? b : -1;
 }
 
-// klib introsort (ksort.h:146-226) of chain ids by weight, greater first
-// (mem_flt's flt_lt, bwamem.c:333-334), step for step: it is not stable
+// klib introsort (ksort.h:146-226) by weight, greater first (mem_flt's
+// flt_lt, bwamem.c:333-334), step for step: it is not stable.  The values are
+// packed keys w << 32 | chain id (one LDS access per comparison); only w is
+// compared.
 struct ByW {
-  const DChain* c;
-  __device__ bool operator()(int x, int y) const { return c[x].w > c[y].w; }
+  __device__ bool operator()(int64_t x, int64_t y) const { return (x >> 32) > (y >> 32); }
 };
-__device__ void c_insert(int* s, int* t, ByW lt) {
-  for (int* i = s + 1; i < t; ++i)
-    for (int* j = i; j > s && lt(*j, *(j - 1)); --j) {
-      const int x = *j;
-      *j = *(j - 1);
-      *(j - 1) = x;
+template <class I, class LT>
+__device__ void c_insert(I* a, int s, int t, LT lt) {  // [s, t)
+  for (int i = s + 1; i < t; ++i)
+    for (int j = i; j > s && lt(a[j], a[j - 1]); --j) {
+      const int64_t x = a[j];
+      a[j] = a[j - 1];
+      a[j - 1] = x;
     }
 }
-__device__ void c_comb(int n, int* a, ByW lt) {
+template <class I, class LT>
+__device__ void c_comb(I* a, int s, int n, LT lt) {  // a[s, s+n)
   const double shrink = 1.2473309501039786540366528676643;
   int gap = n;
   bool swapped;
@@ -215,21 +250,22 @@ __device__ void c_comb(int n, int* a, ByW lt) {
       if (gap == 9 || gap == 10) gap = 11;
     }
     swapped = false;
-    for (int i = 0; i < n - gap; ++i)
+    for (int i = s; i < s + n - gap; ++i)
       if (lt(a[i + gap], a[i])) {
-        const int x = a[i];
+        const int64_t x = a[i];
         a[i] = a[i + gap];
         a[i + gap] = x;
         swapped = true;
       }
   } while (swapped || gap > 2);
-  if (gap != 1) c_insert(a, a + n, lt);
+  if (gap != 1) c_insert(a, s, s + n, lt);
 }
-__device__ void c_introsort(int n, int* a, ByW lt) {
+template <class I, class LT>
+__device__ void c_introsort(int n, I* a, LT lt) {
   if (n < 1) return;
   if (n == 2) {
     if (lt(a[1], a[0])) {
-      const int x = a[0];
+      const int64_t x = a[0];
       a[0] = a[1];
       a[1] = x;
     }
@@ -245,7 +281,7 @@ __device__ void c_introsort(int n, int* a, ByW lt) {
   for (;;) {
     if (s < t) {
       if (--d == 0) {
-        c_comb(t - s + 1, a + s, lt);
+        c_comb(a, s, t - s + 1, lt);
         t = s;
         continue;
       }
@@ -255,7 +291,7 @@ __device__ void c_introsort(int n, int* a, ByW lt) {
       } else {
         k = lt(a[j], a[i]) ? i : j;
       }
-      const int rp = a[k];
+      const int64_t rp = a[k];
       if (k != t) {
         a[k] = a[t];
         a[t] = rp;
@@ -264,12 +300,12 @@ __device__ void c_introsort(int n, int* a, ByW lt) {
         do ++i; while (lt(a[i], rp));
         do --j; while (i <= j && lt(rp, a[j]));
         if (j <= i) break;
-        const int x = a[i];
+        const int64_t x = a[i];
         a[i] = a[j];
         a[j] = x;
       }
       {
-        const int x = a[i];
+        const int64_t x = a[i];
         a[i] = a[t];
         a[t] = x;
       }
@@ -282,7 +318,7 @@ __device__ void c_introsort(int n, int* a, ByW lt) {
       }
     } else {
       if (top == 0) {
-        c_insert(a, a + n, lt);
+        c_insert(a, 0, n, lt);
         return;
       }
       --top;
@@ -293,50 +329,99 @@ __device__ void c_introsort(int n, int* a, ByW lt) {
   }
 }
 
-// ---- one lane per read: mem_chain's loop, the traversal, mem_chain_flt
-__global__ void __launch_bounds__(256) chain_build_kernel(ChainArgs a) {
-  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (r >= a.n_reads) return;
+// ---- one read on one wave: mem_chain's loop, the kbtree traversal,
+// mem_chain_flt, the chains out.  Every lane runs the same sequential code
+// on the same data (wave-uniform: LDS reads broadcast, every lane stores the
+// same value), except the final copy-out, which is lane-parallel.  CH / ND /
+// IX: pointer types of the chains, nodes and index lists (LDS or global).
+template <bool STAGED, class CH, class ND, class IX, class RB, class QI, class S64>
+__device__ void chain_read(const ChainArgs& a, int r, CH* ch, ND* nd, IX* label, IX* slist, IX* ord, RB* rbeg,
+                           QI* qi, S64* sc) {
+  const int lane = (int)(threadIdx.x & 63);
   const int np = a.n_pos[r];
-  a.n_out[r] = 0;
-  a.n_oseed[r] = 0;
-  a.n_sw[r] = 0;
-  if (np == 0) return;
   const int64_t base = a.pos_off[r];
-  DChain* ch = a.chains + base;
-  int32_t* label = a.label + base;
-  int32_t* slist = a.slist + base;
-  int32_t* ord = a.ord + base;
-  const uint64_t* rbeg = a.rbeg + base;
-  const int2* qi = a.qinfo + base;
-  Tree t{a.nodes + node_base(base, r), 0, 1, 0};
-  t.nd[0].n = 0;
-  t.nd[0].internal = 0;
+  uint64_t* dbg = a.dbg ? a.dbg + 8 * (int64_t)r : nullptr;
+  auto stamp = [&](int k) {
+    if (dbg && lane == 0) dbg[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  if constexpr (STAGED) {  // an LDS arena: the seeds staged in, coalesced
+    for (int p = lane; p < np; p += 64) {
+      rbeg[p] = a.rbeg[base + p];
+      qi[p] = reinterpret_cast<const int64_t*>(a.qinfo)[base + p];
+    }
+    wave_sync();
+  }
+  Tree<CH, ND> t{ch, nd, 0, 1, 0};
+  nd[0].n = 0;
+  nd[0].internal = 0;
   int n_ch = 0;
+  // bns_pos2rid's answer for the last contig looked up (its [offset, next
+  // offset) span): a read's seeds mostly fall in one contig
+  int64_t c_lo = 1, c_hi = 0;
+  int c_rid = -1;
+  auto rid_of = [&](int64_t pos_f) -> int {
+    if (pos_f >= a.l_pac) return -1;
+    if (pos_f >= c_lo && pos_f < c_hi) return c_rid;
+    const int m = pos2rid(a, pos_f);
+    c_lo = a.ann_off[m];
+    c_hi = m == a.n_seqs - 1 ? a.l_pac : a.ann_off[m + 1];
+    c_rid = m;
+    return m;
+  };
+  int64_t nsr = (int64_t)rbeg[0];
+  int64_t nq = qi[0];  // qbeg | len << 32 (from LDS when staged; else one seed ahead from global memory)
   for (int p = 0; p < np; ++p) {  // bwamem.c:286-311
-    const int64_t sr = (int64_t)rbeg[p];
-    const int qb = qi[p].x, sl = qi[p].y;
-    const int rid = intv2rid(a, sr, sr + sl);
+    const int64_t sr = nsr;
+    const int qb = (int)(uint32_t)nq, sl = (int)(nq >> 32);
+    if (p + 1 < np) {  // the next seed's loads overlap this one's work
+      nsr = (int64_t)rbeg[p + 1];
+      nq = qi[p + 1];
+    }
+    // bns_intv2rid (bntseq.c:365-373)
+    int rid;
+    if (sr < a.l_pac && sr + sl > a.l_pac) {
+      rid = -2;
+    } else {
+      const int rb_ = rid_of(depos(a.l_pac, sr));
+      const int re_ = sl > 0 ? rid_of(depos(a.l_pac, sr + sl - 1)) : rb_;
+      rid = rb_ == re_ ? rb_ : -1;
+    }
     int lab = -1;
     if (rid >= 0) {
       bool add = true;
       if (t.n_keys) {
         const int lo = t.lower(sr);
         if (lo >= 0) {
-          DChain& c = ch[lo];
           // test_and_merge (bwamem.c:199-221)
-          const int64_t qend = c.last_qbeg + c.last_len, rend = c.last_rbeg + c.last_len;
-          if (rid == c.rid) {
-            if (qb >= c.s0_qbeg && qb + sl <= qend && sr >= c.s0_rbeg && sr + sl <= rend) {
+          const int64_t c_last_rbeg = ch[lo].last_rbeg, c_s0_rbeg = ch[lo].s0_rbeg;
+          const int c_last_qbeg = ch[lo].last_qbeg, c_last_len = ch[lo].last_len, c_s0_qbeg = ch[lo].s0_qbeg;
+          const int64_t qend = c_last_qbeg + c_last_len, rend = c_last_rbeg + c_last_len;
+          if (rid == ch[lo].rid) {
+            if (qb >= c_s0_qbeg && qb + sl <= qend && sr >= c_s0_rbeg && sr + sl <= rend) {
               add = false;  // contained: dropped
-            } else if (!((c.last_rbeg < a.l_pac || c.s0_rbeg < a.l_pac) && sr >= a.l_pac)) {
-              const int64_t x = qb - c.last_qbeg, y = sr - c.last_rbeg;
-              if (y >= 0 && x - y <= a.w && y - x <= a.w && x - c.last_len < a.max_chain_gap &&
-                  y - c.last_len < a.max_chain_gap) {
-                c.last_qbeg = qb;
-                c.last_rbeg = sr;
-                c.last_len = sl;
-                ++c.n;
+            } else if (!((c_last_rbeg < a.l_pac || c_s0_rbeg < a.l_pac) && sr >= a.l_pac)) {
+              const int64_t x = qb - c_last_qbeg, y = sr - c_last_rbeg;
+              if (y >= 0 && x - y <= a.w && y - x <= a.w && x - c_last_len < a.max_chain_gap &&
+                  y - c_last_len < a.max_chain_gap) {
+                ch[lo].last_qbeg = (int16_t)qb;
+                ch[lo].last_rbeg = sr;
+                ch[lo].last_len = (int16_t)sl;
+                ch[lo].n = ch[lo].n + 1;
+                {  // mem_chain_weight's two sweeps, one seed further (bwamem.c:227-240)
+                  const int eq = ch[lo].endq;
+                  int wq = ch[lo].wq;
+                  if (qb >= eq) wq += sl;
+                  else if (qb + sl > eq) wq += qb + sl - eq;
+                  ch[lo].wq = (int16_t)wq;
+                  ch[lo].endq = (int16_t)(eq > qb + sl ? eq : qb + sl);
+                  const int64_t er = ch[lo].endr;
+                  int wr = ch[lo].wr;
+                  if (sr >= er) wr += sl;
+                  else if (sr + sl > er) wr += (int)(sr + sl - er);
+                  ch[lo].wr = (int16_t)(wr < 32767 ? wr : 32767);  // only min(wq, wr) is read
+                  ch[lo].endr = er > sr + sl ? er : sr + sl;
+                }
                 lab = lo;
                 add = false;
               }
@@ -345,43 +430,47 @@ __global__ void __launch_bounds__(256) chain_build_kernel(ChainArgs a) {
         }
       }
       if (add) {
-        DChain& c = ch[n_ch];
-        c.pos = c.s0_rbeg = c.last_rbeg = sr;
-        c.s0_qbeg = c.last_qbeg = qb;
-        c.last_len = sl;
-        c.rid = rid;
-        c.n = 1;
-        c.is_alt = a.is_alt ? (a.is_alt[rid] != 0) : 0;
-        c.w = 0;
-        c.kept = 0;
-        c.first = -1;
+        CH* c = ch + n_ch;
+        c->s0_rbeg = c->last_rbeg = sr;
+        c->endr = sr + sl;
+        c->s0_qbeg = c->last_qbeg = (int16_t)qb;
+        c->last_len = (int16_t)sl;
+        c->endq = (int16_t)(qb + sl);
+        c->wq = c->wr = (int16_t)sl;
+        c->rid = rid;
+        c->n = 1;
+        c->is_alt = (int8_t)(a.is_alt ? (a.is_alt[rid] != 0) : 0);
+        c->kept = 0;
+        c->first = -1;
+        c->w = 0;
         lab = n_ch;
         t.put(n_ch++, sr);
       }
     }
     label[p] = lab;
   }
+  stamp(1);
   // in-order traversal (__kb_traverse, kbtree.h:336-358): the chain order
   int no = 0;
   {
-    int sn[32], si[32], top = -1;
+    int sn[24], si[24], top = -1;
     for (int x = t.root;;) {  // the leftmost path
       sn[++top] = x;
       si[top] = 0;
-      if (!t.nd[x].internal) break;
-      x = t.nd[x].child[0];
+      if (!nd[x].internal) break;
+      x = nd[x].child[0];
     }
     while (top >= 0) {
       const int x = sn[top], i = si[top];
-      if (i < t.nd[x].n) {
-        ord[no++] = t.nd[x].key[i];
+      if (i < nd[x].n) {
+        ord[no++] = nd[x].key[i];
         si[top] = i + 1;
-        if (t.nd[x].internal)
-          for (int y = t.nd[x].child[i + 1];;) {
+        if (nd[x].internal)
+          for (int y = nd[x].child[i + 1];;) {
             sn[++top] = y;
             si[top] = 0;
-            if (!t.nd[y].internal) break;
-            y = t.nd[y].child[0];
+            if (!nd[y].internal) break;
+            y = nd[y].child[0];
           }
       } else {
         --top;
@@ -391,82 +480,105 @@ __global__ void __launch_bounds__(256) chain_build_kernel(ChainArgs a) {
   {  // seed lists in kbtree order, each in merge (= processing) order
     int s = 0;
     for (int k = 0; k < no; ++k) {
-      DChain& c = ch[ord[k]];
-      c.soff = s;
-      c.cur = 0;
-      s += c.n;
+      const int id = ord[k];
+      ch[id].soff = s;
+      ch[id].cur = 0;
+      s += ch[id].n;
     }
     for (int p = 0; p < np; ++p) {
       const int l = label[p];
-      if (l >= 0) slist[ch[l].soff + ch[l].cur++] = p;
+      if (l >= 0) {
+        const int c = ch[l].cur;
+        slist[ch[l].soff + c] = p;
+        ch[l].cur = c + 1;
+      }
     }
   }
+  stamp(2);
   int nout = no;
   if (!a.raw) {  // mem_chain_flt (bwamem.c:336-396)
     int nf = 0;
     for (int k = 0; k < no; ++k) {
-      DChain& c = ch[ord[k]];
-      // mem_chain_weight (bwamem.c:223-244)
-      int64_t end = 0;
-      int wq = 0, wr = 0;
-      for (int j = 0; j < c.n; ++j) {
-        const int2 s = qi[slist[c.soff + j]];
-        if (s.x >= end) wq += s.y;
-        else if (s.x + s.y > end) wq += (int)(s.x + s.y - end);
-        end = end > s.x + s.y ? end : s.x + s.y;
-      }
-      end = 0;
-      for (int j = 0; j < c.n; ++j) {
-        const int p = slist[c.soff + j];
-        const int64_t rb = (int64_t)rbeg[p];
-        const int ln = qi[p].y;
-        if (rb >= end) wr += ln;
-        else if (rb + ln > end) wr += (int)(rb + ln - end);
-        end = end > rb + ln ? end : rb + ln;
-      }
-      int w = wr < wq ? wr : wq;
+      const int id = ord[k];
+      int w = ch[id].wr < ch[id].wq ? ch[id].wr : ch[id].wq;  // mem_chain_weight
       w = w < (1 << 30) ? w : (1 << 30) - 1;
-      c.w = w & ((1 << 29) - 1);  // the 29-bit field of mem_chain_t
-      c.first = -1;
-      c.kept = 0;
-      if (c.w >= a.min_chain_weight) ord[nf++] = ord[k];
+      w &= (1 << 29) - 1;  // the 29-bit field of mem_chain_t
+      ch[id].w = (int16_t)w;
+      ch[id].first = -1;
+      ch[id].kept = 0;
+      if (w >= a.min_chain_weight) ord[nf++] = id;
     }
-    c_introsort(nf, ord, ByW{ch});
+    // sc: 64-bit scratch (the staged seeds or the BWT rows, no longer read)
+    for (int k = lane; k < nf; k += 64) sc[k] = (int64_t)ch[ord[k]].w << 32 | (uint32_t)ord[k];
+    wave_sync();
+    stamp(3);
+    c_introsort(nf, sc, ByW{});
+    wave_sync();
+    stamp(4);
+    for (int k = lane; k < nf; k += 64) ord[k] = (int32_t)(uint32_t)sc[k];
+    wave_sync();
     nout = 0;
     if (nf > 0) {
-      int32_t* kl = label;  // the kept list (label is no longer needed)
+      // the kept list, one packed entry per kept chain: sorted index (the
+      // list's own element) | chain beg | end | w | is_alt, in sc
+      auto kept_entry = [&](int i) -> int64_t {
+        const int c = ord[i];
+        return (int64_t)i | (int64_t)(uint16_t)ch[c].s0_qbeg << 20 |
+               (int64_t)(uint16_t)(ch[c].last_qbeg + ch[c].last_len) << 34 | (int64_t)(uint16_t)ch[c].w << 48 |
+               (int64_t)(ch[c].is_alt != 0) << 63;
+      };
       int nk = 0;
       ch[ord[0]].kept = 3;
-      kl[nk++] = 0;
+      sc[nk++] = kept_entry(0);
+      // the pairwise loop (bwamem.c:355-375): chain i against the kept list,
+      // 64 entries at a time — each lane tests one; the scan stops at the
+      // first entry whose break condition holds (ballot), and every entry up
+      // to it applies its large_ovlp / first updates (distinct chains)
       for (int i = 1; i < nf; ++i) {
-        DChain& ci = ch[ord[i]];
-        const int bi = ci.s0_qbeg, ei = ci.last_qbeg + ci.last_len;
-        bool large = false;
-        int k;
-        for (k = 0; k < nk; ++k) {
-          const int j = kl[k];
-          DChain& cj = ch[ord[j]];
-          const int bj = cj.s0_qbeg, ej = cj.last_qbeg + cj.last_len;
-          const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
-          if (e_min > b_max && (!cj.is_alt || ci.is_alt)) {
-            const int li = ei - bi, lj = ej - bj;
-            const int min_l = li < lj ? li : lj;
-            if (e_min - b_max >= min_l * a.mask_level && min_l < a.max_chain_gap) {
-              large = true;
-              if (cj.first < 0) cj.first = i;
-              if (ci.w < cj.w * a.drop_ratio && cj.w - ci.w >= a.min_seed_len << 1) break;
+        const int ci = ord[i];
+        const int bi = ch[ci].s0_qbeg, ei = ch[ci].last_qbeg + ch[ci].last_len;
+        const int wi = ch[ci].w, ai = ch[ci].is_alt;
+        bool large = false, brk = false;
+        for (int k0 = 0; k0 < nk && !brk; k0 += 64) {
+          const int k = k0 + lane;
+          bool sig = false, drop = false;
+          int j = 0;
+          if (k < nk) {
+            const int64_t e = sc[k];
+            j = (int)(e & 0xfffff);
+            const int bj = (int)((e >> 20) & 0x3fff), ej = (int)((e >> 34) & 0x3fff), wj = (int)((e >> 48) & 0x7fff);
+            const bool aj = e < 0;
+            const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
+            if (e_min > b_max && (!aj || ai)) {
+              const int li = ei - bi, lj = ej - bj;
+              const int min_l = li < lj ? li : lj;
+              if (e_min - b_max >= min_l * a.mask_level && min_l < a.max_chain_gap) {
+                sig = true;
+                drop = wi < wj * a.drop_ratio && wj - wi >= a.min_seed_len << 1;
+              }
             }
           }
+          const uint64_t dm = __builtin_amdgcn_ballot_w64(drop);
+          const int lim = dm ? __builtin_ctzll(dm) : 64;  // lanes <= lim take part
+          brk = dm != 0;
+          const bool act = sig && lane <= lim;
+          if (__builtin_amdgcn_ballot_w64(act)) large = true;
+          if (act) {
+            const int cj = ord[j];
+            if (ch[cj].first < 0) ch[cj].first = i;
+          }
+          wave_sync();
         }
-        if (k == nk) {
-          kl[nk++] = i;
-          ci.kept = large ? 2 : 3;
+        if (!brk) {
+          sc[nk++] = kept_entry(i);
+          ch[ci].kept = (int8_t)(large ? 2 : 3);
         }
       }
-      for (int i = 0; i < nk; ++i) {
-        const DChain& c = ch[ord[kl[i]]];
-        if (c.first >= 0) ch[ord[c.first]].kept = 1;
+      for (int i = lane; i < nk; i += 64) {
+        const int f = ch[ord[(int)(sc[i] & 0xfffff)]].first;
+        if (f >= 0) ch[ord[f]].kept = 1;
       }
+      __threadfence_block();
       int i, k;
       for (i = k = 0; i < nf; ++i) {
         const int kp = ch[ord[i]].kept;
@@ -479,13 +591,109 @@ __global__ void __launch_bounds__(256) chain_build_kernel(ChainArgs a) {
         if (ch[ord[i]].kept != 0) ord[nout++] = ord[i];
     }
   }
+  stamp(5);
+  // the chains out and their seeds, lane-parallel
+  DChain* oc = a.ochains + base;
+  int32_t* os = a.oslist + base;
   int ns = 0;
-  for (int k = 0; k < nout; ++k) ns += ch[ord[k]].n;
-  a.n_out[r] = nout;
-  a.n_oseed[r] = ns;
-  if (!a.raw && nout) {
-    const int len = (int)(a.seq_off[r + 1] - a.seq_off[r]);
-    if (a.sw_tab[len] >= 0) a.n_sw[r] = ns;  // mem_flt_chained_seeds runs (bwamem.c:609-611)
+  for (int k = 0; k < nout; ++k) {
+    const int id = ord[k];
+    const int n = ch[id].n, s0 = ch[id].soff;
+    if (lane == 0) {
+      DChain d;
+      d.pos = ch[id].s0_rbeg;
+      d.rid = ch[id].rid;
+      d.n = n;
+      d.w = a.raw ? 0 : ch[id].w;
+      d.kept = a.raw ? 0 : ch[id].kept;
+      d.first = a.raw ? -1 : ch[id].first;
+      d.is_alt = ch[id].is_alt;
+      d.soff = ns;
+      d.pad_ = 0;
+      oc[k] = d;
+    }
+    for (int j = lane; j < n; j += 64) os[ns + j] = slist[s0 + j];
+    ns += n;
+  }
+  if (lane == 0) {
+    a.n_out[r] = nout;
+    a.n_oseed[r] = ns;
+    int nsw = 0;
+    if (!a.raw && nout) {
+      const int len = (int)(a.seq_off[r + 1] - a.seq_off[r]);
+      if (a.sw_tab[len] >= 0) nsw = ns;  // mem_flt_chained_seeds runs (bwamem.c:609-611)
+    }
+    a.n_sw[r] = nsw;
+  }
+  if (dbg && lane == 0) {
+    dbg[6] = __builtin_amdgcn_s_memrealtime();
+    dbg[7] = (uint64_t)np | (uint64_t)no << 32;
+  }
+}
+
+// reads into bins by their position count (the last bin: global memory);
+// one atomic per wave and bin
+__global__ void __launch_bounds__(256) chain_bin_kernel(ChainArgs a) {
+  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int lane = (int)(threadIdx.x & 63);
+  int b = -1;
+  if (r < a.n_reads) {
+    const int np = a.n_pos[r];
+    if (np == 0) {
+      a.n_out[r] = 0;
+      a.n_oseed[r] = 0;
+      a.n_sw[r] = 0;
+    } else {
+      b = 0;
+      while (b < kLdsBins && np > kBinCap[b]) ++b;
+    }
+  }
+  const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
+  for (int k = 0; k <= kLdsBins; ++k) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(b == k);
+    if (!m) continue;
+    const int leader = __builtin_ctzll(m);
+    int at = 0;
+    if (lane == leader) at = atomicAdd(a.bin_count + k, __builtin_popcountll(m));
+    at = __shfl(at, leader, 64);
+    if (b == k) a.bin_list[(int64_t)k * a.n_reads + at + __builtin_popcountll(m & below)] = r;
+  }
+}
+
+typedef __attribute__((address_space(3))) LChain LdsChain;
+typedef __attribute__((address_space(3))) BNode16 LdsNode;
+typedef __attribute__((address_space(3))) int32_t LdsI32;
+typedef __attribute__((address_space(3))) int64_t LdsI64;
+
+
+// one wave per read of bin B, its arena in LDS
+template <int B>
+__global__ void __launch_bounds__(64) chain_build_lds_kernel(ChainArgs a) {
+  extern __shared__ __align__(16) char smem[];
+  constexpr int cap = kBinCap[B];
+  LdsChain* ch = (LdsChain*)(smem);
+  LdsNode* nd = (LdsNode*)(smem + (size_t)cap * sizeof(LChain));
+  char* tail = smem + (size_t)cap * sizeof(LChain) + lds_nodes_bytes(cap);
+  LdsI64* rb = (LdsI64*)tail;
+  LdsI64* qi = (LdsI64*)(tail + 8 * (size_t)cap);
+  LdsI32* label = (LdsI32*)(tail + 16 * (size_t)cap);
+  LdsI32* slist = label + cap;
+  LdsI32* ord = slist + cap;
+  const int n = a.bin_count[B];
+  const int32_t* list = a.bin_list + (int64_t)B * a.n_reads;
+  for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) chain_read<true>(a, list[i], ch, nd, label, slist, ord, rb, qi, rb);
+}
+
+// one wave per read past the largest bin, its arena in global memory
+__global__ void __launch_bounds__(64) chain_build_glb_kernel(ChainArgs a) {
+  const int n = a.bin_count[kLdsBins];
+  const int32_t* list = a.bin_list + (int64_t)kLdsBins * a.n_reads;
+  for (int i = (int)blockIdx.x; i < n; i += (int)gridDim.x) {
+    const int r = list[i];
+    const int64_t base = a.pos_off[r];
+    chain_read<false>(a, r, a.lchains + base, a.lnodes + node_base(base, r), a.label + base, a.slist + base, a.ord + base,
+               a.rbeg + base, reinterpret_cast<const int64_t*>(a.qinfo) + base,
+               reinterpret_cast<int64_t*>(a.kpos) + base);
   }
 }
 
@@ -498,9 +706,9 @@ __global__ void __launch_bounds__(256) chain_sw_prep_kernel(ChainArgs a, ChainSw
   const int64_t l_pac = a.l_pac;
   int64_t t = s.sw_off[r];
   for (int k = 0; k < a.n_out[r]; ++k) {
-    const DChain& c = a.chains[base + a.ord[base + k]];
+    const DChain& c = a.ochains[base + k];
     for (int j = 0; j < c.n; ++j, ++t) {
-      const int p = a.slist[base + c.soff + j];
+      const int p = a.oslist[base + c.soff + j];
       const int2 qi = a.qinfo[base + p];
       const int64_t sr = (int64_t)a.rbeg[base + p];
       bwagpu_align2_task_t task;
@@ -568,16 +776,18 @@ __global__ void __launch_bounds__(256) chain_sw_apply_kernel(ChainArgs a, ChainS
   int64_t t = s.sw_off[r];
   int ns = 0;
   for (int k = 0; k < a.n_out[r]; ++k) {
-    DChain& c = a.chains[base + a.ord[base + k]];
+    DChain& c = a.ochains[base + k];
+    const int s0 = c.soff;
     int kk = 0;
     for (int j = 0; j < c.n; ++j, ++t) {
-      const int p = a.slist[base + c.soff + j];
+      const int p = a.oslist[base + s0 + j];
       const int sc = s.skip[t] ? -1 : s.res[t].score;
       if (sc < 0 || sc >= min_hsp) {
         a.score[base + p] = sc < 0 ? a.qinfo[base + p].y * a.a : sc;
-        a.slist[base + c.soff + kk++] = p;
+        a.oslist[base + ns + kk++] = p;  // compacted in place (ns + kk <= s0 + j)
       }
     }
+    c.soff = ns;
     c.n = kk;
     ns += kk;
   }
@@ -597,14 +807,14 @@ __global__ void __launch_bounds__(256) chain_pack_kernel(ChainArgs a, ChainPack 
   }
   const float fr = a.frac_rep[r];
   for (int k = 0; k < a.n_out[r]; ++k, ++co) {
-    const DChain& c = a.chains[base + a.ord[base + k]];
+    const DChain c = a.ochains[base + k];
     bwagpu_chain_t o;
     o.pos = c.pos;
     o.rid = c.rid;
     o.n = c.n;
-    o.w = a.raw ? 0 : c.w;
-    o.kept = a.raw ? 0 : c.kept;
-    o.first = a.raw ? -1 : c.first;
+    o.w = c.w;
+    o.kept = c.kept;
+    o.first = c.first;
     o.is_alt = c.is_alt;
     o.frac_rep = fr;
     o.pad_ = 0;
@@ -613,7 +823,7 @@ __global__ void __launch_bounds__(256) chain_pack_kernel(ChainArgs a, ChainPack 
     p.chain_frac[co] = fr;
     p.chain_seed_off[co] = (int32_t)so;
     for (int j = 0; j < c.n; ++j, ++so) {
-      const int q = a.slist[base + c.soff + j];
+      const int q = a.oslist[base + c.soff + j];
       bwagpu_seed_t sd;
       sd.rbeg = (int64_t)a.rbeg[base + q];
       sd.qbeg = a.qinfo[base + q].x;
@@ -685,10 +895,33 @@ hipError_t launch_chain_emit(const ChainArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_chain_build(const ChainArgs& a, hipStream_t st) {
+hipError_t launch_chain_build(const ChainArgs& a, hipStream_t st, const ChainStreams& cs) {
   if (a.n_reads <= 0) return hipSuccess;
-  hipLaunchKernelGGL(chain_build_kernel, lanes(a.n_reads), dim3(256), 0, st, a);
-  return hipGetLastError();
+  hipError_t e = hipMemsetAsync(a.bin_count, 0, sizeof(int32_t) * (kLdsBins + 1), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(chain_bin_kernel, lanes(a.n_reads), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // the bins run side by side (the heavy reads' bins are long, serial walks):
+  // bin 3 on st, bin 2 and the global bin on side[0], bins 0-1 on side[1];
+  // bin counts stay on the device: each launch's workgroups stride over its
+  // bin's list (a resident-size grid for the small bins, fewer for the big)
+  if ((e = hipEventRecord(cs.fork, st)) != hipSuccess) return e;
+  for (int k = 0; k < 2; ++k)
+    if ((e = hipStreamWaitEvent(cs.side[k], cs.fork, 0)) != hipSuccess) return e;
+  const int grid[kLdsBins + 1] = {8192, 2048, 512, 256, 256};
+  const hipStream_t on[kLdsBins] = {cs.side[1], cs.side[1], cs.side[0], st};
+#define BUILD_BIN(B)                                                                                         \
+  hipLaunchKernelGGL(chain_build_lds_kernel<B>, dim3(grid[B]), dim3(64), lds_arena(kBinCap[B]), on[B], a); \
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  BUILD_BIN(3) BUILD_BIN(2) BUILD_BIN(0) BUILD_BIN(1)
+#undef BUILD_BIN
+  hipLaunchKernelGGL(chain_build_glb_kernel, dim3(grid[kLdsBins]), dim3(64), 0, cs.side[0], a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  for (int k = 0; k < 2; ++k) {
+    if ((e = hipEventRecord(cs.join[k], cs.side[k])) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, cs.join[k], 0)) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_chain_sw_prep(const ChainArgs& a, const ChainSw& s, hipStream_t st) {

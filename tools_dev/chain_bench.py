@@ -1,0 +1,50 @@
+"""Chaining benchmark: bwagpu_seqs2chains / bwagpu_seqs2regions over the C2
+batch's reads against the chr21-sized genome's bwa index (bench_data/e2e);
+parity against the reference's ChainsRecord / regions.  One JSON line."""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "bwa-flow_amd", "python"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402,F401
+from bwagpu import workload  # noqa: E402
+from bwagpu.engine import Batch, Engine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--fused", action="store_true")
+    a = ap.parse_args()
+    opt, gref, rbs = workload.load_fixture()
+    rb = rbs[0]
+    b = rb.batch
+    eng = Engine(0, opt, gref.l_pac, gref.ann_offset, gref.ann_len, pac=gref.pac)
+    hdr, words, sa, sa_intv = workload.load_bwa_index(os.path.join(ROOT, "bench_data", "e2e", "ref.fa"))
+    eng.set_bwt(hdr, words, sa, sa_intv)
+    out = eng.seqs2chains(b.seq_off, b.seq)
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        out = eng.seqs2chains(b.seq_off, b.seq)
+    ms = (time.perf_counter() - t0) * 1e3 / a.reps
+    rco, ch, cso, sd = out
+    got = Batch(b.seq_off, b.seq, rco, cso, ch["rid"].copy(), ch["frac_rep"].copy(), sd)
+    res = {"seqs2chains_ms": round(ms, 3), "chains_ok": workload.batch_digest(got) == workload.batch_digest(b)}
+    if a.fused:
+        n, regs = eng.seqs2regions(b.seq_off, b.seq)
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            n, regs = eng.seqs2regions(b.seq_off, b.seq)
+        res["seqs2regions_ms"] = round((time.perf_counter() - t0) * 1e3 / a.reps, 3)
+        res["regions_ok"] = bool(rb.check_compact(regs, n))
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
