@@ -25,15 +25,11 @@ struct Ivl {
 };
 static_assert(sizeof(Ivl) == sizeof(bwagpu_intv_t), "interval layout");
 
-// bwt_occ4 (bwt.c:169-187): occurrences of A/C/G/T in bwt[0..k], $ removed
-__device__ __forceinline__ void occ4(const DevBwt& b, uint64_t k, uint64_t cnt[4]) {
-  if (k == ~0ull) {
-    cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
-    return;
-  }
-  k -= (k >= b.primary);
-  const uint4* p = reinterpret_cast<const uint4*>(b.bwt + (k >> 7 << 4));
-  const uint4 c01 = p[0], c23 = p[1], w0 = p[2], w1 = p[3];
+// the counts of one 128-position block up to position k (bwt_occ4's body,
+// bwt.c:169-187, for k already past the $ adjustment): three
+// equality-popcounts per word of 2-bit bases, A from the position count
+__device__ __forceinline__ void block_counts(uint64_t k, const uint4 c01, const uint4 c23, const uint4 w0, const uint4 w1,
+                                             uint64_t cnt[4]) {
   const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
   const int nfull = (int)((k & 127) >> 4);
   const uint32_t tail = ~((1u << ((~(uint32_t)k & 15) << 1)) - 1);  // fields 0..(k & 15) of word nfull
@@ -53,12 +49,46 @@ __device__ __forceinline__ void occ4(const DevBwt& b, uint64_t k, uint64_t cnt[4
   cnt[3] = ((uint64_t)c23.w << 32 | c23.z) + c3;
 }
 
+// bwt_occ4 (bwt.c:169-187): occurrences of A/C/G/T in bwt[0..k], $ removed
+__device__ __forceinline__ void occ4(const DevBwt& b, uint64_t k, uint64_t cnt[4]) {
+  if (k == ~0ull) {
+    cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
+    return;
+  }
+  k -= (k >= b.primary);
+  const uint4* p = reinterpret_cast<const uint4*>(b.bwt + (k >> 7 << 4));
+  block_counts(k, p[0], p[1], p[2], p[3], cnt);
+}
+
+// bwt_2occ4 (bwt.c:189-214): both ends of an interval; when they fall in the
+// same 128-position block it is fetched once (the second fetch is issued only
+// by the lanes whose ends lie in different blocks)
+__device__ __forceinline__ void occ4x2(const DevBwt& b, uint64_t k, uint64_t l, uint64_t tk[4], uint64_t tl[4]) {
+  if (k == ~0ull || l == ~0ull) {
+    occ4(b, k, tk);
+    occ4(b, l, tl);
+    return;
+  }
+  const uint64_t kk = k - (k >= b.primary), ll = l - (l >= b.primary);
+  const uint4* pk = reinterpret_cast<const uint4*>(b.bwt + (kk >> 7 << 4));
+  uint4 a0 = pk[0], a1 = pk[1], a2 = pk[2], a3 = pk[3];
+  uint4 d0 = a0, d1 = a1, d2 = a2, d3 = a3;
+  if ((kk >> 7) != (ll >> 7)) {
+    const uint4* pl = reinterpret_cast<const uint4*>(b.bwt + (ll >> 7 << 4));
+    d0 = pl[0];
+    d1 = pl[1];
+    d2 = pl[2];
+    d3 = pl[3];
+  }
+  block_counts(kk, a0, a1, a2, a3, tk);
+  block_counts(ll, d0, d1, d2, d3, tl);
+}
+
 // bwt_extend (bwt.c:262-276)
 __device__ __forceinline__ void extend(const DevBwt& b, const Ivl& ik, Ivl ok[4], int is_back) {
   uint64_t tk[4], tl[4];
   const int nb = !is_back;
-  occ4(b, ik.x[nb] - 1, tk);
-  occ4(b, ik.x[nb] - 1 + ik.x[2], tl);
+  occ4x2(b, ik.x[nb] - 1, ik.x[nb] - 1 + ik.x[2], tk, tl);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     ok[i].x[nb] = b.L2[i] + 1 + tk[i];
@@ -77,8 +107,7 @@ __device__ __forceinline__ void extend(const DevBwt& b, const Ivl& ik, Ivl ok[4]
 __device__ __forceinline__ Ivl extend1(const DevBwt& b, const Ivl& ik, int c, int is_back) {
   uint64_t tk[4], tl[4];
   const int nb = !is_back;
-  occ4(b, ik.x[nb] - 1, tk);
-  occ4(b, ik.x[nb] - 1 + ik.x[2], tl);
+  occ4x2(b, ik.x[nb] - 1, ik.x[nb] - 1 + ik.x[2], tk, tl);
   const uint64_t s0 = tl[0] - tk[0], s1 = tl[1] - tk[1], s2 = tl[2] - tk[2], s3 = tl[3] - tk[3];
   const uint64_t tkc = c == 0 ? tk[0] : c == 1 ? tk[1] : c == 2 ? tk[2] : tk[3];
   const uint64_t l2c = c == 0 ? b.L2[0] : c == 1 ? b.L2[1] : c == 2 ? b.L2[2] : b.L2[3];
@@ -168,8 +197,11 @@ __device__ int smem1(const DevBwt& b, int len, const uint8_t* q, int x, int min_
   for (i = x - 1; i >= -1; --i) {  // backward
     const int c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
     curr.n = 0;
+    Ivl pn{};
+    if (prev.n > 0) pn = prev.a[0];
     for (int j = 0; j < prev.n; ++j) {
-      const Ivl p = prev.a[j];
+      const Ivl p = pn;
+      if (j + 1 < prev.n) pn = prev.a[j + 1];  // the next candidate's load overlaps this extension
       Ivl okc{};
       if (c >= 0) {
         if (bg.spend()) return -1;

@@ -10,10 +10,10 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ "$SKIPT" != "1" ]; then
-timeout -k 10 500 python -u -m pytest tests/ -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "pytest failed rc=$?" >> $OUT/gpu_tests.log; tail -30 $OUT/gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "pytest failed rc=$?" >> $OUT/gpu_tests.log; tail -30 $OUT/gpu_tests.log; exit 1; }
 tail -1 $OUT/gpu_tests.log
 fi
-timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 2; }
+timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 2; }
 cat $OUT/bench.json
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-cigar --no-host-path --no-e2e --no-regime > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 3; }
