@@ -173,6 +173,10 @@ struct bwagpu_ctx {
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
+  // BWAGPU_SUBMIT_PROF=1: host time of submit's parts, printed at destroy
+  double sp_check = 0, sp_alloc = 0, sp_copy = 0, sp_h2d = 0, sp_enq = 0, sp_d2h = 0;
+  int64_t sp_n = 0;
+  int sp_on = -1;
   // bwagpu_prof_*: event pairs around the dominant extension launches
   std::vector<hipEvent_t> prof_ev;
   int prof_used = 0;
@@ -316,6 +320,10 @@ int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, 
 
 void destroy_ctx(bwagpu_ctx_t* ctx) {
   if (!ctx) return;
+  if (ctx->sp_on > 0 && ctx->sp_n)
+    fprintf(stderr, "[submit prof] %ld submits, ms each: check %.3f copy %.3f h2d %.3f enqueue %.3f d2h %.3f\n",
+            (long)ctx->sp_n, 1e3 * ctx->sp_check / ctx->sp_n, 1e3 * ctx->sp_copy / ctx->sp_n,
+            1e3 * ctx->sp_h2d / ctx->sp_n, 1e3 * ctx->sp_enq / ctx->sp_n, 1e3 * ctx->sp_d2h / ctx->sp_n);
   (void)hipSetDevice(ctx->device);
   for (auto& s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -393,37 +401,87 @@ int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
   if (b->n_chains && (!b->chain_rid || !b->chain_frac_rep)) return fail(ctx, BWAGPU_E_INVAL, "NULL chain array");
   if (b->n_seeds && !b->seeds) return fail(ctx, BWAGPU_E_INVAL, "NULL seeds");
   if (b->seq_bytes && !b->seq) return fail(ctx, BWAGPU_E_INVAL, "NULL seq");
-  // seeds must lie inside their read and inside [0, 2*l_pac); offsets monotone
+  // seeds must lie inside their read and inside [0, 2*l_pac); offsets
+  // monotone.  Large batches are split over a few threads by read range.
   const int64_t two = ctx->ref.l_pac << 1;
   const int64_t* so = b->seq_off;
   const int32_t* rco = b->read_chain_off;
   const int32_t* cso = b->chain_seed_off;
   const bwagpu_seed_t* sd = b->seeds;
-  int64_t lmax = 0;
-  bool bad_seed = false;
-  for (int r = 0; r < b->n_reads; ++r) {
-    const int64_t l = so[r + 1] - so[r];
-    if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
-    if (l > BWAGPU_MAX_READ_LEN) {
-      char m[128];
-      snprintf(m, sizeof m, "read %d has length %lld > %d", r, (long long)l, BWAGPU_MAX_READ_LEN);
-      return fail(ctx, BWAGPU_E_UNSUPPORTED, m);
-    }
-    lmax = std::max(lmax, l);
-    const int c0 = rco[r], c1 = rco[r + 1];
-    if (c1 < c0) return fail(ctx, BWAGPU_E_INVAL, "read_chain_off not monotone");
-    for (int c = c0; c < c1; ++c) {
-      const int k0 = cso[c], k1 = cso[c + 1];
-      if (k1 < k0) return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off not monotone");
-      for (int k = k0; k < k1; ++k) {  // branch-free accumulation: one test per read
-        const bwagpu_seed_t& s = sd[k];
-        bad_seed |= (s.qbeg < 0) | (s.len <= 0) | ((int64_t)s.qbeg + s.len > l) | (s.rbeg < 0) | (s.rbeg + s.len > two);
+  // 0 ok, 1 seq_off not monotone, 2 read too long (*bad_read), 3 rco, 4 cso, 5 seed
+  auto check_range = [&](int r0, int r1, int64_t* lmax, int* bad_read) -> int {
+    int64_t lm = 0;
+    for (int r = r0; r < r1; ++r) {
+      const int64_t l = so[r + 1] - so[r];
+      if (l < 0) return 1;
+      if (l > BWAGPU_MAX_READ_LEN) {
+        *bad_read = r;
+        return 2;
       }
+      lm = std::max(lm, l);
+      const int c0 = rco[r], c1 = rco[r + 1];
+      if (c1 < c0) return 3;
+      bool bad_seed = false;
+      for (int c = c0; c < c1; ++c) {
+        const int k0 = cso[c], k1 = cso[c + 1];
+        if (k1 < k0) return 4;
+        for (int k = k0; k < k1; ++k) {  // branch-free accumulation: one test per read
+          const bwagpu_seed_t& s = sd[k];
+          bad_seed |= (s.qbeg < 0) | (s.len <= 0) | ((int64_t)s.qbeg + s.len > l) | (s.rbeg < 0) | (s.rbeg + s.len > two);
+        }
+      }
+      if (bad_seed) return 5;
     }
-    if (bad_seed) return fail(ctx, BWAGPU_E_INVAL, "seed outside its read or the reference");
+    *lmax = lm;
+    return 0;
+  };
+  const int nt = b->n_seeds >= (1 << 16) ? 4 : 1;
+  int code[4] = {0, 0, 0, 0}, bad_read[4] = {0, 0, 0, 0};
+  int64_t lmaxs[4] = {0, 0, 0, 0};
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t)
+      th.emplace_back([&, t] {
+        code[t] = check_range((int)((int64_t)b->n_reads * t / nt), (int)((int64_t)b->n_reads * (t + 1) / nt), &lmaxs[t],
+                              &bad_read[t]);
+      });
+    code[0] = check_range(0, (int)((int64_t)b->n_reads / nt), &lmaxs[0], &bad_read[0]);
+    for (auto& x : th) x.join();
   }
-  *lq_max_out = (int)lmax;
+  for (int t = 0; t < nt; ++t) {  // the first failing range reports, as one sequential pass would
+    switch (code[t]) {
+      case 1: return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
+      case 2: {
+        char m[128];
+        snprintf(m, sizeof m, "read %d has length %lld > %d", bad_read[t],
+                 (long long)(so[bad_read[t] + 1] - so[bad_read[t]]), BWAGPU_MAX_READ_LEN);
+        return fail(ctx, BWAGPU_E_UNSUPPORTED, m);
+      }
+      case 3: return fail(ctx, BWAGPU_E_INVAL, "read_chain_off not monotone");
+      case 4: return fail(ctx, BWAGPU_E_INVAL, "chain_seed_off not monotone");
+      case 5: return fail(ctx, BWAGPU_E_INVAL, "seed outside its read or the reference");
+      default: break;
+    }
+  }
+  *lq_max_out = (int)std::max(std::max(lmaxs[0], lmaxs[1]), std::max(lmaxs[2], lmaxs[3]));
   return BWAGPU_OK;
+}
+
+// BWAGPU_H2D=kernel: the staged batch pulled into HBM by the device itself
+// (the pinned buffer is mapped) — one launch in place of the runtime's copy
+// call.  Measured and not the default: the copy call's host cost goes away,
+// but the runtime then blocks in the D2H copy call that follows (submit
+// 3.7 vs 9.1 Mreads/s end to end)
+__global__ void __launch_bounds__(256) pull_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+bool h2d_by_kernel() {
+  static const int v = [] {
+    const char* e = getenv("BWAGPU_H2D");
+    return (e && strcmp(e, "kernel") == 0) ? 1 : 0;
+  }();
+  return v != 0;
 }
 
 // LDS row-buffer bytes per group for reads up to lq_max (see rows_needed)
@@ -665,6 +723,19 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
+  if (ctx->sp_on < 0) {
+    const char* e = getenv("BWAGPU_SUBMIT_PROF");
+    ctx->sp_on = e && e[0] == '1';
+  }
+  using clk = std::chrono::steady_clock;
+  auto t_prev = clk::now();
+  auto lap = [&](double& acc) {
+    if (!ctx->sp_on) return;
+    const auto t = clk::now();
+    acc += std::chrono::duration<double>(t - t_prev).count();
+    t_prev = t;
+  };
+  ctx->sp_n += ctx->sp_on;
   int lq_max = 0;
   int rc = check_batch(ctx, b, &lq_max);
   if (rc) return rc;
@@ -683,6 +754,7 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipHostMalloc(out)");
   HIPC(s.h_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipHostMalloc(out_n)");
   HIPC(s.h_stats.ensure(sizeof(int64_t) * ST_N), "hipHostMalloc(stats)");
+  lap(ctx->sp_check);
   // stage into pinned memory so the caller's buffers are free on return —
   // unless the caller packed into that memory already (bwagpu_chain2aln_stage)
   char* h = s.h_in.as<char>();
@@ -706,8 +778,18 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   }
 
   hipStream_t st = s.stream;
+  lap(ctx->sp_copy);
   HIPC(hipEventRecord(s.ev0, st), "event");
-  HIPC(hipMemcpyAsync(s.d_in.p, s.h_in.p, L.total, hipMemcpyHostToDevice, st), "H2D batch");
+  void* h_dev = nullptr;
+  if (h2d_by_kernel() && hipHostGetDevicePointer(&h_dev, s.h_in.p, 0) == hipSuccess && h_dev) {
+    const size_t n16 = L.total / 16;  // L.total is a multiple of 256
+    hipLaunchKernelGGL(pull_kernel, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 2048)), dim3(256), 0, st,
+                       (const uint4*)h_dev, (uint4*)s.d_in.p, n16);
+    HIPC(hipGetLastError(), "pull launch");
+  } else {
+    HIPC(hipMemcpyAsync(s.d_in.p, s.h_in.p, L.total, hipMemcpyHostToDevice, st), "H2D batch");
+  }
+  lap(ctx->sp_h2d);
   HIPC(hipMemsetAsync(s.d_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset stats");
   char* d = s.d_in.as<char>();
   DevBatch db;
@@ -730,6 +812,7 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
     (void)hipStreamSynchronize(st);
     return rc;
   }
+  lap(ctx->sp_enq);
   HIPC(hipEventRecord(s.ev2, st), "event");
   if (b->n_seeds)
     HIPC(hipMemcpyAsync(s.h_out.p, s.d_out.p, sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds, hipMemcpyDeviceToHost, st),
@@ -739,6 +822,7 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
          "D2H counts");
   HIPC(hipMemcpyAsync(s.h_stats.p, s.d_stats.p, sizeof(int64_t) * ST_N, hipMemcpyDeviceToHost, st), "D2H stats");
   HIPC(hipEventRecord(s.ev3, st), "event");
+  lap(ctx->sp_d2h);
   s.h2d = (int64_t)L.total;
   s.d2h = (int64_t)(sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds + sizeof(int32_t) * (size_t)b->n_reads);
   s.busy = true;
