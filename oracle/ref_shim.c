@@ -213,3 +213,141 @@ int ref_reg2aln_batch(const bwagpu_opt_t *o, const bwagpu_bns_t *gb, const uint8
   free(bns.anns);
   return 0;
 }
+
+/* ---- seeding on the host with the reference's own code (cpu baselines of
+   bench.py's seeding_stage / chaining_stage legs) ----
+   mode 0: the interval search alone — mem_collect_intv's control flow
+   (bwamem.c:120-167, static in the reference build, so restated here as in
+   oracle/gen_seed.c) around the reference's bwt_smem1 / bwt_seed_strategy1 /
+   ks_introsort_mem_intv; mode 1: bwa-flow's SeqsToChains
+   (src/bwa_wrapper.cpp:105-115): the reference's mem_chain -> mem_chain_flt ->
+   mem_flt_chained_seeds.  Reads are handed out in chunks of 64 to n_threads
+   pthreads; the index is loaded once per prefix (bwa_idx_load). */
+#include <sys/time.h>
+#include "bwa.h"
+#include "bwt.h"
+
+typedef struct { size_t n, m; ref_chain_t *a; } ref_chain_v;
+ref_chain_v mem_chain(const mem_opt_t *opt, const bwt_t *bwt, const bntseq_t *bns, int len, const uint8_t *seq,
+                      void *buf);
+int mem_chain_flt(const mem_opt_t *opt, int n_chn, ref_chain_t *a);
+void mem_flt_chained_seeds(const mem_opt_t *opt, const bntseq_t *bns, const uint8_t *pac, int l_query,
+                           const uint8_t *query, int n_chn, ref_chain_t *a);
+void ks_introsort_mem_intv(size_t n, bwtintv_t a[]); /* bwamem.c:90-91 */
+
+static char g_prefix[4096];
+static bwaidx_t *g_idx;
+
+static int collect_count(const mem_opt_t *opt, const bwt_t *bwt, int len, const uint8_t *seq, bwtintv_v *mem,
+                         bwtintv_v *mem1, bwtintv_v *tmpv[2])
+{
+  int i, k, x = 0, old_n;
+  const int split_len = (int)(opt->min_seed_len * opt->split_factor + .499);
+  mem->n = 0;
+  while (x < len) {
+    if (seq[x] < 4) {
+      x = bwt_smem1(bwt, len, seq, x, 1, mem1, tmpv);
+      for (i = 0; i < (int)mem1->n; ++i) {
+        bwtintv_t *p = &mem1->a[i];
+        if ((int)((uint32_t)p->info - (p->info >> 32)) >= opt->min_seed_len) kv_push(bwtintv_t, *mem, *p);
+      }
+    } else ++x;
+  }
+  old_n = (int)mem->n;
+  for (k = 0; k < old_n; ++k) {
+    bwtintv_t *p = &mem->a[k];
+    int start = p->info >> 32, end = (int32_t)p->info;
+    if (end - start < split_len || p->x[2] > (uint64_t)opt->split_width) continue;
+    bwt_smem1(bwt, len, seq, (start + end) >> 1, p->x[2] + 1, mem1, tmpv);
+    for (i = 0; i < (int)mem1->n; ++i)
+      if ((uint32_t)mem1->a[i].info - (mem1->a[i].info >> 32) >= (uint32_t)opt->min_seed_len)
+        kv_push(bwtintv_t, *mem, mem1->a[i]);
+  }
+  if (opt->max_mem_intv > 0) {
+    x = 0;
+    while (x < len) {
+      if (seq[x] < 4) {
+        bwtintv_t m;
+        x = bwt_seed_strategy1(bwt, len, seq, x, opt->min_seed_len, opt->max_mem_intv, &m);
+        if (m.x[2] > 0) kv_push(bwtintv_t, *mem, m);
+      } else ++x;
+    }
+  }
+  ks_introsort_mem_intv(mem->n, mem->a);
+  return (int)mem->n;
+}
+
+typedef struct {
+  const mem_opt_t *opt;
+  int mode;
+  int32_t n_reads;
+  const int64_t *seq_off;
+  const uint8_t *seq;
+  volatile int next;
+  pthread_mutex_t mu;
+  int64_t count;
+} sjob_t;
+
+static void *sworker(void *arg)
+{
+  sjob_t *j = (sjob_t *)arg;
+  bwtintv_v mem = {0, 0, 0}, mem1 = {0, 0, 0}, t0 = {0, 0, 0}, t1 = {0, 0, 0}, *tmpv[2] = {&t0, &t1};
+  int64_t cnt = 0;
+  uint8_t *q = (uint8_t *)malloc(8192);
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    const int r0 = j->next;
+    j->next = r0 + 64;
+    pthread_mutex_unlock(&j->mu);
+    if (r0 >= j->n_reads) break;
+    const int r1 = r0 + 64 < j->n_reads ? r0 + 64 : j->n_reads;
+    for (int r = r0; r < r1; ++r) {
+      const int len = (int)(j->seq_off[r + 1] - j->seq_off[r]);
+      memcpy(q, j->seq + j->seq_off[r], len); /* mem_chain takes a writable copy of the read in bwa-flow too */
+      if (j->mode == 0) {
+        cnt += collect_count(j->opt, g_idx->bwt, len, q, &mem, &mem1, tmpv);
+      } else {
+        ref_chain_v c = mem_chain(j->opt, g_idx->bwt, g_idx->bns, len, q, 0);
+        c.n = mem_chain_flt(j->opt, (int)c.n, c.a);
+        mem_flt_chained_seeds(j->opt, g_idx->bns, g_idx->pac, len, q, (int)c.n, c.a);
+        cnt += (int64_t)c.n;
+        for (size_t k = 0; k < c.n; ++k) free(c.a[k].seeds);
+        free(c.a);
+      }
+    }
+  }
+  free(q);
+  free(mem.a); free(mem1.a); free(t0.a); free(t1.a);
+  pthread_mutex_lock(&j->mu);
+  j->count += cnt;
+  pthread_mutex_unlock(&j->mu);
+  return 0;
+}
+
+double ref_seeding_bench(const char *prefix, int mode, int32_t n_reads, const int64_t *seq_off, const uint8_t *seq,
+                         int n_threads, int reps, int64_t *out_count)
+{
+  if (!g_idx || strcmp(prefix, g_prefix) != 0) {
+    if (g_idx) bwa_idx_destroy(g_idx);
+    bwa_verbose = 1;
+    g_idx = bwa_idx_load(prefix, BWA_IDX_ALL);
+    if (!g_idx) return -1.0;
+    snprintf(g_prefix, sizeof g_prefix, "%s", prefix);
+  }
+  mem_opt_t *opt = mem_opt_init();
+  struct timeval a, b;
+  gettimeofday(&a, 0);
+  int64_t count = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    sjob_t j = {opt, mode, n_reads, seq_off, seq, 0, PTHREAD_MUTEX_INITIALIZER, 0};
+    pthread_t th[256];
+    const int nt = n_threads < 1 ? 1 : n_threads > 256 ? 256 : n_threads;
+    for (int t = 0; t < nt; ++t) pthread_create(&th[t], 0, sworker, &j);
+    for (int t = 0; t < nt; ++t) pthread_join(th[t], 0);
+    count = j.count;
+  }
+  gettimeofday(&b, 0);
+  free(opt);
+  if (out_count) *out_count = count;
+  return (b.tv_sec - a.tv_sec) + 1e-6 * (b.tv_usec - a.tv_usec);
+}
