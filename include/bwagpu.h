@@ -52,6 +52,15 @@
  *       per-seed result records processOutput reads (FPGAPipeline.cpp:90-105)
  *       out, every seed extended as mem_chain2aln extends one seed
  *       (bwa/bwamem.c:717-792) in its chain's window rmax.
+ *   bwagpu_set_bwt / bwagpu_collect_intv / bwagpu_bwt_sa
+ *       seeding's interval search and SA lookups for a batch (bwa_idx_load's
+ *       bwt_t, mem_collect_intv bwamem.c:120-167, bwt_sa bwt.c:86-96).
+ *   bwagpu_seqs2chains
+ *       SeqsToChains' per-read body (src/bwa_wrapper.cpp:118-131: mem_chain,
+ *       mem_chain_flt, mem_flt_chained_seeds) for a whole batch.
+ *   bwagpu_seqs2regions
+ *       SeqsToChains + ChainsToRegions (src/Pipeline.cpp:110-121, 503-544) as
+ *       one device call: reads in, mem_alnreg_v out.
  *   bwagpu_last_error
  *       the what() of fpgaHangError / fpgaResultsError / std::runtime_error
  *       (src/util.h:16-32, OpenCLEnv.h:21-31).
