@@ -49,16 +49,28 @@ struct DevBuf {  // grow-only device buffer
   T* as() const { return (T*)p; }
 };
 
+// BWAGPU_PINNED=nc: the input staging buffers are non-coherent (coarse-grained)
+// pinned memory instead of the default coherent kind (A/B of the H2D copy's
+// host cost)
+unsigned pinned_in_flags() {
+  static const unsigned f = [] {
+    const char* e = getenv("BWAGPU_PINNED");
+    return (e && strcmp(e, "nc") == 0) ? (unsigned)hipHostMallocNonCoherent : (unsigned)hipHostMallocDefault;
+  }();
+  return f;
+}
+
 struct HostBuf {  // grow-only pinned host buffer
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n + n / 4, 4096);
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -746,6 +758,7 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   s.n_seeds = b->n_seeds;
   InLayout L;
   L.make(*b);
+  s.h_in.flags = pinned_in_flags();
   HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
   HIPC(s.d_in.ensure(L.total), "hipMalloc(in)");
   HIPC(s.d_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipMalloc(out)");
@@ -839,8 +852,11 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
   }
   if (ctx->fail_after > 0) --ctx->fail_after;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  // watchdog (SWTask::finish, SWTask.cpp:162-169): poll the completion event
+  // watchdog (SWTask::finish, SWTask.cpp:162-169): poll the completion event,
+  // backing off from 20 to 320 us (every query takes the runtime's lock, which
+  // other host threads driving the device contend for)
   const auto t0 = std::chrono::steady_clock::now();
+  int nap_us = 20;
   for (;;) {
     hipError_t q = hipEventQuery(s.ev3);
     if (q == hipSuccess) break;
@@ -853,7 +869,8 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
             ctx->watchdog_ms) {
       return fail(ctx, BWAGPU_E_HANG, "watchdog: batch did not finish in time");
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    std::this_thread::sleep_for(std::chrono::microseconds(nap_us));
+    nap_us = std::min(nap_us * 2, 320);
   }
   s.busy = false;
   const int64_t* st = s.h_stats.as<int64_t>();
@@ -892,6 +909,7 @@ int bwagpu_chain2aln_stage(bwagpu_ctx_t* ctx, int slot, int32_t n_reads, int32_t
   InLayout L;
   L.make(b);
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  s.h_in.flags = pinned_in_flags();
   HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
   char* h = s.h_in.as<char>();
   b.seq_off = (const int64_t*)(h + L.seq_off);
