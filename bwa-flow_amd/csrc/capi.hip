@@ -161,7 +161,7 @@ struct bwagpu_ctx {
   hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
   // seeding (bwagpu_set_bwt / bwagpu_collect_intv): the resident FM-index and
   // the batch buffers
-  DevBuf bwt_words, sa_d, sa_in, sa_out;
+  DevBuf bwt_words, sa_d, sa_in, sa_out, occ_d, sup_d;
   DevBwt bwt{};
   bool has_bwt = false;
   DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy;
@@ -373,7 +373,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   if (ctx->ch_cs.fork) (void)hipEventDestroy(ctx->ch_cs.fork);
   ctx->ch_slot.d_out.release(); ctx->ch_slot.d_n.release(); ctx->ch_slot.d_stats.release();
   for (DevBuf* b : {&ctx->r2_tasks, &ctx->r2_q, &ctx->r2_out, &ctx->r2_cig, &ctx->r2_md, &ctx->r2_lists, &ctx->r2_z,
-                    &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->sd_off,
+                    &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->occ_d, &ctx->sup_d, &ctx->sd_off,
                     &ctx->sd_seq, &ctx->sd_out, &ctx->sd_n, &ctx->sd_scratch, &ctx->sd_poff, &ctx->sd_pack,
                     &ctx->sd_heavy, &ctx->st_buf, &ctx->st_start, &ctx->st_q, &ctx->st_tasks, &ctx->st_lists,
                     &ctx->st_seen, &ctx->st_ctr, &ctx->st_out, &ctx->ch_npos, &ctx->ch_posoff, &ctx->ch_frac,
@@ -1552,6 +1552,16 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
   for (int i = 0; i < 5; ++i) ctx->bwt.L2[i] = bwt->L2[i];
   ctx->bwt.seq_len = bwt->seq_len;
   ctx->bwt.bwt = ctx->bwt_words.as<uint32_t>();
+  {  // the device occurrence layout (seed.hip: 64-position blocks)
+    HIPC(ctx->occ_d.ensure(2 * sizeof(uint4) * (size_t)occ64_blocks(bwt->seq_len)), "hipMalloc");
+    HIPC(ctx->sup_d.ensure(4 * sizeof(uint64_t) * (size_t)occ64_supers(bwt->seq_len)), "hipMalloc");
+    HIPC(hipMemset(ctx->occ_d.p, 0, 2 * sizeof(uint4) * (size_t)occ64_blocks(bwt->seq_len)), "memset");
+    hipStream_t st = ctx->slot[0].stream;
+    HIPC(launch_build_occ64(ctx->bwt, ctx->occ_d.as<uint4>(), ctx->sup_d.as<uint64_t>(), st), "build_occ64 launch");
+    HIPC(hipStreamSynchronize(st), "sync");
+    ctx->bwt.occ = ctx->occ_d.as<uint4>();
+    ctx->bwt.sup = ctx->sup_d.as<uint64_t>();
+  }
   ctx->bwt.sa = nullptr;
   ctx->bwt.sa_mask = 0;
   ctx->bwt.sa_shift = 0;

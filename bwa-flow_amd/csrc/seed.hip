@@ -25,28 +25,35 @@ struct Ivl {
 };
 static_assert(sizeof(Ivl) == sizeof(bwagpu_intv_t), "interval layout");
 
-// the counts of one 128-position block up to position k (bwt_occ4's body,
-// bwt.c:169-187, for k already past the $ adjustment): three
-// equality-popcounts per word of 2-bit bases, A from the position count
-__device__ __forceinline__ void block_counts(uint64_t k, const uint4 c01, const uint4 c23, const uint4 w0, const uint4 w1,
-                                             uint64_t cnt[4]) {
-  const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-  const int nfull = (int)((k & 127) >> 4);
+// ---- occurrence counting on the device layout
+// bwa's interleaved array (bwt.h:46-57) stores, per 128 positions, four
+// uint64 counts and 8 words of 2-bit bases: 64 B fetched and 8 words counted
+// per lookup.  bwagpu_set_bwt re-lays it out once (build_occ64_kernel): per
+// 64 positions one 32-byte record {uint32 count of A/C/G/T before the block,
+// relative to its 2^32-position superblock; 4 words of bases}, plus 4 uint64
+// counts per superblock.  A lookup is one 32-byte fetch and 4 words counted
+// (three equality-popcounts each, A from the position count); the counts are
+// bwa's exactly (bwt_occ4, bwt.c:169-187).
+__device__ __forceinline__ void block_counts64(uint64_t k, const uint4 hdr, const uint4 w4, const uint64_t* sup,
+                                               uint64_t cnt[4]) {
+  const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+  const int nfull = (int)((k & 63) >> 4);
   const uint32_t tail = ~((1u << ((~(uint32_t)k & 15) << 1)) - 1);  // fields 0..(k & 15) of word nfull
   uint32_t c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const uint32_t m = (i < nfull ? 0xffffffffu : i == nfull ? tail : 0u) & 0x55555555u;
     const uint32_t x1 = w[i] ^ 0x55555555u, x2 = w[i] ^ 0xaaaaaaaau, x3 = ~w[i];
     c1 += __popc(~(x1 | x1 >> 1) & m);
     c2 += __popc(~(x2 | x2 >> 1) & m);
     c3 += __popc(~(x3 | x3 >> 1) & m);
   }
-  const uint32_t c0 = (uint32_t)(k & 127) + 1 - c1 - c2 - c3;
-  cnt[0] = ((uint64_t)c01.y << 32 | c01.x) + c0;
-  cnt[1] = ((uint64_t)c01.w << 32 | c01.z) + c1;
-  cnt[2] = ((uint64_t)c23.y << 32 | c23.x) + c2;
-  cnt[3] = ((uint64_t)c23.w << 32 | c23.z) + c3;
+  const uint32_t c0 = (uint32_t)(k & 63) + 1 - c1 - c2 - c3;
+  const uint64_t* sp = sup + 4 * (k >> 32);
+  cnt[0] = sp[0] + hdr.x + c0;
+  cnt[1] = sp[1] + hdr.y + c1;
+  cnt[2] = sp[2] + hdr.z + c2;
+  cnt[3] = sp[3] + hdr.w + c3;
 }
 
 // bwt_occ4 (bwt.c:169-187): occurrences of A/C/G/T in bwt[0..k], $ removed
@@ -56,13 +63,13 @@ __device__ __forceinline__ void occ4(const DevBwt& b, uint64_t k, uint64_t cnt[4
     return;
   }
   k -= (k >= b.primary);
-  const uint4* p = reinterpret_cast<const uint4*>(b.bwt + (k >> 7 << 4));
-  block_counts(k, p[0], p[1], p[2], p[3], cnt);
+  const uint4* p = b.occ + 2 * (k >> 6);
+  block_counts64(k, p[0], p[1], b.sup, cnt);
 }
 
 // bwt_2occ4 (bwt.c:189-214): both ends of an interval; when they fall in the
-// same 128-position block it is fetched once (the second fetch is issued only
-// by the lanes whose ends lie in different blocks)
+// same block it is fetched once (the second fetch is issued only by the lanes
+// whose ends lie in different blocks)
 __device__ __forceinline__ void occ4x2(const DevBwt& b, uint64_t k, uint64_t l, uint64_t tk[4], uint64_t tl[4]) {
   if (k == ~0ull || l == ~0ull) {
     occ4(b, k, tk);
@@ -70,18 +77,62 @@ __device__ __forceinline__ void occ4x2(const DevBwt& b, uint64_t k, uint64_t l, 
     return;
   }
   const uint64_t kk = k - (k >= b.primary), ll = l - (l >= b.primary);
-  const uint4* pk = reinterpret_cast<const uint4*>(b.bwt + (kk >> 7 << 4));
-  uint4 a0 = pk[0], a1 = pk[1], a2 = pk[2], a3 = pk[3];
-  uint4 d0 = a0, d1 = a1, d2 = a2, d3 = a3;
-  if ((kk >> 7) != (ll >> 7)) {
-    const uint4* pl = reinterpret_cast<const uint4*>(b.bwt + (ll >> 7 << 4));
+  const uint4* pk = b.occ + 2 * (kk >> 6);
+  const uint4 a0 = pk[0], a1 = pk[1];
+  uint4 d0 = a0, d1 = a1;
+  if ((kk >> 6) != (ll >> 6)) {
+    const uint4* pl = b.occ + 2 * (ll >> 6);
     d0 = pl[0];
     d1 = pl[1];
-    d2 = pl[2];
-    d3 = pl[3];
   }
-  block_counts(kk, a0, a1, a2, a3, tk);
-  block_counts(ll, d0, d1, d2, d3, tl);
+  block_counts64(kk, a0, a1, b.sup, tk);
+  block_counts64(ll, d0, d1, b.sup, tl);
+}
+
+// bwt_B0 (bwt.h:86): the base at $-free position x
+__device__ __forceinline__ int base_at(const DevBwt& b, uint64_t x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(b.occ + 2 * (x >> 6) + 1);
+  return (int)(w[(x & 63) >> 4] >> ((~x & 15) << 1) & 3);
+}
+
+// one lane per 64-position block: its record from bwa's array (the bwa block
+// header's counts + the bases of the block's first half before it)
+__global__ void __launch_bounds__(256) build_occ64_kernel(DevBwt b, uint4* __restrict__ occ, uint64_t* __restrict__ sup,
+                                                          uint64_t n_blocks, uint64_t n_sup) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_sup) {  // superblock s starts at position s << 32, a bwa block boundary
+    const uint64_t pos = i << 32;
+    const uint64_t* hb = reinterpret_cast<const uint64_t*>(b.bwt + ((pos >> 7) << 4));
+    for (int c = 0; c < 4; ++c) sup[4 * i + c] = pos < b.seq_len ? hb[c] : 0;
+  }
+  if (i >= n_blocks) return;
+  const uint64_t pos = i << 6;  // first position of the block
+  if (pos >= b.seq_len) return;  // (the spare record is never read)
+  const uint32_t* bb = b.bwt + ((pos >> 7) << 4);
+  const uint64_t* hb = reinterpret_cast<const uint64_t*>(bb);
+  const uint64_t* hs = reinterpret_cast<const uint64_t*>(b.bwt + (((pos >> 32) << 32 >> 7) << 4));
+  uint64_t cnt[4] = {hb[0], hb[1], hb[2], hb[3]};
+  const int half = (int)((pos >> 6) & 1);
+  const uint32_t* w = bb + 8 + 4 * half;
+  if (half) {  // the block's first 64 bases (words 0-3) come before it
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t v = bb[8 + j];
+      const uint32_t x1 = v ^ 0x55555555u, x2 = v ^ 0xaaaaaaaau, x3 = ~v;
+      const uint32_t n1 = __popc(~(x1 | x1 >> 1) & 0x55555555u), n2 = __popc(~(x2 | x2 >> 1) & 0x55555555u),
+                     n3 = __popc(~(x3 | x3 >> 1) & 0x55555555u);
+      cnt[0] += 16 - n1 - n2 - n3;
+      cnt[1] += n1;
+      cnt[2] += n2;
+      cnt[3] += n3;
+    }
+  }
+  uint4 hdr;
+  hdr.x = (uint32_t)(cnt[0] - hs[0]);
+  hdr.y = (uint32_t)(cnt[1] - hs[1]);
+  hdr.z = (uint32_t)(cnt[2] - hs[2]);
+  hdr.w = (uint32_t)(cnt[3] - hs[3]);
+  occ[2 * i] = hdr;
+  occ[2 * i + 1] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // bwt_extend (bwt.c:262-276)
@@ -645,8 +696,7 @@ __global__ void __launch_bounds__(256) bwt_sa_kernel(DevBwt b, int64_t n, const 
       continue;
     }
     const uint64_t x = k - (k > b.primary);
-    const uint32_t w = b.bwt[(x >> 7 << 4) + 8 + ((x & 127) >> 4)];
-    const int c = (int)(w >> ((~(uint32_t)x & 15) << 1) & 3);  // bwt_B0
+    const int c = base_at(b, x);  // bwt_B0
     uint64_t cnt[4];
     occ4(b, k, cnt);  // bwt_occ(k, c); k == seq_len gives the column total
     k = b.L2[c] + cnt[c];
@@ -655,6 +705,13 @@ __global__ void __launch_bounds__(256) bwt_sa_kernel(DevBwt b, int64_t n, const 
 }
 
 }  // namespace
+
+hipError_t launch_build_occ64(const DevBwt& b, uint4* occ, uint64_t* sup, hipStream_t st) {
+  const uint64_t nb = occ64_blocks(b.seq_len), ns = occ64_supers(b.seq_len);
+  const uint64_t n = nb > ns ? nb : ns;
+  hipLaunchKernelGGL(build_occ64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, b, occ, sup, nb, ns);
+  return hipGetLastError();
+}
 
 hipError_t launch_bwt_sa(const DevBwt& b, int64_t n, const uint64_t* k, uint64_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
