@@ -164,7 +164,7 @@ struct bwagpu_ctx {
   DevBuf bwt_words, sa_d, sa_in, sa_out, occ_d, sup_d;
   DevBwt bwt{};
   bool has_bwt = false;
-  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy;
+  DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy, sd_dbg;
   // seeding's chaining (bwagpu_seqs2chains / bwagpu_seqs2regions): per read,
   // per SA position, the kbtree arenas, mem_seed_sw tasks, the packed chains
   DevBuf ch_npos, ch_posoff, ch_frac, ch_nout, ch_noseed, ch_nsw, ch_need, ch_swtab, ch_alt;
@@ -375,7 +375,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   for (DevBuf* b : {&ctx->r2_tasks, &ctx->r2_q, &ctx->r2_out, &ctx->r2_cig, &ctx->r2_md, &ctx->r2_lists, &ctx->r2_z,
                     &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->occ_d, &ctx->sup_d, &ctx->sd_off,
                     &ctx->sd_seq, &ctx->sd_out, &ctx->sd_n, &ctx->sd_scratch, &ctx->sd_poff, &ctx->sd_pack,
-                    &ctx->sd_heavy, &ctx->st_buf, &ctx->st_start, &ctx->st_q, &ctx->st_tasks, &ctx->st_lists,
+                    &ctx->sd_heavy, &ctx->sd_dbg, &ctx->st_buf, &ctx->st_start, &ctx->st_q, &ctx->st_tasks, &ctx->st_lists,
                     &ctx->st_seen, &ctx->st_ctr, &ctx->st_out, &ctx->ch_npos, &ctx->ch_posoff, &ctx->ch_frac,
                     &ctx->ch_nout, &ctx->ch_noseed, &ctx->ch_nsw, &ctx->ch_need, &ctx->ch_swtab, &ctx->ch_alt,
                     &ctx->ch_kpos, &ctx->ch_rbeg, &ctx->ch_qinfo, &ctx->ch_label, &ctx->ch_score, &ctx->ch_slist,
@@ -1659,6 +1659,11 @@ int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads
   a.n_heavy = ctx->sd_heavy.as<int32_t>();
   a.flags = a.heavy + n_reads;
   a.p3_n = a.flags + n_reads;
+  if (getenv("BWAGPU_SEED_DBG")) {  // per-lane tier-1 stamps (tools_dev)
+    HIPC(ctx->sd_dbg.ensure(sizeof(int64_t) * 8 * (size_t)n_reads), "hipMalloc");
+    HIPC(hipMemsetAsync(ctx->sd_dbg.p, 0, sizeof(int64_t) * 8 * (size_t)n_reads, st), "memset");
+    a.dbg = ctx->sd_dbg.as<int64_t>();
+  }
   HIPC(launch_collect_intv(ctx->bwt, a, st), "collect_intv launch");
   return BWAGPU_OK;
 }
@@ -1681,6 +1686,14 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   if ((rc = seed_enqueue(ctx, opt, n_reads, seq_off, seq, bases, max_per_read, true, st, a))) return rc;
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");
+  if (const char* dp = getenv("BWAGPU_SEED_DBG")) {
+    std::vector<int64_t> d(8 * (size_t)n_reads);
+    HIPC(hipMemcpy(d.data(), ctx->sd_dbg.p, sizeof(int64_t) * d.size(), hipMemcpyDeviceToHost), "D2H");
+    if (FILE* f = fopen(dp, "ab")) {
+      fwrite(d.data(), sizeof(int64_t), d.size(), f);
+      fclose(f);
+    }
+  }
   // pack the per-read slots back to back (read order) and copy only those
   std::vector<int64_t> off((size_t)n_reads + 1, 0);
   for (int32_t r = 0; r < n_reads; ++r) {

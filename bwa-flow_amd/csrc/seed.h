@@ -43,6 +43,7 @@ struct SeedArgs {
   int32_t* n_heavy;   // their number
   int32_t* flags;     // n_reads: 1 = handed to tier 2
   int32_t* p3_n;      // n_reads: LAST-like intervals in the read's fourth list
+  int64_t* dbg;       // NULL, or 4 per tier-1 lane: {extensions, steps, start, end} (wall_clock64)
 };
 
 // lists a read needs in the scratch buffer: 4 * (bases + 2 * reads) entries

@@ -14,6 +14,7 @@
 // there with klib's introsort restated step for step (the order of intervals
 // with equal info is the algorithm's).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "seed.h"
 
@@ -174,8 +175,102 @@ __device__ __forceinline__ Ivl extend1(const DevBwt& b, const Ivl& ik, int c, in
 }
 
 __device__ __forceinline__ uint64_t l2_at(const DevBwt& b, int i) {  // L2[i] by selects, not a scratch copy
-  return i == 0 ? b.L2[0] : i == 1 ? b.L2[1] : i == 2 ? b.L2[2] : i == 3 ? b.L2[3] : b.L2[4];
+  // (the empty asm keeps the compiler from turning the selects back into an
+  // indexed copy of the kernel argument in scratch memory)
+  uint64_t l0 = b.L2[0], l1 = b.L2[1], l2 = b.L2[2], l3 = b.L2[3], l4 = b.L2[4];
+  asm volatile("" : "+s"(l0), "+s"(l1), "+s"(l2), "+s"(l3), "+s"(l4));
+  return i == 0 ? l0 : i == 1 ? l1 : i == 2 ? l2 : i == 3 ? l3 : l4;
 }
+
+// bwt_extend's ok[c] in the backward form (is_back = 1; a forward extension
+// runs on the swapped interval), counting only what ok[c] needs: the
+// occurrences of c at both ends and those of the bases above c (bwt.c:
+// 272-275 sums their sizes) — an equality and a comparison popcount per word
+// instead of three equality ones, 32-bit arithmetic inside a superblock, and
+// the superblock table read only when the BWT has positions past 2^32.
+// Intervals always start at row >= 1 (set_intv and every extension give
+// L2[c] + 1 + ...), so k = x[0] - 1 is never bwt_occ's (bwtint_t)-1.
+struct CountsC {
+  uint32_t eq, gt;  // occurrences of c / of bases above c in [superblock start, position]
+};
+__device__ __forceinline__ CountsC counts_c(uint64_t k, const uint4 hdr, const uint4 w4, uint32_t pe_hi, uint32_t pe_lo,
+                                            uint32_t g_or, uint32_t g_lo, int c) {
+  const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+  const int nfull = (int)((k & 63) >> 4);
+  const uint32_t tail = ~((1u << ((~(uint32_t)k & 15) << 1)) - 1);
+  uint32_t eq = c == 0 ? hdr.x : c == 1 ? hdr.y : c == 2 ? hdr.z : hdr.w;
+  uint32_t gt = (c < 1 ? hdr.y : 0u) + (c < 2 ? hdr.z : 0u) + (c < 3 ? hdr.w : 0u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t m = (i < nfull ? 0xffffffffu : i == nfull ? tail : 0u) & 0x55555555u;
+    const uint32_t hi = (w[i] >> 1) & m, lo = w[i] & m;
+    eq += __popc(~((hi ^ pe_hi) | (lo ^ pe_lo)) & m);  // fields equal to c
+    gt += __popc((hi & (lo | g_or)) | (lo & g_lo));    // fields above c
+  }
+  return CountsC{eq, gt};
+}
+
+// the superblock's counts of c and of the bases above c (zero below 2^32)
+__device__ __forceinline__ void sup_c(const DevBwt& b, uint64_t k, int c, uint64_t& eq, uint64_t& gt) {
+  const ulonglong2* sp = reinterpret_cast<const ulonglong2*>(b.sup + 4 * (k >> 32));
+  const ulonglong2 s01 = sp[0], s23 = sp[1];
+  eq = c == 0 ? s01.x : c == 1 ? s01.y : c == 2 ? s23.x : s23.y;
+  gt = (c < 1 ? s01.y : 0ull) + (c < 2 ? s23.x : 0ull) + (c < 3 ? s23.y : 0ull);
+}
+
+// extend_c in two halves, so that a caller can issue other loads between the
+// fetch of the occurrence records and the first use of their data
+struct OccRecs {
+  uint64_t kk, ll;
+  uint4 a0, a1, d0, d1;
+};
+__device__ __forceinline__ OccRecs extend_fetch(const DevBwt& b, const Ivl& ik) {
+  OccRecs o;
+  const uint64_t k = ik.x[0] - 1, l = k + ik.x[2];
+  o.kk = k - (k >= b.primary);
+  o.ll = l - (l >= b.primary);
+  const uint4* pk = b.occ + 2 * (o.kk >> 6);
+  o.a0 = pk[0];
+  o.a1 = pk[1];
+  o.d0 = o.a0;
+  o.d1 = o.a1;
+  if ((o.kk >> 6) != (o.ll >> 6)) {  // the second block only when the ends do not share one
+    const uint4* pl = b.occ + 2 * (o.ll >> 6);
+    o.d0 = pl[0];
+    o.d1 = pl[1];
+  }
+  return o;
+}
+
+__device__ __forceinline__ Ivl extend_finish(const DevBwt& b, const Ivl& ik, int c, const OccRecs& f) {
+  const uint32_t pe_hi = (c & 2) ? 0x55555555u : 0u, pe_lo = (c & 1) ? 0x55555555u : 0u;
+  // field > c: c = 0 -> hi | lo, 1 -> hi, 2 -> hi & lo, 3 -> none
+  const uint32_t g_or = c <= 1 ? 0x55555555u : 0u, g_lo = c == 0 ? 0x55555555u : 0u;
+  const uint32_t g_on = c == 3 ? 0u : 0xffffffffu;
+  const CountsC ck = counts_c(f.kk, f.a0, f.a1, pe_hi, pe_lo, g_or, g_lo, c);
+  const CountsC cl = counts_c(f.ll, f.d0, f.d1, pe_hi, pe_lo, g_or, g_lo, c);
+  uint64_t tk = ck.eq, tl = cl.eq, gk = ck.gt & g_on, gl = cl.gt & g_on;
+  if (b.seq_len >> 32) {  // wave-uniform: the BWT has superblocks past the first
+    uint64_t se, sg;
+    sup_c(b, f.kk, c, se, sg);
+    tk += se;
+    gk += c == 3 ? 0ull : sg;
+    sup_c(b, f.ll, c, se, sg);
+    tl += se;
+    gl += c == 3 ? 0ull : sg;
+  }
+  Ivl o;
+  o.x[0] = l2_at(b, c) + 1 + tk;
+  o.x[2] = tl - tk;
+  o.x[1] = ik.x[1] + (ik.x[0] <= b.primary && ik.x[0] + ik.x[2] - 1 >= b.primary) + (gl - gk);
+  o.info = 0;
+  return o;
+}
+
+__device__ __forceinline__ Ivl extend_c(const DevBwt& b, const Ivl& ik, int c) {
+  return extend_finish(b, ik, c, extend_fetch(b, ik));
+}
+
 
 __device__ __forceinline__ Ivl set_intv(const DevBwt& b, int c) {  // bwt.h:80
   Ivl ik;
@@ -448,6 +543,273 @@ __global__ void __launch_bounds__(256) collect_intv_kernel(DevBwt b, SeedArgs a)
       if ((uint32_t)mem1.a[i].info - (uint32_t)(mem1.a[i].info >> 32) >= (uint32_t)a.min_seed_len) mem.push(mem1.a[i]);
   }
   a.out_n[r] = mem.n;  // passes 1-2; the merge adds pass 3 and sorts
+}
+
+// ---- tier 1, one extension per step: the same two lanes per read as
+// collect_intv_kernel, written so that every iteration of a lane's loop is
+// exactly one bwt_extend followed by a few lines of bookkeeping.  In the
+// nested form (bwt_smem1a's forward loop, its backward rows, the loop over a
+// row's items, mem_collect_intv's passes) the lanes of a wave sit in
+// different loops, and a structured loop nest costs the slowest lane's trip
+// count at every level.  Per-lane stamps (BWAGPU_SEED_DBG,
+// tools_dev/seed_lanes.py) and tools_dev/micro/ext_{chain,real}.hip priced
+// it: a lone wave's dependent fetch is 0.6 us, seed.hip's extension 1.2 us,
+// a nested-form step 3.6 us.  Here the loop carries three intervals (the
+// one being extended, the result, the next one fetched during this
+// extension: the row's next item, or the next row's first item, which is
+// the current row's first push), the base the next step needs is fetched
+// during the extension too, and only the rare transitions (an SMEM's end or
+// start, the forward walk's end, the passes) leave the common path.
+// Results, push orders and the tier-2 hand-over rule are the nested
+// kernel's exactly.
+enum : int { kDone, kFwd, kBwd, kS1 };
+enum : int { gNone, gFwdEnd, gSmemEnd, gNextSmem, gS1Next };
+
+__device__ __forceinline__ void swap01(Ivl& v) {
+  const uint64_t t = v.x[0];
+  v.x[0] = v.x[1];
+  v.x[1] = t;
+}
+
+__global__ void __launch_bounds__(256) collect_intv_step_kernel(DevBwt b, SeedArgs a) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= 2 * a.n_reads) return;
+  const bool last_like = t >= a.n_reads;
+  const int r = last_like ? t - a.n_reads : t;
+  const int64_t q0 = a.seq_off[r];
+  const int len = (int)(a.seq_off[r + 1] - q0);
+  const uint8_t* q = a.seq + q0;
+  Ivl* const base = reinterpret_cast<Ivl*>(a.scratch) + 4 * (q0 + 2 * (int64_t)r);
+  const int lcap = len + 2;
+  Ivl* const m1 = base + 2 * lcap;  // bwt_smem1a's own result list
+  Ivl* const p3 = base + 3 * lcap;  // the LAST-like pass's list
+  Ivl* const mem = reinterpret_cast<Ivl*>(a.out) + (int64_t)r * a.max_per_read;
+  const int cap = a.max_per_read;
+  int left = a.budget;
+  const int64_t t_start = a.dbg ? (int64_t)wall_clock64() : 0;
+  int n_steps = 0;
+
+  int mode = kFwd;
+  int pass = 1, x = 0, k = 0, old_n = 0, mem_n = 0, p3_n = 0;
+  int x0 = 0, i = 0, min_intv = 1, ret = 0;
+  int prv = 0, prev_n = 0, curr_n = 0, m1_n = 0, j = 0, qc = 4;  // qc: the base the next extension adds
+  bool prev_rev = false;
+  uint64_t last_sz = 0, m1_last = 0;
+  Ivl cur{};
+
+  // the rare transitions; on return mode is set for the next extension, or kDone
+  auto rare = [&](int go) {
+    while (go != gNone) {
+      if (go == gFwdEnd) {  // bwt.c:318-324: the list reversed (walked from its end), the lists trade places
+        prv ^= 1;
+        prev_n = curr_n;
+        prev_rev = true;
+        curr_n = 0;
+        j = 0;
+        i = x0 - 1;
+        qc = i >= 0 ? (int)q[i] : 4;
+        if (qc > 3) {  // no extension: only the row's first item (cur, the last push) can reach mem
+          if (m1_n == 0 || (uint64_t)(i + 1) < m1_last) {
+            Ivl h = cur;
+            h.info |= (uint64_t)(i + 1) << 32;
+            m1[m1_n++] = h;
+            m1_last = (uint64_t)(i + 1);
+          }
+          go = gSmemEnd;
+        } else {
+          mode = kBwd;
+          go = gNone;
+        }
+      } else if (go == gSmemEnd) {  // bwt.c:352 (mem reversed) and mem_collect_intv's length filter
+        for (int e = m1_n - 1; e >= 0; --e) {
+          const Ivl v = m1[e];
+          if ((int)((uint32_t)v.info - (uint32_t)(v.info >> 32)) >= a.min_seed_len) {
+            if (mem_n < cap) mem[mem_n] = v;
+            ++mem_n;
+          }
+        }
+        if (pass == 1) x = ret;
+        go = gNextSmem;
+      } else if (go == gNextSmem) {  // mem_collect_intv's passes 1 and 2 (bwamem.c:128-149)
+        int xs = -1, mi = 1;
+        if (pass == 1) {
+          while (x < len && q[x] > 3) ++x;
+          if (x < len) {
+            xs = x;
+          } else {
+            pass = 2;
+            old_n = min(mem_n, cap);
+            k = 0;
+            n_steps = a.budget - left;  // (debug stamps: pass 1's share)
+          }
+        } else if (k >= old_n) {
+          a.out_n[r] = mem_n;  // passes 1-2; the merge adds pass 3 and sorts
+          mode = kDone;
+          go = gNone;
+        } else {
+          const Ivl pk = mem[k++];
+          const int start = (int)(pk.info >> 32), end = (int)(int32_t)pk.info;
+          if (end - start >= a.split_len && pk.x[2] <= (uint64_t)a.split_width) {
+            xs = (start + end) >> 1;
+            mi = (int)(pk.x[2] + 1);
+          }
+        }
+        if (xs >= 0) {  // bwt_smem1a's start (bwt.c:298-304)
+          m1_n = 0;
+          x0 = xs;
+          const int c0 = q[xs];
+          if (c0 > 3) {
+            ret = xs + 1;
+            go = gSmemEnd;
+          } else {
+            min_intv = mi < 1 ? 1 : mi;
+            cur = set_intv(b, c0);
+            cur.info = (uint64_t)(xs + 1);
+            curr_n = 0;
+            i = xs + 1;
+            qc = i < len ? (int)q[i] : 4;
+            if (qc > 3) {
+              base[(prv ^ 1) * lcap] = cur;
+              curr_n = 1;
+              ret = (int)cur.info;
+              go = gFwdEnd;
+            } else {
+              mode = kFwd;
+              go = gNone;
+            }
+          }
+        }
+      } else {  // gS1Next: bwamem.c:150-165 around bwt_seed_strategy1 (bwt.c:358-378)
+        if (a.max_mem_intv > 0)
+          while (x < len && q[x] > 3) ++x;
+        if (a.max_mem_intv <= 0 || x >= len) {
+          a.p3_n[r] = p3_n;
+          mode = kDone;
+          go = gNone;
+        } else {
+          cur = set_intv(b, q[x]);
+          x0 = x;
+          i = x + 1;
+          qc = i < len ? (int)q[i] : 4;
+          if (qc > 3) {
+            x = i < len ? i + 1 : len;
+          } else {
+            mode = kS1;
+            go = gNone;
+          }
+        }
+      }
+    }
+  };
+
+  Ivl pre{};
+  int go = last_like ? gS1Next : gNextSmem;
+  for (;;) {
+    if (go != gNone) rare(go);
+    if (mode == kDone) break;
+    const bool back = mode == kBwd;
+    if (--left < 0) {  // tier 2 takes the read
+      if (atomicCAS(a.flags + r, 0, 1) == 0) a.heavy[atomicAdd(a.n_heavy, 1)] = r;
+      break;
+    }
+    // fetched during the extension: the base after this one, and (backward)
+    // the row's next item or the next row's first one
+    // (issued after the extension's fetch, unconditionally, from clamped
+    // addresses, so that nothing waits for them before that fetch is out)
+    Ivl in = cur;
+    if (!back) swap01(in);
+    const OccRecs recs = extend_fetch(b, in);
+    const int qn_pos = back ? i - 1 : i + 1;
+    const int qn_raw = q[min(max(qn_pos, 0), len - 1)];
+    const int pre_at = j + 1 < prev_n ? prv * lcap + (prev_rev ? prev_n - 2 - j : j + 1) : (prv ^ 1) * lcap;
+    pre = base[back ? pre_at : 0];
+    Ivl res = extend_finish(b, in, back ? qc : 3 - qc, recs);
+    if (!back) swap01(res);
+    const int qn = qn_pos >= 0 && qn_pos < len ? qn_raw : 4;
+    go = gNone;
+    if (mode == kBwd) {  // bwt.c:327-349
+      bool first_push = false;
+      if (res.x[2] < (uint64_t)min_intv) {
+        if (curr_n == 0 && (m1_n == 0 || (uint64_t)(i + 1) < m1_last)) {
+          Ivl h = cur;
+          h.info |= (uint64_t)(i + 1) << 32;
+          m1[m1_n++] = h;
+          m1_last = (uint64_t)(i + 1);
+        }
+      } else if (curr_n == 0 || res.x[2] != last_sz) {
+        res.info = cur.info;
+        base[(prv ^ 1) * lcap + curr_n] = res;
+        first_push = curr_n == 0;
+        ++curr_n;
+        last_sz = res.x[2];
+      }
+      if (++j < prev_n) {
+        cur = pre;
+      } else if (curr_n == 0) {
+        go = gSmemEnd;
+      } else {  // the next row
+        cur = first_push ? res : pre;
+        prv ^= 1;
+        prev_n = curr_n;
+        prev_rev = false;
+        curr_n = 0;
+        j = 0;
+        --i;
+        qc = qn;
+        if (qc > 3) {  // an ambiguous base or the read's start: as in rare(gFwdEnd)
+          if (m1_n == 0 || (uint64_t)(i + 1) < m1_last) {
+            Ivl h = cur;
+            h.info |= (uint64_t)(i + 1) << 32;
+            m1[m1_n++] = h;
+            m1_last = (uint64_t)(i + 1);
+          }
+          go = gSmemEnd;
+        }
+      }
+    } else if (mode == kFwd) {  // bwt.c:305-317
+      if (res.x[2] != cur.x[2]) {
+        base[(prv ^ 1) * lcap + curr_n++] = cur;
+        ret = (int)cur.info;
+        if (res.x[2] < (uint64_t)min_intv) go = gFwdEnd;
+      }
+      if (go == gNone) {
+        cur = res;
+        cur.info = (uint64_t)(i + 1);
+        ++i;
+        qc = qn;
+        if (qc > 3) {  // an ambiguous base or the read's end
+          base[(prv ^ 1) * lcap + curr_n++] = cur;
+          ret = (int)cur.info;
+          go = gFwdEnd;
+        }
+      }
+    } else {  // kS1 (bwt.c:365-377)
+      if (res.x[2] < (uint64_t)a.max_mem_intv && i - x0 >= a.min_seed_len) {
+        if (res.x[2] > 0) {
+          res.info = (uint64_t)x0 << 32 | (uint64_t)(i + 1);
+          if (p3_n < lcap) p3[p3_n] = res;
+          ++p3_n;
+        }
+        x = i + 1;
+        go = gS1Next;
+      } else {
+        cur = res;
+        ++i;
+        qc = qn;
+        if (qc > 3) {
+          x = i < len ? i + 1 : len;
+          go = gS1Next;
+        }
+      }
+    }
+  }
+  if (a.dbg) {
+    int64_t* d = a.dbg + 4 * (int64_t)t;
+    d[0] = a.budget - left;
+    d[1] = n_steps;
+    d[2] = t_start;
+    d[3] = (int64_t)wall_clock64();
+  }
 }
 
 // tier 1's two halves of a read joined (bwamem.c:166: the sort of all)
@@ -731,7 +1093,12 @@ hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t s
   hipError_t e = hipMemsetAsync(a.n_heavy, 0, sizeof(int32_t), st);
   if (e == hipSuccess) e = hipMemsetAsync(a.flags, 0, sizeof(int32_t) * (size_t)a.n_reads, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(collect_intv_kernel, dim3((2 * a.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  // BWAGPU_SEED_STEP=1: the one-extension-per-step form (A/B)
+  static const bool step = getenv("BWAGPU_SEED_STEP") && atoi(getenv("BWAGPU_SEED_STEP"));
+  if (step)
+    hipLaunchKernelGGL(collect_intv_step_kernel, dim3((2 * a.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  else
+    hipLaunchKernelGGL(collect_intv_kernel, dim3((2 * a.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(tier1_merge_kernel, dim3((a.n_reads + 255) / 256), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -33,11 +33,18 @@ def main():
     ap.add_argument("--cpu-reads", type=int, default=4000)
     ap.add_argument("--budget", type=int, default=-1, help="bwt_extend calls per read on one lane (-1: library default)")
     ap.add_argument("--mult", type=str, default="", help="comma list: also time k copies of the batch in one call")
+    ap.add_argument("--reads", type=str, default="", help="first:count: only these reads of the batch")
     a = ap.parse_args()
     z = np.load(os.path.join(ROOT, "bench_data", "c2_bwt.npz"))
     hdr, words = z["hdr"], z["words"]
     _, _, batches = load_fixture(with_ref=False)
     b = batches[0].batch
+    if a.reads:
+        f, c = (int(v) for v in a.reads.split(":"))
+        so = b.seq_off[f:f + c + 1]
+        b = type("B", (), dict(seq_off=(so - so[0]).astype(np.int64), seq=b.seq[so[0]:so[-1]], n_reads=c))
+        a.check = min(a.check, c)
+        a.cpu_reads = min(a.cpu_reads, c)
     refd = G.load_ref()
     opt, *_ = G.load_chain_set("c1_default")
     eng = Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
