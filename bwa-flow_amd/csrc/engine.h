@@ -169,9 +169,15 @@ enum {
 // MI355X_MICROARCH.md "dequeue"; measured here: 7.9 -> 6.6 ms per C2 batch
 // when the nine lists' heads moved off the two shared lines)
 constexpr int kQHStride = 32;
-constexpr int kQHWords = kSpecRounds * kSpecBins * 8 * kQHStride;
-// pair-kernel task order (spec_sort_*): 1024 keys = (left qlen / 8, right qlen / 8)
+// + one head per list for the lane kernel (spec_extl_kernel), after the sharded ones
+constexpr int kQHLaneBase = kSpecRounds * kSpecBins * 8 * kQHStride;
+constexpr int kQHWords = kQHLaneBase + kSpecRounds * kSpecBins * kQHStride;
+// pair-kernel task order (spec_sort_*): 1024 keys = (left qlen / 8, right qlen / 8);
+// with the lane kernel on, keys 0 .. kLaneKeys-1 hold its tasks (both sides'
+// qlen <= kLaneQ), largest (ql/8 + qr/8) first, and the pair kernel's keys follow
 constexpr int kSortKeys = 1024;
+constexpr int kLaneQ = 63;                          // spec_extl_kernel: both sides' qlen <= kLaneQ
+constexpr int kLaneKeys = 2 * (kLaneQ >> 3) + 1;    // (ql / 8 + qr / 8) <= 2 (kLaneQ / 8)
 constexpr int kSortWords = kSpecRounds * 2 * kSortKeys;
 // task list `list` (= round * kSpecBins + bin) starts at this entry of SpecArgs::tasks
 __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_seeds) {

@@ -3123,15 +3123,22 @@ __device__ __forceinline__ void store_ext_half(SeedExt* dst, const SeedExt& e) {
 // PMAX = the bin's largest CPL: ceil(read length / 32) (qlen + 1 <= read length)
 template <int PMAX>
 __global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
-                                                           int tb_bytes, int sorted) {
+                                                           int tb_bytes, int sorted, int lane) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int hf = (int)(threadIdx.x >> 5) & 1;
   // per half: left rows, right rows, the task context
   uint8_t* const tbl = lds + (size_t)(threadIdx.x >> 5) * (2 * tb_bytes + sizeof(PairCtx));
   uint8_t* const tbr = tbl + tb_bytes;
   LdsCtx* const cx = (LdsCtx*)(tbr + tb_bytes);
-  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const int2* tl = (sorted ? a.stasks : a.tasks) + spec_list_off(list, b.n_chains, b.n_seeds);
+  if (lane) {  // the first n_lane sorted tasks are spec_extl_kernel's
+    const int round = list / kSpecBins, bin = list % kSpecBins;
+    const int nl = uni(__hip_atomic_load(&a.sorth[(round * 2 + bin) * kSortKeys + kLaneKeys - 1], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT));
+    tl += nl;
+    n -= nl;
+  }
   ShardQ qq;
   qq.init(a.qh + 8 * kQHStride * list, n);
   long long spec_cells = 0;
@@ -3169,6 +3176,269 @@ __global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref,
 // LDS bytes of a spec_ext2_kernel workgroup
 static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size_t)tb_bytes + sizeof(PairCtx)); }
 
+// ---------------------------------------------------- one seed per lane
+// The short tasks of a list — both sides' qlen <= kLaneQ — run one seed per
+// LANE: each lane is a scalar ksw_extend2 (ksw.c:380-479, in the row-major form
+// of oracle/ksw_ext.c) with its eh[] row in LDS, and walks its own seed through
+// extend_seed (bwamem.c:717-792) as a state machine.  The wave steps every
+// lane's current DP row together; a lane whose seed is done stores its SeedExt
+// and claims the next task at once (wave-aggregated), so lanes never wait for
+// the wave's longest task.  Per DP cell: two LDS reads (the packed H|E word,
+// the query's score shift), one LDS write and ~18 VALU, against one row's
+// scans and reductions per 32 columns in extend_pair: for qlen <= 63 the
+// per-row fixed cost of the wave forms dominates.
+//
+// LDS per wave: eh[j][lane] = H(i-1, j-1) | E(i, j) << 16 (both >= 0 and
+// < 2^16: scores stay below 1024 * max(mat) for reads up to 1023 bp), and
+// qs[j][lane] = 6 * query base: the score of target base t against query base
+// q is the signed 6-bit field q of a per-row word (host check: every mat
+// entry in [-32, 31]).  The lane index is the fastest dimension, so lanes at
+// different columns never share an LDS bank for the 32-bit words.
+static_assert(kLaneQ + 1 <= 1024 && (kLaneQ & 7) == 7, "lane kernel: qlen bound");
+constexpr size_t kLaneLds = (size_t)(kLaneQ + 1) * 64 * 5;  // 10240 B per wave (qs has a spare row)
+
+// pac byte p, clamped into the array (l_pac / 4 + 1 bytes): a prefetch past
+// either end of a window is never used
+__device__ __forceinline__ uint32_t pac_byte(const DevRef& ref, int64_t p) {
+  p = p < 0 ? 0 : (p > (ref.l_pac >> 2) ? (ref.l_pac >> 2) : p);
+  return ref.pac[p];
+}
+
+__global__ void __launch_bounds__(64) spec_extl_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = (int)(threadIdx.x & 63);
+  uint32_t* const eh = reinterpret_cast<uint32_t*>(lds) + lane;  // column j at eh[64 j]
+  uint8_t* const qs = lds + (size_t)(kLaneQ + 1) * 64 * 4 + lane;  // column j at qs[64 j]
+  const int round = list / kSpecBins, bin = list % kSpecBins;
+  const int n_lane = __hip_atomic_load(&a.sorth[(round * 2 + bin) * kSortKeys + kLaneKeys - 1], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  int32_t* head = a.qh + kQHLaneBase + list * kQHStride;
+  uint32_t S0 = 0, S1 = 0, S2 = 0, S3 = 0;  // per target base: the five scores as 6-bit fields
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    S0 |= (uint32_t)(o.mat[0 * 5 + q] & 63) << (6 * q);
+    S1 |= (uint32_t)(o.mat[1 * 5 + q] & 63) << (6 * q);
+    S2 |= (uint32_t)(o.mat[2 * 5 + q] & 63) << (6 * q);
+    S3 |= (uint32_t)(o.mat[3 * 5 + q] & 63) << (6 * q);
+  }
+  const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
+  // the task (seed) and its extend_seed state
+  int pos = -1, qbeg = 0, len = 0, lq = 0, phase = 4;
+  int64_t rbeg = 0, wlo = 0, whi = 0, qoff = 0, rb = 0, re = 0;
+  int score = 0, truesc = 0, qb = 0, qe = 0, sc0 = 0, aw0 = 0, aw1 = 0, cells = 0, rows = 0, calls = 0;
+  // the current ksw_extend2 call
+  bool incall = false, alive = true;
+  int qlen = 0, tlen = 0, h0 = 0, w = 0, i = 0, lo = 0, hi = 0;
+  int best = 0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0;
+  // the target row's base of row i: pac position f = f0 + fd * i of one strand
+  // (rev: complemented); its byte and the next one in the walk are held, the
+  // one after is loaded when the walk enters a new byte (4 rows ahead)
+  int64_t f0 = 0, fcur = 0;
+  int fd = 1;
+  bool rev = false;
+  uint32_t tb0 = 0, tb1 = 0;
+  const uint32_t* const seqw = reinterpret_cast<const uint32_t*>(b.seq);
+  const int64_t seq_last_w = (b.seq_off[b.n_reads] - 1) >> 2;
+  long long spec_cells = 0;
+  for (;;) {
+    if (alive && !incall && phase >= 4) {  // the seed is done (or none yet): store it, take the next
+      if (pos >= 0) {
+        SeedExt e;
+        e.rb = rb;
+        e.re = re;
+        e.qb = qb;
+        e.qe = qe;
+        e.score = score;
+        e.truesc = truesc;
+        e.w = aw0 > aw1 ? aw0 : aw1;
+        e.cells = cells;
+        e.rows = rows;
+        e.calls = calls + 1;  // + 1: a computed slot is never all-zero
+        a.ext[pos] = e;
+        spec_cells += cells;
+        pos = -1;
+      }
+      const int m = wave_append(head, true);
+      if (m >= n_lane) {
+        alive = false;
+      } else {
+        const int2 tk = tl[m];
+        pos = tk.x;
+        const int c = tk.y;
+        const int rd = a.chain_read[c];
+        const bwagpu_seed_t s = a.prog[pos];
+        const ChainWin cw = a.win[c];
+        qoff = b.seq_off[rd];
+        lq = (int)(b.seq_off[rd + 1] - qoff);
+        rbeg = s.rbeg;
+        qbeg = s.qbeg;
+        len = s.len;
+        wlo = cw.lo;
+        whi = cw.hi;
+        const int qlenR = lq - (qbeg + len);
+        phase = qbeg != 0 ? 0 : (qlenR != 0 ? 2 : 4);
+        score = qbeg != 0 ? -1 : len * o.a;  // bwamem.c:753
+        truesc = score;
+        qb = 0;
+        qe = lq;
+        sc0 = 0;
+        aw0 = aw1 = o.w;
+        rb = rbeg;
+        re = rbeg + len;
+        cells = rows = calls = 0;
+      }
+    }
+    if (alive && !incall && phase < 4) {  // set up the next ksw_extend2 call of the seed
+      const bool left = phase < 2;
+      const int t = phase & 1;
+      const int qlenR = lq - (qbeg + len);
+      qlen = left ? qbeg : qlenR;
+      const int64_t x0 = left ? rbeg - 1 : rbeg + len;
+      tlen = left ? (int)(rbeg - wlo) : (int)(whi - x0);
+      rev = x0 >= ref.l_pac;  // the window lies on one strand (finish_window)
+      f0 = rev ? (ref.l_pac << 1) - 1 - x0 : x0;
+      fd = (rev ? -1 : 1) * (left ? -1 : 1);
+      fcur = f0 >> 2;
+      tb0 = pac_byte(ref, fcur);
+      tb1 = pac_byte(ref, fcur + fd);
+      const int qa = left ? qbeg - 1 : qbeg + len, qd = left ? -1 : 1;
+      const int eb = left ? o.pen_clip5 : o.pen_clip3;
+      if (t == 0) sc0 = score;
+      h0 = left ? len * o.a : sc0;
+      w = o.w << t;
+      if (left) aw0 = w;
+      else aw1 = w;
+      const int mi = band_cap_dev(qlen, o.max_mat, eb, o.o_ins, e_ins);
+      const int md = band_cap_dev(qlen, o.max_mat, eb, o.o_del, e_del);
+      w = min(w, min(mi, md));
+      // the query's score shifts: its bytes [first, first + qlen) of seq in
+      // (kLaneQ + 4) / 4 + 1 word loads issued together (not one dependent byte
+      // load per column), then column j <- byte qa + qd * j
+      {
+        const int64_t first = qoff + (left ? qa - (qlen - 1) : qa);
+        const int64_t w0 = first >> 2;
+        const int sh0 = (int)(first & 3);
+        constexpr int NW = (kLaneQ + 4) / 4 + 1;
+        uint32_t wv[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) wv[k] = 4 * k < sh0 + qlen ? seqw[min(w0 + k, seq_last_w)] : 0u;
+#pragma unroll
+        for (int t = 0; t < 4 * NW; ++t) {
+          const int u = t - sh0;  // byte first + u
+          const int j = qd > 0 ? u : qlen - 1 - u;
+          if (u >= 0 && u < qlen) qs[64 * j] = (uint8_t)(6 * ((wv[t >> 2] >> (8 * (t & 3))) & 0xffu));
+        }
+      }
+      // eh row -1 (ksw.c:392-395)
+      for (int j = 0; j <= qlen; ++j) eh[64 * j] = (uint32_t)(j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0));
+      best = h0;
+      bi = bj = ei = -1;
+      esc = -1;
+      off = 0;
+      lo = 0;
+      hi = qlen;
+      i = 0;
+      incall = true;
+    }
+    if (!__builtin_amdgcn_ballot_w64(alive)) break;
+    if (incall) {  // one DP row of the lane's call (oracle/ksw_ext.c's loop body)
+      bool end = i >= tlen;
+      if (!end) {
+        const int64_t fp = f0 + (int64_t)fd * i;
+        if ((fp >> 2) != fcur) {  // entered the next byte: shift, load the one after
+          fcur = fp >> 2;
+          tb0 = tb1;
+          tb1 = pac_byte(ref, fcur + fd);
+        }
+        const int bse = (int)(tb0 >> ((~(int)fp & 3) << 1)) & 3;
+        const int t = rev ? 3 - bse : bse;
+        const uint32_t S = t == 0 ? S0 : (t == 1 ? S1 : (t == 2 ? S2 : S3));
+        lo = max(lo, i - w);
+        hi = min(min(hi, i + w + 1), qlen);
+        int left = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
+        int f = 0, rk = -1;
+        const int l0 = min(lo, kLaneQ);  // lo > qlen only on an empty last row
+        uint32_t hw = eh[64 * l0];       // column j's words are read one column ahead
+        int q6 = qs[64 * l0];
+        for (int j = lo; j < hi; ++j) {
+          const uint32_t hwn = eh[64 * (j + 1)];  // j + 1 <= qlen <= kLaneQ: in the lane's rows
+          const int q6n = qs[64 * (j + 1)];
+          int mv = (int)(hw & 0xffffu);
+          const int ev = (int)(hw >> 16);
+          const int sc = __builtin_amdgcn_sbfe((int)S, q6, 6);
+          mv = mv ? mv + sc : 0;
+          const int h = max(max(mv, ev), f);
+          rk = max(rk, (h << 10) | j);  // ties -> the last column (ksw.c:436-437)
+          const int en = max(max(ev - e_del, mv - oe_del), 0);
+          f = max(max(f - e_ins, mv - oe_ins), 0);
+          eh[64 * j] = (uint32_t)left | ((uint32_t)en << 16);
+          left = h;
+          hw = hwn;
+          q6 = q6n;
+        }
+        eh[64 * hi] = (uint32_t)left;  // {H(i, hi-1), 0}
+        cells += max(hi - lo, 0);
+        rows += 1;
+        if (max(lo, hi) == qlen) {  // ksw.c:450-453
+          if (!(esc > left)) ei = i;
+          esc = max(esc, left);
+        }
+        const int rmax = rk >> 10, rarg = rk & 1023;
+        if (rmax <= 0) {
+          end = true;
+        } else if (rmax > best) {
+          best = rmax;
+          bi = i;
+          bj = rarg;
+          off = max(off, abs(rarg - i));
+        } else if (o.zdrop > 0) {
+          const int di = i - bi, dj = rarg - bj;
+          const int drop = di > dj ? best - rmax - (di - dj) * e_del : best - rmax - (dj - di) * e_ins;
+          end = drop > o.zdrop;
+        }
+        if (!end) {  // the zero-trimmed band (ksw.c:466-469)
+          int j = lo;
+          while (j < hi && eh[64 * j] == 0u) ++j;
+          lo = j;
+          j = hi;
+          while (j >= lo && eh[64 * j] == 0u) --j;
+          hi = min(j + 2, qlen);
+          end = ++i >= tlen;
+        }
+      }
+      if (end) {  // the call's result -> extend_seed (bwamem.c:717-792)
+        incall = false;
+        calls += 1;
+        const bool left = phase < 2;
+        const int t = phase & 1;
+        const int qlenR = lq - (qbeg + len);
+        const int aw = o.w << t;
+        const int eb = left ? o.pen_clip5 : o.pen_clip3;
+        const int prev = score;
+        score = best;
+        if (t == 0 && !(score == prev || off < (aw >> 1) + (aw >> 2))) {
+          phase += 1;  // the band retry
+        } else {
+          const bool local = esc <= 0 || esc <= score - eb;
+          if (left) {
+            qb = local ? qbeg - (bj + 1) : 0;
+            rb = rbeg - (local ? bi + 1 : ei + 1);
+            truesc = local ? score : esc;
+            phase = qlenR != 0 ? 2 : 4;
+          } else {
+            qe = local ? qbeg + len + bj + 1 : lq;
+            re = (rbeg + len) + (local ? bi + 1 : ei + 1);
+            truesc = truesc + (local ? score : esc) - sc0;
+            phase = 4;
+          }
+        }
+      }
+    }
+  }
+  if (spec_cells) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
 // Task order for the pair kernel: the two seeds a wave takes should need the
 // same phases for about as long — a half whose seed has no left side, or a
 // much shorter one, idles while the other runs (EXEC).  A counting sort of
@@ -3178,15 +3448,19 @@ static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size
 // per block and key to reserve the block's range).  Claims then take entries
 // 8 apart in the sorted list (the sharded queue), which have about the same
 // key.  The order changes nothing but which seeds share a wave.
-__device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, int2 tk) {
+__device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, int2 tk, int lane) {
   const bwagpu_seed_t s = a.prog[tk.x];
   const int rd = a.chain_read[tk.y];
   const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
   const int ql = min(s.qbeg, 255), qr = min(max(lq - s.qbeg - s.len, 0), 255);
-  return (ql >> 3) << 5 | (qr >> 3);
+  const int k = (ql >> 3) << 5 | (qr >> 3);
+  if (!lane) return k;
+  // the lane kernel's tasks first, the larger ones first (LPT order)
+  if (ql <= kLaneQ && qr <= kLaneQ) return (kLaneKeys - 1) - ((ql >> 3) + (qr >> 3));
+  return min(k + kLaneKeys - ((kLaneQ + 1) >> 3), kSortKeys - 1);  // k >= (kLaneQ + 1) / 8 here
 }
 
-__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round, int lane) {
   __shared__ int hist[kSortKeys];
   const int list = round * kSpecBins + (int)blockIdx.y;
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
@@ -3196,7 +3470,7 @@ __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, i
   const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
   const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
   const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
-  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) atomicAdd(&hist[pair_key(b, a, tl[i])], 1);
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) atomicAdd(&hist[pair_key(b, a, tl[i], lane)], 1);
   __syncthreads();
   for (int k = threadIdx.x; k < kSortKeys; k += 256)
     if (hist[k]) atomicAdd(&gh[k], hist[k]);
@@ -3228,7 +3502,7 @@ __global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
   }
 }
 
-__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round, int lane) {
   __shared__ int cnt[kSortKeys];
   const int list = round * kSpecBins + (int)blockIdx.y;
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
@@ -3250,7 +3524,7 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
       keys[m] = -1;
       if (i < i1) {
         tk[m] = tl[i];
-        keys[m] = pair_key(b, a, tk[m]);
+        keys[m] = pair_key(b, a, tk[m], lane);
         rank[m] = atomicAdd(&cnt[keys[m]], 1);
       }
     }
@@ -3283,6 +3557,22 @@ static int ext_pair_mode() {
   return v;
 }
 static bool ext_pair_enabled() { return ext_pair_mode() != 0; }
+// Short tasks one per lane (spec_extl_kernel) beside the pair kernel, on sorted
+// lists only.  BWAGPU_EXT_LANE: 0 (default) = off, 1 = before the pair kernel
+// on the same stream, 2 = concurrently on the side stream (A/B: DESIGN.md §3).
+static int ext_lane_mode() {
+  static const int v = [] {
+    const char* e = getenv("BWAGPU_EXT_LANE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+// the lane kernel's 6-bit score fields need every mat entry in [-32, 31]
+static bool lane_scores_ok(const DevOpt& o) {
+  for (int k = 0; k < 25; ++k)
+    if (o.mat[k] < -32 || o.mat[k] > 31) return false;
+  return true;
+}
 
 // ============================================================ FPGA wire format
 // bwagpu_sw_stream (include/bwagpu.h).  Lane per read record: the record's
@@ -4257,25 +4547,49 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const bool pair = ext_pair_enabled();
   const size_t lds2 = ext2_lds(tb_bytes);
   const int sorted = ext_pair_mode() == 2 ? 1 : 0;
+  const int lmode = pair && sorted && lane_scores_ok(o) ? ext_lane_mode() : 0;
+  const int lane = lmode ? 1 : 0;
   if (pair && sorted) {
-    hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
+    hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round, lane);
     hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
-    hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
+    hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round, lane);
   }
+  // the lane kernel of list `li` on the side stream (mode 2) or on st (mode 1)
+  const bool conc = lmode == 2 && ss.side;
+  const int nbl = lane ? resident_blocks(spec_extl_kernel, kLaneLds) : 0;
+  auto lane_launch = [&](int li) {
+    if (conc) {
+      (void)hipEventRecord(ss.fork, st);
+      (void)hipStreamWaitEvent(ss.side, ss.fork, 0);
+    }
+    hipLaunchKernelGGL(spec_extl_kernel, dim3(nbl), dim3(64), kLaneLds, conc ? ss.side : st, o, ref, b, a, li);
+  };
+  auto lane_join = [&]() {
+    if (conc) {
+      (void)hipEventRecord(ss.join, ss.side);
+      (void)hipStreamWaitEvent(st, ss.join, 0);
+    }
+  };
   int nb = pair ? resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2) : resident_blocks(spec_ext_kernel<3>, lds);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
+  if (lane) lane_launch(l + 0);
   if (pair)
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 0, tb_bytes, sorted);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 0,
+                       tb_bytes, sorted, lane);
   else
     hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
+  if (lane) lane_join();
   if (prof) {
     (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
     *ss.pool_used += 2;
   }
   if (pair) {
     nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 1, tb_bytes, sorted);
+    if (lane) lane_launch(l + 1);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 1,
+                       tb_bytes, sorted, lane);
+    if (lane) lane_join();
   } else {
     nb = resident_blocks(spec_ext_kernel<4>, lds);
     hipLaunchKernelGGL(spec_ext_kernel<4>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 1, tb_bytes);
