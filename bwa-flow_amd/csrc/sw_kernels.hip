@@ -574,6 +574,14 @@ __device__ __forceinline__ ExtOut extend_wave_blk(const DevOpt& o, int qlen, con
   return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
 }
 
+// extend_pair's band trim: 1 (default) = DPP min/max reductions over each
+// half, 0 = a ballot per row and readlanes of the half's first/last lane
+// (same-box A/B, DESIGN.md §3: equal stage throughput at 96 VGPRs, 3-4 %
+// longer launches)
+#ifndef BWAGPU_TRIM_DPP
+#define BWAGPU_TRIM_DPP 1
+#endif
+
 // CD is uniform per call (qlen is): one compiled body per segment count
 // (CD 2..4 on blocked columns with -DBWAGPU_BLK=1: bit-exact, measured slower)
 #ifndef BWAGPU_BLK
@@ -797,9 +805,29 @@ __device__ __forceinline__ ExtOut extend_pair(const DevOpt& o, int qlen, const u
     const int lo_l = min(max(lo - j0, 0), 31), hi_l = min(max(hix, 0), 31);
     const uint32_t mf = nzm & ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);   // [lo, hi)
     const uint32_t ml = mf | (nzm & ((unsigned)hix < (unsigned)CPL ? 1u << hix : 0u));  // + column hi
+#if BWAGPU_TRIM_DPP
     int cl = mf ? j0 + (int)__builtin_ctz(mf) : 0x7fff;
     int ch = ml ? j0 + 31 - (int)__builtin_clz(ml) : -1;
     row_minmax(cl, ch);
+#else
+    // the first / last non-zero column of [lo, hi] per half: the half's first /
+    // last lane holding one (a ballot), then that lane's first / last slot
+    // (readlane).  The first one is taken over [lo, hi] rather than [lo, hi):
+    // nlo = min(cl, hi) is the same either way.
+    int cl, ch;
+    {
+      const int fl = j0 + (int)__builtin_ctz(ml | 0x80000000u), ll = j0 + 31 - (int)__builtin_clz(ml | 1u);
+      const uint64_t bm = __builtin_amdgcn_ballot_w64(ml != 0u);
+      const uint32_t m0 = (uint32_t)bm, m1 = (uint32_t)(bm >> 32);
+      const int cl0 = m0 ? __builtin_amdgcn_readlane(fl, __builtin_ctz(m0 | 0x80000000u)) : 0x7fff;
+      const int ch0 = m0 ? __builtin_amdgcn_readlane(ll, 31 - __builtin_clz(m0 | 1u)) : -1;
+      const int cl1 = m1 ? __builtin_amdgcn_readlane(fl, 32 + __builtin_ctz(m1 | 0x80000000u)) : 0x7fff;
+      const int ch1 = m1 ? __builtin_amdgcn_readlane(ll, 63 - __builtin_clz(m1 | 1u)) : -1;
+      const bool h1 = (threadIdx.x & 32) != 0;
+      cl = h1 ? cl1 : cl0;
+      ch = h1 ? ch1 : ch0;
+    }
+#endif
     if (i > 0) {
       const int rkr = half_max(rkp);
       if (row_end(rkr, vi - 1)) {
@@ -807,8 +835,10 @@ __device__ __forceinline__ ExtOut extend_pair(const DevOpt& o, int qlen, const u
         break;
       }
     }
+#if BWAGPU_TRIM_DPP
     cl = half_min(cl);
     ch = half_max(ch);
+#endif
     const int nlo = min(cl, hi);
     const int nhi = min(max(ch, nlo - 1) + 2, qlen);
     rkp = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
@@ -3557,6 +3587,17 @@ static int ext_pair_mode() {
   return v;
 }
 static bool ext_pair_enabled() { return ext_pair_mode() != 0; }
+// BWAGPU_EXT2_GRID_PCT: the pair kernel's grid as a percentage of the
+// resident capacity (default 100; the waves pull tasks from the queue, so a
+// smaller grid only lowers its occupancy and leaves CUs to the other stream)
+static int ext2_grid(int nb) {
+  static const int pct = [] {
+    const char* e = getenv("BWAGPU_EXT2_GRID_PCT");
+    const int v = e ? atoi(e) : 100;
+    return v < 10 ? 10 : (v > 100 ? 100 : v);
+  }();
+  return std::max(1, nb * pct / 100);
+}
 // Short tasks one per lane (spec_extl_kernel) beside the pair kernel, on sorted
 // lists only.  BWAGPU_EXT_LANE: 0 (default) = off, 1 = before the pair kernel
 // on the same stream, 2 = concurrently on the side stream (A/B: DESIGN.md §3).
@@ -4575,7 +4616,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
   if (lane) lane_launch(l + 0);
   if (pair)
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 0,
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a, l + 0,
                        tb_bytes, sorted, lane);
   else
     hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
@@ -4587,7 +4628,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   if (pair) {
     nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
     if (lane) lane_launch(l + 1);
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(nb), dim3(kBlock), lds2, st, o, ref, b, a, l + 1,
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a, l + 1,
                        tb_bytes, sorted, lane);
     if (lane) lane_join();
   } else {
