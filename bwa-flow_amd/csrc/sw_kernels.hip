@@ -3587,16 +3587,31 @@ static int ext_pair_mode() {
   return v;
 }
 static bool ext_pair_enabled() { return ext_pair_mode() != 0; }
-// BWAGPU_EXT2_GRID_PCT: the pair kernel's grid as a percentage of the
-// resident capacity (default 100; the waves pull tasks from the queue, so a
-// smaller grid only lowers its occupancy and leaves CUs to the other stream)
+// The pair kernel's grid: its waves pull tasks from the queue, so the grid
+// only sets its occupancy.  Default: 2 workgroups per CU (8 waves per CU, 2
+// per SIMD) instead of the resident capacity (5 per SIMD): the batch on the
+// other caller stream (the bench's ping-pong) and this batch's selection
+// kernels keep the rest, and an even count per CU beats an uneven one.
+// Same-box sweep: capacity 19.87, 60 % 20.74, 50 % 20.66,
+// 2/CU (40 %) 21.74, 30 % 20.16, 1/CU 19.72 Mreads/s.
+// BWAGPU_EXT2_GRID_PCT (percent of capacity) or BWAGPU_EXT2_BLOCKS_PER_CU override.
 static int ext2_grid(int nb) {
   static const int pct = [] {
     const char* e = getenv("BWAGPU_EXT2_GRID_PCT");
-    const int v = e ? atoi(e) : 100;
-    return v < 10 ? 10 : (v > 100 ? 100 : v);
+    const int v = e ? atoi(e) : 0;
+    return v <= 0 ? 0 : (v < 10 ? 10 : (v > 100 ? 100 : v));
   }();
-  return std::max(1, nb * pct / 100);
+  if (pct) return std::max(1, nb * pct / 100);
+  static const int per_cu = [] {
+    const char* e = getenv("BWAGPU_EXT2_BLOCKS_PER_CU");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : v;
+  }();
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    return nb;
+  return std::max(1, std::min(nb, per_cu * ncu));
 }
 // Short tasks one per lane (spec_extl_kernel) beside the pair kernel, on sorted
 // lists only.  BWAGPU_EXT_LANE: 0 (default) = off, 1 = before the pair kernel
