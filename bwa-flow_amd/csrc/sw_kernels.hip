@@ -4565,6 +4565,20 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
   if constexpr (WRITE) block_stats<64>(tl, a.stats);
 }
 
+// BWAGPU_LIGHT_BLOCKS_PER_CU: spec_select_light's grid in workgroups per CU
+// (0 = the resident capacity)
+static int light_grid(int nb) {
+  static const int per_cu = [] {
+    const char* e = getenv("BWAGPU_LIGHT_BLOCKS_PER_CU");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  int dev = 0, ncu = 0;
+  if (!per_cu || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    return nb;
+  return std::max(1, std::min(nb, per_cu * ncu));
+}
+
 // The two selection shapes of one pass: heavy reads on `side` (when given)
 // concurrently with the light reads on `st`; `st` continues once both are done.
 template <int MODE>
@@ -4578,7 +4592,7 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
   }
   if (MODE != SEL_REDO) {
     const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
-    const int nb = resident_blocks(spec_select_light<MODE>, lds);
+    const int nb = light_grid(resident_blocks(spec_select_light<MODE>, lds));
     hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
   }
   if (MODE != SEL_REDO) {  // heavy reads with pair matrices: all pairs at once, then one scan per read
