@@ -1463,6 +1463,8 @@ int bwagpu_debug_fail_wait(bwagpu_ctx_t* ctx, int after_n_waits, int code) {
   return BWAGPU_OK;
 }
 
+int bwagpu_debug_ext_lane(int mode) { return set_ext_lane_mode(mode); }
+
 int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   if (!ctx || !out) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");

@@ -226,6 +226,10 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
 // LDS bytes per workgroup of the largest spec launch; regions the redo pass
 // holds in LDS for target rows of tb_bytes (must stay > 0)
 size_t spec_select_lds(int tb_bytes);
+// the lane kernel for short extension tasks (spec_extl_kernel): 0 off, 1 before
+// the pair kernel, 2 beside it on the side stream; process-wide; returns the
+// previous mode (mode < 0: query only)
+int set_ext_lane_mode(int mode);
 int spec_redo_cap(int tb_bytes);
 
 // ---------------------------------------------------------------- FPGA wire format

@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <tuple>
 
@@ -3595,7 +3596,7 @@ static bool ext_pair_enabled() { return ext_pair_mode() != 0; }
 // Same-box sweep: capacity 19.87, 60 % 20.74, 50 % 20.66,
 // 2/CU (40 %) 21.74, 30 % 20.16, 1/CU 19.72 Mreads/s.
 // BWAGPU_EXT2_GRID_PCT (percent of capacity) or BWAGPU_EXT2_BLOCKS_PER_CU override.
-static int ext2_grid(int nb) {
+static int ext2_grid(int nb, int round) {
   static const int pct = [] {
     const char* e = getenv("BWAGPU_EXT2_GRID_PCT");
     const int v = e ? atoi(e) : 0;
@@ -3607,21 +3608,37 @@ static int ext2_grid(int nb) {
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : v;
   }();
+  static const int per_cu_b = [] {  // rounds B and C (BWAGPU_EXT2_BLOCKS_PER_CU_B; default: the same)
+    const char* e = getenv("BWAGPU_EXT2_BLOCKS_PER_CU_B");
+    const int v = e ? atoi(e) : 0;
+    return v < 0 ? 0 : v;
+  }();
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
     return nb;
-  return std::max(1, std::min(nb, per_cu * ncu));
+  const int k = round > 0 && per_cu_b ? per_cu_b : per_cu;
+  return std::max(1, std::min(nb, k * ncu));
 }
 // Short tasks one per lane (spec_extl_kernel) beside the pair kernel, on sorted
 // lists only.  BWAGPU_EXT_LANE: 0 (default) = off, 1 = before the pair kernel
 // on the same stream, 2 = concurrently on the side stream (A/B: DESIGN.md §3).
+static std::atomic<int> g_ext_lane{-1};  // -1: not read from the environment yet
 static int ext_lane_mode() {
-  static const int v = [] {
+  int v = g_ext_lane.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = getenv("BWAGPU_EXT_LANE");
-    return e ? atoi(e) : 0;
-  }();
+    int want = e ? atoi(e) : 0;
+    want = want < 0 ? 0 : (want > 2 ? 2 : want);
+    g_ext_lane.compare_exchange_strong(v, want);
+    v = g_ext_lane.load(std::memory_order_relaxed);
+  }
   return v;
+}
+int set_ext_lane_mode(int mode) {  // process-wide; -> the previous mode (mode < 0: query only)
+  const int prev = ext_lane_mode();
+  if (mode >= 0) g_ext_lane.store(mode > 2 ? 2 : mode, std::memory_order_relaxed);
+  return prev;
 }
 // the lane kernel's 6-bit score fields need every mat entry in [-32, 31]
 static bool lane_scores_ok(const DevOpt& o) {
@@ -4645,7 +4662,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
   if (lane) lane_launch(l + 0);
   if (pair)
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a, l + 0,
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb, round)), dim3(kBlock), lds2, st, o, ref, b, a, l + 0,
                        tb_bytes, sorted, lane);
   else
     hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
@@ -4657,7 +4674,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   if (pair) {
     nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
     if (lane) lane_launch(l + 1);
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a, l + 1,
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb, round)), dim3(kBlock), lds2, st, o, ref, b, a, l + 1,
                        tb_bytes, sorted, lane);
     if (lane) lane_join();
   } else {

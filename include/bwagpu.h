@@ -503,6 +503,11 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
    score, truesc, w, cells, rows, calls + 1; calls == 0: not computed) of the
    last device-entry batch on `stream`, n = its seed count */
 int bwagpu_debug_spec_ext(bwagpu_ctx_t *ctx, void *stream, void *host_out, int32_t n);
+/* tuning / tests (process-wide): the short extension tasks one seed per lane
+    — 0 off (the default, or BWAGPU_EXT_LANE), 1 before the
+   two-seeds-per-wave kernel, 2 beside it; returns the previous mode, mode < 0
+   only queries.  Results do not depend on it. */
+int bwagpu_debug_ext_lane(int mode);
 int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
 
 #ifdef __cplusplus
