@@ -4110,6 +4110,15 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
 // A seed that must be extended but has no result: SEL_EMULATE marks it a
 // round-B task (pending: neither extended nor skipped, as in the per-seed
 // form); SEL_FINAL sends the read to the redo pass.
+// A misprediction in the final pass of a light read (a seed the replay must
+// extend has no result: ~10-20 per C2 batch) is extended inline
+// (BWAGPU_LIGHT_INLINE=1, the default), which takes the kernel to 129 VGPRs
+// (3 waves per SIMD).  0 sends it to round C + the redo pass like one of a
+// longer read (82 VGPRs): bit-exact, but 19.8-19.9 vs 21.6-21.7 Mreads/s on
+// C2 (C3 1.04 vs 1.12-1.20 ms per batch), DESIGN.md §3.
+#ifndef BWAGPU_LIGHT_INLINE
+#define BWAGPU_LIGHT_INLINE 1
+#endif
 template <int MODE>
 #ifndef BWAGPU_LIGHT_WPE
 #define BWAGPU_LIGHT_WPE 1  // no occupancy cap: 6 waves/SIMD (80 VGPRs, spills) measured 5% slower per batch
@@ -4273,7 +4282,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWA
       const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
       if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
     } else {
-      if (miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
+      if (BWAGPU_LIGHT_INLINE && miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
         const bwagpu_seed_t sm = uni_seed(a.prog[d.s0 + miss]);
         const int cm_id = uni(__shfl(cid, miss, 64));
         ChainWin cw = a.win[d.c0 + cm_id];
@@ -4286,7 +4295,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWA
         __builtin_amdgcn_wave_barrier();
         continue;
       }
-      if (miss >= 0) {  // longer reads: round C + the redo pass (the C = 3 body holds reads <= 192 bp)
+      if (miss >= 0) {  // round C + the redo pass (BWAGPU_LIGHT_INLINE=1: reads > 160 bp only)
         const int list = 2 * kSpecBins + spec_bin(d.lq);
         if (r == miss) {
           const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
