@@ -4605,6 +4605,17 @@ static int light_grid(int nb) {
   return std::max(1, std::min(nb, per_cu * ncu));
 }
 
+// BWAGPU_SCAN_GRID: spec_scan_kernel's grid (one wave per workgroup, a static
+// stride over the heavy reads; default 1024)
+static int scan_grid() {
+  static const int v = [] {
+    const char* e = getenv("BWAGPU_SCAN_GRID");
+    const int g = e ? atoi(e) : 1024;
+    return g < 64 ? 64 : (g > 8192 ? 8192 : g);
+  }();
+  return v;
+}
+
 // The two selection shapes of one pass: heavy reads on `side` (when given)
 // concurrently with the light reads on `st`; `st` continues once both are done.
 template <int MODE>
@@ -4624,7 +4635,7 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
   if (MODE != SEL_REDO) {  // heavy reads with pair matrices: all pairs at once, then one scan per read
     const int nb = resident_blocks(spec_pairs_kernel, 0);
     hipLaunchKernelGGL(spec_pairs_kernel, dim3(nb), dim3(kBlock), 0, hs, o, b, a, MODE == SEL_FINAL ? 1 : 0);
-    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(1024), dim3(64), (size_t)kScanLds + 2 * (size_t)tb_bytes, hs, o,
+    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(scan_grid()), dim3(64), (size_t)kScanLds + 2 * (size_t)tb_bytes, hs, o,
                        ref, b, a, tb_bytes);
   }
   // the rest (no matrix; the redo list): one wave per read, per seed
