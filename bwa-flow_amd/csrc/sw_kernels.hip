@@ -3213,11 +3213,14 @@ static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size
 // of oracle/ksw_ext.c) with its eh[] row in LDS, and walks its own seed through
 // extend_seed (bwamem.c:717-792) as a state machine.  The wave steps every
 // lane's current DP row together; a lane whose seed is done stores its SeedExt
-// and claims the next task at once (wave-aggregated), so lanes never wait for
-// the wave's longest task.  Per DP cell: two LDS reads (the packed H|E word,
-// the query's score shift), one LDS write and ~18 VALU, against one row's
-// scans and reductions per 32 columns in extend_pair: for qlen <= 63 the
-// per-row fixed cost of the wave forms dominates.
+// and claims the next task at once (wave-aggregated), so lanes do not wait
+// for the end of the wave's longest task, only for its widest row.  Per DP
+// cell: two LDS reads (the packed H|E word, the query's score shift), one LDS
+// write and ~18 VALU, against one row's scans and reductions per 32 columns
+// in extend_pair, whose per-row fixed cost dominates at short qlens.
+// Opt-in (BWAGPU_EXT_LANE / bwagpu_debug_ext_lane): a lane runs its seed
+// serially, and the measured launch is set by that latency (61 vs ~270
+// Gcells/s).
 //
 // LDS per wave: eh[j][lane] = H(i-1, j-1) | E(i, j) << 16 (both >= 0 and
 // < 2^16: scores stay below 1024 * max(mat) for reads up to 1023 bp), and
@@ -3226,7 +3229,7 @@ static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size
 // entry in [-32, 31]).  The lane index is the fastest dimension, so lanes at
 // different columns never share an LDS bank for the 32-bit words.
 static_assert(kLaneQ + 1 <= 1024 && (kLaneQ & 7) == 7, "lane kernel: qlen bound");
-constexpr size_t kLaneLds = (size_t)(kLaneQ + 1) * 64 * 5;  // 10240 B per wave (qs has a spare row)
+constexpr size_t kLaneLds = (size_t)(kLaneQ + 1) * 64 * 5;  // 20480 B per wave at kLaneQ 63 (qs has a spare row)
 
 // pac byte p, clamped into the array (l_pac / 4 + 1 bytes): a prefetch past
 // either end of a window is never used
