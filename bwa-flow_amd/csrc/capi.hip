@@ -182,6 +182,7 @@ struct bwagpu_ctx {
   // bwt_extend calls tier 1 spends on a read before tier 2 (one wave per read)
   // takes it: ~p90 of the C2 batch's per-read counts (mean 666, p90 975)
   int seed_budget = 1024;
+  int sup_shift = 32;  // bwagpu_debug_sup_shift: superblock size of the next set_bwt
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
@@ -431,12 +432,15 @@ int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
         return 2;
       }
       lm = std::max(lm, l);
+      // every offset is range-checked BEFORE it indexes: a range may start
+      // anywhere, and a later read's failing check must not come after an
+      // earlier read walked past the caller's arrays
       const int c0 = rco[r], c1 = rco[r + 1];
-      if (c1 < c0) return 3;
+      if (c0 < 0 || c1 < c0 || c1 > b->n_chains) return 3;
       bool bad_seed = false;
       for (int c = c0; c < c1; ++c) {
         const int k0 = cso[c], k1 = cso[c + 1];
-        if (k1 < k0) return 4;
+        if (k0 < 0 || k1 < k0 || k1 > b->n_seeds) return 4;
         for (int k = k0; k < k1; ++k) {  // branch-free accumulation: one test per read
           const bwagpu_seed_t& s = sd[k];
           bad_seed |= (s.qbeg < 0) | (s.len <= 0) | ((int64_t)s.qbeg + s.len > l) | (s.rbeg < 0) | (s.rbeg + s.len > two);
@@ -1556,7 +1560,8 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
   ctx->bwt.bwt = ctx->bwt_words.as<uint32_t>();
   {  // the device occurrence layout (seed.hip: 64-position blocks)
     HIPC(ctx->occ_d.ensure(2 * sizeof(uint4) * (size_t)occ64_blocks(bwt->seq_len)), "hipMalloc");
-    HIPC(ctx->sup_d.ensure(4 * sizeof(uint64_t) * (size_t)occ64_supers(bwt->seq_len)), "hipMalloc");
+    ctx->bwt.sup_shift = ctx->sup_shift;
+    HIPC(ctx->sup_d.ensure(4 * sizeof(uint64_t) * (size_t)occ64_supers(bwt->seq_len, ctx->sup_shift)), "hipMalloc");
     HIPC(hipMemset(ctx->occ_d.p, 0, 2 * sizeof(uint4) * (size_t)occ64_blocks(bwt->seq_len)), "memset");
     hipStream_t st = ctx->slot[0].stream;
     HIPC(launch_build_occ64(ctx->bwt, ctx->occ_d.as<uint4>(), ctx->sup_d.as<uint64_t>(), st), "build_occ64 launch");
@@ -1720,6 +1725,12 @@ extern "C" int bwagpu_debug_seed_budget(bwagpu_ctx_t* ctx, int32_t budget) {
   return BWAGPU_OK;
 }
 
+extern "C" int bwagpu_debug_sup_shift(bwagpu_ctx_t* ctx, int32_t shift) {
+  if (!ctx || shift < 7 || shift > 32) return BWAGPU_E_INVAL;  // a superblock is whole 128-position bwa blocks
+  ctx->sup_shift = shift;
+  return BWAGPU_OK;
+}
+
 // The FPGA back end's own job (sw_top, xlnx/XCLAgent.cpp:89-106) on its wire
 // format: the host walks the record chain (one load per read record — the
 // "end" words of packReadData, FPGAPipeline.cpp:258,336) and checks lengths;
@@ -1811,6 +1822,12 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
       !(copt->drop_ratio >= 0))
     return fail(ctx, BWAGPU_E_INVAL, "bad chaining options");
   if (!ctx->bwt.sa) return fail(ctx, BWAGPU_E_INVAL, "no suffix array: pass it to bwagpu_set_bwt");
+  {  // the largest LDS bin's arena (chain.h) needs gfx950's 160 KB per workgroup
+    int lds_max = 0;
+    HIPC(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device), "attribute");
+    if ((size_t)lds_max < lds_arena(kBinCap[kLdsBins - 1]))
+      return fail(ctx, BWAGPU_E_UNSUPPORTED, "device LDS per workgroup is smaller than the chaining arena");
+  }
   int64_t bases = 0;
   int rc = seed_validate(ctx, sopt, n_reads, seq_off, seq, &bases);
   if (rc) return rc;

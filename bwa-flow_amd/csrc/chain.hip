@@ -11,7 +11,8 @@
 // in LDS: each step of the walk is a chain of dependent accesses (~25 per
 // seed), which LDS answers in ~100 cycles where L2 takes several hundred.
 // Reads are binned by their SA position count (LDS arenas for 32 / 128 / 512 /
-// 1664 positions, up to 157 KB); the rare larger reads run the same code on a
+// 1536 positions, kBinCap in chain.h, up to ~154 KB: gfx950's 160 KB LDS;
+// run_chaining refuses a device with less); the rare larger reads run the same code on a
 // global-memory arena.  The kbtree is restated as a B-tree of chain ids with
 // the reference's node search, split and in-order traversal (t = 5): chains
 // with EQUAL positions exist (tandem repeats), and their order — and which of

@@ -15,7 +15,8 @@ struct DevBwt {
   uint64_t seq_len;
   const uint32_t* bwt;   // bwa's layout (bwt.h:46-57): 128-base blocks of 4 uint64 counts + 8 words of 2-bit bases
   const uint4* occ;      // the device layout (build_occ64): 64-base blocks of 32 B, see seed.hip
-  const uint64_t* sup;   // its 64-bit counts per 2^32 positions: 4 per superblock
+  const uint64_t* sup;   // its 64-bit counts per 2^sup_shift positions: 4 per superblock
+  int sup_shift;         // log2 of the superblock size: 32 (a test build of the index may use less, >= 7)
   const uint64_t* sa;    // sampled suffix array (NULL if not uploaded)
   uint64_t sa_mask;      // sa_intv - 1
   int sa_shift;          // log2(sa_intv)
@@ -23,9 +24,10 @@ struct DevBwt {
 
 // the device occurrence layout of a BWT of seq_len positions ($ removed):
 // blocks of 64 positions (2 x uint4 each) and one 4 x uint64 superblock
-// record per 2^32 positions
+// record per 2^shift positions (32 in production; bwagpu_debug_sup_shift
+// lowers it so that small test indexes cross superblock boundaries)
 inline uint64_t occ64_blocks(uint64_t seq_len) { return (seq_len + 63) / 64 + 1; }
-inline uint64_t occ64_supers(uint64_t seq_len) { return (seq_len >> 32) + 2; }
+inline uint64_t occ64_supers(uint64_t seq_len, int shift) { return (seq_len >> shift) + 2; }
 // builds b.occ / b.sup from b.bwt (every other field of b set)
 hipError_t launch_build_occ64(const DevBwt& b, uint4* occ, uint64_t* sup, hipStream_t st);
 

@@ -31,12 +31,12 @@ static_assert(sizeof(Ivl) == sizeof(bwagpu_intv_t), "interval layout");
 // uint64 counts and 8 words of 2-bit bases: 64 B fetched and 8 words counted
 // per lookup.  bwagpu_set_bwt re-lays it out once (build_occ64_kernel): per
 // 64 positions one 32-byte record {uint32 count of A/C/G/T before the block,
-// relative to its 2^32-position superblock; 4 words of bases}, plus 4 uint64
+// relative to its 2^32-position superblock (sup_shift); 4 words of bases}, plus 4 uint64
 // counts per superblock.  A lookup is one 32-byte fetch and 4 words counted
 // (three equality-popcounts each, A from the position count); the counts are
 // bwa's exactly (bwt_occ4, bwt.c:169-187).
 __device__ __forceinline__ void block_counts64(uint64_t k, const uint4 hdr, const uint4 w4, const uint64_t* sup,
-                                               uint64_t cnt[4]) {
+                                               int sup_shift, uint64_t cnt[4]) {
   const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
   const int nfull = (int)((k & 63) >> 4);
   const uint32_t tail = ~((1u << ((~(uint32_t)k & 15) << 1)) - 1);  // fields 0..(k & 15) of word nfull
@@ -50,7 +50,7 @@ __device__ __forceinline__ void block_counts64(uint64_t k, const uint4 hdr, cons
     c3 += __popc(~(x3 | x3 >> 1) & m);
   }
   const uint32_t c0 = (uint32_t)(k & 63) + 1 - c1 - c2 - c3;
-  const uint64_t* sp = sup + 4 * (k >> 32);
+  const uint64_t* sp = sup + 4 * (k >> sup_shift);
   cnt[0] = sp[0] + hdr.x + c0;
   cnt[1] = sp[1] + hdr.y + c1;
   cnt[2] = sp[2] + hdr.z + c2;
@@ -65,7 +65,7 @@ __device__ __forceinline__ void occ4(const DevBwt& b, uint64_t k, uint64_t cnt[4
   }
   k -= (k >= b.primary);
   const uint4* p = b.occ + 2 * (k >> 6);
-  block_counts64(k, p[0], p[1], b.sup, cnt);
+  block_counts64(k, p[0], p[1], b.sup, b.sup_shift, cnt);
 }
 
 // bwt_2occ4 (bwt.c:189-214): both ends of an interval; when they fall in the
@@ -86,8 +86,8 @@ __device__ __forceinline__ void occ4x2(const DevBwt& b, uint64_t k, uint64_t l, 
     d0 = pl[0];
     d1 = pl[1];
   }
-  block_counts64(kk, a0, a1, b.sup, tk);
-  block_counts64(ll, d0, d1, b.sup, tl);
+  block_counts64(kk, a0, a1, b.sup, b.sup_shift, tk);
+  block_counts64(ll, d0, d1, b.sup, b.sup_shift, tl);
 }
 
 // bwt_B0 (bwt.h:86): the base at $-free position x
@@ -101,8 +101,8 @@ __device__ __forceinline__ int base_at(const DevBwt& b, uint64_t x) {
 __global__ void __launch_bounds__(256) build_occ64_kernel(DevBwt b, uint4* __restrict__ occ, uint64_t* __restrict__ sup,
                                                           uint64_t n_blocks, uint64_t n_sup) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_sup) {  // superblock s starts at position s << 32, a bwa block boundary
-    const uint64_t pos = i << 32;
+  if (i < n_sup) {  // superblock s starts at position s << sup_shift, a bwa block boundary
+    const uint64_t pos = i << b.sup_shift;
     const uint64_t* hb = reinterpret_cast<const uint64_t*>(b.bwt + ((pos >> 7) << 4));
     for (int c = 0; c < 4; ++c) sup[4 * i + c] = pos < b.seq_len ? hb[c] : 0;
   }
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) build_occ64_kernel(DevBwt b, uint4* __res
   if (pos >= b.seq_len) return;  // (the spare record is never read)
   const uint32_t* bb = b.bwt + ((pos >> 7) << 4);
   const uint64_t* hb = reinterpret_cast<const uint64_t*>(bb);
-  const uint64_t* hs = reinterpret_cast<const uint64_t*>(b.bwt + (((pos >> 32) << 32 >> 7) << 4));
+  const uint64_t* hs = reinterpret_cast<const uint64_t*>(b.bwt + (((pos >> b.sup_shift) << b.sup_shift >> 7) << 4));
   uint64_t cnt[4] = {hb[0], hb[1], hb[2], hb[3]};
   const int half = (int)((pos >> 6) & 1);
   const uint32_t* w = bb + 8 + 4 * half;
@@ -212,7 +212,7 @@ __device__ __forceinline__ CountsC counts_c(uint64_t k, const uint4 hdr, const u
 
 // the superblock's counts of c and of the bases above c (zero below 2^32)
 __device__ __forceinline__ void sup_c(const DevBwt& b, uint64_t k, int c, uint64_t& eq, uint64_t& gt) {
-  const ulonglong2* sp = reinterpret_cast<const ulonglong2*>(b.sup + 4 * (k >> 32));
+  const ulonglong2* sp = reinterpret_cast<const ulonglong2*>(b.sup + 4 * (k >> b.sup_shift));
   const ulonglong2 s01 = sp[0], s23 = sp[1];
   eq = c == 0 ? s01.x : c == 1 ? s01.y : c == 2 ? s23.x : s23.y;
   gt = (c < 1 ? s01.y : 0ull) + (c < 2 ? s23.x : 0ull) + (c < 3 ? s23.y : 0ull);
@@ -250,7 +250,7 @@ __device__ __forceinline__ Ivl extend_finish(const DevBwt& b, const Ivl& ik, int
   const CountsC ck = counts_c(f.kk, f.a0, f.a1, pe_hi, pe_lo, g_or, g_lo, c);
   const CountsC cl = counts_c(f.ll, f.d0, f.d1, pe_hi, pe_lo, g_or, g_lo, c);
   uint64_t tk = ck.eq, tl = cl.eq, gk = ck.gt & g_on, gl = cl.gt & g_on;
-  if (b.seq_len >> 32) {  // wave-uniform: the BWT has superblocks past the first
+  if (b.seq_len >> b.sup_shift) {  // wave-uniform: the BWT has superblocks past the first
     uint64_t se, sg;
     sup_c(b, f.kk, c, se, sg);
     tk += se;
@@ -1069,7 +1069,7 @@ __global__ void __launch_bounds__(256) bwt_sa_kernel(DevBwt b, int64_t n, const 
 }  // namespace
 
 hipError_t launch_build_occ64(const DevBwt& b, uint4* occ, uint64_t* sup, hipStream_t st) {
-  const uint64_t nb = occ64_blocks(b.seq_len), ns = occ64_supers(b.seq_len);
+  const uint64_t nb = occ64_blocks(b.seq_len), ns = occ64_supers(b.seq_len, b.sup_shift);
   const uint64_t n = nb > ns ? nb : ns;
   hipLaunchKernelGGL(build_occ64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, b, occ, sup, nb, ns);
   return hipGetLastError();

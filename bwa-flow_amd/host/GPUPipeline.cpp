@@ -238,20 +238,21 @@ static void parallel_ranges(int n, F f) {  // f(begin, end) over [0, n) in host_
     f(0, n);
     return;
   }
-  std::atomic<int> left{t - 1};
+  // the count is decremented under the lock: a task touches m / done only while
+  // holding m, and the caller cannot see left == 0 (and unwind this frame)
+  // before the last task has released it
+  int left = t - 1;
   std::mutex m;
   std::condition_variable done;
   for (int k = 1; k < t; ++k)
     HostPool::get().post([&, k] {
       f((int)((int64_t)n * k / t), (int)((int64_t)n * (k + 1) / t));
-      if (left.fetch_sub(1) == 1) {
-        std::lock_guard<std::mutex> g(m);
-        done.notify_all();
-      }
+      std::lock_guard<std::mutex> g(m);
+      if (--left == 0) done.notify_all();
     });
   f(0, (int)((int64_t)n / t));
   std::unique_lock<std::mutex> g(m);
-  done.wait(g, [&] { return left.load() == 0; });
+  done.wait(g, [&] { return left == 0; });
 }
 
 void FlatBatch::pack(const ChainsRecord& rec) {
@@ -480,6 +481,14 @@ void ChainReaper::release(mem_chain_v* chains, int batch_num) {
   cv_.notify_one();
 }
 
+void ChainReaper::hold(bool on) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    held_ = on;
+  }
+  cv_.notify_all();
+}
+
 void ChainReaper::drain() {
   std::unique_lock<std::mutex> g(mu_);
   idle_.wait(g, [this] { return q_.empty() && !busy_; });
@@ -488,7 +497,7 @@ void ChainReaper::drain() {
 void ChainReaper::run() {
   std::unique_lock<std::mutex> g(mu_);
   for (;;) {
-    cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+    cv_.wait(g, [this] { return stop_ || (!q_.empty() && !held_); });
     if (q_.empty()) return;  // stop_ and nothing left
     auto job = q_.front();
     q_.pop_front();

@@ -109,13 +109,16 @@ class ChainReaper {
   // records freed inline because kMaxQueued were already waiting
   int inline_frees() const { return n_inline_.load(); }
   static constexpr size_t kMaxQueued = 4 * BWAGPU_NUM_SLOTS;
+  // tests: while held the thread frees nothing (a reaper that has fallen
+  // behind), so releases past kMaxQueued take the inline path
+  void hold(bool on);
 
  private:
   void run();
   std::mutex mu_;
   std::condition_variable cv_, idle_;
   std::deque<std::pair<mem_chain_v*, int>> q_;
-  bool stop_ = false, busy_ = false, started_ = false;
+  bool stop_ = false, busy_ = false, started_ = false, held_ = false;
   std::atomic<int> n_inline_{0};
   std::thread th_;
 };

@@ -256,6 +256,10 @@ class Engine:
                                               C.byref(n)), "sw_stream")
         return out[:n.value]
 
+    def sup_shift(self, shift: int):
+        """superblock size 2^shift of the occurrence layout the NEXT set_bwt builds (tests; default 32)"""
+        self._check(self.lib.bwagpu_debug_sup_shift(self.ctx, shift), "sup_shift")
+
     def seed_budget(self, budget: int):
         """bwt_extend calls a read gets on one lane before the wave kernel takes it (0: all on waves)"""
         self._check(self.lib.bwagpu_debug_seed_budget(self.ctx, budget), "seed_budget")

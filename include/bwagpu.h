@@ -474,6 +474,14 @@ int bwagpu_seqs2regions(bwagpu_ctx_t *ctx, const bwagpu_seedopt_t *sopt, const b
    read to the wave kernel.  Results do not depend on it. */
 int bwagpu_debug_seed_budget(bwagpu_ctx_t *ctx, int32_t budget);
 
+/* Tests: the device occurrence layout keeps 32-bit counts relative to
+   superblocks of 2^shift positions (default 32: only indexes past 2^32
+   positions, e.g. GRCh38's 6.2 G, have more than one).  A smaller shift
+   (7..32) for the NEXT bwagpu_set_bwt makes a small index cross superblock
+   boundaries, so that the superblock table and the relative counts are
+   exercised on the golden fixtures.  Results do not depend on it. */
+int bwagpu_debug_sup_shift(bwagpu_ctx_t *ctx, int32_t shift);
+
 /* diagnostics: while dev_ptr != NULL every chain2aln launch on this device
    writes 8 x uint32 per read index r at dev_ptr[8r..8r+7]: start and end
    s_memrealtime (100 MHz, lo/hi), DP rows, DP cells, HW_ID, XCC_ID.

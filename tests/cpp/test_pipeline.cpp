@@ -133,6 +133,8 @@ int main(int argc, char** argv) {
     size_t released = 0;
     {
       ChainReaper reaper;
+      const bool held = getenv("TEST_REAPER_HOLD") != nullptr;  // a reaper that has fallen behind
+      if (held) reaper.hold(true);
       std::vector<std::thread> th;
       const int t = std::max(cpu_workers, 1);
       for (int k = 0; k < t; ++k)
@@ -140,6 +142,7 @@ int main(int argc, char** argv) {
           for (size_t i = (size_t)k; i < recs.size(); i += (size_t)t) reaper.release(recs[i].chains, recs[i].batch_num);
         });
       for (auto& x : th) x.join();
+      if (held) reaper.hold(false);
       reaper.drain();
       released = recs.size();
       const size_t heap2 = mallinfo2().uordblks;

@@ -26,9 +26,11 @@ from bwagpu.engine import Engine
 pytestmark = pytest.mark.gpu
 
 
-def make_engine(opt):
+def make_engine(opt, sup_shift=None):
     refd = G.load_ref()
     e = Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
+    if sup_shift is not None:
+        e.sup_shift(sup_shift)
     hdr, words = G.load_seed_bwt()
     sa_intv, sa, _, _ = G.load_seed_sa()
     e.set_bwt(hdr, words, sa, sa_intv)
@@ -68,6 +70,31 @@ def test_filtered_chains_golden(engines, name):
     g = G.load_chain_gold(name)
     got = dev_chains(engines(g["opt"]), g, False)
     assert final_mismatch(got, g["final"]) is None
+
+
+@pytest.mark.parametrize("shift", [9, 16])
+def test_chains_golden_across_superblocks(shift):
+    """the occurrence layout's superblock table and its 32-bit relative counts
+    (seed.hip block_counts64 / sup_c) only come into play past 2^32 positions,
+    i.e. on a human-sized index; with superblocks of 2^shift positions the
+    golden index (~2 M positions) crosses hundreds of them, and every interval
+    and chain must stay the reference's"""
+    from test_chain_oracle import final_mismatch, raw_mismatch
+    eng, key = None, None
+    try:
+        for name in G.CHAIN_GOLD_SETS:
+            g = G.load_chain_gold(name)
+            o = g["opt"]
+            k = (o["a"], o["b"], o["w"], o["o_del"], o["e_del"], o["o_ins"], o["e_ins"])
+            if k != key:
+                if eng is not None:
+                    eng.close()
+                eng, key = make_engine(o, shift), k
+            assert raw_mismatch(dev_chains(eng, g, True), g["raw"]) is None, name
+            assert final_mismatch(dev_chains(eng, g, False), g["final"]) is None, name
+    finally:
+        if eng is not None:
+            eng.close()
 
 
 @pytest.mark.parametrize("name", G.CHAIN_SETS)

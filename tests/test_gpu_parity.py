@@ -152,6 +152,19 @@ def test_error_conditions(refd):
     with pytest.raises(BwaGpuError) as e:
         eng.chain2aln(mal)
     assert e.value.code == abi.E_INVAL
+    # offsets that span their arrays but are not monotone: refused before any
+    # offset indexes past the caller's arrays (read 0 claims chains 0..4 of 2,
+    # chain 0 claims seeds 0..2 of 1)
+    sd = np.zeros(2, abi.SEED_DTYPE)
+    sd["len"] = 1
+    for rco, cso, ns in (([0, 5, 2], [0, 1, 2], 2), ([0, 2, 2], [0, 3, 1], 1)):
+        mal = Batch(np.array([0, 5, 10]), np.zeros(10, np.uint8), np.array(rco, np.int32), np.array(cso, np.int32),
+                    np.zeros(2, np.int32), np.zeros(2, np.float32), sd[:ns])
+        with pytest.raises(BwaGpuError) as e:
+            eng.chain2aln(mal)
+        assert e.value.code == abi.E_INVAL
+    regs, n = eng.chain2aln(sub)  # and the engine still serves
+    assert n.sum() > 0
     eng.close()
 
 

@@ -86,7 +86,24 @@ def test_chain_reaper_frees_every_record(exe, tmp_path, inline):
     # class); a leak would leave about all of built_bytes
     assert info["built_bytes"] > 400_000
     assert info["left_bytes"] < min(256 * 1024, info["built_bytes"] // 2), info
-    assert inline or info["inline_frees"] >= 0
+    # with the reaper off every free is inline and none is counted as a fallback
+    assert not inline or info["inline_frees"] == 0
+
+
+def test_chain_reaper_bounded_queue(exe, tmp_path):
+    """a reaper that has fallen behind (held: it frees nothing) queues at most
+    ChainReaper::kMaxQueued records; every later release frees inline on the
+    releasing thread, and after drain() the heap is back where it started"""
+    d = str(tmp_path)
+    b, _, _ = write_inputs(d, "c1_default")
+    env = dict(os.environ, BWAGPU_CHAIN_REAPER="1", TEST_REAPER_HOLD="1")
+    p = subprocess.run([exe, d, "reaper", "37", "4"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr
+    info = json.loads(p.stdout.strip().splitlines()[-1])
+    k_max_queued = 4 * 4  # 4 * BWAGPU_NUM_SLOTS
+    assert info["records"] == -(-b.n_reads // 37) > k_max_queued
+    assert info["inline_frees"] == info["records"] - k_max_queued, info
+    assert info["left_bytes"] < min(256 * 1024, info["built_bytes"] // 2), info
 
 
 @pytest.mark.gpu
