@@ -49,17 +49,6 @@ struct DevBuf {  // grow-only device buffer
   T* as() const { return (T*)p; }
 };
 
-// BWAGPU_PINNED=nc: the input staging buffers are non-coherent (coarse-grained)
-// pinned memory instead of the default coherent kind (A/B of the H2D copy's
-// host cost)
-unsigned pinned_in_flags() {
-  static const unsigned f = [] {
-    const char* e = getenv("BWAGPU_PINNED");
-    return (e && strcmp(e, "nc") == 0) ? (unsigned)hipHostMallocNonCoherent : (unsigned)hipHostMallocDefault;
-  }();
-  return f;
-}
-
 struct HostBuf {  // grow-only pinned host buffer
   void* p = nullptr;
   size_t cap = 0;
@@ -186,10 +175,6 @@ struct bwagpu_ctx {
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
-  // BWAGPU_SUBMIT_PROF=1: host time of submit's parts, printed at destroy
-  double sp_check = 0, sp_alloc = 0, sp_copy = 0, sp_h2d = 0, sp_enq = 0, sp_d2h = 0;
-  int64_t sp_n = 0;
-  int sp_on = -1;
   // bwagpu_prof_*: event pairs around the dominant extension launches
   std::vector<hipEvent_t> prof_ev;
   int prof_used = 0;
@@ -333,10 +318,6 @@ int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, 
 
 void destroy_ctx(bwagpu_ctx_t* ctx) {
   if (!ctx) return;
-  if (ctx->sp_on > 0 && ctx->sp_n)
-    fprintf(stderr, "[submit prof] %ld submits, ms each: check %.3f copy %.3f h2d %.3f enqueue %.3f d2h %.3f\n",
-            (long)ctx->sp_n, 1e3 * ctx->sp_check / ctx->sp_n, 1e3 * ctx->sp_copy / ctx->sp_n,
-            1e3 * ctx->sp_h2d / ctx->sp_n, 1e3 * ctx->sp_enq / ctx->sp_n, 1e3 * ctx->sp_d2h / ctx->sp_n);
   (void)hipSetDevice(ctx->device);
   for (auto& s : ctx->slot) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -483,23 +464,6 @@ int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
   return BWAGPU_OK;
 }
 
-// BWAGPU_H2D=kernel: the staged batch pulled into HBM by the device itself
-// (the pinned buffer is mapped) — one launch in place of the runtime's copy
-// call.  Measured and not the default: the copy call's host cost goes away,
-// but the runtime then blocks in the D2H copy call that follows (submit
-// 3.7 vs 9.1 Mreads/s end to end)
-__global__ void __launch_bounds__(256) pull_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
-}
-
-bool h2d_by_kernel() {
-  static const int v = [] {
-    const char* e = getenv("BWAGPU_H2D");
-    return (e && strcmp(e, "kernel") == 0) ? 1 : 0;
-  }();
-  return v != 0;
-}
-
 // LDS row-buffer bytes per group for reads up to lq_max (see rows_needed)
 int tb_bytes_for(const DevOpt& o, int lq_max) {
   const int eb = std::max(o.pen_clip5, o.pen_clip3);
@@ -518,21 +482,12 @@ bool use_read_kernels() {
   return e && (strcmp(e, "fast") == 0 || strcmp(e, "read") == 0);
 }
 
-bool use_grp_kernels() {
-  // BWAGPU_C2A_GRP=1: the 16-lane group kernels for reads <= 256 bp instead of
-  // the wave-per-read kernels (bit-identical; slower on C2 — DESIGN.md §3)
-  const char* eg = getenv("BWAGPU_C2A_GRP");
-  return eg && eg[0] == '1';
-}
-
 // dynamic LDS bytes of variant v's launch for reads up to lq_max
 size_t variant_lds(const DevOpt& o, int v, int lq_max) {
   const Variant& vk = kVariants[v];
-  const int lqv = std::min(lq_max, vk.kind == VK_GRP ? 256 : vk.max_len());
+  const int lqv = std::min(lq_max, vk.max_len());
   const int tb = tb_bytes_for(o, std::max(lqv, 1));
-  return vk.kind == VK_FAST  ? (size_t)(kBlock / 64) * fast_wave_lds(tb)
-         : vk.kind == VK_GRP ? (size_t)(kBlock / 16) * grp_group_lds(tb)
-                             : (size_t)tb * (kBlock / vk.G);
+  return vk.kind == VK_FAST ? (size_t)(kBlock / 64) * fast_wave_lds(tb) : (size_t)tb * (kBlock / vk.G);
 }
 
 // Options that need more LDS per workgroup than a launch may take are refused
@@ -544,10 +499,7 @@ int check_lds(bwagpu_ctx_t* ctx, int lq_max) {
       return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
     return BWAGPU_OK;
   }
-  const bool grp = use_grp_kernels();
   for (int v = 0; v < kNumVariants; ++v) {
-    const Variant& vk = kVariants[v];
-    if ((vk.kind == VK_GRP) != grp && vk.kind != VK_GENERIC) continue;
     if (variant_lds(ctx->opt, v, lq_max) > 64 * 1024)
       return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
   }
@@ -644,9 +596,8 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   HIPC(launch_chain_prep(ctx->opt, ctx->ref, db, s.d_win.as<ChainWin>(), s.d_srt.as<uint64_t>(),
                          s.d_prog.as<bwagpu_seed_t>(), d_stats, st),
        "chain_prep launch");
-  const bool grp = use_grp_kernels();
   HIPC(launch_read_order(db, bins, s.d_counts.as<int32_t>() + kHistOff, s.d_counts.as<int32_t>(),
-                         s.d_desc.as<ReadDesc>(), read_list, d_stats, grp, st),
+                         s.d_desc.as<ReadDesc>(), read_list, d_stats, st),
        "read order launch");
   C2AArgs a;
   a.read_list = read_list;
@@ -659,9 +610,7 @@ int enqueue_chain2aln(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max
   a.out_n = d_n;
   a.stats = d_stats;
   for (int v = 0; v < kNumVariants; ++v) {
-    const Variant& vk = kVariants[v];
-    if ((vk.kind == VK_GRP) != grp && vk.kind != VK_GENERIC) continue;  // gets no reads
-    const int lqv = std::min(lq_max, vk.kind == VK_GRP ? 256 : vk.max_len());
+    const int lqv = std::min(lq_max, kVariants[v].max_len());
     const int tb = tb_bytes_for(ctx->opt, std::max(lqv, 1));
     HIPC(launch_chain2aln(v, ctx->opt, ctx->ref, db, db.n_reads, tb, a, st), "chain2aln launch");
   }
@@ -739,19 +688,6 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
-  if (ctx->sp_on < 0) {
-    const char* e = getenv("BWAGPU_SUBMIT_PROF");
-    ctx->sp_on = e && e[0] == '1';
-  }
-  using clk = std::chrono::steady_clock;
-  auto t_prev = clk::now();
-  auto lap = [&](double& acc) {
-    if (!ctx->sp_on) return;
-    const auto t = clk::now();
-    acc += std::chrono::duration<double>(t - t_prev).count();
-    t_prev = t;
-  };
-  ctx->sp_n += ctx->sp_on;
   int lq_max = 0;
   int rc = check_batch(ctx, b, &lq_max);
   if (rc) return rc;
@@ -762,7 +698,6 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   s.n_seeds = b->n_seeds;
   InLayout L;
   L.make(*b);
-  s.h_in.flags = pinned_in_flags();
   HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
   HIPC(s.d_in.ensure(L.total), "hipMalloc(in)");
   HIPC(s.d_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipMalloc(out)");
@@ -771,7 +706,6 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipHostMalloc(out)");
   HIPC(s.h_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipHostMalloc(out_n)");
   HIPC(s.h_stats.ensure(sizeof(int64_t) * ST_N), "hipHostMalloc(stats)");
-  lap(ctx->sp_check);
   // stage into pinned memory so the caller's buffers are free on return —
   // unless the caller packed into that memory already (bwagpu_chain2aln_stage)
   char* h = s.h_in.as<char>();
@@ -795,18 +729,8 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   }
 
   hipStream_t st = s.stream;
-  lap(ctx->sp_copy);
   HIPC(hipEventRecord(s.ev0, st), "event");
-  void* h_dev = nullptr;
-  if (h2d_by_kernel() && hipHostGetDevicePointer(&h_dev, s.h_in.p, 0) == hipSuccess && h_dev) {
-    const size_t n16 = L.total / 16;  // L.total is a multiple of 256
-    hipLaunchKernelGGL(pull_kernel, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 2048)), dim3(256), 0, st,
-                       (const uint4*)h_dev, (uint4*)s.d_in.p, n16);
-    HIPC(hipGetLastError(), "pull launch");
-  } else {
-    HIPC(hipMemcpyAsync(s.d_in.p, s.h_in.p, L.total, hipMemcpyHostToDevice, st), "H2D batch");
-  }
-  lap(ctx->sp_h2d);
+  HIPC(hipMemcpyAsync(s.d_in.p, s.h_in.p, L.total, hipMemcpyHostToDevice, st), "H2D batch");
   HIPC(hipMemsetAsync(s.d_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset stats");
   char* d = s.d_in.as<char>();
   DevBatch db;
@@ -829,7 +753,6 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
     (void)hipStreamSynchronize(st);
     return rc;
   }
-  lap(ctx->sp_enq);
   HIPC(hipEventRecord(s.ev2, st), "event");
   if (b->n_seeds)
     HIPC(hipMemcpyAsync(s.h_out.p, s.d_out.p, sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds, hipMemcpyDeviceToHost, st),
@@ -839,7 +762,6 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
          "D2H counts");
   HIPC(hipMemcpyAsync(s.h_stats.p, s.d_stats.p, sizeof(int64_t) * ST_N, hipMemcpyDeviceToHost, st), "D2H stats");
   HIPC(hipEventRecord(s.ev3, st), "event");
-  lap(ctx->sp_d2h);
   s.h2d = (int64_t)L.total;
   s.d2h = (int64_t)(sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds + sizeof(int32_t) * (size_t)b->n_reads);
   s.busy = true;
@@ -913,7 +835,6 @@ int bwagpu_chain2aln_stage(bwagpu_ctx_t* ctx, int slot, int32_t n_reads, int32_t
   InLayout L;
   L.make(b);
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  s.h_in.flags = pinned_in_flags();
   HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
   char* h = s.h_in.as<char>();
   b.seq_off = (const int64_t*)(h + L.seq_off);
@@ -981,12 +902,8 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   if (n == 0) return BWAGPU_OK;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   // validate and bin on the host
-  // bins: [0, kNumExtVariants) wave kernels, then the 16-lane-group kernels
-  // (CPL 4, 8); BWAGPU_EXT_WAVE=1 keeps every task on the wave kernels (A/B)
-  constexpr int kGrpBins = 2;
-  std::vector<int32_t> lists[kNumExtVariants + kGrpBins];
-  const char* ew = getenv("BWAGPU_EXT_WAVE");
-  const bool grp = !(ew && ew[0] == '1');
+  // bins: the wave kernels by column segments
+  std::vector<int32_t> lists[kNumExtVariants];
   bool t5 = false;
   int lq_max = 1;
   for (int32_t k = 0; k < n; ++k) {
@@ -998,8 +915,6 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
     int v = kNumExtVariants - 1;
     for (int i = kNumExtVariants - 1; i >= 0; --i)
       if (t.qlen + 1 <= kExtVariants[i].max_len()) v = i;
-    if (grp && t.qlen + 1 <= 64) v = kNumExtVariants;
-    else if (grp && t.qlen + 1 <= 128) v = kNumExtVariants + 1;
     lists[v].push_back(k);
     lq_max = std::max(lq_max, t.qlen + 1);
   }
@@ -1039,9 +954,9 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   (void)hipEventRecord(e0, st);
   int32_t off = 0;
   std::vector<int32_t> all;
-  for (int v = 0; v < kNumExtVariants + kGrpBins; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
+  for (int v = 0; v < kNumExtVariants; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
   if ((rc = ck(hipMemcpyAsync(d_list.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D"))) return rc;
-  for (int v = 0; v < kNumExtVariants + kGrpBins; ++v) {
+  for (int v = 0; v < kNumExtVariants; ++v) {
     const int32_t nv = (int32_t)lists[v].size();
     if (nv) {
       int rows = 16;
@@ -1053,19 +968,14 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
         rows = std::max(rows, std::min(t.tlen, t.qlen + we + 1));
       }
       const int tb = (rows + 2 + 15) & ~15;
-      const int gpb = v < kNumExtVariants ? kBlock / kExtVariants[v].G : kBlock / 16;
+      const int gpb = kBlock / kExtVariants[v].G;
       if ((size_t)tb * gpb > 64 * 1024) {
         cleanup();
         return fail(ctx, BWAGPU_E_UNSUPPORTED, "task needs too many LDS rows");
       }
-      hipError_t e =
-          v < kNumExtVariants
-              ? launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off, nv,
-                              d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
-                              d_stats.as<int64_t>(), st)
-              : launch_extend_grp(v == kNumExtVariants ? 4 : 8, t5, ctx->opt, d_tasks.as<bwagpu_ext_task_t>(),
-                                  d_list.as<int32_t>() + off, nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb,
-                                  d_res.as<bwagpu_ext_result_t>(), d_stats.as<int64_t>(), st);
+      hipError_t e = launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off,
+                                   nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
+                                   d_stats.as<int64_t>(), st);
       if ((rc = ck(e, "extend launch"))) return rc;
     }
     off += nv;
@@ -1467,7 +1377,6 @@ int bwagpu_debug_fail_wait(bwagpu_ctx_t* ctx, int after_n_waits, int code) {
   return BWAGPU_OK;
 }
 
-int bwagpu_debug_ext_lane(int mode) { return set_ext_lane_mode(mode); }
 
 int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   if (!ctx || !out) return BWAGPU_E_INVAL;
@@ -1534,6 +1443,22 @@ int bwagpu_prof_read(bwagpu_ctx_t* ctx, double* total_ms, int32_t* launches) {
   }
   *total_ms = t;
   *launches = ctx->prof_used / 2;
+  return BWAGPU_OK;
+}
+
+int bwagpu_prof_intervals(bwagpu_ctx_t* ctx, double* start_ms, double* end_ms, int32_t max, int32_t* n) {
+  if (!ctx || !n || max < 0 || (max && (!start_ms || !end_ms))) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  int k = 0;
+  for (int i = 0; i + 1 < ctx->prof_used && k < max; i += 2, ++k) {
+    HIPC(hipEventSynchronize(ctx->prof_ev[i + 1]), "hipEventSynchronize");
+    float a = 0, b = 0;
+    HIPC(hipEventElapsedTime(&a, ctx->prof_ev[0], ctx->prof_ev[i]), "hipEventElapsedTime");
+    HIPC(hipEventElapsedTime(&b, ctx->prof_ev[0], ctx->prof_ev[i + 1]), "hipEventElapsedTime");
+    start_ms[k] = a;
+    end_ms[k] = b;
+  }
+  *n = k;
   return BWAGPU_OK;
 }
 

@@ -64,18 +64,17 @@ enum { ERR_RID = 1, ERR_LEN = 2 };
 
 // Kernel variants: G lanes per read ("group"), C = max DP columns per lane.
 // A read of length l needs G*C >= l (+1 column for eh[qlen], qlen <= l-1).
-enum { VK_FAST = 0, VK_GENERIC = 1, VK_GRP = 2 };
+enum { VK_FAST = 0, VK_GENERIC = 1 };
 struct Variant {
   int G, C;
-  int kind;  // VK_GRP: chain2aln_grp_kernel (16-lane groups, columns = longest extension)
-             // VK_FAST: chain2aln_fast_kernel (wave per read), VK_GENERIC: chain2aln_kernel
+  int kind;  // VK_FAST: chain2aln_fast_kernel (wave per read), VK_GENERIC: chain2aln_kernel
   __host__ __device__ int max_len() const { return G * C; }
 };
-// limits of the fast and group kernels: one lane (slot) per seed / chain / region of a read
+// limits of the fast kernel: one lane (slot) per seed / chain / region of a read
 constexpr int kFastMaxSeeds = 32;
 constexpr int kFastMaxChains = 32;
 constexpr int kSeqLds = 256;  // LDS bytes for the read's bases (fast variants: lq <= 256)
-constexpr int kNumVariants = 7;
+constexpr int kNumVariants = 3;
 extern const Variant kVariants[kNumVariants];
 // bare ksw_extend2 task lists (bwagpu_extend_batch): wave kernels by columns
 constexpr int kNumExtVariants = 3;
@@ -93,7 +92,7 @@ hipError_t launch_chain_prep(const DevOpt& o, const DevRef& ref, const DevBatch&
 // writes read_list[pos] and desc[pos] (bins: n_reads scratch, hist: 3*256
 // zeroed counters, counts: per-variant read counts)
 hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, int32_t* counts, ReadDesc* desc,
-                             int32_t* list, int64_t* stats, bool grp, hipStream_t st);
+                             int32_t* list, int64_t* stats, hipStream_t st);
 // read_list: reads sorted by key; d_count: per-variant counts (device); the
 // variant's reads start at the sum of the lower variants' counts; max_list
 // bounds the grid
@@ -113,18 +112,11 @@ hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, con
                             int tb_bytes, const C2AArgs& a, hipStream_t st);
 // LDS bytes per wave of chain2aln_fast_kernel for target row buffers of tb bytes
 size_t fast_wave_lds(int tb);
-// LDS bytes per 16-lane group of chain2aln_grp_kernel
-size_t grp_group_lds(int tb);
 
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,
                          bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
-
-// 16-lane-group ksw_extend2 over a task list: cpl = 4 (qlen + 1 <= 64) or 8 (<= 128)
-hipError_t launch_extend_grp(int cpl, bool t5, const DevOpt& o, const bwagpu_ext_task_t* tasks,
-                             const int32_t* task_list, int32_t n_list, const uint8_t* qpool, const uint8_t* tpool,
-                             int tb_bytes, bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
 
 // ---------------------------------------------------------------- speculative path
 // mem_chain2aln as (1) extension tasks computed ahead of the sequential
@@ -169,15 +161,9 @@ enum {
 // MI355X_MICROARCH.md "dequeue"; measured here: 7.9 -> 6.6 ms per C2 batch
 // when the nine lists' heads moved off the two shared lines)
 constexpr int kQHStride = 32;
-// + one head per list for the lane kernel (spec_extl_kernel), after the sharded ones
-constexpr int kQHLaneBase = kSpecRounds * kSpecBins * 8 * kQHStride;
-constexpr int kQHWords = kQHLaneBase + kSpecRounds * kSpecBins * kQHStride;
-// pair-kernel task order (spec_sort_*): 1024 keys = (left qlen / 8, right qlen / 8);
-// with the lane kernel on, keys 0 .. kLaneKeys-1 hold its tasks (both sides'
-// qlen <= kLaneQ), largest (ql/8 + qr/8) first, and the pair kernel's keys follow
+constexpr int kQHWords = kSpecRounds * kSpecBins * 8 * kQHStride;
+// pair-kernel task order (spec_sort_*): 1024 keys = (left qlen / 8, right qlen / 8)
 constexpr int kSortKeys = 1024;
-constexpr int kLaneQ = 63;                          // spec_extl_kernel: both sides' qlen <= kLaneQ
-constexpr int kLaneKeys = 2 * (kLaneQ >> 3) + 1;    // (ql / 8 + qr / 8) <= 2 (kLaneQ / 8)
 constexpr int kSortWords = kSpecRounds * 2 * kSortKeys;
 // task list `list` (= round * kSpecBins + bin) starts at this entry of SpecArgs::tasks
 __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_seeds) {
@@ -229,7 +215,6 @@ size_t spec_select_lds(int tb_bytes);
 // the lane kernel for short extension tasks (spec_extl_kernel): 0 off, 1 before
 // the pair kernel, 2 beside it on the side stream; process-wide; returns the
 // previous mode (mode < 0: query only)
-int set_ext_lane_mode(int mode);
 int spec_redo_cap(int tb_bytes);
 
 // ---------------------------------------------------------------- FPGA wire format

@@ -42,8 +42,7 @@
 
 namespace bwagpu {
 
-const Variant kVariants[kNumVariants] = {{16, 4, VK_GRP},  {16, 8, VK_GRP},  {16, 10, VK_GRP},   {16, 16, VK_GRP},
-                                         {64, 3, VK_FAST}, {64, 4, VK_FAST}, {64, 16, VK_GENERIC}};
+const Variant kVariants[kNumVariants] = {{64, 3, VK_FAST}, {64, 4, VK_FAST}, {64, 16, VK_GENERIC}};
 const Variant kExtVariants[kNumExtVariants] = {{64, 3, VK_FAST}, {64, 4, VK_FAST}, {64, 16, VK_GENERIC}};
 
 // wave-uniform max of a group-uniform value over the wave's ACTIVE groups (for
@@ -163,9 +162,6 @@ constexpr int NEG = -(1 << 29);
 //    columns past qlen sit after every real column and need no masking;
 //  * the reference's special eh[] writes (eh[lo].h = first-column value,
 //    eh[hi] = {h1, 0}, ksw.c:420-429,449) are single-lane selects.
-#ifndef BWAGPU_DEFER_RK
-#define BWAGPU_DEFER_RK 1
-#endif
 // x <- inclusive max-scan over the wave (row_shr 1/2/4/8, row_bcast 15/31)
 // and r <- wave max in lane 63 (row_ror 8/4/2/1, row_bcast 15/31), the two
 // dependency chains interleaved: every DPP read is 2 wait states after the
@@ -236,7 +232,6 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
   int cells = vgpr(0);
   int rows = tlen;
   int tnext = tlen > 0 ? tb[0] : 0;
-#if BWAGPU_DEFER_RK
   // The row maximum of row i-1 is reduced while row i's F scan runs: the two
   // 6-step DPP chains interleave in one asm block (scan_reduce), and row i-1's
   // exit test moves to row i, whose results are dropped if row i-1 exits.
@@ -254,7 +249,6 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     bj = up ? mj : bj;
     return __builtin_amdgcn_ballot_w64(brk) != 0;
   };
-#endif
   for (int i = 0; i < tlen; ++i) {
     const int t = __builtin_amdgcn_readfirstlane(tnext);
     tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
@@ -281,12 +275,8 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       M[c] = m;
       const int u = inb[c] ? max(m + Kc[c], jEc[c]) : jEc[c];
       int x = c == 0 ? u : max(u, carry);
-#if BWAGPU_DEFER_RK
       if (c == 0) scan_reduce(x, rkp);
       else x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
-#else
-      x = max_bc31(max_bc15(max_shr8(max_shr4(max_shr2(max_shr1(x))))));
-#endif
       EX[c] = dpp<DPP_WAVE_SHR1>(carry, x);  // lane 0 takes the carry from the segments before
       if (c + 1 < CD) carry = __builtin_amdgcn_readlane(x, 63);
     }
@@ -346,7 +336,6 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
       if (jl < 0) jl = nlo - 1;
       nhi = min(jl + 2, qlen);
     }
-#if BWAGPU_DEFER_RK
     if (i > 0 && row_end(__builtin_amdgcn_readlane(rkp, 63), vi - 1)) {
       rows = i;  // row i-1 was the last row: row i never ran
       break;
@@ -366,228 +355,15 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     int rkr = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rkp))))));
     (void)row_end(__builtin_amdgcn_readlane(rkr, 63), vi - 1);
   }
-#else
-    rk = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rk))))));
-    rk = __builtin_amdgcn_readlane(rk, 63);
-    cells += wd;
-    {  // ksw.c:450-453
-      const bool atend = max(lo, hi) == qlen;
-      ei = (atend && !(esc > h1)) ? vi : ei;
-      esc = atend ? max(esc, h1) : esc;
-    }
-    // ksw.c:454-465, all lanes alike.  The row's updates come before the one
-    // exit test: on an exit row they are no-ops (a z-drop exit has m <= max,
-    // and m == 0 cannot beat max >= h0 >= 0), and the trimmed band is unused.
-    // drop: exactly one of (di-dj)*e_del, (dj-di)*e_ins is positive (both are
-    // 0 when di == dj), which is the branch ksw.c:461-463 takes.
-    const int mrow = rk >> 10, mj = rk & 1023;
-    const bool up = mrow > best;
-    const int di = vi - bi, dj = mj - bj;
-    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
-    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
-    off = up ? max(off, abs(mj - vi)) : off;
-    best = up ? mrow : best;
-    bi = up ? vi : bi;
-    bj = up ? mj : bj;
-    vi += 1;
-    lo = nlo;
-    hi = nhi;
-    if (__builtin_amdgcn_ballot_w64(brk)) {
-      rows = i + 1;
-      break;
-    }
-  }
-#endif
   tl.cells += __builtin_amdgcn_readfirstlane(cells);
   tl.rows += rows;
   tl.calls += 1;
-#ifdef BWAGPU_CD_STATS
-  if (g_trace && r == 0) {  // diagnostics: rows / cells / calls per segment count
-    atomicAdd(&g_trace[4 * CD + 0], (uint32_t)rows);
-    atomicAdd(&g_trace[4 * CD + 1], (uint32_t)__builtin_amdgcn_readfirstlane(cells));
-    atomicAdd(&g_trace[4 * CD + 2], 1u);
-  }
-#endif
   auto u = [](int x) { return __builtin_amdgcn_readfirstlane(x); };
   return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
 }
 
-// ------------------------------------------------ ksw_extend2, blocked columns
-// The same extension with the query's columns BLOCKED over the wave: lane r
-// holds columns j = r*CPL + c, c < CPL (CPL = ceil((qlen+1)/64)).  The row's
-// cross-lane work no longer grows with the segment count: ONE exclusive
-// max-plus scan (the in-lane part of F runs sequentially, as in gext_row), ONE
-// shift of H(i, j-1) into the next lane, ONE row-max reduction (interleaved
-// with the next row's scan), and the band trim by two ballots + readlanes.
-// Per row (ksw.c:415-470), as gext_row on 16-lane groups:
-//  * M_j = H(i-1,j-1) ? H(i-1,j-1) + S(t_i, q_j) : 0;
-//  * F: with A_c = (in band ? M_c : NEG) - oe_ins and T the lane's running
-//    max(T - e_ins, A_c), F entering the lane is max(0, max_{r'<r} T_r' -
-//    (r-1-r')*CPL*e_ins): one exclusive wave scan of T + r*CPL*e_ins;
-//  * the stored H of column j is H(i, j-1); column lo takes left0 (lane 0 via
-//    the shift's old value, other lanes from an out-of-band column = 0), and
-//    eh[hi] = {h1, 0} (ksw.c:449) is the same update applied to column hi with
-//    E cleared: [lo, hi] updates under one rule;
-//  * h1 = H(i, hi-1) is one readlane of the lane holding column hi.
-template <int CPL, bool T5>
-__device__ __forceinline__ ExtOut extend_wave_blk(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
-                                                  int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
-                                                  int h0, Tally& tl) {
-  const int r = (int)(threadIdx.x & 63);
-  const int e_del = o.e_del, e_ins = o.e_ins, o_del = o.o_del, oe_ins = o.oe_ins;
-  constexpr int KS = 2;  // bits of the in-lane column in the row-max key (CPL <= 4)
-  static_assert(CPL >= 1 && CPL <= 4, "blocked columns: CPL <= 4");
-  const int j0 = r * CPL;
-  int hh[CPL], ee[CPL];
-  uint32_t pf[CPL];
-  uint32_t pf4[T5 ? CPL : 1];
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int j = j0 + c;
-    const int qb = j < qlen ? qp[qa + qd * j] : 0;
-    pf[c] = qprof_word(o, qb);
-    if (T5) pf4[c] = (uint32_t)(uint8_t)qprof4_val(o, qb);
-    const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);  // ksw.c:392-395
-    hh[c] = j <= qlen ? v : 0;
-    ee[c] = 0;
-  }
-  {  // band clamp (ksw.c:399-407)
-    const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
-    const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, e_del);
-    w = __builtin_amdgcn_readfirstlane(min(w, min(mi, md)));
-  }
-  const int rE = e_ins * CPL * r;  // the lane's offset in the scan
-  int best = vgpr(h0), bi = vgpr(-1), bj = vgpr(-1), ei = vgpr(-1), esc = vgpr(-1), off = vgpr(0);
-  int lo = vgpr(0), hi = vgpr(qlen);
-  int iw = vgpr(-w), iw1 = vgpr(w + 1);
-  int gl = vgpr(h0 - o.o_del - e_del);
-  int vi = vgpr(0);
-  int cells = vgpr(0);
-  int rows = tlen;
-  int tnext = tlen > 0 ? tb[0] : 0;
-  int rkp = 0;  // row i-1's per-lane key, reduced during row i's scan
-  auto row_end = [&](int rkr, int vk) -> bool {  // ksw.c:454-465 of row vk
-    const int mrow = rkr >> 10, mj = rkr & 1023;
-    const bool up = mrow > best;
-    const int di = vk - bi, dj = mj - bj;
-    const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
-    const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
-    off = up ? max(off, abs(mj - vk)) : off;
-    best = up ? mrow : best;
-    bi = up ? vk : bi;
-    bj = up ? mj : bj;
-    return __builtin_amdgcn_ballot_w64(brk) != 0;
-  };
-  for (int i = 0; i < tlen; ++i) {
-    const int t = __builtin_amdgcn_readfirstlane(tnext);
-    tnext = tb[i + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
-    lo = max(lo, iw);
-    hi = min(min(hi, iw1), qlen);
-    iw += 1;
-    iw1 += 1;
-    const int wd = usat32(hi, lo);
-    const int left0 = lo == 0 ? max(gl, 0) : 0;
-    gl -= e_del;
-    const int sh = (t & 3) << 3;
-    const int x = j0 - lo;
-    int M[CPL], A[CPL];
-    int T = 0;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const bool ib = (unsigned)(x + c) < (unsigned)wd;
-      int sc;
-      if (T5 && t == 4) sc = (int)(int8_t)(pf4[c] & 0xff);
-      else sc = __builtin_amdgcn_sbfe((int)pf[c], sh, 8);
-      const int m = hh[c] ? hh[c] + sc : 0;
-      M[c] = m;
-      A[c] = (ib ? m : NEG) - oe_ins;
-      T = max(T - e_ins, A[c]);
-    }
-    int sx = T + rE;
-    scan_reduce(sx, rkp);  // inclusive scan of this row + row i-1's max
-    const int EX = dpp<DPP_WAVE_SHR1>(NEG, sx);
-    int f = max(EX - rE + e_ins * CPL, 0);
-    int hm[CPL];
-    int lk = 0, h1c = 0;
-    const int hix = hi - j0;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const unsigned d = (unsigned)(x + c);
-      const bool ib = d < (unsigned)wd, ib2 = d <= (unsigned)wd;
-      if (c > 0) f = max(max(f - e_ins, A[c - 1]), 0);
-      const int h = max(max(M[c], ee[c]), f);
-      hm[c] = ib ? h : 0;
-      const int en = usat32(max(ee[c], M[c] - o_del), e_del);
-      lk = max(lk, (hm[c] << KS) + c);
-      ee[c] = ib ? en : (ib2 ? 0 : ee[c]);
-      if (c > 0) {
-        hh[c] = ib2 ? hm[c - 1] : hh[c];
-        h1c = hix == c ? hm[c - 1] : h1c;
-      }
-    }
-    const int hs0 = dpp<DPP_WAVE_SHR1>(left0, hm[CPL - 1]);  // H(i, j0-1); lane 0: left0
-    hh[0] = (unsigned)x <= (unsigned)wd ? hs0 : hh[0];
-    h1c = hix == 0 ? hs0 : h1c;
-    const int hi_s = __builtin_amdgcn_readfirstlane(hi);
-    const int h1 = __builtin_amdgcn_readlane(h1c, hi_s / CPL);
-    // band trim for the next row (ksw.c:466-469)
-    uint32_t nzm = 0;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) nzm |= (uint32_t)((hh[c] | ee[c]) != 0) << c;
-    const int lo_l = min(max(lo - j0, 0), 7), hi_l = min(max(hix, 0), 7);
-    const uint32_t mf = nzm & ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);  // [lo, hi)
-    const uint32_t ml = mf | (nzm & (hi_l == hix ? 1u << hi_l : 0u));     // [lo, hi]
-    const uint64_t bf = __builtin_amdgcn_ballot_w64(mf != 0), bl = __builtin_amdgcn_ballot_w64(ml != 0);
-    int nlo = hi_s, jl = -1;
-    if (bf) {
-      const int ln = (int)__builtin_ctzll(bf);
-      nlo = min(ln * CPL + (int)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)mf, ln)), hi_s);
-    }
-    if (bl) {
-      const int ln = 63 - (int)__builtin_clzll(bl);
-      jl = ln * CPL + 31 - (int)__builtin_clz((uint32_t)__builtin_amdgcn_readlane((int)ml, ln));
-    }
-    jl = max(jl, nlo - 1);
-    const int nhi = min(jl + 2, qlen);
-    if (i > 0 && row_end(__builtin_amdgcn_readlane(rkp, 63), vi - 1)) {
-      rows = i;  // row i-1 was the last row: row i never ran
-      break;
-    }
-    rkp = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
-    cells += wd;
-    {  // ksw.c:450-453
-      const bool atend = max(lo, hi) == qlen;
-      ei = (atend && !(esc > h1)) ? vi : ei;
-      esc = atend ? max(esc, h1) : esc;
-    }
-    vi += 1;
-    lo = nlo;
-    hi = nhi;
-  }
-  if (rows == tlen && tlen > 0) {  // the last row's bookkeeping (its exit test is moot)
-    int rkr = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rkp))))));
-    (void)row_end(__builtin_amdgcn_readlane(rkr, 63), vi - 1);
-  }
-  tl.cells += __builtin_amdgcn_readfirstlane(cells);
-  tl.rows += rows;
-  tl.calls += 1;
-  auto u = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
-  return ExtOut{u(best), u(bj) + 1, u(bi) + 1, u(ei) + 1, u(esc), u(off)};
-}
-
-// extend_pair's band trim: 1 (default) = DPP min/max reductions over each
-// half, 0 = a ballot per row and readlanes of the half's first/last lane
-// (same-box A/B, DESIGN.md §3: equal stage throughput at 96 VGPRs, 3-4 %
-// longer launches)
-#ifndef BWAGPU_TRIM_DPP
-#define BWAGPU_TRIM_DPP 1
-#endif
-
 // CD is uniform per call (qlen is): one compiled body per segment count
-// (CD 2..4 on blocked columns with -DBWAGPU_BLK=1: bit-exact, measured slower)
-#ifndef BWAGPU_BLK
-#define BWAGPU_BLK 0
-#endif
+// (blocked columns were measured slower: DESIGN.md §3)
 template <int C, bool T5>
 __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp,
                                                     int qa, int qd, int tlen, const uint8_t* tb, int w,
@@ -602,12 +378,7 @@ __device__ __forceinline__ ExtOut extend_wave_dispatch(const DevOpt& o, int qlen
   h0 = __builtin_amdgcn_readfirstlane(h0);
   const int cd = (qlen + 64) >> 6;  // ceil((qlen+1)/64)
 #define EXT_SEG(n)                                                                                          \
-  if (n <= C && cd == n) {                                                                                  \
-    if (BWAGPU_BLK && n >= 2 && n <= 4)                                                                     \
-      return extend_wave_blk<(n <= C && n <= 4 ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, \
-                                                           h0, tl);                                         \
-    return extend_wave<(n <= C ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);    \
-  }
+  if (n <= C && cd == n) return extend_wave<(n <= C ? n : 1), T5>(o, qlen, qp, qa, qd, tlen, tb, w, end_bonus, zdrop, h0, tl);
   EXT_SEG(1) EXT_SEG(2) EXT_SEG(3) EXT_SEG(4) EXT_SEG(5) EXT_SEG(6) EXT_SEG(7) EXT_SEG(8)
   EXT_SEG(9) EXT_SEG(10) EXT_SEG(11) EXT_SEG(12) EXT_SEG(13) EXT_SEG(14) EXT_SEG(15) EXT_SEG(16)
 #undef EXT_SEG
@@ -806,29 +577,9 @@ __device__ __forceinline__ ExtOut extend_pair(const DevOpt& o, int qlen, const u
     const int lo_l = min(max(lo - j0, 0), 31), hi_l = min(max(hix, 0), 31);
     const uint32_t mf = nzm & ((1u << hi_l) - 1u) & ~((1u << lo_l) - 1u);   // [lo, hi)
     const uint32_t ml = mf | (nzm & ((unsigned)hix < (unsigned)CPL ? 1u << hix : 0u));  // + column hi
-#if BWAGPU_TRIM_DPP
     int cl = mf ? j0 + (int)__builtin_ctz(mf) : 0x7fff;
     int ch = ml ? j0 + 31 - (int)__builtin_clz(ml) : -1;
     row_minmax(cl, ch);
-#else
-    // the first / last non-zero column of [lo, hi] per half: the half's first /
-    // last lane holding one (a ballot), then that lane's first / last slot
-    // (readlane).  The first one is taken over [lo, hi] rather than [lo, hi):
-    // nlo = min(cl, hi) is the same either way.
-    int cl, ch;
-    {
-      const int fl = j0 + (int)__builtin_ctz(ml | 0x80000000u), ll = j0 + 31 - (int)__builtin_clz(ml | 1u);
-      const uint64_t bm = __builtin_amdgcn_ballot_w64(ml != 0u);
-      const uint32_t m0 = (uint32_t)bm, m1 = (uint32_t)(bm >> 32);
-      const int cl0 = m0 ? __builtin_amdgcn_readlane(fl, __builtin_ctz(m0 | 0x80000000u)) : 0x7fff;
-      const int ch0 = m0 ? __builtin_amdgcn_readlane(ll, 31 - __builtin_clz(m0 | 1u)) : -1;
-      const int cl1 = m1 ? __builtin_amdgcn_readlane(fl, 32 + __builtin_ctz(m1 | 0x80000000u)) : 0x7fff;
-      const int ch1 = m1 ? __builtin_amdgcn_readlane(ll, 63 - __builtin_clz(m1 | 1u)) : -1;
-      const bool h1 = (threadIdx.x & 32) != 0;
-      cl = h1 ? cl1 : cl0;
-      ch = h1 ? ch1 : ch0;
-    }
-#endif
     if (i > 0) {
       const int rkr = half_max(rkp);
       if (row_end(rkr, vi - 1)) {
@@ -836,10 +587,8 @@ __device__ __forceinline__ ExtOut extend_pair(const DevOpt& o, int qlen, const u
         break;
       }
     }
-#if BWAGPU_TRIM_DPP
     cl = half_min(cl);
     ch = half_max(ch);
-#endif
     const int nlo = min(cl, hi);
     const int nhi = min(max(ch, nlo - 1) + 2, qlen);
     rkp = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
@@ -883,187 +632,6 @@ __device__ __forceinline__ ExtOut extend_pair_dispatch(const DevOpt& o, int qlen
   EXT_PAIR(1) EXT_PAIR(2) EXT_PAIR(3) EXT_PAIR(4) EXT_PAIR(5) EXT_PAIR(6) EXT_PAIR(7) EXT_PAIR(8)
 #undef EXT_PAIR
   return ExtOut{-1, 0, 0, 0, -1, 0};  // unreachable: cpl <= PMAX by construction
-}
-
-// ------------------------------------------------ ksw_extend2, 16-lane groups
-// One extension per 16-lane group (one DPP row), FOUR extensions per wave that
-// share every instruction of a DP row.  Columns are BLOCKED: lane r of the
-// group holds columns j = r*CPL + c, c < CPL (qlen + 1 <= 16*CPL).  Every
-// group-uniform quantity (band, maxima, break state) is a per-lane VGPR value
-// identical over the group's lanes, so the four groups of a wave run their rows
-// in lock step, each with its own band, and leave the row loop independently.
-//
-// Per row (ksw.c:415-470):
-//  * M_j = H(i-1,j-1) ? H(i-1,j-1) + S(t_i, q_j) : 0, masked to NEG outside
-//    the band [lo, hi);
-//  * F: F(i,j) = max_{k<j}(t_k - (j-1-k)e_ins) over t_k = max(M_k - oe_ins, 0).
-//    With v_k = M_k + k*e_ins - oe_ins and P_c = max(0, v_0..v_c) (in-lane
-//    prefix), F at the lane's first column comes from ONE exclusive group
-//    scan of U = P_{CPL-1} + e_ins*(r*CPL - CPL + 1); inside the lane
-//    F_c = sat(max(F_in - e_ins, P_{c-1}) - (c-1)e_ins) for c >= 1;
-//  * H = max(M, E, F); the H value stored for column j is H(i, j-1) (the lane's
-//    own previous column, or the DPP-shifted last column of the lane below;
-//    lane 0 of the group injects the first-column value left0, ksw.c:420-423);
-//    the reference's eh[hi] = {h1, 0} write (ksw.c:449) is the same update
-//    applied to column hi with E cleared, so [lo, hi] is updated in one rule;
-//  * row max + LAST argmax: group max of (H << 10 | j), in-lane as H << KS | c;
-//  * band trim (ksw.c:466-469): per-lane bitmask of non-zero columns, first
-//    column in [lo, hi) by a group min, last in [lo, hi] by a group max.
-template <int CPL, bool T5>
-struct GrpExt {
-  int hh[CPL], ee[CPL];
-  uint32_t pf[CPL];
-  uint32_t pf4[T5 ? CPL : 1];
-  int lo, hi, iw, iw1, gl, vi, best, bi, bj, ei, esc, off, cells, tlen, zdrop, qlen;
-  uint32_t tb;  // LDS byte offset of target row 0
-  int tnext;
-};
-
-__device__ __forceinline__ int g16_max(int v) { return max_ror1(max_ror2(max_ror4(max_ror8(v)))); }
-__device__ __forceinline__ int g16_min(int v) { return min_ror1(min_ror2(min_ror4(min_ror8(v)))); }
-
-// Q(j) = query base of column j (j < qlen); tb/lds: target rows in LDS
-template <int CPL, bool T5, typename Q>
-__device__ __forceinline__ void gext_init(GrpExt<CPL, T5>& s, const DevOpt& o, int r, int qlen, Q qbase, int tlen,
-                                          uint32_t tb, const uint8_t* lds, int w, int end_bonus, int zdrop, int h0) {
-  const int e_ins = o.e_ins, oe_ins = o.oe_ins;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int j = r * CPL + c;
-    const int qb = j < qlen ? qbase(j) : 0;
-    s.pf[c] = qprof_word(o, qb);
-    if (T5) s.pf4[c] = (uint32_t)(uint8_t)qprof4_val(o, qb);
-    // row -1 of eh[] (ksw.c:392-395)
-    const int v = j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0);
-    s.hh[c] = j <= qlen ? v : 0;
-    s.ee[c] = 0;
-  }
-  const int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, e_ins);
-  const int md = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_del, o.e_del);
-  w = min(w, min(mi, md));
-  s.best = h0;
-  s.bi = s.bj = s.ei = s.esc = -1;
-  s.off = 0;
-  s.lo = 0;
-  s.hi = qlen;
-  s.iw = -w;
-  s.iw1 = w + 1;
-  s.gl = h0 - o.o_del - o.e_del;
-  s.vi = 0;
-  s.cells = 0;
-  s.tlen = tlen;
-  s.zdrop = zdrop;
-  s.qlen = qlen;
-  s.tb = tb;
-  s.tnext = tlen > 0 ? lds[tb] : 0;
-}
-
-// one DP row of every active group; returns true (group-uniform) when the
-// extension is finished (break or last row)
-template <int CPL, bool T5>
-__device__ __forceinline__ bool gext_row(GrpExt<CPL, T5>& s, const DevOpt& o, int r, const uint8_t* lds) {
-  const int e_del = o.e_del, e_ins = o.e_ins, o_del = o.o_del, oe_ins = o.oe_ins;
-  constexpr int KS = CPL > 8 ? 4 : 3;  // bits of the in-lane column in the row-max key
-  const int j0 = r * CPL;
-  const int t = s.tnext;
-  s.tnext = lds[s.tb + s.vi + 1];  // prefetch (the buffer is 2 rows longer than any call reads)
-  s.lo = max(s.lo, s.iw);
-  s.hi = min(min(s.hi, s.iw1), s.qlen);
-  s.iw += 1;
-  s.iw1 += 1;
-  const int lo = s.lo, hi = s.hi;
-  const int wd = usat32(hi, lo);
-  const int left0 = lo == 0 ? max(s.gl, 0) : 0;
-  s.gl -= e_del;
-  const int sh = (t & 3) << 3;
-  const int x = j0 - lo;
-  int M[CPL], A[CPL];
-  int T = 0;  // F carried to the next column from this lane's columns alone (clamped at the end)
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const bool ib = (unsigned)(x + c) < (unsigned)wd;
-    int sc;
-    if (T5 && t == 4) sc = (int)(int8_t)(s.pf4[c] & 0xff);
-    else sc = __builtin_amdgcn_sbfe((int)s.pf[c], sh, 8);
-    const int m = s.hh[c] ? s.hh[c] + sc : 0;
-    M[c] = m;
-    A[c] = (ib ? m : NEG) - oe_ins;  // t_c before the clamp at 0
-    T = max(T - e_ins, A[c]);
-  }
-  // exclusive group scan: F entering the lane's first column is
-  // max(0, max_{r'<r} T_{r'} - (r-1-r')*CPL*e_ins)
-  const int U = T + e_ins * CPL * r;
-  // the band tests are recomputed below rather than kept as 2*CPL live SGPR
-  // masks across the scan (which spilled)
-  int xb = x;
-  asm volatile("" : "+v"(xb));
-  const int inc = max_shr8(max_shr4(max_shr2(max_shr1(U))));
-  const int EX = dpp<DPP_ROW_SHR(1)>(NEG, inc);
-  int f = max(EX - e_ins * CPL * (r - 1), 0);
-  int hm[CPL];
-  int lk = 0;
-  const int hix = hi - j0;
-  int h1c = 0;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const unsigned d = (unsigned)(xb + c);
-    const bool ib = d < (unsigned)wd, ib2 = d <= (unsigned)wd;
-    if (c > 0) f = max(max(f - e_ins, A[c - 1]), 0);
-    const int h = max(max(M[c], s.ee[c]), f);
-    hm[c] = ib ? h : 0;
-    const int en = usat32(max(s.ee[c], M[c] - o_del), e_del);
-    lk = max(lk, (hm[c] << KS) + c);
-    s.ee[c] = ib ? en : (ib2 ? 0 : s.ee[c]);
-    if (c > 0) {
-      s.hh[c] = ib2 ? hm[c - 1] : s.hh[c];
-      h1c = hix == c ? hm[c - 1] : h1c;
-    }
-  }
-  const int hs0 = dpp<DPP_ROW_SHR(1)>(left0, hm[CPL - 1]);  // H(i, j0-1); group lane 0: left0
-  s.hh[0] = (unsigned)xb <= (unsigned)wd ? hs0 : s.hh[0];
-  h1c = hix == 0 ? hs0 : h1c;
-  // band trim for the next row: non-zero columns of the updated state
-  uint32_t nzm = 0;
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) nzm |= (uint32_t)min((uint32_t)(s.hh[c] | s.ee[c]), 1u) << c;
-  const int lo_l = min(max(lo - j0, 0), 31), hi_l = min(max(hi - j0, 0), 31);
-  const uint32_t below_lo = (1u << lo_l) - 1u, below_hi = (1u << hi_l) - 1u;
-  const uint32_t at_hi = (hi_l == hi - j0) ? (1u << hi_l) : 0u;
-  const uint32_t mf = nzm & below_hi & ~below_lo;   // [lo, hi)
-  const uint32_t ml = mf | (nzm & at_hi);            // [lo, hi]
-  const int fcand = mf ? j0 + __builtin_ctz(mf) : 1 << 20;
-  const int lcand = ml ? j0 + 31 - __builtin_clz(ml) : -1;
-  const int key = ((lk >> KS) << 10) | (j0 + (lk & ((1 << KS) - 1)));
-  const int rk = g16_max(key);
-  const int h1 = g16_max(h1c);
-  const int nlo = min(g16_min(fcand), hi);
-  const int jl = max(g16_max(lcand), nlo - 1);
-  const int nhi = min(jl + 2, s.qlen);
-  s.cells += wd;
-  {  // ksw.c:450-453
-    const bool atend = max(lo, hi) == s.qlen;
-    s.ei = (atend && !(s.esc > h1)) ? s.vi : s.ei;
-    s.esc = atend ? max(s.esc, h1) : s.esc;
-  }
-  // ksw.c:454-465 (see extend_wave: updates before the single exit test)
-  const int mrow = rk >> 10, mj = rk & 1023;
-  const bool up = mrow > s.best;
-  const int di = s.vi - s.bi, dj = mj - s.bj;
-  const int drop = s.best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
-  const bool brk = mrow == 0 || (!up && s.zdrop > 0 && drop > s.zdrop);
-  s.off = up ? max(s.off, abs(mj - s.vi)) : s.off;
-  s.best = up ? mrow : s.best;
-  s.bi = up ? s.vi : s.bi;
-  s.bj = up ? mj : s.bj;
-  s.vi += 1;
-  s.lo = nlo;
-  s.hi = nhi;
-  return brk || s.vi >= s.tlen;
-}
-
-template <int CPL, bool T5>
-__device__ __forceinline__ ExtOut gext_out(const GrpExt<CPL, T5>& s) {
-  return ExtOut{s.best, s.bj + 1, s.bi + 1, s.ei + 1, s.esc, s.off};
 }
 
 // rows that extend_group can read for (qlen, w, end_bonus)
@@ -1233,32 +801,17 @@ __global__ void __launch_bounds__(256) chain_prep_kernel(DevOpt o, DevRef ref, D
 constexpr int kCostBins = 256;
 constexpr int kBins = kNumVariants * kCostBins;
 
-// grp: the 16-lane group kernel, sized by the read's longest possible
-// extension (max over its seeds of qbeg, lq - qbeg - len; + 1 column)
-__device__ __forceinline__ int read_variant(const DevBatch& b, int rd, int lq, bool grp) {
+__device__ __forceinline__ int read_variant(const DevBatch& b, int rd, int lq) {
   const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
   const int s0 = b.chain_seed_off[c0], s1 = b.chain_seed_off[c1];
   const bool small = s1 - s0 <= kFastMaxSeeds && c1 - c0 <= kFastMaxChains;
-  if (grp && small && lq <= 256) {
-    int need = 1;
-    bool ok = true;
-    for (int k = s0; k < s1; ++k) {
-      const bwagpu_seed_t t = b.seeds[k];
-      ok = ok && t.qbeg >= 0 && t.len > 0 && t.qbeg + t.len <= lq;
-      need = max(need, max(t.qbeg, lq - t.qbeg - t.len) + 1);
-    }
-    if (ok)
-      for (int k = 0; k < kNumVariants; ++k)
-        if (kVariants[k].kind == VK_GRP && need <= kVariants[k].max_len()) return k;
-  }
   for (int k = 0; k < kNumVariants; ++k)
-    if (kVariants[k].kind != VK_GRP && lq <= kVariants[k].max_len() && (small || kVariants[k].kind != VK_FAST))
-      return k;
+    if (lq <= kVariants[k].max_len() && (small || kVariants[k].kind != VK_FAST)) return k;
   return -1;
 }
 
 __global__ void __launch_bounds__(256) read_bins_kernel(DevBatch b, int32_t* bins, int32_t* hist, int32_t* counts,
-                                                        int64_t* stats, int grp) {
+                                                        int64_t* stats) {
   __shared__ int h[kBins];
   for (int k = threadIdx.x; k < kBins; k += blockDim.x) h[k] = 0;
   __syncthreads();
@@ -1266,7 +819,7 @@ __global__ void __launch_bounds__(256) read_bins_kernel(DevBatch b, int32_t* bin
   int v = -1;
   if (rd < b.n_reads) {
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
-    v = read_variant(b, rd, lq, grp != 0);
+    v = read_variant(b, rd, lq);
     const int c0 = b.read_chain_off[rd], c1 = b.read_chain_off[rd + 1];
     uint32_t cost = 0;
     int nseed = 0;
@@ -1360,10 +913,10 @@ __global__ void __launch_bounds__(256) read_scatter_kernel(DevBatch b, const int
 }
 
 hipError_t launch_read_order(const DevBatch& b, int32_t* bins, int32_t* hist, int32_t* counts, ReadDesc* desc,
-                             int32_t* list, int64_t* stats, bool grp, hipStream_t st) {
+                             int32_t* list, int64_t* stats, hipStream_t st) {
   if (b.n_reads == 0) return hipSuccess;
   const int nb = (b.n_reads + 255) / 256;
-  hipLaunchKernelGGL(read_bins_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, counts, stats, grp ? 1 : 0);
+  hipLaunchKernelGGL(read_bins_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, counts, stats);
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(256), 0, st, hist);
   hipLaunchKernelGGL(read_scatter_kernel, dim3(nb), dim3(256), 0, st, b, bins, hist, desc, list);
   return hipGetLastError();
@@ -1740,10 +1293,7 @@ constexpr int kRegBytes = 88 * kFastMaxSeeds;  // LDS region records per wave
 constexpr int kFastWaveLds(int tb) { return 2 * LaneTab::BYTES + kRegBytes + 2 * tb; }
 
 template <int C>
-#ifndef BWAGPU_FAST_WPE
-#define BWAGPU_FAST_WPE 5  // waves per SIMD the fast kernel is compiled for (A/B builds override)
-#endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWAGPU_FAST_WPE))) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) chain2aln_fast_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
                                                                 int variant, int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int r = (int)(threadIdx.x & 63);
@@ -1925,417 +1475,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWA
   block_stats<64>(tl, a.stats);
 }
 
-// ------------------------------------------------------------ chain2aln, 16-lane groups
-// mem_chain2aln (bwamem.c:641-795) with FOUR reads per wave, one per 16-lane
-// group (one DPP row).  Each group walks its reads, chains and seeds with its
-// own control state (a small state machine, all values group-uniform VGPRs);
-// whenever a group reaches a ksw_extend2 it parks in the DP, and the wave runs
-// the DP rows of every parked group together (gext_row: blocked columns, 16
-// lanes x CPL).  When one group's extension ends, the wave leaves the row loop,
-// that group runs its control code up to its next extension (the only
-// divergent section) and the row loop resumes.
-//
-// Per-read data lives in registers, two items per lane (lane r holds seeds /
-// chains / regions r and r + 16; a read has at most 32 of each) and is read
-// group-uniformly with ds_bpermute; only the read's bases and the two target
-// row buffers of the current seed sit in LDS (kGrpSeq + 2 * tb bytes per
-// group), so occupancy is set by VGPRs.
-constexpr int kGrpSeq = 272;  // a read's bases (<= 256) from its first aligned dword
-
-__device__ __forceinline__ int gperm(int v0, int v1, int idx, int gbase) {
-  const int v = idx < 16 ? v0 : v1;
-  return __builtin_amdgcn_ds_bpermute((gbase + (idx & 15)) << 2, v);
-}
-__device__ __forceinline__ int64_t gperm64(const int64_t* v, int idx, int gbase) {
-  const int lo = gperm((int)(uint32_t)v[0], (int)(uint32_t)v[1], idx, gbase);
-  const int hi = gperm((int)(uint32_t)((uint64_t)v[0] >> 32), (int)(uint32_t)((uint64_t)v[1] >> 32), idx, gbase);
-  return (int64_t)((uint64_t)(uint32_t)hi << 32 | (uint32_t)lo);
-}
-// any / sum over the 16 lanes of the group
-__device__ __forceinline__ bool gany(bool p, int gbase) {
-  return ((__builtin_amdgcn_ballot_w64(p) >> gbase) & 0xffffull) != 0;
-}
-__device__ __forceinline__ int gsum16(int v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
-  return v;
-}
-
-// target rows of the current seed, both sides in one round trip: left rows
-// x0l - k (k < nl) into tbl, right rows x0r + k (k < nr) into tbr.  Lane r
-// takes rows [16r, 16r + 16) of each side per pass: they are 16 consecutive
-// positions of the forward pac (ascending or descending), so two aligned
-// dwords hold them all (bases [16D, 16D + 32), MSB-first per byte as
-// _get_pac, bntseq.c:225); the 16 bytes go to LDS as one 128-bit write.
-// Rows past n are garbage (the buffer is n rounded up to 16 long).
-// A lane whose dword pair would pass the end of the pac buffer (l_pac/4 + 1
-// bytes) reads its rows byte by byte instead.
-__device__ __forceinline__ void fill_side16(uint8_t* tb, int64_t x0, int dir, int n, const DevRef& ref, int r,
-                                            int base) {
-  const int k0 = base + 16 * r;
-  if (k0 >= n) return;
-  const bool rev = x0 >= ref.l_pac;  // a window never spans both strands
-  const int64_t fb = rev ? (ref.l_pac << 1) - 1 - x0 : x0;
-  const int sg = rev ? -dir : dir;
-  const int64_t f0 = sg > 0 ? fb + k0 : fb - k0;  // row k0
-  const int64_t flo = max(sg > 0 ? f0 : f0 - 15, (int64_t)0);
-  const int64_t D = flo >> 4;
-  const int64_t dmax = ((ref.l_pac >> 2) + 1) / 4 - 2;
-  const uint32_t cmask = rev ? 0x03030303u : 0u;  // complement of the reverse strand
-  if (D <= dmax) {
-    const uint32_t* p32 = reinterpret_cast<const uint32_t*>(ref.pac) + D;
-    const uint64_t win64 = (uint64_t)p32[0] | (uint64_t)p32[1] << 32;
-    const int pb = (int)(f0 - 16 * D);
-    uint32_t w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int p = (pb + sg * (4 * q + i)) & 31;
-        v |= ((uint32_t)(win64 >> ((p & ~3) * 2 + 6 - 2 * (p & 3))) & 3u) << (8 * i);
-      }
-      w[q] = v ^ cmask;
-    }
-    *reinterpret_cast<uint4*>(tb + k0) = make_uint4(w[0], w[1], w[2], w[3]);
-  } else {  // the last bytes of the pac: row by row
-#pragma nounroll
-    for (int j = 0; j < 16; ++j) {
-      int64_t f = f0 + sg * j;
-      f = f < 0 ? 0 : (f >= ref.l_pac ? ref.l_pac - 1 : f);
-      const uint32_t bse = ((uint32_t)ref.pac[f >> 2] >> ((~f & 3) << 1)) & 3u;
-      tb[k0 + j] = (uint8_t)(rev ? 3u - bse : bse);
-    }
-  }
-}
-
-__device__ __forceinline__ void fill_two16(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
-                                           const DevRef& ref, int r) {
-  const int n = max(nl, nr);
-  for (int base = 0; base < n; base += 256) {
-    fill_side16(tbl, x0l, -1, nl, ref, r, base);
-    fill_side16(tbr, x0r, 1, nr, ref, r, base);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-enum { GM_READ = 0, GM_SEED, GM_SIDE, GM_DP, GM_EXTDONE, GM_DONE };
-
-template <int CPL>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) chain2aln_grp_kernel(DevOpt o, DevRef ref, DevBatch b, C2AArgs a,
-                                                               int variant, int tb_bytes) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int GPB = kBlock / 16;
-  const int r = (int)(threadIdx.x & 15);
-  const int gbase = (int)(threadIdx.x & 48);
-  const int gib = (int)(threadIdx.x >> 4);
-  const uint32_t sq_off = (uint32_t)(gib * (kGrpSeq + 2 * tb_bytes));
-  const uint32_t tbl_off = sq_off + kGrpSeq, tbr_off = tbl_off + tb_bytes;
-  int base = 0;
-  for (int v = 0; v < variant; ++v) base += a.counts[v];
-  const int n_list = a.counts[variant];
-  // static zig-zag deal over the resident groups (cost-sorted list: LPT-like)
-  const int NG = (int)gridDim.x * GPB, G = (int)blockIdx.x * GPB + gib;
-  auto pos = [&](int round) { return round * NG + ((round & 1) ? NG - 1 - G : G); };
-  long long t_cells = 0, t_rows = 0, t_calls = 0;
-  // scalars picked by side are read into locals first: a select between two
-  // fields of `o` would make the compiler copy the struct to scratch
-  const int pc5 = o.pen_clip5, pc3 = o.pen_clip3, ow = o.w, oa = o.a;
-
-  // ---- group state (group-uniform)
-  int mode = GM_READ, round = 0;
-  int rd = 0, lq = 0, nch = 0, s0 = 0, qa0 = 0;  // qa0: LDS offset of base 0 of the read
-  // the read's seeds (processing order) / chains / regions, two per lane
-  int64_t Srb[2] = {0, 0}, Clo[2] = {0, 0}, Chi[2] = {0, 0}, Rrb[2] = {0, 0}, Rre[2] = {0, 0};
-  int Sx[2] = {0, 0}, Ccs[2] = {0, 0}, Crid[2] = {0, 0}, Cfr[2] = {0, 0}, Rq[2] = {0, 0}, Rw[2] = {0, 0};
-  int c = 0, cs0 = 0, cs1 = 0, e = 0, nreg = 0, rid = 0, frac = 0;
-  uint32_t skipped = 0;
-  int64_t clo = 0, chi = 0, srb = 0, rb = 0, re = 0;
-  int sqb = 0, slen = 0, side = 0, t = 0, score = 0, truesc = 0, qb = 0, qe = 0, sc0 = 0, prev = 0, aw0 = 0, aw1 = 0;
-  GrpExt<CPL, false> s;
-
-  // start the extension of the current side (try t); tlen == 0 ends at once
-  auto start_ext = [&]() {
-    const bool left = side == 0;
-    const int qlen = left ? sqb : lq - sqb - slen;
-    const int64_t x0 = left ? srb - 1 : srb + slen;
-    const int tlen = (int)(left ? srb - clo : chi - x0);
-    const int qa = qa0 + (left ? sqb - 1 : sqb + slen);
-    const int dir = left ? -1 : 1;
-    const int h0 = left ? slen * oa : sc0;  // sc0: the score before this side (a retry keeps h0)
-    const int w = ow << t;
-    aw0 = left ? w : aw0;  // value selects: a conditional lvalue would keep these in scratch
-    aw1 = left ? aw1 : w;
-    gext_init(s, o, r, qlen, [&](int j) { return (int)lds[qa + dir * j]; }, tlen, left ? tbl_off : tbr_off, lds, w,
-              left ? pc5 : pc3, o.zdrop, h0);
-    mode = tlen > 0 ? GM_DP : GM_EXTDONE;
-  };
-
-#ifdef BWAGPU_GRP_STATS
-  // diagnostics: wave time in control vs DP rows, row iterations, group-rows
-  uint64_t st_ctrl = 0, st_dp = 0, st_it = 0, st_gr = 0;
-#endif
-  for (;;) {
-#ifdef BWAGPU_GRP_STATS
-    const uint64_t tc0 = __builtin_amdgcn_s_memtime();
-#endif
-    // ---- control: every group that is not in the DP runs to its next extension
-    while (mode != GM_DP && mode != GM_DONE) {
-      if (mode == GM_READ) {
-        const int p = pos(round);
-        if (p >= n_list) {
-          mode = GM_DONE;
-          break;
-        }
-        ++round;
-        const ReadDesc d = a.desc[base + p];
-        rd = d.rd;
-        lq = d.lq;
-        nch = d.nch;
-        s0 = d.s0;
-        const int ns = d.ns;
-        nreg = 0;
-        skipped = 0;
-        if (ns == 0) {
-          if (r == 0) a.out_n[rd] = 0;
-          continue;
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int i = r + 16 * k;
-          const bwagpu_seed_t sd = a.prog[s0 + min(i, ns - 1)];
-          Srb[k] = sd.rbeg;
-          Sx[k] = sd.qbeg | sd.len << 9 | (sd.pad_ ? 1 << 18 : 0);
-          const int cc = d.c0 + min(i, nch - 1);
-          Ccs[k] = (b.chain_seed_off[cc] - s0) | (b.chain_seed_off[cc + 1] - s0) << 8;
-          const ChainWin wn = a.win[cc];
-          Clo[k] = wn.lo;
-          Chi[k] = wn.hi;
-          Crid[k] = b.chain_rid[cc];
-          Cfr[k] = __float_as_int(b.chain_frac_rep[cc]);
-        }
-        {  // the read's bases, by aligned dwords
-          const uint32_t* q = reinterpret_cast<const uint32_t*>(b.seq) + (d.qoff >> 2);
-          const int ndw = (int)(((d.qoff & 3) + lq + 3) >> 2);
-          uint32_t* sq = reinterpret_cast<uint32_t*>(lds + sq_off);
-          for (int k = r; k < ndw; k += 16) sq[k] = q[k];
-          qa0 = (int)sq_off + (int)(d.qoff & 3);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        c = -1;
-        e = cs1 = 0;
-        mode = GM_SEED;
-      } else if (mode == GM_SEED) {
-        if (e >= cs1) {  // next chain
-          ++c;
-          if (c >= nch) {
-            if (r == 0) a.out_n[rd] = nreg;
-            mode = GM_READ;
-            continue;
-          }
-          const int cs = gperm(Ccs[0], Ccs[1], c, gbase);
-          cs0 = cs & 0xff;
-          cs1 = cs >> 8;
-          e = cs0;
-          clo = gperm64(Clo, c, gbase);
-          chi = gperm64(Chi, c, gbase);
-          if (chi < clo) e = cs1;  // flagged by prep (the reference would assert)
-          rid = gperm(Crid[0], Crid[1], c, gbase);
-          frac = gperm(Cfr[0], Cfr[1], c, gbase);
-          continue;
-        }
-        srb = gperm64(Srb, e, gbase);
-        {
-          const int x = gperm(Sx[0], Sx[1], e, gbase);
-          sqb = x & 511;
-          slen = (x >> 9) & 511;
-        }
-        if (nreg > 0) {
-          // containment in an existing region (bwamem.c:678-697), regions r, r + 16
-          bool hit = false;
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int R_qb = Rq[k] & 511, R_qe = (Rq[k] >> 9) & 511, R_sl = (Rq[k] >> 18) & 511, R_w = Rw[k];
-            const int64_t R_rb = Rrb[k], R_re = Rre[k];
-            const bool inside = !(srb < R_rb || srb + slen > R_re || sqb < R_qb || sqb + slen > R_qe) &&
-                                !(slen - R_sl > .1 * lq);
-            const int qd1 = sqb - R_qb;
-            const int64_t rd1 = srb - R_rb;
-            const int g1 = max_gap_len(o, qd1 < rd1 ? qd1 : (int)rd1);
-            const int bw1 = g1 < R_w ? g1 : R_w;
-            const int qd2 = R_qe - (sqb + slen);
-            const int64_t rd2 = R_re - (srb + slen);
-            const int g2 = max_gap_len(o, qd2 < rd2 ? qd2 : (int)rd2);
-            const int bw2 = g2 < R_w ? g2 : R_w;
-            const bool near = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
-            hit = hit || (r + 16 * k < nreg && inside && near);
-          }
-          if (gany(hit, gbase)) {
-            // an overlapping seed among those already visited (bwamem.c:698-707), seeds r, r + 16
-            bool ov = false;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              const int i = r + 16 * k;
-              const int p_qb = Sx[k] & 511, p_len = (Sx[k] >> 9) & 511, p_flag = Sx[k] >> 18;
-              const int64_t p_rb = Srb[k];
-              const bool a1 = sqb <= p_qb && sqb + slen - p_qb >= slen >> 2 && (int64_t)(p_qb - sqb) != p_rb - srb;
-              const bool b1 = p_qb <= sqb && p_qb + p_len - sqb >= slen >> 2 && (int64_t)(sqb - p_qb) != srb - p_rb;
-              const bool live = i >= cs0 && i < e && !((skipped >> i) & 1u) && p_flag == 0;
-              ov = ov || (live && !(p_len < slen * .95) && (a1 || b1));
-            }
-            if (!gany(ov, gbase)) {
-              skipped |= 1u << e;
-              ++e;
-              continue;
-            }
-          }
-        }
-        // ---- extend (bwamem.c:717-792); both target windows in one round trip
-        {
-          const int qlenL = sqb, qlenR = lq - (sqb + slen);
-          const int64_t x0L = srb - 1, x0R = srb + slen;
-          const int tlenL = (int)(srb - clo), tlenR = (int)(chi - x0R);
-          fill_two16(lds + tbl_off, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0,
-                     lds + tbr_off, x0R, qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref, r);
-        }
-        score = truesc = -1;
-        qb = 0;
-        qe = lq;
-        sc0 = 0;
-        aw0 = aw1 = o.w;
-        rb = srb;
-        re = srb + slen;
-        side = 0;
-        mode = GM_SIDE;
-      } else if (mode == GM_SIDE) {
-        if (side == 0 && sqb == 0) {  // bwamem.c:753
-          score = truesc = slen * o.a;
-          side = 1;
-          continue;
-        }
-        if (side == 1 && lq - sqb - slen == 0) side = 2;  // bwamem.c:781
-        if (side == 2) {
-          // seedcov over the chain's seeds (bwamem.c:784-788), seeds r, r + 16
-          int cov = 0;
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int i = r + 16 * k;
-            const int p_qb = Sx[k] & 511, p_len = (Sx[k] >> 9) & 511;
-            const int64_t p_rb = Srb[k];
-            const bool in =
-                i >= cs0 && i < cs1 && p_qb >= qb && p_qb + p_len <= qe && p_rb >= rb && p_rb + p_len <= re;
-            cov += in ? p_len : 0;
-          }
-          cov = gsum16(cov);
-          // the region as its 88-byte record (rest zero: bwamem.c:718), lane r: dwords r, r + 16
-          const int wmax = aw0 > aw1 ? aw0 : aw1;
-          uint32_t* const dst = reinterpret_cast<uint32_t*>(a.out + s0 + nreg);
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int dw = r + 16 * k;
-            uint32_t v = 0;
-            v = dw == 0 ? (uint32_t)rb : v;
-            v = dw == 1 ? (uint32_t)((uint64_t)rb >> 32) : v;
-            v = dw == 2 ? (uint32_t)re : v;
-            v = dw == 3 ? (uint32_t)((uint64_t)re >> 32) : v;
-            v = dw == 4 ? (uint32_t)qb : v;
-            v = dw == 5 ? (uint32_t)qe : v;
-            v = dw == 6 ? (uint32_t)rid : v;
-            v = dw == 7 ? (uint32_t)score : v;
-            v = dw == 8 ? (uint32_t)truesc : v;
-            v = dw == 13 ? (uint32_t)wmax : v;
-            v = dw == 14 ? (uint32_t)cov : v;
-            v = dw == 17 ? (uint32_t)slen : v;
-            v = dw == 19 ? (uint32_t)frac : v;
-            if (dw < 22) dst[dw] = v;
-          }
-          // the containment fields of region nreg, kept by lane nreg & 15
-          if (r == (nreg & 15)) {
-            const int k = nreg >> 4;
-            const int q = qb | qe << 9 | slen << 18;
-            Rrb[0] = k == 0 ? rb : Rrb[0];
-            Rrb[1] = k == 1 ? rb : Rrb[1];
-            Rre[0] = k == 0 ? re : Rre[0];
-            Rre[1] = k == 1 ? re : Rre[1];
-            Rq[0] = k == 0 ? q : Rq[0];
-            Rq[1] = k == 1 ? q : Rq[1];
-            Rw[0] = k == 0 ? wmax : Rw[0];
-            Rw[1] = k == 1 ? wmax : Rw[1];
-          }
-          ++nreg;
-          ++e;
-          mode = GM_SEED;
-          continue;
-        }
-        sc0 = score;
-        t = 0;
-        prev = score;
-        start_ext();
-      } else {  // GM_EXTDONE
-        const ExtOut x = gext_out(s);
-        t_cells += s.cells;
-        t_rows += s.vi;
-        t_calls += 1;
-        score = x.score;
-        const int aw = side == 0 ? aw0 : aw1;
-        if (t == 0 && !(score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {  // MAX_BAND_TRY (bwamem.c:639)
-          t = 1;
-          prev = score;
-          start_ext();
-          continue;
-        }
-        const bool left = side == 0;
-        const int eb = left ? pc5 : pc3;
-        const bool local = x.gscore <= 0 || x.gscore <= score - eb;
-        if (left) {
-          qb = local ? sqb - x.qle : 0;
-          rb = srb - (local ? x.tle : x.gtle);
-          truesc = local ? score : x.gscore;
-        } else {
-          qe = local ? sqb + slen + x.qle : lq;
-          re = srb + slen + (local ? x.tle : x.gtle);
-          truesc += (local ? score : x.gscore) - sc0;
-        }
-        ++side;
-        mode = GM_SIDE;
-      }
-    }
-    // ---- the DP rows of every parked group, together
-#ifdef BWAGPU_GRP_STATS
-    const uint64_t tc1 = __builtin_amdgcn_s_memtime();
-    st_ctrl += tc1 - tc0;
-#endif
-    if (__builtin_amdgcn_ballot_w64(mode == GM_DP) == 0) break;
-    bool fin = false;
-    do {
-#ifdef BWAGPU_GRP_STATS
-      st_it += 1;
-      st_gr += __builtin_popcountll(__builtin_amdgcn_ballot_w64(mode == GM_DP)) >> 4;
-#endif
-      if (mode == GM_DP) fin = gext_row(s, o, r, lds);
-    } while (__builtin_amdgcn_ballot_w64(mode == GM_DP && fin) == 0);
-    if (mode == GM_DP && fin) mode = GM_EXTDONE;
-#ifdef BWAGPU_GRP_STATS
-    st_dp += __builtin_amdgcn_s_memtime() - tc1;
-#endif
-  }
-#ifdef BWAGPU_GRP_STATS
-  if (g_trace && (threadIdx.x & 63) == 0) {
-    atomicAdd(&g_trace[8 * CPL + 0], (uint32_t)(st_ctrl >> 8));
-    atomicAdd(&g_trace[8 * CPL + 1], (uint32_t)(st_dp >> 8));
-    atomicAdd(&g_trace[8 * CPL + 2], (uint32_t)st_it);
-    atomicAdd(&g_trace[8 * CPL + 3], (uint32_t)st_gr);
-    atomicAdd(&g_trace[8 * CPL + 4], 1u);
-  }
-#endif
-  Tally tl{r == 0 ? t_cells : 0, r == 0 ? t_rows : 0, r == 0 ? t_calls : 0};
-  block_stats<64>(tl, a.stats);
-}
-
 // ------------------------------------------------------------ extend batch
 template <int G, int C, bool T5>
 __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_ext_task_t* __restrict__ tasks,
@@ -2374,72 +1513,6 @@ __global__ void __launch_bounds__(kBlock) extend_kernel(DevOpt o, const bwagpu_e
     if (r != 0) tl = Tally{0, 0, 0};
   }
   block_stats<G>(tl, stats);
-}
-
-// bare task list, 16-lane groups: each group takes tasks li, li + NG, ... and
-// the wave runs the rows of its four groups together until one of them
-// finishes; a finished group stores its result and starts its next task while
-// the others wait (the only divergent section).
-template <int CPL, bool T5>
-__global__ void __launch_bounds__(kBlock) extend_grp_kernel(DevOpt o, const bwagpu_ext_task_t* __restrict__ tasks,
-                                                            const int32_t* __restrict__ task_list, int32_t n_list,
-                                                            const uint8_t* __restrict__ qpool,
-                                                            const uint8_t* __restrict__ tpool, int tb_bytes,
-                                                            bwagpu_ext_result_t* res, int64_t* stats) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int GPB = kBlock / 16;
-  const int gib = (int)(threadIdx.x >> 4);
-  const int r = (int)(threadIdx.x & 15);
-  const int NG = (int)gridDim.x * GPB;
-  const uint32_t tb = (uint32_t)(gib * tb_bytes);
-  int li = (int)blockIdx.x * GPB + gib;
-  long long cells = 0, rows = 0, calls = 0;
-  GrpExt<CPL, T5> s;
-  int k = -1;
-  bool act = false;
-  for (;;) {
-    // groups without a task take the next one (tasks with nothing to do are
-    // answered right here)
-    while (!act && li < n_list) {
-      k = task_list[li];
-      const bwagpu_ext_task_t t = tasks[k];
-      if (t.h0 <= 0 || t.tlen == 0) {
-        // h0 <= 0: the reference asserts (ksw.c:385); tlen == 0: no rows
-        const bwagpu_ext_result_t z = t.h0 <= 0 ? bwagpu_ext_result_t{-1, 0, 0, 0, -1, 0}
-                                                : bwagpu_ext_result_t{t.h0, 0, 0, 0, -1, 0};
-        if (r == 0) res[k] = z;
-        calls += t.h0 > 0;
-        li += NG;
-        continue;
-      }
-      const int nr = rows_needed(o, t.qlen, t.tlen, t.w, t.end_bonus);
-      const uint8_t* tp = tpool + t.toff;
-      for (int base = 0; base < nr; base += 16) lds[tb + min(base + r, nr - 1)] = tp[min(base + r, nr - 1)];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint8_t* q = qpool + t.qoff;
-      gext_init(s, o, r, t.qlen, [&](int j) { return (int)q[j]; }, t.tlen, tb, lds, t.w, t.end_bonus, t.zdrop,
-                t.h0);
-      act = true;
-    }
-    if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-    bool fin = false;
-    do {
-      if (act) fin = gext_row(s, o, r, lds);
-    } while (__builtin_amdgcn_ballot_w64(act && fin) == 0);
-    if (act && fin) {
-      const ExtOut x = gext_out(s);
-      if (r == 0) res[k] = bwagpu_ext_result_t{x.score, x.qle, x.tle, x.gtle, x.gscore, x.max_off};
-      cells += s.cells;
-      rows += s.vi;
-      calls += 1;
-      act = false;
-      li += NG;
-    }
-  }
-  Tally tl{r == 0 ? cells : 0, r == 0 ? rows : 0, r == 0 ? calls : 0};
-  block_stats<64>(tl, stats);
 }
 
 // ------------------------------------------------------------ launchers
@@ -2504,30 +1577,13 @@ static hipError_t launch_c2a_t(const DevOpt& o, const DevRef& ref, const DevBatc
   return hipGetLastError();
 }
 
-size_t grp_group_lds(int tb) { return (size_t)(kGrpSeq + 2 * tb); }
-
-template <int CPL>
-static hipError_t launch_c2a_grp(const DevOpt& o, const DevRef& ref, const DevBatch& b, int variant, int32_t n,
-                                 int tb, const C2AArgs& a, hipStream_t st) {
-  constexpr int GPB = kBlock / 16;
-  const size_t lds = (size_t)GPB * grp_group_lds(tb);
-  const int cap = resident_blocks(chain2aln_grp_kernel<CPL>, lds);
-  const int nb = std::min((n + GPB - 1) / GPB, cap);
-  hipLaunchKernelGGL((chain2aln_grp_kernel<CPL>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, variant, tb);
-  return hipGetLastError();
-}
-
 hipError_t launch_chain2aln(int variant, const DevOpt& o, const DevRef& ref, const DevBatch& b, int32_t max_list,
                             int tb_bytes, const C2AArgs& a, hipStream_t st) {
   if (max_list == 0) return hipSuccess;
   switch (variant) {
-    case 0: return launch_c2a_grp<4>(o, ref, b, 0, max_list, tb_bytes, a, st);
-    case 1: return launch_c2a_grp<8>(o, ref, b, 1, max_list, tb_bytes, a, st);
-    case 2: return launch_c2a_grp<10>(o, ref, b, 2, max_list, tb_bytes, a, st);
-    case 3: return launch_c2a_grp<16>(o, ref, b, 3, max_list, tb_bytes, a, st);
-    case 4: return launch_c2a_fast<3>(o, ref, b, 4, max_list, tb_bytes, a, st);
-    case 5: return launch_c2a_fast<4>(o, ref, b, 5, max_list, tb_bytes, a, st);
-    case 6: return launch_c2a_t<64, 16>(o, ref, b, 6, max_list, tb_bytes, a, st);
+    case 0: return launch_c2a_fast<3>(o, ref, b, 0, max_list, tb_bytes, a, st);
+    case 1: return launch_c2a_fast<4>(o, ref, b, 1, max_list, tb_bytes, a, st);
+    case 2: return launch_c2a_t<64, 16>(o, ref, b, 2, max_list, tb_bytes, a, st);
   }
   return hipErrorInvalidValue;
 }
@@ -2541,32 +1597,6 @@ static hipError_t launch_ext_t(const DevOpt& o, const bwagpu_ext_task_t* tasks, 
   hipLaunchKernelGGL((extend_kernel<G, C, T5>), dim3(nb), dim3(kBlock), (size_t)GPB * tb, st, o, tasks, list, n,
                      qp, tp, tb, res, stats);
   return hipGetLastError();
-}
-
-template <int CPL, bool T5>
-static hipError_t launch_ext_grp_t(const DevOpt& o, const bwagpu_ext_task_t* tasks, const int32_t* list, int32_t n,
-                                   const uint8_t* qp, const uint8_t* tp, int tb, bwagpu_ext_result_t* res,
-                                   int64_t* stats, hipStream_t st) {
-  constexpr int GPB = kBlock / 16;
-  const size_t lds = (size_t)GPB * tb;
-  const int cap = resident_blocks(extend_grp_kernel<CPL, T5>, lds);
-  const int nb = std::min((n + GPB - 1) / GPB, cap);
-  hipLaunchKernelGGL((extend_grp_kernel<CPL, T5>), dim3(nb), dim3(kBlock), lds, st, o, tasks, list, n, qp, tp, tb,
-                     res, stats);
-  return hipGetLastError();
-}
-
-hipError_t launch_extend_grp(int cpl, bool t5, const DevOpt& o, const bwagpu_ext_task_t* tasks,
-                             const int32_t* task_list, int32_t n_list, const uint8_t* qpool, const uint8_t* tpool,
-                             int tb_bytes, bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st) {
-  if (n_list == 0) return hipSuccess;
-  if (cpl == 4)
-    return t5 ? launch_ext_grp_t<4, true>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st)
-              : launch_ext_grp_t<4, false>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st);
-  if (cpl == 8)
-    return t5 ? launch_ext_grp_t<8, true>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st)
-              : launch_ext_grp_t<8, false>(o, tasks, task_list, n_list, qpool, tpool, tb_bytes, res, stats, st);
-  return hipErrorInvalidValue;
 }
 
 hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t, const bwagpu_ext_task_t* tasks,
@@ -2957,10 +1987,8 @@ __device__ __forceinline__ bwagpu_seed_t uni_seed(const bwagpu_seed_t& s) {
 }
 
 // Extension tasks of one list (round * kSpecBins + bin): one wave per task,
-// claimed BWAGPU_EXT_CLAIM at a time from the sharded queue.
-#ifndef BWAGPU_EXT_CLAIM
-#define BWAGPU_EXT_CLAIM 1
-#endif
+// claimed one at a time from the sharded queue (a wave holding a second task
+// while others idle at the end of the list cost more: DESIGN.md §5).
 template <int C>
 __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
                                                           int tb_bytes) {
@@ -2974,8 +2002,8 @@ __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, 
   qq.init(a.qh + 8 * kQHStride * list, n);
   long long spec_cells = 0;
   int m0, cap;
-  while (qq.claim(BWAGPU_EXT_CLAIM, m0, cap)) {
-    for (int m = m0; m < m0 + BWAGPU_EXT_CLAIM && m < cap; ++m) {
+  while (qq.claim(1, m0, cap)) {
+    for (int m = m0; m < m0 + 1 && m < cap; ++m) {
       const int2 tk = tl[qq.shard + 8 * m];
       const int pos = uni(tk.x), c = uni(tk.y);
       const int rd = uni(a.chain_read[c]);
@@ -3154,22 +2182,15 @@ __device__ __forceinline__ void store_ext_half(SeedExt* dst, const SeedExt& e) {
 // PMAX = the bin's largest CPL: ceil(read length / 32) (qlen + 1 <= read length)
 template <int PMAX>
 __global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
-                                                           int tb_bytes, int sorted, int lane) {
+                                                           int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int hf = (int)(threadIdx.x >> 5) & 1;
   // per half: left rows, right rows, the task context
   uint8_t* const tbl = lds + (size_t)(threadIdx.x >> 5) * (2 * tb_bytes + sizeof(PairCtx));
   uint8_t* const tbr = tbl + tb_bytes;
   LdsCtx* const cx = (LdsCtx*)(tbr + tb_bytes);
-  int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const int2* tl = (sorted ? a.stasks : a.tasks) + spec_list_off(list, b.n_chains, b.n_seeds);
-  if (lane) {  // the first n_lane sorted tasks are spec_extl_kernel's
-    const int round = list / kSpecBins, bin = list % kSpecBins;
-    const int nl = uni(__hip_atomic_load(&a.sorth[(round * 2 + bin) * kSortKeys + kLaneKeys - 1], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT));
-    tl += nl;
-    n -= nl;
-  }
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);  // in pair order (spec_sort_*)
   ShardQ qq;
   qq.init(a.qh + 8 * kQHStride * list, n);
   long long spec_cells = 0;
@@ -3207,272 +2228,6 @@ __global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref,
 // LDS bytes of a spec_ext2_kernel workgroup
 static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size_t)tb_bytes + sizeof(PairCtx)); }
 
-// ---------------------------------------------------- one seed per lane
-// The short tasks of a list — both sides' qlen <= kLaneQ — run one seed per
-// LANE: each lane is a scalar ksw_extend2 (ksw.c:380-479, in the row-major form
-// of oracle/ksw_ext.c) with its eh[] row in LDS, and walks its own seed through
-// extend_seed (bwamem.c:717-792) as a state machine.  The wave steps every
-// lane's current DP row together; a lane whose seed is done stores its SeedExt
-// and claims the next task at once (wave-aggregated), so lanes do not wait
-// for the end of the wave's longest task, only for its widest row.  Per DP
-// cell: two LDS reads (the packed H|E word, the query's score shift), one LDS
-// write and ~18 VALU, against one row's scans and reductions per 32 columns
-// in extend_pair, whose per-row fixed cost dominates at short qlens.
-// Opt-in (BWAGPU_EXT_LANE / bwagpu_debug_ext_lane): a lane runs its seed
-// serially, and the measured launch is set by that latency (61 vs ~270
-// Gcells/s).
-//
-// LDS per wave: eh[j][lane] = H(i-1, j-1) | E(i, j) << 16 (both >= 0 and
-// < 2^16: scores stay below 1024 * max(mat) for reads up to 1023 bp), and
-// qs[j][lane] = 6 * query base: the score of target base t against query base
-// q is the signed 6-bit field q of a per-row word (host check: every mat
-// entry in [-32, 31]).  The lane index is the fastest dimension, so lanes at
-// different columns never share an LDS bank for the 32-bit words.
-static_assert(kLaneQ + 1 <= 1024 && (kLaneQ & 7) == 7, "lane kernel: qlen bound");
-constexpr size_t kLaneLds = (size_t)(kLaneQ + 1) * 64 * 5;  // 20480 B per wave at kLaneQ 63 (qs has a spare row)
-
-// pac byte p, clamped into the array (l_pac / 4 + 1 bytes): a prefetch past
-// either end of a window is never used
-__device__ __forceinline__ uint32_t pac_byte(const DevRef& ref, int64_t p) {
-  p = p < 0 ? 0 : (p > (ref.l_pac >> 2) ? (ref.l_pac >> 2) : p);
-  return ref.pac[p];
-}
-
-__global__ void __launch_bounds__(64) spec_extl_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = (int)(threadIdx.x & 63);
-  uint32_t* const eh = reinterpret_cast<uint32_t*>(lds) + lane;  // column j at eh[64 j]
-  uint8_t* const qs = lds + (size_t)(kLaneQ + 1) * 64 * 4 + lane;  // column j at qs[64 j]
-  const int round = list / kSpecBins, bin = list % kSpecBins;
-  const int n_lane = __hip_atomic_load(&a.sorth[(round * 2 + bin) * kSortKeys + kLaneKeys - 1], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
-  int32_t* head = a.qh + kQHLaneBase + list * kQHStride;
-  uint32_t S0 = 0, S1 = 0, S2 = 0, S3 = 0;  // per target base: the five scores as 6-bit fields
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    S0 |= (uint32_t)(o.mat[0 * 5 + q] & 63) << (6 * q);
-    S1 |= (uint32_t)(o.mat[1 * 5 + q] & 63) << (6 * q);
-    S2 |= (uint32_t)(o.mat[2 * 5 + q] & 63) << (6 * q);
-    S3 |= (uint32_t)(o.mat[3 * 5 + q] & 63) << (6 * q);
-  }
-  const int e_del = o.e_del, e_ins = o.e_ins, oe_del = o.oe_del, oe_ins = o.oe_ins;
-  // the task (seed) and its extend_seed state
-  int pos = -1, qbeg = 0, len = 0, lq = 0, phase = 4;
-  int64_t rbeg = 0, wlo = 0, whi = 0, qoff = 0, rb = 0, re = 0;
-  int score = 0, truesc = 0, qb = 0, qe = 0, sc0 = 0, aw0 = 0, aw1 = 0, cells = 0, rows = 0, calls = 0;
-  // the current ksw_extend2 call
-  bool incall = false, alive = true;
-  int qlen = 0, tlen = 0, h0 = 0, w = 0, i = 0, lo = 0, hi = 0;
-  int best = 0, bi = -1, bj = -1, ei = -1, esc = -1, off = 0;
-  // the target row's base of row i: pac position f = f0 + fd * i of one strand
-  // (rev: complemented); its byte and the next one in the walk are held, the
-  // one after is loaded when the walk enters a new byte (4 rows ahead)
-  int64_t f0 = 0, fcur = 0;
-  int fd = 1;
-  bool rev = false;
-  uint32_t tb0 = 0, tb1 = 0;
-  const uint32_t* const seqw = reinterpret_cast<const uint32_t*>(b.seq);
-  const int64_t seq_last_w = (b.seq_off[b.n_reads] - 1) >> 2;
-  long long spec_cells = 0;
-  for (;;) {
-    if (alive && !incall && phase >= 4) {  // the seed is done (or none yet): store it, take the next
-      if (pos >= 0) {
-        SeedExt e;
-        e.rb = rb;
-        e.re = re;
-        e.qb = qb;
-        e.qe = qe;
-        e.score = score;
-        e.truesc = truesc;
-        e.w = aw0 > aw1 ? aw0 : aw1;
-        e.cells = cells;
-        e.rows = rows;
-        e.calls = calls + 1;  // + 1: a computed slot is never all-zero
-        a.ext[pos] = e;
-        spec_cells += cells;
-        pos = -1;
-      }
-      const int m = wave_append(head, true);
-      if (m >= n_lane) {
-        alive = false;
-      } else {
-        const int2 tk = tl[m];
-        pos = tk.x;
-        const int c = tk.y;
-        const int rd = a.chain_read[c];
-        const bwagpu_seed_t s = a.prog[pos];
-        const ChainWin cw = a.win[c];
-        qoff = b.seq_off[rd];
-        lq = (int)(b.seq_off[rd + 1] - qoff);
-        rbeg = s.rbeg;
-        qbeg = s.qbeg;
-        len = s.len;
-        wlo = cw.lo;
-        whi = cw.hi;
-        const int qlenR = lq - (qbeg + len);
-        phase = qbeg != 0 ? 0 : (qlenR != 0 ? 2 : 4);
-        score = qbeg != 0 ? -1 : len * o.a;  // bwamem.c:753
-        truesc = score;
-        qb = 0;
-        qe = lq;
-        sc0 = 0;
-        aw0 = aw1 = o.w;
-        rb = rbeg;
-        re = rbeg + len;
-        cells = rows = calls = 0;
-      }
-    }
-    if (alive && !incall && phase < 4) {  // set up the next ksw_extend2 call of the seed
-      const bool left = phase < 2;
-      const int t = phase & 1;
-      const int qlenR = lq - (qbeg + len);
-      qlen = left ? qbeg : qlenR;
-      const int64_t x0 = left ? rbeg - 1 : rbeg + len;
-      tlen = left ? (int)(rbeg - wlo) : (int)(whi - x0);
-      rev = x0 >= ref.l_pac;  // the window lies on one strand (finish_window)
-      f0 = rev ? (ref.l_pac << 1) - 1 - x0 : x0;
-      fd = (rev ? -1 : 1) * (left ? -1 : 1);
-      fcur = f0 >> 2;
-      tb0 = pac_byte(ref, fcur);
-      tb1 = pac_byte(ref, fcur + fd);
-      const int qa = left ? qbeg - 1 : qbeg + len, qd = left ? -1 : 1;
-      const int eb = left ? o.pen_clip5 : o.pen_clip3;
-      if (t == 0) sc0 = score;
-      h0 = left ? len * o.a : sc0;
-      w = o.w << t;
-      if (left) aw0 = w;
-      else aw1 = w;
-      const int mi = band_cap_dev(qlen, o.max_mat, eb, o.o_ins, e_ins);
-      const int md = band_cap_dev(qlen, o.max_mat, eb, o.o_del, e_del);
-      w = min(w, min(mi, md));
-      // the query's score shifts: its bytes [first, first + qlen) of seq in
-      // (kLaneQ + 4) / 4 + 1 word loads issued together (not one dependent byte
-      // load per column), then column j <- byte qa + qd * j
-      {
-        const int64_t first = qoff + (left ? qa - (qlen - 1) : qa);
-        const int64_t w0 = first >> 2;
-        const int sh0 = (int)(first & 3);
-        constexpr int NW = (kLaneQ + 4) / 4 + 1;
-        uint32_t wv[NW];
-#pragma unroll
-        for (int k = 0; k < NW; ++k) wv[k] = 4 * k < sh0 + qlen ? seqw[min(w0 + k, seq_last_w)] : 0u;
-#pragma unroll
-        for (int t = 0; t < 4 * NW; ++t) {
-          const int u = t - sh0;  // byte first + u
-          const int j = qd > 0 ? u : qlen - 1 - u;
-          if (u >= 0 && u < qlen) qs[64 * j] = (uint8_t)(6 * ((wv[t >> 2] >> (8 * (t & 3))) & 0xffu));
-        }
-      }
-      // eh row -1 (ksw.c:392-395)
-      for (int j = 0; j <= qlen; ++j) eh[64 * j] = (uint32_t)(j == 0 ? h0 : max(h0 - oe_ins - (j - 1) * e_ins, 0));
-      best = h0;
-      bi = bj = ei = -1;
-      esc = -1;
-      off = 0;
-      lo = 0;
-      hi = qlen;
-      i = 0;
-      incall = true;
-    }
-    if (!__builtin_amdgcn_ballot_w64(alive)) break;
-    if (incall) {  // one DP row of the lane's call (oracle/ksw_ext.c's loop body)
-      bool end = i >= tlen;
-      if (!end) {
-        const int64_t fp = f0 + (int64_t)fd * i;
-        if ((fp >> 2) != fcur) {  // entered the next byte: shift, load the one after
-          fcur = fp >> 2;
-          tb0 = tb1;
-          tb1 = pac_byte(ref, fcur + fd);
-        }
-        const int bse = (int)(tb0 >> ((~(int)fp & 3) << 1)) & 3;
-        const int t = rev ? 3 - bse : bse;
-        const uint32_t S = t == 0 ? S0 : (t == 1 ? S1 : (t == 2 ? S2 : S3));
-        lo = max(lo, i - w);
-        hi = min(min(hi, i + w + 1), qlen);
-        int left = lo == 0 ? max(h0 - (o.o_del + e_del * (i + 1)), 0) : 0;
-        int f = 0, rk = -1;
-        const int l0 = min(lo, kLaneQ);  // lo > qlen only on an empty last row
-        uint32_t hw = eh[64 * l0];       // column j's words are read one column ahead
-        int q6 = qs[64 * l0];
-        for (int j = lo; j < hi; ++j) {
-          const uint32_t hwn = eh[64 * (j + 1)];  // j + 1 <= qlen <= kLaneQ: in the lane's rows
-          const int q6n = qs[64 * (j + 1)];
-          int mv = (int)(hw & 0xffffu);
-          const int ev = (int)(hw >> 16);
-          const int sc = __builtin_amdgcn_sbfe((int)S, q6, 6);
-          mv = mv ? mv + sc : 0;
-          const int h = max(max(mv, ev), f);
-          rk = max(rk, (h << 10) | j);  // ties -> the last column (ksw.c:436-437)
-          const int en = max(max(ev - e_del, mv - oe_del), 0);
-          f = max(max(f - e_ins, mv - oe_ins), 0);
-          eh[64 * j] = (uint32_t)left | ((uint32_t)en << 16);
-          left = h;
-          hw = hwn;
-          q6 = q6n;
-        }
-        eh[64 * hi] = (uint32_t)left;  // {H(i, hi-1), 0}
-        cells += max(hi - lo, 0);
-        rows += 1;
-        if (max(lo, hi) == qlen) {  // ksw.c:450-453
-          if (!(esc > left)) ei = i;
-          esc = max(esc, left);
-        }
-        const int rmax = rk >> 10, rarg = rk & 1023;
-        if (rmax <= 0) {
-          end = true;
-        } else if (rmax > best) {
-          best = rmax;
-          bi = i;
-          bj = rarg;
-          off = max(off, abs(rarg - i));
-        } else if (o.zdrop > 0) {
-          const int di = i - bi, dj = rarg - bj;
-          const int drop = di > dj ? best - rmax - (di - dj) * e_del : best - rmax - (dj - di) * e_ins;
-          end = drop > o.zdrop;
-        }
-        if (!end) {  // the zero-trimmed band (ksw.c:466-469)
-          int j = lo;
-          while (j < hi && eh[64 * j] == 0u) ++j;
-          lo = j;
-          j = hi;
-          while (j >= lo && eh[64 * j] == 0u) --j;
-          hi = min(j + 2, qlen);
-          end = ++i >= tlen;
-        }
-      }
-      if (end) {  // the call's result -> extend_seed (bwamem.c:717-792)
-        incall = false;
-        calls += 1;
-        const bool left = phase < 2;
-        const int t = phase & 1;
-        const int qlenR = lq - (qbeg + len);
-        const int aw = o.w << t;
-        const int eb = left ? o.pen_clip5 : o.pen_clip3;
-        const int prev = score;
-        score = best;
-        if (t == 0 && !(score == prev || off < (aw >> 1) + (aw >> 2))) {
-          phase += 1;  // the band retry
-        } else {
-          const bool local = esc <= 0 || esc <= score - eb;
-          if (left) {
-            qb = local ? qbeg - (bj + 1) : 0;
-            rb = rbeg - (local ? bi + 1 : ei + 1);
-            truesc = local ? score : esc;
-            phase = qlenR != 0 ? 2 : 4;
-          } else {
-            qe = local ? qbeg + len + bj + 1 : lq;
-            re = (rbeg + len) + (local ? bi + 1 : ei + 1);
-            truesc = truesc + (local ? score : esc) - sc0;
-            phase = 4;
-          }
-        }
-      }
-    }
-  }
-  if (spec_cells) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
-}
-
 // Task order for the pair kernel: the two seeds a wave takes should need the
 // same phases for about as long — a half whose seed has no left side, or a
 // much shorter one, idles while the other runs (EXEC).  A counting sort of
@@ -3482,19 +2237,15 @@ __global__ void __launch_bounds__(64) spec_extl_kernel(DevOpt o, DevRef ref, Dev
 // per block and key to reserve the block's range).  Claims then take entries
 // 8 apart in the sorted list (the sharded queue), which have about the same
 // key.  The order changes nothing but which seeds share a wave.
-__device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, int2 tk, int lane) {
+__device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, int2 tk) {
   const bwagpu_seed_t s = a.prog[tk.x];
   const int rd = a.chain_read[tk.y];
   const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
   const int ql = min(s.qbeg, 255), qr = min(max(lq - s.qbeg - s.len, 0), 255);
-  const int k = (ql >> 3) << 5 | (qr >> 3);
-  if (!lane) return k;
-  // the lane kernel's tasks first, the larger ones first (LPT order)
-  if (ql <= kLaneQ && qr <= kLaneQ) return (kLaneKeys - 1) - ((ql >> 3) + (qr >> 3));
-  return min(k + kLaneKeys - ((kLaneQ + 1) >> 3), kSortKeys - 1);  // k >= (kLaneQ + 1) / 8 here
+  return (ql >> 3) << 5 | (qr >> 3);
 }
 
-__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round, int lane) {
+__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
   __shared__ int hist[kSortKeys];
   const int list = round * kSpecBins + (int)blockIdx.y;
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
@@ -3504,7 +2255,7 @@ __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, i
   const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
   const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
   const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
-  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) atomicAdd(&hist[pair_key(b, a, tl[i], lane)], 1);
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) atomicAdd(&hist[pair_key(b, a, tl[i])], 1);
   __syncthreads();
   for (int k = threadIdx.x; k < kSortKeys; k += 256)
     if (hist[k]) atomicAdd(&gh[k], hist[k]);
@@ -3536,7 +2287,7 @@ __global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
   }
 }
 
-__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round, int lane) {
+__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round) {
   __shared__ int cnt[kSortKeys];
   const int list = round * kSpecBins + (int)blockIdx.y;
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
@@ -3558,7 +2309,7 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
       keys[m] = -1;
       if (i < i1) {
         tk[m] = tl[i];
-        keys[m] = pair_key(b, a, tk[m], lane);
+        keys[m] = pair_key(b, a, tk[m]);
         rank[m] = atomicAdd(&cnt[keys[m]], 1);
       }
     }
@@ -3577,77 +2328,24 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
   }
 }
 
-// The extension rounds' first two length bins run two seeds per wave
-// (spec_ext2_kernel) on key-sorted lists by default.  BWAGPU_EXT_PAIR: 0 = one
-// seed per wave (spec_ext_kernel), 1 = pairs in list order, 2 (default) =
-// pairs of sorted tasks.  A/B on the C2 bench: 0.89-0.91 vs
-// 0.92-0.94 ms per C = 3 launch, 3.25-3.35 vs 3.47-3.50 ms per step; mode 1
-// 1.07 ms (a third of the lanes idle while the other half's seed runs).
-static int ext_pair_mode() {
-  static const int v = [] {
-    const char* e = getenv("BWAGPU_EXT_PAIR");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-static bool ext_pair_enabled() { return ext_pair_mode() != 0; }
 // The pair kernel's grid: its waves pull tasks from the queue, so the grid
-// only sets its occupancy.  Default: 2 workgroups per CU (8 waves per CU, 2
-// per SIMD) instead of the resident capacity (5 per SIMD): the batch on the
-// other caller stream (the bench's ping-pong) and this batch's selection
-// kernels keep the rest, and an even count per CU beats an uneven one.
-// Same-box sweep: capacity 19.87, 60 % 20.74, 50 % 20.66,
-// 2/CU (40 %) 21.74, 30 % 20.16, 1/CU 19.72 Mreads/s.
-// BWAGPU_EXT2_GRID_PCT (percent of capacity) or BWAGPU_EXT2_BLOCKS_PER_CU override.
-static int ext2_grid(int nb, int round) {
-  static const int pct = [] {
-    const char* e = getenv("BWAGPU_EXT2_GRID_PCT");
-    const int v = e ? atoi(e) : 0;
-    return v <= 0 ? 0 : (v < 10 ? 10 : (v > 100 ? 100 : v));
-  }();
-  if (pct) return std::max(1, nb * pct / 100);
+// only sets its occupancy.  2 workgroups per CU (8 waves per CU, 2 per SIMD)
+// instead of the resident capacity (5 per SIMD): the batch on the other caller
+// stream (the bench's ping-pong) and this batch's selection kernels keep the
+// rest, and an even count per CU beats an uneven one.  Same-box sweep
+// (DESIGN.md §3): capacity 19.87, 60 % 20.74, 50 % 20.66, 2/CU (40 %) 21.74,
+// 30 % 20.16, 1/CU 19.72 Mreads/s.  BWAGPU_EXT2_BLOCKS_PER_CU overrides.
+static int ext2_grid(int nb) {
   static const int per_cu = [] {
     const char* e = getenv("BWAGPU_EXT2_BLOCKS_PER_CU");
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : v;
   }();
-  static const int per_cu_b = [] {  // rounds B and C (BWAGPU_EXT2_BLOCKS_PER_CU_B; default: the same)
-    const char* e = getenv("BWAGPU_EXT2_BLOCKS_PER_CU_B");
-    const int v = e ? atoi(e) : 0;
-    return v < 0 ? 0 : v;
-  }();
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
     return nb;
-  const int k = round > 0 && per_cu_b ? per_cu_b : per_cu;
-  return std::max(1, std::min(nb, k * ncu));
-}
-// Short tasks one per lane (spec_extl_kernel) beside the pair kernel, on sorted
-// lists only.  BWAGPU_EXT_LANE: 0 (default) = off, 1 = before the pair kernel
-// on the same stream, 2 = concurrently on the side stream (A/B: DESIGN.md §3).
-static std::atomic<int> g_ext_lane{-1};  // -1: not read from the environment yet
-static int ext_lane_mode() {
-  int v = g_ext_lane.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("BWAGPU_EXT_LANE");
-    int want = e ? atoi(e) : 0;
-    want = want < 0 ? 0 : (want > 2 ? 2 : want);
-    g_ext_lane.compare_exchange_strong(v, want);
-    v = g_ext_lane.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-int set_ext_lane_mode(int mode) {  // process-wide; -> the previous mode (mode < 0: query only)
-  const int prev = ext_lane_mode();
-  if (mode >= 0) g_ext_lane.store(mode > 2 ? 2 : mode, std::memory_order_relaxed);
-  return prev;
-}
-// the lane kernel's 6-bit score fields need every mat entry in [-32, 31]
-static bool lane_scores_ok(const DevOpt& o) {
-  for (int k = 0; k < 25; ++k)
-    if (o.mat[k] < -32 || o.mat[k] > 31) return false;
-  return true;
+  return std::max(1, std::min(nb, per_cu * ncu));
 }
 
 // ============================================================ FPGA wire format
@@ -3756,8 +2454,8 @@ __global__ void __launch_bounds__(kBlock) stream_ext_kernel(DevOpt o, DevRef ref
   ShardQ qq;
   qq.init(a.ctr + kStrHeads + 8 * kQHStride * bin, n);
   int m0, cap;
-  while (qq.claim(BWAGPU_EXT_CLAIM, m0, cap)) {
-    for (int m = m0; m < m0 + BWAGPU_EXT_CLAIM && m < cap; ++m) {
+  while (qq.claim(1, m0, cap)) {
+    for (int m = m0; m < m0 + 1 && m < cap; ++m) {
       const int t = uni(L[qq.shard + 8 * m]);
       const StreamTask& T = a.tasks[t];
       const bwagpu_seed_t s = uni_seed(T.s);
@@ -4114,19 +2812,12 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
 // round-B task (pending: neither extended nor skipped, as in the per-seed
 // form); SEL_FINAL sends the read to the redo pass.
 // A misprediction in the final pass of a light read (a seed the replay must
-// extend has no result: ~10-20 per C2 batch) is extended inline
-// (BWAGPU_LIGHT_INLINE=1, the default), which takes the kernel to 129 VGPRs
-// (3 waves per SIMD).  0 sends it to round C + the redo pass like one of a
-// longer read (82 VGPRs): bit-exact, but 19.8-19.9 vs 21.6-21.7 Mreads/s on
-// C2 (C3 1.04 vs 1.12-1.20 ms per batch), DESIGN.md §3.
-#ifndef BWAGPU_LIGHT_INLINE
-#define BWAGPU_LIGHT_INLINE 1
-#endif
+// extend has no result: ~10-20 per C2 batch) is extended inline, which takes
+// the kernel to 129 VGPRs (3 waves per SIMD).  Sending it to round C + the
+// redo pass like one of a longer read instead (82 VGPRs) is bit-exact, but
+// measured 19.8-19.9 vs 21.6-21.7 Mreads/s on C2.
 template <int MODE>
-#ifndef BWAGPU_LIGHT_WPE
-#define BWAGPU_LIGHT_WPE 1  // no occupancy cap: 6 waves/SIMD (80 VGPRs, spills) measured 5% slower per batch
-#endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWAGPU_LIGHT_WPE))) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
+__global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
                                                             int tb_bytes) {
   constexpr bool WRITE = MODE != SEL_EMULATE;
   __shared__ int32_t MG[kMglN];
@@ -4285,7 +2976,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWA
       const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
       if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
     } else {
-      if (BWAGPU_LIGHT_INLINE && miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
+      if (miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
         const bwagpu_seed_t sm = uni_seed(a.prog[d.s0 + miss]);
         const int cm_id = uni(__shfl(cid, miss, 64));
         ChainWin cw = a.win[d.c0 + cm_id];
@@ -4298,7 +2989,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BWA
         __builtin_amdgcn_wave_barrier();
         continue;
       }
-      if (miss >= 0) {  // round C + the redo pass (BWAGPU_LIGHT_INLINE=1: reads > 160 bp only)
+      if (miss >= 0) {  // round C + the redo pass (reads > 160 bp)
         const int list = 2 * kSpecBins + spec_bin(d.lq);
         if (r == miss) {
           const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
@@ -4594,30 +3285,9 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
   if constexpr (WRITE) block_stats<64>(tl, a.stats);
 }
 
-// BWAGPU_LIGHT_BLOCKS_PER_CU: spec_select_light's grid in workgroups per CU
-// (0 = the resident capacity)
-static int light_grid(int nb) {
-  static const int per_cu = [] {
-    const char* e = getenv("BWAGPU_LIGHT_BLOCKS_PER_CU");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
-  int dev = 0, ncu = 0;
-  if (!per_cu || hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-    return nb;
-  return std::max(1, std::min(nb, per_cu * ncu));
-}
-
-// BWAGPU_SCAN_GRID: spec_scan_kernel's grid (one wave per workgroup, a static
-// stride over the heavy reads; default 1024)
-static int scan_grid() {
-  static const int v = [] {
-    const char* e = getenv("BWAGPU_SCAN_GRID");
-    const int g = e ? atoi(e) : 1024;
-    return g < 64 ? 64 : (g > 8192 ? 8192 : g);
-  }();
-  return v;
-}
+// spec_scan_kernel's grid: one wave per workgroup, a static stride over the
+// heavy reads (256-2048 measured within the noise)
+constexpr int kScanGrid = 1024;
 
 // The two selection shapes of one pass: heavy reads on `side` (when given)
 // concurrently with the light reads on `st`; `st` continues once both are done.
@@ -4632,13 +3302,13 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
   }
   if (MODE != SEL_REDO) {
     const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
-    const int nb = light_grid(resident_blocks(spec_select_light<MODE>, lds));
+    const int nb = resident_blocks(spec_select_light<MODE>, lds);
     hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
   }
   if (MODE != SEL_REDO) {  // heavy reads with pair matrices: all pairs at once, then one scan per read
     const int nb = resident_blocks(spec_pairs_kernel, 0);
     hipLaunchKernelGGL(spec_pairs_kernel, dim3(nb), dim3(kBlock), 0, hs, o, b, a, MODE == SEL_FINAL ? 1 : 0);
-    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(scan_grid()), dim3(64), (size_t)kScanLds + 2 * (size_t)tb_bytes, hs, o,
+    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(kScanGrid), dim3(64), (size_t)kScanLds + 2 * (size_t)tb_bytes, hs, o,
                        ref, b, a, tb_bytes);
   }
   // the rest (no matrix; the redo list): one wave per read, per seed
@@ -4654,56 +3324,24 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
                              int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
-  const bool pair = ext_pair_enabled();
   const size_t lds2 = ext2_lds(tb_bytes);
-  const int sorted = ext_pair_mode() == 2 ? 1 : 0;
-  const int lmode = pair && sorted && lane_scores_ok(o) ? ext_lane_mode() : 0;
-  const int lane = lmode ? 1 : 0;
-  if (pair && sorted) {
-    hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round, lane);
-    hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
-    hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round, lane);
-  }
-  // the lane kernel of list `li` on the side stream (mode 2) or on st (mode 1)
-  const bool conc = lmode == 2 && ss.side;
-  const int nbl = lane ? resident_blocks(spec_extl_kernel, kLaneLds) : 0;
-  auto lane_launch = [&](int li) {
-    if (conc) {
-      (void)hipEventRecord(ss.fork, st);
-      (void)hipStreamWaitEvent(ss.side, ss.fork, 0);
-    }
-    hipLaunchKernelGGL(spec_extl_kernel, dim3(nbl), dim3(64), kLaneLds, conc ? ss.side : st, o, ref, b, a, li);
-  };
-  auto lane_join = [&]() {
-    if (conc) {
-      (void)hipEventRecord(ss.join, ss.side);
-      (void)hipStreamWaitEvent(st, ss.join, 0);
-    }
-  };
-  int nb = pair ? resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2) : resident_blocks(spec_ext_kernel<3>, lds);
+  // the first two length bins' lists in pair order (spec_sort_*), then two
+  // seeds per wave; the third (reads > 256 bp) one seed per wave
+  hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
+  hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
+  hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
+  int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  if (lane) lane_launch(l + 0);
-  if (pair)
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb, round)), dim3(kBlock), lds2, st, o, ref, b, a, l + 0,
-                       tb_bytes, sorted, lane);
-  else
-    hipLaunchKernelGGL(spec_ext_kernel<3>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 0, tb_bytes);
-  if (lane) lane_join();
+  hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                     l + 0, tb_bytes);
   if (prof) {
     (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
     *ss.pool_used += 2;
   }
-  if (pair) {
-    nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
-    if (lane) lane_launch(l + 1);
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb, round)), dim3(kBlock), lds2, st, o, ref, b, a, l + 1,
-                       tb_bytes, sorted, lane);
-    if (lane) lane_join();
-  } else {
-    nb = resident_blocks(spec_ext_kernel<4>, lds);
-    hipLaunchKernelGGL(spec_ext_kernel<4>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 1, tb_bytes);
-  }
+  nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
+  hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                     l + 1, tb_bytes);
   nb = resident_blocks(spec_ext_kernel<16>, lds);
   hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 2, tb_bytes);
 }

@@ -334,6 +334,14 @@ class Engine:
         """time the next max_launches launches of the dominant extension kernel"""
         self._check(self.lib.bwagpu_prof_start(self.ctx, max_launches), "prof_start")
 
+    def prof_intervals(self, max_n: int = 4096):
+        """-> float64[n, 2]: each timed launch's [start, end] in ms from the first event"""
+        a = np.zeros(max(max_n, 1), np.float64)
+        b = np.zeros(max(max_n, 1), np.float64)
+        n = C.c_int32(0)
+        self._check(self.lib.bwagpu_prof_intervals(self.ctx, _ptr(a), _ptr(b), int(max_n), C.byref(n)), "prof_intervals")
+        return np.stack([a[:n.value], b[:n.value]], axis=1)
+
     def prof_read(self) -> tuple[float, int]:
         """-> (summed kernel ms, launches timed) since prof_start"""
         ms, n = C.c_double(), C.c_int32()

@@ -494,10 +494,13 @@ int bwagpu_debug_set_trace(bwagpu_ctx_t *ctx, void *dev_ptr);
 int bwagpu_debug_fail_wait(bwagpu_ctx_t *ctx, int after_n_waits, int code);
 
 /* kernel timing (bench.py's roofline): after bwagpu_prof_start(ctx, n) the
-   next n launches of the dominant extension kernel (spec_ext_kernel<3>, one
-   per extension round of a chain2aln batch) are bracketed by HIP events on the
-   stream they run on; bwagpu_prof_read waits for them and returns the summed
-   kernel time and the number of launches timed.  bwagpu_prof_start(ctx, 0)
+   next n launches of the dominant extension kernel (the first length bin's
+   extension kernel, one per extension round of a chain2aln batch) are
+   bracketed by HIP events on the stream they run on; bwagpu_prof_read waits
+   for them and returns the summed kernel time and the number of launches
+   timed; bwagpu_prof_intervals returns each launch's [start, end] in ms from
+   the first event, so that launches of different streams that overlap can be
+   counted once (their union).  bwagpu_prof_start(ctx, 0)
    turns timing off.  Diagnostics; the reference prints per-phase stage times
    instead (src/fpga/FPGAPipeline.cpp:557-578). */
 int bwagpu_prof_start(bwagpu_ctx_t *ctx, int max_launches);
@@ -511,12 +514,8 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
    score, truesc, w, cells, rows, calls + 1; calls == 0: not computed) of the
    last device-entry batch on `stream`, n = its seed count */
 int bwagpu_debug_spec_ext(bwagpu_ctx_t *ctx, void *stream, void *host_out, int32_t n);
-/* tuning / tests (process-wide): the short extension tasks one seed per lane
-    — 0 off (the default, or BWAGPU_EXT_LANE), 1 before the
-   two-seeds-per-wave kernel, 2 beside it; returns the previous mode, mode < 0
-   only queries.  Results do not depend on it. */
-int bwagpu_debug_ext_lane(int mode);
 int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
+int bwagpu_prof_intervals(bwagpu_ctx_t *ctx, double *start_ms, double *end_ms, int32_t max, int32_t *n);
 
 #ifdef __cplusplus
 }

@@ -26,23 +26,21 @@ def refd():
     return G.load_ref()
 
 
-@pytest.fixture(params=["spec", "wave", "grp"])
+@pytest.fixture(params=["spec", "wave"])
 def c2a_path(request, monkeypatch):
     """mem_chain2aln paths: speculative extension tasks + selection passes
-    (default), or the per-read kernels (BWAGPU_C2A_PATH=fast): wave per read,
-    or 16-lane groups, four reads per wave (BWAGPU_C2A_GRP=1)"""
+    (default), or the per-read kernels (BWAGPU_C2A_PATH=fast: a wave per read),
+    an independent implementation kept as a cross-check"""
     if request.param == "spec":
         monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
     else:
         monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
-    monkeypatch.setenv("BWAGPU_C2A_GRP", "1" if request.param == "grp" else "0")
     return request.param
 
 
-@pytest.fixture(params=["grp", "wave"])
-def ext_path(request, monkeypatch):
-    """bare ksw_extend2 lists: 16-lane groups for qlen < 128 (default) or wave kernels only"""
-    monkeypatch.setenv("BWAGPU_EXT_WAVE", "1" if request.param == "wave" else "0")
+@pytest.fixture(params=["wave"])
+def ext_path(request):
+    """bare ksw_extend2 lists: the wave kernels"""
     return request.param
 
 

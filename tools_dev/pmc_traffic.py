@@ -15,11 +15,15 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bwa-flow_amd", "python"))
+from bwagpu.provenance import source_digest  # noqa: E402
 
 d, tag, wl, steps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
 ours = ("bwagpu::",)
-out = {"tag": tag, "workload": wl, "per_launch": {}}
+out = {"tag": tag, "workload": wl, "source_digest": source_digest(), "per_launch": {}}
 tot = collections.defaultdict(float)
 for sub, c in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
     per = collections.defaultdict(list)
