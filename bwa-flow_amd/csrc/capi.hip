@@ -902,8 +902,10 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   if (n == 0) return BWAGPU_OK;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   // validate and bin on the host
-  // bins: the wave kernels by column segments
-  std::vector<int32_t> lists[kNumExtVariants];
+  // bins: the wave kernels by column segments, then the four-per-wave kernel
+  // (packed 16-bit DP) for the tasks it takes (extend4_kernel)
+  std::vector<int32_t> lists[kNumExtVariants + 1];
+  const bool quad = ext_form() == 0;
   bool t5 = false;
   int lq_max = 1;
   for (int32_t k = 0; k < n; ++k) {
@@ -915,6 +917,12 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
     int v = kNumExtVariants - 1;
     for (int i = kNumExtVariants - 1; i >= 0; --i)
       if (t.qlen + 1 <= kExtVariants[i].max_len()) v = i;
+    if (quad && t.h0 > 0 && t.qlen >= 1 && t.qlen + 1 <= 256 &&
+        quad_bound_ok(ctx->opt, t.h0 + (long)t.qlen * ctx->opt.max_mat)) {
+      bool nt = true;  // no N in the target rows
+      for (int64_t i = t.toff; i < t.toff + t.tlen && nt; ++i) nt = tpool[i] <= 3;
+      if (nt) v = kNumExtVariants;
+    }
     lists[v].push_back(k);
     lq_max = std::max(lq_max, t.qlen + 1);
   }
@@ -954,9 +962,9 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   (void)hipEventRecord(e0, st);
   int32_t off = 0;
   std::vector<int32_t> all;
-  for (int v = 0; v < kNumExtVariants; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
+  for (int v = 0; v <= kNumExtVariants; ++v) all.insert(all.end(), lists[v].begin(), lists[v].end());
   if ((rc = ck(hipMemcpyAsync(d_list.p, all.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, st), "H2D"))) return rc;
-  for (int v = 0; v < kNumExtVariants; ++v) {
+  for (int v = 0; v <= kNumExtVariants; ++v) {
     const int32_t nv = (int32_t)lists[v].size();
     if (nv) {
       int rows = 16;
@@ -968,14 +976,19 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
         rows = std::max(rows, std::min(t.tlen, t.qlen + we + 1));
       }
       const int tb = (rows + 2 + 15) & ~15;
-      const int gpb = kBlock / kExtVariants[v].G;
+      const int gpb = v < kNumExtVariants ? kBlock / kExtVariants[v].G : 2 * kBlock / 32;
       if ((size_t)tb * gpb > 64 * 1024) {
         cleanup();
         return fail(ctx, BWAGPU_E_UNSUPPORTED, "task needs too many LDS rows");
       }
-      hipError_t e = launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off,
-                                   nv, d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
-                                   d_stats.as<int64_t>(), st);
+      hipError_t e =
+          v < kNumExtVariants
+              ? launch_extend(v, t5, ctx->opt, n, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off, nv,
+                              d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
+                              d_stats.as<int64_t>(), st)
+              : launch_extend4(ctx->opt, d_tasks.as<bwagpu_ext_task_t>(), d_list.as<int32_t>() + off, nv,
+                               d_q.as<uint8_t>(), d_t.as<uint8_t>(), tb, d_res.as<bwagpu_ext_result_t>(),
+                               d_stats.as<int64_t>(), st);
       if ((rc = ck(e, "extend launch"))) return rc;
     }
     off += nv;
@@ -1415,6 +1428,8 @@ int bwagpu_debug_spec_ext(bwagpu_ctx_t* ctx, void* stream, void* host_out, int32
        "hipMemcpy(ext)");
   return BWAGPU_OK;
 }
+
+int bwagpu_debug_ext_form(int form) { return set_ext_form(form); }
 
 int bwagpu_prof_start(bwagpu_ctx_t* ctx, int max_launches) {
   if (!ctx || max_launches < 0) return BWAGPU_E_INVAL;

@@ -117,6 +117,11 @@ hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t n_tasks,
                          const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes,
                          bwagpu_ext_result_t* res, int64_t* stats, hipStream_t st);
+// four tasks per wave (packed 16-bit DP): h0 > 0, no N in the target rows,
+// qlen + 1 <= 256, scores within quad_scores_ok
+hipError_t launch_extend4(const DevOpt& o, const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
+                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes, bwagpu_ext_result_t* res,
+                          int64_t* stats, hipStream_t st);
 
 // ---------------------------------------------------------------- speculative path
 // mem_chain2aln as (1) extension tasks computed ahead of the sequential
@@ -207,6 +212,11 @@ struct SpecStreams {
   int pool_n = 0;
   int* pool_used = nullptr;
 };
+// bwagpu_debug_ext_form: 0 = four seeds per wave where the scores fit (default), 1 = two per wave
+int set_ext_form(int form);
+bool quad_scores_ok(const DevOpt& o, int lq);
+bool quad_bound_ok(const DevOpt& o, long hb);
+int ext_form();
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, hipStream_t st, const SpecStreams& ss);
 // LDS bytes per workgroup of the largest spec launch; regions the redo pass

@@ -634,6 +634,294 @@ __device__ __forceinline__ ExtOut extend_pair_dispatch(const DevOpt& o, int qlen
   return ExtOut{-1, 0, 0, 0, -1, 0};  // unreachable: cpl <= PMAX by construction
 }
 
+// ------------------------------------------------ ksw_extend2, four per wave (packed 16-bit)
+// FOUR extensions per wave: each 32-lane half runs two ksw_extend2 calls in
+// lock step, call A in the low and call B in the high 16 bits of every DP
+// register (v_pk_* ops: one instruction per column slot serves both).  Lane r
+// of a half holds columns j = r*CPL + c of both calls, as in extend_pair.
+// Every per-call quantity (band, maxima, break state) is uniform over its
+// half; the band bounds, the E/H rows and the row maxima are packed, the
+// row-end bookkeeping (ksw.c:454-465) runs per call in 32 bits.
+// 16-bit ranges (quad_scores_ok on the host): H <= lq * max(mat) < 4096, so
+// the row-max key H << KS | c and H * 2^sK + 128 (below) fit; no NEG sentinel
+// is needed because every F contribution is clamped at 0 (a contribution <= 0
+// never changes F = max(0, ...), ksw.c:446):
+//  * M' = min(hh + S, hh * 2^sK), 2^sK > max(mat): hh + S where hh > 0, and
+//    <= 0 where hh == 0 (ksw.c:430 sets M = 0 there; h = max(M, e, f) and the
+//    E / F terms then see a value <= 0 either way).  S comes from v_perm_b32
+//    on the two calls' profile words (bytes biased by 128) with a per-row
+//    selector of the two target bases;
+//  * F: A_c = min_u16(M - oe_ins, CAP_c) with CAP = 0xFFFF in band [lo, hi)
+//    and 0 outside (cells right of the band only feed F of cells right of it);
+//    the lane total T = max(sat(T - e_ins), A_c) >= 0, one inclusive max-scan
+//    of T + (j0 + CPL) e_ins over the half (identity 0, two ops per DPP step),
+//    F at the lane's first column = sat(EX - j0 e_ins);
+//  * H stored for column j is H(i, j-1) within [lo, hi] (R = j <= hi), E in
+//    band and 0 at column hi (ksw.c:449); columns left of lo become 0 (they are
+//    never read again: lo only grows), columns right of hi keep their values;
+//  * band trim (ksw.c:466-469): first non-zero column >= lo (a min over the
+//    half) and last non-zero column <= hi (a max): a column left of lo is 0
+//    here and one at or right of hi cannot move nlo = min(cl, hi);
+//  * gscore / max_ie (ksw.c:450-453) on the lane owning column qlen-1.
+// A call that ends (m == 0, z-drop, or its last target row) freezes with an
+// empty band (lo = 0x7fff, hi = 0) while the others run on.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+namespace pk16 {
+__device__ __forceinline__ s16x2 S(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ u16x2 U(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t W(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t W(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t pk(int lo, int hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
+__device__ __forceinline__ int lo16(uint32_t x) { return (int)(int16_t)(x & 0xffffu); }
+__device__ __forceinline__ int hi16(uint32_t x) { return (int)(int16_t)(x >> 16); }
+__device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return W(U(a) + U(b)); }
+__device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return W(U(a) - U(b)); }
+__device__ __forceinline__ uint32_t mad(uint32_t a, uint32_t b, uint32_t c) { return W(U(a) * U(b) + U(c)); }
+__device__ __forceinline__ uint32_t smax(uint32_t a, uint32_t b) { return W(__builtin_elementwise_max(S(a), S(b))); }
+__device__ __forceinline__ uint32_t smin(uint32_t a, uint32_t b) { return W(__builtin_elementwise_min(S(a), S(b))); }
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return W(__builtin_elementwise_max(U(a), U(b))); }
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return W(__builtin_elementwise_min(U(a), U(b))); }
+__device__ __forceinline__ uint32_t usat(uint32_t a, uint32_t b) { return W(__builtin_elementwise_sub_sat(U(a), U(b))); }
+__device__ __forceinline__ uint32_t ssat(uint32_t a, uint32_t b) { return W(__builtin_elementwise_sub_sat(S(a), S(b))); }
+__device__ __forceinline__ uint32_t neg15(uint32_t a) { return W(S(a) >> (s16x2){15, 15}); }  // 0xffff where < 0
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+constexpr uint32_t ONE = 0x00010001u;
+// DPP moves of whole registers (bound_ctrl: a lane without a source reads 0)
+template <int CTRL>
+__device__ __forceinline__ uint32_t mov0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+// inclusive max-scan over each 32-lane half of packed values >= 0 (identity 0)
+__device__ __forceinline__ uint32_t half_scan_umax(uint32_t x) {
+  x = umax(x, mov0<DPP_ROW_SHR(1)>(x));
+  x = umax(x, mov0<DPP_ROW_SHR(2)>(x));
+  x = umax(x, mov0<DPP_ROW_SHR(4)>(x));
+  x = umax(x, mov0<DPP_ROW_SHR(8)>(x));
+  // rows 1 / 3 take the last lane of rows 0 / 2; rows 0 / 2 an identity 0
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142 /* row_bcast:15 */, 0xA, 0xF, false);
+  return umax(x, t);
+}
+// the whole half's min / max of packed values, in every lane of the half
+__device__ __forceinline__ uint32_t half_umin(uint32_t x) {
+  x = umin(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
+  x = umin(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(4), 0xF, 0xF, false));
+  x = umin(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(2), 0xF, 0xF, false));
+  x = umin(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(1), 0xF, 0xF, false));
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return umin((uint32_t)p[0], (uint32_t)p[1]);
+}
+__device__ __forceinline__ uint32_t half_smax(uint32_t x) {
+  x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
+  x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(4), 0xF, 0xF, false));
+  x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(2), 0xF, 0xF, false));
+  x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(1), 0xF, 0xF, false));
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return smax((uint32_t)p[0], (uint32_t)p[1]);
+}
+}  // namespace pk16
+
+// one ksw_extend2 call of a sub-slot (per lane, uniform over its half)
+struct QCall {
+  int qlen, qa, qd, tlen, w, eb, zdrop, h0;
+  const uint8_t* q;   // query bytes: column j at q[qa + qd * j]
+  const uint8_t* tb;  // target rows (LDS), at least tlen + 1 bytes
+};
+
+// a sub-slot without a task: no rows (its result is ignored)
+__device__ __forceinline__ QCall quad_idle(const uint8_t* seq, const uint8_t* tb) {
+  QCall q;
+  q.qlen = 1;
+  q.tlen = 0;
+  q.qa = 0;
+  q.qd = 1;
+  q.eb = 0;
+  q.h0 = 1;
+  q.w = 1;
+  q.zdrop = 0;
+  q.q = seq;
+  q.tb = tb;
+  return q;
+}
+
+// ksw.c:454-465 for one call from its row's reduced key H << 10 | j; true = exit
+__device__ __forceinline__ bool quad_row_end(int rkr, int i, int e_del, int e_ins, int zdrop, int& best, int& bi,
+                                             int& bj, int& off) {
+  const int mrow = rkr >> 10, mj = rkr & 1023;
+  const bool up = mrow > best;
+  const int di = i - bi, dj = mj - bj;
+  const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
+  const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
+  off = up ? max(off, abs(mj - i)) : off;
+  best = up ? mrow : best;
+  bi = up ? i : bi;
+  bj = up ? mj : bj;
+  return brk;
+}
+
+template <int CPL>
+__device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa, ExtOut& xb,
+                                            Tally32& ta, Tally32& tbl) {
+  using namespace pk16;
+  int r;  // the lane index behind an opaque move (see extend_pair)
+  asm volatile("v_and_b32 %0, 31, %1" : "=v"(r) : "v"((int)threadIdx.x));
+  constexpr int KS = CPL <= 2 ? 1 : (CPL <= 4 ? 2 : (CPL <= 8 ? 3 : 4));  // in-lane column bits of the key
+  static_assert(CPL >= 1 && CPL <= 8, "four extensions per wave: CPL <= 8");
+  const int e_del = o.e_del, e_ins = o.e_ins, oe_ins = o.oe_ins;
+  const int j0 = r * CPL;
+  const uint32_t J0 = pk(j0, j0);
+  const uint32_t EI1 = pk(e_ins, e_ins), ED1 = pk(e_del, e_del);
+  const uint32_t MB_OE = pk(128 + oe_ins, 128 + oe_ins), MB_OD = pk(128 + o.o_del, 128 + o.o_del);
+  const int sk = 32 - __builtin_clz((unsigned)max(o.max_mat, 1));  // 2^sk > max(mat)
+  const uint32_t KSH = pk(1 << sk, 1 << sk);
+  const uint32_t RE = pk(e_ins * j0, e_ins * j0), RE2 = pk(e_ins * (j0 + CPL), e_ins * (j0 + CPL));
+  uint32_t hh[CPL], ee[CPL], pfa[CPL], pfb[CPL], qm[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j = j0 + c;
+    const int qva = A.q[A.qa + A.qd * min(j, A.qlen - 1)];  // unconditional loads (qlen >= 1)
+    const int qvb = Bc.q[Bc.qa + Bc.qd * min(j, Bc.qlen - 1)];
+    pfa[c] = qprof_word(o, j < A.qlen ? qva : 0) ^ 0x80808080u;  // bytes biased by 128
+    pfb[c] = qprof_word(o, j < Bc.qlen ? qvb : 0) ^ 0x80808080u;
+    const int va = j == 0 ? A.h0 : max(A.h0 - oe_ins - (j - 1) * e_ins, 0);  // ksw.c:392-395
+    const int vb = j == 0 ? Bc.h0 : max(Bc.h0 - oe_ins - (j - 1) * e_ins, 0);
+    hh[c] = pk(j <= A.qlen ? va : 0, j <= Bc.qlen ? vb : 0);
+    ee[c] = 0;
+    qm[c] = pk(j == A.qlen - 1 ? 0xffff : 0, j == Bc.qlen - 1 ? 0xffff : 0);
+  }
+  // band clamp (ksw.c:399-407)
+  const int wa = min(A.w, min(band_cap_dev(A.qlen, o.max_mat, A.eb, o.o_ins, e_ins),
+                              band_cap_dev(A.qlen, o.max_mat, A.eb, o.o_del, e_del)));
+  const int wb = min(Bc.w, min(band_cap_dev(Bc.qlen, o.max_mat, Bc.eb, o.o_ins, e_ins),
+                               band_cap_dev(Bc.qlen, o.max_mat, Bc.eb, o.o_del, e_del)));
+  const uint32_t QL = pk(A.qlen, Bc.qlen);
+  uint32_t LO = 0, HI = QL;
+  uint32_t IW = pk(-wa, -wb), IW1 = pk(wa + 1, wb + 1);
+  uint32_t GL = pk(A.h0 - o.o_del - e_del, Bc.h0 - o.o_del - e_del);  // h0 - (o_del + e_del (i+1))
+  uint32_t EI = pk(-1, -1), ESC = pk(-1, -1);
+  int besta = A.h0, bia = -1, bja = -1, offa = 0, bestb = Bc.h0, bib = -1, bjb = -1, offb = 0;
+  int cellsa = 0, cellsb = 0, rowsa = max(A.tlen, 0), rowsb = max(Bc.tlen, 0);
+  bool deada = false, deadb = false;
+  int tna = A.tb[0], tnb = Bc.tb[0];
+  for (int i = 0;; ++i) {
+    deada = deada || i >= A.tlen;
+    deadb = deadb || i >= Bc.tlen;
+    if (!__builtin_amdgcn_ballot_w64(!deada || !deadb)) break;
+    const uint32_t DM = pk(deada ? 0xffff : 0, deadb ? 0xffff : 0);
+    const int ta = tna, tbb = tnb;
+    tna = A.tb[min(i + 1, max(A.tlen - 1, 0))];  // prefetch
+    tnb = Bc.tb[min(i + 1, max(Bc.tlen - 1, 0))];
+    // the band (ksw.c:415-419); an ended call: lo = 0x7fff, hi = 0
+    LO = sel(DM, 0x7fff7fffu, smax(LO, IW));
+    HI = sel(DM, 0u, smin(smin(HI, IW1), QL));
+    IW = add(IW, ONE);
+    IW1 = add(IW1, ONE);
+    const uint32_t WD = usat(HI, LO);
+    const uint32_t LEFT0 = sub(umin(LO, ONE), ONE) & smax(GL, 0u);  // the first-column value where lo == 0
+    GL = ssat(GL, ED1);
+    const uint32_t SEL = (uint32_t)ta | ((uint32_t)tbb << 16) | 0x0c040c00u;
+    const uint32_t HI1 = add(HI, ONE);
+    uint32_t MB[CPL], AA[CPL], CAP[CPL], R[CPL], GEL[CPL];
+    uint32_t T = 0;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const uint32_t JC = add(J0, pk(c, c));
+      const uint32_t ltlo = neg15(sub(JC, LO));  // j < lo
+      R[c] = neg15(sub(JC, HI1));                // j <= hi
+      GEL[c] = ~ltlo;
+      CAP[c] = neg15(sub(JC, HI)) & ~ltlo;       // lo <= j < hi
+      const uint32_t sb = __builtin_amdgcn_perm(pfb[c], pfa[c], SEL);
+      const uint32_t mb = smin(add(hh[c], sb), mad(hh[c], KSH, 0x00800080u));  // M' + 128
+      MB[c] = mb;
+      AA[c] = umin(sub(mb, MB_OE), CAP[c]);
+      T = smax(usat(T, EI1), AA[c]);
+    }
+    const uint32_t sx = half_scan_umax(add(T, RE2));
+    uint32_t EX = mov0<DPP_WAVE_SHR1>(sx);
+    EX = r == 0 ? 0u : EX;  // lanes 0 and 32: no column to the left in the half
+    uint32_t f = usat(EX, RE);
+    uint32_t LK = 0, H1Q = 0, hm[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      if (c > 0) f = smax(usat(f, EI1), AA[c - 1]);
+      const uint32_t h = smax(smax(sub(MB[c], 0x00800080u), ee[c]), f);
+      hm[c] = umin(h, CAP[c]);
+      const uint32_t en = usat(smax(ee[c], sub(MB[c], MB_OD)), ED1);
+      LK = umax(LK, mad(hm[c], pk(1 << KS, 1 << KS), pk(c, c)));
+      ee[c] = sel(R[c], umin(en, CAP[c]), ee[c]);
+      if (c > 0) hh[c] = sel(R[c], hm[c - 1], hh[c]);
+      H1Q |= hm[c] & qm[c];
+    }
+    uint32_t hs0 = mov0<DPP_WAVE_SHR1>(hm[CPL - 1]);  // H(i, j0 - 1)
+    hs0 = r == 0 ? LEFT0 : hs0;
+    hh[0] = sel(R[0], hs0, hh[0]);
+    // band trim candidates: first non-zero column >= lo, last non-zero <= hi
+    uint32_t CL = 0x7fff7fffu, CH = 0xffffffffu;
+#pragma unroll
+    for (int c = CPL - 1; c >= 0; --c) {
+      const uint32_t nz = sub(0u, umin(hh[c] | ee[c], ONE));
+      CL = sel(nz & GEL[c], add(J0, pk(c, c)), CL);
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const uint32_t nz = sub(0u, umin(hh[c] | ee[c], ONE));
+      CH = sel(nz & R[c], add(J0, pk(c, c)), CH);
+    }
+    // the row maxima (key H << 10 | j, ksw.c:433) and the trim, reduced over the half
+    const uint32_t lka = LK & 0xffffu, lkb = LK >> 16;
+    int ka = (int)(((lka >> KS) << 10) | (uint32_t)(j0 + (int)(lka & ((1u << KS) - 1))));
+    int kb = (int)(((lkb >> KS) << 10) | (uint32_t)(j0 + (int)(lkb & ((1u << KS) - 1))));
+    CL = half_umin(CL);
+    CH = half_smax(CH);
+    ka = half_max(row_max32(ka));
+    kb = half_max(row_max32(kb));
+    // ksw.c:450-453 (meaningful on the owner of column qlen-1)
+    {
+      const uint32_t AT = sub(umin(sub(smax(LO, HI), QL), ONE), ONE);  // 0xffff where max(lo, hi) == qlen
+      EI = sel(AT & ~neg15(sub(H1Q, ESC)), pk(i, i), EI);
+      ESC = sel(AT, smax(ESC, H1Q), ESC);
+    }
+    cellsa += (int)(WD & 0xffffu);
+    cellsb += (int)(WD >> 16);
+    // branch-free: an ended call's row maximum is 0, which changes nothing
+    const bool ba = quad_row_end(ka, i, e_del, e_ins, A.zdrop, besta, bia, bja, offa);
+    const bool bb = quad_row_end(kb, i, e_del, e_ins, Bc.zdrop, bestb, bib, bjb, offb);
+    rowsa = !deada && ba ? i + 1 : rowsa;
+    rowsb = !deadb && bb ? i + 1 : rowsb;
+    deada = deada || ba;
+    deadb = deadb || bb;
+    // the next row's band (ksw.c:466-469)
+    const uint32_t NLO = smin(CL, HI);
+    LO = NLO;
+    HI = smin(add(smax(CH, sub(NLO, ONE)), pk(2, 2)), QL);
+  }
+  // gscore / max_ie from the owner of column qlen-1 of each call
+  const int hb = (int)(threadIdx.x & 32);
+  const uint32_t ea = __shfl(pk(lo16(EI), lo16(ESC)), hb + (A.qlen - 1) / CPL, 64);
+  const uint32_t eb = __shfl(pk(hi16(EI), hi16(ESC)), hb + (Bc.qlen - 1) / CPL, 64);
+  xa = ExtOut{besta, bja + 1, bia + 1, lo16(ea) + 1, hi16(ea), offa};
+  xb = ExtOut{bestb, bjb + 1, bib + 1, lo16(eb) + 1, hi16(eb), offb};
+  ta.cells += cellsa;
+  ta.rows += rowsa;
+  ta.calls += 1;
+  tbl.cells += cellsb;
+  tbl.rows += rowsb;
+  tbl.calls += 1;
+}
+
+// CPL = ceil((qlen+1)/32) of the wave's longest active call (all four run one body)
+template <int PMAX>
+__device__ __forceinline__ void extend_quad_dispatch(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa,
+                                                     ExtOut& xb, Tally32& ta, Tally32& tbl) {
+  const int qm = max(max(__builtin_amdgcn_readlane(A.qlen, 0), __builtin_amdgcn_readlane(Bc.qlen, 0)),
+                     max(__builtin_amdgcn_readlane(A.qlen, 32), __builtin_amdgcn_readlane(Bc.qlen, 32)));
+  const int cpl = (qm + 32) >> 5;
+#define EXT_QUAD(n) \
+  if (n <= PMAX && cpl == n) return extend_quad<(n <= PMAX ? n : 1)>(o, A, Bc, xa, xb, ta, tbl);
+  EXT_QUAD(1) EXT_QUAD(2) EXT_QUAD(3) EXT_QUAD(4) EXT_QUAD(5) EXT_QUAD(6) EXT_QUAD(7) EXT_QUAD(8)
+#undef EXT_QUAD
+}
+
 // rows that extend_group can read for (qlen, w, end_bonus)
 __device__ __forceinline__ int rows_needed(const DevOpt& o, int qlen, int tlen, int w, int end_bonus) {
   int mi = band_cap_dev(qlen, o.max_mat, end_bonus, o.o_ins, o.e_ins);
@@ -1616,6 +1904,92 @@ hipError_t launch_extend(int variant, bool t5, const DevOpt& o, int32_t, const b
   return hipErrorInvalidValue;
 }
 
+// bare task list, four per wave (extend_quad): sub-slot s of the grid takes
+// tasks s, s + NS, ... of the list; all four sub-slots of a wave run their
+// current calls together, and one whose call ended takes its next task at the
+// call boundary.  Every task has h0 > 0, no N in its target rows and
+// qlen + 1 <= 32 * PMAX (the host routes the rest to extend_kernel).
+template <int PMAX>
+__global__ void __launch_bounds__(kBlock) extend4_kernel(DevOpt o, const bwagpu_ext_task_t* __restrict__ tasks,
+                                                         const int32_t* __restrict__ task_list, int32_t n_list,
+                                                         const uint8_t* __restrict__ qpool,
+                                                         const uint8_t* __restrict__ tpool, int tb_bytes,
+                                                         bwagpu_ext_result_t* res, int64_t* stats) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int r = (int)(threadIdx.x & 31);
+  const int half = (int)(blockIdx.x * (kBlock / 32) + (threadIdx.x >> 5));  // global half index
+  const int NS = (int)gridDim.x * (kBlock / 32) * 2;                         // sub-slots in the grid
+  uint8_t* const tba = lds + (size_t)(threadIdx.x >> 5) * 2 * tb_bytes;
+  uint8_t* const tbb = tba + tb_bytes;
+  int la = 2 * half, lb = 2 * half + 1;  // list positions of the sub-slots' tasks
+  int ka = -1, kb = -1;                 // their task indices, -1: none
+  long long cells = 0, rows = 0, calls = 0;
+  QCall ca = quad_idle(qpool, tba), cb = quad_idle(qpool, tbb);
+  auto take = [&](int& li, int& k, QCall& c, uint8_t* tb) {
+    k = -1;
+    c = quad_idle(qpool, tb);
+    if (li >= n_list) return;
+    k = task_list[li];
+    li += NS;
+    const bwagpu_ext_task_t t = tasks[k];
+    const int nr = rows_needed(o, t.qlen, t.tlen, t.w, t.end_bonus);
+    for (int base = 0; base < nr; base += 32) tb[min(base + r, nr - 1)] = tpool[t.toff + min(base + r, nr - 1)];
+    c.qlen = t.qlen;
+    c.qa = 0;
+    c.qd = 1;
+    c.tlen = t.tlen;
+    c.w = t.w;
+    c.eb = t.end_bonus;
+    c.zdrop = t.zdrop;
+    c.h0 = t.h0;
+    c.q = qpool + t.qoff;
+    c.tb = tb;
+  };
+  take(la, ka, ca, tba);
+  take(lb, kb, cb, tbb);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  while (__builtin_amdgcn_ballot_w64(ka >= 0 || kb >= 0)) {
+    ExtOut xa, xb;
+    Tally32 ta{0, 0, 0}, tb{0, 0, 0};
+    extend_quad_dispatch<PMAX>(o, ca, cb, xa, xb, ta, tb);
+    if (ka >= 0) {
+      if (r == 0) res[ka] = bwagpu_ext_result_t{xa.score, xa.qle, xa.tle, xa.gtle, xa.gscore, xa.max_off};
+      cells += ta.cells;
+      rows += ta.rows;
+      calls += ta.calls;
+    }
+    if (kb >= 0) {
+      if (r == 0) res[kb] = bwagpu_ext_result_t{xb.score, xb.qle, xb.tle, xb.gtle, xb.gscore, xb.max_off};
+      cells += tb.cells;
+      rows += tb.rows;
+      calls += tb.calls;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (ka >= 0) take(la, ka, ca, tba);
+    if (kb >= 0) take(lb, kb, cb, tbb);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  Tally tl{r == 0 ? cells : 0, r == 0 ? rows : 0, r == 0 ? calls : 0};
+  block_stats<64>(tl, stats);
+}
+
+hipError_t launch_extend4(const DevOpt& o, const bwagpu_ext_task_t* tasks, const int32_t* task_list, int32_t n_list,
+                          const uint8_t* qpool, const uint8_t* tpool, int tb_bytes, bwagpu_ext_result_t* res,
+                          int64_t* stats, hipStream_t st) {
+  if (n_list == 0) return hipSuccess;
+  const size_t lds = (size_t)(kBlock / 32) * 2 * tb_bytes;
+  const int nb = std::min((n_list + 15) / 16, std::max(1, resident_blocks(extend4_kernel<8>, lds) / 2));
+  hipLaunchKernelGGL(extend4_kernel<8>, dim3(nb), dim3(kBlock), lds, st, o, tasks, task_list, n_list, qpool, tpool,
+                     tb_bytes, res, stats);
+  return hipGetLastError();
+}
+
 // ============================================================ speculative chain2aln
 // mem_chain2aln (bwamem.c:641-795) restructured for load balance on
 // reference-seeded batches, where a few reads (tandem repeats: hundreds of
@@ -2227,6 +2601,197 @@ __global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref,
 
 // LDS bytes of a spec_ext2_kernel workgroup
 static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size_t)tb_bytes + sizeof(PairCtx)); }
+
+// ---------------------------------------------------- four seeds per wave
+// The same extension tasks with two seeds per 32-lane half, packed in the
+// 16-bit halves of the DP registers (extend_quad).  Each sub-slot (half x
+// low/high) walks its own seed through extend_seed's state machine
+// (bwamem.c:717-792: left side with the band retry, right side from the left
+// score, local vs to-end), held in registers; the four sub-slots call
+// extend_quad together, and a sub-slot whose seed is done takes the next task
+// of the list at once (one claim per call boundary for all the sub-slots that
+// need one), so a wave idles only inside a call whose four rows counts differ.
+struct QTask {
+  int64_t rbeg, wlo, whi, qoff, rb, re;
+  int pos, qbeg, len, lq, phase, score, truesc, qb, qe, sc0, aw0, aw1, cells, rows, calls;
+};
+
+// the task's seed, window and read; both target windows into the sub-slot's LDS rows
+__device__ __forceinline__ void qtask_start(QTask& t, const DevOpt& o, const DevRef& ref, const DevBatch& b,
+                                            const SpecArgs& a, int2 tk, uint8_t* tl, uint8_t* tr) {
+  const int rd = a.chain_read[tk.y];
+  const bwagpu_seed_t s = a.prog[tk.x];
+  const ChainWin cw = a.win[tk.y];
+  t.pos = tk.x;
+  t.rbeg = s.rbeg;
+  t.wlo = cw.lo;
+  t.whi = cw.hi;
+  t.qoff = b.seq_off[rd];
+  t.lq = (int)(b.seq_off[rd + 1] - t.qoff);
+  t.qbeg = s.qbeg;
+  t.len = s.len;
+  const int qlenL = t.qbeg, qlenR = t.lq - (t.qbeg + t.len);
+  const int64_t x0R = t.rbeg + t.len;
+  fill_two_half(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, (int)(t.rbeg - t.wlo), o.w << 1, o.pen_clip5) : 0, tr,
+                x0R, qlenR ? rows_needed(o, qlenR, (int)(t.whi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
+  t.phase = qlenL != 0 ? 0 : (qlenR != 0 ? 2 : 4);
+  const int sc = qlenL != 0 ? -1 : t.len * o.a;  // bwamem.c:753
+  t.score = sc;
+  t.truesc = sc;
+  t.qb = 0;
+  t.qe = t.lq;
+  t.sc0 = 0;
+  t.aw0 = o.w;
+  t.aw1 = o.w;
+  t.rb = t.rbeg;
+  t.re = t.rbeg + t.len;
+  t.cells = t.rows = t.calls = 0;
+}
+
+// the ksw_extend2 call of the task's phase (0/1: left try 0/1, 2/3: right)
+__device__ __forceinline__ QCall qtask_call(QTask& t, const DevOpt& o, const uint8_t* seq, const uint8_t* tl,
+                                            const uint8_t* tr) {
+  const bool left = t.phase < 2;
+  const int tt = t.phase & 1;
+  const int qlenR = t.lq - (t.qbeg + t.len);
+  const int64_t x0 = left ? t.rbeg - 1 : t.rbeg + t.len;
+  QCall q;
+  q.qlen = left ? t.qbeg : qlenR;
+  q.tlen = left ? (int)(t.rbeg - t.wlo) : (int)(t.whi - x0);
+  q.qa = left ? t.qbeg - 1 : t.qbeg + t.len;
+  q.qd = left ? -1 : 1;
+  q.eb = left ? o.pen_clip5 : o.pen_clip3;
+  if (tt == 0) t.sc0 = t.score;
+  q.h0 = left ? t.len * o.a : t.sc0;
+  q.w = o.w << tt;
+  if (left) t.aw0 = q.w;
+  else t.aw1 = q.w;
+  q.zdrop = o.zdrop;
+  q.q = seq + t.qoff;
+  q.tb = left ? tl : tr;
+  return q;
+}
+
+// the call's result into the task (bwamem.c:737-792); true = the seed is done
+__device__ __forceinline__ bool qtask_advance(QTask& t, const DevOpt& o, const ExtOut& x, const Tally32& tl) {
+  const bool left = t.phase < 2;
+  const int tt = t.phase & 1;
+  t.cells += tl.cells;
+  t.rows += tl.rows;
+  t.calls += tl.calls;
+  const int prev = t.score;
+  t.score = x.score;
+  const int aw = o.w << tt;
+  if (tt == 0 && !(x.score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {  // the band retry (MAX_BAND_TRY)
+    t.phase += 1;
+    return false;
+  }
+  const int eb = left ? o.pen_clip5 : o.pen_clip3;
+  const bool local = x.gscore <= 0 || x.gscore <= x.score - eb;
+  if (left) {
+    t.qb = local ? t.qbeg - x.qle : 0;
+    t.rb = t.rbeg - (local ? x.tle : x.gtle);
+    t.truesc = local ? x.score : x.gscore;
+    t.phase = t.lq - (t.qbeg + t.len) != 0 ? 2 : 4;
+  } else {
+    t.qe = local ? t.qbeg + t.len + x.qle : t.lq;
+    t.re = t.rbeg + t.len + (local ? x.tle : x.gtle);
+    t.truesc += (local ? x.score : x.gscore) - t.sc0;
+    t.phase = 4;
+  }
+  return t.phase >= 4;
+}
+
+__device__ __forceinline__ SeedExt qtask_ext(const QTask& t) {
+  SeedExt e;
+  e.rb = t.rb;
+  e.re = t.re;
+  e.qb = t.qb;
+  e.qe = t.qe;
+  e.score = t.score;
+  e.truesc = t.truesc;
+  e.w = t.aw0 > t.aw1 ? t.aw0 : t.aw1;
+  e.cells = t.cells;
+  e.rows = t.rows;
+  e.calls = t.calls + 1;  // + 1: a computed slot is never all-zero
+  return e;
+}
+
+// Extension tasks of one list (in pair order, spec_sort_*), four per wave.
+// PMAX = the bin's largest CPL: ceil(read length / 32).
+template <int PMAX>
+__global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                           int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int hf = (int)(threadIdx.x >> 5) & 1;
+  // per half: A left, A right, B left, B right target rows
+  uint8_t* const tal = lds + (size_t)(threadIdx.x >> 5) * 4 * tb_bytes;
+  uint8_t* const tar = tal + tb_bytes;
+  uint8_t* const tbl = tar + tb_bytes;
+  uint8_t* const tbr = tbl + tb_bytes;
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  ShardQ qq;
+  qq.init(a.qh + 8 * kQHStride * list, n);
+  QTask sa, sb;
+  bool ha = false, hb = false, more = n > 0;
+  long long spec_cells = 0;
+  for (;;) {
+    if (more) {  // every sub-slot without a seed takes the next entry: one claim for the wave
+      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha), nb = __builtin_amdgcn_ballot_w64(!hb);
+      const int n0 = (int)(na & 1) + (int)(nb & 1), n1 = (int)((na >> 32) & 1) + (int)((nb >> 32) & 1);
+      if (n0 + n1 > 0) {
+        int m0, cap;
+        if (qq.claim(n0 + n1, m0, cap)) {
+          const int ia = m0 + (hf ? n0 : 0), ib = ia + (ha ? 0 : 1);
+          if (!ha && ia < cap) {
+            qtask_start(sa, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
+            ha = true;
+          }
+          if (!hb && ib < cap) {
+            qtask_start(sb, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
+            hb = true;
+          }
+        } else {
+          more = false;
+        }
+      }
+    }
+    if (ha && sa.phase >= 4) {  // a seed spanning the whole read: no extension (bwamem.c:753, 781)
+      store_ext_half(a.ext + sa.pos, qtask_ext(sa));
+      ha = false;
+    }
+    if (hb && sb.phase >= 4) {
+      store_ext_half(a.ext + sb.pos, qtask_ext(sb));
+      hb = false;
+    }
+    if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
+      if (!more) break;
+      continue;
+    }
+    const QCall ca = ha ? qtask_call(sa, o, b.seq, tal, tar) : quad_idle(b.seq, tal);
+    const QCall cb = hb ? qtask_call(sb, o, b.seq, tbl, tbr) : quad_idle(b.seq, tbl);
+    ExtOut xa, xb;
+    Tally32 ta{0, 0, 0}, tb{0, 0, 0};
+    extend_quad_dispatch<PMAX>(o, ca, cb, xa, xb, ta, tb);
+    if (ha && qtask_advance(sa, o, xa, ta)) {
+      store_ext_half(a.ext + sa.pos, qtask_ext(sa));
+      spec_cells += sa.cells;
+      ha = false;
+    }
+    if (hb && qtask_advance(sb, o, xb, tb)) {
+      store_ext_half(a.ext + sb.pos, qtask_ext(sb));
+      spec_cells += sb.cells;
+      hb = false;
+    }
+  }
+  if ((threadIdx.x & 31) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+// LDS bytes of a spec_ext4_kernel workgroup
+static size_t ext4_lds(int tb_bytes) { return (size_t)(kBlock / 32) * 4 * (size_t)tb_bytes; }
+
 
 // Task order for the pair kernel: the two seeds a wave takes should need the
 // same phases for about as long — a half whose seed has no left side, or a
@@ -3320,29 +3885,66 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
   }
 }
 
+// The first two length bins' extension kernel: four seeds per wave
+// (spec_ext4_kernel, packed 16-bit DP) when every score of the bin fits the
+// packed ranges, else two per wave (spec_ext2_kernel, 32-bit).
+// bwagpu_debug_ext_form(1) forces two per wave (tests, A/B).
+static std::atomic<int> g_ext_form{0};
+int ext_form() { return g_ext_form.load(std::memory_order_relaxed); }
+int set_ext_form(int form) {  // process-wide; -> the previous form (form < 0: query only)
+  const int prev = g_ext_form.load(std::memory_order_relaxed);
+  if (form >= 0) g_ext_form.store(form > 1 ? 1 : form, std::memory_order_relaxed);
+  return prev;
+}
+// the packed ranges (extend_quad) for reads up to lq: H <= lq * max(mat) < 4096
+// (the row-max key H << KS | c, KS <= 3), H * 2^sk + 128 < 2^15 (2^sk >
+// max(mat)), and the scan values H + 33 * CPL * e_ins < 2^15
+bool quad_bound_ok(const DevOpt& o, long hb) {  // hb: a bound on every H of the call
+  if (o.max_mat < 1 || o.max_mat > 15) return false;
+  const int sk = 32 - __builtin_clz((unsigned)o.max_mat);
+  for (int k = 0; k < 25; ++k)
+    if (o.mat[k] < -127 || o.mat[k] > 127) return false;
+  return hb < 4096 && (hb << sk) + 128 < 32768 && hb + 33L * 8 * o.e_ins < 32768 && o.o_del + 128L < 32768 &&
+         o.oe_ins + 128L < 32768 && o.e_del < 32768;
+}
+bool quad_scores_ok(const DevOpt& o, int lq) { return quad_bound_ok(o, (long)lq * o.max_mat); }
+
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
                              int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
-  const size_t lds2 = ext2_lds(tb_bytes);
-  // the first two length bins' lists in pair order (spec_sort_*), then two
-  // seeds per wave; the third (reads > 256 bp) one seed per wave
+  const bool quad = g_ext_form.load(std::memory_order_relaxed) == 0 && quad_scores_ok(o, kSpecBinLen[1]);
+  const size_t lds2 = quad ? ext4_lds(tb_bytes) : ext2_lds(tb_bytes);
+  // the first two length bins' lists in pair order (spec_sort_*), then two or
+  // four seeds per wave; the third (reads > 256 bp) one seed per wave
   hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
   hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
   hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
-  int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
-                     l + 0, tb_bytes);
+  if (quad) {
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[0] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext4_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 0, tb_bytes);
+  } else {
+    const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 0, tb_bytes);
+  }
   if (prof) {
     (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
     *ss.pool_used += 2;
   }
-  nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
-  hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
-                     l + 1, tb_bytes);
-  nb = resident_blocks(spec_ext_kernel<16>, lds);
+  if (quad) {
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext4_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 1, tb_bytes);
+  } else {
+    const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 1, tb_bytes);
+  }
+  const int nb = resident_blocks(spec_ext_kernel<16>, lds);
   hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 2, tb_bytes);
 }
 

@@ -14,3 +14,21 @@ for p in (os.path.join(REPO, "bwa-flow_amd", "python"), os.path.join(REPO, "orac
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (gfx950)")
+
+
+def set_c2a_path(path, monkeypatch):
+    """mem_chain2aln paths of the GPU tests:
+      spec  the speculative extension tasks + selection passes, first two
+            read-length bins four seeds per wave (packed 16-bit DP, the default)
+      pair  the same with two seeds per wave (32-bit DP; bwagpu_debug_ext_form(1))
+      fast  the per-read kernels (BWAGPU_C2A_PATH=fast: a wave per read), an
+            independent implementation kept as a cross-check
+    The extension form is process-wide: restored by the caller's teardown."""
+    from bwagpu import abi
+    lib = abi.load()
+    if path == "fast":
+        monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
+    else:
+        monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
+    prev = lib.bwagpu_debug_ext_form(1 if path == "pair" else 0)
+    return lambda: lib.bwagpu_debug_ext_form(prev)

@@ -14,19 +14,18 @@ import pytest
 
 import golden_io as G
 import refseed
+from conftest import set_c2a_path
 from bwagpu import abi
 from bwagpu.engine import Engine, compact
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not refseed.available(), reason="oracle/_ref/gen_golden not built")]
 
 
-@pytest.fixture(params=["spec", "fast"])
+@pytest.fixture(params=["spec", "pair", "fast"])
 def c2a_path(request, monkeypatch):
-    if request.param == "spec":
-        monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
-    else:
-        monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
-    return request.param
+    restore = set_c2a_path(request.param, monkeypatch)
+    yield request.param
+    restore()
 
 
 @pytest.mark.parametrize("length,pairs", [("150", 33334), ("mix", 24000)])

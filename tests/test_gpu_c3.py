@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from bwagpu import workload
+from conftest import set_c2a_path
 from bwagpu.engine import Engine
 
 pytestmark = pytest.mark.gpu
@@ -31,15 +32,13 @@ def eng(c3):
     e.close()
 
 
-@pytest.mark.parametrize("path", ["spec", "fast"])
+@pytest.mark.parametrize("path", ["spec", "pair", "fast"])
 @pytest.mark.parametrize("name", ["c3", "c5"])
 def test_chain2aln_grch38(c3, eng, name, path, monkeypatch):
-    if path == "fast":
-        monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
-    else:
-        monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
+    restore = set_c2a_path(path, monkeypatch)
     s = c3[2][name]
     regs, n = eng.chain2aln(s.batch)
+    restore()
     why = s.check(regs, n)
     assert why is None, why
     assert eng.last_stats()["ext_calls"] > 0

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import golden_io as G
+from conftest import set_c2a_path
 import oracle
 from bwagpu import abi
 from bwagpu.engine import Batch, BwaGpuError, Engine, compact
@@ -26,22 +27,22 @@ def refd():
     return G.load_ref()
 
 
-@pytest.fixture(params=["spec", "wave"])
+@pytest.fixture(params=["spec", "pair", "fast"])
 def c2a_path(request, monkeypatch):
-    """mem_chain2aln paths: speculative extension tasks + selection passes
-    (default), or the per-read kernels (BWAGPU_C2A_PATH=fast: a wave per read),
-    an independent implementation kept as a cross-check"""
-    if request.param == "spec":
-        monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
-    else:
-        monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
-    return request.param
+    """mem_chain2aln paths (conftest.set_c2a_path)"""
+    restore = set_c2a_path(request.param, monkeypatch)
+    yield request.param
+    restore()
 
 
-@pytest.fixture(params=["wave"])
+@pytest.fixture(params=["quad", "wave"])
 def ext_path(request):
-    """bare ksw_extend2 lists: the wave kernels"""
-    return request.param
+    """bare ksw_extend2 lists: four per wave with packed 16-bit DP where a task
+    fits (default), or the wave kernels only (bwagpu_debug_ext_form(1))"""
+    lib = abi.load()
+    prev = lib.bwagpu_debug_ext_form(0 if request.param == "quad" else 1)
+    yield request.param
+    lib.bwagpu_debug_ext_form(prev)
 
 
 def make_engine(refd, opt):
