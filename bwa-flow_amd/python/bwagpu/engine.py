@@ -256,6 +256,20 @@ class Engine:
                                               C.byref(n)), "sw_stream")
         return out[:n.value]
 
+    def quad_ok(self, lq: int = 256) -> bool:
+        """whether the first two read-length bins run four seeds per wave with
+        these options (sw_kernels.hip quad_scores_ok: every score of a read of
+        up to lq bases fits the packed 16-bit ranges)"""
+        o = self.opt
+        mat = list(o.mat)
+        mm = max(mat) if mat else 0
+        if mm < 1 or mm > 15 or min(mat) < -127:
+            return False
+        sk = int(mm).bit_length()
+        hb = lq * mm
+        return (hb < 4096 and (hb << sk) + 128 < 32768 and hb + 33 * 8 * o.e_ins < 32768
+                and o.o_del + 128 < 32768 and o.o_ins + o.e_ins + 128 < 32768 and o.e_del < 32768)
+
     def sup_shift(self, shift: int):
         """superblock size 2^shift of the occurrence layout the NEXT set_bwt builds (tests; default 32)"""
         self._check(self.lib.bwagpu_debug_sup_shift(self.ctx, shift), "sup_shift")
