@@ -684,7 +684,13 @@ __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return W(__bu
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return W(__builtin_elementwise_min(U(a), U(b))); }
 __device__ __forceinline__ uint32_t usat(uint32_t a, uint32_t b) { return W(__builtin_elementwise_sub_sat(U(a), U(b))); }
 __device__ __forceinline__ uint32_t ssat(uint32_t a, uint32_t b) { return W(__builtin_elementwise_sub_sat(S(a), S(b))); }
-__device__ __forceinline__ uint32_t neg15(uint32_t a) { return W(S(a) >> (s16x2){15, 15}); }  // 0xffff where < 0
+// the empty asm keeps a mask opaque: otherwise LLVM turns mask & a | ~mask & b
+// back into per-half compares + v_cndmask + v_perm (5 ops for 1)
+__device__ __forceinline__ uint32_t opq(uint32_t x) {
+  asm("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t neg15(uint32_t a) { return opq(W(S(a) >> (s16x2){15, 15})); }  // 0xffff where < 0
 __device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 constexpr uint32_t ONE = 0x00010001u;
 // DPP moves of whole registers (bound_ctrl: a lane without a source reads 0)
@@ -801,12 +807,10 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   uint32_t EI = pk(-1, -1), ESC = pk(-1, -1);
   int besta = A.h0, bia = -1, bja = -1, offa = 0, bestb = Bc.h0, bib = -1, bjb = -1, offb = 0;
   int cellsa = 0, cellsb = 0, rowsa = max(A.tlen, 0), rowsb = max(Bc.tlen, 0);
-  bool deada = false, deadb = false;
+  bool deada = A.tlen <= 0, deadb = Bc.tlen <= 0;
   int tna = A.tb[0], tnb = Bc.tb[0];
-  for (int i = 0;; ++i) {
-    deada = deada || i >= A.tlen;
-    deadb = deadb || i >= Bc.tlen;
-    if (!__builtin_amdgcn_ballot_w64(!deada || !deadb)) break;
+  // rows run while a call of the wave is live; the exit test is at the bottom
+  for (int i = 0; __builtin_amdgcn_ballot_w64(!deada || !deadb); ++i) {
     const uint32_t DM = pk(deada ? 0xffff : 0, deadb ? 0xffff : 0);
     const int ta = tna, tbb = tnb;
     tna = A.tb[min(i + 1, max(A.tlen - 1, 0))];  // prefetch
@@ -817,7 +821,7 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     IW = add(IW, ONE);
     IW1 = add(IW1, ONE);
     const uint32_t WD = usat(HI, LO);
-    const uint32_t LEFT0 = sub(umin(LO, ONE), ONE) & smax(GL, 0u);  // the first-column value where lo == 0
+    const uint32_t LEFT0 = neg15(sub(LO, ONE)) & smax(GL, 0u);  // the first-column value where lo == 0
     GL = ssat(GL, ED1);
     const uint32_t SEL = (uint32_t)ta | ((uint32_t)tbb << 16) | 0x0c040c00u;
     const uint32_t HI1 = add(HI, ONE);
@@ -859,12 +863,12 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     uint32_t CL = 0x7fff7fffu, CH = 0xffffffffu;
 #pragma unroll
     for (int c = CPL - 1; c >= 0; --c) {
-      const uint32_t nz = sub(0u, umin(hh[c] | ee[c], ONE));
+      const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));  // 0xffff where H or E is non-zero (both >= 0)
       CL = sel(nz & GEL[c], add(J0, pk(c, c)), CL);
     }
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      const uint32_t nz = sub(0u, umin(hh[c] | ee[c], ONE));
+      const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));
       CH = sel(nz & R[c], add(J0, pk(c, c)), CH);
     }
     // the row maxima (key H << 10 | j, ksw.c:433) and the trim, reduced over the half
@@ -877,7 +881,7 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     kb = half_max(row_max32(kb));
     // ksw.c:450-453 (meaningful on the owner of column qlen-1)
     {
-      const uint32_t AT = sub(umin(sub(smax(LO, HI), QL), ONE), ONE);  // 0xffff where max(lo, hi) == qlen
+      const uint32_t AT = neg15(sub(umin(sub(smax(LO, HI), QL), ONE), ONE));  // 0xffff where max(lo, hi) == qlen
       EI = sel(AT & ~neg15(sub(H1Q, ESC)), pk(i, i), EI);
       ESC = sel(AT, smax(ESC, H1Q), ESC);
     }
@@ -888,8 +892,8 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     const bool bb = quad_row_end(kb, i, e_del, e_ins, Bc.zdrop, bestb, bib, bjb, offb);
     rowsa = !deada && ba ? i + 1 : rowsa;
     rowsb = !deadb && bb ? i + 1 : rowsb;
-    deada = deada || ba;
-    deadb = deadb || bb;
+    deada = deada || ba || i + 1 >= A.tlen;  // a break, or its last target row
+    deadb = deadb || bb || i + 1 >= Bc.tlen;
     // the next row's band (ksw.c:466-469)
     const uint32_t NLO = smin(CL, HI);
     LO = NLO;
