@@ -146,8 +146,7 @@ PROTOS = {
     "bwagpu_debug_spec_counters": (C.c_int, [_VP, _VP, _VP]),
     "bwagpu_debug_spec_ext": (C.c_int, [_VP, _VP, _VP, C.c_int32]),
     "bwagpu_prof_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
-    "bwagpu_prof_intervals": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int32,
-                                        C.POINTER(C.c_int32)]),
+    "bwagpu_prof_intervals": (C.c_int, [_VP, _VP, _VP, C.c_int32, C.POINTER(C.c_int32)]),
     "bwagpu_set_bwt": (C.c_int, [_VP, C.POINTER(BwtC)]),
     "bwagpu_debug_seed_budget": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_debug_sup_shift": (C.c_int, [_VP, C.c_int32]),

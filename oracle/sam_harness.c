@@ -687,6 +687,74 @@ static void writer_put(writer_t *wr, bseq1_t *seqs, int n)
   pthread_mutex_unlock(&wr->mu);
 }
 
+/* gpuchain: the device stage runs one record ahead (bwa-flow's kflow
+   pipeline: SeqsToChains -> ChainsToRegions of record i+1 proceed while the SAM
+   stage works on record i, src/main.cpp:262-371, kflow/include/kflow/Pipeline.h:98-144).
+   A feeder thread owns its own device context and calls bwagpu_seqs2regions per
+   record, in order, at most FEED_DEPTH records ahead of the main thread, which
+   does the host post-processing, mem_pestat and the SAM passes (the SAM cache
+   on a second context) and hands the record to the writer; record order and
+   every per-record computation are those of the serial loop, so the SAM is the
+   same bytes. */
+enum { FEED_DEPTH = 2 };
+typedef struct {
+  int r0, n;
+  hw_t *w;
+} feed_job_t;
+typedef struct {
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+  feed_job_t *jobs;
+  int n_jobs, produced, consumed;
+  bwagpu_ctx_t *ctx;
+  const mem_opt_t *opt;
+  const bwaidx_t *idx;
+  bseq1_t *all;
+  int T;
+  double t_busy, t_dev;
+} feeder_t;
+static void *feeder_main(void *arg)
+{
+  feeder_t *f = (feeder_t *)arg;
+  for (int b = 0; b < f->n_jobs; ++b) {
+    pthread_mutex_lock(&f->mu);
+    while (f->produced - f->consumed >= FEED_DEPTH) pthread_cond_wait(&f->cv, &f->mu);
+    pthread_mutex_unlock(&f->mu);
+    feed_job_t *j = &f->jobs[b];
+    hw_t *w = (hw_t *)calloc(1, sizeof(hw_t));
+    w->opt = f->opt;
+    w->idx = f->idx;
+    w->seqs = f->all + j->r0;
+    w->chn = (chain_v *)calloc(j->n, sizeof(chain_v));
+    w->regs = (mem_alnreg_v *)calloc(j->n, sizeof(mem_alnreg_v));
+    w->n_processed = j->r0;
+    const double t0 = realtime();
+    seqs2regions_gpu(f->ctx, w, j->n, f->T, &f->t_dev);
+    f->t_busy += realtime() - t0;
+    pthread_mutex_lock(&f->mu);
+    j->w = w;
+    ++f->produced;
+    pthread_cond_broadcast(&f->cv);
+    pthread_mutex_unlock(&f->mu);
+  }
+  return 0;
+}
+static hw_t *feeder_take(feeder_t *f, int b)
+{
+  pthread_mutex_lock(&f->mu);
+  while (f->produced <= b) pthread_cond_wait(&f->cv, &f->mu);
+  hw_t *w = f->jobs[b].w;
+  pthread_mutex_unlock(&f->mu);
+  return w;
+}
+static void feeder_done(feeder_t *f)
+{
+  pthread_mutex_lock(&f->mu);
+  ++f->consumed;
+  pthread_cond_broadcast(&f->cv);
+  pthread_mutex_unlock(&f->mu);
+}
+
 int main(int argc, char *argv[])
 {
   if (argc < 7) {
@@ -796,9 +864,26 @@ int main(int argc, char *argv[])
     }
   }
   bwagpu_samcache_t *cache = 0;
+  /* gpuchain: the SAM cache on a context of its own (the feeder thread's
+     records run on ctx meanwhile) */
+  bwagpu_ctx_t *ctx_sam = ctx;
+  if (is_chain) {
+    bwagpu_opt_t go;
+    memset(&go, 0, sizeof go);
+    go.a = opt->a; go.b = opt->b; go.o_del = opt->o_del; go.e_del = opt->e_del; go.o_ins = opt->o_ins;
+    go.e_ins = opt->e_ins; go.pen_clip5 = opt->pen_clip5; go.pen_clip3 = opt->pen_clip3; go.w = opt->w;
+    go.zdrop = opt->zdrop;
+    memcpy(go.mat, opt->mat, 25);
+    const bntseq_t *bns = idx->bns;
+    int64_t *ao = (int64_t *)malloc(8 * bns->n_seqs);
+    int32_t *al = (int32_t *)malloc(4 * bns->n_seqs);
+    for (int i = 0; i < bns->n_seqs; ++i) { ao[i] = bns->anns[i].offset; al[i] = bns->anns[i].len; }
+    bwagpu_bns_t gb = {bns->l_pac, bns->n_seqs, 0, ao, al};
+    if (G.create(0, &go, &gb, idx->pac, &ctx_sam)) { fprintf(stderr, "bwagpu_create (SAM context) failed\n"); return 3; }
+  }
   /* first-launch capacities sized for short reads (2x150: a handful of CIGAR
      ops, MD well under 128 bytes); the rare longer ones are re-run with room */
-  if (is_sam && G.sc_create(ctx, 16, 128, &cache)) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
+  if (is_sam && G.sc_create(ctx_sam, 16, 128, &cache)) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
   int64_t n_passes = 0;
 
   FILE *out = fopen(outp, "w");
@@ -817,15 +902,47 @@ int main(int argc, char *argv[])
   writer_t wr = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, out, 0, 0, 0, 0};
   pthread_t wth;
   pthread_create(&wth, 0, writer_main, &wr);
+  /* the batches: reads until >= K bases, an even count (getKseqBatch / bseq_read) */
+  int n_jobs = 0;
+  feed_job_t *jobs = (feed_job_t *)calloc(n_all + 1, sizeof(feed_job_t));
   for (int r0 = 0; r0 < n_all;) {
-    /* a batch: reads until >= K bases, an even count (getKseqBatch / bseq_read) */
     int r1 = r0;
     int64_t bases = 0;
     while (r1 < n_all && bases < K) bases += all[r1++].l_seq;
     if ((r1 - r0) & 1) ++r1;
-    const int n = r1 - r0;
+    jobs[n_jobs].r0 = r0;
+    jobs[n_jobs++].n = r1 - r0;
+    r0 = r1;
+  }
+  feeder_t fd = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, jobs, n_jobs, 0, 0, ctx, opt, idx, all,
+                 T / 4 > 2 ? T / 4 : 2, 0, 0};
+  pthread_t fth;
+  if (is_chain) pthread_create(&fth, 0, feeder_main, &fd);
+  for (int b = 0; b < n_jobs; ++b) {
+    const int r0 = jobs[b].r0, n = jobs[b].n;
     bseq1_t *seqs = all + r0;
-    if (is_ref) {
+    if (is_chain) {
+      /* the feeder ran SeqsToChains + ChainsToRegions of this record */
+      t0 = realtime();
+      hw_t *wp = feeder_take(&fd, b);
+      t_seed += realtime() - t0; /* the main thread's wait for the device stage */
+      hw_t w = *wp;
+      free(wp);
+      t0 = realtime();
+      kt_for(T, w_free_chains, &w, n);
+      kt_for(T, w_post, &w, n);
+      t_post += realtime() - t0;
+      mem_pestat_t pes[4];
+      const double tq = realtime();
+      mem_pestat(opt, idx->bns->l_pac, n, w.regs, pes);
+      g_t_pestat += realtime() - tq;
+      w.pes = pes;
+      sam_passes(cache, &w, n, T, &n_passes, &t_flush);
+      t_sam += realtime() - t0;
+      free(w.chn);
+      free(w.regs);
+      feeder_done(&fd);
+    } else if (is_ref) {
       t0 = realtime();
       mem_process_seqs(opt, idx->bwt, idx->bns, idx->pac, n_processed, n, seqs, 0);
       t_ext += realtime() - t0;
@@ -833,13 +950,11 @@ int main(int argc, char *argv[])
       hw_t w = {opt, idx, seqs, (chain_v *)calloc(n, sizeof(chain_v)), (mem_alnreg_v *)calloc(n, sizeof(mem_alnreg_v)),
                 0, n_processed};
       t0 = realtime();
-      if (is_chain) seqs2regions_gpu(ctx, &w, n, T, &t_seed_dev); /* seeding + chain2aln: seed_s */
-      else if (is_seed) seed_gpu(ctx, &w, n, T, &t_seed_dev);
+      if (is_seed) seed_gpu(ctx, &w, n, T, &t_seed_dev);
       else kt_for(T, w_seed, &w, n);
       t_seed += realtime() - t0;
       t0 = realtime();
-      if (is_chain) {
-      } else if (is_gpu) ext_gpu(ctx, &w, n, T);
+      if (is_gpu) ext_gpu(ctx, &w, n, T);
       else kt_for(T, w_ext_cpu, &w, n);
       t_ext += realtime() - t0;
       t0 = realtime();
@@ -861,8 +976,12 @@ int main(int argc, char *argv[])
     writer_put(&wr, seqs, n); /* waits for the previous batch's output */
     t_out += realtime() - t_o;
     n_processed += n;
-    r0 = r1;
   }
+  if (is_chain) {
+    pthread_join(fth, 0);
+    t_seed_dev = fd.t_dev;
+  }
+  free(jobs);
   {
     const double t_o = realtime();
     writer_wait(&wr);
@@ -881,10 +1000,11 @@ int main(int argc, char *argv[])
                   "\"sam_s\": %.4f, \"flush_s\": %.4f, \"sam_passes\": %ld, \"align2_calls\": %ld, "
                   "\"reg2aln_calls\": %ld, \"seed_device_s\": %.4f, \"post_s\": %.4f, \"out_s\": %.4f, \"ext_flat_s\": %.4f, "
                   "\"ext_call_s\": %.4f, \"ext_unflat_s\": %.4f, \"pass0_s\": %.4f, \"pass1_s\": %.4f, \"pass2_s\": %.4f, "
-                  "\"clear_s\": %.4f, \"pestat_s\": %.4f, \"total_s\": %.4f}\n",
+                  "\"clear_s\": %.4f, \"pestat_s\": %.4f, \"feeder_s\": %.4f, \"total_s\": %.4f}\n",
           mode, (long)n_processed, T, t_seed, t_ext, t_sam, t_flush, (long)n_passes, (long)st[4], (long)st[5],
-          t_seed_dev, t_post, t_out, g_t_flat, g_t_call, g_t_unflat, g_t_pass[0], g_t_pass[1], g_t_pass[2], g_t_clear, g_t_pestat, t_all);
+          t_seed_dev, t_post, t_out, g_t_flat, g_t_call, g_t_unflat, g_t_pass[0], g_t_pass[1], g_t_pass[2], g_t_clear, g_t_pestat, fd.t_busy, t_all);
   if (cache) G.sc_destroy(cache);
+  if (ctx_sam && ctx_sam != ctx) G.destroy(ctx_sam);
   if (ctx) G.destroy(ctx);
   free(all);
   free(opt);
