@@ -2721,6 +2721,62 @@ __device__ __forceinline__ SeedExt qtask_ext(const QTask& t) {
   return e;
 }
 
+// The sub-slots' task states wait in LDS while a call runs (loaded before and
+// stored after it): kept in registers across extend_quad they cost ~50 VGPRs,
+// which at 2 waves per SIMD left the other caller stream's selection kernels
+// no room on the SIMD.
+static_assert(sizeof(QTask) <= 112, "QTask layout");
+constexpr int kQTaskLds = 112;
+typedef volatile __attribute__((address_space(3))) QTask LdsQ;
+__device__ __forceinline__ void qpark(LdsQ* p, const QTask& t) {
+  p->rbeg = t.rbeg;
+  p->wlo = t.wlo;
+  p->whi = t.whi;
+  p->qoff = t.qoff;
+  p->rb = t.rb;
+  p->re = t.re;
+  p->pos = t.pos;
+  p->qbeg = t.qbeg;
+  p->len = t.len;
+  p->lq = t.lq;
+  p->phase = t.phase;
+  p->score = t.score;
+  p->truesc = t.truesc;
+  p->qb = t.qb;
+  p->qe = t.qe;
+  p->sc0 = t.sc0;
+  p->aw0 = t.aw0;
+  p->aw1 = t.aw1;
+  p->cells = t.cells;
+  p->rows = t.rows;
+  p->calls = t.calls;
+}
+__device__ __forceinline__ QTask qload(LdsQ* p) {
+  QTask t;
+  t.rbeg = p->rbeg;
+  t.wlo = p->wlo;
+  t.whi = p->whi;
+  t.qoff = p->qoff;
+  t.rb = p->rb;
+  t.re = p->re;
+  t.pos = p->pos;
+  t.qbeg = p->qbeg;
+  t.len = p->len;
+  t.lq = p->lq;
+  t.phase = p->phase;
+  t.score = p->score;
+  t.truesc = p->truesc;
+  t.qb = p->qb;
+  t.qe = p->qe;
+  t.sc0 = p->sc0;
+  t.aw0 = p->aw0;
+  t.aw1 = p->aw1;
+  t.cells = p->cells;
+  t.rows = p->rows;
+  t.calls = p->calls;
+  return t;
+}
+
 // Extension tasks of one list (in pair order, spec_sort_*), four per wave.
 // PMAX = the bin's largest CPL: ceil(read length / 32).
 template <int PMAX>
@@ -2728,16 +2784,17 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
                                                            int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int hf = (int)(threadIdx.x >> 5) & 1;
-  // per half: A left, A right, B left, B right target rows
-  uint8_t* const tal = lds + (size_t)(threadIdx.x >> 5) * 4 * tb_bytes;
+  // per half: A left, A right, B left, B right target rows, then A's and B's task states
+  uint8_t* const tal = lds + (size_t)(threadIdx.x >> 5) * (4 * (size_t)tb_bytes + 2 * kQTaskLds);
   uint8_t* const tar = tal + tb_bytes;
   uint8_t* const tbl = tar + tb_bytes;
   uint8_t* const tbr = tbl + tb_bytes;
+  LdsQ* const qa = (LdsQ*)(tbr + tb_bytes);
+  LdsQ* const qb = (LdsQ*)(tbr + tb_bytes + kQTaskLds);
   const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
   ShardQ qq;
   qq.init(a.qh + 8 * kQHStride * list, n);
-  QTask sa, sb;
   bool ha = false, hb = false, more = n > 0;
   long long spec_cells = 0;
   for (;;) {
@@ -2749,44 +2806,61 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
         if (qq.claim(n0 + n1, m0, cap)) {
           const int ia = m0 + (hf ? n0 : 0), ib = ia + (ha ? 0 : 1);
           if (!ha && ia < cap) {
-            qtask_start(sa, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
-            ha = true;
+            QTask t;
+            qtask_start(t, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
+            if (t.phase >= 4) store_ext_half(a.ext + t.pos, qtask_ext(t));  // a whole-read seed (bwamem.c:753, 781)
+            else qpark(qa, t);
+            ha = t.phase < 4;
           }
           if (!hb && ib < cap) {
-            qtask_start(sb, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
-            hb = true;
+            QTask t;
+            qtask_start(t, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
+            if (t.phase >= 4) store_ext_half(a.ext + t.pos, qtask_ext(t));
+            else qpark(qb, t);
+            hb = t.phase < 4;
           }
         } else {
           more = false;
         }
       }
     }
-    if (ha && sa.phase >= 4) {  // a seed spanning the whole read: no extension (bwamem.c:753, 781)
-      store_ext_half(a.ext + sa.pos, qtask_ext(sa));
-      ha = false;
-    }
-    if (hb && sb.phase >= 4) {
-      store_ext_half(a.ext + sb.pos, qtask_ext(sb));
-      hb = false;
-    }
     if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
       if (!more) break;
       continue;
     }
-    const QCall ca = ha ? qtask_call(sa, o, b.seq, tal, tar) : quad_idle(b.seq, tal);
-    const QCall cb = hb ? qtask_call(sb, o, b.seq, tbl, tbr) : quad_idle(b.seq, tbl);
+    QCall ca = quad_idle(b.seq, tal), cb = quad_idle(b.seq, tbl);
+    if (ha) {
+      QTask t = qload(qa);
+      ca = qtask_call(t, o, b.seq, tal, tar);
+      qpark(qa, t);
+    }
+    if (hb) {
+      QTask t = qload(qb);
+      cb = qtask_call(t, o, b.seq, tbl, tbr);
+      qpark(qb, t);
+    }
     ExtOut xa, xb;
     Tally32 ta{0, 0, 0}, tb{0, 0, 0};
     extend_quad_dispatch<PMAX>(o, ca, cb, xa, xb, ta, tb);
-    if (ha && qtask_advance(sa, o, xa, ta)) {
-      store_ext_half(a.ext + sa.pos, qtask_ext(sa));
-      spec_cells += sa.cells;
-      ha = false;
+    if (ha) {
+      QTask t = qload(qa);
+      if (qtask_advance(t, o, xa, ta)) {
+        store_ext_half(a.ext + t.pos, qtask_ext(t));
+        spec_cells += t.cells;
+        ha = false;
+      } else {
+        qpark(qa, t);
+      }
     }
-    if (hb && qtask_advance(sb, o, xb, tb)) {
-      store_ext_half(a.ext + sb.pos, qtask_ext(sb));
-      spec_cells += sb.cells;
-      hb = false;
+    if (hb) {
+      QTask t = qload(qb);
+      if (qtask_advance(t, o, xb, tb)) {
+        store_ext_half(a.ext + t.pos, qtask_ext(t));
+        spec_cells += t.cells;
+        hb = false;
+      } else {
+        qpark(qb, t);
+      }
     }
   }
   if ((threadIdx.x & 31) == 0 && spec_cells)
@@ -2794,7 +2868,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
 }
 
 // LDS bytes of a spec_ext4_kernel workgroup
-static size_t ext4_lds(int tb_bytes) { return (size_t)(kBlock / 32) * 4 * (size_t)tb_bytes; }
+static size_t ext4_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (4 * (size_t)tb_bytes + 2 * kQTaskLds); }
 
 
 // Task order for the pair kernel: the two seeds a wave takes should need the
