@@ -918,7 +918,7 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
     for (int i = kNumExtVariants - 1; i >= 0; --i)
       if (t.qlen + 1 <= kExtVariants[i].max_len()) v = i;
     if (quad && t.h0 > 0 && t.qlen >= 1 && t.qlen + 1 <= 256 &&
-        quad_bound_ok(ctx->opt, t.h0 + (long)t.qlen * ctx->opt.max_mat)) {
+        quad_bound_ok(ctx->opt, t.h0 + (long)t.qlen * ctx->opt.max_mat) && quad_rows_ok(ctx->opt, t.tlen)) {
       bool nt = true;  // no N in the target rows
       for (int64_t i = t.toff; i < t.toff + t.tlen && nt; ++i) nt = tpool[i] <= 3;
       if (nt) v = kNumExtVariants;

@@ -678,6 +678,7 @@ __device__ __forceinline__ int hi16(uint32_t x) { return (int)(int16_t)(x >> 16)
 __device__ __forceinline__ uint32_t add(uint32_t a, uint32_t b) { return W(U(a) + U(b)); }
 __device__ __forceinline__ uint32_t sub(uint32_t a, uint32_t b) { return W(U(a) - U(b)); }
 __device__ __forceinline__ uint32_t mad(uint32_t a, uint32_t b, uint32_t c) { return W(U(a) * U(b) + U(c)); }
+__device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) { return W(U(a) * U(b)); }
 __device__ __forceinline__ uint32_t smax(uint32_t a, uint32_t b) { return W(__builtin_elementwise_max(S(a), S(b))); }
 __device__ __forceinline__ uint32_t smin(uint32_t a, uint32_t b) { return W(__builtin_elementwise_min(S(a), S(b))); }
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return W(__builtin_elementwise_max(U(a), U(b))); }
@@ -750,21 +751,6 @@ __device__ __forceinline__ QCall quad_idle(const uint8_t* seq, const uint8_t* tb
   return q;
 }
 
-// ksw.c:454-465 for one call from its row's reduced key H << 10 | j; true = exit
-__device__ __forceinline__ bool quad_row_end(int rkr, int i, int e_del, int e_ins, int zdrop, int& best, int& bi,
-                                             int& bj, int& off) {
-  const int mrow = rkr >> 10, mj = rkr & 1023;
-  const bool up = mrow > best;
-  const int di = i - bi, dj = mj - bj;
-  const int drop = best - mrow - max(__mul24(di - dj, e_del), __mul24(dj - di, e_ins));
-  const bool brk = mrow == 0 || (!up && zdrop > 0 && drop > zdrop);
-  off = up ? max(off, abs(mj - i)) : off;
-  best = up ? mrow : best;
-  bi = up ? i : bi;
-  bj = up ? mj : bj;
-  return brk;
-}
-
 template <int CPL>
 __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa, ExtOut& xb,
                                             Tally32& ta, Tally32& tbl) {
@@ -805,13 +791,18 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   uint32_t IW = pk(-wa, -wb), IW1 = pk(wa + 1, wb + 1);
   uint32_t GL = pk(A.h0 - o.o_del - e_del, Bc.h0 - o.o_del - e_del);  // h0 - (o_del + e_del (i+1))
   uint32_t EI = pk(-1, -1), ESC = pk(-1, -1);
-  int besta = A.h0, bia = -1, bja = -1, offa = 0, bestb = Bc.h0, bib = -1, bjb = -1, offb = 0;
-  int cellsa = 0, cellsb = 0, rowsa = max(A.tlen, 0), rowsb = max(Bc.tlen, 0);
-  bool deada = A.tlen <= 0, deadb = Bc.tlen <= 0;
+  // the row-end state of both calls, packed (ksw.c:454-465): max, its cell,
+  // max_off, the rows run, and DM = 0xffff once a call has ended
+  uint32_t BEST = pk(A.h0, Bc.h0), BI = pk(-1, -1), BJ = pk(-1, -1), OFF = 0, I = 0;
+  uint32_t ROWS = pk(max(A.tlen, 0), max(Bc.tlen, 0));
+  uint32_t DM = pk(A.tlen <= 0 ? 0xffff : 0, Bc.tlen <= 0 ? 0xffff : 0);
+  const uint32_t ZD = pk(min(A.zdrop, 32767), min(Bc.zdrop, 32767));
+  const uint32_t ZDM = pk(A.zdrop > 0 ? 0xffff : 0, Bc.zdrop > 0 ? 0xffff : 0);
+  const uint32_t TL2 = pk(A.tlen - 2, Bc.tlen - 2);  // i + 1 >= tlen <=> tlen - 2 - i < 0
+  int cellsa = 0, cellsb = 0;
   int tna = A.tb[0], tnb = Bc.tb[0];
   // rows run while a call of the wave is live; the exit test is at the bottom
-  for (int i = 0; __builtin_amdgcn_ballot_w64(!deada || !deadb); ++i) {
-    const uint32_t DM = pk(deada ? 0xffff : 0, deadb ? 0xffff : 0);
+  for (int i = 0; __builtin_amdgcn_ballot_w64(DM != 0xffffffffu); ++i) {
     const int ta = tna, tbb = tnb;
     tna = A.tb[min(i + 1, max(A.tlen - 1, 0))];  // prefetch
     tnb = Bc.tb[min(i + 1, max(Bc.tlen - 1, 0))];
@@ -887,13 +878,22 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     }
     cellsa += (int)(WD & 0xffffu);
     cellsb += (int)(WD >> 16);
-    // branch-free: an ended call's row maximum is 0, which changes nothing
-    const bool ba = quad_row_end(ka, i, e_del, e_ins, A.zdrop, besta, bia, bja, offa);
-    const bool bb = quad_row_end(kb, i, e_del, e_ins, Bc.zdrop, bestb, bib, bjb, offb);
-    rowsa = !deada && ba ? i + 1 : rowsa;
-    rowsb = !deadb && bb ? i + 1 : rowsb;
-    deada = deada || ba || i + 1 >= A.tlen;  // a break, or its last target row
-    deadb = deadb || bb || i + 1 >= Bc.tlen;
+    // ksw.c:454-465 on both calls at once (16-bit: quad_rows_ok); branch-free:
+    // an ended call's row maximum is 0, which changes nothing but its break
+    {
+      const uint32_t MROW = pk(ka >> 10, kb >> 10), MJ = pk(ka & 1023, kb & 1023);
+      const uint32_t UP = neg15(sub(BEST, MROW));  // m > max
+      const uint32_t DD = sub(sub(I, BI), sub(MJ, BJ));
+      const uint32_t DROP = sub(sub(BEST, MROW), smax(mul(DD, ED1), mul(sub(0u, DD), EI1)));
+      const uint32_t BRK = neg15(sub(MROW, ONE)) | (~UP & ZDM & neg15(ssat(ZD, DROP)));  // m == 0 or a z-drop
+      ROWS = sel(~DM & BRK, add(I, ONE), ROWS);
+      OFF = sel(UP, smax(OFF, smax(sub(MJ, I), sub(I, MJ))), OFF);
+      BEST = sel(UP, MROW, BEST);
+      BI = sel(UP, I, BI);
+      BJ = sel(UP, MJ, BJ);
+      DM = DM | BRK | neg15(sub(TL2, I));  // a break, or its last target row
+      I = add(I, ONE);
+    }
     // the next row's band (ksw.c:466-469)
     const uint32_t NLO = smin(CL, HI);
     LO = NLO;
@@ -903,13 +903,13 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   const int hb = (int)(threadIdx.x & 32);
   const uint32_t ea = __shfl(pk(lo16(EI), lo16(ESC)), hb + (A.qlen - 1) / CPL, 64);
   const uint32_t eb = __shfl(pk(hi16(EI), hi16(ESC)), hb + (Bc.qlen - 1) / CPL, 64);
-  xa = ExtOut{besta, bja + 1, bia + 1, lo16(ea) + 1, hi16(ea), offa};
-  xb = ExtOut{bestb, bjb + 1, bib + 1, lo16(eb) + 1, hi16(eb), offb};
+  xa = ExtOut{lo16(BEST), lo16(BJ) + 1, lo16(BI) + 1, lo16(ea) + 1, hi16(ea), lo16(OFF)};
+  xb = ExtOut{hi16(BEST), hi16(BJ) + 1, hi16(BI) + 1, lo16(eb) + 1, hi16(eb), hi16(OFF)};
   ta.cells += cellsa;
-  ta.rows += rowsa;
+  ta.rows += lo16(ROWS);
   ta.calls += 1;
   tbl.cells += cellsb;
-  tbl.rows += rowsb;
+  tbl.rows += hi16(ROWS);
   tbl.calls += 1;
 }
 
@@ -3986,12 +3986,19 @@ bool quad_bound_ok(const DevOpt& o, long hb) {  // hb: a bound on every H of the
          o.oe_ins + 128L < 32768 && o.e_del < 32768;
 }
 bool quad_scores_ok(const DevOpt& o, int lq) { return quad_bound_ok(o, (long)lq * o.max_mat); }
+// the packed row-end state for calls of up to `rows` target rows: i, |i - j|
+// and the z-drop term max((di - dj) e_del, (dj - di) e_ins) (di <= rows,
+// dj <= 256) within 16 bits beside H < 4096
+bool quad_rows_ok(const DevOpt& o, long rows) {
+  return rows >= 0 && rows < 16384 && (rows + 256) * std::max(o.e_del, o.e_ins) < 28672;
+}
 
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
                              int tb_bytes, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
-  const bool quad = g_ext_form.load(std::memory_order_relaxed) == 0 && quad_scores_ok(o, kSpecBinLen[1]);
+  const bool quad = g_ext_form.load(std::memory_order_relaxed) == 0 && quad_scores_ok(o, kSpecBinLen[1]) &&
+                    quad_rows_ok(o, tb_bytes);
   const size_t lds2 = quad ? ext4_lds(tb_bytes) : ext2_lds(tb_bytes);
   // the first two length bins' lists in pair order (spec_sort_*), then two or
   // four seeds per wave; the third (reads > 256 bp) one seed per wave

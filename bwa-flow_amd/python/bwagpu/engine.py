@@ -268,7 +268,8 @@ class Engine:
         sk = int(mm).bit_length()
         hb = lq * mm
         return (hb < 4096 and (hb << sk) + 128 < 32768 and hb + 33 * 8 * o.e_ins < 32768
-                and o.o_del + 128 < 32768 and o.o_ins + o.e_ins + 128 < 32768 and o.e_del < 32768)
+                and o.o_del + 128 < 32768 and o.o_ins + o.e_ins + 128 < 32768 and o.e_del < 32768
+                and (lq + 2 * o.w + 18 + 256) * max(o.e_del, o.e_ins) < 28672)  # quad_rows_ok(tb rows)
 
     def sup_shift(self, shift: int):
         """superblock size 2^shift of the occurrence layout the NEXT set_bwt builds (tests; default 32)"""
