@@ -1380,6 +1380,7 @@ int bwagpu_debug_set_trace(bwagpu_ctx_t* ctx, void* dev_ptr) {
   if (!ctx) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   HIPC(set_trace(dev_ptr), "set trace");
+  HIPC(set_trace_spec(dev_ptr), "set trace");
   return BWAGPU_OK;
 }
 

@@ -259,6 +259,7 @@ hipError_t launch_sw_stream(const DevOpt& o, const DevRef& ref, const StreamArgs
 
 // diagnostics: per-read trace buffer (device pointer, 8 x u32 per read; NULL = off)
 hipError_t set_trace(void* dev_ptr);
+hipError_t set_trace_spec(void* dev_ptr);  // spec.hip's copy of the trace pointer
 
 // rows a task can touch: the band is empty once i - w >= qlen (ksw.c:417-419),
 // so rows i <= qlen + w are the most ever read (the last one only to break)

@@ -1,0 +1,1767 @@
+// spec.hip — the speculative mem_chain2aln (default path of
+// bwagpu_chain2aln): extension task rounds on persistent grids
+// (one, two or four ksw_extend2 calls per wave, ksw_dev.h) and the selection
+// passes that replay bwa's sequential seed logic (bwamem.c:641-795) exactly
+// over the precomputed extensions.
+#include "ksw_dev.h"
+
+namespace bwagpu {
+
+// per-read selection trace (bwagpu_debug_set_trace; this file's copy)
+__device__ uint32_t* g_trace = nullptr;
+hipError_t set_trace_spec(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p)); }
+
+// ============================================================ speculative chain2aln
+// mem_chain2aln (bwamem.c:641-795) restructured for load balance on
+// reference-seeded batches, where a few reads (tandem repeats: hundreds of
+// seeds, one region each) carry more DP than thousands of ordinary reads and,
+// run serially by one wave, set the stage's critical path.
+//
+// The one sequential dependency of mem_chain2aln is the decision whether a
+// seed is extended at all: the containment test against the read's regions so
+// far (bwamem.c:678-697) and the overlapping-seed test (698-707).  The
+// extension itself (717-792: left ksw_extend2 with the band retry, right
+// ksw_extend2 from the left score, local vs to-end choice) depends only on the
+// seed, the read and its chain's window.  So:
+//   round A   extend the first seed (processing order) of every chain — it is
+//             almost always extended; one wave per task, dynamic queue;
+//   emulate   replay the sequential logic per read with the round-A regions:
+//             every seed that would be extended and has no result yet becomes
+//             a round-B task (its region unknown, so later seeds of the read
+//             are tested against fewer regions: a superset is predicted);
+//   round B   extend those;
+//   final     replay the sequential logic exactly, with every result it needs
+//             precomputed except rare mispredictions, which it computes inline.
+// Output = the reference's regions, byte for byte; the stats count only the DP
+// of extensions mem_chain2aln performs (spec work is a separate diagnostic).
+
+// lane per chain: window (bwamem.c:648-668 + bns_fetch_seq's clipping), the
+// round-A task (the chain's first seed in processing order) and, for chains
+// of up to kOrderLane seeds, the processing order; longer chains are listed
+// for spec_order_kernel, which does their window and order one workgroup
+// each (a lane looping over ~170 seeds was this kernel's tail).  chain_read
+// comes from spec_reads_kernel.
+__global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  bool task = false, longc = false;
+  int bin = 0, s0 = 0;
+  if (c < b.n_chains) {
+    const int rd = a.chain_read[c];
+    s0 = b.chain_seed_off[c];
+    const int ns = b.chain_seed_off[c + 1] - s0;
+    const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+    if (ns <= 0) {
+      a.win[c] = ChainWin{0, 0};
+    } else {
+      int64_t wlo = ref.l_pac << 1, whi = 0;
+      longc = ns > kOrderLane;
+      if (!longc) {
+        // the processing order (descending key score<<32|i, bwamem.c:671-676),
+        // ranked in registers
+        uint64_t key[kOrderLane];
+#pragma unroll
+        for (int t = 0; t < kOrderLane; ++t) {
+          key[t] = ~0ull;
+          if (t < ns) {
+            const bwagpu_seed_t v = b.seeds[s0 + t];
+            key[t] = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)t;
+            seed_reach(o, v, lq, wlo, whi);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < kOrderLane; ++t) {
+          if (t < ns) {
+            int rank = 0;
+#pragma unroll
+            for (int u = 0; u < kOrderLane; ++u) rank += key[u] < key[t];
+            bwagpu_seed_t v = b.seeds[s0 + t];
+            v.pad_ = key[t] == 0 ? 1 : 0;
+            a.prog[s0 + ns - 1 - rank] = v;
+            a.seedchain[s0 + ns - 1 - rank] = c;
+          }
+        }
+      }
+      const bool ok = finish_window(ref, b.chain_rid[c], b.seeds[s0].rbeg, wlo, whi);
+      if (!ok) {
+        atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_RID);
+        a.win[c] = ChainWin{0, -1};
+      } else {
+        if (!longc) a.win[c] = ChainWin{wlo, whi};
+        task = lq <= BWAGPU_MAX_READ_LEN;
+        bin = spec_bin(lq);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kSpecBins; ++k) {
+    const int p = wave_append(&a.ctr[SPC_CNT + k], task && bin == k);
+    if (p >= 0) a.tasks[(size_t)k * b.n_chains + p] = make_int2(s0, c);
+  }
+  const int p = wave_append(&a.ctr[SPC_LONG_N], longc);
+  if (p >= 0) a.longc[p] = c;
+}
+
+// rows are triangular: row k holds words w < ceil(k / 64) (only seeds j < k
+// count); tri_off(k) = sum over i < k of ceil(i / 64)
+__host__ __device__ inline int64_t tri_off(int k) {
+  if (k <= 1) return 0;
+  const int64_t q = (k - 1) >> 6;
+  return 32 * q * (q + 1) + (int64_t)(k - 1 - 64 * q) * (q + 1);
+}
+
+// lane per read: length check, and the list of heavy reads (selected first)
+__global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a) {
+  const int rd = blockIdx.x * blockDim.x + threadIdx.x;
+  bool heavy = false;
+  int ns = 0;
+  if (rd < b.n_reads) {
+    const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+    if (lq > BWAGPU_MAX_READ_LEN) atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_LEN);
+    ReadDesc d;
+    d.qoff = b.seq_off[rd];
+    d.rd = rd;
+    d.lq = lq;
+    d.c0 = b.read_chain_off[rd];
+    d.nch = b.read_chain_off[rd + 1] - d.c0;
+    d.s0 = b.chain_seed_off[d.c0];
+    d.ns = b.chain_seed_off[d.c0 + d.nch] - d.s0;
+    a.rdesc[rd] = d;
+    for (int c = d.c0; c < d.c0 + d.nch; ++c) a.chain_read[c] = rd;
+    heavy = d.ns > kSelLight || d.nch > kSelLight;
+    ns = d.ns;
+  }
+  const int p = wave_append(&a.ctr[SPC_HEAVY_N], heavy);
+  if (p >= 0) {
+    a.heavy[p] = rd;
+    // the read's pair matrices (kSelMatMaxSeeds seeds at most, and room left)
+    const long long words = 2 * tri_off(ns);
+    int woff = -1, col = 0;
+    if (ns <= kSelMatMaxSeeds) {
+      const long long o = (long long)atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr[SPC_MATW64]),
+                                               (unsigned long long)words);
+      if (o + words <= a.mat_words) {
+        woff = (int)o;
+        col = atomicAdd(&a.ctr[SPC_HCOLS], ns);
+        for (int i = 0; i < ns; ++i) a.colent[col + i] = p;
+      }
+    }
+    a.hinfo[p] = make_int4(rd, woff, col, ns);
+  }
+}
+
+// The processing order (descending key score<<32|i, bwamem.c:671-676) of
+// the chains spec_chain_kernel listed (more than kOrderLane seeds), by
+// ranking: keys are unique, so rank = the number of smaller keys.  One
+// workgroup per chain with the keys staged in LDS (a lane looping over global
+// keys made the longest chain, ~170 seeds, a 250 us tail).  pad_ = 1 flags
+// the key that is 0 from the start (skipped by the overlap test like a
+// marked seed, bwamem.c:700).
+constexpr int kOrderBlocks = 1024;
+constexpr int kOrderLds = 4096;  // longer chains rank against global memory
+__device__ __forceinline__ uint64_t order_key(const bwagpu_seed_t* sd, int i) {
+  return (uint64_t)(uint32_t)sd[i].score << 32 | (uint32_t)i;
+}
+__global__ void __launch_bounds__(256) spec_order_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+  __shared__ uint64_t keys[kOrderLds];
+  __shared__ int64_t wred[2][4];
+  const int tid = (int)threadIdx.x;
+  const int n_long = __hip_atomic_load(&a.ctr[SPC_LONG_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int gi = (int)blockIdx.x; gi < n_long; gi += (int)gridDim.x) {
+    const int g = a.longc[gi];
+    const int s0 = b.chain_seed_off[g], ns = b.chain_seed_off[g + 1] - s0;
+    const bwagpu_seed_t* sd = b.seeds + s0;
+    const bool in_lds = ns <= kOrderLds;
+    const int rd = a.chain_read[g];
+    const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+    int64_t wlo = ref.l_pac << 1, whi = 0;
+    for (int i = tid; i < ns; i += 256) {
+      const bwagpu_seed_t v = sd[i];
+      if (in_lds) keys[i] = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
+      seed_reach(o, v, lq, wlo, whi);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      wlo = min(wlo, (int64_t)__shfl_xor((long long)wlo, m, 64));
+      whi = max(whi, (int64_t)__shfl_xor((long long)whi, m, 64));
+    }
+    if ((tid & 63) == 0) {
+      wred[0][tid >> 6] = wlo;
+      wred[1][tid >> 6] = whi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      wlo = min(min(wred[0][0], wred[0][1]), min(wred[0][2], wred[0][3]));
+      whi = max(max(wred[1][0], wred[1][1]), max(wred[1][2], wred[1][3]));
+      if (finish_window(ref, b.chain_rid[g], sd[0].rbeg, wlo, whi)) a.win[g] = ChainWin{wlo, whi};
+    }
+    for (int i = tid; i < ns; i += 256) {
+      bwagpu_seed_t v = sd[i];
+      const uint64_t ki = (uint64_t)(uint32_t)v.score << 32 | (uint32_t)i;
+      int rank = 0;
+      if (in_lds)
+        for (int j = 0; j < ns; ++j) rank += keys[j] < ki;
+      else
+        for (int j = 0; j < ns; ++j) rank += order_key(sd, j) < ki;
+      v.pad_ = ki == 0 ? 1 : 0;
+      a.prog[s0 + ns - 1 - rank] = v;
+      a.seedchain[s0 + ns - 1 - rank] = g;
+    }
+    __syncthreads();
+  }
+}
+
+
+// Extension tasks of one list (round * kSpecBins + bin): one wave per task,
+// claimed one at a time from the sharded queue (a wave holding a second task
+// while others idle at the end of the list cost more: DESIGN.md §5).
+template <int C>
+__global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                          int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int wib = uni((int)(threadIdx.x >> 6));
+  uint8_t* const tbl = lds + wib * 2 * tb_bytes;
+  uint8_t* const tbr = tbl + tb_bytes;
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  ShardQ qq;
+  qq.init(a.qh + 8 * kQHStride * list, n);
+  long long spec_cells = 0;
+  int m0, cap;
+  while (qq.claim(1, m0, cap)) {
+    for (int m = m0; m < m0 + 1 && m < cap; ++m) {
+      const int2 tk = tl[qq.shard + 8 * m];
+      const int pos = uni(tk.x), c = uni(tk.y);
+      const int rd = uni(a.chain_read[c]);
+      const int64_t qoff = uni64(b.seq_off[rd]);
+      const int lq = uni((int)(b.seq_off[rd + 1] - qoff));
+      const bwagpu_seed_t s = uni_seed(a.prog[pos]);
+      ChainWin cw = a.win[c];
+      cw.lo = uni64(cw.lo);
+      cw.hi = uni64(cw.hi);
+      const SeedExt e = extend_seed<C>(o, ref, s, lq, b.seq + qoff, cw, tbl, tbr);
+      store_ext(a.ext + pos, e);
+      spec_cells += e.cells;
+    }
+  }
+  if ((threadIdx.x & 63) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+// ---------------------------------------------------- two seeds per wave
+// The same extension tasks with one seed per 32-lane half (extend_pair).
+// Everything below is per lane and uniform over a half; the halves diverge
+// only through EXEC (a half without a left side, a retry or a task waits for
+// the other).
+//
+// Both target windows of the half's seed into its LDS rows (fill_two on 32
+// lanes: 4 loads per side per lane in flight, 128 rows per side per pass).
+__device__ __forceinline__ void fill_two_half(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
+                                              const DevRef& ref) {
+  const int r = (int)(threadIdx.x & 31);
+  const int64_t two1 = (ref.l_pac << 1) - 1;
+  const int n = max(nl, nr);
+  for (int base = 0; base < n; base += 128) {
+    uint32_t raw[8];
+    int sh[8], kk[8];
+    bool rev[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const bool left = m < 4;
+      const int nn = left ? nl : nr;
+      const int k = min(base + (m & 3) * 32 + r, max(nn - 1, 0));
+      kk[m] = k;
+      const int64_t x = left ? x0l - k : x0r + k;
+      rev[m] = x >= ref.l_pac;
+      int64_t f = rev[m] ? two1 - x : x;
+      f = f < 0 ? 0 : (f >= ref.l_pac ? ref.l_pac - 1 : f);  // only for an empty side (nn == 0)
+      raw[m] = ref.pac[f >> 2];
+      sh[m] = (int)((~f & 3) << 1);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int bse = (raw[m] >> sh[m]) & 3;
+      const uint8_t v = (uint8_t)(rev[m] ? 3 - bse : bse);
+      if (m < 4) {
+        if (nl > 0) tbl[kk[m]] = v;
+      } else {
+        if (nr > 0) tbr[kk[m]] = v;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One half's task and the state of its extension, in LDS for the whole task:
+// re-read (volatile, LDS address space) around every call, so that none of it
+// occupies VGPRs across the DP loop.
+struct PairCtx {
+  int64_t rbeg, lo, hi, qoff;  // the seed, its chain's window, its read
+  int32_t qbeg, len, lq, phase;
+  int64_t rb, re;              // the region so far
+  int32_t score, truesc, qb, qe, sc0, aw0, aw1, cells, rows, calls, pad_[2];
+};
+static_assert(sizeof(PairCtx) == 112, "PairCtx layout");
+typedef volatile __attribute__((address_space(3))) PairCtx LdsCtx;
+
+// extend_seed (bwamem.c:717-792) for the half's seed, as a state machine with
+// ONE extend_pair call site: phase 0/1 = left side try 0/1 (MAX_BAND_TRY,
+// bwamem.c:639), 2/3 = right side, 4 = done; a half whose phases are over
+// leaves the loop (EXEC) while the other finishes.
+template <int PMAX>
+__device__ __forceinline__ SeedExt extend_seed2(const DevOpt& o, const DevRef& ref, LdsCtx* cx, const uint8_t* seq,
+                                                uint8_t* tbl, uint8_t* tbr) {
+  {
+    const int64_t rbeg = cx->rbeg, lo = cx->lo, hi = cx->hi;
+    const int qbeg = cx->qbeg, len = cx->len, lq = cx->lq;
+    const int qlenL = qbeg, qlenR = lq - (qbeg + len);
+    const int64_t x0R = rbeg + len;
+    fill_two_half(tbl, rbeg - 1, qlenL ? rows_needed(o, qlenL, (int)(rbeg - lo), o.w << 1, o.pen_clip5) : 0, tbr, x0R,
+                  qlenR ? rows_needed(o, qlenR, (int)(hi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
+    cx->phase = qbeg != 0 ? 0 : (qlenR != 0 ? 2 : 4);
+    const int sc = qbeg != 0 ? -1 : len * o.a;  // bwamem.c:753
+    cx->score = sc;
+    cx->truesc = sc;
+    cx->qb = 0;
+    cx->qe = lq;
+    cx->sc0 = 0;
+    cx->aw0 = o.w;
+    cx->aw1 = o.w;
+    cx->rb = rbeg;
+    cx->re = rbeg + len;
+    cx->cells = 0;
+    cx->rows = 0;
+    cx->calls = 0;
+  }
+  for (;;) {
+    const int phase = cx->phase;
+    if (phase >= 4) break;
+    const int64_t rbeg = cx->rbeg;
+    const int qbeg = cx->qbeg, len = cx->len, lq = cx->lq;
+    const bool left = phase < 2;
+    const int t = phase & 1;
+    const int qlenR = lq - (qbeg + len);
+    const int qlen = left ? qbeg : qlenR;
+    const int64_t x0 = left ? rbeg - 1 : rbeg + len;
+    const int tlen = left ? (int)(rbeg - cx->lo) : (int)(cx->hi - x0);
+    const int qa = left ? qbeg - 1 : qbeg + len;
+    const int eb = left ? o.pen_clip5 : o.pen_clip3;
+    if (t == 0) cx->sc0 = cx->score;
+    const int h0 = left ? len * o.a : cx->sc0;
+    const int aw = o.w << t;
+    if (left) cx->aw0 = aw;
+    else cx->aw1 = aw;
+    Tally32 tl{0, 0, 0};
+    const ExtOut x = extend_pair_dispatch<PMAX>(o, qlen, seq + cx->qoff, qa, left ? -1 : 1, tlen, left ? tbl : tbr, aw,
+                                             eb, o.zdrop, h0, tl);
+    cx->cells = cx->cells + tl.cells;
+    cx->rows = cx->rows + tl.rows;
+    cx->calls = cx->calls + tl.calls;
+    const int prev = cx->score;
+    const int score = x.score;
+    cx->score = score;
+    if (t == 0 && !(score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {
+      cx->phase = phase + 1;  // the band retry
+      continue;
+    }
+    const bool local = x.gscore <= 0 || x.gscore <= score - eb;
+    if (left) {
+      cx->qb = local ? qbeg - x.qle : 0;
+      cx->rb = rbeg - (local ? x.tle : x.gtle);
+      cx->truesc = local ? score : x.gscore;
+      cx->phase = qlenR != 0 ? 2 : 4;
+    } else {
+      cx->qe = local ? qa + x.qle : lq;
+      cx->re = x0 + (local ? x.tle : x.gtle);
+      cx->truesc = cx->truesc + (local ? score : x.gscore) - cx->sc0;
+      cx->phase = 4;
+    }
+  }
+  SeedExt e;
+  e.rb = cx->rb;
+  e.re = cx->re;
+  e.qb = cx->qb;
+  e.qe = cx->qe;
+  e.score = cx->score;
+  e.truesc = cx->truesc;
+  const int aw0 = cx->aw0, aw1 = cx->aw1;
+  e.w = aw0 > aw1 ? aw0 : aw1;
+  e.cells = cx->cells;
+  e.rows = cx->rows;
+  e.calls = cx->calls + 1;  // + 1: a computed slot is never all-zero
+  return e;
+}
+
+__device__ __forceinline__ void store_ext_half(SeedExt* dst, const SeedExt& e) {
+  const int d = (int)(threadIdx.x & 31);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&e);
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) v = d == k ? w[k] : v;
+  if (d < 12) reinterpret_cast<uint32_t*>(dst)[d] = v;
+}
+
+// Extension tasks of one list, two per wave: a wave claims two consecutive
+// entries of a shard (one atomic), lanes 0-31 take the first, 32-63 the second.
+// PMAX = the bin's largest CPL: ceil(read length / 32) (qlen + 1 <= read length)
+template <int PMAX>
+__global__ void __launch_bounds__(kBlock) spec_ext2_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                           int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int hf = (int)(threadIdx.x >> 5) & 1;
+  // per half: left rows, right rows, the task context
+  uint8_t* const tbl = lds + (size_t)(threadIdx.x >> 5) * (2 * tb_bytes + sizeof(PairCtx));
+  uint8_t* const tbr = tbl + tb_bytes;
+  LdsCtx* const cx = (LdsCtx*)(tbr + tb_bytes);
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);  // in pair order (spec_sort_*)
+  ShardQ qq;
+  qq.init(a.qh + 8 * kQHStride * list, n);
+  long long spec_cells = 0;
+  int m0, cap;
+  while (qq.claim(2, m0, cap)) {
+    const int m = m0 + hf;
+    if (m < cap) {
+      const int2 tk = tl[qq.shard + 8 * m];
+      const int pos = tk.x, c = tk.y;
+      if ((threadIdx.x & 31) == 0) {
+        const int rd = a.chain_read[c];
+        const bwagpu_seed_t s = a.prog[pos];
+        const ChainWin cw = a.win[c];
+        const int64_t qoff = b.seq_off[rd];
+        cx->rbeg = s.rbeg;
+        cx->lo = cw.lo;
+        cx->hi = cw.hi;
+        cx->qoff = qoff;
+        cx->qbeg = s.qbeg;
+        cx->len = s.len;
+        cx->lq = (int)(b.seq_off[rd + 1] - qoff);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const SeedExt e = extend_seed2<PMAX>(o, ref, cx, b.seq, tbl, tbr);
+      store_ext_half(a.ext + pos, e);
+      spec_cells += e.cells;
+    }
+  }
+  if ((threadIdx.x & 31) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+// LDS bytes of a spec_ext2_kernel workgroup
+static size_t ext2_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (2 * (size_t)tb_bytes + sizeof(PairCtx)); }
+
+// ---------------------------------------------------- four seeds per wave
+// The same extension tasks with two seeds per 32-lane half, packed in the
+// 16-bit halves of the DP registers (extend_quad).  Each sub-slot (half x
+// low/high) walks its own seed through extend_seed's state machine
+// (bwamem.c:717-792: left side with the band retry, right side from the left
+// score, local vs to-end), held in registers; the four sub-slots call
+// extend_quad together, and a sub-slot whose seed is done takes the next task
+// of the list at once (one claim per call boundary for all the sub-slots that
+// need one), so a wave idles only inside a call whose four rows counts differ.
+struct QTask {
+  int64_t rbeg, wlo, whi, qoff, rb, re;
+  int pos, qbeg, len, lq, phase, score, truesc, qb, qe, sc0, aw0, aw1, cells, rows, calls;
+};
+
+// the task's seed, window and read; both target windows into the sub-slot's LDS rows
+__device__ __forceinline__ void qtask_start(QTask& t, const DevOpt& o, const DevRef& ref, const DevBatch& b,
+                                            const SpecArgs& a, int2 tk, uint8_t* tl, uint8_t* tr) {
+  const int rd = a.chain_read[tk.y];
+  const bwagpu_seed_t s = a.prog[tk.x];
+  const ChainWin cw = a.win[tk.y];
+  t.pos = tk.x;
+  t.rbeg = s.rbeg;
+  t.wlo = cw.lo;
+  t.whi = cw.hi;
+  t.qoff = b.seq_off[rd];
+  t.lq = (int)(b.seq_off[rd + 1] - t.qoff);
+  t.qbeg = s.qbeg;
+  t.len = s.len;
+  const int qlenL = t.qbeg, qlenR = t.lq - (t.qbeg + t.len);
+  const int64_t x0R = t.rbeg + t.len;
+  fill_two_half(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, (int)(t.rbeg - t.wlo), o.w << 1, o.pen_clip5) : 0, tr,
+                x0R, qlenR ? rows_needed(o, qlenR, (int)(t.whi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
+  t.phase = qlenL != 0 ? 0 : (qlenR != 0 ? 2 : 4);
+  const int sc = qlenL != 0 ? -1 : t.len * o.a;  // bwamem.c:753
+  t.score = sc;
+  t.truesc = sc;
+  t.qb = 0;
+  t.qe = t.lq;
+  t.sc0 = 0;
+  t.aw0 = o.w;
+  t.aw1 = o.w;
+  t.rb = t.rbeg;
+  t.re = t.rbeg + t.len;
+  t.cells = t.rows = t.calls = 0;
+}
+
+// the ksw_extend2 call of the task's phase (0/1: left try 0/1, 2/3: right)
+__device__ __forceinline__ QCall qtask_call(QTask& t, const DevOpt& o, const uint8_t* seq, const uint8_t* tl,
+                                            const uint8_t* tr) {
+  const bool left = t.phase < 2;
+  const int tt = t.phase & 1;
+  const int qlenR = t.lq - (t.qbeg + t.len);
+  const int64_t x0 = left ? t.rbeg - 1 : t.rbeg + t.len;
+  QCall q;
+  q.qlen = left ? t.qbeg : qlenR;
+  q.tlen = left ? (int)(t.rbeg - t.wlo) : (int)(t.whi - x0);
+  q.qa = left ? t.qbeg - 1 : t.qbeg + t.len;
+  q.qd = left ? -1 : 1;
+  q.eb = left ? o.pen_clip5 : o.pen_clip3;
+  if (tt == 0) t.sc0 = t.score;
+  q.h0 = left ? t.len * o.a : t.sc0;
+  q.w = o.w << tt;
+  if (left) t.aw0 = q.w;
+  else t.aw1 = q.w;
+  q.zdrop = o.zdrop;
+  q.q = seq + t.qoff;
+  q.tb = left ? tl : tr;
+  return q;
+}
+
+// the call's result into the task (bwamem.c:737-792); true = the seed is done
+__device__ __forceinline__ bool qtask_advance(QTask& t, const DevOpt& o, const ExtOut& x, const Tally32& tl) {
+  const bool left = t.phase < 2;
+  const int tt = t.phase & 1;
+  t.cells += tl.cells;
+  t.rows += tl.rows;
+  t.calls += tl.calls;
+  const int prev = t.score;
+  t.score = x.score;
+  const int aw = o.w << tt;
+  if (tt == 0 && !(x.score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {  // the band retry (MAX_BAND_TRY)
+    t.phase += 1;
+    return false;
+  }
+  const int eb = left ? o.pen_clip5 : o.pen_clip3;
+  const bool local = x.gscore <= 0 || x.gscore <= x.score - eb;
+  if (left) {
+    t.qb = local ? t.qbeg - x.qle : 0;
+    t.rb = t.rbeg - (local ? x.tle : x.gtle);
+    t.truesc = local ? x.score : x.gscore;
+    t.phase = t.lq - (t.qbeg + t.len) != 0 ? 2 : 4;
+  } else {
+    t.qe = local ? t.qbeg + t.len + x.qle : t.lq;
+    t.re = t.rbeg + t.len + (local ? x.tle : x.gtle);
+    t.truesc += (local ? x.score : x.gscore) - t.sc0;
+    t.phase = 4;
+  }
+  return t.phase >= 4;
+}
+
+__device__ __forceinline__ SeedExt qtask_ext(const QTask& t) {
+  SeedExt e;
+  e.rb = t.rb;
+  e.re = t.re;
+  e.qb = t.qb;
+  e.qe = t.qe;
+  e.score = t.score;
+  e.truesc = t.truesc;
+  e.w = t.aw0 > t.aw1 ? t.aw0 : t.aw1;
+  e.cells = t.cells;
+  e.rows = t.rows;
+  e.calls = t.calls + 1;  // + 1: a computed slot is never all-zero
+  return e;
+}
+
+// The sub-slots' task states wait in LDS while a call runs (loaded before and
+// stored after it): kept in registers across extend_quad they cost ~50 VGPRs,
+// which at 2 waves per SIMD left the other caller stream's selection kernels
+// no room on the SIMD.
+static_assert(sizeof(QTask) <= 112, "QTask layout");
+constexpr int kQTaskLds = 112;
+typedef volatile __attribute__((address_space(3))) QTask LdsQ;
+__device__ __forceinline__ void qpark(LdsQ* p, const QTask& t) {
+  p->rbeg = t.rbeg;
+  p->wlo = t.wlo;
+  p->whi = t.whi;
+  p->qoff = t.qoff;
+  p->rb = t.rb;
+  p->re = t.re;
+  p->pos = t.pos;
+  p->qbeg = t.qbeg;
+  p->len = t.len;
+  p->lq = t.lq;
+  p->phase = t.phase;
+  p->score = t.score;
+  p->truesc = t.truesc;
+  p->qb = t.qb;
+  p->qe = t.qe;
+  p->sc0 = t.sc0;
+  p->aw0 = t.aw0;
+  p->aw1 = t.aw1;
+  p->cells = t.cells;
+  p->rows = t.rows;
+  p->calls = t.calls;
+}
+__device__ __forceinline__ QTask qload(LdsQ* p) {
+  QTask t;
+  t.rbeg = p->rbeg;
+  t.wlo = p->wlo;
+  t.whi = p->whi;
+  t.qoff = p->qoff;
+  t.rb = p->rb;
+  t.re = p->re;
+  t.pos = p->pos;
+  t.qbeg = p->qbeg;
+  t.len = p->len;
+  t.lq = p->lq;
+  t.phase = p->phase;
+  t.score = p->score;
+  t.truesc = p->truesc;
+  t.qb = p->qb;
+  t.qe = p->qe;
+  t.sc0 = p->sc0;
+  t.aw0 = p->aw0;
+  t.aw1 = p->aw1;
+  t.cells = p->cells;
+  t.rows = p->rows;
+  t.calls = p->calls;
+  return t;
+}
+
+// Extension tasks of one list (in pair order, spec_sort_*), four per wave.
+// PMAX = the bin's largest CPL: ceil(read length / 32).
+template <int PMAX>
+__global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                           int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int hf = (int)(threadIdx.x >> 5) & 1;
+  // per half: A left, A right, B left, B right target rows, then A's and B's task states
+  uint8_t* const tal = lds + (size_t)(threadIdx.x >> 5) * (4 * (size_t)tb_bytes + 2 * kQTaskLds);
+  uint8_t* const tar = tal + tb_bytes;
+  uint8_t* const tbl = tar + tb_bytes;
+  uint8_t* const tbr = tbl + tb_bytes;
+  LdsQ* const qa = (LdsQ*)(tbr + tb_bytes);
+  LdsQ* const qb = (LdsQ*)(tbr + tb_bytes + kQTaskLds);
+  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  ShardQ qq;
+  qq.init(a.qh + 8 * kQHStride * list, n);
+  bool ha = false, hb = false, more = n > 0;
+  long long spec_cells = 0;
+  for (;;) {
+    if (more) {  // every sub-slot without a seed takes the next entry: one claim for the wave
+      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha), nb = __builtin_amdgcn_ballot_w64(!hb);
+      const int n0 = (int)(na & 1) + (int)(nb & 1), n1 = (int)((na >> 32) & 1) + (int)((nb >> 32) & 1);
+      if (n0 + n1 > 0) {
+        int m0, cap;
+        if (qq.claim(n0 + n1, m0, cap)) {
+          const int ia = m0 + (hf ? n0 : 0), ib = ia + (ha ? 0 : 1);
+          if (!ha && ia < cap) {
+            QTask t;
+            qtask_start(t, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
+            if (t.phase >= 4) store_ext_half(a.ext + t.pos, qtask_ext(t));  // a whole-read seed (bwamem.c:753, 781)
+            else qpark(qa, t);
+            ha = t.phase < 4;
+          }
+          if (!hb && ib < cap) {
+            QTask t;
+            qtask_start(t, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
+            if (t.phase >= 4) store_ext_half(a.ext + t.pos, qtask_ext(t));
+            else qpark(qb, t);
+            hb = t.phase < 4;
+          }
+        } else {
+          more = false;
+        }
+      }
+    }
+    if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
+      if (!more) break;
+      continue;
+    }
+    QCall ca = quad_idle(b.seq, tal), cb = quad_idle(b.seq, tbl);
+    if (ha) {
+      QTask t = qload(qa);
+      ca = qtask_call(t, o, b.seq, tal, tar);
+      qpark(qa, t);
+    }
+    if (hb) {
+      QTask t = qload(qb);
+      cb = qtask_call(t, o, b.seq, tbl, tbr);
+      qpark(qb, t);
+    }
+    ExtOut xa, xb;
+    Tally32 ta{0, 0, 0}, tb{0, 0, 0};
+    extend_quad_dispatch<PMAX>(o, ca, cb, xa, xb, ta, tb);
+    if (ha) {
+      QTask t = qload(qa);
+      if (qtask_advance(t, o, xa, ta)) {
+        store_ext_half(a.ext + t.pos, qtask_ext(t));
+        spec_cells += t.cells;
+        ha = false;
+      } else {
+        qpark(qa, t);
+      }
+    }
+    if (hb) {
+      QTask t = qload(qb);
+      if (qtask_advance(t, o, xb, tb)) {
+        store_ext_half(a.ext + t.pos, qtask_ext(t));
+        spec_cells += t.cells;
+        hb = false;
+      } else {
+        qpark(qb, t);
+      }
+    }
+  }
+  if ((threadIdx.x & 31) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+// LDS bytes of a spec_ext4_kernel workgroup
+static size_t ext4_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (4 * (size_t)tb_bytes + 2 * kQTaskLds); }
+
+
+// Task order for the pair kernel: the two seeds a wave takes should need the
+// same phases for about as long — a half whose seed has no left side, or a
+// much shorter one, idles while the other runs (EXEC).  A counting sort of
+// the C = 3 / 4 lists of a round by key = (left qlen / 8, right qlen / 8):
+// count (per-block LDS histograms, one global atomic per block and key),
+// scan (one block per list), scatter (per-block LDS ranks, one global atomic
+// per block and key to reserve the block's range).  Claims then take entries
+// 8 apart in the sorted list (the sharded queue), which have about the same
+// key.  The order changes nothing but which seeds share a wave.
+__device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, int2 tk) {
+  const bwagpu_seed_t s = a.prog[tk.x];
+  const int rd = a.chain_read[tk.y];
+  const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
+  const int ql = min(s.qbeg, 255), qr = min(max(lq - s.qbeg - s.len, 0), 255);
+  return (ql >> 3) << 5 | (qr >> 3);
+}
+
+__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
+  __shared__ int hist[kSortKeys];
+  const int list = round * kSpecBins + (int)blockIdx.y;
+  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  for (int k = threadIdx.x; k < kSortKeys; k += 256) hist[k] = 0;
+  __syncthreads();
+  const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) atomicAdd(&hist[pair_key(b, a, tl[i])], 1);
+  __syncthreads();
+  for (int k = threadIdx.x; k < kSortKeys; k += 256)
+    if (hist[k]) atomicAdd(&gh[k], hist[k]);
+}
+
+__global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
+  __shared__ int part[256];
+  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.x) * kSortKeys;
+  const int t = (int)threadIdx.x;  // 4 keys per thread
+  int v[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = gh[4 * t + k];
+    s += v[k];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the per-thread sums
+    const int x = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int base = part[t] - s;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    gh[4 * t + k] = base;  // the key's first position (a cursor from here on)
+    base += v[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round) {
+  __shared__ int cnt[kSortKeys];
+  const int list = round * kSpecBins + (int)blockIdx.y;
+  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  for (int k = threadIdx.x; k < kSortKeys; k += 256) cnt[k] = 0;
+  __syncthreads();
+  const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const size_t off = spec_list_off(list, b.n_chains, b.n_seeds);
+  const int2* tl = a.tasks + off;
+  int2* out = a.stasks + off;
+  const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  constexpr int kPer = 16;  // entries per thread held across the barrier
+  int keys[kPer], rank[kPer];
+  int2 tk[kPer];
+  for (int base = i0; base < i1; base += 256 * kPer) {
+#pragma unroll
+    for (int m = 0; m < kPer; ++m) {
+      const int i = base + m * 256 + (int)threadIdx.x;
+      keys[m] = -1;
+      if (i < i1) {
+        tk[m] = tl[i];
+        keys[m] = pair_key(b, a, tk[m]);
+        rank[m] = atomicAdd(&cnt[keys[m]], 1);
+      }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kSortKeys; k += 256) {
+      const int c = cnt[k];
+      cnt[k] = c ? atomicAdd(&gh[k], c) : 0;  // this pass's range of key k
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kPer; ++m)
+      if (keys[m] >= 0) out[cnt[keys[m]] + rank[m]] = tk[m];
+    __syncthreads();
+    for (int k = threadIdx.x; k < kSortKeys; k += 256) cnt[k] = 0;
+    __syncthreads();
+  }
+}
+
+// The pair kernel's grid: its waves pull tasks from the queue, so the grid
+// only sets its occupancy.  2 workgroups per CU (8 waves per CU, 2 per SIMD)
+// instead of the resident capacity (5 per SIMD): the batch on the other caller
+// stream (the bench's ping-pong) and this batch's selection kernels keep the
+// rest, and an even count per CU beats an uneven one.  Same-box sweep
+// (DESIGN.md §3): capacity 19.87, 60 % 20.74, 50 % 20.66, 2/CU (40 %) 21.74,
+// 30 % 20.16, 1/CU 19.72 Mreads/s.  BWAGPU_EXT2_BLOCKS_PER_CU overrides.
+static int ext2_grid(int nb) {
+  static const int per_cu = [] {
+    const char* e = getenv("BWAGPU_EXT2_BLOCKS_PER_CU");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : v;
+  }();
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    return nb;
+  return std::max(1, std::min(nb, per_cu * ncu));
+}
+
+
+// The sequential logic of mem_chain2aln over one read's chains, by one wave.
+// A seed that is extended but has no result yet:
+//   SEL_EMULATE  becomes a round-B task (its region stays unknown in this pass);
+//   SEL_FINAL    becomes a round-C task and the read goes to the redo list
+//                (its later decisions depend on that region);
+//   SEL_REDO     (the redo list only) is computed inline — the pass that
+//                guarantees every read completes.
+// SEL_FINAL and SEL_REDO write the read's mem_alnreg_v.
+// Two shapes: LIGHT reads (<= kSelLight seeds, so every chain and the region
+// list fit one lane slot) four waves per workgroup, 2 KB of LDS each; HEAVY
+// reads one wave per workgroup with up to 64 KB of LDS region records (beyond
+// that: the region's seed slot in regpos[] and its SeedExt, re-read with
+// workgroup-scope atomics), chains of <= 256 seeds in four VGPR slots (longer:
+// prog[] and skip flags in skipf[]).  The two shapes run concurrently on two
+// streams.
+enum { SEL_EMULATE = 0, SEL_FINAL = 1, SEL_REDO = 2 };
+struct RegRec {  // a region's containment fields (bwamem.c:682-696)
+  int64_t rb, re;
+  int32_t qb, qe, w, seedlen0;
+};
+constexpr int kSelHeavyLds = 64 * 1024;
+constexpr int kSelExtCache = 256;  // a heavy chain's SeedExt records staged in LDS
+__host__ __device__ constexpr int sel_light_wave_lds() { return kSelLight * (int)sizeof(RegRec); }
+__host__ __device__ constexpr int sel_heavy_cap(int mode, int tb) {
+  return (kSelHeavyLds - 4 * (BWAGPU_MAX_READ_LEN + 1) - kSelExtCache * (int)(sizeof(SeedExt) + sizeof(bwagpu_seed_t)) -
+          (mode == SEL_REDO ? 2 * tb : 0)) / (int)sizeof(RegRec);
+}
+
+// max_gap_len (cal_max_gap, bwamem.c:630-637) of every length a containment
+// test can ask for (min(qd, rd) of a region holding the seed: 0..lq-1),
+// tabulated in LDS per workgroup instead of two divisions per lane and region
+constexpr int kMglN = BWAGPU_MAX_READ_LEN + 1;
+
+// near(s, p): the two gap tests of bwamem.c:688-696 for a region p that holds s
+__device__ __forceinline__ bool seed_near(const int32_t* MG, const bwagpu_seed_t& s, const RegRec& p) {
+  const int qd1 = s.qbeg - p.qb;
+  const int64_t rd1 = s.rbeg - p.rb;
+  const int g1 = MG[min(max(qd1 < rd1 ? qd1 : (int)rd1, 0), kMglN - 1)];
+  const int bw1 = g1 < p.w ? g1 : p.w;
+  const int qd2 = p.qe - (s.qbeg + s.len);
+  const int64_t rd2 = p.re - (s.rbeg + s.len);
+  const int g2 = MG[min(max(qd2 < rd2 ? qd2 : (int)rd2, 0), kMglN - 1)];
+  const int bw2 = g2 < p.w ? g2 : p.w;
+  return (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+}
+
+// the 88-byte mem_alnreg_t (rest zero: bwamem.c:718); lane d writes dword d
+__device__ __forceinline__ void write_region(bwagpu_alnreg_t* dst, const SeedExt& e, int rid, int cov, int slen,
+                                             float frac) {
+  const int r = (int)(threadIdx.x & 63);
+  const int dw = r < 21 ? r : 21;
+  uint32_t v = 0;
+  v = dw == 0 ? (uint32_t)e.rb : v;
+  v = dw == 1 ? (uint32_t)((uint64_t)e.rb >> 32) : v;
+  v = dw == 2 ? (uint32_t)e.re : v;
+  v = dw == 3 ? (uint32_t)((uint64_t)e.re >> 32) : v;
+  v = dw == 4 ? (uint32_t)e.qb : v;
+  v = dw == 5 ? (uint32_t)e.qe : v;
+  v = dw == 6 ? (uint32_t)rid : v;
+  v = dw == 7 ? (uint32_t)e.score : v;
+  v = dw == 8 ? (uint32_t)e.truesc : v;
+  v = dw == 13 ? (uint32_t)e.w : v;
+  v = dw == 14 ? (uint32_t)cov : v;
+  v = dw == 17 ? (uint32_t)slen : v;
+  v = dw == 19 ? __float_as_uint(frac) : v;
+  reinterpret_cast<uint32_t*>(dst)[dw] = v;
+}
+
+// a region's containment record into LDS (lanes 0-7 one field each)
+__device__ __forceinline__ void put_regrec(RegRec* dst, const SeedExt& e, int slen) {
+  const int r = (int)(threadIdx.x & 63);
+  const int f = r < 8 ? r : 7;
+  int32_t v = 0;
+  v = f == 0 ? (int32_t)(uint32_t)e.rb : v;
+  v = f == 1 ? (int32_t)((uint64_t)e.rb >> 32) : v;
+  v = f == 2 ? (int32_t)(uint32_t)e.re : v;
+  v = f == 3 ? (int32_t)((uint64_t)e.re >> 32) : v;
+  v = f == 4 ? e.qb : v;
+  v = f == 5 ? e.qe : v;
+  v = f == 6 ? e.w : v;
+  v = f == 7 ? slen : v;
+  if (r < 8) reinterpret_cast<int32_t*>(dst)[f] = v;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// diagnostics (bwagpu_debug_set_trace): per read and selection pass, 8 words
+// at g_trace[(pass * n_reads + rd) * 8]: start / end s_memrealtime (100 MHz),
+// seeds, regions, XCC id, shape (1 light, 2 heavy)
+__device__ __forceinline__ void trace_read(int pass, int n_reads, int rd, uint64_t t0, int ns, int nreg, int shape) {
+  uint32_t* const tr = g_trace;
+  if (!tr) return;
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  const int r = (int)(threadIdx.x & 63);
+  const int d = r < 7 ? r : 7;
+  uint32_t v = (uint32_t)shape;
+  v = d == 0 ? (uint32_t)t0 : v;
+  v = d == 1 ? (uint32_t)(t0 >> 32) : v;
+  v = d == 2 ? (uint32_t)t1 : v;
+  v = d == 3 ? (uint32_t)(t1 >> 32) : v;
+  v = d == 4 ? (uint32_t)ns : v;
+  v = d == 5 ? (uint32_t)nreg : v;
+  v = d == 6 ? __builtin_amdgcn_s_getreg((31 << 11) | 20) : v;
+  if (r < 8) tr[((size_t)pass * n_reads + rd) * 8 + d] = v;
+}
+
+template <int MODE, bool HEAVY>
+__global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int tb_bytes) {
+  static_assert(HEAVY, "one-wave heavy shape only");
+  constexpr bool WRITE = MODE != SEL_EMULATE;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int r = (int)(threadIdx.x & 63);
+  // LDS: max_gap_len table | chain seeds (pad_ = skip flag | 2 * pending) |
+  // their SeedExt records | region records | (redo) target rows
+  int32_t* const MG = reinterpret_cast<int32_t*>(lds);
+  bwagpu_seed_t* const SC = reinterpret_cast<bwagpu_seed_t*>(lds + 4 * kMglN);
+  SeedExt* const EC = reinterpret_cast<SeedExt*>(SC + kSelExtCache);
+  RegRec* const R = reinterpret_cast<RegRec*>(EC + kSelExtCache);
+  const int cap_reg = sel_heavy_cap(MODE, tb_bytes);
+  uint8_t* const tbl = reinterpret_cast<uint8_t*>(R + cap_reg);
+  uint8_t* const tbr = tbl + tb_bytes;
+  for (int x = r; x < kMglN; x += 64) MG[x] = max_gap_len(o, x);
+  Tally tl{0, 0, 0};
+  const int n_list = uni(__hip_atomic_load(&a.ctr[MODE == SEL_REDO ? SPC_REDO_N : SPC_HEAVY_N], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+  const int32_t* const hlist = MODE == SEL_REDO ? a.redo : a.heavy;
+  for (;;) {
+    int t = 0;
+    if (r == 0) t = atomicAdd(&a.ctr[SPC_SEL_CUR + MODE], 1);
+    t = uni(__shfl(t, 0, 64));
+    if (t >= n_list) break;
+    if (MODE != SEL_REDO && uni(a.hinfo[t].y) >= 0) continue;  // the pair-matrix kernels' read
+    const int rd = uni(hlist[t]);
+    const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const ReadDesc d = uniform_desc(a.rdesc[rd]);
+    if (d.lq > BWAGPU_MAX_READ_LEN) continue;  // flagged by spec_reads_kernel
+    const uint8_t* const q = b.seq + d.qoff;
+    const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+    bool redo = false;
+    Tally rt{0, 0, 0};
+    int nreg = 0;
+    for (int c = d.c0; c < d.c0 + d.nch && !redo; ++c) {
+      const int s0 = uni(b.chain_seed_off[c]), ns = uni(b.chain_seed_off[c + 1]) - s0;
+      if (ns == 0) continue;
+      ChainWin cw = a.win[c];
+      cw.lo = uni64(cw.lo);
+      cw.hi = uni64(cw.hi);
+      if (cw.hi < cw.lo) continue;  // flagged by spec_chain_kernel (the reference would assert)
+      const int rid = uni(b.chain_rid[c]);
+      const float frac = __int_as_float(uni(__float_as_int(b.chain_frac_rep[c])));
+      // the chain's seeds (processing order) and their extension results, staged
+      // in LDS (chains of more than kSelExtCache seeds: prog[] / ext[] / skipf[])
+      const bool big = ns > kSelExtCache;
+      for (int i = r; i < min(ns, kSelExtCache); i += 64) {
+        bwagpu_seed_t v = a.prog[s0 + i];
+        v.pad_ = v.pad_ != 0 ? 1 : 0;
+        SC[i] = v;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ext + s0 + i);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(EC + i);
+#pragma unroll
+        for (int w = 0; w < 12; ++w) dst[w] = __hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (big)
+        for (int i = r; i < ns; i += 64)
+          __hip_atomic_store(&a.skipf[s0 + i], a.prog[s0 + i].pad_ != 0 ? 1 : 0, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      mem_fence_group();
+      auto seed_at = [&](int i) -> bwagpu_seed_t { return i < kSelExtCache ? SC[i] : a.prog[s0 + i]; };
+      auto flag_at = [&](int i) -> int {
+        return i < kSelExtCache ? SC[i].pad_
+                                : __hip_atomic_load(&a.skipf[s0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      auto set_flag = [&](int i, int f) {
+        if (r == 0) {
+          if (i < kSelExtCache) SC[i].pad_ |= f;
+          else __hip_atomic_store(&a.skipf[s0 + i], f | 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        mem_fence_group();
+      };
+      for (int k = 0; k < ns; ++k) {
+        const bwagpu_seed_t s = uni_seed(seed_at(k));
+        // containment in a region so far (bwamem.c:678-697), one region per lane
+        bool hit = false;
+        for (int base = 0; base < nreg && !hit; base += 64) {
+          const int i = min(base + r, nreg - 1);
+          RegRec p;
+          if (i < cap_reg) {
+            p = R[i];
+          } else {
+            const int pp = __hip_atomic_load(&a.regpos[d.s0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const SeedExt* pe = a.ext + pp;
+            p.rb = __hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.re = __hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.qb = __hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.qe = __hip_atomic_load(&pe->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.w = __hip_atomic_load(&pe->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            p.seedlen0 = a.prog[pp].len;
+          }
+          const bool inside = base + r < nreg &&
+                              !(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) &&
+                              !(s.len - p.seedlen0 >= rep_lim);
+          if (__builtin_amdgcn_ballot_w64(inside) == 0) continue;
+          hit = __builtin_amdgcn_ballot_w64(inside && seed_near(MG, s, p)) != 0;
+        }
+        if (hit) {
+          // a long overlapping seed of this chain already visited (bwamem.c:698-707)
+          const int len95 = uni((int)ceil(s.len * .95));  // t->len < s->len * .95 <=> t->len < ceil(...)
+          bool ov = false;
+          for (int base = 0; base < k && !ov; base += 64) {
+            const int i = min(base + r, k - 1);
+            const bwagpu_seed_t t = seed_at(i);
+            const bool tsk = (flag_at(i) & 1) != 0;
+            const bool a1 = s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 && (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg;
+            const bool b1 = t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 && (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg;
+            ov = __builtin_amdgcn_ballot_w64(base + r < k && !tsk && t.len >= len95 && (a1 || b1)) != 0;
+          }
+          if (!ov) {  // skipped: srt[k] = 0 (bwamem.c:709)
+            set_flag(k, 1);
+            continue;
+          }
+        }
+        // ---- this seed is extended (bwamem.c:717-792)
+        const int pos = s0 + k;
+        const SeedExt* const pe = k < kSelExtCache ? EC + k : a.ext + pos;
+        SeedExt e;
+        e.calls = uni(__hip_atomic_load(&pe->calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (e.calls == 0) {  // no result yet
+          if constexpr (MODE == SEL_REDO) {
+            e = extend_seed<16>(o, ref, s, d.lq, q, cw, tbl, tbr);
+            store_ext(a.ext + pos, e);
+            mem_fence_group();
+            if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+          } else if constexpr (MODE == SEL_EMULATE) {
+            set_flag(k, 2);  // pending: collected per chain below
+            continue;        // its region stays unknown in this pass
+          } else {
+            const int list = 2 * kSpecBins + spec_bin(d.lq);
+            if (r == 0) {
+              const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+              a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(pos, c);
+              a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+            }
+            redo = true;  // the rest of this read waits for the redo pass
+            break;
+          }
+        } else {
+          e.rb = uni64(__hip_atomic_load(&pe->rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.re = uni64(__hip_atomic_load(&pe->re, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.qb = uni(__hip_atomic_load(&pe->qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.qe = uni(__hip_atomic_load(&pe->qe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.score = uni(__hip_atomic_load(&pe->score, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.truesc = uni(__hip_atomic_load(&pe->truesc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.w = uni(__hip_atomic_load(&pe->w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.cells = uni(__hip_atomic_load(&pe->cells, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          e.rows = uni(__hip_atomic_load(&pe->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        }
+        if constexpr (WRITE) {
+          // seedcov over the chain's seeds (bwamem.c:784-788)
+          long long cov = 0;
+          for (int base = 0; base < ns; base += 64) {
+            const int i = base + r;
+            const bwagpu_seed_t t = seed_at(min(i, ns - 1));
+            const bool in = i < ns && t.qbeg >= e.qb && t.qbeg + t.len <= e.qe && t.rbeg >= e.rb && t.rbeg + t.len <= e.re;
+            cov += in ? t.len : 0;
+          }
+          cov = grp_sum64(cov, 64);
+          write_region(a.out + d.s0 + nreg, e, rid, (int)cov, s.len, frac);
+          rt.cells += e.cells;
+          rt.rows += e.rows;
+          rt.calls += e.calls - 1;
+        }
+        if (nreg < cap_reg) {
+          put_regrec(R + nreg, e, s.len);
+        } else {
+          if (r == 0) __hip_atomic_store(&a.regpos[d.s0 + nreg], pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          mem_fence_group();
+        }
+        ++nreg;
+      }
+      if constexpr (MODE == SEL_EMULATE) {  // this chain's round-B tasks
+        const int list = kSpecBins + spec_bin(d.lq);
+        for (int base = 0; base < ns; base += 64) {
+          const int i = base + r;
+          const bool pnd = i < ns && (flag_at(min(i, ns - 1)) & 2) != 0;
+          const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
+          if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(s0 + i, c);
+        }
+      }
+    }
+    if (MODE != SEL_REDO) trace_read(MODE, b.n_reads, rd, t_start, d.ns, nreg, 2);
+    if constexpr (WRITE) {
+      if (!redo) {
+        a.out_n[rd] = nreg;
+        tl.cells += rt.cells;
+        tl.rows += rt.rows;
+        tl.calls += rt.calls;
+      }
+    }
+  }
+  if constexpr (WRITE) {
+    if (r != 0) tl = Tally{0, 0, 0};
+    block_stats<64>(tl, a.stats);
+  }
+}
+
+// LIGHT reads (<= kSelLight seeds and chains): the whole read in registers,
+// lane i = seed i of the read in processing order (chain-major, as prog[]
+// stores them) with its SeedExt; lane c = chain c.  mem_chain2aln's
+// sequential decisions depend on each other only through two bit sets — the
+// seeds extended so far (their regions) and the seeds skipped so far — so:
+//   1. pairs: for every seed k, the 64-bit masks of earlier seeds j whose
+//      region would hold it (bwamem.c:678-697: C) and of earlier seeds of its
+//      chain that overlap it (698-707, before the skip filter: O), and its
+//      seedcov if extended (784-788) — lane-parallel, no loop-carried state;
+//   2. scan: the sequential logic on scalar masks only:
+//        hit = C[k] & extended;  skipped = hit && !(O[k] & ~skipped);
+//   3. output: every extended seed's record lane-parallel at its rank.
+// A seed that must be extended but has no result: SEL_EMULATE marks it a
+// round-B task (pending: neither extended nor skipped, as in the per-seed
+// form); SEL_FINAL sends the read to the redo pass.
+// A misprediction in the final pass of a light read (a seed the replay must
+// extend has no result: ~10-20 per C2 batch) is extended inline, which takes
+// the kernel to 129 VGPRs (3 waves per SIMD).  Sending it to round C + the
+// redo pass like one of a longer read instead (82 VGPRs) is bit-exact, but
+// measured 19.8-19.9 vs 21.6-21.7 Mreads/s on C2.
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
+                                                            int tb_bytes) {
+  constexpr bool WRITE = MODE != SEL_EMULATE;
+  __shared__ int32_t MG[kMglN];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lrows[];  // per wave: target rows of an inline extension
+  uint8_t* const tbl = lrows + (threadIdx.x >> 6) * 2 * tb_bytes;
+  uint8_t* const tbr = tbl + tb_bytes;
+  for (int x = threadIdx.x; x < kMglN; x += kBlock) MG[x] = max_gap_len(o, x);
+  __syncthreads();
+  const int r = (int)(threadIdx.x & 63);
+  const uint64_t lt_mask = r ? (~0ull >> (64 - r)) : 0ull;  // lanes below r
+  Tally tl{0, 0, 0};
+  // static deal: wave w takes reads w, w + NW, ... (light reads cost about the
+  // same; no queue atomics), the next read's descriptor in flight meanwhile
+  const int NW = (int)gridDim.x * (kBlock / 64);
+  int rd = (int)blockIdx.x * (kBlock / 64) + uni((int)(threadIdx.x >> 6));
+  ReadDesc dn{};
+  if (rd < b.n_reads) dn = a.rdesc[rd];
+  for (; rd < b.n_reads; rd += NW) {
+    const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const ReadDesc d = uniform_desc(dn);
+    if (rd + NW < b.n_reads) dn = a.rdesc[rd + NW];
+    if (d.ns > kSelLight || d.nch > kSelLight) continue;  // the heavy kernel's read
+    if (d.lq > BWAGPU_MAX_READ_LEN) continue;             // flagged by spec_reads_kernel
+    if (d.ns == 0) {
+      if (WRITE) a.out_n[rd] = 0;
+      continue;
+    }
+    // a miss of the final pass is computed inline and the read starts over
+    // with it (a region changes only later decisions; light reads are cheap)
+    for (;;) {
+    // everything of the read, one round trip
+    const int ci = min(r, max(d.nch - 1, 0)), si = min(r, d.ns - 1);
+    const int cs_l = b.chain_seed_off[d.c0 + ci] - d.s0, ce_l = b.chain_seed_off[d.c0 + ci + 1] - d.s0;
+    const ChainWin cw_l = a.win[d.c0 + ci];
+    const int rid_l = b.chain_rid[d.c0 + ci];
+    const float fr_l = b.chain_frac_rep[d.c0 + ci];
+    const bwagpu_seed_t sd = a.prog[d.s0 + si];
+    const SeedExt x = a.ext[d.s0 + si];  // earlier launches, or this wave's inline extension
+    // this seed's chain (a chain with a flagged window is never processed)
+    int cid = 0, rid = 0;
+    float frac = 0.f;
+    bool vchain = false;
+    for (int c = 0; c < d.nch; ++c) {
+      const int cs = __builtin_amdgcn_readlane(cs_l, c), ce = __builtin_amdgcn_readlane(ce_l, c);
+      const bool in = r >= cs && r < ce;
+      const bool ok = readlane64(cw_l.hi, c) >= readlane64(cw_l.lo, c);
+      cid = in ? c : cid;
+      vchain = in ? ok : vchain;
+      rid = in ? __builtin_amdgcn_readlane(rid_l, c) : rid;
+      frac = in ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fr_l), c)) : frac;
+    }
+    const bool present = r < d.ns && vchain;
+    const bool computed = present && x.calls != 0;
+    const uint64_t present_m = __builtin_amdgcn_ballot_w64(present);
+    const uint64_t computed_m = __builtin_amdgcn_ballot_w64(computed);
+    const uint64_t pad_m = __builtin_amdgcn_ballot_w64(r < d.ns && sd.pad_ != 0);
+    const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+    // ---- 1. pair masks: lane p = (k, j) = (p / S, p % S) with S the seed count
+    // rounded up to a power of two (8..64), 64 / S values of k per pass; pass
+    // `it`'s ballots land in lane it (c_*, o_*); seedcov of k's region in lane k
+    const int S = d.ns <= 8 ? 8 : d.ns <= 16 ? 16 : d.ns <= 32 ? 32 : 64;
+    const int lgS = S == 8 ? 3 : S == 16 ? 4 : S == 32 ? 5 : 6;
+    const int npass = (S * S) >> 6;
+    uint32_t c_lo = 0, c_hi = 0, o_lo = 0, o_hi = 0;
+    int cov = 0;
+    const int j = r & (S - 1);
+    const int jl = min(j, d.ns - 1) << 2;
+    // seed j of this lane (and its region), gathered once
+    const int64_t j_rbeg = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)(sd.rbeg >> 32)) << 32 |
+                                     (uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)sd.rbeg));
+    const int j_qbeg = __builtin_amdgcn_ds_bpermute(jl, sd.qbeg), j_len = __builtin_amdgcn_ds_bpermute(jl, sd.len);
+    const int j_cid = __builtin_amdgcn_ds_bpermute(jl, cid);
+    const bool j_pad = __builtin_amdgcn_ds_bpermute(jl, sd.pad_) != 0;
+    const bool j_done = __builtin_amdgcn_ds_bpermute(jl, computed ? 1 : 0) != 0;
+    RegRec pj;
+    pj.rb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)(x.rb >> 32)) << 32 |
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)x.rb));
+    pj.re = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)(x.re >> 32)) << 32 |
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(jl, (int)x.re));
+    pj.qb = __builtin_amdgcn_ds_bpermute(jl, x.qb);
+    pj.qe = __builtin_amdgcn_ds_bpermute(jl, x.qe);
+    pj.w = __builtin_amdgcn_ds_bpermute(jl, x.w);
+    pj.seedlen0 = j_len;
+    for (int it = 0; it < npass; ++it) {
+      const int k = (it << (6 - lgS)) + (r >> lgS);
+      const int kl = min(k, d.ns - 1) << 2;
+      bwagpu_seed_t sk;
+      sk.rbeg = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)(sd.rbeg >> 32)) << 32 |
+                          (uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)sd.rbeg));
+      sk.qbeg = __builtin_amdgcn_ds_bpermute(kl, sd.qbeg);
+      sk.len = __builtin_amdgcn_ds_bpermute(kl, sd.len);
+      const int k_cid = __builtin_amdgcn_ds_bpermute(kl, cid);
+      const bool valid = k < d.ns && j < d.ns;
+      // C: the region of seed j holds seed k (bwamem.c:682-696)
+      const bool inside = valid && j < k && j_done &&
+                          !(sk.rbeg < pj.rb || sk.rbeg + sk.len > pj.re || sk.qbeg < pj.qb || sk.qbeg + sk.len > pj.qe) &&
+                          !(sk.len - j_len >= rep_lim);
+      uint64_t cm = __builtin_amdgcn_ballot_w64(inside);
+      if (cm) cm = __builtin_amdgcn_ballot_w64(inside && seed_near(MG, sk, pj));
+      // O: seed j of k's chain overlaps it (bwamem.c:701-704; t->len < s->len * .95 <=> t->len < ceil(...))
+      const int len95 = (int)ceil(sk.len * .95);
+      const bool a1 = sk.qbeg <= j_qbeg && sk.qbeg + sk.len - j_qbeg >= sk.len >> 2 &&
+                      (int64_t)(j_qbeg - sk.qbeg) != j_rbeg - sk.rbeg;
+      const bool b1 = j_qbeg <= sk.qbeg && j_qbeg + j_len - sk.qbeg >= sk.len >> 2 &&
+                      (int64_t)(sk.qbeg - j_qbeg) != sk.rbeg - j_rbeg;
+      const uint64_t om = __builtin_amdgcn_ballot_w64(valid && j < k && j_cid == k_cid && !j_pad && j_len >= len95 && (a1 || b1));
+      c_lo = r == it ? (uint32_t)cm : c_lo;
+      c_hi = r == it ? (uint32_t)(cm >> 32) : c_hi;
+      o_lo = r == it ? (uint32_t)om : o_lo;
+      o_hi = r == it ? (uint32_t)(om >> 32) : o_hi;
+      if (WRITE) {  // seedcov of k's region over its chain's seeds (bwamem.c:784-788)
+        const int64_t krb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)(x.rb >> 32)) << 32 |
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)x.rb));
+        const int64_t kre = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)(x.re >> 32)) << 32 |
+                                      (uint32_t)__builtin_amdgcn_ds_bpermute(kl, (int)x.re));
+        const int kqb = __builtin_amdgcn_ds_bpermute(kl, x.qb), kqe = __builtin_amdgcn_ds_bpermute(kl, x.qe);
+        int v = valid && j_cid == k_cid && j_qbeg >= kqb && j_qbeg + j_len <= kqe && j_rbeg >= krb &&
+                        j_rbeg + j_len <= kre ? j_len : 0;
+        for (int m = 1; m < S; m <<= 1) v += __shfl_xor(v, m, 64);
+        // lane k takes the sum of its group (lane (k - first k of the pass) * S)
+        const int src = (r - (it << (6 - lgS))) << lgS;
+        const int got = __builtin_amdgcn_ds_bpermute(min(max(src, 0), 63) << 2, v);
+        cov = (r >= (it << (6 - lgS)) && r < ((it + 1) << (6 - lgS))) ? got : cov;
+      }
+    }
+    // ---- 2. the sequential decisions, on scalar masks
+    uint64_t ext = 0, skip = pad_m, pend = 0;
+    int miss = -1;
+    for (int k = 0; k < d.ns; ++k) {
+      const uint64_t bit = 1ull << k;
+      if (!(present_m & bit)) continue;
+      const int it = (k << lgS) >> 6, sh = (k << lgS) & 63;
+      const uint64_t fld = S == 64 ? ~0ull : ((1ull << S) - 1);
+      const uint64_t cm = ((uint64_t)__builtin_amdgcn_readlane(c_hi, it) << 32 | (uint32_t)__builtin_amdgcn_readlane(c_lo, it)) >> sh & fld;
+      if (cm & ext) {
+        const uint64_t om = ((uint64_t)__builtin_amdgcn_readlane(o_hi, it) << 32 | (uint32_t)__builtin_amdgcn_readlane(o_lo, it)) >> sh & fld;
+        if (!(om & ~skip)) {  // skipped: srt[k] = 0 (bwamem.c:709)
+          skip |= bit;
+          continue;
+        }
+      }
+      if (!(computed_m & bit)) {
+        if (MODE == SEL_EMULATE) {
+          pend |= bit;  // a round-B task; its region stays unknown in this pass
+          continue;
+        }
+        miss = k;
+        break;
+      }
+      ext |= bit;
+    }
+    // ---- 3. outputs
+    if constexpr (MODE == SEL_EMULATE) {
+      const int list = kSpecBins + spec_bin(d.lq);
+      const bool pnd = (pend >> r) & 1;
+      const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
+      if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
+    } else {
+      if (miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
+        const bwagpu_seed_t sm = uni_seed(a.prog[d.s0 + miss]);
+        const int cm_id = uni(__shfl(cid, miss, 64));
+        ChainWin cw = a.win[d.c0 + cm_id];
+        cw.lo = uni64(cw.lo);
+        cw.hi = uni64(cw.hi);
+        const SeedExt e = extend_seed<3>(o, ref, sm, d.lq, b.seq + d.qoff, cw, tbl, tbr);
+        store_ext(a.ext + d.s0 + miss, e);
+        if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+        mem_fence_group();
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
+      if (miss >= 0) {  // round C + the redo pass (reads > 160 bp)
+        const int list = 2 * kSpecBins + spec_bin(d.lq);
+        if (r == miss) {
+          const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+          a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
+          a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+        }
+        break;  // the redo pass writes this read
+      }
+      const bool mine = (ext >> r) & 1;
+      if (mine) {  // the region of seed r, at its rank (bwamem.c:718-792 field by field; rest zero)
+        const int slot = (int)__popcll(ext & lt_mask);
+        uint2* dst = reinterpret_cast<uint2*>(a.out + d.s0 + slot);
+        dst[0] = make_uint2((uint32_t)x.rb, (uint32_t)((uint64_t)x.rb >> 32));
+        dst[1] = make_uint2((uint32_t)x.re, (uint32_t)((uint64_t)x.re >> 32));
+        dst[2] = make_uint2((uint32_t)x.qb, (uint32_t)x.qe);
+        dst[3] = make_uint2((uint32_t)rid, (uint32_t)x.score);
+        dst[4] = make_uint2((uint32_t)x.truesc, 0u);
+        dst[5] = make_uint2(0u, 0u);
+        dst[6] = make_uint2(0u, (uint32_t)x.w);
+        dst[7] = make_uint2((uint32_t)cov, 0u);
+        dst[8] = make_uint2(0u, (uint32_t)sd.len);
+        dst[9] = make_uint2(0u, __float_as_uint(frac));
+        dst[10] = make_uint2(0u, 0u);
+        tl.cells += x.cells;
+        tl.rows += x.rows;
+        tl.calls += x.calls - 1;
+      }
+      if (r == 0) a.out_n[rd] = (int)__popcll(ext);
+    }
+    trace_read(MODE, b.n_reads, rd, t_start, d.ns, (int)__popcll(ext), 1);
+    break;
+    }  // the read's attempts
+  }
+  if constexpr (WRITE) block_stats<64>(tl, a.stats);
+}
+
+// HEAVY reads with pair matrices (<= kSelMatMaxSeeds seeds).  The same
+// decomposition as the light kernel, at a size where one wave cannot hold the
+// read:
+//   spec_pairs_kernel — one wave per column k (a seed) of a heavy read, over
+//     every column of every such read at once: 64-bit words of C[k] (earlier
+//     seeds whose region would hold k: bwamem.c:678-697) and O[k] (earlier
+//     seeds of k's chain overlapping it: 698-707), and k's seedcov (784-788);
+//   spec_scan_kernel  — one wave per read: the sequential decisions on bit
+//     sets (lane w holds word w of the extended / skipped / pending sets), then
+//     every extended seed's record lane-parallel at its rank.
+__global__ void __launch_bounds__(kBlock) spec_pairs_kernel(DevOpt o, DevBatch b, SpecArgs a, int with_cov) {
+  __shared__ int32_t MG[kMglN];
+  for (int x = threadIdx.x; x < kMglN; x += kBlock) MG[x] = max_gap_len(o, x);
+  __syncthreads();
+  const int r = (int)(threadIdx.x & 63);
+  const int ncol = uni(__hip_atomic_load(&a.ctr[SPC_HCOLS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int nwv = (int)gridDim.x * (kBlock / 64);
+  for (int x = (int)blockIdx.x * (kBlock / 64) + uni((int)(threadIdx.x >> 6)); x < ncol; x += nwv) {
+    const int t = uni(a.colent[x]);
+    const int4 hi = a.hinfo[t];
+    const int rd = uni(hi.x), woff = uni(hi.y), col = uni(hi.z), ns = uni(hi.w);
+    const int k = x - col, nw = (ns + 63) >> 6;
+    const ReadDesc d = uniform_desc(a.rdesc[rd]);
+    const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+    const bwagpu_seed_t s = uni_seed(a.prog[d.s0 + k]);
+    const int ck = uni(a.seedchain[d.s0 + k]);
+    const int len95 = uni((int)ceil(s.len * .95));  // t->len < s->len * .95 <=> t->len < ceil(...)
+    const SeedExt ek = a.ext[d.s0 + k];
+    const bool k_done = uni(ek.calls) != 0;
+    const int64_t krb = uni64(ek.rb), kre = uni64(ek.re);
+    const int kqb = uni(ek.qb), kqe = uni(ek.qe);
+    int cov = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int j = 64 * w + r, jj = min(j, ns - 1);
+      const bwagpu_seed_t sj = a.prog[d.s0 + jj];
+      const int cj = a.seedchain[d.s0 + jj];
+      const SeedExt ej = a.ext[d.s0 + jj];
+      RegRec p;
+      p.rb = ej.rb;
+      p.re = ej.re;
+      p.qb = ej.qb;
+      p.qe = ej.qe;
+      p.w = ej.w;
+      p.seedlen0 = sj.len;
+      const bool inside = j < k && ej.calls != 0 &&
+                          !(s.rbeg < p.rb || s.rbeg + s.len > p.re || s.qbeg < p.qb || s.qbeg + s.len > p.qe) &&
+                          !(s.len - sj.len >= rep_lim);
+      uint64_t cm = __builtin_amdgcn_ballot_w64(inside);
+      if (cm) cm = __builtin_amdgcn_ballot_w64(inside && seed_near(MG, s, p));
+      const bool a1 = s.qbeg <= sj.qbeg && s.qbeg + s.len - sj.qbeg >= s.len >> 2 &&
+                      (int64_t)(sj.qbeg - s.qbeg) != sj.rbeg - s.rbeg;
+      const bool b1 = sj.qbeg <= s.qbeg && sj.qbeg + sj.len - s.qbeg >= s.len >> 2 &&
+                      (int64_t)(s.qbeg - sj.qbeg) != s.rbeg - sj.rbeg;
+      const uint64_t om = __builtin_amdgcn_ballot_w64(j < k && cj == ck && sj.pad_ == 0 && sj.len >= len95 && (a1 || b1));
+      if (r == 0 && 64 * w < k) {
+        a.mat[woff + tri_off(k) + w] = cm;
+        a.mat[woff + tri_off(ns) + tri_off(k) + w] = om;
+      }
+      if (with_cov && k_done)
+        cov += (j < ns && cj == ck && sj.qbeg >= kqb && sj.qbeg + sj.len <= kqe && sj.rbeg >= krb &&
+                sj.rbeg + sj.len <= kre) ? sj.len : 0;
+    }
+    if (with_cov) {
+      cov = (int)grp_sum64(cov, 64);
+      if (r == 0) a.cov[d.s0 + k] = cov;
+    }
+  }
+}
+
+constexpr int kScanLds = 64 * 1024;  // a read's C and O matrices staged in LDS when they fit
+
+// The final pass over a heavy read computes a missing extension INLINE (the
+// read's wave runs extend_seed, then sets the new region's containment bits in
+// column k of C for every later seed, and k's seedcov) and carries on: a
+// region only changes the decisions of the seeds after it, so the scan state
+// up to k stays valid.  (Deferring such a read to round C + the serial redo
+// pass cost 2.4-2.6 ms on one read of 1,167 seeds and 749 regions.)
+__device__ __forceinline__ void heavy_fill_missing(const DevOpt& o, const DevRef& ref, const DevBatch& b,
+                                                   const SpecArgs& a, const ReadDesc& d, int k, int ns,
+                                                   uint64_t* C, uint8_t* tbl, uint8_t* tbr) {
+  const int r = (int)(threadIdx.x & 63);
+  const bwagpu_seed_t sk = uni_seed(a.prog[d.s0 + k]);
+  const int ck = uni(a.seedchain[d.s0 + k]);
+  ChainWin cw = a.win[ck];
+  cw.lo = uni64(cw.lo);
+  cw.hi = uni64(cw.hi);
+  const SeedExt e = extend_seed<3>(o, ref, sk, d.lq, b.seq + d.qoff, cw, tbl, tbr);  // reads <= 192 bp
+  store_ext(a.ext + d.s0 + k, e);
+  if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+  // region k as the containment tests see it (bwamem.c:682-696)
+  RegRec p;
+  p.rb = e.rb;
+  p.re = e.re;
+  p.qb = e.qb;
+  p.qe = e.qe;
+  p.w = e.w;
+  p.seedlen0 = sk.len;
+  const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
+  int cov = 0;
+  for (int base = 0; base < ns; base += 64) {
+    const int j = base + r, jj = min(j, ns - 1);
+    const bwagpu_seed_t sj = a.prog[d.s0 + jj];
+    // column k of C for the later seeds j > k (the pairs kernel's predicate)
+    bool in = j > k && j < ns && !(sj.rbeg < p.rb || sj.rbeg + sj.len > p.re || sj.qbeg < p.qb || sj.qbeg + sj.len > p.qe) &&
+              !(sj.len - sk.len >= rep_lim);
+    if (in) {
+      const int qd1 = sj.qbeg - p.qb;
+      const int64_t rd1 = sj.rbeg - p.rb;
+      const int g1 = max_gap_len(o, max(qd1 < rd1 ? qd1 : (int)rd1, 0));
+      const int bw1 = g1 < p.w ? g1 : p.w;
+      const int qd2 = p.qe - (sj.qbeg + sj.len);
+      const int64_t rd2 = p.re - (sj.rbeg + sj.len);
+      const int g2 = max_gap_len(o, max(qd2 < rd2 ? qd2 : (int)rd2, 0));
+      const int bw2 = g2 < p.w ? g2 : p.w;
+      in = (qd1 - rd1 < bw1 && rd1 - qd1 < bw1) || (qd2 - rd2 < bw2 && rd2 - qd2 < bw2);
+    }
+    if (in) C[tri_off(j) + (k >> 6)] |= 1ull << (k & 63);  // word k>>6 of row j: this lane's alone
+    // seedcov of k (bwamem.c:784-788): its chain's seeds inside region k
+    const int cj = a.seedchain[d.s0 + jj];
+    cov += (j < ns && cj == ck && sj.qbeg >= p.qb && sj.qbeg + sj.len <= p.qe && sj.rbeg >= p.rb &&
+            sj.rbeg + sj.len <= p.re) ? sj.len : 0;
+  }
+  cov = (int)grp_sum64(cov, 64);
+  if (r == 0) a.cov[d.s0 + k] = cov;
+  // the wave re-reads C (LDS or its own global writes) and ext/cov next
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int tb_bytes) {
+  constexpr bool WRITE = MODE != SEL_EMULATE;
+  extern __shared__ __attribute__((aligned(16))) uint64_t M[];
+  uint8_t* const tbl = reinterpret_cast<uint8_t*>(M) + kScanLds;
+  uint8_t* const tbr = tbl + tb_bytes;
+  const int r = (int)(threadIdx.x & 63);
+  const uint64_t lt_mask = r ? (~0ull >> (64 - r)) : 0ull;
+  const int nh = uni(__hip_atomic_load(&a.ctr[SPC_HEAVY_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  Tally tl{0, 0, 0};
+  for (int t = (int)blockIdx.x; t < nh; t += (int)gridDim.x) {
+    const int4 hi = a.hinfo[t];
+    const int rd = uni(hi.x), woff = uni(hi.y), ns = uni(hi.w);
+    if (woff < 0) continue;  // no matrix: the per-seed heavy kernel's read
+    const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const int nw = (ns + 63) >> 6;
+    const ReadDesc d = uniform_desc(a.rdesc[rd]);
+    if (d.lq > BWAGPU_MAX_READ_LEN) continue;
+    const int64_t tw = tri_off(ns);
+    const uint64_t* Cg = a.mat + woff;
+    const bool staged = 2 * tw * 8 <= kScanLds;
+    if (staged) {
+      for (int i = r; i < 2 * tw; i += 64) M[i] = Cg[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    uint64_t* C = staged ? M : a.mat + woff;
+    const uint64_t* O = C + tw;
+    // per-word sets: lane w holds word w
+    uint64_t present_w = 0, computed_w = 0, skip_w = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int j = 64 * w + r, jj = min(j, ns - 1);
+      const bwagpu_seed_t sj = a.prog[d.s0 + jj];
+      const ChainWin cw = a.win[a.seedchain[d.s0 + jj]];
+      const bool pres = j < ns && cw.hi >= cw.lo;  // seeds of a flagged chain are never processed
+      const uint64_t pm = __builtin_amdgcn_ballot_w64(pres);
+      const uint64_t cm = __builtin_amdgcn_ballot_w64(pres && a.ext[d.s0 + jj].calls != 0);
+      const uint64_t km = __builtin_amdgcn_ballot_w64(j < ns && sj.pad_ != 0);
+      present_w = r == w ? pm : present_w;
+      computed_w = r == w ? cm : computed_w;
+      skip_w = r == w ? km : skip_w;
+    }
+    uint64_t ext_w = 0, pend_w = 0;
+    int miss = -1;
+    for (int k = 0; k < ns; ++k) {
+      const int kw = k >> 6;
+      const uint64_t kbit = 1ull << (k & 63);
+      const uint64_t pres = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(present_w >> 32), kw) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)present_w, kw);
+      if (!(pres & kbit)) continue;
+      const int nwk = (k + 63) >> 6;  // words of row k
+      const uint64_t cw = r < nwk ? C[tri_off(k) + r] : 0;
+      if (__builtin_amdgcn_ballot_w64((cw & ext_w) != 0)) {
+        const uint64_t ow = r < nwk ? O[tri_off(k) + r] : 0;
+        if (!__builtin_amdgcn_ballot_w64((ow & ~skip_w) != 0)) {  // skipped: srt[k] = 0 (bwamem.c:709)
+          skip_w |= r == kw ? kbit : 0;
+          continue;
+        }
+      }
+      const uint64_t comp = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(computed_w >> 32), kw) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)computed_w, kw);
+      if (!(comp & kbit)) {
+        if (MODE == SEL_EMULATE) {
+          pend_w |= r == kw ? kbit : 0;  // a round-B task; its region stays unknown
+          continue;
+        }
+        if (d.lq > kSpecBinLen[0]) {  // longer reads: round C + the redo pass
+          miss = k;
+          break;
+        }
+        heavy_fill_missing(o, ref, b, a, d, k, ns, C, tbl, tbr);
+        computed_w |= r == kw ? kbit : 0;
+      }
+      ext_w |= r == kw ? kbit : 0;
+    }
+    int nreg = 0;
+    if constexpr (MODE == SEL_EMULATE) {
+      const int list = kSpecBins + spec_bin(d.lq);
+      for (int w = 0; w < nw; ++w) {
+        const uint64_t pw = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(pend_w >> 32), w) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)pend_w, w);
+        const int j = 64 * w + r;
+        const bool pnd = (pw >> r) & 1;
+        const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
+        if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + j, a.seedchain[d.s0 + j]);
+      }
+    } else {
+      if (miss >= 0) {
+        if (r == 0) {
+          const int list = 2 * kSpecBins + spec_bin(d.lq);
+          const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
+          a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + miss, a.seedchain[d.s0 + miss]);
+          a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
+        }
+        continue;  // the redo pass writes this read
+      }
+      for (int w = 0; w < nw; ++w) {
+        const uint64_t ew = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(ext_w >> 32), w) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)ext_w, w);
+        const int j = 64 * w + r;
+        if ((ew >> r) & 1) {  // the region of seed j at its rank (bwamem.c:718-792; rest zero)
+          const int slot = nreg + (int)__popcll(ew & lt_mask);
+          const SeedExt x = a.ext[d.s0 + j];
+          const int c = a.seedchain[d.s0 + j];
+          uint2* dst = reinterpret_cast<uint2*>(a.out + d.s0 + slot);
+          dst[0] = make_uint2((uint32_t)x.rb, (uint32_t)((uint64_t)x.rb >> 32));
+          dst[1] = make_uint2((uint32_t)x.re, (uint32_t)((uint64_t)x.re >> 32));
+          dst[2] = make_uint2((uint32_t)x.qb, (uint32_t)x.qe);
+          dst[3] = make_uint2((uint32_t)b.chain_rid[c], (uint32_t)x.score);
+          dst[4] = make_uint2((uint32_t)x.truesc, 0u);
+          dst[5] = make_uint2(0u, 0u);
+          dst[6] = make_uint2(0u, (uint32_t)x.w);
+          dst[7] = make_uint2((uint32_t)a.cov[d.s0 + j], 0u);
+          dst[8] = make_uint2(0u, (uint32_t)a.prog[d.s0 + j].len);
+          dst[9] = make_uint2(0u, __float_as_uint(b.chain_frac_rep[c]));
+          dst[10] = make_uint2(0u, 0u);
+          tl.cells += x.cells;
+          tl.rows += x.rows;
+          tl.calls += x.calls - 1;
+        }
+        nreg += (int)__popcll(ew);
+      }
+      if (r == 0) a.out_n[rd] = nreg;
+    }
+    trace_read(MODE, b.n_reads, rd, t_start, ns, nreg, 3);
+  }
+  if constexpr (WRITE) block_stats<64>(tl, a.stats);
+}
+
+// spec_scan_kernel's grid: one wave per workgroup, a static stride over the
+// heavy reads (256-2048 measured within the noise)
+constexpr int kScanGrid = 1024;
+
+// The two selection shapes of one pass: heavy reads on `side` (when given)
+// concurrently with the light reads on `st`; `st` continues once both are done.
+template <int MODE>
+static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int tb_bytes,
+                          hipStream_t st, const SpecStreams& ss) {
+  hipStream_t hs = st;
+  if (MODE != SEL_REDO && ss.side) {
+    (void)hipEventRecord(ss.fork, st);
+    (void)hipStreamWaitEvent(ss.side, ss.fork, 0);
+    hs = ss.side;
+  }
+  if (MODE != SEL_REDO) {
+    const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
+    const int nb = resident_blocks(spec_select_light<MODE>, lds);
+    hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
+  }
+  if (MODE != SEL_REDO) {  // heavy reads with pair matrices: all pairs at once, then one scan per read
+    const int nb = resident_blocks(spec_pairs_kernel, 0);
+    hipLaunchKernelGGL(spec_pairs_kernel, dim3(nb), dim3(kBlock), 0, hs, o, b, a, MODE == SEL_FINAL ? 1 : 0);
+    hipLaunchKernelGGL((spec_scan_kernel<MODE>), dim3(kScanGrid), dim3(64), (size_t)kScanLds + 2 * (size_t)tb_bytes, hs, o,
+                       ref, b, a, tb_bytes);
+  }
+  // the rest (no matrix; the redo list): one wave per read, per seed
+  hipLaunchKernelGGL((spec_select_kernel<MODE, true>), dim3(MODE == SEL_REDO ? 256 : 1024), dim3(64),
+                     (size_t)kSelHeavyLds, hs, o, ref, b, a, tb_bytes);
+  if (hs != st) {
+    (void)hipEventRecord(ss.join, hs);
+    (void)hipStreamWaitEvent(st, ss.join, 0);
+  }
+}
+
+// The first two length bins' extension kernel: four seeds per wave
+// (spec_ext4_kernel, packed 16-bit DP) when every score of the bin fits the
+// packed ranges, else two per wave (spec_ext2_kernel, 32-bit).
+// bwagpu_debug_ext_form(1) forces two per wave (tests, A/B).
+static std::atomic<int> g_ext_form{0};
+int ext_form() { return g_ext_form.load(std::memory_order_relaxed); }
+int set_ext_form(int form) {  // process-wide; -> the previous form (form < 0: query only)
+  const int prev = g_ext_form.load(std::memory_order_relaxed);
+  if (form >= 0) g_ext_form.store(form > 1 ? 1 : form, std::memory_order_relaxed);
+  return prev;
+}
+// the packed ranges (extend_quad) for reads up to lq: H <= lq * max(mat) < 4096
+// (the row-max key H << KS | c, KS <= 3), H * 2^sk + 128 < 2^15 (2^sk >
+// max(mat)), and the scan values H + 33 * CPL * e_ins < 2^15
+bool quad_bound_ok(const DevOpt& o, long hb) {  // hb: a bound on every H of the call
+  if (o.max_mat < 1 || o.max_mat > 15) return false;
+  const int sk = 32 - __builtin_clz((unsigned)o.max_mat);
+  for (int k = 0; k < 25; ++k)
+    if (o.mat[k] < -127 || o.mat[k] > 127) return false;
+  return hb < 4096 && (hb << sk) + 128 < 32768 && hb + 33L * 8 * o.e_ins < 32768 && o.o_del + 128L < 32768 &&
+         o.oe_ins + 128L < 32768 && o.e_del < 32768;
+}
+bool quad_scores_ok(const DevOpt& o, int lq) { return quad_bound_ok(o, (long)lq * o.max_mat); }
+// the packed row-end state for calls of up to `rows` target rows: i, |i - j|
+// and the z-drop term max((di - dj) e_del, (dj - di) e_ins) (di <= rows,
+// dj <= 256) within 16 bits beside H < 4096
+bool quad_rows_ok(const DevOpt& o, long rows) {
+  return rows >= 0 && rows < 16384 && (rows + 256) * std::max(o.e_del, o.e_ins) < 28672;
+}
+
+static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
+                             int tb_bytes, hipStream_t st, const SpecStreams& ss) {
+  const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
+  const int l = round * kSpecBins;
+  const bool quad = g_ext_form.load(std::memory_order_relaxed) == 0 && quad_scores_ok(o, kSpecBinLen[1]) &&
+                    quad_rows_ok(o, tb_bytes);
+  const size_t lds2 = quad ? ext4_lds(tb_bytes) : ext2_lds(tb_bytes);
+  // the first two length bins' lists in pair order (spec_sort_*), then two or
+  // four seeds per wave; the third (reads > 256 bp) one seed per wave
+  hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
+  hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
+  hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
+  const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
+  if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
+  if (quad) {
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[0] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext4_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 0, tb_bytes);
+  } else {
+    const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 0, tb_bytes);
+  }
+  if (prof) {
+    (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
+    *ss.pool_used += 2;
+  }
+  if (quad) {
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext4_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 1, tb_bytes);
+  } else {
+    const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+                       l + 1, tb_bytes);
+  }
+  const int nb = resident_blocks(spec_ext_kernel<16>, lds);
+  hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 2, tb_bytes);
+}
+
+// prep -> round A -> emulate -> round B -> final -> round C -> redo, one stream
+hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
+                                 int tb_bytes, hipStream_t st, const SpecStreams& ss) {
+  if (b.n_reads == 0) return hipSuccess;
+  hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
+  if (b.n_chains) {
+    hipLaunchKernelGGL(spec_chain_kernel, dim3((b.n_chains + 255) / 256), dim3(256), 0, st, o, ref, b, a);
+    hipLaunchKernelGGL(spec_order_kernel, dim3(kOrderBlocks), dim3(256), 0, st, o, ref, b, a);
+  }
+  if (b.n_chains) {
+    launch_ext_round(o, ref, b, a, 0, tb_bytes, st, ss);
+    launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st, ss);
+    launch_ext_round(o, ref, b, a, 1, tb_bytes, st, ss);
+  }
+  launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
+  if (b.n_chains) {
+    launch_ext_round(o, ref, b, a, 2, tb_bytes, st, ss);
+    launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
+  }
+  return hipGetLastError();
+}
+
+size_t spec_select_lds(int tb_bytes) { return (size_t)kSelHeavyLds + 0 * tb_bytes; }
+int spec_redo_cap(int tb_bytes) { return sel_heavy_cap(SEL_REDO, tb_bytes); }
+
+}  // namespace bwagpu

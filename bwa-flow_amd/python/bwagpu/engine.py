@@ -258,7 +258,7 @@ class Engine:
 
     def quad_ok(self, lq: int = 256) -> bool:
         """whether the first two read-length bins run four seeds per wave with
-        these options (sw_kernels.hip quad_scores_ok: every score of a read of
+        these options (spec.hip quad_scores_ok: every score of a read of
         up to lq bases fits the packed 16-bit ranges)"""
         o = self.opt
         mat = list(o.mat)
