@@ -217,6 +217,7 @@ int set_ext_form(int form);
 bool quad_scores_ok(const DevOpt& o, int lq);
 bool quad_bound_ok(const DevOpt& o, long hb);
 bool quad_rows_ok(const DevOpt& o, long rows);
+bool quad_key8_ok(const DevOpt& o, int lq);
 int ext_form();
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, hipStream_t st, const SpecStreams& ss);

@@ -702,6 +702,14 @@ __device__ __forceinline__ uint32_t half_umin(uint32_t x) {
   const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
   return umin((uint32_t)p[0], (uint32_t)p[1]);
 }
+__device__ __forceinline__ uint32_t half_umax(uint32_t x) {
+  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(4), 0xF, 0xF, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(2), 0xF, 0xF, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(1), 0xF, 0xF, false));
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return umax((uint32_t)p[0], (uint32_t)p[1]);
+}
 __device__ __forceinline__ uint32_t half_smax(uint32_t x) {
   x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
   x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(4), 0xF, 0xF, false));
@@ -735,7 +743,9 @@ __device__ __forceinline__ QCall quad_idle(const uint8_t* seq, const uint8_t* tb
   return q;
 }
 
-template <int CPL>
+// K8: the row-max key is H << 8 | j, packed, one reduction for both calls
+// (every H < 256: quad_key8_ok); else H << KS | c widened to H << 10 | j per call.
+template <int CPL, bool K8>
 __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa, ExtOut& xb,
                                             Tally32& ta, Tally32& tbl) {
   using namespace pk16;
@@ -826,7 +836,10 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       const uint32_t h = smax(smax(sub(MB[c], 0x00800080u), ee[c]), f);
       hm[c] = umin(h, CAP[c]);
       const uint32_t en = usat(smax(ee[c], sub(MB[c], MB_OD)), ED1);
-      LK = umax(LK, mad(hm[c], pk(1 << KS, 1 << KS), pk(c, c)));
+      if constexpr (K8)
+        LK = umax(LK, mad(hm[c], pk(256, 256), add(J0, pk(c, c))));
+      else
+        LK = umax(LK, mad(hm[c], pk(1 << KS, 1 << KS), pk(c, c)));
       ee[c] = sel(R[c], umin(en, CAP[c]), ee[c]);
       if (c > 0) hh[c] = sel(R[c], hm[c - 1], hh[c]);
       H1Q |= hm[c] & qm[c];
@@ -846,14 +859,24 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));
       CH = sel(nz & R[c], add(J0, pk(c, c)), CH);
     }
-    // the row maxima (key H << 10 | j, ksw.c:433) and the trim, reduced over the half
-    const uint32_t lka = LK & 0xffffu, lkb = LK >> 16;
-    int ka = (int)(((lka >> KS) << 10) | (uint32_t)(j0 + (int)(lka & ((1u << KS) - 1))));
-    int kb = (int)(((lkb >> KS) << 10) | (uint32_t)(j0 + (int)(lkb & ((1u << KS) - 1))));
+    // the row maxima (ksw.c:433: the LAST column of the maximum) and the trim,
+    // reduced over the half: MROW = the row's max H, MJ = its column
+    uint32_t MROW, MJ;
+    if constexpr (K8) {
+      const uint32_t K = half_umax(LK);
+      MROW = W(U(K) >> (u16x2){8, 8});
+      MJ = K & 0x00ff00ffu;
+    } else {
+      const uint32_t lka = LK & 0xffffu, lkb = LK >> 16;
+      int ka = (int)(((lka >> KS) << 10) | (uint32_t)(j0 + (int)(lka & ((1u << KS) - 1))));
+      int kb = (int)(((lkb >> KS) << 10) | (uint32_t)(j0 + (int)(lkb & ((1u << KS) - 1))));
+      ka = half_max(row_max32(ka));
+      kb = half_max(row_max32(kb));
+      MROW = pk(ka >> 10, kb >> 10);
+      MJ = pk(ka & 1023, kb & 1023);
+    }
     CL = half_umin(CL);
     CH = half_smax(CH);
-    ka = half_max(row_max32(ka));
-    kb = half_max(row_max32(kb));
     // ksw.c:450-453 (meaningful on the owner of column qlen-1)
     {
       const uint32_t AT = neg15(sub(umin(sub(smax(LO, HI), QL), ONE), ONE));  // 0xffff where max(lo, hi) == qlen
@@ -865,7 +888,6 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     // ksw.c:454-465 on both calls at once (16-bit: quad_rows_ok); branch-free:
     // an ended call's row maximum is 0, which changes nothing but its break
     {
-      const uint32_t MROW = pk(ka >> 10, kb >> 10), MJ = pk(ka & 1023, kb & 1023);
       const uint32_t UP = neg15(sub(BEST, MROW));  // m > max
       const uint32_t DD = sub(sub(I, BI), sub(MJ, BJ));
       const uint32_t DROP = sub(sub(BEST, MROW), smax(mul(DD, ED1), mul(sub(0u, DD), EI1)));
@@ -898,14 +920,14 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
 }
 
 // CPL = ceil((qlen+1)/32) of the wave's longest active call (all four run one body)
-template <int PMAX>
+template <int PMAX, bool K8>
 __device__ __forceinline__ void extend_quad_dispatch(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa,
                                                      ExtOut& xb, Tally32& ta, Tally32& tbl) {
   const int qm = max(max(__builtin_amdgcn_readlane(A.qlen, 0), __builtin_amdgcn_readlane(Bc.qlen, 0)),
                      max(__builtin_amdgcn_readlane(A.qlen, 32), __builtin_amdgcn_readlane(Bc.qlen, 32)));
   const int cpl = (qm + 32) >> 5;
 #define EXT_QUAD(n) \
-  if (n <= PMAX && cpl == n) return extend_quad<(n <= PMAX ? n : 1)>(o, A, Bc, xa, xb, ta, tbl);
+  if (n <= PMAX && cpl == n) return extend_quad<(n <= PMAX ? n : 1), K8>(o, A, Bc, xa, xb, ta, tbl);
   EXT_QUAD(1) EXT_QUAD(2) EXT_QUAD(3) EXT_QUAD(4) EXT_QUAD(5) EXT_QUAD(6) EXT_QUAD(7) EXT_QUAD(8)
 #undef EXT_QUAD
 }

@@ -626,7 +626,7 @@ __device__ __forceinline__ QTask qload(LdsQ* p) {
 
 // Extension tasks of one list (in pair order, spec_sort_*), four per wave.
 // PMAX = the bin's largest CPL: ceil(read length / 32).
-template <int PMAX>
+template <int PMAX, bool K8>
 __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
                                                            int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -688,7 +688,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
     }
     ExtOut xa, xb;
     Tally32 ta{0, 0, 0}, tb{0, 0, 0};
-    extend_quad_dispatch<PMAX>(o, ca, cb, xa, xb, ta, tb);
+    extend_quad_dispatch<PMAX, K8>(o, ca, cb, xa, xb, ta, tb);
     if (ha) {
       QTask t = qload(qa);
       if (qtask_advance(t, o, xa, ta)) {
@@ -1692,6 +1692,8 @@ bool quad_bound_ok(const DevOpt& o, long hb) {  // hb: a bound on every H of the
          o.oe_ins + 128L < 32768 && o.e_del < 32768;
 }
 bool quad_scores_ok(const DevOpt& o, int lq) { return quad_bound_ok(o, (long)lq * o.max_mat); }
+// the 8-bit-column row-max key (extend_quad<.., true>): every H of reads up to lq < 256
+bool quad_key8_ok(const DevOpt& o, int lq) { return (long)lq * o.max_mat <= 255; }
 // the packed row-end state for calls of up to `rows` target rows: i, |i - j|
 // and the z-drop term max((di - dj) e_del, (dj - di) e_ins) (di <= rows,
 // dj <= 256) within 16 bits beside H < 4096
@@ -1713,10 +1715,14 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  if (quad) {
-    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[0] / 32>, lds2);
-    hipLaunchKernelGGL(spec_ext4_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
-                       l + 0, tb_bytes);
+  if (quad && quad_key8_ok(o, kSpecBinLen[0])) {
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[0] / 32, true>, lds2);
+    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[0] / 32, true>), dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o,
+                       ref, b, a, l + 0, tb_bytes);
+  } else if (quad) {
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32, false>, lds2);
+    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o,
+                       ref, b, a, l + 0, tb_bytes);
   } else {
     const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
     hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
@@ -1727,9 +1733,9 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
     *ss.pool_used += 2;
   }
   if (quad) {
-    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32>, lds2);
-    hipLaunchKernelGGL(spec_ext4_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
-                       l + 1, tb_bytes);
+    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32, false>, lds2);
+    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o,
+                       ref, b, a, l + 1, tb_bytes);
   } else {
     const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
     hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,

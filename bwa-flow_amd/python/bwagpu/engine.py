@@ -271,6 +271,11 @@ class Engine:
                 and o.o_del + 128 < 32768 and o.o_ins + o.e_ins + 128 < 32768 and o.e_del < 32768
                 and (lq + 2 * o.w + 18 + 256) * max(o.e_del, o.e_ins) < 28672)  # quad_rows_ok(tb rows)
 
+    def quad_key8_ok(self, lq: int = 160) -> bool:
+        """whether reads of up to lq bases take the 8-bit-column row-max key
+        (spec.hip quad_key8_ok: every H < 256)"""
+        return lq * max(list(self.opt.mat)) <= 255
+
     def sup_shift(self, shift: int):
         """superblock size 2^shift of the occurrence layout the NEXT set_bwt builds (tests; default 32)"""
         self._check(self.lib.bwagpu_debug_sup_shift(self.ctx, shift), "sup_shift")
