@@ -172,6 +172,7 @@ struct bwagpu_ctx {
   // takes it: ~p90 of the C2 batch's per-read counts (mean 666, p90 975)
   int seed_budget = 1024;
   int sup_shift = 32;  // bwagpu_debug_sup_shift: superblock size of the next set_bwt
+  int dev_read_len = BWAGPU_MAX_READ_LEN;  // bwagpu_set_device_read_len
   // bwagpu_debug_fail_wait: after fail_after more successful waits, _wait
   // returns fail_code once (tests of the stage's recovery path)
   int fail_after = -1, fail_code = 0;
@@ -568,11 +569,12 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
     HIPC(hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming), "hipEventCreate");
     HIPC(hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming), "hipEventCreate");
   }
+  a.lq_bound = lq_max;
   const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
   s.spec.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
   s.spec.pool_n = (int)ctx->prof_ev.size();
   s.spec.pool_used = &ctx->prof_used;
-  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, st, s.spec), "spec chain2aln launch");
+  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, s.spec), "spec chain2aln launch");
   return BWAGPU_OK;
 }
 
@@ -867,8 +869,11 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwag
                             int32_t* dev_n, int64_t* dev_stats, void* stream) {
   if (!ctx || !db_in || !dev_out || !dev_n) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  // reads are bounded by BWAGPU_MAX_READ_LEN; the LDS row buffer is sized for it
-  int rc = check_lds(ctx, BWAGPU_MAX_READ_LEN);
+  // reads are bounded by bwagpu_set_device_read_len (default BWAGPU_MAX_READ_LEN)
+  // on the speculative path, by BWAGPU_MAX_READ_LEN on the per-read one; the
+  // LDS row buffers are sized for the bound
+  const int lq_bound = use_read_kernels() ? BWAGPU_MAX_READ_LEN : ctx->dev_read_len;
+  int rc = check_lds(ctx, lq_bound);
   if (rc) return rc;
   hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
   int k = 0;
@@ -893,7 +898,7 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwag
     stats = s.d_stats.as<int64_t>();
     HIPC(hipMemsetAsync(stats, 0, sizeof(int64_t) * ST_N, st), "memset stats");
   }
-  return enqueue_chain2aln(ctx, s, db, BWAGPU_MAX_READ_LEN, dev_out, dev_n, stats, st);
+  return enqueue_chain2aln(ctx, s, db, lq_bound, dev_out, dev_n, stats, st);
 }
 
 int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* tasks, const uint8_t* qpool,
@@ -1663,6 +1668,12 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
 extern "C" int bwagpu_debug_seed_budget(bwagpu_ctx_t* ctx, int32_t budget) {
   if (!ctx || budget < 0) return BWAGPU_E_INVAL;
   ctx->seed_budget = budget;
+  return BWAGPU_OK;
+}
+
+extern "C" int bwagpu_set_device_read_len(bwagpu_ctx_t* ctx, int32_t max_len) {
+  if (!ctx || max_len < 1 || max_len > BWAGPU_MAX_READ_LEN) return BWAGPU_E_INVAL;
+  ctx->dev_read_len = max_len;
   return BWAGPU_OK;
 }
 

@@ -177,6 +177,7 @@ __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_se
                     : (size_t)kSpecBins * n_chains + ((size_t)(round - 1) * kSpecBins + bin) * n_seeds;
 }
 struct SpecArgs {
+  int lq_bound;               // reads longer than this set ERR_LEN and are skipped
   ChainWin* win;              // per chain
   int32_t* chain_read;        // per chain
   bwagpu_seed_t* prog;        // per seed, processing order (pad_ = 1: key 0)
@@ -220,7 +221,7 @@ bool quad_rows_ok(const DevOpt& o, long rows);
 bool quad_key8_ok(const DevOpt& o, int lq);
 int ext_form();
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
-                                 int tb_bytes, hipStream_t st, const SpecStreams& ss);
+                                 int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss);
 // LDS bytes per workgroup of the largest spec launch; regions the redo pass
 // holds in LDS for target rows of tb_bytes (must stay > 0)
 size_t spec_select_lds(int tb_bytes);

@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, D
         a.win[c] = ChainWin{0, -1};
       } else {
         if (!longc) a.win[c] = ChainWin{wlo, whi};
-        task = lq <= BWAGPU_MAX_READ_LEN;
+        task = lq <= a.lq_bound;
         bin = spec_bin(lq);
       }
     }
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a)
   int ns = 0;
   if (rd < b.n_reads) {
     const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
-    if (lq > BWAGPU_MAX_READ_LEN) atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_LEN);
+    if (lq > a.lq_bound) atomicOr((unsigned long long*)&a.stats[ST_ERR], (unsigned long long)ERR_LEN);
     ReadDesc d;
     d.qoff = b.seq_off[rd];
     d.rd = rd;
@@ -975,7 +975,7 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
     const int rd = uni(hlist[t]);
     const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const ReadDesc d = uniform_desc(a.rdesc[rd]);
-    if (d.lq > BWAGPU_MAX_READ_LEN) continue;  // flagged by spec_reads_kernel
+    if (d.lq > a.lq_bound) continue;  // flagged by spec_reads_kernel
     const uint8_t* const q = b.seq + d.qoff;
     const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
     bool redo = false;
@@ -1189,7 +1189,7 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
     const ReadDesc d = uniform_desc(dn);
     if (rd + NW < b.n_reads) dn = a.rdesc[rd + NW];
     if (d.ns > kSelLight || d.nch > kSelLight) continue;  // the heavy kernel's read
-    if (d.lq > BWAGPU_MAX_READ_LEN) continue;             // flagged by spec_reads_kernel
+    if (d.lq > a.lq_bound) continue;                      // flagged by spec_reads_kernel
     if (d.ns == 0) {
       if (WRITE) a.out_n[rd] = 0;
       continue;
@@ -1521,7 +1521,7 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
     const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const int nw = (ns + 63) >> 6;
     const ReadDesc d = uniform_desc(a.rdesc[rd]);
-    if (d.lq > BWAGPU_MAX_READ_LEN) continue;
+    if (d.lq > a.lq_bound) continue;  // flagged by spec_reads_kernel
     const int64_t tw = tri_off(ns);
     const uint64_t* Cg = a.mat + woff;
     const bool staged = 2 * tw * 8 <= kScanLds;
@@ -1701,10 +1701,17 @@ bool quad_rows_ok(const DevOpt& o, long rows) {
   return rows >= 0 && rows < 16384 && (rows + 256) * std::max(o.e_del, o.e_ins) < 28672;
 }
 
+// Only the bins the batch's longest read reaches are launched: a persistent
+// grid over an empty list still waits for CU slots that the other caller
+// stream's extension kernel holds, and its stream waits with it.  Round C
+// (mispredicted seeds of long reads: rare) runs on small grids for the same
+// reason.
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
-                             int tb_bytes, hipStream_t st, const SpecStreams& ss) {
+                             int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
+  const bool bin1 = lq_max > kSpecBinLen[0], bin2 = lq_max > kSpecBinLen[1];
+  const auto grid = [round](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb); };
   const bool quad = g_ext_form.load(std::memory_order_relaxed) == 0 && quad_scores_ok(o, kSpecBinLen[1]) &&
                     quad_rows_ok(o, tb_bytes);
   const size_t lds2 = quad ? ext4_lds(tb_bytes) : ext2_lds(tb_bytes);
@@ -1717,37 +1724,40 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
   if (quad && quad_key8_ok(o, kSpecBinLen[0])) {
     const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[0] / 32, true>, lds2);
-    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[0] / 32, true>), dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o,
+    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[0] / 32, true>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 0, tb_bytes);
   } else if (quad) {
     const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32, false>, lds2);
-    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o,
+    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 0, tb_bytes);
   } else {
     const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[0] / 32>, dim3(grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
                        l + 0, tb_bytes);
   }
   if (prof) {
     (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
     *ss.pool_used += 2;
   }
+  if (!bin1) return;
   if (quad) {
     const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32, false>, lds2);
-    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o,
+    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 1, tb_bytes);
   } else {
     const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);
-    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(ext2_grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
+    hipLaunchKernelGGL(spec_ext2_kernel<kSpecBinLen[1] / 32>, dim3(grid(nb)), dim3(kBlock), lds2, st, o, ref, b, a,
                        l + 1, tb_bytes);
   }
+  if (!bin2) return;
   const int nb = resident_blocks(spec_ext_kernel<16>, lds);
-  hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, l + 2, tb_bytes);
+  hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(round == 2 ? std::min(nb, 64) : nb), dim3(kBlock), lds, st, o, ref, b, a,
+                     l + 2, tb_bytes);
 }
 
 // prep -> round A -> emulate -> round B -> final -> round C -> redo, one stream
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
-                                 int tb_bytes, hipStream_t st, const SpecStreams& ss) {
+                                 int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   if (b.n_reads == 0) return hipSuccess;
   hipLaunchKernelGGL(spec_reads_kernel, dim3((b.n_reads + 255) / 256), dim3(256), 0, st, b, a);
   if (b.n_chains) {
@@ -1755,13 +1765,13 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
     hipLaunchKernelGGL(spec_order_kernel, dim3(kOrderBlocks), dim3(256), 0, st, o, ref, b, a);
   }
   if (b.n_chains) {
-    launch_ext_round(o, ref, b, a, 0, tb_bytes, st, ss);
+    launch_ext_round(o, ref, b, a, 0, tb_bytes, lq_max, st, ss);
     launch_select<SEL_EMULATE>(o, ref, b, a, tb_bytes, st, ss);
-    launch_ext_round(o, ref, b, a, 1, tb_bytes, st, ss);
+    launch_ext_round(o, ref, b, a, 1, tb_bytes, lq_max, st, ss);
   }
   launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
   if (b.n_chains) {
-    launch_ext_round(o, ref, b, a, 2, tb_bytes, st, ss);
+    launch_ext_round(o, ref, b, a, 2, tb_bytes, lq_max, st, ss);
     launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
   }
   return hipGetLastError();

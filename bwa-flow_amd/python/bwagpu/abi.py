@@ -150,6 +150,7 @@ PROTOS = {
     "bwagpu_set_bwt": (C.c_int, [_VP, C.POINTER(BwtC)]),
     "bwagpu_debug_seed_budget": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_debug_sup_shift": (C.c_int, [_VP, C.c_int32]),
+    "bwagpu_set_device_read_len": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_debug_ext_form": (C.c_int, [C.c_int]),
     "bwagpu_bwt_sa": (C.c_int, [_VP, C.c_int64, _VP, _VP]),
     "bwagpu_sw_stream": (C.c_int, [_VP, _VP, C.c_int64, _VP, C.c_int32, C.POINTER(C.c_int32)]),

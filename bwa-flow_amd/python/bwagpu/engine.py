@@ -276,6 +276,10 @@ class Engine:
         (spec.hip quad_key8_ok: every H < 256)"""
         return lq * max(list(self.opt.mat)) <= 255
 
+    def set_device_read_len(self, max_len: int):
+        """bound on the read lengths of later device batches (bwagpu_set_device_read_len)"""
+        self._check(self.lib.bwagpu_set_device_read_len(self.ctx, int(max_len)), "set_device_read_len")
+
     def sup_shift(self, shift: int):
         """superblock size 2^shift of the occurrence layout the NEXT set_bwt builds (tests; default 32)"""
         self._check(self.lib.bwagpu_debug_sup_shift(self.ctx, shift), "sup_shift")

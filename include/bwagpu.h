@@ -352,6 +352,14 @@ int bwagpu_chain2aln_results(bwagpu_ctx_t *ctx, int slot, const bwagpu_alnreg_t 
 int bwagpu_chain2aln_device(bwagpu_ctx_t *ctx, const bwagpu_batch_t *dev_batch,
                             bwagpu_alnreg_t *dev_out, int32_t *dev_n, int64_t *dev_stats,
                             void *stream);
+/* A bound on the read lengths of later _device batches (1..BWAGPU_MAX_READ_LEN,
+   default BWAGPU_MAX_READ_LEN; the host entries take the exact maximum from
+   seq_off).  The device sizes its LDS row buffers for it and launches only the
+   length bins it reaches (a persistent grid over an empty bin still waits for
+   the CU slots another stream's kernel holds).  A longer read sets
+   dev_stats[3] bit 2 (as a read over BWAGPU_MAX_READ_LEN does) and gets no
+   regions.  The per-read path (BWAGPU_C2A_PATH=fast) ignores it. */
+int bwagpu_set_device_read_len(bwagpu_ctx_t *ctx, int32_t max_len);
 
 int bwagpu_extend_batch(bwagpu_ctx_t *ctx, int32_t n_tasks, const bwagpu_ext_task_t *tasks,
                         const uint8_t *qpool, int64_t qpool_len, const uint8_t *tpool,

@@ -69,6 +69,7 @@ def test_null_arguments_are_rejected():
     assert lib.bwagpu_set_watchdog_ms(None, 5) == abi.E_INVAL
     assert lib.bwagpu_chain2aln(None, None, None, None) == abi.E_INVAL
     assert lib.bwagpu_last_error(None) == b"NULL context"
+    assert lib.bwagpu_set_device_read_len(None, 150) == abi.E_INVAL
 
 
 LAYOUT_C = r"""

@@ -243,6 +243,46 @@ def test_device_entry_point_with_torch_buffers(refd):
     eng.close()
 
 
+def test_device_entry_read_len_bound(refd):
+    """bwagpu_set_device_read_len: the exact bound gives the same regions (the
+    longer length bins are not launched); a bound below the longest read sets
+    the length error flag; out-of-range bounds are refused"""
+    torch = pytest.importorskip("torch")
+    from bwagpu.synth import SynthRef, synth_batch
+    sref = SynthRef(78, 2_000_000, 3)
+    batch = synth_batch(sref, 9, 300, 0, 19)  # mixed read lengths
+    opt = abi.default_opt()
+    eng = Engine(0, opt, sref.l_pac, sref.ann_offset, sref.ann_len, pac=sref.pac)
+    want, want_n = eng.chain2aln(batch)
+    lq = np.diff(batch.seq_off)
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(batch, k)).view(np.uint8)).to(dev)
+         for k in ("seq_off", "seq", "read_chain_off", "chain_seed_off", "chain_rid", "chain_frac_rep", "seeds")}
+    bc = abi.BatchC()
+    bc.n_reads, bc.n_chains, bc.n_seeds = batch.n_reads, batch.n_chains, batch.n_seeds
+    bc.seq_bytes = int(batch.seq_off[-1])
+    for k in t:
+        setattr(bc, k, t[k].data_ptr())
+    stream = torch.cuda.current_stream().cuda_stream
+    for bound, err in ((int(lq.max()), 0), (160, 2 if lq.max() > 160 else 0), (int(lq.max()) - 1, 2)):
+        eng.set_device_read_len(bound)
+        out = torch.zeros(batch.n_seeds * 88, dtype=torch.uint8, device=dev)
+        n = torch.zeros(batch.n_reads, dtype=torch.int32, device=dev)
+        stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        eng.chain2aln_device(bc, out.data_ptr(), n.data_ptr(), stats.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert int(stats[3]) & 2 == err, bound
+        if err == 0:
+            nn = n.cpu().numpy()
+            assert np.array_equal(nn, want_n)
+            regs = out.cpu().numpy().view(abi.ALNREG_DTYPE)
+            assert G.region_mismatch(compact(batch, regs, nn), compact(batch, want, want_n)) is None
+    for bad in (0, abi.MAX_READ_LEN + 1):
+        with pytest.raises(BwaGpuError):
+            eng.set_device_read_len(bad)
+    eng.close()
+
+
 @pytest.mark.parametrize("len_mode,min_seed,pairs", [(150, 19, 800), (0, 19, 600), (250, 12, 400), (400, 12, 300),
                                                      (700, 8, 150), (1000, 8, 60)])
 def test_synthetic_batches_vs_oracle(len_mode, min_seed, pairs, c2a_path):
