@@ -209,6 +209,89 @@ def _unpack_seq(seq2: np.ndarray, npos: np.ndarray, n: int) -> np.ndarray:
     return s
 
 
+C3R_FIXTURE = os.path.join(REPO, "tests", "golden", "c3_refseed.npz")
+
+
+class GoldenInGrch38:
+    """the reference-seeded C2 genome (GoldenRef, the c2_refseed fixture's, 3
+    contigs) twice around the GRCh38-shaped one: copy A at forward offset 0
+    (contigs 0-2), the 195 GRCh38 contigs, copy B at the end (contigs 198-200);
+    every offset is a multiple of 4 (the contig before a gap takes the pad
+    bases, A).  Even reads of a translated batch go to copy A, whose reverse
+    strand lies past 2-strand 2^32; odd reads to copy B, past forward 2^31.
+    A golden coordinate x (either strand) becomes, in copy B, x + offB (forward
+    p -> p + offB, reverse 2l-1-p -> 2L-1-(p + offB) = x + offB as L = offB + l);
+    in copy A, x on the forward strand and x + 2(L - l) on the reverse."""
+
+    def __init__(self, grch=None, golden=None):
+        from .synth import GoldenRef, Grch38Ref
+        z = np.load(C2_FIXTURE, allow_pickle=False)
+        grch = grch if grch is not None else Grch38Ref(38)
+        golden = golden if golden is not None else GoldenRef(int(z["genome_len"]), int(z["genome_seed"]))
+
+        def body(pac, n):  # the bytes of n bases, pad bases of the last byte zeroed (A)
+            h = np.asarray(pac[:(n + 3) // 4], np.uint8).copy()
+            if n & 3:
+                h[-1] &= np.uint8((0xff << (2 * (4 - (n & 3)))) & 0xff)
+            return h
+
+        self.lg = lg = int(golden.l_pac)
+        lr = int(grch.l_pac)
+        self.off_grch = (lg + 3) & ~3
+        self.off_b = (self.off_grch + lr + 3) & ~3
+        self.l_pac = self.off_b + lg
+        ga, gl = np.asarray(golden.ann_offset, np.int64), np.asarray(golden.ann_len, np.int64)
+        self.ann_offset = np.concatenate([ga, np.asarray(grch.ann_offset, np.int64) + self.off_grch, ga + self.off_b])
+        ann_len = np.concatenate([gl, np.asarray(grch.ann_len, np.int64), gl])
+        ann_len[len(gl) - 1] += self.off_grch - lg
+        ann_len[len(gl) + len(grch.ann_len) - 1] += self.off_b - self.off_grch - lr
+        self.ann_len = ann_len.astype(np.int32)
+        self.rid_b = len(gl) + len(grch.ann_len)
+        self.pac = np.concatenate([body(golden.pac, lg), body(grch.pac, lr), body(golden.pac, lg)])
+
+    def translate(self, b: Batch) -> Batch:
+        """a batch on the golden genome -> the same batch here (even reads on
+        copy A, odd reads on copy B)"""
+        nch = np.diff(b.read_chain_off)
+        chain_b = np.repeat((np.arange(b.n_reads) & 1).astype(bool), nch)
+        seed_b = np.repeat(chain_b, np.diff(b.chain_seed_off))
+        seeds = b.seeds.copy()
+        x = seeds["rbeg"].astype(np.int64)
+        seeds["rbeg"] = np.where(seed_b, x + self.off_b, np.where(x < self.lg, x, x + 2 * (self.l_pac - self.lg)))
+        rid = np.where(chain_b, b.chain_rid + self.rid_b, b.chain_rid).astype(np.int32)
+        return Batch(b.seq_off, b.seq, b.read_chain_off, b.chain_seed_off, rid, b.chain_frac_rep, seeds)
+
+
+class C3RefSet:
+    """C2 batch 0's reference-seeded chains, translated into the GRCh38-shaped
+    genome past 2^31 (GoldenInGrch38), with the reference's answers there"""
+
+    def __init__(self, z, batch: Batch):
+        self.name = "c3_refseed"
+        self.batch = batch
+        if batch_digest(batch) != z["batch_sha256"].tobytes():
+            raise RuntimeError("translated c3_refseed batch differs from the fixture's")
+        self.reg_n = z["reg_n"].astype(np.int32)
+        self.regs_sha256 = z["regs_sha256"].tobytes()
+        self.regs_chunks = z["regs_chunks"]
+        self.coverage = dict(zip(C3_COVERAGE_KEYS, z["coverage"].tolist()))
+
+    check = C3Set.check
+
+
+def load_c3_refseed(path: str = C3R_FIXTURE, grch=None, golden=None):
+    """-> (opt dict, GoldenInGrch38, C3RefSet); raises if the regenerated
+    genome or the translated batch differs from the one the reference ran on"""
+    z = np.load(path, allow_pickle=False)
+    opt = dict(zip(OPT_KEYS, z["opt_int"].tolist()))
+    opt["mat"] = z["opt_mat"].astype(np.int8)
+    g = GoldenInGrch38(grch, golden)
+    if hashlib.sha256(g.pac).digest() != z["pac_sha256"].tobytes():
+        raise RuntimeError("regenerated golden-in-GRCh38 genome differs from the fixture's")
+    _, _, bs = load_fixture(with_ref=False)
+    return opt, g, C3RefSet(z, g.translate(bs[int(z["c2_batch"])].batch))
+
+
 def load_fixture(path: str = C2_FIXTURE, with_ref: bool = True):
     """-> (opt dict, GoldenRef or None, [RefBatch]); raises if the regenerated
     genome differs from the one the reference indexed"""

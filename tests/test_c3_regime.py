@@ -66,3 +66,29 @@ def test_cigar_oracle_matches_fixture(c3):
     jobs = workload.reg2aln_jobs(s.batch, regs, n)
     out = oracle.reg2aln("oracle", opt, R, jobs, s.batch.seq, workload.C3_MAX_OPS, workload.C3_MAX_MD)
     assert s.check_cigar(jobs, *out) is None
+
+
+@pytest.fixture(scope="module")
+def c3r(c3):
+    return workload.load_c3_refseed(grch=c3[1])
+
+
+def test_refseed_in_grch38_covers_the_regime(c3r):
+    """C2's reference-seeded chains (bwa's own seeding) translated past forward
+    2^31 (copy B) and 2-strand 2^32 (copy A's reverse strand) in a 0.8 GB pac"""
+    opt, g, s = c3r
+    assert len(g.ann_len) == 201 and g.l_pac > 3_190_000_000 and g.pac.nbytes > 256 << 20
+    assert int(g.ann_offset[-1]) + int(g.ann_len[-1]) == g.l_pac
+    cov = s.coverage
+    assert cov["seeds_fwd_ge_2^31"] > 50_000 and cov["seeds_ge_2^32"] > 50_000
+    assert cov["regs_fwd_ge_2^31"] > 20_000 and cov["regs_ge_2^32"] > 20_000
+
+
+@pytest.mark.parametrize("which", ["oracle", "ref"])
+def test_refseed_in_grch38_cpu_paths_match_fixture(c3r, which):
+    opt, g, s = c3r
+    if which == "ref" and oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    R = oracle.Ref(g.l_pac, g.ann_offset, g.ann_len, g.pac)
+    regs, n, _ = oracle.chain2aln(which, opt, R, s.batch, n_threads=min(8, os.cpu_count() or 1))
+    assert s.check(regs, n) is None

@@ -7,7 +7,10 @@ seeds sit past 2^31 (forward) and 2^32 (2-strand), in all 195 contigs and
 across contig junctions.  The GPU's mem_chain2aln output must match the
 reference's (oracle/_ref mem_chain2aln, recorded as digests) byte for byte, on
 both kernel paths; the CIGAR kernel (bns_pos2rid over 195 contigs) must match
-the reference's mem_reg2aln on every region.
+the reference's mem_reg2aln on every region.  And the C2 fixture's
+reference-seeded chains (bwa's own seeding) translated into that regime
+(tests/golden/c3_refseed.npz: two copies of the golden genome around the
+GRCh38-shaped contigs, seeds past forward 2^31 and 2-strand 2^32).
 """
 import numpy as np
 import pytest
@@ -54,3 +57,15 @@ def test_reg2aln_grch38(c3, eng, name):
     why = s.check_cigar(jobs, aln, cig, md)
     assert why is None, why
     assert len(np.unique(aln["rid"])) == 195
+
+
+@pytest.mark.parametrize("path", ["spec", "pair", "fast"])
+def test_chain2aln_refseed_in_grch38(c3, path, monkeypatch):
+    opt, g, s = workload.load_c3_refseed(grch=c3[1])
+    e = Engine(0, opt, g.l_pac, g.ann_offset, g.ann_len, pac=g.pac)
+    restore = set_c2a_path(path, monkeypatch)
+    regs, n = e.chain2aln(s.batch)
+    restore()
+    why = s.check(regs, n)
+    e.close()
+    assert why is None, why
