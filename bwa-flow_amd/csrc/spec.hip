@@ -7,6 +7,11 @@
 
 namespace bwagpu {
 
+// The selection and bookkeeping kernels are latency-bound chains that share
+// CUs with the other caller stream's persistent extension kernel; at wave
+// priority 3 their instructions issue ahead of its (priority 0) waves.
+__device__ __forceinline__ void sel_prio() { __builtin_amdgcn_s_setprio(3); }
+
 // per-read selection trace (bwagpu_debug_set_trace; this file's copy)
 __device__ uint32_t* g_trace = nullptr;
 hipError_t set_trace_spec(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p)); }
@@ -42,6 +47,7 @@ hipError_t set_trace_spec(void* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_trace
 // each (a lane looping over ~170 seeds was this kernel's tail).  chain_read
 // comes from spec_reads_kernel.
 __global__ void __launch_bounds__(256) spec_chain_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+  sel_prio();
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   bool task = false, longc = false;
   int bin = 0, s0 = 0;
@@ -111,6 +117,7 @@ __host__ __device__ inline int64_t tri_off(int k) {
 
 // lane per read: length check, and the list of heavy reads (selected first)
 __global__ void __launch_bounds__(256) spec_reads_kernel(DevBatch b, SpecArgs a) {
+  sel_prio();
   const int rd = blockIdx.x * blockDim.x + threadIdx.x;
   bool heavy = false;
   int ns = 0;
@@ -162,6 +169,7 @@ __device__ __forceinline__ uint64_t order_key(const bwagpu_seed_t* sd, int i) {
   return (uint64_t)(uint32_t)sd[i].score << 32 | (uint32_t)i;
 }
 __global__ void __launch_bounds__(256) spec_order_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a) {
+  sel_prio();
   __shared__ uint64_t keys[kOrderLds];
   __shared__ int64_t wred[2][4];
   const int tid = (int)threadIdx.x;
@@ -736,6 +744,7 @@ __device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, in
 }
 
 __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
+  sel_prio();
   __shared__ int hist[kSortKeys];
   const int list = round * kSpecBins + (int)blockIdx.y;
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
@@ -752,6 +761,7 @@ __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, i
 }
 
 __global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
+  sel_prio();
   __shared__ int part[256];
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.x) * kSortKeys;
   const int t = (int)threadIdx.x;  // 4 keys per thread
@@ -778,6 +788,7 @@ __global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
 }
 
 __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round) {
+  sel_prio();
   __shared__ int cnt[kSortKeys];
   const int list = round * kSpecBins + (int)blockIdx.y;
   int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
@@ -948,6 +959,7 @@ __device__ __forceinline__ void trace_read(int pass, int n_reads, int rd, uint64
 
 template <int MODE, bool HEAVY>
 __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int tb_bytes) {
+  sel_prio();
   static_assert(HEAVY, "one-wave heavy shape only");
   constexpr bool WRITE = MODE != SEL_EMULATE;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1168,6 +1180,7 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
 template <int MODE>
 __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
                                                             int tb_bytes) {
+  sel_prio();
   constexpr bool WRITE = MODE != SEL_EMULATE;
   __shared__ int32_t MG[kMglN];
   extern __shared__ __attribute__((aligned(16))) uint8_t lrows[];  // per wave: target rows of an inline extension
@@ -1386,6 +1399,7 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
 //     sets (lane w holds word w of the extended / skipped / pending sets), then
 //     every extended seed's record lane-parallel at its rank.
 __global__ void __launch_bounds__(kBlock) spec_pairs_kernel(DevOpt o, DevBatch b, SpecArgs a, int with_cov) {
+  sel_prio();
   __shared__ int32_t MG[kMglN];
   for (int x = threadIdx.x; x < kMglN; x += kBlock) MG[x] = max_gap_len(o, x);
   __syncthreads();
@@ -1506,6 +1520,7 @@ __device__ __forceinline__ void heavy_fill_missing(const DevOpt& o, const DevRef
 
 template <int MODE>
 __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int tb_bytes) {
+  sel_prio();
   constexpr bool WRITE = MODE != SEL_EMULATE;
   extern __shared__ __attribute__((aligned(16))) uint64_t M[];
   uint8_t* const tbl = reinterpret_cast<uint8_t*>(M) + kScanLds;
