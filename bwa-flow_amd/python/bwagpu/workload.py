@@ -274,9 +274,11 @@ class C3RefSet:
         self.reg_n = z["reg_n"].astype(np.int32)
         self.regs_sha256 = z["regs_sha256"].tobytes()
         self.regs_chunks = z["regs_chunks"]
+        self.cigar_chunks = z["cigar_chunks"]
         self.coverage = dict(zip(C3_COVERAGE_KEYS, z["coverage"].tolist()))
 
     check = C3Set.check
+    check_cigar = C3Set.check_cigar
 
 
 def load_c3_refseed(path: str = C3R_FIXTURE, grch=None, golden=None):

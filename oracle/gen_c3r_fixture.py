@@ -8,10 +8,11 @@ translated into a GRCh38-shaped reference: the golden genome twice, before
 and after the 195 GRCh38-shaped contigs (bwagpu.workload.GoldenInGrch38); the
 even reads' chains go to the first copy (its reverse strand lies past 2-strand
 2^32), the odd reads' to the second (past forward 2^31); the pac is 0.80 GB.
-The expected regions are the REFERENCE's: mem_chain2aln (bwa/bwamem.c:641-795)
-through oracle/_ref/libbwaref.so on the combined genome.  Stored: the pac
-digest, the translated batch's digest, per-read region counts, the SHA-256 of
-the 88-byte records and per-256-read chunk digests.
+The expected answers are the REFERENCE's, through oracle/_ref/libbwaref.so on
+the combined genome: mem_chain2aln (bwa/bwamem.c:641-795) and mem_reg2aln
+(bwa/bwamem.c:1104-1174) on every output region.  Stored: the pac digest, the
+translated batch's digest, per-read region counts, the SHA-256 of the 88-byte
+records, per-256-read chunk digests of the regions and of the CIGAR/MD output.
 
     python oracle/gen_c3r_fixture.py [--out tests/golden/c3_refseed.npz]
 """
@@ -53,6 +54,10 @@ def main():
     regs, n, _ = oracle.chain2aln("ref", opt, R, b, n_threads=a.threads)
     t_ref = time.time() - t1
     c = np.ascontiguousarray(compact(b, regs, n))
+    jobs = workload.reg2aln_jobs(b, regs, n)
+    t1 = time.time()
+    aln, cig, md = oracle.reg2aln("ref", opt, R, jobs, b.seq, workload.C3_MAX_OPS, workload.C3_MAX_MD)
+    t_cig = time.time() - t1
     st = workload.c3_coverage(g, b, c)
     # the translation must not change the answer's shape: same counts as on the golden genome
     assert np.array_equal(n.astype(np.int32), bs[C2_BATCH].reg_n), "region counts differ from the C2 fixture's"
@@ -63,9 +68,10 @@ def main():
                reg_n=n.astype(np.uint16),
                regs_sha256=np.frombuffer(hashlib.sha256(c.tobytes()).digest(), np.uint8),
                regs_chunks=workload.chunk_digests(b, c, n),
+               cigar_chunks=workload.cigar_chunk_digests(jobs, aln, cig, md),
                coverage=np.array([st[k] for k in workload.C3_COVERAGE_KEYS], np.int64))
     print(f"{b.n_reads} reads, {b.n_chains} chains, {b.n_seeds} seeds, {len(c)} regions (reference "
-          f"mem_chain2aln {t_ref:.1f} s on {a.threads} threads); {st}", file=sys.stderr)
+          f"mem_chain2aln {t_ref:.1f} s on {a.threads} threads), {len(jobs)} CIGAR jobs ({t_cig:.1f} s); {st}", file=sys.stderr)
     np.savez_compressed(a.out, **out)
     print(f"wrote {a.out}: {os.path.getsize(a.out) / 1e6:.2f} MB", file=sys.stderr)
 

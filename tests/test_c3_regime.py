@@ -92,3 +92,12 @@ def test_refseed_in_grch38_cpu_paths_match_fixture(c3r, which):
     R = oracle.Ref(g.l_pac, g.ann_offset, g.ann_len, g.pac)
     regs, n, _ = oracle.chain2aln(which, opt, R, s.batch, n_threads=min(8, os.cpu_count() or 1))
     assert s.check(regs, n) is None
+
+
+def test_refseed_in_grch38_cigars_match_fixture(c3r):
+    opt, g, s = c3r
+    R = oracle.Ref(g.l_pac, g.ann_offset, g.ann_len, g.pac)
+    regs, n, _ = oracle.chain2aln("oracle", opt, R, s.batch, n_threads=min(8, os.cpu_count() or 1))
+    jobs = workload.reg2aln_jobs(s.batch, regs, n)
+    aln, cig, md = oracle.reg2aln("oracle", opt, R, jobs, s.batch.seq, workload.C3_MAX_OPS, workload.C3_MAX_MD)
+    assert s.check_cigar(jobs, aln, cig, md) is None

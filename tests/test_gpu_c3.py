@@ -69,3 +69,16 @@ def test_chain2aln_refseed_in_grch38(c3, path, monkeypatch):
     why = s.check(regs, n)
     e.close()
     assert why is None, why
+
+
+def test_reg2aln_refseed_in_grch38(c3):
+    opt, g, s = workload.load_c3_refseed(grch=c3[1])
+    e = Engine(0, opt, g.l_pac, g.ann_offset, g.ann_len, pac=g.pac)
+    regs, n = e.chain2aln(s.batch)
+    jobs = workload.reg2aln_jobs(s.batch, regs, n)
+    aln, cig, md = e.reg2aln_batch(jobs, s.batch.seq, workload.C3_MAX_OPS, workload.C3_MAX_MD)
+    e.close()
+    assert len(jobs) == int(np.sum(s.reg_n))
+    why = s.check_cigar(jobs, aln, cig, md)
+    assert why is None, why
+    assert set(np.unique(aln["rid"]).tolist()) <= {0, 1, 2, 198, 199, 200}
