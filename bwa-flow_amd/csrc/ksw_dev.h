@@ -677,6 +677,7 @@ __device__ __forceinline__ uint32_t opq(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t neg15(uint32_t a) { return opq(W(S(a) >> (s16x2){15, 15})); }  // 0xffff where < 0
 __device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
 constexpr uint32_t ONE = 0x00010001u;
 // DPP moves of whole registers (bound_ctrl: a lane without a source reads 0)
 template <int CTRL>
@@ -702,13 +703,29 @@ __device__ __forceinline__ uint32_t half_umin(uint32_t x) {
   const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
   return umin((uint32_t)p[0], (uint32_t)p[1]);
 }
-__device__ __forceinline__ uint32_t half_umax(uint32_t x) {
-  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
-  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(4), 0xF, 0xF, false));
-  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(2), 0xF, 0xF, false));
-  x = umax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(1), 0xF, 0xF, false));
-  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-  return umax((uint32_t)p[0], (uint32_t)p[1]);
+// the half's umax of K, umin of L and smax of H at once: three independent
+// chains step by step, so no DPP read waits on the write just before it
+__device__ __forceinline__ void half_red3(uint32_t& K, uint32_t& L, uint32_t& H) {
+#define RED3_STEP(CTRL)                                                                  \
+  {                                                                                      \
+    const uint32_t k = (uint32_t)__builtin_amdgcn_mov_dpp((int)K, CTRL, 0xF, 0xF, false); \
+    const uint32_t l = (uint32_t)__builtin_amdgcn_mov_dpp((int)L, CTRL, 0xF, 0xF, false); \
+    const uint32_t h = (uint32_t)__builtin_amdgcn_mov_dpp((int)H, CTRL, 0xF, 0xF, false); \
+    K = umax(K, k);                                                                      \
+    L = umin(L, l);                                                                      \
+    H = smax(H, h);                                                                      \
+  }
+  RED3_STEP(DPP_ROW_ROR(8))
+  RED3_STEP(DPP_ROW_ROR(4))
+  RED3_STEP(DPP_ROW_ROR(2))
+  RED3_STEP(DPP_ROW_ROR(1))
+#undef RED3_STEP
+  const auto pk_ = __builtin_amdgcn_permlane16_swap(K, K, false, false);
+  const auto pl = __builtin_amdgcn_permlane16_swap(L, L, false, false);
+  const auto ph = __builtin_amdgcn_permlane16_swap(H, H, false, false);
+  K = umax((uint32_t)pk_[0], (uint32_t)pk_[1]);
+  L = umin((uint32_t)pl[0], (uint32_t)pl[1]);
+  H = smax((uint32_t)ph[0], (uint32_t)ph[1]);
 }
 __device__ __forceinline__ uint32_t half_smax(uint32_t x) {
   x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
@@ -863,7 +880,8 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     // reduced over the half: MROW = the row's max H, MJ = its column
     uint32_t MROW, MJ;
     if constexpr (K8) {
-      const uint32_t K = half_umax(LK);
+      uint32_t K = LK;
+      half_red3(K, CL, CH);
       MROW = W(U(K) >> (u16x2){8, 8});
       MJ = K & 0x00ff00ffu;
     } else {
@@ -874,9 +892,9 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       kb = half_max(row_max32(kb));
       MROW = pk(ka >> 10, kb >> 10);
       MJ = pk(ka & 1023, kb & 1023);
+      CL = half_umin(CL);
+      CH = half_smax(CH);
     }
-    CL = half_umin(CL);
-    CH = half_smax(CH);
     // ksw.c:450-453 (meaningful on the owner of column qlen-1)
     {
       const uint32_t AT = neg15(sub(umin(sub(smax(LO, HI), QL), ONE), ONE));  // 0xffff where max(lo, hi) == qlen

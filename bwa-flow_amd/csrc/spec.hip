@@ -740,7 +740,8 @@ __device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, in
   const int rd = a.chain_read[tk.y];
   const int lq = (int)(b.seq_off[rd + 1] - b.seq_off[rd]);
   const int ql = min(s.qbeg, 255), qr = min(max(lq - s.qbeg - s.len, 0), 255);
-  return (ql >> 3) << 5 | (qr >> 3);
+  // descending: the longest tasks first, so the grid's tail is short ones
+  return (kSortKeys - 1) - ((ql >> 3) << 5 | (qr >> 3));
 }
 
 __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {

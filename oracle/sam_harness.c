@@ -602,7 +602,44 @@ static void ext_gpu(bwagpu_ctx_t *ctx, hw_t *w, int n, int T)
    text) is final for every pair without a miss; the pairs that missed (their
    rescue found a hit, so they print a region pass 0 could not know) are
    flushed and redone alone until none misses. */
-static void w_free_regs(void *data, int i, int tid) { free(((hw_t *)data)->regs[i].a); }
+
+/* The cache clear and the regions' free after a batch's SAM passes run on a
+   thread of their own while the next batch (on the other cache) aligns; a
+   cache is reused two batches later, after its clearer is joined. */
+typedef struct {
+  bwagpu_samcache_t *cache;
+  mem_alnreg_v *regs;
+  int n, live;
+  double t;
+  pthread_t th;
+} clearer_t;
+static void *clearer_main(void *arg)
+{
+  clearer_t *c = (clearer_t *)arg;
+  const double t0 = realtime();
+  G.sc_clear(c->cache);
+  for (int i = 0; i < c->n; ++i) free(c->regs[i].a);
+  free(c->regs);
+  c->t = realtime() - t0;
+  return 0;
+}
+static void clearer_join(clearer_t *c)
+{
+  if (!c->live) return;
+  pthread_join(c->th, 0);
+  g_t_clear += c->t;
+  c->live = 0;
+}
+static void clearer_start(clearer_t *c, bwagpu_samcache_t *cache, mem_alnreg_v *regs, int n)
+{
+  c->cache = cache;
+  c->regs = regs;
+  c->n = n;
+  c->live = 1;
+  pthread_create(&c->th, 0, clearer_main, c);
+}
+
+/* the passes; the caller clears `cache` and frees w->regs afterwards */
 static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t *n_passes, double *t_flush)
 {
   const int np = n >> 1;
@@ -630,10 +667,6 @@ static void sam_passes(bwagpu_samcache_t *cache, hw_t *w, int n, int T, int64_t 
   }
   bwagpu_sam_hooks_quiet(0);
   bwagpu_sam_hooks_attach(0);
-  const double tc = realtime();
-  G.sc_clear(cache);
-  kt_for(T, w_free_regs, w, n);
-  g_t_clear += realtime() - tc;
   free(pairs);
   free(miss);
 }
@@ -863,7 +896,9 @@ int main(int argc, char *argv[])
       free(alt);
     }
   }
-  bwagpu_samcache_t *cache = 0;
+  bwagpu_samcache_t *caches[2] = {0, 0};
+  clearer_t clr[2];
+  memset(clr, 0, sizeof clr);
   /* gpuchain: the SAM cache on a context of its own (the feeder thread's
      records run on ctx meanwhile) */
   bwagpu_ctx_t *ctx_sam = ctx;
@@ -883,7 +918,8 @@ int main(int argc, char *argv[])
   }
   /* first-launch capacities sized for short reads (2x150: a handful of CIGAR
      ops, MD well under 128 bytes); the rare longer ones are re-run with room */
-  if (is_sam && G.sc_create(ctx_sam, 16, 128, &cache)) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
+  for (int k = 0; k < 2 && is_sam; ++k)
+    if (G.sc_create(ctx_sam, 16, 128, &caches[k])) { fprintf(stderr, "bwagpu_samcache_create failed\n"); return 3; }
   int64_t n_passes = 0;
 
   FILE *out = fopen(outp, "w");
@@ -937,10 +973,11 @@ int main(int argc, char *argv[])
       mem_pestat(opt, idx->bns->l_pac, n, w.regs, pes);
       g_t_pestat += realtime() - tq;
       w.pes = pes;
-      sam_passes(cache, &w, n, T, &n_passes, &t_flush);
+      clearer_join(&clr[b & 1]);
+      sam_passes(caches[b & 1], &w, n, T, &n_passes, &t_flush);
+      clearer_start(&clr[b & 1], caches[b & 1], w.regs, n);
       t_sam += realtime() - t0;
       free(w.chn);
-      free(w.regs);
       feeder_done(&fd);
     } else if (is_ref) {
       t0 = realtime();
@@ -966,11 +1003,16 @@ int main(int argc, char *argv[])
       mem_pestat(opt, idx->bns->l_pac, n, w.regs, pes);
       g_t_pestat += realtime() - tq;
       w.pes = pes;
-      if (is_sam) sam_passes(cache, &w, n, T, &n_passes, &t_flush);
-      else kt_for(T, w_sam, &w, n >> 1);
+      if (is_sam) {
+        clearer_join(&clr[b & 1]);
+        sam_passes(caches[b & 1], &w, n, T, &n_passes, &t_flush);
+        clearer_start(&clr[b & 1], caches[b & 1], w.regs, n);
+      } else {
+        kt_for(T, w_sam, &w, n >> 1);
+        free(w.regs);
+      }
       t_sam += realtime() - t0;
       free(w.chn);
-      free(w.regs);
     }
     const double t_o = realtime();
     writer_put(&wr, seqs, n); /* waits for the previous batch's output */
@@ -995,7 +1037,14 @@ int main(int argc, char *argv[])
   fclose(out);
   t_all = realtime() - t_all;
   int64_t st[8] = {0};
-  if (cache) G.sc_stats(cache, st);
+  clearer_join(&clr[0]);
+  clearer_join(&clr[1]);
+  for (int k = 0; k < 2; ++k)
+    if (caches[k]) {
+      int64_t s2[8];
+      G.sc_stats(caches[k], s2);
+      for (int i = 0; i < 8; ++i) st[i] += s2[i];
+    }
   fprintf(stderr, "{\"mode\": \"%s\", \"reads\": %ld, \"threads\": %d, \"seed_s\": %.4f, \"ext_s\": %.4f, "
                   "\"sam_s\": %.4f, \"flush_s\": %.4f, \"sam_passes\": %ld, \"align2_calls\": %ld, "
                   "\"reg2aln_calls\": %ld, \"seed_device_s\": %.4f, \"post_s\": %.4f, \"out_s\": %.4f, \"ext_flat_s\": %.4f, "
@@ -1003,7 +1052,8 @@ int main(int argc, char *argv[])
                   "\"clear_s\": %.4f, \"pestat_s\": %.4f, \"feeder_s\": %.4f, \"total_s\": %.4f}\n",
           mode, (long)n_processed, T, t_seed, t_ext, t_sam, t_flush, (long)n_passes, (long)st[4], (long)st[5],
           t_seed_dev, t_post, t_out, g_t_flat, g_t_call, g_t_unflat, g_t_pass[0], g_t_pass[1], g_t_pass[2], g_t_clear, g_t_pestat, fd.t_busy, t_all);
-  if (cache) G.sc_destroy(cache);
+  for (int k = 0; k < 2; ++k)
+    if (caches[k]) G.sc_destroy(caches[k]);
   if (ctx_sam && ctx_sam != ctx) G.destroy(ctx_sam);
   if (ctx) G.destroy(ctx);
   free(all);
