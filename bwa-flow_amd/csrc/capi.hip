@@ -163,6 +163,7 @@ struct bwagpu_ctx {
   DevBuf ch_ocoff, ch_osoff, ch_rco, ch_cso, ch_rid, ch_cfrac, ch_out, ch_seeds;
   DevBuf ch_regoff, ch_regc;
   HostBuf chh_tot, chh_rco, chh_cso, chh_chains, chh_seeds, chh_regs, chh_n;
+  HostBuf sdh_in;  // the reads of a seeding call, staged for the H2D
   Slot ch_slot;  // chain2aln scratch of bwagpu_seqs2regions
   ChainStreams ch_cs{};  // created on first use
   bool has_alt = false;
@@ -367,7 +368,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
                     &ctx->ch_cso, &ctx->ch_rid, &ctx->ch_cfrac, &ctx->ch_out, &ctx->ch_seeds, &ctx->ch_regoff,
                     &ctx->ch_regc})
     b->release();
-  for (HostBuf* b : {&ctx->chh_tot, &ctx->chh_rco, &ctx->chh_cso, &ctx->chh_chains, &ctx->chh_seeds, &ctx->chh_regs,
+  for (HostBuf* b : {&ctx->sdh_in, &ctx->chh_tot, &ctx->chh_rco, &ctx->chh_cso, &ctx->chh_chains, &ctx->chh_seeds, &ctx->chh_regs,
                      &ctx->chh_n})
     b->release();
   if (ctx->own_pac && ctx->d_pac) (void)hipFree(ctx->d_pac);
@@ -1560,22 +1561,42 @@ int seed_validate(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_read
   if (n_reads == 0) return BWAGPU_OK;
   const int64_t nb = seq_off[n_reads] - seq_off[0];
   if (seq_off[0] != 0 || nb < 0 || (nb && !seq)) return fail(ctx, BWAGPU_E_INVAL, "seq_off must start at 0");
-  for (int32_t r = 0; r < n_reads; ++r) {
-    const int64_t l = seq_off[r + 1] - seq_off[r];
-    if (l < 0) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
-    if (l > BWAGPU_MAX_SEED_READ) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_SEED_READ");
-  }
-  {  // every base is nt4 (0..4): eight bytes at a time, (b & 0x7f) + 0x7b carries into bit 7 iff b > 4
-    int64_t i = 0;
+  // the read lengths and every base (nt4: 0..4), on up to 8 threads for a
+  // batch of megabases (one thread takes ~1 ms per 10 Mbases)
+  const int nt = nb >= (1 << 22) ? 8 : 1;
+  int len_bad[8] = {}, base_bad[8] = {};
+  auto part = [&](int t) {
+    for (int32_t r = (int32_t)((int64_t)n_reads * t / nt); r < (int32_t)((int64_t)n_reads * (t + 1) / nt); ++r) {
+      const int64_t l = seq_off[r + 1] - seq_off[r];
+      if (l < 0) len_bad[t] |= 1;
+      if (l > BWAGPU_MAX_SEED_READ) len_bad[t] |= 2;
+    }
+    // eight bytes at a time: (b & 0x7f) + 0x7b carries into bit 7 iff b > 4
+    int64_t i = (nb * t / nt) & ~(int64_t)7;
+    const int64_t e = t == nt - 1 ? nb : (nb * (t + 1) / nt) & ~(int64_t)7;
     uint64_t bad = 0;
-    for (; i + 8 <= nb; i += 8) {
+    for (; i + 8 <= e; i += 8) {
       uint64_t w;
       memcpy(&w, seq + i, 8);
       bad |= (((w & 0x7f7f7f7f7f7f7f7fULL) + 0x7b7b7b7b7b7b7b7bULL) | w) & 0x8080808080808080ULL;
     }
-    for (; i < nb; ++i) bad |= seq[i] > 4;
-    if (bad) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
+    for (; i < e; ++i) bad |= seq[i] > 4;
+    base_bad[t] = bad != 0;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
   }
+  int lb = 0, bb = 0;
+  for (int t = 0; t < nt; ++t) {
+    lb |= len_bad[t];
+    bb |= base_bad[t];
+  }
+  if (lb & 1) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
+  if (lb & 2) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_SEED_READ");
+  if (bb) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
   *bases = nb;
   return BWAGPU_OK;
 }
@@ -1589,10 +1610,22 @@ int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads
   HIPC(ctx->sd_out.ensure(sizeof(bwagpu_intv_t) * (size_t)n_reads * (size_t)max_per_read), "hipMalloc");
   HIPC(ctx->sd_n.ensure(sizeof(int32_t) * (size_t)n_reads), "hipMalloc");
   HIPC(ctx->sd_scratch.ensure(sizeof(bwagpu_intv_t) * (size_t)seed_scratch_entries(bases, n_reads)), "hipMalloc");
-  if (upload) {
-    HIPC(hipMemcpyAsync(ctx->sd_off.p, seq_off, sizeof(int64_t) * ((size_t)n_reads + 1), hipMemcpyHostToDevice, st),
-         "H2D");
-    if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, seq, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
+  if (upload) {  // through a pinned staging buffer filled on a few threads (a pageable H2D runs at a fraction)
+    const size_t ob = sizeof(int64_t) * ((size_t)n_reads + 1);
+    HIPC(ctx->sdh_in.ensure(ob + (size_t)bases), "hipHostMalloc");
+    char* const pin = ctx->sdh_in.as<char>();
+    const int nt = bases >= (1 << 22) ? 8 : 1;
+    auto part = [&](int t) {
+      const size_t b0 = (size_t)bases * t / nt, b1 = (size_t)bases * (t + 1) / nt;
+      memcpy(pin + ob + b0, seq + b0, b1 - b0);
+      if (t == 0) memcpy(pin, seq_off, ob);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+    HIPC(hipMemcpyAsync(ctx->sd_off.p, pin, ob, hipMemcpyHostToDevice, st), "H2D");
+    if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, pin + ob, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
   }
   a = SeedArgs{};
   a.n_reads = n_reads;
@@ -1892,10 +1925,8 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
   HIPC(launch_chain_emit(a, st), "chain_emit launch");
   if (P) HIPC(launch_bwt_sa(ctx->bwt, P, a.kpos, a.rbeg, st), "bwt_sa launch");
   if (!ctx->ch_cs.fork) {
-    for (int k = 0; k < 2; ++k) {
-      HIPC(hipStreamCreateWithFlags(&ctx->ch_cs.side[k], hipStreamNonBlocking), "hipStreamCreate");
-      HIPC(hipEventCreateWithFlags(&ctx->ch_cs.join[k], hipEventDisableTiming), "hipEventCreate");
-    }
+    HIPC(hipStreamCreateWithFlags(&ctx->ch_cs.side[0], hipStreamNonBlocking), "hipStreamCreate");
+    HIPC(hipEventCreateWithFlags(&ctx->ch_cs.join[0], hipEventDisableTiming), "hipEventCreate");
     HIPC(hipEventCreateWithFlags(&ctx->ch_cs.fork, hipEventDisableTiming), "hipEventCreate");
   }
   const char* dbg_env = getenv("BWAGPU_CHAIN_PHASES");

@@ -135,6 +135,46 @@ struct Tree {
     }
   }
 
+  // lower() that also remembers where kb_putp would insert pos: when the
+  // descent reached a leaf and no node on it is full, kb_putp's own descent
+  // (the same finds on the same nodes, no split on the way) ends at that leaf
+  // after key index `leaf_i` — put_at() then inserts there without a second
+  // walk from the root.  Otherwise leaf = -1 and put() walks.
+  __device__ int lower_at(int64_t pos, int& leaf, int& leaf_i) const {
+    int lo = -1, r = 0, key;
+    bool full = false;
+    leaf = -1;
+    for (int x = root;;) {
+      const int i = find(x, pos, r, key);
+      full = full || nd[x].n == kBN;
+      if (i >= 0 && r == 0) return key;
+      if (i >= 0) lo = key;
+      if (!nd[x].internal) {
+        if (!full) {
+          leaf = x;
+          leaf_i = i;
+        }
+        return lo;
+      }
+      x = nd[x].child[i + 1];
+    }
+  }
+
+  __device__ void put_at(int k, int x, int i) {  // kb_putp's leaf insertion (kbtree.h:186-195)
+    const int lane = (int)(threadIdx.x & 63);
+    ++n_keys;
+    const int xn = nd[x].n;
+    int kv = 0;
+    const bool mv = lane > i && lane < xn;  // keys i+1..xn-1 move up one
+    if (mv) kv = nd[x].key[lane];
+    wave_sync();
+    if (mv) nd[x].key[lane + 1] = kv;
+    wave_sync();
+    nd[x].key[i + 1] = k;
+    nd[x].n = xn + 1;
+    wave_sync();
+  }
+
   __device__ void split(int x, int i, int y) {  // __kb_split (kbtree.h:152-167)
     const int lane = (int)(threadIdx.x & 63);
     const int z = n_nodes++;
@@ -391,8 +431,9 @@ __device__ void chain_read(const ChainArgs& a, int r, CH* ch, ND* nd, IX* label,
     int lab = -1;
     if (rid >= 0) {
       bool add = true;
+      int leaf = -1, leaf_i = 0;
       if (t.n_keys) {
-        const int lo = t.lower(sr);
+        const int lo = t.lower_at(sr, leaf, leaf_i);
         if (lo >= 0) {
           // test_and_merge (bwamem.c:199-221)
           const int64_t c_last_rbeg = ch[lo].last_rbeg, c_s0_rbeg = ch[lo].s0_rbeg;
@@ -445,7 +486,8 @@ __device__ void chain_read(const ChainArgs& a, int r, CH* ch, ND* nd, IX* label,
         c->first = -1;
         c->w = 0;
         lab = n_ch;
-        t.put(n_ch++, sr);
+        if (leaf >= 0) t.put_at(n_ch++, leaf, leaf_i);
+        else t.put(n_ch++, sr);
       }
     }
     label[p] = lab;
@@ -903,14 +945,15 @@ hipError_t launch_chain_build(const ChainArgs& a, hipStream_t st, const ChainStr
   hipLaunchKernelGGL(chain_bin_kernel, lanes(a.n_reads), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the bins run side by side (the heavy reads' bins are long, serial walks):
-  // bin 3 on st, bin 2 and the global bin on side[0], bins 0-1 on side[1];
+  // bin 3 (the longest) on st, bins 2, 0, 1 and the global bin after one
+  // another on ONE side stream (with more streams than the process's hardware
+  // queues, a second side stream shared st's queue and waited behind bin 3);
   // bin counts stay on the device: each launch's workgroups stride over its
   // bin's list (a resident-size grid for the small bins, fewer for the big)
   if ((e = hipEventRecord(cs.fork, st)) != hipSuccess) return e;
-  for (int k = 0; k < 2; ++k)
-    if ((e = hipStreamWaitEvent(cs.side[k], cs.fork, 0)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(cs.side[0], cs.fork, 0)) != hipSuccess) return e;
   const int grid[kLdsBins + 1] = {8192, 2048, 512, 256, 256};
-  const hipStream_t on[kLdsBins] = {cs.side[1], cs.side[1], cs.side[0], st};
+  const hipStream_t on[kLdsBins] = {cs.side[0], cs.side[0], cs.side[0], st};
 #define BUILD_BIN(B)                                                                                         \
   hipLaunchKernelGGL(chain_build_lds_kernel<B>, dim3(grid[B]), dim3(64), lds_arena(kBinCap[B]), on[B], a); \
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -918,11 +961,8 @@ hipError_t launch_chain_build(const ChainArgs& a, hipStream_t st, const ChainStr
 #undef BUILD_BIN
   hipLaunchKernelGGL(chain_build_glb_kernel, dim3(grid[kLdsBins]), dim3(64), 0, cs.side[0], a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  for (int k = 0; k < 2; ++k) {
-    if ((e = hipEventRecord(cs.join[k], cs.side[k])) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(st, cs.join[k], 0)) != hipSuccess) return e;
-  }
-  return hipSuccess;
+  if ((e = hipEventRecord(cs.join[0], cs.side[0])) != hipSuccess) return e;
+  return hipStreamWaitEvent(st, cs.join[0], 0);
 }
 
 hipError_t launch_chain_sw_prep(const ChainArgs& a, const ChainSw& s, hipStream_t st) {

