@@ -290,14 +290,20 @@ class Engine:
 
     def collect_intv(self, seq_off: np.ndarray, seq: np.ndarray, min_seed_len: int = 19, split_width: int = 10,
                      max_mem_intv: int = 20, split_factor: float = 1.5, max_per_read: int = 256,
-                     out_cap: int | None = None):
-        """mem_collect_intv (bwa/bwamem.c:120-167) per read -> (counts int32[n], intervals INTV_DTYPE[sum])"""
+                     out_cap: int | None = None, out: np.ndarray | None = None):
+        """mem_collect_intv (bwa/bwamem.c:120-167) per read -> (counts int32[n], intervals INTV_DTYPE[sum]);
+        out: the caller's INTV_DTYPE buffer to fill (reused across calls; its length is the capacity)"""
         seq_off = np.ascontiguousarray(seq_off, np.int64)
         seq = np.ascontiguousarray(seq, np.uint8)
         n = len(seq_off) - 1
         o = abi.SeedOpt(min_seed_len, split_width, max_mem_intv, split_factor)
-        cap = max(n, 1) * max_per_read if out_cap is None else out_cap
-        out = np.zeros(max(cap, 1), abi.INTV_DTYPE)
+        if out is not None:
+            if out.dtype != abi.INTV_DTYPE or not out.flags.c_contiguous:
+                raise ValueError("out must be a contiguous INTV_DTYPE array")
+            cap = len(out)
+        else:
+            cap = max(n, 1) * max_per_read if out_cap is None else out_cap
+            out = np.zeros(max(cap, 1), abi.INTV_DTYPE)
         cnt = np.zeros(max(n, 1), np.int32)
         self._check(self.lib.bwagpu_collect_intv(self.ctx, C.byref(o), n, _ptr(seq_off), _ptr(seq), max_per_read,
                                                  _ptr(out), cap, _ptr(cnt)), "collect_intv")
