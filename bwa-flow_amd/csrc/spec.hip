@@ -1459,6 +1459,8 @@ __global__ void __launch_bounds__(kBlock) spec_pairs_kernel(DevOpt o, DevBatch b
   }
 }
 
+__device__ __forceinline__ uint64_t lane64(uint64_t v, int l) { return (uint64_t)readlane64((int64_t)v, l); }
+
 constexpr int kScanLds = 64 * 1024;  // a read's C and O matrices staged in LDS when they fit
 
 // The final pass over a heavy read computes a missing extension INLINE (the
@@ -1563,38 +1565,71 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
       computed_w = r == w ? cm : computed_w;
       skip_w = r == w ? km : skip_w;
     }
+    // Blocks of 64 seeds: the tests of seed k against the regions and skips of
+    // the earlier blocks (final by then) run lane-parallel, lane r for seed
+    // 64 * bw + r over its row's earlier words; only the in-block word is
+    // decided seed by seed, on scalar masks.  (One seed per step cost ~256 ns:
+    // a dependent row load, a ballot and a branch per seed.)
     uint64_t ext_w = 0, pend_w = 0;
     int miss = -1;
-    for (int k = 0; k < ns; ++k) {
-      const int kw = k >> 6;
-      const uint64_t kbit = 1ull << (k & 63);
-      const uint64_t pres = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(present_w >> 32), kw) << 32 |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)present_w, kw);
-      if (!(pres & kbit)) continue;
-      const int nwk = (k + 63) >> 6;  // words of row k
-      const uint64_t cw = r < nwk ? C[tri_off(k) + r] : 0;
-      if (__builtin_amdgcn_ballot_w64((cw & ext_w) != 0)) {
-        const uint64_t ow = r < nwk ? O[tri_off(k) + r] : 0;
-        if (!__builtin_amdgcn_ballot_w64((ow & ~skip_w) != 0)) {  // skipped: srt[k] = 0 (bwamem.c:709)
-          skip_w |= r == kw ? kbit : 0;
-          continue;
+    for (int bw = 0; bw < nw && miss < 0; ++bw) {
+      const int kb = 64 * bw, k = kb + r;
+      const bool valid = k < ns;
+      const int64_t row = tri_off(valid ? k : ns - 1);
+      bool cb = false;
+      for (int w = 0; w < bw; ++w) cb |= (C[row + w] & lane64(ext_w, w)) != 0;
+      uint64_t cin = valid && r > 0 ? C[row + bw] : 0;
+      // O matters only where a region contains seed k
+      bool need = valid && (cb || cin != 0), ob = false;
+      uint64_t oin = 0;
+      if (__builtin_amdgcn_ballot_w64(need)) {
+        if (need) {
+          for (int w = 0; w < bw; ++w) ob |= (O[row + w] & ~lane64(skip_w, w)) != 0;
+          oin = r > 0 ? O[row + bw] : 0;
         }
       }
-      const uint64_t comp = (uint64_t)__builtin_amdgcn_readlane((uint32_t)(computed_w >> 32), kw) << 32 |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)computed_w, kw);
-      if (!(comp & kbit)) {
-        if (MODE == SEL_EMULATE) {
-          pend_w |= r == kw ? kbit : 0;  // a round-B task; its region stays unknown
-          continue;
+      const uint64_t cbm = __builtin_amdgcn_ballot_w64(valid && cb);
+      uint64_t obm = __builtin_amdgcn_ballot_w64(valid && ob);
+      const uint64_t pres = lane64(present_w, bw);
+      uint64_t comp = lane64(computed_w, bw), skp = lane64(skip_w, bw), ext = 0, pend = 0;
+      const int nb = min(64, ns - kb);
+      for (int i = 0; i < nb; ++i) {
+        const uint64_t bit = 1ull << i;
+        if (!(pres & bit)) continue;
+        if ((cbm & bit) || (lane64(cin, i) & ext)) {
+          if (!(obm & bit) && !(lane64(oin, i) & ~skp)) {  // skipped: srt[k] = 0 (bwamem.c:709)
+            skp |= bit;
+            continue;
+          }
         }
-        if (d.lq > kSpecBinLen[0]) {  // longer reads: round C + the redo pass
-          miss = k;
-          break;
+        if (!(comp & bit)) {
+          if (MODE == SEL_EMULATE) {
+            pend |= bit;  // a round-B task; its region stays unknown
+            continue;
+          }
+          if (d.lq > kSpecBinLen[0]) {  // longer reads: round C + the redo pass
+            miss = kb + i;
+            break;
+          }
+          heavy_fill_missing(o, ref, b, a, d, kb + i, ns, C, tbl, tbr);
+          comp |= bit;
+          cin = valid && r > 0 ? C[row + bw] : 0;  // column kb + i of the later rows
+          const bool fresh = valid && !need && cin != 0;
+          if (__builtin_amdgcn_ballot_w64(fresh)) {
+            if (fresh) {
+              for (int w = 0; w < bw; ++w) ob |= (O[row + w] & ~lane64(skip_w, w)) != 0;
+              oin = O[row + bw];
+            }
+            need = need || fresh;
+            obm = __builtin_amdgcn_ballot_w64(valid && ob);
+          }
         }
-        heavy_fill_missing(o, ref, b, a, d, k, ns, C, tbl, tbr);
-        computed_w |= r == kw ? kbit : 0;
+        ext |= bit;
       }
-      ext_w |= r == kw ? kbit : 0;
+      ext_w = r == bw ? ext : ext_w;
+      skip_w = r == bw ? skp : skip_w;
+      pend_w = r == bw ? pend : pend_w;
+      computed_w = r == bw ? comp : computed_w;
     }
     int nreg = 0;
     if constexpr (MODE == SEL_EMULATE) {
