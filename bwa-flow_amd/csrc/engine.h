@@ -213,7 +213,8 @@ struct SpecStreams {
   int pool_n = 0;
   int* pool_used = nullptr;
 };
-// bwagpu_debug_ext_form: 0 = four seeds per wave where the scores fit (default), 1 = two per wave
+// bwagpu_debug_ext_form: 0 = eight / four seeds per wave where the scores fit (default), 1 = two per
+// wave, 2 = four per wave
 int set_ext_form(int form);
 bool quad_scores_ok(const DevOpt& o, int lq);
 bool quad_bound_ok(const DevOpt& o, long hb);

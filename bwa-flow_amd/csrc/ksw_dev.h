@@ -684,12 +684,15 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t mov0(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
-// inclusive max-scan over each 32-lane half of packed values >= 0 (identity 0)
-__device__ __forceinline__ uint32_t half_scan_umax(uint32_t x) {
+// inclusive max-scan over each G-lane group (G = 16: a DPP row, 32: a half)
+// of packed values >= 0 (identity 0)
+template <int G>
+__device__ __forceinline__ uint32_t grp_scan_umax(uint32_t x) {
   x = umax(x, mov0<DPP_ROW_SHR(1)>(x));
   x = umax(x, mov0<DPP_ROW_SHR(2)>(x));
   x = umax(x, mov0<DPP_ROW_SHR(4)>(x));
   x = umax(x, mov0<DPP_ROW_SHR(8)>(x));
+  if constexpr (G == 16) return x;
   // rows 1 / 3 take the last lane of rows 0 / 2; rows 0 / 2 an identity 0
   const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142 /* row_bcast:15 */, 0xA, 0xF, false);
   return umax(x, t);
@@ -703,9 +706,10 @@ __device__ __forceinline__ uint32_t half_umin(uint32_t x) {
   const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
   return umin((uint32_t)p[0], (uint32_t)p[1]);
 }
-// the half's umax of K, umin of L and smax of H at once: three independent
+// the group's umax of K, umin of L and smax of H at once: three independent
 // chains step by step, so no DPP read waits on the write just before it
-__device__ __forceinline__ void half_red3(uint32_t& K, uint32_t& L, uint32_t& H) {
+template <int G>
+__device__ __forceinline__ void grp_red3(uint32_t& K, uint32_t& L, uint32_t& H) {
 #define RED3_STEP(CTRL)                                                                  \
   {                                                                                      \
     const uint32_t k = (uint32_t)__builtin_amdgcn_mov_dpp((int)K, CTRL, 0xF, 0xF, false); \
@@ -720,6 +724,7 @@ __device__ __forceinline__ void half_red3(uint32_t& K, uint32_t& L, uint32_t& H)
   RED3_STEP(DPP_ROW_ROR(2))
   RED3_STEP(DPP_ROW_ROR(1))
 #undef RED3_STEP
+  if constexpr (G == 16) return;  // a DPP row: done
   const auto pk_ = __builtin_amdgcn_permlane16_swap(K, K, false, false);
   const auto pl = __builtin_amdgcn_permlane16_swap(L, L, false, false);
   const auto ph = __builtin_amdgcn_permlane16_swap(H, H, false, false);
@@ -762,14 +767,18 @@ __device__ __forceinline__ QCall quad_idle(const uint8_t* seq, const uint8_t* tb
 
 // K8: the row-max key is H << 8 | j, packed, one reduction for both calls
 // (every H < 256: quad_key8_ok); else H << KS | c widened to H << 10 | j per call.
-template <int CPL, bool K8>
+// G = the lanes of a group (two calls): 32 (four calls per wave) or 16 (eight
+// calls per wave, K8 only: every scan and reduction stays inside a DPP row).
+template <int G, int CPL, bool K8>
 __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa, ExtOut& xb,
                                             Tally32& ta, Tally32& tbl) {
   using namespace pk16;
-  int r;  // the lane index behind an opaque move (see extend_pair)
-  asm volatile("v_and_b32 %0, 31, %1" : "=v"(r) : "v"((int)threadIdx.x));
+  static_assert(G == 32 || (G == 16 && K8), "eight calls per wave: the 8-bit key form only");
+  int r;  // the lane index in its group, behind an opaque move (see extend_pair)
+  if constexpr (G == 16) asm volatile("v_and_b32 %0, 15, %1" : "=v"(r) : "v"((int)threadIdx.x));
+  else asm volatile("v_and_b32 %0, 31, %1" : "=v"(r) : "v"((int)threadIdx.x));
   constexpr int KS = CPL <= 2 ? 1 : (CPL <= 4 ? 2 : (CPL <= 8 ? 3 : 4));  // in-lane column bits of the key
-  static_assert(CPL >= 1 && CPL <= 8, "four extensions per wave: CPL <= 8");
+  static_assert(CPL >= 1 && CPL * G <= 256, "columns per call: < 256 (16-bit j, 8-bit key)");
   const int e_del = o.e_del, e_ins = o.e_ins, oe_ins = o.oe_ins;
   const int j0 = r * CPL;
   const uint32_t J0 = pk(j0, j0);
@@ -842,9 +851,14 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       AA[c] = umin(sub(mb, MB_OE), CAP[c]);
       T = smax(usat(T, EI1), AA[c]);
     }
-    const uint32_t sx = half_scan_umax(add(T, RE2));
-    uint32_t EX = mov0<DPP_WAVE_SHR1>(sx);
-    EX = r == 0 ? 0u : EX;  // lanes 0 and 32: no column to the left in the half
+    const uint32_t sx = grp_scan_umax<G>(add(T, RE2));
+    uint32_t EX;
+    if constexpr (G == 16) {
+      EX = mov0<DPP_ROW_SHR(1)>(sx);  // a row's lane 0 reads 0: no column to its left
+    } else {
+      EX = mov0<DPP_WAVE_SHR1>(sx);
+      EX = r == 0 ? 0u : EX;  // lanes 0 and 32: no column to the left in the half
+    }
     uint32_t f = usat(EX, RE);
     uint32_t LK = 0, H1Q = 0, hm[CPL];
 #pragma unroll
@@ -861,8 +875,13 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       if (c > 0) hh[c] = sel(R[c], hm[c - 1], hh[c]);
       H1Q |= hm[c] & qm[c];
     }
-    uint32_t hs0 = mov0<DPP_WAVE_SHR1>(hm[CPL - 1]);  // H(i, j0 - 1)
-    hs0 = r == 0 ? LEFT0 : hs0;
+    uint32_t hs0;  // H(i, j0 - 1); the group's first lane: the first-column value
+    if constexpr (G == 16) {
+      hs0 = (uint32_t)__builtin_amdgcn_update_dpp((int)LEFT0, (int)hm[CPL - 1], DPP_ROW_SHR(1), 0xF, 0xF, false);
+    } else {
+      hs0 = mov0<DPP_WAVE_SHR1>(hm[CPL - 1]);
+      hs0 = r == 0 ? LEFT0 : hs0;
+    }
     hh[0] = sel(R[0], hs0, hh[0]);
     // band trim candidates: first non-zero column >= lo, last non-zero <= hi
     uint32_t CL = 0x7fff7fffu, CH = 0xffffffffu;
@@ -881,7 +900,7 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     uint32_t MROW, MJ;
     if constexpr (K8) {
       uint32_t K = LK;
-      half_red3(K, CL, CH);
+      grp_red3<G>(K, CL, CH);
       MROW = W(U(K) >> (u16x2){8, 8});
       MJ = K & 0x00ff00ffu;
     } else {
@@ -924,7 +943,7 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     HI = smin(add(smax(CH, sub(NLO, ONE)), pk(2, 2)), QL);
   }
   // gscore / max_ie from the owner of column qlen-1 of each call
-  const int hb = (int)(threadIdx.x & 32);
+  const int hb = (int)(threadIdx.x & (64 - G));  // the group's first lane
   const uint32_t ea = __shfl(pk(lo16(EI), lo16(ESC)), hb + (A.qlen - 1) / CPL, 64);
   const uint32_t eb = __shfl(pk(hi16(EI), hi16(ESC)), hb + (Bc.qlen - 1) / CPL, 64);
   xa = ExtOut{lo16(BEST), lo16(BJ) + 1, lo16(BI) + 1, lo16(ea) + 1, hi16(ea), lo16(OFF)};
@@ -937,16 +956,19 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   tbl.calls += 1;
 }
 
-// CPL = ceil((qlen+1)/32) of the wave's longest active call (all four run one body)
-template <int PMAX, bool K8>
+// CPL = ceil((qlen+1)/G) of the wave's longest active call (all run one body)
+template <int G, int PMAX, bool K8>
 __device__ __forceinline__ void extend_quad_dispatch(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa,
                                                      ExtOut& xb, Tally32& ta, Tally32& tbl) {
-  const int qm = max(max(__builtin_amdgcn_readlane(A.qlen, 0), __builtin_amdgcn_readlane(Bc.qlen, 0)),
-                     max(__builtin_amdgcn_readlane(A.qlen, 32), __builtin_amdgcn_readlane(Bc.qlen, 32)));
-  const int cpl = (qm + 32) >> 5;
+  int qm = 0;
+#pragma unroll
+  for (int g = 0; g < 64; g += G)
+    qm = max(qm, max(__builtin_amdgcn_readlane(A.qlen, g), __builtin_amdgcn_readlane(Bc.qlen, g)));
+  const int cpl = (qm + G) / G;
 #define EXT_QUAD(n) \
-  if (n <= PMAX && cpl == n) return extend_quad<(n <= PMAX ? n : 1), K8>(o, A, Bc, xa, xb, ta, tbl);
-  EXT_QUAD(1) EXT_QUAD(2) EXT_QUAD(3) EXT_QUAD(4) EXT_QUAD(5) EXT_QUAD(6) EXT_QUAD(7) EXT_QUAD(8)
+  if (n <= PMAX && cpl == n) return extend_quad<G, (n <= PMAX ? n : 1), K8>(o, A, Bc, xa, xb, ta, tbl);
+  EXT_QUAD(1) EXT_QUAD(2) EXT_QUAD(3) EXT_QUAD(4) EXT_QUAD(5) EXT_QUAD(6) EXT_QUAD(7) EXT_QUAD(8) EXT_QUAD(9)
+  EXT_QUAD(10)
 #undef EXT_QUAD
 }
 

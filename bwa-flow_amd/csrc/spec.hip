@@ -263,12 +263,13 @@ __global__ void __launch_bounds__(kBlock) spec_ext_kernel(DevOpt o, DevRef ref, 
 //
 // Both target windows of the half's seed into its LDS rows (fill_two on 32
 // lanes: 4 loads per side per lane in flight, 128 rows per side per pass).
+template <int G = 32>
 __device__ __forceinline__ void fill_two_half(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
                                               const DevRef& ref) {
-  const int r = (int)(threadIdx.x & 31);
+  const int r = (int)(threadIdx.x & (G - 1));
   const int64_t two1 = (ref.l_pac << 1) - 1;
   const int n = max(nl, nr);
-  for (int base = 0; base < n; base += 128) {
+  for (int base = 0; base < n; base += 4 * G) {
     uint32_t raw[8];
     int sh[8], kk[8];
     bool rev[8];
@@ -276,7 +277,7 @@ __device__ __forceinline__ void fill_two_half(uint8_t* tbl, int64_t x0l, int nl,
     for (int m = 0; m < 8; ++m) {
       const bool left = m < 4;
       const int nn = left ? nl : nr;
-      const int k = min(base + (m & 3) * 32 + r, max(nn - 1, 0));
+      const int k = min(base + (m & 3) * G + r, max(nn - 1, 0));
       kk[m] = k;
       const int64_t x = left ? x0l - k : x0r + k;
       rev[m] = x >= ref.l_pac;
@@ -401,8 +402,10 @@ __device__ __forceinline__ SeedExt extend_seed2(const DevOpt& o, const DevRef& r
   return e;
 }
 
+template <int G = 32>
 __device__ __forceinline__ void store_ext_half(SeedExt* dst, const SeedExt& e) {
-  const int d = (int)(threadIdx.x & 31);
+  static_assert(G >= 12, "a SeedExt is 12 words");
+  const int d = (int)(threadIdx.x & (G - 1));
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&e);
   uint32_t v = 0;
 #pragma unroll
@@ -476,6 +479,7 @@ struct QTask {
 };
 
 // the task's seed, window and read; both target windows into the sub-slot's LDS rows
+template <int G>
 __device__ __forceinline__ void qtask_start(QTask& t, const DevOpt& o, const DevRef& ref, const DevBatch& b,
                                             const SpecArgs& a, int2 tk, uint8_t* tl, uint8_t* tr) {
   const int rd = a.chain_read[tk.y];
@@ -491,7 +495,7 @@ __device__ __forceinline__ void qtask_start(QTask& t, const DevOpt& o, const Dev
   t.len = s.len;
   const int qlenL = t.qbeg, qlenR = t.lq - (t.qbeg + t.len);
   const int64_t x0R = t.rbeg + t.len;
-  fill_two_half(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, (int)(t.rbeg - t.wlo), o.w << 1, o.pen_clip5) : 0, tr,
+  fill_two_half<G>(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, (int)(t.rbeg - t.wlo), o.w << 1, o.pen_clip5) : 0, tr,
                 x0R, qlenR ? rows_needed(o, qlenR, (int)(t.whi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
   t.phase = qlenL != 0 ? 0 : (qlenR != 0 ? 2 : 4);
   const int sc = qlenL != 0 ? -1 : t.len * o.a;  // bwamem.c:753
@@ -632,15 +636,18 @@ __device__ __forceinline__ QTask qload(LdsQ* p) {
   return t;
 }
 
-// Extension tasks of one list (in pair order, spec_sort_*), four per wave.
-// PMAX = the bin's largest CPL: ceil(read length / 32).
-template <int PMAX, bool K8>
+// Extension tasks of one list (in pair order, spec_sort_*), two per G-lane
+// group: four (G = 32) or eight (G = 16) per wave.
+// PMAX = the bin's largest CPL: ceil(read length / G).
+template <int G, int PMAX, bool K8>
 __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
                                                            int tb_bytes) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int hf = (int)(threadIdx.x >> 5) & 1;
-  // per half: A left, A right, B left, B right target rows, then A's and B's task states
-  uint8_t* const tal = lds + (size_t)(threadIdx.x >> 5) * (4 * (size_t)tb_bytes + 2 * kQTaskLds);
+  // the groups' first lanes, and those below this lane's group
+  constexpr uint64_t kLead = G == 16 ? 0x0001000100010001ull : 0x0000000100000001ull;
+  const uint64_t below = kLead & ((1ull << ((int)threadIdx.x & (64 - G))) - 1);
+  // per group: A left, A right, B left, B right target rows, then A's and B's task states
+  uint8_t* const tal = lds + (size_t)(threadIdx.x / G) * (4 * (size_t)tb_bytes + 2 * kQTaskLds);
   uint8_t* const tar = tal + tb_bytes;
   uint8_t* const tbl = tar + tb_bytes;
   uint8_t* const tbr = tbl + tb_bytes;
@@ -654,23 +661,23 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
   long long spec_cells = 0;
   for (;;) {
     if (more) {  // every sub-slot without a seed takes the next entry: one claim for the wave
-      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha), nb = __builtin_amdgcn_ballot_w64(!hb);
-      const int n0 = (int)(na & 1) + (int)(nb & 1), n1 = (int)((na >> 32) & 1) + (int)((nb >> 32) & 1);
-      if (n0 + n1 > 0) {
+      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha) & kLead, nb = __builtin_amdgcn_ballot_w64(!hb) & kLead;
+      const int nn = __popcll(na) + __popcll(nb);
+      if (nn > 0) {
         int m0, cap;
-        if (qq.claim(n0 + n1, m0, cap)) {
-          const int ia = m0 + (hf ? n0 : 0), ib = ia + (ha ? 0 : 1);
+        if (qq.claim(nn, m0, cap)) {
+          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (ha ? 0 : 1);
           if (!ha && ia < cap) {
             QTask t;
-            qtask_start(t, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
-            if (t.phase >= 4) store_ext_half(a.ext + t.pos, qtask_ext(t));  // a whole-read seed (bwamem.c:753, 781)
+            qtask_start<G>(t, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
+            if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));  // a whole-read seed (bwamem.c:753, 781)
             else qpark(qa, t);
             ha = t.phase < 4;
           }
           if (!hb && ib < cap) {
             QTask t;
-            qtask_start(t, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
-            if (t.phase >= 4) store_ext_half(a.ext + t.pos, qtask_ext(t));
+            qtask_start<G>(t, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
+            if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
             else qpark(qb, t);
             hb = t.phase < 4;
           }
@@ -696,11 +703,11 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
     }
     ExtOut xa, xb;
     Tally32 ta{0, 0, 0}, tb{0, 0, 0};
-    extend_quad_dispatch<PMAX, K8>(o, ca, cb, xa, xb, ta, tb);
+    extend_quad_dispatch<G, PMAX, K8>(o, ca, cb, xa, xb, ta, tb);
     if (ha) {
       QTask t = qload(qa);
       if (qtask_advance(t, o, xa, ta)) {
-        store_ext_half(a.ext + t.pos, qtask_ext(t));
+        store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
         spec_cells += t.cells;
         ha = false;
       } else {
@@ -710,7 +717,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
     if (hb) {
       QTask t = qload(qb);
       if (qtask_advance(t, o, xb, tb)) {
-        store_ext_half(a.ext + t.pos, qtask_ext(t));
+        store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
         spec_cells += t.cells;
         hb = false;
       } else {
@@ -718,12 +725,12 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
       }
     }
   }
-  if ((threadIdx.x & 31) == 0 && spec_cells)
+  if ((threadIdx.x & (G - 1)) == 0 && spec_cells)
     atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
 }
 
 // LDS bytes of a spec_ext4_kernel workgroup
-static size_t ext4_lds(int tb_bytes) { return (size_t)(kBlock / 32) * (4 * (size_t)tb_bytes + 2 * kQTaskLds); }
+static size_t ext4_lds(int tb_bytes, int g) { return (size_t)(kBlock / g) * (4 * (size_t)tb_bytes + 2 * kQTaskLds); }
 
 
 // Task order for the pair kernel: the two seeds a wave takes should need the
@@ -1720,15 +1727,16 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
   }
 }
 
-// The first two length bins' extension kernel: four seeds per wave
-// (spec_ext4_kernel, packed 16-bit DP) when every score of the bin fits the
-// packed ranges, else two per wave (spec_ext2_kernel, 32-bit).
-// bwagpu_debug_ext_form(1) forces two per wave (tests, A/B).
+// The first two length bins' extension kernel: eight seeds per wave for the
+// first bin and four for the second (spec_ext4_kernel, packed 16-bit DP) when
+// every score of the bin fits the packed ranges, else two per wave
+// (spec_ext2_kernel, 32-bit).  bwagpu_debug_ext_form(1) forces two per wave,
+// (2) four per wave in the first bin too (tests, A/B).
 static std::atomic<int> g_ext_form{0};
 int ext_form() { return g_ext_form.load(std::memory_order_relaxed); }
 int set_ext_form(int form) {  // process-wide; -> the previous form (form < 0: query only)
   const int prev = g_ext_form.load(std::memory_order_relaxed);
-  if (form >= 0) g_ext_form.store(form > 1 ? 1 : form, std::memory_order_relaxed);
+  if (form >= 0) g_ext_form.store(form > 2 ? 1 : form, std::memory_order_relaxed);
   return prev;
 }
 // the packed ranges (extend_quad) for reads up to lq: H <= lq * max(mat) < 4096
@@ -1763,23 +1771,29 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const int l = round * kSpecBins;
   const bool bin1 = lq_max > kSpecBinLen[0], bin2 = lq_max > kSpecBinLen[1];
   const auto grid = [round](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb); };
-  const bool quad = g_ext_form.load(std::memory_order_relaxed) == 0 && quad_scores_ok(o, kSpecBinLen[1]) &&
-                    quad_rows_ok(o, tb_bytes);
-  const size_t lds2 = quad ? ext4_lds(tb_bytes) : ext2_lds(tb_bytes);
-  // the first two length bins' lists in pair order (spec_sort_*), then two or
-  // four seeds per wave; the third (reads > 256 bp) one seed per wave
+  const int form = g_ext_form.load(std::memory_order_relaxed);
+  const bool quad = form != 1 && quad_scores_ok(o, kSpecBinLen[1]) && quad_rows_ok(o, tb_bytes);
+  const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]), oct = key8 && form == 0;
+  const size_t lds2 = quad ? ext4_lds(tb_bytes, 32) : ext2_lds(tb_bytes);
+  // the first two length bins' lists in pair order (spec_sort_*), then two,
+  // four or eight seeds per wave; the third (reads > 256 bp) one seed per wave
   hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
   hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
   hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  if (quad && quad_key8_ok(o, kSpecBinLen[0])) {
-    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[0] / 32, true>, lds2);
-    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[0] / 32, true>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
+  if (oct) {
+    const size_t lds8 = ext4_lds(tb_bytes, 16);
+    const int nb = resident_blocks(spec_ext4_kernel<16, kSpecBinLen[0] / 16, true>, lds8);
+    hipLaunchKernelGGL((spec_ext4_kernel<16, kSpecBinLen[0] / 16, true>), dim3(grid(nb)), dim3(kBlock), lds8, st, o,
+                       ref, b, a, l + 0, tb_bytes);
+  } else if (key8) {
+    const int nb = resident_blocks(spec_ext4_kernel<32, kSpecBinLen[0] / 32, true>, lds2);
+    hipLaunchKernelGGL((spec_ext4_kernel<32, kSpecBinLen[0] / 32, true>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 0, tb_bytes);
   } else if (quad) {
-    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32, false>, lds2);
-    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
+    const int nb = resident_blocks(spec_ext4_kernel<32, kSpecBinLen[1] / 32, false>, lds2);
+    hipLaunchKernelGGL((spec_ext4_kernel<32, kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 0, tb_bytes);
   } else {
     const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[0] / 32>, lds2);
@@ -1792,8 +1806,8 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   }
   if (!bin1) return;
   if (quad) {
-    const int nb = resident_blocks(spec_ext4_kernel<kSpecBinLen[1] / 32, false>, lds2);
-    hipLaunchKernelGGL((spec_ext4_kernel<kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
+    const int nb = resident_blocks(spec_ext4_kernel<32, kSpecBinLen[1] / 32, false>, lds2);
+    hipLaunchKernelGGL((spec_ext4_kernel<32, kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 1, tb_bytes);
   } else {
     const int nb = resident_blocks(spec_ext2_kernel<kSpecBinLen[1] / 32>, lds2);

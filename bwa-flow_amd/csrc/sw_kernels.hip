@@ -911,7 +911,7 @@ __global__ void __launch_bounds__(kBlock) extend4_kernel(DevOpt o, const bwagpu_
   while (__builtin_amdgcn_ballot_w64(ka >= 0 || kb >= 0)) {
     ExtOut xa, xb;
     Tally32 ta{0, 0, 0}, tb{0, 0, 0};
-    extend_quad_dispatch<PMAX, false>(o, ca, cb, xa, xb, ta, tb);
+    extend_quad_dispatch<32, PMAX, false>(o, ca, cb, xa, xb, ta, tb);
     if (ka >= 0) {
       if (r == 0) res[ka] = bwagpu_ext_result_t{xa.score, xa.qle, xa.tle, xa.gtle, xa.gscore, xa.max_off};
       cells += ta.cells;

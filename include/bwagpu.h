@@ -524,8 +524,9 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
 int bwagpu_debug_spec_ext(bwagpu_ctx_t *ctx, void *stream, void *host_out, int32_t n);
 int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
 /* tests / A-B (process-wide): the extension kernel of the first two read-length
-   bins — 0 (default) four seeds per wave with packed 16-bit DP where every
-   score of the bin fits (else two per wave), 1 two seeds per wave (32-bit DP);
+   bins — 0 (default) packed 16-bit DP where every score of the bin fits (else
+   two per wave): eight seeds per wave in the first bin, four in the second;
+   1 two seeds per wave (32-bit DP); 2 four seeds per wave in both bins;
    returns the previous form, form < 0 only queries.  Results do not depend on it. */
 int bwagpu_debug_ext_form(int form);
 int bwagpu_prof_intervals(bwagpu_ctx_t *ctx, double *start_ms, double *end_ms, int32_t max, int32_t *n);

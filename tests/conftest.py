@@ -19,7 +19,9 @@ def pytest_configure(config):
 def set_c2a_path(path, monkeypatch):
     """mem_chain2aln paths of the GPU tests:
       spec  the speculative extension tasks + selection passes, first two
-            read-length bins four seeds per wave (packed 16-bit DP, the default)
+            read-length bins with packed 16-bit DP (the default: eight seeds
+            per wave in the first bin, four in the second)
+      quad  the same with four seeds per wave in both bins (bwagpu_debug_ext_form(2))
       pair  the same with two seeds per wave (32-bit DP; bwagpu_debug_ext_form(1))
       fast  the per-read kernels (BWAGPU_C2A_PATH=fast: a wave per read), an
             independent implementation kept as a cross-check
@@ -30,5 +32,5 @@ def set_c2a_path(path, monkeypatch):
         monkeypatch.setenv("BWAGPU_C2A_PATH", "fast")
     else:
         monkeypatch.delenv("BWAGPU_C2A_PATH", raising=False)
-    prev = lib.bwagpu_debug_ext_form(1 if path == "pair" else 0)
+    prev = lib.bwagpu_debug_ext_form({"pair": 1, "quad": 2}.get(path, 0))
     return lambda: lib.bwagpu_debug_ext_form(prev)

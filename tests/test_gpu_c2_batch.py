@@ -21,7 +21,7 @@ from bwagpu.engine import Engine, compact
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not refseed.available(), reason="oracle/_ref/gen_golden not built")]
 
 
-@pytest.fixture(params=["spec", "pair", "fast"])
+@pytest.fixture(params=["spec", "quad", "pair", "fast"])
 def c2a_path(request, monkeypatch):
     restore = set_c2a_path(request.param, monkeypatch)
     yield request.param

@@ -35,7 +35,7 @@ def eng(c3):
     e.close()
 
 
-@pytest.mark.parametrize("path", ["spec", "pair", "fast"])
+@pytest.mark.parametrize("path", ["spec", "quad", "pair", "fast"])
 @pytest.mark.parametrize("name", ["c3", "c5"])
 def test_chain2aln_grch38(c3, eng, name, path, monkeypatch):
     restore = set_c2a_path(path, monkeypatch)
@@ -59,7 +59,7 @@ def test_reg2aln_grch38(c3, eng, name):
     assert len(np.unique(aln["rid"])) == 195
 
 
-@pytest.mark.parametrize("path", ["spec", "pair", "fast"])
+@pytest.mark.parametrize("path", ["spec", "quad", "pair", "fast"])
 def test_chain2aln_refseed_in_grch38(c3, path, monkeypatch):
     opt, g, s = workload.load_c3_refseed(grch=c3[1])
     e = Engine(0, opt, g.l_pac, g.ann_offset, g.ann_len, pac=g.pac)

@@ -27,7 +27,7 @@ def refd():
     return G.load_ref()
 
 
-@pytest.fixture(params=["spec", "pair", "fast"])
+@pytest.fixture(params=["spec", "quad", "pair", "fast"])
 def c2a_path(request, monkeypatch):
     """mem_chain2aln paths (conftest.set_c2a_path)"""
     restore = set_c2a_path(request.param, monkeypatch)

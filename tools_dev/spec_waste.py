@@ -43,4 +43,8 @@ for k, rb in enumerate(bs):
                         "cells_computed": int(sc[3]), "cells_reference": int(s[0]), "ext_calls_reference": int(s[2]),
                         "waste_frac": round(1 - s[0] / sc[3], 4), "redo_inline": int(sc[4]),
                         "heavy_reads": int(sc[5]), "redo_reads": int(sc[6])}
+    if sc[8]:  # a lib with tools_dev/ab/quad_occupancy_diag.patch: four-per-wave loop occupancy
+        loops, cols, rows = int(sc[8]), int(sc[9]), int(sc[10])
+        out[f"batch{k}"]["quad"] = {"wave_rows": loops, "call_rows": rows, "row_occupancy": round(rows / (4 * loops), 4),
+                                    "slot_cells": cols * 32 * 4, "cell_occupancy": round(sc[3] / (cols * 128), 4)}
 print(json.dumps(out))
