@@ -95,22 +95,33 @@ struct Tree {
   ND* nd;
   int root, n_nodes, n_keys;
 
+  // a node in registers, loaded in one round of independent LDS reads: lane l
+  // holds key[l] (l < kBN) and child[l] (l <= kBN)
+  struct Row {
+    int n, internal, k, c;
+  };
+  __device__ Row row(int x) const {
+    const int lane = (int)(threadIdx.x & 63);
+    Row v;
+    v.n = nd[x].n;
+    v.internal = nd[x].internal;
+    v.k = lane < kBN ? (int)nd[x].key[lane] : 0;
+    v.c = lane <= kBN ? (int)nd[x].child[lane] : 0;
+    return v;
+  }
+
   // first key >= pos (r = 0 if equal, else -1 after stepping back to the last
   // key < pos); past the end the last key with r = 1 (kbtree.h:100-113);
   // *key = the key at the returned index
-  __device__ int find(int x, int64_t pos, int& r, int& key) const {
+  __device__ int find(const Row& v, int64_t pos, int& r, int& key) const {
     const int lane = (int)(threadIdx.x & 63);
-    const int n = nd[x].n;
+    const int n = v.n;
     if (n == 0) {
       r = -1;
       return -1;
     }
-    int k = 0;
     int64_t kp = 0;
-    if (lane < n) {
-      k = nd[x].key[lane];
-      kp = ch[k].s0_rbeg;
-    }
+    if (lane < n) kp = ch[v.k].s0_rbeg;
     const int b = __builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < n && kp < pos));
     int i;
     if (b == n) {
@@ -120,18 +131,20 @@ struct Tree {
       r = pcmp(pos, readlane64(kp, b));
       i = r < 0 ? b - 1 : b;
     }
-    key = i >= 0 ? __builtin_amdgcn_readlane(k, i) : -1;
+    key = i >= 0 ? __builtin_amdgcn_readlane(v.k, i) : -1;
     return i;
   }
+  __device__ int find(int x, int64_t pos, int& r, int& key) const { return find(row(x), pos, r, key); }
 
   __device__ int lower(int64_t pos) const {  // kb_intervalp's lower (kbtree.h:130-147)
     int lo = -1, r = 0, key;
     for (int x = root;;) {
-      const int i = find(x, pos, r, key);
+      const Row v = row(x);
+      const int i = find(v, pos, r, key);
       if (i >= 0 && r == 0) return key;
       if (i >= 0) lo = key;
-      if (!nd[x].internal) return lo;
-      x = nd[x].child[i + 1];
+      if (!v.internal) return lo;
+      x = __builtin_amdgcn_readlane(v.c, i + 1);
     }
   }
 
@@ -145,18 +158,19 @@ struct Tree {
     bool full = false;
     leaf = -1;
     for (int x = root;;) {
-      const int i = find(x, pos, r, key);
-      full = full || nd[x].n == kBN;
+      const Row v = row(x);
+      const int i = find(v, pos, r, key);
+      full = full || v.n == kBN;
       if (i >= 0 && r == 0) return key;
       if (i >= 0) lo = key;
-      if (!nd[x].internal) {
+      if (!v.internal) {
         if (!full) {
           leaf = x;
           leaf_i = i;
         }
         return lo;
       }
-      x = nd[x].child[i + 1];
+      x = __builtin_amdgcn_readlane(v.c, i + 1);
     }
   }
 

@@ -822,7 +822,10 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   int cellsa = 0, cellsb = 0;
   int tna = A.tb[0], tnb = Bc.tb[0];
   // rows run while a call of the wave is live; the exit test is at the bottom
-  for (int i = 0; __builtin_amdgcn_ballot_w64(DM != 0xffffffffu); ++i) {
+  // (bottom-tested: with the test at the top LLVM copied the loop-carried
+  // state between registers on every row)
+  int i = 0;
+  if (__builtin_amdgcn_ballot_w64(DM != 0xffffffffu)) do {
     const int ta = tna, tbb = tnb;
     tna = A.tb[min(i + 1, max(A.tlen - 1, 0))];  // prefetch
     tnb = Bc.tb[min(i + 1, max(Bc.tlen - 1, 0))];
@@ -941,7 +944,11 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     const uint32_t NLO = smin(CL, HI);
     LO = NLO;
     HI = smin(add(smax(CH, sub(NLO, ONE)), pk(2, 2)), QL);
-  }
+    ++i;
+    // the next row's target bases stay loaded in this row (else LLVM moves the
+    // loads to the next row's top, in front of their only use)
+    asm volatile("" : "+v"(tna), "+v"(tnb));
+  } while (__builtin_amdgcn_ballot_w64(DM != 0xffffffffu));
   // gscore / max_ie from the owner of column qlen-1 of each call
   const int hb = (int)(threadIdx.x & (64 - G));  // the group's first lane
   const uint32_t ea = __shfl(pk(lo16(EI), lo16(ESC)), hb + (A.qlen - 1) / CPL, 64);
