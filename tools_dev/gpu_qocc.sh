@@ -8,3 +8,5 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 BWAGPU_LIB=$GRAFT_REPO_ROOT/bwa-flow_amd/lib/alt/libbwagpu.so timeout -k 10 300 python -u tools_dev/spec_waste.py > $OUT/waste.json 2> $OUT/waste.err || { tail $OUT/waste.err; exit 1; }
 cat $OUT/waste.json
+EXT_FORM=2 BWAGPU_LIB=$GRAFT_REPO_ROOT/bwa-flow_amd/lib/alt/libbwagpu.so timeout -k 10 300 python -u tools_dev/spec_waste.py > $OUT/waste2.json 2> $OUT/waste2.err || { tail $OUT/waste2.err; exit 1; }
+cat $OUT/waste2.json

@@ -21,6 +21,8 @@ FIELDS = ("seq_off", "seq", "read_chain_off", "chain_seed_off", "chain_rid", "ch
 dev = torch.device("cuda:0")
 opt, ref, bs = workload.load_fixture()
 eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
+if os.environ.get("EXT_FORM"):  # bwagpu_debug_ext_form for the A/B
+    abi.load().bwagpu_debug_ext_form(int(os.environ["EXT_FORM"]))
 out = {}
 for k, rb in enumerate(bs):
     b = rb.batch
@@ -45,6 +47,7 @@ for k, rb in enumerate(bs):
                         "heavy_reads": int(sc[5]), "redo_reads": int(sc[6])}
     if sc[8]:  # a lib with tools_dev/ab/quad_occupancy_diag.patch: four-per-wave loop occupancy
         loops, cols, rows = int(sc[8]), int(sc[9]), int(sc[10])
-        out[f"batch{k}"]["quad"] = {"wave_rows": loops, "call_rows": rows, "row_occupancy": round(rows / (4 * loops), 4),
-                                    "slot_cells": cols * 32 * 4, "cell_occupancy": round(sc[3] / (cols * 128), 4)}
+        # loops: group-rows (x 2 call slots), cols: call-slot columns over the rows
+        out[f"batch{k}"]["quad"] = {"group_rows": loops, "call_rows": rows, "row_occupancy": round(rows / (2 * loops), 4),
+                                    "slot_cells": cols, "cell_occupancy": round(sc[3] / cols, 4)}
 print(json.dumps(out))
