@@ -174,6 +174,29 @@ struct Tree {
     }
   }
 
+  // lower() for a tree whose keys are distinct, per lane (each lane its own
+  // pos and path): the key of the largest position <= pos, or -1
+  __device__ int lower_lane(int64_t pos) const {
+    int lo = -1;
+    for (int x = root;;) {
+      const int n = nd[x].n;
+      int c = 0;
+      for (int j = 0; j < kBN; ++j) {
+        if (j < n) {
+          const int k = nd[x].key[j];
+          const int64_t kp = ch[k].s0_rbeg;
+          if (kp == pos) return k;
+          if (kp < pos) {
+            c = j + 1;
+            lo = k;
+          }
+        }
+      }
+      if (!nd[x].internal) return lo;
+      x = nd[x].child[c];
+    }
+  }
+
   __device__ void put_at(int k, int x, int i) {  // kb_putp's leaf insertion (kbtree.h:186-195)
     const int lane = (int)(threadIdx.x & 63);
     ++n_keys;
@@ -424,66 +447,82 @@ __device__ void chain_read(const ChainArgs& a, int r, CH* ch, ND* nd, IX* label,
     c_rid = m;
     return m;
   };
-  int64_t nsr = (int64_t)rbeg[0];
-  int64_t nq = qi[0];  // qbeg | len << 32 (from LDS when staged; else one seed ahead from global memory)
-  for (int p = 0; p < np; ++p) {  // bwamem.c:286-311
-    const int64_t sr = nsr;
-    const int qb = (int)(uint32_t)nq, sl = (int)(nq >> 32);
-    if (p + 1 < np) {  // the next seed's loads overlap this one's work
-      nsr = (int64_t)rbeg[p + 1];
-      nq = qi[p + 1];
+  // Blocks of 64 seeds.  Lane-parallel per block: the seed, its contig
+  // (bns_intv2rid) and, while no two chains share a position, its lower bound
+  // in the tree as it stands — the chain with the largest position <= the
+  // seed's, the only one kb_intervalp can return when positions are
+  // distinct.  Serially: test_and_merge against that chain, and for a new
+  // chain its insertion, after which the block's later seeds whose bound the
+  // new position becomes take it.  Once two chains share a position (tandem
+  // repeats), which of them kbtree returns depends on the tree's shape, and
+  // every seed walks the tree itself (lower_at) as before.
+  bool dup = false;
+  for (int p0 = 0; p0 < np; p0 += 64) {  // bwamem.c:286-311
+    const int nb = min(64, np - p0);
+    const bool in = lane < nb;
+    const int pl = p0 + (in ? lane : 0);
+    const int64_t sr_l = (int64_t)rbeg[pl];
+    const int64_t q_l = qi[pl];  // qbeg | len << 32
+    const int qb_l = (int)(uint32_t)q_l, sl_l = (int)(q_l >> 32);
+    int rid_l = -1;
+    if (in) {  // bns_intv2rid (bntseq.c:365-373)
+      if (sr_l < a.l_pac && sr_l + sl_l > a.l_pac) {
+        rid_l = -2;
+      } else {
+        const int rb_ = rid_of(depos(a.l_pac, sr_l));
+        const int re_ = sl_l > 0 ? rid_of(depos(a.l_pac, sr_l + sl_l - 1)) : rb_;
+        rid_l = rb_ == re_ ? rb_ : -1;
+      }
     }
-    // bns_intv2rid (bntseq.c:365-373)
-    int rid;
-    if (sr < a.l_pac && sr + sl > a.l_pac) {
-      rid = -2;
-    } else {
-      const int rb_ = rid_of(depos(a.l_pac, sr));
-      const int re_ = sl > 0 ? rid_of(depos(a.l_pac, sr + sl - 1)) : rb_;
-      rid = rb_ == re_ ? rb_ : -1;
-    }
-    int lab = -1;
-    if (rid >= 0) {
+    int lo_l = -1, lab_l = -1;
+    if (!dup && t.n_keys && in && rid_l >= 0) lo_l = t.lower_lane(sr_l);
+    int64_t lp_l = lo_l >= 0 ? (int64_t)ch[lo_l].s0_rbeg : INT64_MIN;
+    const uint64_t live = __builtin_amdgcn_ballot_w64(in && rid_l >= 0);
+    for (int q = 0; q < nb; ++q) {
+      if (!((live >> q) & 1)) continue;
+      const int rid = __builtin_amdgcn_readlane(rid_l, q);
+      const int64_t sr = readlane64(sr_l, q);
+      const int qb = __builtin_amdgcn_readlane(qb_l, q), sl = __builtin_amdgcn_readlane(sl_l, q);
+      int lab = -1;
       bool add = true;
       int leaf = -1, leaf_i = 0;
-      if (t.n_keys) {
-        const int lo = t.lower_at(sr, leaf, leaf_i);
-        if (lo >= 0) {
-          // test_and_merge (bwamem.c:199-221)
-          const int64_t c_last_rbeg = ch[lo].last_rbeg, c_s0_rbeg = ch[lo].s0_rbeg;
-          const int c_last_qbeg = ch[lo].last_qbeg, c_last_len = ch[lo].last_len, c_s0_qbeg = ch[lo].s0_qbeg;
-          const int64_t qend = c_last_qbeg + c_last_len, rend = c_last_rbeg + c_last_len;
-          if (rid == ch[lo].rid) {
-            if (qb >= c_s0_qbeg && qb + sl <= qend && sr >= c_s0_rbeg && sr + sl <= rend) {
-              add = false;  // contained: dropped
-            } else if (!((c_last_rbeg < a.l_pac || c_s0_rbeg < a.l_pac) && sr >= a.l_pac)) {
-              const int64_t x = qb - c_last_qbeg, y = sr - c_last_rbeg;
-              if (y >= 0 && x - y <= a.w && y - x <= a.w && x - c_last_len < a.max_chain_gap &&
-                  y - c_last_len < a.max_chain_gap) {
-                ch[lo].last_qbeg = (int16_t)qb;
-                ch[lo].last_rbeg = sr;
-                ch[lo].last_len = (int16_t)sl;
-                ch[lo].n = ch[lo].n + 1;
-                {  // mem_chain_weight's two sweeps, one seed further (bwamem.c:227-240)
-                  const int eq = ch[lo].endq;
-                  int wq = ch[lo].wq;
-                  if (qb >= eq) wq += sl;
-                  else if (qb + sl > eq) wq += qb + sl - eq;
-                  ch[lo].wq = (int16_t)wq;
-                  ch[lo].endq = (int16_t)(eq > qb + sl ? eq : qb + sl);
-                  const int64_t er = ch[lo].endr;
-                  int wr = ch[lo].wr;
-                  if (sr >= er) wr += sl;
-                  else if (sr + sl > er) wr += (int)(sr + sl - er);
-                  ch[lo].wr = (int16_t)(wr < 32767 ? wr : 32767);  // only min(wq, wr) is read
-                  ch[lo].endr = er > sr + sl ? er : sr + sl;
-                }
-                lab = lo;
-                add = false;
+      const int lo = !dup ? __builtin_amdgcn_readlane(lo_l, q) : (t.n_keys ? t.lower_at(sr, leaf, leaf_i) : -1);
+      if (lo >= 0) {
+        // test_and_merge (bwamem.c:199-221)
+        const int64_t c_last_rbeg = ch[lo].last_rbeg, c_s0_rbeg = ch[lo].s0_rbeg;
+        const int c_last_qbeg = ch[lo].last_qbeg, c_last_len = ch[lo].last_len, c_s0_qbeg = ch[lo].s0_qbeg;
+        const int64_t qend = c_last_qbeg + c_last_len, rend = c_last_rbeg + c_last_len;
+        if (rid == ch[lo].rid) {
+          if (qb >= c_s0_qbeg && qb + sl <= qend && sr >= c_s0_rbeg && sr + sl <= rend) {
+            add = false;  // contained: dropped
+          } else if (!((c_last_rbeg < a.l_pac || c_s0_rbeg < a.l_pac) && sr >= a.l_pac)) {
+            const int64_t x = qb - c_last_qbeg, y = sr - c_last_rbeg;
+            if (y >= 0 && x - y <= a.w && y - x <= a.w && x - c_last_len < a.max_chain_gap &&
+                y - c_last_len < a.max_chain_gap) {
+              ch[lo].last_qbeg = (int16_t)qb;
+              ch[lo].last_rbeg = sr;
+              ch[lo].last_len = (int16_t)sl;
+              ch[lo].n = ch[lo].n + 1;
+              {  // mem_chain_weight's two sweeps, one seed further (bwamem.c:227-240)
+                const int eq = ch[lo].endq;
+                int wq = ch[lo].wq;
+                if (qb >= eq) wq += sl;
+                else if (qb + sl > eq) wq += qb + sl - eq;
+                ch[lo].wq = (int16_t)wq;
+                ch[lo].endq = (int16_t)(eq > qb + sl ? eq : qb + sl);
+                const int64_t er = ch[lo].endr;
+                int wr = ch[lo].wr;
+                if (sr >= er) wr += sl;
+                else if (sr + sl > er) wr += (int)(sr + sl - er);
+                ch[lo].wr = (int16_t)(wr < 32767 ? wr : 32767);  // only min(wq, wr) is read
+                ch[lo].endr = er > sr + sl ? er : sr + sl;
               }
+              lab = lo;
+              add = false;
             }
           }
         }
+        if (add && c_s0_rbeg == sr) dup = true;  // the new chain will share lo's position
       }
       if (add) {
         CH* c = ch + n_ch;
@@ -500,11 +539,18 @@ __device__ void chain_read(const ChainArgs& a, int r, CH* ch, ND* nd, IX* label,
         c->first = -1;
         c->w = 0;
         lab = n_ch;
-        if (leaf >= 0) t.put_at(n_ch++, leaf, leaf_i);
-        else t.put(n_ch++, sr);
+        if (leaf >= 0) t.put_at(n_ch, leaf, leaf_i);
+        else t.put(n_ch, sr);
+        // the later seeds of the block whose lower bound the new position becomes
+        const bool aff = lane > q && lp_l < sr && sr <= sr_l;
+        lo_l = aff ? n_ch : lo_l;
+        lp_l = aff ? sr : lp_l;
+        ++n_ch;
       }
+      lab_l = lane == q ? lab : lab_l;
     }
-    label[p] = lab;
+    if (in) label[p0 + lane] = lab_l;
+    wave_sync();
   }
   stamp(1);
   // in-order traversal (__kb_traverse, kbtree.h:336-358): the chain order

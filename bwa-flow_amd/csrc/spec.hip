@@ -861,7 +861,7 @@ static int ext2_grid(int nb) {
 // The sequential logic of mem_chain2aln over one read's chains, by one wave.
 // A seed that is extended but has no result yet:
 //   SEL_EMULATE  becomes a round-B task (its region stays unknown in this pass);
-//   SEL_FINAL    becomes a round-C task and the read goes to the redo list
+//   SEL_FINAL    is listed (the round-C list, a diagnostic count) and the read goes to the redo list
 //                (its later decisions depend on that region);
 //   SEL_REDO     (the redo list only) is computed inline — the pass that
 //                guarantees every read completes.
@@ -1182,9 +1182,10 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
 // form); SEL_FINAL sends the read to the redo pass.
 // A misprediction in the final pass of a light read (a seed the replay must
 // extend has no result: ~10-20 per C2 batch) is extended inline, which takes
-// the kernel to 129 VGPRs (3 waves per SIMD).  Sending it to round C + the
-// redo pass like one of a longer read instead (82 VGPRs) is bit-exact, but
-// measured 19.8-19.9 vs 21.6-21.7 Mreads/s on C2.
+// the kernel to 129 VGPRs (3 waves per SIMD).  Sending it to the redo pass
+// like one of a longer read instead (82 VGPRs) is bit-exact, but measured
+// 19.8-19.9 vs 21.6-21.7 Mreads/s on C2 in round 3 and 29.4-30.2 vs 36.9-37.3
+// in round 4.
 template <int MODE>
 __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
                                                             int tb_bytes) {
@@ -1359,7 +1360,7 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
         __builtin_amdgcn_wave_barrier();
         continue;
       }
-      if (miss >= 0) {  // round C + the redo pass (reads > 160 bp)
+      if (miss >= 0) {  // the redo pass (reads > 160 bp)
         const int list = 2 * kSpecBins + spec_bin(d.lq);
         if (r == miss) {
           const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
@@ -1614,7 +1615,7 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
             pend |= bit;  // a round-B task; its region stays unknown
             continue;
           }
-          if (d.lq > kSpecBinLen[0]) {  // longer reads: round C + the redo pass
+          if (d.lq > kSpecBinLen[0]) {  // longer reads: the redo pass
             miss = kb + i;
             break;
           }
@@ -1820,7 +1821,12 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
                      l + 2, tb_bytes);
 }
 
-// prep -> round A -> emulate -> round B -> final -> round C -> redo, one stream
+// prep -> round A -> emulate -> round B -> final -> redo, one stream.  The
+// final pass's misses in reads over 160 bp and in heavy reads without a pair
+// matrix (round-C lists: a handful per batch, none on C2) are computed by the
+// redo pass inline: a launch of its own for them waited ~0.18 ms per batch for
+// CU slots the other caller stream's extension kernel held, even over an
+// empty list.
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   if (b.n_reads == 0) return hipSuccess;
@@ -1835,10 +1841,7 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
     launch_ext_round(o, ref, b, a, 1, tb_bytes, lq_max, st, ss);
   }
   launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
-  if (b.n_chains) {
-    launch_ext_round(o, ref, b, a, 2, tb_bytes, lq_max, st, ss);
-    launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
-  }
+  if (b.n_chains) launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
   return hipGetLastError();
 }
 

@@ -14,3 +14,5 @@ import json;d=json.load(open('$OUT/b.json'));print(d['value'],d['ms_per_step'],d
 g=d.get('regime_grch38',{})
 for k,v in g.items():
   if isinstance(v,dict): print(k, {x:v[x] for x in v if x in ('ms_per_batch','value','parity_all_steps','ext_busy_ms_per_batch')})"
+timeout -k 10 300 python -u tools_dev/spec_trace.py > $OUT/trace.json 2> $OUT/trace.err || { tail $OUT/trace.err; exit 4; }
+timeout -k 10 300 python -u tools_dev/spec_waste.py > $OUT/waste.json 2> $OUT/waste.err || { tail $OUT/waste.err; exit 5; }
