@@ -843,13 +843,17 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
 // stream (the bench's ping-pong) and this batch's selection kernels keep the
 // rest, and an even count per CU beats an uneven one.  Same-box sweep
 // (DESIGN.md §3): capacity 19.87, 60 % 20.74, 50 % 20.66, 2/CU (40 %) 21.74,
-// 30 % 20.16, 1/CU 19.72 Mreads/s.  BWAGPU_EXT2_BLOCKS_PER_CU overrides.
-static int ext2_grid(int nb) {
-  static const int per_cu = [] {
+// 30 % 20.16, 1/CU 19.72 Mreads/s.  The packed kernels (two 209 / 198-VGPR
+// waves per SIMD at 2/CU) run at 1 workgroup per CU: 37.97-38.04 against
+// 36.99-37.17 Mreads/s on C2, C3 0.66 against 0.78-0.79 ms per batch (same
+// box).  BWAGPU_EXT2_BLOCKS_PER_CU overrides both.
+static int ext2_grid(int nb, bool packed) {
+  static const int env_cu = [] {
     const char* e = getenv("BWAGPU_EXT2_BLOCKS_PER_CU");
-    const int v = e ? atoi(e) : 2;
-    return v < 1 ? 1 : v;
+    const int v = e ? atoi(e) : 0;
+    return v < 0 ? 0 : v;
   }();
+  const int per_cu = env_cu ? env_cu : (packed ? 1 : 2);
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       ncu <= 0)
@@ -1771,9 +1775,9 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
   const bool bin1 = lq_max > kSpecBinLen[0], bin2 = lq_max > kSpecBinLen[1];
-  const auto grid = [round](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb); };
   const int form = g_ext_form.load(std::memory_order_relaxed);
   const bool quad = form != 1 && quad_scores_ok(o, kSpecBinLen[1]) && quad_rows_ok(o, tb_bytes);
+  const auto grid = [round, quad](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb, quad); };
   const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]), oct = key8 && form == 0;
   const size_t lds2 = quad ? ext4_lds(tb_bytes, 32) : ext2_lds(tb_bytes);
   // the first two length bins' lists in pair order (spec_sort_*), then two,
