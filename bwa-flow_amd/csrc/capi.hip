@@ -114,12 +114,70 @@ struct Slot {
     spec = SpecStreams{};
   }
   HostBuf h_in, h_out, h_n, h_stats;
+  // the submit/wait path's results: regions written densely (read r's at
+  // h_dense[h_off[r] ..]) by dense_copy_kernel straight into pinned memory;
+  // h_out (the slot layout) is filled from them only when asked for
+  HostBuf h_dense, h_off;
+  DevBuf d_off;
+  size_t in_rco = 0, in_cso = 0;  // where the batch's offsets sit in h_in
+  bool slot_view = false;         // h_out holds the last batch's slot layout
   bool busy = false;
   int32_t n_reads = 0, n_seeds = 0;
   std::chrono::steady_clock::time_point t_submit;
   bwagpu_stats_t last{};
   int64_t h2d = 0, d2h = 0;
 };
+
+// Per-read offsets of the dense result layout: off[r] = n[0] + ... + n[r-1]
+// (one workgroup; a batch has < 2^31 regions), written to the device (for the
+// copy) and to pinned host memory (for the caller).
+constexpr int kDenseScanBlock = 1024;
+__global__ void __launch_bounds__(kDenseScanBlock) dense_scan_kernel(const int32_t* __restrict__ n, int nr,
+                                                                     int32_t* __restrict__ off,
+                                                                     int32_t* __restrict__ h_off) {
+  __shared__ int32_t part[kDenseScanBlock];
+  const int t = (int)threadIdx.x;
+  const int per = (nr + kDenseScanBlock - 1) / kDenseScanBlock;
+  const int r0 = min(t * per, nr), r1 = min(r0 + per, nr);
+  int sum = 0;
+  for (int r = r0; r < r1; ++r) sum += n[r];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < kDenseScanBlock; d <<= 1) {  // inclusive scan of the parts
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int r = r0; r < r1; ++r) {
+    off[r] = run;
+    h_off[r] = run;
+    run += n[r];
+  }
+  if (t == kDenseScanBlock - 1) {
+    off[nr] = part[t];
+    h_off[nr] = part[t];
+  }
+}
+
+// Regions of read r from its slots (chain_seed_off[read_chain_off[r]], the
+// ABI's layout) to dense[off[r] ..], 16 lanes per read, 8-byte words: the
+// D2H moves the sum of n (~1.8 regions per read on C2) instead of every seed slot.
+__global__ void __launch_bounds__(256) dense_copy_kernel(const bwagpu_alnreg_t* __restrict__ out,
+                                                         const int32_t* __restrict__ n,
+                                                         const int32_t* __restrict__ off,
+                                                         const int32_t* __restrict__ rco,
+                                                         const int32_t* __restrict__ cso, int nr,
+                                                         bwagpu_alnreg_t* __restrict__ dense) {
+  constexpr int kW = (int)(sizeof(bwagpu_alnreg_t) / 8);
+  const int r = (int)((blockIdx.x * 256u + threadIdx.x) >> 4), l = (int)(threadIdx.x & 15);
+  if (r >= nr) return;
+  const int words = n[r] * kW;
+  const uint2* src = reinterpret_cast<const uint2*>(out + cso[rco[r]]);
+  uint2* dst = reinterpret_cast<uint2*>(dense + off[r]);
+  for (int w = l; w < words; w += 16) dst[w] = src[w];
+}
 
 }  // namespace
 
@@ -132,6 +190,7 @@ struct bwagpu_ctx {
   int64_t* d_ann_off = nullptr;
   int32_t* d_ann_len = nullptr;
   int watchdog_ms = 10000;
+  int ext_form = 0;  // bwagpu_ctx_ext_form (the process default when made)
   Slot slot[BWAGPU_NUM_SLOTS];
   // bwagpu_chain2aln_device: the caller's streams, one per slot's scratch (a
   // stream always reuses the same scratch, so its launches never race)
@@ -296,6 +355,7 @@ int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, 
     return BWAGPU_E_INVAL;
   }
   ctx->device = device;
+  ctx->ext_form = set_ext_form(-1);
   *made = ctx;
   HIPC(hipSetDevice(device), "hipSetDevice");
   HIPC(hipMalloc(&ctx->d_ann_off, sizeof(int64_t) * bns->n_seqs), "hipMalloc(ann_offset)");
@@ -326,6 +386,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     s.d_in.release(); s.release_scratch();
     s.d_out.release(); s.d_n.release(); s.d_stats.release();
     s.h_in.release(); s.h_out.release(); s.h_n.release(); s.h_stats.release();
+    s.h_dense.release(); s.h_off.release(); s.d_off.release();
     if (s.ev0) (void)hipEventDestroy(s.ev0);
     if (s.ev1) (void)hipEventDestroy(s.ev1);
     if (s.ev2) (void)hipEventDestroy(s.ev2);
@@ -566,12 +627,24 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.out_n = d_n;
   a.stats = d_stats;
   if (!s.spec.side) {
+    const char* pe = getenv("BWAGPU_SIDE_PRIO");
+    if (pe && pe[0] == '2') {  // a CU-masked stream (every CU): a hardware queue of its own
+      int cus = 0;
+      HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device), "attribute");
+      std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+      HIPC(hipExtStreamCreateWithCUMask(&s.spec.side, (uint32_t)mask.size(), mask.data()), "hipStreamCreate(side)");
+    } else if (pe && pe[0] == '1') {
+      int least = 0, greatest = 0;
+      HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
+      HIPC(hipStreamCreateWithPriority(&s.spec.side, hipStreamNonBlocking, greatest), "hipStreamCreate(side)");
+    } else
     HIPC(hipStreamCreateWithFlags(&s.spec.side, hipStreamNonBlocking), "hipStreamCreate(side)");
     HIPC(hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming), "hipEventCreate");
     HIPC(hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming), "hipEventCreate");
   }
   a.lq_bound = lq_max;
   const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
+  s.spec.form = ctx->ext_form;
   s.spec.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
   s.spec.pool_n = (int)ctx->prof_ev.size();
   s.spec.pool_used = &ctx->prof_used;
@@ -687,6 +760,21 @@ int bwagpu_set_watchdog_ms(bwagpu_ctx_t* ctx, int ms) {
   return BWAGPU_OK;
 }
 
+namespace {
+// the ABI's slot layout (read r's regions from chain_seed_off[read_chain_off[r]])
+// from a finished batch's dense results; the offsets come from the staged input
+void expand_slots(const Slot& s, bwagpu_alnreg_t* dst) {
+  const char* h = s.h_in.as<const char>();
+  const int32_t* rco = (const int32_t*)(h + s.in_rco);
+  const int32_t* cso = (const int32_t*)(h + s.in_cso);
+  const int32_t* n = s.h_n.as<const int32_t>();
+  const int32_t* off = s.h_off.as<const int32_t>();
+  const bwagpu_alnreg_t* src = s.h_dense.as<const bwagpu_alnreg_t>();
+  for (int32_t r = 0; r < s.n_reads; ++r)
+    if (n[r]) memcpy(dst + cso[rco[r]], src + off[r], sizeof(bwagpu_alnreg_t) * (size_t)n[r]);
+}
+}  // namespace
+
 int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b) {
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
@@ -706,9 +794,12 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   HIPC(s.d_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipMalloc(out)");
   HIPC(s.d_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipMalloc(out_n)");
   HIPC(s.d_stats.ensure(sizeof(int64_t) * ST_N), "hipMalloc(stats)");
-  HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipHostMalloc(out)");
+  HIPC(s.h_dense.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(b->n_seeds, 1)), "hipHostMalloc(out)");
   HIPC(s.h_n.ensure(sizeof(int32_t) * (size_t)std::max(b->n_reads, 1)), "hipHostMalloc(out_n)");
+  HIPC(s.h_off.ensure(sizeof(int32_t) * (size_t)(b->n_reads + 1)), "hipHostMalloc(out_off)");
+  HIPC(s.d_off.ensure(sizeof(int32_t) * (size_t)(b->n_reads + 1)), "hipMalloc(out_off)");
   HIPC(s.h_stats.ensure(sizeof(int64_t) * ST_N), "hipHostMalloc(stats)");
+  s.slot_view = false;
   // stage into pinned memory so the caller's buffers are free on return —
   // unless the caller packed into that memory already (bwagpu_chain2aln_stage)
   char* h = s.h_in.as<char>();
@@ -757,16 +848,28 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
     return rc;
   }
   HIPC(hipEventRecord(s.ev2, st), "event");
-  if (b->n_seeds)
-    HIPC(hipMemcpyAsync(s.h_out.p, s.d_out.p, sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds, hipMemcpyDeviceToHost, st),
-         "D2H regions");
+  // the results: per-read offsets, then the regions densely into pinned memory
+  // (the device writes them over PCIe: only the sum of n is moved, not the
+  // n_seeds slots the kernels fill)
+  int32_t* h_off_dev = nullptr;
+  bwagpu_alnreg_t* h_dense_dev = nullptr;
+  HIPC(hipHostGetDevicePointer((void**)&h_off_dev, s.h_off.p, 0), "hipHostGetDevicePointer");
+  HIPC(hipHostGetDevicePointer((void**)&h_dense_dev, s.h_dense.p, 0), "hipHostGetDevicePointer");
+  hipLaunchKernelGGL(dense_scan_kernel, dim3(1), dim3(kDenseScanBlock), 0, st, s.d_n.as<int32_t>(), b->n_reads,
+                     s.d_off.as<int32_t>(), h_off_dev);
+  if (b->n_reads)
+    hipLaunchKernelGGL(dense_copy_kernel, dim3((unsigned)((b->n_reads + 15) / 16)), dim3(256), 0, st,
+                       s.d_out.as<bwagpu_alnreg_t>(), s.d_n.as<int32_t>(), s.d_off.as<int32_t>(), db.read_chain_off,
+                       db.chain_seed_off, b->n_reads, h_dense_dev);
+  HIPC(hipGetLastError(), "dense results launch");
   if (b->n_reads)
     HIPC(hipMemcpyAsync(s.h_n.p, s.d_n.p, sizeof(int32_t) * (size_t)b->n_reads, hipMemcpyDeviceToHost, st),
          "D2H counts");
   HIPC(hipMemcpyAsync(s.h_stats.p, s.d_stats.p, sizeof(int64_t) * ST_N, hipMemcpyDeviceToHost, st), "D2H stats");
   HIPC(hipEventRecord(s.ev3, st), "event");
   s.h2d = (int64_t)L.total;
-  s.d2h = (int64_t)(sizeof(bwagpu_alnreg_t) * (size_t)b->n_seeds + sizeof(int32_t) * (size_t)b->n_reads);
+  s.in_rco = L.rco;
+  s.in_cso = L.cso;
   s.busy = true;
   return BWAGPU_OK;
 }
@@ -811,13 +914,15 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
   s.last.cells = st[ST_CELLS];
   s.last.rows = st[ST_ROWS];
   s.last.ext_calls = st[ST_CALLS];
+  const int32_t* off = s.h_off.as<int32_t>();
+  s.d2h = (int64_t)sizeof(bwagpu_alnreg_t) * off[s.n_reads] + (int64_t)sizeof(int32_t) * (2 * (int64_t)s.n_reads + 1);
   s.last.h2d_bytes = s.h2d;
   s.last.d2h_bytes = s.d2h;
   if (st[ST_ERR] & ERR_LEN) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_READ_LEN");
   // on a flagged chain the results are still copied: every other chain's
   // regions are valid, the flagged ones were skipped (the caller's error path)
   if (out_n && s.n_reads) memcpy(out_n, s.h_n.p, sizeof(int32_t) * (size_t)s.n_reads);
-  if (out_regs && s.n_seeds) memcpy(out_regs, s.h_out.p, sizeof(bwagpu_alnreg_t) * (size_t)s.n_seeds);
+  if (out_regs && s.n_seeds) expand_slots(s, out_regs);
   if (st[ST_ERR] & ERR_RID)
     return fail(ctx, BWAGPU_E_RESULTS, "a chain's first seed is not inside contig chain_rid (bwamem.c:669 assert)");
   return BWAGPU_OK;
@@ -855,8 +960,25 @@ int bwagpu_chain2aln_results(bwagpu_ctx_t* ctx, int slot, const bwagpu_alnreg_t*
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS || !regs || !n) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot's batch still in flight (wait first)");
+  if (!s.slot_view) {  // the slot layout, built from the dense results once per batch
+    HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(s.n_seeds, 1)), "hipHostMalloc(out)");
+    if (s.n_seeds) expand_slots(s, s.h_out.as<bwagpu_alnreg_t>());
+    s.slot_view = true;
+  }
   *regs = s.h_out.as<const bwagpu_alnreg_t>();
   *n = s.h_n.as<const int32_t>();
+  return BWAGPU_OK;
+}
+
+int bwagpu_chain2aln_results_dense(bwagpu_ctx_t* ctx, int slot, const bwagpu_alnreg_t** regs, const int32_t** n,
+                                   const int32_t** off) {
+  if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS || !regs || !n || !off) return BWAGPU_E_INVAL;
+  Slot& s = ctx->slot[slot];
+  if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot's batch still in flight (wait first)");
+  if (!s.h_dense.p || !s.h_off.p) return fail(ctx, BWAGPU_E_INVAL, "slot has no results");
+  *regs = s.h_dense.as<const bwagpu_alnreg_t>();
+  *n = s.h_n.as<const int32_t>();
+  *off = s.h_off.as<const int32_t>();
   return BWAGPU_OK;
 }
 
@@ -911,7 +1033,7 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
   // bins: the wave kernels by column segments, then the four-per-wave kernel
   // (packed 16-bit DP) for the tasks it takes (extend4_kernel)
   std::vector<int32_t> lists[kNumExtVariants + 1];
-  const bool quad = ext_form() == 0;
+  const bool quad = ctx->ext_form == 0;
   bool t5 = false;
   int lq_max = 1;
   for (int32_t k = 0; k < n; ++k) {
@@ -1437,6 +1559,18 @@ int bwagpu_debug_spec_ext(bwagpu_ctx_t* ctx, void* stream, void* host_out, int32
 }
 
 int bwagpu_debug_ext_form(int form) { return set_ext_form(form); }
+
+int bwagpu_ctx_ext_form(bwagpu_ctx_t* ctx, int form) {
+  if (!ctx) return BWAGPU_E_INVAL;
+  const int prev = ctx->ext_form;
+  if (form >= 0) ctx->ext_form = form > 2 ? 1 : form;
+  return prev;
+}
+
+int bwagpu_debug_ext_kernel(bwagpu_ctx_t* ctx, int32_t lq_max) {
+  if (!ctx || lq_max < 1 || lq_max > BWAGPU_MAX_READ_LEN) return BWAGPU_E_INVAL;
+  return ext_kernel_for(ctx->opt, ctx->ext_form, tb_bytes_for(ctx->opt, lq_max));
+}
 
 int bwagpu_prof_start(bwagpu_ctx_t* ctx, int max_launches) {
   if (!ctx || max_launches < 0) return BWAGPU_E_INVAL;

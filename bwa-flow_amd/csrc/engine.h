@@ -212,10 +212,18 @@ struct SpecStreams {
   hipEvent_t* pool = nullptr;
   int pool_n = 0;
   int* pool_used = nullptr;
+  // the context's extension form (bwagpu_ctx_ext_form): 0 = eight / four seeds
+  // per wave where the scores fit (default), 1 = two per wave, 2 = four per wave
+  int form = 0;
 };
-// bwagpu_debug_ext_form: 0 = eight / four seeds per wave where the scores fit (default), 1 = two per
-// wave, 2 = four per wave
+// the form new contexts start with (bwagpu_debug_ext_form; process-wide default)
 int set_ext_form(int form);
+// the first length bin's extension kernel launch_ext_round picks for `form`
+// and options `o` with target row buffers of tb_bytes: 8 = eight seeds per
+// wave (spec_ext4_kernel<16,10,true>), 4 = four per wave with the 8-bit key
+// (<32,5,true>), 5 = four per wave (<32,8,false>), 2 = two per wave
+// (spec_ext2_kernel<5>)
+int ext_kernel_for(const DevOpt& o, int form, int tb_bytes);
 bool quad_scores_ok(const DevOpt& o, int lq);
 bool quad_bound_ok(const DevOpt& o, long hb);
 bool quad_rows_ok(const DevOpt& o, long rows);

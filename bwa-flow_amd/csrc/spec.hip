@@ -532,6 +532,10 @@ __device__ __forceinline__ QCall qtask_call(QTask& t, const DevOpt& o, const uin
   q.zdrop = o.zdrop;
   q.q = seq + t.qoff;
   q.tb = left ? tl : tr;
+  // rows past qlen + w + 1 have an empty band (ksw.c:415-419: m == 0 breaks
+  // there), so the cap changes no result; it keeps tlen inside the packed
+  // kernels' 16-bit row counters for chain windows of 32 kb and more
+  q.tlen = rows_needed(o, q.qlen, q.tlen, q.w, q.eb);
   return q;
 }
 
@@ -1739,11 +1743,16 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
 // The first two length bins' extension kernel: eight seeds per wave for the
 // first bin and four for the second (spec_ext4_kernel, packed 16-bit DP) when
 // every score of the bin fits the packed ranges, else two per wave
-// (spec_ext2_kernel, 32-bit).  bwagpu_debug_ext_form(1) forces two per wave,
-// (2) four per wave in the first bin too (tests, A/B).
+// (spec_ext2_kernel, 32-bit).  Form 1 (bwagpu_ctx_ext_form, per context)
+// forces two per wave, 2 four per wave in the first bin too (tests, A/B).
 static std::atomic<int> g_ext_form{0};
 int ext_form() { return g_ext_form.load(std::memory_order_relaxed); }
-int set_ext_form(int form) {  // process-wide; -> the previous form (form < 0: query only)
+int ext_kernel_for(const DevOpt& o, int form, int tb_bytes) {  // launch_ext_round's choice, first bin
+  const bool quad = form != 1 && quad_scores_ok(o, kSpecBinLen[1]) && quad_rows_ok(o, tb_bytes);
+  const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]);
+  return key8 ? (form == 0 ? 8 : 4) : (quad ? 5 : 2);
+}
+int set_ext_form(int form) {  // the default of contexts made later; -> the previous one (form < 0: query only)
   const int prev = g_ext_form.load(std::memory_order_relaxed);
   if (form >= 0) g_ext_form.store(form > 2 ? 1 : form, std::memory_order_relaxed);
   return prev;
@@ -1779,7 +1788,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
   const int l = round * kSpecBins;
   const bool bin1 = lq_max > kSpecBinLen[0], bin2 = lq_max > kSpecBinLen[1];
-  const int form = g_ext_form.load(std::memory_order_relaxed);
+  const int form = ss.form;
   const bool quad = form != 1 && quad_scores_ok(o, kSpecBinLen[1]) && quad_rows_ok(o, tb_bytes);
   const auto grid = [round, quad](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb, quad); };
   const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]), oct = key8 && form == 0;

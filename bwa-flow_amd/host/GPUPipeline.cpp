@@ -400,6 +400,30 @@ mem_alnreg_v* FlatBatch::unpack_from(const bwagpu_alnreg_t* rg, const int32_t* n
   return av;
 }
 
+mem_alnreg_v* FlatBatch::unpack_dense(const bwagpu_alnreg_t* rg, const int32_t* nn, const int32_t* off,
+                                      int batch_num) {
+  mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
+  if (!av) throw std::runtime_error("Memory allocation failed");
+  std::atomic<bool> oom{false};
+  parallel_ranges(batch_num, [&](int r0, int r1) {
+    for (int i = r0; i < r1; ++i) {
+      const size_t k = (size_t)nn[i];
+      av[i].n = av[i].m = k;
+      av[i].a = nullptr;
+      if (k) {
+        av[i].a = (mem_alnreg_t*)malloc(sizeof(mem_alnreg_t) * k);
+        if (!av[i].a) {
+          oom = true;
+          continue;
+        }
+        memcpy(av[i].a, &rg[off[i]], sizeof(mem_alnreg_t) * k);
+      }
+    }
+  });
+  if (oom) throw std::runtime_error("Memory allocation failed");
+  return av;
+}
+
 mem_alnreg_v* FlatBatch::unpack(int batch_num) const {
   mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
   if (!av) throw std::runtime_error("Memory allocation failed");
@@ -626,13 +650,23 @@ void ChainsToRegionsGPU::compute(int wid) {
     out.seqs = j.rec.seqs;
     const bwagpu_alnreg_t* rg = nullptr;
     const int32_t* nn = nullptr;
-    if (bwagpu_chain2aln_results(ctx, j.slot, &rg, &nn) != BWAGPU_OK) {
+    const int32_t* off = nullptr;
+    if (bwagpu_chain2aln_results_dense(ctx, j.slot, &rg, &nn, &off) != BWAGPU_OK) {
       fail_all("results", BWAGPU_E_INVAL);
       return;
     }
-    out.alnreg = j.flat->unpack_from(rg, nn, j.rec.batch_num);
-    reaper_.release(j.rec.chains, j.rec.batch_num);
-    out.chains = nullptr;
+    bwagpu_stats_t ds{};
+    if (bwagpu_last_stats(ctx, j.slot, &ds) == BWAGPU_OK) {
+      dev_ns_[0] += (long long)(ds.kernel_ms * 1e6);
+      dev_ns_[1] += (long long)((ds.total_ms - ds.kernel_ms) * 1e6);
+    }
+    out.alnreg = FlatBatch::unpack_dense(rg, nn, off, j.rec.batch_num);
+    if (own_ == ChainOwnership::kForward) {
+      out.chains = j.rec.chains;  // RegionsToSam frees them (Pipeline.cpp:559)
+    } else {
+      reaper_.release(j.rec.chains, j.rec.batch_num);
+      out.chains = nullptr;
+    }
     ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     n_gpu_.fetch_add(1);
     if (wid < kMaxWorkers) per_worker_[wid].fetch_add(1);

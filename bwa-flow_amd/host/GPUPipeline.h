@@ -9,9 +9,11 @@
 //                          fallback), same compute(wid) protocol
 //
 // Results are bit-identical to ChainsToRegions::compute (src/Pipeline.cpp:
-// 503-544), including ownership: chains are freed and the output record's
-// chains is NULL; alnreg and every alnreg[i].a are malloc'd (freeAligns,
-// bwa_wrapper.cpp:824-830, can free them).
+// 503-544); alnreg and every alnreg[i].a are malloc'd (freeAligns,
+// bwa_wrapper.cpp:824-830, can free them).  The chains go one of two ways
+// (ChainOwnership): forwarded in the output record for RegionsToSam to free
+// (Pipeline.cpp:559), as the FPGA stage does (FPGAPipeline.cpp:434), or freed
+// here and NULL forwarded, as the CPU stage does (Pipeline.cpp:526-537).
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -86,8 +88,11 @@ struct FlatBatch {
   int pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec);
   // ~ processOutput (FPGAPipeline.cpp:29-130): regions into malloc'd mem_alnreg_v
   mem_alnreg_v* unpack(int batch_num) const;
-  // the same from a slot's pinned results (bwagpu_chain2aln_results)
+  // the same from a slot's pinned results in the slot layout (bwagpu_chain2aln_results)
   mem_alnreg_v* unpack_from(const bwagpu_alnreg_t* regs, const int32_t* n, int batch_num) const;
+  // ... and from the dense ones (bwagpu_chain2aln_results_dense: read i's at regs[off[i]])
+  static mem_alnreg_v* unpack_dense(const bwagpu_alnreg_t* regs, const int32_t* n, const int32_t* off,
+                                    int batch_num);
 };
 
 // frees the chains of a record the way ChainsToRegions::compute does
@@ -123,16 +128,27 @@ class ChainReaper {
   std::thread th_;
 };
 
+// Who frees a record's chains once its regions are made.
+enum class ChainOwnership {
+  kForward,  // the output record carries them; RegionsToSam frees them (Pipeline.cpp:559),
+             // as after ChainsToRegionsFPGA (FPGAPipeline.cpp:434)
+  kFree,     // freed by the stage (its ChainReaper), chains = NULL forwarded, as after
+             // ChainsToRegions::compute (Pipeline.cpp:526-537)
+};
+
 class ChainsToRegionsGPU
     : public kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH> {
  public:
-  ChainsToRegionsGPU(int n = 1, ChainsToRegions* stage = nullptr, GPUEnv* env = nullptr)
+  ChainsToRegionsGPU(int n = 1, ChainsToRegions* stage = nullptr, GPUEnv* env = nullptr,
+                     ChainOwnership own = ChainOwnership::kForward)
       : kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH>(n, false),
         n_active_(n),
         cpu_stage_(stage),
-        env_(env) {}
+        env_(env),
+        own_(own) {}
 
   void compute(int wid) override;
+  ChainOwnership chain_ownership() const { return own_; }
 
   // counters (tests / logging)
   int records_on_gpu() const { return n_gpu_.load(); }
@@ -151,6 +167,11 @@ class ChainsToRegionsGPU
   void phase_seconds(double out[4]) const {
     for (int i = 0; i < 4; ++i) out[i] = (double)ns_[i].load() * 1e-9;
   }
+  // device-side totals over the GPU records, seconds (HIP events of each
+  // batch, bwagpu_last_stats): [0] kernels, [1] H2D + results to host
+  void device_seconds(double out[2]) const {
+    for (int i = 0; i < 2; ++i) out[i] = (double)dev_ns_[i].load() * 1e-9;
+  }
 
  private:
   RegionsRecord on_cpu(const ChainsRecord& rec);
@@ -162,5 +183,7 @@ class ChainsToRegionsGPU
   std::atomic<int> n_gpu_{0}, n_cpu_{0}, n_failed_{0};
   std::atomic<int> per_worker_[kMaxWorkers] = {};
   std::atomic<long long> ns_[4] = {};
+  std::atomic<long long> dev_ns_[2] = {};
+  ChainOwnership own_;
   ChainReaper reaper_;
 };

@@ -5,9 +5,11 @@
 // bwa-flow's SeqsToChains hands them over (src/Pipeline.cpp:110-121) — go
 // through a kflow pipeline whose stage 4 is ChainsToRegionsGPU alone
 // (--disable_sw_cpu, main.cpp:320-329): FlatBatch::pack -> bwagpu submit (pinned
-// staging, H2D, kernels) -> wait (D2H) -> malloc'd mem_alnreg_v per read, chains
-// freed; a consumer thread plays RegionsToSam and frees the regions.  The
-// records are built before the clock starts (that is SeqsToChains' work).
+// staging, H2D, kernels, the regions written densely to pinned memory) -> wait ->
+// malloc'd mem_alnreg_v per read; a consumer thread plays RegionsToSam: it
+// frees the regions, and the chains when the stage forwards them
+// (ChainOwnership::kForward, the FPGA stage's way; kFree: the stage frees them).
+// The records are built before the clock starts (that is SeqsToChains' work).
 #include <stdlib.h>
 #include <string.h>
 
@@ -53,16 +55,23 @@ ChainsRecord make_record(const bwagpu_batch_t& b, bseq1_t* seqs, uint64_t start_
 extern "C" {
 
 // Runs reps x n_batches records through the stage on up to max_devices
-// devices with per_device stage workers (bwagpu contexts) on each.  times[0] = wall seconds from the first record in to the last
-// record out and the stage's last chain freed, times[1..4] = the stage's phase totals (pack, submit, wait,
-// post; summed over workers), times[5] = records on the GPU, times[6] =
-// records the CPU fallback took, times[7] = stage workers (contexts) used.  The regions of the
-// LAST rep of batch k go to out_n[k][r] / out_regs[k] (compact, read order).
-// Returns 0, or the number of records whose chains were not freed.
+// devices with per_device stage workers (bwagpu contexts) on each; chain_mode
+// 0 = ChainOwnership::kForward (the consumer frees the chains, as RegionsToSam
+// does), 1 = kFree.  times[0] = wall seconds from the first record in to the
+// last record out and every chain freed, times[1..4] = the stage's phase
+// totals (pack, submit, wait, post; summed over workers), times[5] = records
+// on the GPU, times[6] = records the CPU fallback took, times[7] = stage
+// workers (contexts) used, times[8..9] = device kernels / H2D + results (HIP
+// events, summed over the GPU records).  The regions of the LAST rep of batch
+// k go to out_n[k][r] / out_regs[k] (compact, read order).  Returns 0, or the
+// number of records whose chains were not where the mode puts them.
 int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t* pac, int n_batches,
-                 const bwagpu_batch_t* batches, int reps, int max_devices, int per_device, double* times,
-                 int32_t** out_n, bwagpu_alnreg_t** out_regs) {
-  if (!opt || !bns || !pac || n_batches <= 0 || !batches || reps <= 0 || !times || per_device < 1) return -1;
+                 const bwagpu_batch_t* batches, int reps, int max_devices, int per_device, int chain_mode,
+                 double* times, int32_t** out_n, bwagpu_alnreg_t** out_regs) {
+  if (!opt || !bns || !pac || n_batches <= 0 || !batches || reps <= 0 || !times || per_device < 1 ||
+      chain_mode < 0 || chain_mode > 1)
+    return -1;
+  const ChainOwnership own = chain_mode == 0 ? ChainOwnership::kForward : ChainOwnership::kFree;
   GPUEnv env(*opt, *bns, pac, max_devices, 10000, per_device);
   const int n_dev = env.num_devices();
   if (n_dev == 0) return -2;
@@ -82,7 +91,7 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
     for (int k = 0; k < n_batches; ++k)
       recs.push_back(make_record(batches[k], seqs[k].data(), (uint64_t)(rep * n_batches + k)));
 
-  ChainsToRegionsGPU stage(n_dev, nullptr, &env);
+  ChainsToRegionsGPU stage(n_dev, nullptr, &env, own);
   kestrelFlow::Pipeline pipe(1);
   pipe.addStage(0, &stage);
   pipe.start();
@@ -93,7 +102,12 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
     for (size_t got = 0; got < recs.size(); ++got) {
       RegionsRecord o;
       q->pop(o);
-      if (o.chains != nullptr) ++bad;
+      if (own == ChainOwnership::kForward) {
+        if (o.chains == nullptr && o.batch_num > 0) ++bad;
+        freeChainsRecordChains(o.chains, o.batch_num);  // RegionsToSam (Pipeline.cpp:559)
+      } else if (o.chains != nullptr) {
+        ++bad;
+      }
       const int k = (int)(o.start_idx % (uint64_t)n_batches);
       const bool keep = o.start_idx / (uint64_t)n_batches == (uint64_t)(reps - 1) && out_n && out_regs;
       size_t at = 0;
@@ -122,6 +136,7 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
   times[5] = stage.records_on_gpu();
   times[6] = stage.records_on_cpu();
   times[7] = n_dev;
+  stage.device_seconds(times + 8);
   return bad;
 }
 

@@ -133,6 +133,7 @@ PROTOS = {
     "bwagpu_chain2aln_stage": (C.c_int, [_VP, C.c_int, C.c_int32, C.c_int32, C.c_int32, C.c_int64,
                                          C.POINTER(BatchC)]),
     "bwagpu_chain2aln_results": (C.c_int, [_VP, C.c_int, C.POINTER(_VP), C.POINTER(_VP)]),
+    "bwagpu_chain2aln_results_dense": (C.c_int, [_VP, C.c_int, C.POINTER(_VP), C.POINTER(_VP), C.POINTER(_VP)]),
     "bwagpu_chain2aln": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP]),
     "bwagpu_chain2aln_device": (C.c_int, [_VP, C.POINTER(BatchC), _VP, _VP, _VP, _VP]),
     "bwagpu_extend_batch": (C.c_int, [_VP, C.c_int32, _VP, _VP, C.c_int64, _VP, C.c_int64, _VP]),
@@ -152,6 +153,8 @@ PROTOS = {
     "bwagpu_debug_sup_shift": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_set_device_read_len": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_debug_ext_form": (C.c_int, [C.c_int]),
+    "bwagpu_ctx_ext_form": (C.c_int, [_VP, C.c_int]),
+    "bwagpu_debug_ext_kernel": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_bwt_sa": (C.c_int, [_VP, C.c_int64, _VP, _VP]),
     "bwagpu_sw_stream": (C.c_int, [_VP, _VP, C.c_int64, _VP, C.c_int32, C.POINTER(C.c_int32)]),
     "bwagpu_collect_intv": (C.c_int, [_VP, C.POINTER(SeedOpt), C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int64,

@@ -174,6 +174,28 @@ class Engine:
         self._check(self.lib.bwagpu_chain2aln_wait(self.ctx, slot, _ptr(regs), _ptr(n)), "wait")
         return regs[:batch.n_seeds], n[:batch.n_reads]
 
+    def wait_dense(self, slot: int, batch: Batch, out=None):
+        """-> (regs, n): the slot's results in read order without slot gaps
+        (bwagpu_chain2aln_results_dense: only these regions crossed PCIe);
+        `out` = (regs, n) arrays to fill instead of fresh ones"""
+        self._check(self.lib.bwagpu_chain2aln_wait(self.ctx, slot, None, None), "wait")
+        rp, np_, op = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(self.lib.bwagpu_chain2aln_results_dense(self.ctx, slot, C.byref(rp), C.byref(np_), C.byref(op)),
+                    "results_dense")
+        nr = batch.n_reads
+        cnt = np.ctypeslib.as_array(C.cast(np_, C.POINTER(C.c_int32)), (max(nr, 1),))[:nr] if nr else np.zeros(0, np.int32)
+        tot = int(np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_int32)), (nr + 1,))[nr])
+        if out is None:
+            regs, n = np.zeros(max(tot, 1), abi.ALNREG_DTYPE), np.zeros(max(nr, 1), np.int32)
+        else:
+            regs, n = out
+            if len(regs) < tot or len(n) < nr:
+                raise ValueError("wait_dense: out arrays too small")
+        n[:nr] = cnt
+        if tot:
+            C.memmove(regs.ctypes.data, rp.value, tot * abi.ALNREG_DTYPE.itemsize)
+        return regs[:tot], n[:nr]
+
     def chain2aln_device(self, dev_batch: abi.BatchC, dev_out: int, dev_n: int, dev_stats: int | None,
                          stream: int | None):
         self._check(self.lib.bwagpu_chain2aln_device(self.ctx, C.byref(dev_batch), C.c_void_p(dev_out),
@@ -256,25 +278,22 @@ class Engine:
                                               C.byref(n)), "sw_stream")
         return out[:n.value]
 
-    def quad_ok(self, lq: int = 256) -> bool:
-        """whether the first two read-length bins run four seeds per wave with
-        these options (spec.hip quad_scores_ok: every score of a read of
-        up to lq bases fits the packed 16-bit ranges)"""
-        o = self.opt
-        mat = list(o.mat)
-        mm = max(mat) if mat else 0
-        if mm < 1 or mm > 15 or min(mat) < -127:
-            return False
-        sk = int(mm).bit_length()
-        hb = lq * mm
-        return (hb < 4096 and (hb << sk) + 128 < 32768 and hb + 33 * 8 * o.e_ins < 32768
-                and o.o_del + 128 < 32768 and o.o_ins + o.e_ins + 128 < 32768 and o.e_del < 32768
-                and (lq + 2 * o.w + 18 + 256) * max(o.e_del, o.e_ins) < 28672)  # quad_rows_ok(tb rows)
+    # bwagpu_debug_ext_kernel codes -> the first bin's extension kernel
+    EXT_KERNELS = {8: "spec_ext4_kernel<16, 10, true>", 4: "spec_ext4_kernel<32, 5, true>",
+                   5: "spec_ext4_kernel<32, 8, false>", 2: "spec_ext2_kernel<5>"}
 
-    def quad_key8_ok(self, lq: int = 160) -> bool:
-        """whether reads of up to lq bases take the 8-bit-column row-max key
-        (spec.hip quad_key8_ok: every H < 256)"""
-        return lq * max(list(self.opt.mat)) <= 255
+    def ext_kernel(self, lq_max: int = 256) -> str:
+        """the first length bin's extension kernel this context launches for
+        reads of up to lq_max bases (the C side's own decision, spec.hip
+        ext_kernel_for)"""
+        k = self.lib.bwagpu_debug_ext_kernel(self.ctx, int(lq_max))
+        if k not in self.EXT_KERNELS:
+            raise BwaGpuError(k, "debug_ext_kernel")
+        return self.EXT_KERNELS[k]
+
+    def ext_form(self, form: int = -1) -> int:
+        """this context's extension form (bwagpu_ctx_ext_form); -> the previous one"""
+        return self.lib.bwagpu_ctx_ext_form(self.ctx, int(form))
 
     def set_device_read_len(self, max_len: int):
         """bound on the read lengths of later device batches (bwagpu_set_device_read_len)"""

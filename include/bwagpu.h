@@ -340,6 +340,14 @@ int bwagpu_chain2aln(bwagpu_ctx_t *ctx, const bwagpu_batch_t *batch, bwagpu_alnr
 int bwagpu_chain2aln_stage(bwagpu_ctx_t *ctx, int slot, int32_t n_reads, int32_t n_chains, int32_t n_seeds,
                            int64_t seq_bytes, bwagpu_batch_t *view);
 int bwagpu_chain2aln_results(bwagpu_ctx_t *ctx, int slot, const bwagpu_alnreg_t **regs, const int32_t **n);
+/* The same results as the device returns them: read r's n[r] regions at
+   regs[off[r] .. off[r] + n[r]) (off[r] = n[0] + ... + n[r-1], off has n_reads
+   + 1 entries), i.e. processOutput's order without the slot gaps
+   (FPGAPipeline.cpp:29-130).  Only these bytes cross PCIe; _results and
+   _wait's out_regs rebuild the slot layout from them on the host.  Valid until
+   the slot's next _submit. */
+int bwagpu_chain2aln_results_dense(bwagpu_ctx_t *ctx, int slot, const bwagpu_alnreg_t **regs, const int32_t **n,
+                                   const int32_t **off);
 /* all pointers in dev_batch / dev_out / dev_n are device pointers; stream is a
    hipStream_t (NULL = the context's slot-0 stream); asynchronous; dev_stats
    (device, 4 x int64: cells, rows, ext_calls, error flag) may be NULL.
@@ -523,12 +531,20 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
    last device-entry batch on `stream`, n = its seed count */
 int bwagpu_debug_spec_ext(bwagpu_ctx_t *ctx, void *stream, void *host_out, int32_t n);
 int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
-/* tests / A-B (process-wide): the extension kernel of the first two read-length
-   bins — 0 (default) packed 16-bit DP where every score of the bin fits (else
-   two per wave): eight seeds per wave in the first bin, four in the second;
-   1 two seeds per wave (32-bit DP); 2 four seeds per wave in both bins;
-   returns the previous form, form < 0 only queries.  Results do not depend on it. */
+/* tests / A-B: the extension kernel of the first two read-length bins — 0
+   (default) packed 16-bit DP where every score of the bin fits (else two per
+   wave): eight seeds per wave in the first bin, four in the second; 1 two
+   seeds per wave (32-bit DP); 2 four seeds per wave in both bins.  Results do
+   not depend on it.  bwagpu_ctx_ext_form sets one context's form;
+   bwagpu_debug_ext_form sets the form contexts created afterwards start with.
+   Both return the previous form; form < 0 only queries. */
 int bwagpu_debug_ext_form(int form);
+int bwagpu_ctx_ext_form(bwagpu_ctx_t *ctx, int form);
+/* the first length bin's extension kernel this context launches for reads of
+   up to lq_max bases: 8 = eight seeds per wave (spec_ext4_kernel<16,10,true>),
+   4 = four per wave with the 8-bit row-max key (<32,5,true>), 5 = four per
+   wave (<32,8,false>), 2 = two per wave (spec_ext2_kernel<5>) */
+int bwagpu_debug_ext_kernel(bwagpu_ctx_t *ctx, int32_t lq_max);
 int bwagpu_prof_intervals(bwagpu_ctx_t *ctx, double *start_ms, double *end_ms, int32_t max, int32_t *n);
 
 #ifdef __cplusplus

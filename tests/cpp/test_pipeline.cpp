@@ -19,6 +19,9 @@
 //   mode gpu_badrid the sole stage, record 1 holding a chain outside its
 //                   contig: the error path (reported, chain skipped), the
 //                   device stays in service
+// TEST_CHAIN_MODE=free: the GPU stage frees the chains (the CPU stage's
+// ownership) instead of forwarding them (the FPGA stage's, the default); the
+// consumer frees forwarded chains as RegionsToSam does (Pipeline.cpp:559)
 //   mode reaper     no stage: every record's chains go through a ChainReaper
 //                   (the GPU stage's background frees) from cpu_workers
 //                   threads at once; after drain() the heap must be back to
@@ -198,7 +201,10 @@ int main(int argc, char** argv) {
         bad_rid_read = (int)rr.start_idx + i;
       }
   }
-  ChainsToRegionsGPU gpu_stage(mode == "accx_none" ? 2 : std::max(n_dev, 1), &cpu_stage, env);
+  const char* cm = getenv("TEST_CHAIN_MODE");
+  const bool free_mode = cm && std::string(cm) == "free";
+  ChainsToRegionsGPU gpu_stage(mode == "accx_none" ? 2 : std::max(n_dev, 1), &cpu_stage, env,
+                               free_mode ? ChainOwnership::kFree : ChainOwnership::kForward);
   kestrelFlow::Pipeline pipe(1);
   if (sole) {
     pipe.addStage(0, &gpu_stage);
@@ -226,9 +232,13 @@ int main(int argc, char** argv) {
             [](const RegionsRecord& a, const RegionsRecord& b) { return a.start_idx < b.start_idx; });
   FILE* fr = fopen((dir + "/out_regs.bin").c_str(), "wb");
   FILE* fn = fopen((dir + "/out_n.bin").c_str(), "wb");
-  int bad = 0;
+  int bad = 0, forwarded = 0;
   for (auto& o : outs) {
-    if (o.chains != nullptr) bad++;  // ownership: chains freed, NULL forwarded
+    if (o.chains != nullptr) {  // forwarded: RegionsToSam's free (Pipeline.cpp:559)
+      forwarded++;
+      if (free_mode) bad++;  // the stage should have freed them and forwarded NULL
+      freeChainsRecordChains(o.chains, o.batch_num);
+    }
     for (int i = 0; i < o.batch_num; ++i) {
       const int32_t k = (int32_t)o.alnreg[i].n;
       fwrite(&k, 4, 1, fn);
@@ -240,9 +250,9 @@ int main(int argc, char** argv) {
   fclose(fr);
   fclose(fn);
   printf("{\"records\": %zu, \"outputs\": %zu, \"on_gpu\": %d, \"gpu_fallback_cpu\": %d, \"devices\": %d, "
-         "\"bad_ownership\": %d, \"failed\": %d, \"bad_rid_read\": %d, \"w0\": %d, \"w1\": %d, "
+         "\"bad_ownership\": %d, \"forwarded\": %d, \"failed\": %d, \"bad_rid_read\": %d, \"w0\": %d, \"w1\": %d, "
          "\"accx_on_at_end\": %d, \"rccl\": %d, \"env\": \"%s\"}\n",
-         recs.size(), outs.size(), gpu_stage.records_on_gpu(), gpu_stage.records_on_cpu(), n_dev, bad,
+         recs.size(), outs.size(), gpu_stage.records_on_gpu(), gpu_stage.records_on_cpu(), n_dev, bad, forwarded,
          gpu_stage.records_failed(), bad_rid_read, gpu_stage.records_of_worker(0), gpu_stage.records_of_worker(1),
          cpu_stage.useAccx() ? 1 : 0, env && env->used_rccl() ? 1 : 0, env ? env->status().c_str() : "");
   const int failed = gpu_stage.records_failed();

@@ -44,8 +44,10 @@ def write_inputs(d, name):
     return b, regs, n
 
 
-def run(exe, d, mode, per_rec, workers, rc=0):
-    p = subprocess.run([exe, d, mode, str(per_rec), str(workers)], capture_output=True, text=True, timeout=600)
+def run(exe, d, mode, per_rec, workers, rc=0, chain_mode="forward"):
+    env = dict(os.environ, TEST_CHAIN_MODE=chain_mode)
+    p = subprocess.run([exe, d, mode, str(per_rec), str(workers)], capture_output=True, text=True, timeout=600,
+                       env=env)
     assert p.returncode == rc, p.stderr
     info = json.loads(p.stdout.strip().splitlines()[-1])
     n = np.fromfile(os.path.join(d, "out_n.bin"), np.int32)
@@ -109,14 +111,20 @@ def test_chain_reaper_bounded_queue(exe, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_default", "c5_mixed"])
 @pytest.mark.parametrize("mode", ["gpu", "gpu_only"])
-def test_pipeline_gpu_stage(exe, tmp_path, name, mode):
+@pytest.mark.parametrize("chain_mode", ["forward", "free"])
+def test_pipeline_gpu_stage(exe, tmp_path, name, mode, chain_mode):
+    """chain ownership: forwarded in the GPU records for RegionsToSam to free
+    (the FPGA stage's, FPGAPipeline.cpp:434) or freed by the stage with NULL
+    forwarded (the CPU stage's, Pipeline.cpp:526-537); records the CPU stage
+    made always carry NULL"""
     d = str(tmp_path)
     b, want_regs, want_n = write_inputs(d, name)
-    info, regs, n = run(exe, d, mode, 50, 2)
+    info, regs, n = run(exe, d, mode, 50, 2, chain_mode=chain_mode)
     assert info["devices"] >= 1 and info["on_gpu"] > 0 and info["gpu_fallback_cpu"] == 0
     if mode == "gpu_only":
         assert info["on_gpu"] == info["records"]
     assert info["bad_ownership"] == 0
+    assert info["forwarded"] == (info["on_gpu"] if chain_mode == "forward" else 0), info
     check(regs, n, want_regs, want_n)
 
 

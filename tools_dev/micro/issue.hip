@@ -33,6 +33,16 @@ __global__ void k(int* out, int seed) {
       REP8(asm volatile("s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0");)
     } else if (MODE == 9) {  // 16 VALU + 16 SALU, SALU dependent chain (like band bookkeeping)
       REP8(asm volatile("v_add_u32 %0, %0, %1\n s_mul_i32 %4, %4, %5\n v_xor_b32 %2, %2, %3\n s_mul_hi_u32 %4, %4, %5" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+s"(s0), "+s"(s1));)
+    } else if (MODE == 10) {  // 32 packed 16-bit add/max on 4 independent chains (extend_quad's bulk)
+      REP8(asm volatile("v_pk_add_u16 %0, %0, %1\n v_pk_max_i16 %2, %2, %3\n v_pk_add_u16 %1, %1, %0\n v_pk_max_i16 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 11) {  // 32 packed 16-bit min/sub-saturate on 4 independent chains
+      REP8(asm volatile("v_pk_min_u16 %0, %0, %1\n v_pk_sub_u16 %2, %2, %3 clamp\n v_pk_min_u16 %1, %1, %0\n v_pk_sub_u16 %3, %3, %2 clamp" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 12) {  // 32 v_perm / v_bfi / v_bitop3 / v_pk_mad_u16
+      REP8(asm volatile("v_perm_b32 %0, %1, %2, %3\n v_bfi_b32 %1, %2, %3, %0\n v_bitop3_b32 %2, %3, %0, %1 bitop3:0xca\n v_pk_mad_u16 %3, %0, %1, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 13) {  // 32 packed 16-bit ops, ONE dependent chain
+      REP8(asm volatile("v_pk_add_u16 %0, %0, %1\n v_pk_max_i16 %0, %0, %1\n v_pk_sub_u16 %0, %0, %1 clamp\n v_pk_min_u16 %0, %0, %1" : "+v"(v0) : "v"(v1));)
+    } else if (MODE == 14) {  // 32 plain 32-bit max/min/sub on 4 chains (the unpacked form of mode 10)
+      REP8(asm volatile("v_max_i32 %0, %0, %1\n v_min_u32 %2, %2, %3\n v_sub_u32 %1, %1, %0\n v_max_i32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
     }
   }
   if ((v0 ^ v1 ^ v2 ^ v3 ^ s0 ^ s1 ^ s2 ^ s3) == 0x12345) out[threadIdx.x] = 1;
@@ -46,9 +56,12 @@ int main() {
   int* out;
   hipMalloc(&out, 4096 * 4);
   const char* names[] = {"VALU indep", "SALU indep", "VALU+SALU mix", "DPP 4 chains", "DPP+s_nop1 1 chain",
-                         "VALU dep chain", "SALU dep chain", "readlane rt", "s_nop 0", "VALU + SALU chain"};
+                         "VALU dep chain", "SALU dep chain", "readlane rt", "s_nop 0", "VALU + SALU chain",
+                         "pk16 add/max 4 chains", "pk16 min/subsat 4 chains", "perm/bfi/bitop3/pk_mad",
+                         "pk16 dep chain", "i32 max/min/sub 4 chains"};
   printf("{\"cus\": %d, \"clock_khz\": %d, \"results\": [\n", ncu, clk);
-  for (int mode = 0; mode < 10; ++mode) {
+  const int m0 = getenv("ISSUE_MODE0") ? atoi(getenv("ISSUE_MODE0")) : 0;
+  for (int mode = m0; mode < 15; ++mode) {
     for (int W : {1, 2, 4, 5, 8}) {
       hipEvent_t a, b;
       hipEventCreate(&a);
@@ -66,6 +79,11 @@ int main() {
           case 7: hipLaunchKernelGGL(k<7>, g, blk, 0, 0, out, 1); break;
           case 8: hipLaunchKernelGGL(k<8>, g, blk, 0, 0, out, 1); break;
           case 9: hipLaunchKernelGGL(k<9>, g, blk, 0, 0, out, 1); break;
+          case 10: hipLaunchKernelGGL(k<10>, g, blk, 0, 0, out, 1); break;
+          case 11: hipLaunchKernelGGL(k<11>, g, blk, 0, 0, out, 1); break;
+          case 12: hipLaunchKernelGGL(k<12>, g, blk, 0, 0, out, 1); break;
+          case 13: hipLaunchKernelGGL(k<13>, g, blk, 0, 0, out, 1); break;
+          case 14: hipLaunchKernelGGL(k<14>, g, blk, 0, 0, out, 1); break;
         }
       };
       launch();
@@ -80,7 +98,7 @@ int main() {
       const int per_iter = (mode == 4) ? 16 : (mode == 7 ? 32 : 32);
       const double per_instr_simd = cycles / ((double)ITERS * per_iter * W);  // SIMD cycles per wave-instruction
       printf("  {\"mode\": \"%s\", \"waves_per_simd\": %d, \"us\": %.1f, \"simd_cycles_per_instr\": %.3f}%s\n", names[mode],
-             W, ms / 5 * 1e3, per_instr_simd, (mode == 9 && W == 8) ? "" : ",");
+             W, ms / 5 * 1e3, per_instr_simd, (mode == 14 && W == 8) ? "" : ",");
     }
   }
   printf("]}\n");
