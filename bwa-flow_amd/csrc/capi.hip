@@ -648,7 +648,12 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   s.spec.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
   s.spec.pool_n = (int)ctx->prof_ev.size();
   s.spec.pool_used = &ctx->prof_used;
-  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, s.spec), "spec chain2aln launch");
+  SpecStreams ss = s.spec;
+  {
+    const char* pe = getenv("BWAGPU_SIDE_PRIO");
+    if (pe && pe[0] == '3') ss.side = nullptr;  // A/B: heavy selection on the caller's stream
+  }
+  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, ss), "spec chain2aln launch");
   return BWAGPU_OK;
 }
 

@@ -6,9 +6,9 @@
 // through a kflow pipeline whose stage 4 is ChainsToRegionsGPU alone
 // (--disable_sw_cpu, main.cpp:320-329): FlatBatch::pack -> bwagpu submit (pinned
 // staging, H2D, kernels, the regions written densely to pinned memory) -> wait ->
-// malloc'd mem_alnreg_v per read; a consumer thread plays RegionsToSam: it
-// frees the regions, and the chains when the stage forwards them
-// (ChainOwnership::kForward, the FPGA stage's way; kFree: the stage frees them).
+// malloc'd mem_alnreg_v per read; a second stage of sink_workers threads plays
+// RegionsToSam: it frees the regions, and the chains when the stage forwards
+// them (ChainOwnership::kForward, the FPGA stage's way; kFree: the stage frees them).
 // The records are built before the clock starts (that is SeqsToChains' work).
 #include <stdlib.h>
 #include <string.h>
@@ -50,13 +50,52 @@ ChainsRecord make_record(const bwagpu_batch_t& b, bseq1_t* seqs, uint64_t start_
   return rec;
 }
 
+// RegionsToSam's side of the records (src/Pipeline.cpp:547-560): frees the
+// chains a record carries (Pipeline.cpp:559) and its regions, on n workers
+// like the real stage; keeps the regions of the last rep for the parity check.
+class RegionsSink : public kestrelFlow::MapStage<RegionsRecord, int, COMPUTE_DEPTH, COMPUTE_DEPTH> {
+ public:
+  RegionsSink(int n, ChainOwnership own, int n_batches, int reps, int32_t** out_n, bwagpu_alnreg_t** out_regs)
+      : kestrelFlow::MapStage<RegionsRecord, int, COMPUTE_DEPTH, COMPUTE_DEPTH>(n),
+        own_(own), n_batches_(n_batches), reps_(reps), out_n_(out_n), out_regs_(out_regs) {}
+  int compute(RegionsRecord const& o) override {
+    int bad = 0;
+    if (own_ == ChainOwnership::kForward) {
+      if (o.chains == nullptr && o.batch_num > 0) bad = 1;
+      freeChainsRecordChains(o.chains, o.batch_num);
+    } else if (o.chains != nullptr) {
+      bad = 1;
+    }
+    const int k = (int)(o.start_idx % (uint64_t)n_batches_);
+    const bool keep = o.start_idx / (uint64_t)n_batches_ == (uint64_t)(reps_ - 1) && out_n_ && out_regs_;
+    size_t at = 0;
+    for (int r = 0; r < o.batch_num; ++r) {
+      const size_t m = o.alnreg[r].n;
+      if (keep) {
+        out_n_[k][r] = (int32_t)m;
+        if (m) memcpy(out_regs_[k] + at, o.alnreg[r].a, sizeof(bwagpu_alnreg_t) * m);
+        at += m;
+      }
+      free(o.alnreg[r].a);
+    }
+    free(o.alnreg);
+    return bad;
+  }
+
+ private:
+  ChainOwnership own_;
+  int n_batches_, reps_;
+  int32_t** out_n_;
+  bwagpu_alnreg_t** out_regs_;
+};
+
 }  // namespace
 
 extern "C" {
 
 // Runs reps x n_batches records through the stage on up to max_devices
 // devices with per_device stage workers (bwagpu contexts) on each; chain_mode
-// 0 = ChainOwnership::kForward (the consumer frees the chains, as RegionsToSam
+// 0 = ChainOwnership::kForward (the sink stage frees the chains, as RegionsToSam
 // does), 1 = kFree.  times[0] = wall seconds from the first record in to the
 // last record out and every chain freed, times[1..4] = the stage's phase
 // totals (pack, submit, wait, post; summed over workers), times[5] = records
@@ -67,9 +106,9 @@ extern "C" {
 // number of records whose chains were not where the mode puts them.
 int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t* pac, int n_batches,
                  const bwagpu_batch_t* batches, int reps, int max_devices, int per_device, int chain_mode,
-                 double* times, int32_t** out_n, bwagpu_alnreg_t** out_regs) {
+                 int sink_workers, double* times, int32_t** out_n, bwagpu_alnreg_t** out_regs) {
   if (!opt || !bns || !pac || n_batches <= 0 || !batches || reps <= 0 || !times || per_device < 1 ||
-      chain_mode < 0 || chain_mode > 1)
+      chain_mode < 0 || chain_mode > 1 || sink_workers < 1)
     return -1;
   const ChainOwnership own = chain_mode == 0 ? ChainOwnership::kForward : ChainOwnership::kFree;
   GPUEnv env(*opt, *bns, pac, max_devices, 10000, per_device);
@@ -92,35 +131,19 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
       recs.push_back(make_record(batches[k], seqs[k].data(), (uint64_t)(rep * n_batches + k)));
 
   ChainsToRegionsGPU stage(n_dev, nullptr, &env, own);
-  kestrelFlow::Pipeline pipe(1);
+  RegionsSink sink(sink_workers, own, n_batches, reps, out_n, out_regs);
+  kestrelFlow::Pipeline pipe(2);
   pipe.addStage(0, &stage);
+  pipe.addStage(1, &sink);
   pipe.start();
   int bad = 0;
   std::chrono::steady_clock::time_point t_end;
-  std::thread consumer([&] {  // RegionsToSam's side: take the records, free the regions
-    auto* q = pipe.output<RegionsRecord>();
+  std::thread consumer([&] {
+    auto* q = pipe.output<int>();
     for (size_t got = 0; got < recs.size(); ++got) {
-      RegionsRecord o;
-      q->pop(o);
-      if (own == ChainOwnership::kForward) {
-        if (o.chains == nullptr && o.batch_num > 0) ++bad;
-        freeChainsRecordChains(o.chains, o.batch_num);  // RegionsToSam (Pipeline.cpp:559)
-      } else if (o.chains != nullptr) {
-        ++bad;
-      }
-      const int k = (int)(o.start_idx % (uint64_t)n_batches);
-      const bool keep = o.start_idx / (uint64_t)n_batches == (uint64_t)(reps - 1) && out_n && out_regs;
-      size_t at = 0;
-      for (int r = 0; r < o.batch_num; ++r) {
-        const size_t m = o.alnreg[r].n;
-        if (keep) {
-          out_n[k][r] = (int32_t)m;
-          if (m) memcpy(out_regs[k] + at, o.alnreg[r].a, sizeof(bwagpu_alnreg_t) * m);
-          at += m;
-        }
-        free(o.alnreg[r].a);
-      }
-      free(o.alnreg);
+      int b = 0;
+      q->pop(b);
+      bad += b;
     }
     t_end = std::chrono::steady_clock::now();
   });

@@ -25,7 +25,8 @@ def set_c2a_path(path, monkeypatch):
       pair  the same with two seeds per wave (32-bit DP; bwagpu_debug_ext_form(1))
       fast  the per-read kernels (BWAGPU_C2A_PATH=fast: a wave per read), an
             independent implementation kept as a cross-check
-    The extension form is process-wide: restored by the caller's teardown."""
+    The form is the default of contexts created afterwards (bwagpu_debug_ext_form;
+    bwagpu_ctx_ext_form sets one context's): restored by the caller's teardown."""
     from bwagpu import abi
     lib = abi.load()
     if path == "fast":

@@ -335,3 +335,49 @@ def test_many_seed_reads_vs_oracle(len_mode, piece, c2a_path):
     assert np.array_equal(n, on)
     assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
     eng.close()
+
+
+def far_seed_batch(b: Batch, ann_offset, ann_len, dist: int, n_reads: int) -> Batch:
+    """a copy of the batch where the first chain of each of the first n_reads
+    reads with a forward-strand chain gets one more seed `dist` bases
+    downstream of its first seed (same query interval): a chain window of
+    more than `dist` bases, as a chain collected along a tandem repeat has"""
+    seeds, cso = [], [0]
+    done = 0
+    for c in range(b.n_chains):
+        s0, s1 = int(b.chain_seed_off[c]), int(b.chain_seed_off[c + 1])
+        chain = [tuple(int(x) for x in sd) for sd in b.seeds[s0:s1]]
+        first_of_read = c in set(int(x) for x in b.read_chain_off[:-1])
+        if chain and first_of_read and done < n_reads:
+            rid = int(b.chain_rid[c])
+            rb, qb, ln, sc, _ = chain[0]
+            end = int(ann_offset[rid]) + int(ann_len[rid])
+            if rb >= int(ann_offset[rid]) and rb + dist + ln < end:
+                chain.append((rb + dist, qb, ln, sc, 0))
+                done += 1
+        seeds.extend(chain)
+        cso.append(len(seeds))
+    assert done == n_reads
+    arr = np.array(seeds, dtype=abi.SEED_DTYPE)
+    return Batch(b.seq_off, b.seq, b.read_chain_off, np.array(cso, np.int32), b.chain_rid, b.chain_frac_rep, arr)
+
+
+@pytest.mark.parametrize("dist", [40_000, 70_000])
+def test_chain_window_past_16_bits(refd, dist, c2a_path):
+    """chain windows of 40 and 70 kb: a seed's target length (the window
+    distance, ksw_extend2's tlen) no longer fits the packed kernels' 16-bit
+    row counters; rows past qlen + w + 1 have an empty band (ksw.c:415-419),
+    so the call is capped there with every output unchanged, on every path,
+    against the oracle"""
+    opt, batch, _, _ = G.load_chain_set("c1_default")
+    sub = batch.subset(range(400))
+    b = far_seed_batch(sub, refd["ann_offset"], refd["ann_len"], dist, 120)
+    eng = make_engine(refd, opt)
+    regs, n = eng.chain2aln(b)
+    st = eng.last_stats()
+    ref = oracle.Ref(refd["l_pac"], refd["ann_offset"], refd["ann_len"], refd["pac"])
+    oregs, on, ost = oracle.chain2aln("oracle", opt, ref, b)
+    assert np.array_equal(n, on), f"{int((n != on).sum())} reads with a different region count"
+    assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
+    assert (st["cells"], st["rows"], st["ext_calls"]) == tuple(int(x) for x in ost[:3])
+    eng.close()

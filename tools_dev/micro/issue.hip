@@ -41,6 +41,26 @@ __global__ void k(int* out, int seed) {
       REP8(asm volatile("v_perm_b32 %0, %1, %2, %3\n v_bfi_b32 %1, %2, %3, %0\n v_bitop3_b32 %2, %3, %0, %1 bitop3:0xca\n v_pk_mad_u16 %3, %0, %1, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
     } else if (MODE == 13) {  // 32 packed 16-bit ops, ONE dependent chain
       REP8(asm volatile("v_pk_add_u16 %0, %0, %1\n v_pk_max_i16 %0, %0, %1\n v_pk_sub_u16 %0, %0, %1 clamp\n v_pk_min_u16 %0, %0, %1" : "+v"(v0) : "v"(v1));)
+    } else if (MODE == 15) {  // 32 packed f16 add/max on 4 chains
+      REP8(asm volatile("v_pk_add_f16 %0, %0, %1\n v_pk_max_f16 %2, %2, %3\n v_pk_add_f16 %1, %1, %0\n v_pk_max_f16 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 16) {  // 32 packed f16 maximum3 / minimum3 on 4 chains
+      REP8(asm volatile("v_pk_maximum3_f16 %0, %0, %1, %2\n v_pk_minimum3_f16 %1, %1, %2, %3\n v_pk_maximum3_f16 %2, %2, %3, %0\n v_pk_minimum3_f16 %3, %3, %0, %1" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 17) {  // 32 packed f16 fma / mul on 4 chains
+      REP8(asm volatile("v_pk_fma_f16 %0, %0, %1, %2\n v_pk_mul_f16 %1, %1, %2\n v_pk_fma_f16 %2, %2, %3, %0\n v_pk_mul_f16 %3, %3, %0" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 18) {  // 32 i32 add / sub on 4 chains
+      REP8(asm volatile("v_add_u32 %0, %0, %1\n v_sub_u32 %2, %2, %3\n v_add_u32 %1, %1, %0\n v_sub_u32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 19) {  // 32 i32 max on 4 chains
+      REP8(asm volatile("v_max_i32 %0, %0, %1\n v_max_i32 %2, %2, %3\n v_max_i32 %1, %1, %0\n v_max_i32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 20) {  // 32 i32 max3 / add3 on 4 chains
+      REP8(asm volatile("v_max3_i32 %0, %0, %1, %2\n v_add3_u32 %1, %1, %2, %3\n v_max3_i32 %2, %2, %3, %0\n v_add3_u32 %3, %3, %0, %1" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 21) {  // 32 f32 add / max on 4 chains
+      REP8(asm volatile("v_add_f32 %0, %0, %1\n v_max_f32 %2, %2, %3\n v_add_f32 %1, %1, %0\n v_max_f32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 22) {  // 32 v_xor / v_and / v_or / v_not on 4 chains
+      REP8(asm volatile("v_xor_b32 %0, %0, %1\n v_and_b32 %2, %2, %3\n v_or_b32 %1, %1, %0\n v_xor_b32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 23) {  // 32 v_pk_add_u16 only on 4 chains
+      REP8(asm volatile("v_pk_add_u16 %0, %0, %1\n v_pk_add_u16 %2, %2, %3\n v_pk_add_u16 %1, %1, %0\n v_pk_add_u16 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
+    } else if (MODE == 24) {  // 32 v_cndmask / v_bfi on 4 chains
+      REP8(asm volatile("v_bfi_b32 %0, %0, %1, %2\n v_bfi_b32 %1, %1, %2, %3\n v_bfi_b32 %2, %2, %3, %0\n v_bfi_b32 %3, %3, %0, %1" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
     } else if (MODE == 14) {  // 32 plain 32-bit max/min/sub on 4 chains (the unpacked form of mode 10)
       REP8(asm volatile("v_max_i32 %0, %0, %1\n v_min_u32 %2, %2, %3\n v_sub_u32 %1, %1, %0\n v_max_i32 %3, %3, %2" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));)
     }
@@ -58,10 +78,12 @@ int main() {
   const char* names[] = {"VALU indep", "SALU indep", "VALU+SALU mix", "DPP 4 chains", "DPP+s_nop1 1 chain",
                          "VALU dep chain", "SALU dep chain", "readlane rt", "s_nop 0", "VALU + SALU chain",
                          "pk16 add/max 4 chains", "pk16 min/subsat 4 chains", "perm/bfi/bitop3/pk_mad",
-                         "pk16 dep chain", "i32 max/min/sub 4 chains"};
+                         "pk16 dep chain", "i32 max/min/sub 4 chains", "pk f16 add/max", "pk f16 maximum3/minimum3",
+                         "pk f16 fma/mul", "i32 add/sub", "i32 max", "i32 max3/add3", "f32 add/max", "xor/and/or",
+                         "pk u16 add only", "bfi"};
   printf("{\"cus\": %d, \"clock_khz\": %d, \"results\": [\n", ncu, clk);
   const int m0 = getenv("ISSUE_MODE0") ? atoi(getenv("ISSUE_MODE0")) : 0;
-  for (int mode = m0; mode < 15; ++mode) {
+  for (int mode = m0; mode < 25; ++mode) {
     for (int W : {1, 2, 4, 5, 8}) {
       hipEvent_t a, b;
       hipEventCreate(&a);
@@ -84,6 +106,16 @@ int main() {
           case 12: hipLaunchKernelGGL(k<12>, g, blk, 0, 0, out, 1); break;
           case 13: hipLaunchKernelGGL(k<13>, g, blk, 0, 0, out, 1); break;
           case 14: hipLaunchKernelGGL(k<14>, g, blk, 0, 0, out, 1); break;
+          case 15: hipLaunchKernelGGL(k<15>, g, blk, 0, 0, out, 1); break;
+          case 16: hipLaunchKernelGGL(k<16>, g, blk, 0, 0, out, 1); break;
+          case 17: hipLaunchKernelGGL(k<17>, g, blk, 0, 0, out, 1); break;
+          case 18: hipLaunchKernelGGL(k<18>, g, blk, 0, 0, out, 1); break;
+          case 19: hipLaunchKernelGGL(k<19>, g, blk, 0, 0, out, 1); break;
+          case 20: hipLaunchKernelGGL(k<20>, g, blk, 0, 0, out, 1); break;
+          case 21: hipLaunchKernelGGL(k<21>, g, blk, 0, 0, out, 1); break;
+          case 22: hipLaunchKernelGGL(k<22>, g, blk, 0, 0, out, 1); break;
+          case 23: hipLaunchKernelGGL(k<23>, g, blk, 0, 0, out, 1); break;
+          case 24: hipLaunchKernelGGL(k<24>, g, blk, 0, 0, out, 1); break;
         }
       };
       launch();
@@ -98,7 +130,7 @@ int main() {
       const int per_iter = (mode == 4) ? 16 : (mode == 7 ? 32 : 32);
       const double per_instr_simd = cycles / ((double)ITERS * per_iter * W);  // SIMD cycles per wave-instruction
       printf("  {\"mode\": \"%s\", \"waves_per_simd\": %d, \"us\": %.1f, \"simd_cycles_per_instr\": %.3f}%s\n", names[mode],
-             W, ms / 5 * 1e3, per_instr_simd, (mode == 14 && W == 8) ? "" : ",");
+             W, ms / 5 * 1e3, per_instr_simd, (mode == 24 && W == 8) ? "" : ",");
     }
   }
   printf("]}\n");
