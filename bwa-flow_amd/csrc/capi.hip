@@ -633,10 +633,11 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
       HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device), "attribute");
       std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
       HIPC(hipExtStreamCreateWithCUMask(&s.spec.side, (uint32_t)mask.size(), mask.data()), "hipStreamCreate(side)");
-    } else if (pe && pe[0] == '1') {
+    } else if (pe && (pe[0] == '1' || pe[0] == '4')) {
       int least = 0, greatest = 0;
       HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
-      HIPC(hipStreamCreateWithPriority(&s.spec.side, hipStreamNonBlocking, greatest), "hipStreamCreate(side)");
+      HIPC(hipStreamCreateWithPriority(&s.spec.side, hipStreamNonBlocking, pe[0] == '1' ? greatest : least),
+           "hipStreamCreate(side)");
     } else
     HIPC(hipStreamCreateWithFlags(&s.spec.side, hipStreamNonBlocking), "hipStreamCreate(side)");
     HIPC(hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming), "hipEventCreate");

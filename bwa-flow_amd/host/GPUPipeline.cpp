@@ -468,13 +468,22 @@ static bool reaper_enabled() {
   return on;
 }
 
+int ChainReaper::threads() {
+  static const int n = [] {
+    const char* e = getenv("BWAGPU_REAPER_THREADS");
+    return std::max(1, std::min(e ? atoi(e) : 2, 16));
+  }();
+  return n;
+}
+
 ChainReaper::~ChainReaper() {
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
   }
   cv_.notify_all();
-  if (th_.joinable()) th_.join();  // run() frees what is left before it returns
+  for (auto& t : th_)
+    if (t.joinable()) t.join();  // run() frees what is left before it returns
 }
 
 void ChainReaper::release(mem_chain_v* chains, int batch_num) {
@@ -488,7 +497,7 @@ void ChainReaper::release(mem_chain_v* chains, int batch_num) {
     std::lock_guard<std::mutex> g(mu_);
     if (!started_) {
       started_ = true;
-      th_ = std::thread([this] { run(); });
+      for (int k = 0; k < threads(); ++k) th_.emplace_back([this] { run(); });
     }
     // bounded: when the reaper falls behind, the releasing worker frees this
     // record itself (chain memory cannot grow without limit)
@@ -515,7 +524,7 @@ void ChainReaper::hold(bool on) {
 
 void ChainReaper::drain() {
   std::unique_lock<std::mutex> g(mu_);
-  idle_.wait(g, [this] { return q_.empty() && !busy_; });
+  idle_.wait(g, [this] { return q_.empty() && busy_ == 0; });
 }
 
 void ChainReaper::run() {
@@ -525,12 +534,12 @@ void ChainReaper::run() {
     if (q_.empty()) return;  // stop_ and nothing left
     auto job = q_.front();
     q_.pop_front();
-    busy_ = true;
+    ++busy_;
     g.unlock();
     freeChainsRecordChains(job.first, job.second);
     g.lock();
-    busy_ = false;
-    if (q_.empty()) idle_.notify_all();
+    --busy_;
+    if (q_.empty() && busy_ == 0) idle_.notify_all();
   }
 }
 

@@ -98,10 +98,12 @@ struct FlatBatch {
 // frees the chains of a record the way ChainsToRegions::compute does
 void freeChainsRecordChains(mem_chain_v* chains, int batch_num);
 
-// One background thread that frees the records' chains (freeChainsRecordChains)
-// in arrival order, so the stage workers do not: the frees go back into the
-// producing stage's glibc arena, and one thread freeing avoids the workers
-// contending for its lock.  drain() returns once everything queued is freed.
+// Background threads that free the records' chains (freeChainsRecordChains)
+// in arrival order, so the stage workers do not.  A record's chains come from
+// one SeqsToChains worker's glibc arena; one thread per record keeps a
+// record's frees on one arena lock, and several threads free different
+// records (different arenas) at once: threads() of them, BWAGPU_REAPER_THREADS
+// (default 2).  drain() returns once everything queued is freed.
 // BWAGPU_CHAIN_REAPER=0 frees inline on the worker instead.
 class ChainReaper {
  public:
@@ -114,7 +116,8 @@ class ChainReaper {
   // records freed inline because kMaxQueued were already waiting
   int inline_frees() const { return n_inline_.load(); }
   static constexpr size_t kMaxQueued = 4 * BWAGPU_NUM_SLOTS;
-  // tests: while held the thread frees nothing (a reaper that has fallen
+  static int threads();
+  // tests: while held the threads free nothing (a reaper that has fallen
   // behind), so releases past kMaxQueued take the inline path
   void hold(bool on);
 
@@ -123,12 +126,16 @@ class ChainReaper {
   std::mutex mu_;
   std::condition_variable cv_, idle_;
   std::deque<std::pair<mem_chain_v*, int>> q_;
-  bool stop_ = false, busy_ = false, started_ = false, held_ = false;
+  bool stop_ = false, started_ = false, held_ = false;
+  int busy_ = 0;
   std::atomic<int> n_inline_{0};
-  std::thread th_;
+  std::vector<std::thread> th_;
 };
 
-// Who frees a record's chains once its regions are made.
+// Who frees a record's chains once its regions are made.  kFree (the
+// default) frees them on the stage's reaper threads; kForward hands them on
+// exactly as the FPGA stage does.  Either is correct under RegionsToSam,
+// which frees only non-NULL chains (Pipeline.cpp:559).
 enum class ChainOwnership {
   kForward,  // the output record carries them; RegionsToSam frees them (Pipeline.cpp:559),
              // as after ChainsToRegionsFPGA (FPGAPipeline.cpp:434)
@@ -140,7 +147,7 @@ class ChainsToRegionsGPU
     : public kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH> {
  public:
   ChainsToRegionsGPU(int n = 1, ChainsToRegions* stage = nullptr, GPUEnv* env = nullptr,
-                     ChainOwnership own = ChainOwnership::kForward)
+                     ChainOwnership own = ChainOwnership::kFree)
       : kestrelFlow::MapPartitionStage<ChainsRecord, RegionsRecord, COMPUTE_DEPTH, COMPUTE_DEPTH>(n, false),
         n_active_(n),
         cpu_stage_(stage),

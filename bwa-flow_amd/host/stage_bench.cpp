@@ -125,10 +125,21 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
       seqs[k][r].seq = (char*)b.seq + b.seq_off[r];
     }
   }
-  std::vector<ChainsRecord> recs;
-  for (int rep = 0; rep < reps; ++rep)
-    for (int k = 0; k < n_batches; ++k)
-      recs.push_back(make_record(batches[k], seqs[k].data(), (uint64_t)(rep * n_batches + k)));
+  // the records are built by several threads, as SeqsToChains' workers make
+  // them: each record's chains sit in its builder's glibc arena
+  std::vector<ChainsRecord> recs((size_t)reps * n_batches);
+  {
+    std::vector<std::thread> builders;
+    const int nt = 8;
+    for (int t = 0; t < nt; ++t)
+      builders.emplace_back([&, t] {
+        for (size_t i = (size_t)t; i < recs.size(); i += nt) {
+          const int k = (int)(i % (size_t)n_batches);
+          recs[i] = make_record(batches[k], seqs[k].data(), (uint64_t)i);
+        }
+      });
+    for (auto& b : builders) b.join();
+  }
 
   ChainsToRegionsGPU stage(n_dev, nullptr, &env, own);
   RegionsSink sink(sink_workers, own, n_batches, reps, out_n, out_regs);
