@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -94,12 +95,19 @@ struct InLayout {
 };
 
 struct Slot {
+  // created on first use (lazy_stream): the device entry runs on the caller's
+  // streams, and every stream a context creates takes a place on one of the
+  // process's hardware queues (GPU_MAX_HW_QUEUES) the caller's streams and
+  // the selection side streams share
   hipStream_t stream = nullptr;
+  std::once_flag stream_once;
+  hipError_t stream_err = hipSuccess;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
   DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks;
-  SpecStreams spec;  // created on first use
+  SpecStreams spec;  // created on first use (choose_side)
+  bool side_chosen = false;
   void release_scratch() {
     d_win.release(); d_srt.release(); d_prog.release(); d_desc.release(); d_lists.release(); d_counts.release();
     d_cread.release(); d_ext.release(); d_tasks.release(); d_ctr.release(); d_regpos.release(); d_skipf.release();
@@ -112,6 +120,7 @@ struct Slot {
     if (spec.fork) (void)hipEventDestroy(spec.fork);
     if (spec.join) (void)hipEventDestroy(spec.join);
     spec = SpecStreams{};
+    side_chosen = false;
   }
   HostBuf h_in, h_out, h_n, h_stats;
   // the submit/wait path's results: regions written densely (read r's at
@@ -127,6 +136,46 @@ struct Slot {
   bwagpu_stats_t last{};
   int64_t h2d = 0, d2h = 0;
 };
+
+hipError_t lazy_stream(Slot& s, hipStream_t* st) {
+  std::call_once(s.stream_once, [&s] { s.stream_err = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking); });
+  *st = s.stream;
+  return s.stream_err;
+}
+
+// Side-stream probes.  HIP maps every stream of the process onto one of
+// GPU_MAX_HW_QUEUES hardware queues (4 on the pool's boxes), and work on two
+// streams that share a queue runs in submission order: a selection side
+// stream on the same queue as a caller stream serializes the two (the GRCh38
+// regime leg of round 4: 2.56 against 1.75 ms per batch).
+// Whether two streams share a queue is measured: a ~150 us spin on `a`, then
+// an empty kernel on `b`; b done while a still spins = separate queues.
+__global__ void side_probe_spin(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+__global__ void side_probe_nop() {}
+
+bool streams_concurrent(hipStream_t a, hipStream_t b) {
+  hipEvent_t ea = nullptr, eb = nullptr;
+  if (hipEventCreateWithFlags(&ea, hipEventDisableTiming) != hipSuccess) return false;
+  if (hipEventCreateWithFlags(&eb, hipEventDisableTiming) != hipSuccess) {
+    (void)hipEventDestroy(ea);
+    return false;
+  }
+  hipLaunchKernelGGL(side_probe_spin, dim3(1), dim3(64), 0, a, (uint64_t)15000);
+  bool conc = false;
+  if (hipGetLastError() == hipSuccess && hipEventRecord(ea, a) == hipSuccess) {
+    hipLaunchKernelGGL(side_probe_nop, dim3(1), dim3(64), 0, b);
+    if (hipGetLastError() == hipSuccess && hipEventRecord(eb, b) == hipSuccess &&
+        hipEventSynchronize(eb) == hipSuccess)
+      conc = hipEventQuery(ea) == hipErrorNotReady;
+  }
+  (void)hipEventSynchronize(ea);
+  (void)hipEventDestroy(ea);
+  (void)hipEventDestroy(eb);
+  return conc;
+}
 
 // Per-read offsets of the dense result layout: off[r] = n[0] + ... + n[r-1]
 // (one workgroup; a batch has < 2^31 regions), written to the device (for the
@@ -183,6 +232,10 @@ __global__ void __launch_bounds__(256) dense_copy_kernel(const bwagpu_alnreg_t* 
 
 struct bwagpu_ctx {
   int device = 0;
+  // caller streams seen by the spec path, and side streams retired after a
+  // later caller turned out to share their hardware queue (choose_side)
+  std::mutex side_mu;
+  std::vector<hipStream_t> callers, side_graveyard;
   DevOpt opt{};
   DevRef ref{};
   bool own_pac = false;
@@ -365,7 +418,6 @@ int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, 
   HIPC(hipMemcpy(ctx->d_ann_len, bns->ann_len, sizeof(int32_t) * bns->n_seqs, hipMemcpyHostToDevice),
        "upload ann_len");
   for (auto& s : ctx->slot) {
-    HIPC(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
     HIPC(hipEventCreate(&s.ev0), "hipEventCreate");
     HIPC(hipEventCreate(&s.ev1), "hipEventCreate");
     HIPC(hipEventCreate(&s.ev2), "hipEventCreate");
@@ -376,6 +428,15 @@ int create_common(int device, const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, 
   ctx->ref.ann_offset = ctx->d_ann_off;
   ctx->ref.ann_len = ctx->d_ann_len;
   return BWAGPU_OK;
+}
+
+// every Slot of a context whose spec path may hold a side stream
+std::vector<Slot*> all_slots(bwagpu_ctx_t* ctx) {
+  std::vector<Slot*> v;
+  for (auto& x : ctx->slot) v.push_back(&x);
+  for (auto& x : ctx->dev_scratch) v.push_back(&x);
+  v.push_back(&ctx->ch_slot);
+  return v;
 }
 
 void destroy_ctx(bwagpu_ctx_t* ctx) {
@@ -399,6 +460,11 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     s.release_scratch();
     s.d_stats.release();
   }
+  for (hipStream_t x : ctx->side_graveyard) {
+    (void)hipStreamSynchronize(x);
+    (void)hipStreamDestroy(x);
+  }
+  ctx->side_graveyard.clear();
   for (hipEvent_t e : ctx->prof_ev) (void)hipEventDestroy(e);
   ctx->prof_ev.clear();
   for (int i = 0; i < bwagpu_ctx::kA2Streams; ++i) {
@@ -569,6 +635,59 @@ int check_lds(bwagpu_ctx_t* ctx, int lq_max) {
   return BWAGPU_OK;
 }
 
+// The caller stream st of a spec-path batch: a side stream for its heavy
+// selection kernels on a hardware queue that none of this context's caller
+// streams and other side streams use (streams_concurrent), or none at all
+// (the heavy selection then runs on st) when six candidates all share one.
+// A caller stream seen for the first time retires the side streams that share
+// its queue (their slots choose again at their next batch).
+void register_caller_locked(bwagpu_ctx_t* ctx, hipStream_t st) {
+  for (hipStream_t c : ctx->callers)
+    if (c == st) return;
+  for (Slot* x : all_slots(ctx))
+    if (x->side_chosen && x->spec.side && hipStreamSynchronize(x->spec.side) == hipSuccess &&
+        !streams_concurrent(x->spec.side, st)) {  // spin on the (drained) side, probe st
+      ctx->side_graveyard.push_back(x->spec.side);  // may still hold queued work: destroyed with the context
+      x->spec.side = nullptr;
+      x->side_chosen = false;
+    }
+  ctx->callers.push_back(st);
+}
+
+hipError_t choose_side(bwagpu_ctx_t* ctx, Slot& s, hipStream_t st) {
+  std::lock_guard<std::mutex> g(ctx->side_mu);
+  register_caller_locked(ctx, st);
+  if (s.side_chosen) return hipSuccess;
+  if (!s.spec.fork) {
+    hipError_t e = hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  std::vector<hipStream_t> avoid = ctx->callers;
+  for (Slot* x : all_slots(ctx))
+    if (x != &s && x->side_chosen && x->spec.side) avoid.push_back(x->spec.side);
+  std::vector<hipStream_t> tried;  // kept until the end: each holds its queue's place
+  hipStream_t pick = nullptr;
+  hipError_t e = hipSuccess;
+  for (int t = 0; t < 6 && !pick; ++t) {
+    hipStream_t c = nullptr;
+    if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) break;
+    bool ok = true;
+    for (hipStream_t a : avoid)
+      if (!streams_concurrent(a, c)) {
+        ok = false;
+        break;
+      }
+    if (ok) pick = c;
+    else tried.push_back(c);
+  }
+  for (hipStream_t c : tried) (void)hipStreamDestroy(c);  // only the probe ran on them
+  if (e != hipSuccess) return e;
+  s.spec.side = pick;
+  s.side_chosen = true;
+  return hipSuccess;
+}
+
 int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwagpu_alnreg_t* d_out, int32_t* d_n,
                  int64_t* d_stats, hipStream_t st) {
   const size_t nc = (size_t)std::max(db.n_chains, 1), ns = (size_t)std::max(db.n_seeds, 1),
@@ -626,35 +745,14 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;
-  if (!s.spec.side) {
-    const char* pe = getenv("BWAGPU_SIDE_PRIO");
-    if (pe && pe[0] == '2') {  // a CU-masked stream (every CU): a hardware queue of its own
-      int cus = 0;
-      HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device), "attribute");
-      std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
-      HIPC(hipExtStreamCreateWithCUMask(&s.spec.side, (uint32_t)mask.size(), mask.data()), "hipStreamCreate(side)");
-    } else if (pe && (pe[0] == '1' || pe[0] == '4')) {
-      int least = 0, greatest = 0;
-      HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
-      HIPC(hipStreamCreateWithPriority(&s.spec.side, hipStreamNonBlocking, pe[0] == '1' ? greatest : least),
-           "hipStreamCreate(side)");
-    } else
-    HIPC(hipStreamCreateWithFlags(&s.spec.side, hipStreamNonBlocking), "hipStreamCreate(side)");
-    HIPC(hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming), "hipEventCreate");
-    HIPC(hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming), "hipEventCreate");
-  }
+  HIPC(choose_side(ctx, s, st), "side stream");
   a.lq_bound = lq_max;
   const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
   s.spec.form = ctx->ext_form;
   s.spec.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
   s.spec.pool_n = (int)ctx->prof_ev.size();
   s.spec.pool_used = &ctx->prof_used;
-  SpecStreams ss = s.spec;
-  {
-    const char* pe = getenv("BWAGPU_SIDE_PRIO");
-    if (pe && pe[0] == '3') ss.side = nullptr;  // A/B: heavy selection on the caller's stream
-  }
-  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, ss), "spec chain2aln launch");
+  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, s.spec), "spec chain2aln launch");
   return BWAGPU_OK;
 }
 
@@ -828,7 +926,8 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
     if (b->seq_bytes) memcpy(h + L.seq, b->seq, (size_t)b->seq_bytes);
   }
 
-  hipStream_t st = s.stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(s, &st), "hipStreamCreate");
   HIPC(hipEventRecord(s.ev0, st), "event");
   HIPC(hipMemcpyAsync(s.d_in.p, s.h_in.p, L.total, hipMemcpyHostToDevice, st), "H2D batch");
   HIPC(hipMemsetAsync(s.d_stats.p, 0, sizeof(int64_t) * ST_N, st), "memset stats");
@@ -1004,7 +1103,8 @@ int bwagpu_chain2aln_device(bwagpu_ctx_t* ctx, const bwagpu_batch_t* db_in, bwag
   const int lq_bound = use_read_kernels() ? BWAGPU_MAX_READ_LEN : ctx->dev_read_len;
   int rc = check_lds(ctx, lq_bound);
   if (rc) return rc;
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  hipStream_t st = (hipStream_t)stream;
+  if (!st) HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   int k = 0;
   while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] && ctx->dev_stream[k] != st) ++k;
   if (k == BWAGPU_NUM_SLOTS) return fail(ctx, BWAGPU_E_INVAL, "more than BWAGPU_NUM_SLOTS streams on one context");
@@ -1067,7 +1167,8 @@ int bwagpu_extend_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_ext_task_t* t
     if (tpool[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "target base > 4");
   // LDS rows needed per task (rows_needed on the host) -> per-variant max
   Slot& s = ctx->slot[0];
-  hipStream_t st = s.stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(s, &st), "hipStreamCreate");
   DevBuf d_tasks, d_list, d_q, d_t, d_res, d_stats;
   auto cleanup = [&]() {
     d_tasks.release(); d_list.release(); d_q.release(); d_t.release(); d_res.release(); d_stats.release();
@@ -1253,7 +1354,8 @@ int bwagpu_reg2aln_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_reg2aln_task
     cost[(size_t)k] = zb + lq + rl;
   }
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = ctx->slot[0].stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   HIPC(ctx->r2_tasks.ensure(sizeof(bwagpu_reg2aln_task_t) * n), "hipMalloc");
   HIPC(ctx->r2_q.ensure((size_t)qpool_len + 1), "hipMalloc");
   HIPC(ctx->r2_out.ensure(sizeof(bwagpu_aln_t) * n), "hipMalloc");
@@ -1414,7 +1516,8 @@ int bwagpu_align2_batch(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_t
     if (tpool[i] > 4) return fail(ctx, BWAGPU_E_INVAL, "target base > 4");
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   Slot& s = ctx->slot[0];
-  hipStream_t st = s.stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(s, &st), "hipStreamCreate");
   HIPC(ctx->a2_tasks.ensure(sizeof(bwagpu_align2_task_t) * n), "hipMalloc");
   HIPC(ctx->a2_q.ensure((size_t)qpool_len + 1), "hipMalloc");
   HIPC(ctx->a2_t.ensure((size_t)tpool_len + 1), "hipMalloc");
@@ -1488,7 +1591,8 @@ int bwagpu_align2_device(bwagpu_ctx_t* ctx, int32_t n, const bwagpu_align2_task_
   if (n == 0) return BWAGPU_OK;
   if (const char* why = align2_opt_unsupported(ctx->opt)) return fail(ctx, BWAGPU_E_UNSUPPORTED, why);
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  hipStream_t st = (hipStream_t)stream;
+  if (!st) HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   HIPC(ctx->a2_lists.ensure(sizeof(int32_t) * (size_t)kA2Bins * n), "hipMalloc");
   HIPC(ctx->a2_boff.ensure(sizeof(int64_t) * n), "hipMalloc");
   // counts[kA2Bins] | cursors[kA2Bins] | scratch cursor (u64) | stats[ST_N]
@@ -1529,7 +1633,8 @@ int bwagpu_debug_fail_wait(bwagpu_ctx_t* ctx, int after_n_waits, int code) {
 int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   if (!ctx || !out) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  hipStream_t st = (hipStream_t)stream;
+  if (!st) HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   int k = 0;
   while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] != st) ++k;
   if (k == BWAGPU_NUM_SLOTS || !ctx->dev_scratch[k].d_ctr.p) return fail(ctx, BWAGPU_E_INVAL, "no device-entry batch on this stream");
@@ -1553,7 +1658,8 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
 int bwagpu_debug_spec_ext(bwagpu_ctx_t* ctx, void* stream, void* host_out, int32_t n) {
   if (!ctx || !host_out || n < 0) return BWAGPU_E_INVAL;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->slot[0].stream;
+  hipStream_t st = (hipStream_t)stream;
+  if (!st) HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   int k = 0;
   while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] != st) ++k;
   if (k == BWAGPU_NUM_SLOTS || !ctx->dev_scratch[k].d_ext.p || ctx->dev_scratch[k].d_ext.cap < sizeof(SeedExt) * (size_t)n)
@@ -1650,7 +1756,8 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
     ctx->bwt.sup_shift = ctx->sup_shift;
     HIPC(ctx->sup_d.ensure(4 * sizeof(uint64_t) * (size_t)occ64_supers(bwt->seq_len, ctx->sup_shift)), "hipMalloc");
     HIPC(hipMemset(ctx->occ_d.p, 0, 2 * sizeof(uint4) * (size_t)occ64_blocks(bwt->seq_len)), "memset");
-    hipStream_t st = ctx->slot[0].stream;
+    hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
     HIPC(launch_build_occ64(ctx->bwt, ctx->occ_d.as<uint4>(), ctx->sup_d.as<uint64_t>(), st), "build_occ64 launch");
     HIPC(hipStreamSynchronize(st), "sync");
     ctx->bwt.occ = ctx->occ_d.as<uint4>();
@@ -1680,7 +1787,8 @@ extern "C" int bwagpu_bwt_sa(bwagpu_ctx_t* ctx, int64_t n, const uint64_t* k, ui
     if (k[i] > ctx->bwt.seq_len) return fail(ctx, BWAGPU_E_INVAL, "BWT position past seq_len");
   if (n == 0) return BWAGPU_OK;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = ctx->slot[0].stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   HIPC(ctx->sa_in.ensure(sizeof(uint64_t) * (size_t)n), "hipMalloc");
   HIPC(ctx->sa_out.ensure(sizeof(uint64_t) * (size_t)n), "hipMalloc");
   HIPC(hipMemcpyAsync(ctx->sa_in.p, k, sizeof(uint64_t) * (size_t)n, hipMemcpyHostToDevice, st), "H2D");
@@ -1807,7 +1915,8 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
   if (rc) return rc;
   if (n_reads == 0) return BWAGPU_OK;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = ctx->slot[0].stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   SeedArgs a;
   if ((rc = seed_enqueue(ctx, opt, n_reads, seq_off, seq, bases, max_per_read, true, st, a))) return rc;
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
@@ -1885,7 +1994,8 @@ extern "C" int bwagpu_sw_stream(bwagpu_ctx_t* ctx, const int32_t* i_buf, int64_t
   if ((size_t)(kBlock / 64) * 2 * tb > 64 * 1024)
     return fail(ctx, BWAGPU_E_UNSUPPORTED, "LDS row buffer too large for these options (w, pen_clip, read length)");
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
-  hipStream_t st = ctx->slot[0].stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   const size_t cap = (size_t)std::max(o_cap_tasks, 1), nr = starts.size();
   HIPC(ctx->st_buf.ensure(sizeof(int32_t) * (size_t)i_words), "hipMalloc");
   HIPC(ctx->st_start.ensure(sizeof(int64_t) * nr), "hipMalloc");
@@ -2164,7 +2274,8 @@ extern "C" int bwagpu_seqs2chains(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sop
                                   bwagpu_chains_t* out) {
   if (!ctx || !sopt || !copt || !out || n_reads < 0 || (n_reads && !seq_off)) return BWAGPU_E_INVAL;
   *out = bwagpu_chains_t{};
-  hipStream_t st = ctx->slot[0].stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   int64_t nc = 0, ns = 0;
   int lq = 0;
   int rc = run_chaining(ctx, sopt, copt, n_reads, seq_off, seq, raw != 0, st, &nc, &ns, &lq);
@@ -2211,7 +2322,8 @@ extern "C" int bwagpu_seqs2regions(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* so
   for (int32_t r = 0; r < n_reads; ++r)
     if (seq_off[r + 1] - seq_off[r] > BWAGPU_MAX_READ_LEN)
       return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_READ_LEN");
-  hipStream_t st = ctx->slot[0].stream;
+  hipStream_t st = nullptr;
+  HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   int64_t nc = 0, ns = 0;
   int lq = 0;
   int rc = run_chaining(ctx, sopt, copt, n_reads, seq_off, seq, false, st, &nc, &ns, &lq);
