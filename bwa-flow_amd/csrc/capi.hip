@@ -911,19 +911,40 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
                       (const void*)b->seeds == (const void*)(h + L.seeds) &&
                       (const void*)b->seq == (const void*)(h + L.seq) &&
                       (const void*)b->chain_seed_off == (const void*)(h + L.cso);
-  if (staged) {
-  } else if (b->n_reads) {
-    memcpy(h + L.seq_off, b->seq_off, sizeof(int64_t) * (size_t)(b->n_reads + 1));
-    memcpy(h + L.rco, b->read_chain_off, sizeof(int32_t) * (size_t)(b->n_reads + 1));
-  }
-  if (!staged) {
+  if (!staged && b->n_reads) {
+    // the staging copy (~20 MB for a C2 record) on a few threads: one thread's
+    // memcpy into pinned pages runs at a fraction of the host's bandwidth
+    struct Piece {
+      char* dst;
+      const void* src;
+      size_t n;
+    };
+    std::vector<Piece> pieces = {
+        {h + L.seq_off, b->seq_off, sizeof(int64_t) * (size_t)(b->n_reads + 1)},
+        {h + L.rco, b->read_chain_off, sizeof(int32_t) * (size_t)(b->n_reads + 1)},
+        {h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1)},
+        {h + L.rid, b->chain_rid, sizeof(int32_t) * (size_t)b->n_chains},
+        {h + L.frac, b->chain_frac_rep, sizeof(float) * (size_t)b->n_chains},
+        {h + L.seeds, b->seeds, sizeof(bwagpu_seed_t) * (size_t)b->n_seeds},
+        {h + L.seq, b->seq, (size_t)b->seq_bytes}};
+    size_t total = 0;
+    for (const Piece& q : pieces) total += q.n;
+    const int nt = total >= ((size_t)4 << 20) ? 4 : 1;
+    auto copy_part = [&](int t) {  // byte range [total*t/nt, total*(t+1)/nt) of the concatenation
+      const size_t lo = total * (size_t)t / (size_t)nt, hi = total * (size_t)(t + 1) / (size_t)nt;
+      size_t at = 0;
+      for (const Piece& q : pieces) {
+        const size_t a = std::max(lo, at), e = std::min(hi, at + q.n);
+        if (a < e) memcpy(q.dst + (a - at), (const char*)q.src + (a - at), e - a);
+        at += q.n;
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(copy_part, t);
+    copy_part(0);
+    for (auto& x : th) x.join();
+  } else if (!staged) {
     memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
-    if (b->n_chains) {
-      memcpy(h + L.rid, b->chain_rid, sizeof(int32_t) * (size_t)b->n_chains);
-      memcpy(h + L.frac, b->chain_frac_rep, sizeof(float) * (size_t)b->n_chains);
-    }
-    if (b->n_seeds) memcpy(h + L.seeds, b->seeds, sizeof(bwagpu_seed_t) * (size_t)b->n_seeds);
-    if (b->seq_bytes) memcpy(h + L.seq, b->seq, (size_t)b->seq_bytes);
   }
 
   hipStream_t st = nullptr;

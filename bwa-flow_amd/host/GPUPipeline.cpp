@@ -544,6 +544,18 @@ void ChainReaper::run() {
 }
 
 // ------------------------------------------------------- ChainsToRegionsGPU
+// records a worker keeps in flight (its context's slots in use): every slot
+// is a stream of its own, and with its selection side stream each takes a
+// hardware queue (GPU_MAX_HW_QUEUES = 4 by default); BWAGPU_STAGE_SLOTS
+// (1..BWAGPU_NUM_SLOTS, default 2)
+int stage_slots() {
+  static const int n = [] {
+    const char* e = getenv("BWAGPU_STAGE_SLOTS");
+    return std::max(1, std::min(e ? atoi(e) : 2, BWAGPU_NUM_SLOTS));
+  }();
+  return n;
+}
+
 RegionsRecord ChainsToRegionsGPU::on_cpu(const ChainsRecord& rec) {
   // finishUpOnCPU (FPGAPipeline.cpp:526-551): the whole record goes through
   // the CPU stage's body; a GPU batch is all-or-nothing, so start_seq = 0
@@ -580,7 +592,8 @@ void ChainsToRegionsGPU::compute(int wid) {
     FlatBatch* flat;
     int slot;
   };
-  std::vector<FlatBatch> flats(BWAGPU_NUM_SLOTS);
+  const int nslots = stage_slots();
+  std::vector<FlatBatch> flats(nslots);
   std::deque<Job> inflight;
   long long submitted = 0;
   bool more = true;
@@ -594,7 +607,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     retire();
   };
   for (;;) {
-    if (more && inflight.size() < BWAGPU_NUM_SLOTS) {
+    if (more && inflight.size() < (size_t)nslots) {
       ChainsRecord rec;
       bool ready = getInput(rec);
       if (!ready && inflight.empty()) {
@@ -608,7 +621,7 @@ void ChainsToRegionsGPU::compute(int wid) {
         if (!ready) more = false;
       }
       if (ready) {
-        const int sl = (int)(submitted % BWAGPU_NUM_SLOTS);
+        const int sl = (int)(submitted % nslots);
         inflight.push_back(Job{rec, &flats[sl], sl});
         Job& j = inflight.back();
         auto t0 = std::chrono::steady_clock::now();

@@ -176,24 +176,28 @@ class Engine:
 
     def wait_dense(self, slot: int, batch: Batch, out=None):
         """-> (regs, n): the slot's results in read order without slot gaps
-        (bwagpu_chain2aln_results_dense: only these regions crossed PCIe);
-        `out` = (regs, n) arrays to fill instead of fresh ones"""
+        (bwagpu_chain2aln_results_dense: only these regions crossed PCIe).
+        out=None: numpy views onto the slot's pinned result buffers, valid
+        until the slot's next submit (no host copy); `out` = (regs, n) arrays
+        to copy into instead"""
         self._check(self.lib.bwagpu_chain2aln_wait(self.ctx, slot, None, None), "wait")
         rp, np_, op = C.c_void_p(), C.c_void_p(), C.c_void_p()
         self._check(self.lib.bwagpu_chain2aln_results_dense(self.ctx, slot, C.byref(rp), C.byref(np_), C.byref(op)),
                     "results_dense")
         nr = batch.n_reads
-        cnt = np.ctypeslib.as_array(C.cast(np_, C.POINTER(C.c_int32)), (max(nr, 1),))[:nr] if nr else np.zeros(0, np.int32)
+        if nr == 0:
+            return np.zeros(0, abi.ALNREG_DTYPE), np.zeros(0, np.int32)
+        cnt = np.ctypeslib.as_array(C.cast(np_, C.POINTER(C.c_int32)), (nr,))
         tot = int(np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_int32)), (nr + 1,))[nr])
+        view = (np.ctypeslib.as_array(C.cast(rp, C.POINTER(C.c_uint8)), (tot * abi.ALNREG_DTYPE.itemsize,))
+                .view(abi.ALNREG_DTYPE) if tot else np.zeros(0, abi.ALNREG_DTYPE))
         if out is None:
-            regs, n = np.zeros(max(tot, 1), abi.ALNREG_DTYPE), np.zeros(max(nr, 1), np.int32)
-        else:
-            regs, n = out
-            if len(regs) < tot or len(n) < nr:
-                raise ValueError("wait_dense: out arrays too small")
+            return view, cnt
+        regs, n = out
+        if len(regs) < tot or len(n) < nr:
+            raise ValueError("wait_dense: out arrays too small")
         n[:nr] = cnt
-        if tot:
-            C.memmove(regs.ctypes.data, rp.value, tot * abi.ALNREG_DTYPE.itemsize)
+        regs[:tot] = view
         return regs[:tot], n[:nr]
 
     def chain2aln_device(self, dev_batch: abi.BatchC, dev_out: int, dev_n: int, dev_stats: int | None,
