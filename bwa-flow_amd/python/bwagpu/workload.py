@@ -19,6 +19,9 @@ from .synth import GoldenRef
 
 REPO = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", ".."))
 C2_FIXTURE = os.path.join(REPO, "tests", "golden", "c2_refseed.npz")
+# one mixed 2x100 / 2x150 / 2x250 ChainsRecord on the same genome, seeded and
+# chained by the reference (oracle/gen_c2_fixture.py --length mix): BASELINE.json configs[4]
+C5_FIXTURE = os.path.join(REPO, "tests", "golden", "c5_refseed.npz")
 OPT_KEYS = ("a", "b", "o_del", "e_del", "o_ins", "e_ins", "pen_clip5", "pen_clip3", "w", "zdrop")
 
 

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""TEST INFRASTRUCTURE: make tests/golden/c2_refseed.npz, the bench's C2 workload.
+"""TEST INFRASTRUCTURE: make tests/golden/c2_refseed.npz, the bench's C2 workload
+(and, with --length mix, tests/golden/c5_refseed.npz: one mixed 2x100/150/250
+ChainsRecord of the same genome, the bench's c5_refseed leg).
 
 Runs oracle/_ref/gen_golden (the REFERENCE's own bwa index + seeding +
 chaining + mem_chain2aln, see gen_golden.c) on a chr21-sized synthetic genome
@@ -22,6 +24,8 @@ The genome itself is not stored (11.7 MB of 2-bit bases): it is a pure
 function of (length, seed 1234) and bwa's N filling (bntseq.c:261, srand48(11)).
 
     python oracle/gen_c2_fixture.py [--out tests/golden/c2_refseed.npz]
+    python oracle/gen_c2_fixture.py --length mix --pairs 30000 --batches 1 --read-seed 2027 \
+        --out tests/golden/c5_refseed.npz
 """
 import argparse
 import hashlib
@@ -59,10 +63,14 @@ def pack_reads(seq, seq_off):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden", "c2_refseed.npz"))
+    ap.add_argument("--length", default="150", help="150 | mix (2x100 / 2x150 / 2x250 pairs in thirds)")
+    ap.add_argument("--pairs", type=int, default=PAIRS)
+    ap.add_argument("--batches", type=int, default=2)
+    ap.add_argument("--read-seed", type=int, default=READ_SEED)
     a = ap.parse_args()
     gen = os.path.join(HERE, "_ref", "gen_golden")
     with tempfile.TemporaryDirectory(prefix="c2fix_") as d:
-        subprocess.run([gen, d, str(READ_SEED), str(PAIRS), "150", "0", str(GENOME_LEN), "0"], check=True)
+        subprocess.run([gen, d, str(a.read_seed), str(a.pairs), a.length, "0", str(GENOME_LEN), "0"], check=True)
         pac = rd(d, "pac", np.uint8)
         l_pac = int(rd(d, "l_pac", np.int64)[0])
         ann_offset, ann_len = rd(d, "ann_offset", np.int64), rd(d, "ann_len", np.int32)
@@ -74,13 +82,15 @@ def main():
         opt_int, opt_mat = rd(d, "opt_int", np.int32), rd(d, "opt_mat", np.int8)
     assert l_pac == GENOME_LEN
     n_reads = len(seq_off) - 1
-    assert n_reads == 2 * BATCH_READS, n_reads
+    assert n_reads == 2 * a.pairs, n_reads
+    per = n_reads // a.batches
+    per -= per & 1  # whole pairs per batch
     out = dict(genome_len=np.int64(l_pac), genome_seed=np.int64(1234), ann_offset=ann_offset, ann_len=ann_len,
                pac_sha256=np.frombuffer(hashlib.sha256(pac.tobytes()).digest(), np.uint8),
-               opt_int=opt_int, opt_mat=opt_mat, n_batches=np.int32(2), read_seed=np.int64(READ_SEED))
+               opt_int=opt_int, opt_mat=opt_mat, n_batches=np.int32(a.batches), read_seed=np.int64(a.read_seed))
     reg_off = np.concatenate([[0], np.cumsum(reg_n)])
-    for k in range(2):
-        r0, r1 = k * BATCH_READS, (k + 1) * BATCH_READS
+    for k in range(a.batches):
+        r0, r1 = k * per, (k + 1) * per
         c0, c1 = int(rco[r0]), int(rco[r1])
         s0, s1 = int(cso[c0]), int(cso[c1])
         q0, q1 = int(seq_off[r0]), int(seq_off[r1])

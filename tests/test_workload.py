@@ -54,3 +54,21 @@ def test_cpu_paths_match_fixture_digest(c2, which):
         k = int(np.argmax(n2 > 0))
         regs2[rb.batch.read_seed_off()[k]]["score"] += 1
         assert not rb.check(regs2, n2)
+
+
+def test_c5_refseed_fixture_matches_the_oracle(c2):
+    """tests/golden/c5_refseed.npz (the bench's c5_refseed leg): one mixed
+    2x100 / 2x150 / 2x250 ChainsRecord seeded by the reference on the C2 genome;
+    the oracle reproduces the reference's regions on it (per-read counts and
+    the SHA-256 of every record)"""
+    _, ref, _ = c2
+    opt, _, bs = workload.load_fixture(workload.C5_FIXTURE, with_ref=False)
+    z = np.load(workload.C5_FIXTURE)
+    import hashlib
+    assert hashlib.sha256(ref.pac.tobytes()).digest() == z["pac_sha256"].tobytes()
+    rb = bs[0]
+    lens = set(np.diff(rb.batch.seq_off).tolist())
+    assert {100, 150, 250} <= lens and int(rb.batch.seq_off[-1]) > 9_000_000
+    R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
+    regs, n, _ = oracle.chain2aln("oracle", opt, R, rb.batch, n_threads=min(8, os.cpu_count() or 1))
+    assert rb.check(regs, n)
