@@ -1291,92 +1291,6 @@ __device__ __forceinline__ SeedExt extend_seed(const DevOpt& o, const DevRef& re
   return e;
 }
 
-// extend_seed for ONE seed on a whole wave with the band retry run ahead:
-// each side's try 0 (w) and try 1 (2w, MAX_BAND_TRY, bwamem.c:639) run at
-// once, one per 32-lane half (extend_pair), and the retry test picks the try
-// the reference would have ended with (its tallies count only the calls the
-// reference makes).  Two DP calls of latency instead of up to four: the form
-// for an extension one wave needs before it can go on (a final pass's miss).
-// Reads up to 32 * PMAX - 1 bases.
-template <int PMAX>
-__device__ __forceinline__ SeedExt extend_seed_tries(const DevOpt& o, const DevRef& ref, const bwagpu_seed_t& s,
-                                                     int lq, const uint8_t* q, const ChainWin& cw, uint8_t* tbl,
-                                                     uint8_t* tbr) {
-  const int hf = (int)((threadIdx.x >> 5) & 1);  // this half's try
-  Tally tl{0, 0, 0};
-  const int qlenL = s.qbeg, qlenR = lq - (s.qbeg + s.len);
-  const int64_t x0L = s.rbeg - 1, x0R = s.rbeg + s.len;
-  const int tlenL = (int)(s.rbeg - cw.lo), tlenR = (int)(cw.hi - x0R);
-  fill_two(tbl, x0L, qlenL ? rows_needed(o, qlenL, tlenL, o.w << 1, o.pen_clip5) : 0, tbr, x0R,
-           qlenR ? rows_needed(o, qlenR, tlenR, o.w << 1, o.pen_clip3) : 0, ref);
-  int score = -1, truesc = -1, qb = 0, qe = lq, sc0 = 0;
-  int aw0 = o.w, aw1 = o.w;
-  int64_t rb = s.rbeg, re = s.rbeg + s.len;
-#pragma nounroll
-  for (int side = 0; side < 2; ++side) {
-    const bool left = side == 0;
-    if (left && s.qbeg == 0) {  // bwamem.c:753
-      score = truesc = s.len * o.a;
-      continue;
-    }
-    if (!left && qlenR == 0) continue;  // bwamem.c:781
-    const int qlen = left ? qlenL : qlenR;
-    const int64_t x0 = left ? x0L : x0R;
-    const int tlen = left ? tlenL : tlenR;
-    const int qa = left ? s.qbeg - 1 : s.qbeg + s.len;
-    const int eb = left ? o.pen_clip5 : o.pen_clip3;
-    const int h0 = left ? s.len * o.a : score;
-    sc0 = score;
-    Tally32 t32{0, 0, 0};
-    const ExtOut xh = extend_pair_dispatch<PMAX>(o, qlen, q, qa, left ? -1 : 1, tlen, left ? tbl : tbr, o.w << hf, eb,
-                                                 o.zdrop, h0, t32);
-    // both tries' outputs on every lane (half 0: try 0, half 1: try 1)
-    ExtOut y0, y1;
-    y0.score = __builtin_amdgcn_readlane(xh.score, 0);
-    y0.qle = __builtin_amdgcn_readlane(xh.qle, 0);
-    y0.tle = __builtin_amdgcn_readlane(xh.tle, 0);
-    y0.gtle = __builtin_amdgcn_readlane(xh.gtle, 0);
-    y0.gscore = __builtin_amdgcn_readlane(xh.gscore, 0);
-    y0.max_off = __builtin_amdgcn_readlane(xh.max_off, 0);
-    y1.score = __builtin_amdgcn_readlane(xh.score, 32);
-    y1.qle = __builtin_amdgcn_readlane(xh.qle, 32);
-    y1.tle = __builtin_amdgcn_readlane(xh.tle, 32);
-    y1.gtle = __builtin_amdgcn_readlane(xh.gtle, 32);
-    y1.gscore = __builtin_amdgcn_readlane(xh.gscore, 32);
-    y1.max_off = __builtin_amdgcn_readlane(xh.max_off, 32);
-    const int aw = o.w;
-    const bool stop0 = y0.score == score || y0.max_off < (aw >> 1) + (aw >> 2);  // no retry (bwamem.c:739, 765)
-    const ExtOut x = stop0 ? y0 : y1;
-    tl.cells += __builtin_amdgcn_readlane(t32.cells, 0) + (stop0 ? 0 : __builtin_amdgcn_readlane(t32.cells, 32));
-    tl.rows += __builtin_amdgcn_readlane(t32.rows, 0) + (stop0 ? 0 : __builtin_amdgcn_readlane(t32.rows, 32));
-    tl.calls += stop0 ? 1 : 2;
-    score = x.score;
-    aw0 = left ? (stop0 ? aw : aw << 1) : aw0;
-    aw1 = left ? aw1 : (stop0 ? aw : aw << 1);
-    const bool local = x.gscore <= 0 || x.gscore <= score - eb;
-    if (left) {
-      qb = local ? s.qbeg - x.qle : 0;
-      rb = s.rbeg - (local ? x.tle : x.gtle);
-      truesc = local ? score : x.gscore;
-    } else {
-      qe = local ? qa + x.qle : lq;
-      re = x0 + (local ? x.tle : x.gtle);
-      truesc += (local ? score : x.gscore) - sc0;
-    }
-  }
-  SeedExt e;
-  e.rb = rb;
-  e.re = re;
-  e.qb = qb;
-  e.qe = qe;
-  e.score = score;
-  e.truesc = truesc;
-  e.w = aw0 > aw1 ? aw0 : aw1;
-  e.cells = (int32_t)tl.cells;
-  e.rows = (int32_t)tl.rows;
-  e.calls = (int32_t)tl.calls + 1;  // + 1: a computed slot is never all-zero
-  return e;
-}
 
 __device__ __forceinline__ void store_ext(SeedExt* dst, const SeedExt& e) {
   const int d = (int)(threadIdx.x & 63);
