@@ -276,6 +276,7 @@ struct bwagpu_ctx {
   DevBuf ch_regoff, ch_regc;
   HostBuf chh_tot, chh_rco, chh_cso, chh_chains, chh_seeds, chh_regs, chh_n;
   HostBuf sdh_in;  // the reads of a seeding call, staged for the H2D
+  hipEvent_t sdh_done = nullptr;  // recorded after the H2D out of sdh_in
   Slot ch_slot;  // chain2aln scratch of bwagpu_seqs2regions
   ChainStreams ch_cs{};  // created on first use
   bool has_alt = false;
@@ -459,6 +460,10 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
     Slot& s = ctx->dev_scratch[k];
     s.release_scratch();
     s.d_stats.release();
+  }
+  if (ctx->sdh_done) {
+    (void)hipEventSynchronize(ctx->sdh_done);
+    (void)hipEventDestroy(ctx->sdh_done);
   }
   for (hipStream_t x : ctx->side_graveyard) {
     (void)hipStreamSynchronize(x);
@@ -1881,6 +1886,10 @@ int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads
   HIPC(ctx->sd_scratch.ensure(sizeof(bwagpu_intv_t) * (size_t)seed_scratch_entries(bases, n_reads)), "hipMalloc");
   if (upload) {  // through a pinned staging buffer filled on a few threads (a pageable H2D runs at a fraction)
     const size_t ob = sizeof(int64_t) * ((size_t)n_reads + 1);
+    // the previous call's H2D may still read the buffer (a caller that
+    // returned early on an error never synchronized its stream)
+    if (ctx->sdh_done) HIPC(hipEventSynchronize(ctx->sdh_done), "hipEventSynchronize");
+    else HIPC(hipEventCreateWithFlags(&ctx->sdh_done, hipEventDisableTiming), "hipEventCreate");
     HIPC(ctx->sdh_in.ensure(ob + (size_t)bases), "hipHostMalloc");
     char* const pin = ctx->sdh_in.as<char>();
     const int nt = bases >= (1 << 22) ? 8 : 1;
@@ -1895,6 +1904,7 @@ int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads
     for (auto& x : th) x.join();
     HIPC(hipMemcpyAsync(ctx->sd_off.p, pin, ob, hipMemcpyHostToDevice, st), "H2D");
     if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, pin + ob, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
+    HIPC(hipEventRecord(ctx->sdh_done, st), "hipEventRecord");
   }
   a = SeedArgs{};
   a.n_reads = n_reads;
