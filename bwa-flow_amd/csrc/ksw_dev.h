@@ -773,7 +773,7 @@ template <int G, int CPL, bool K8>
 __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa, ExtOut& xb,
                                             Tally32& ta, Tally32& tbl) {
   using namespace pk16;
-  static_assert(G == 32 || (G == 16 && K8), "eight calls per wave: the 8-bit key form only");
+  static_assert(G == 32 || G == 16, "four (G = 32) or eight (G = 16) calls per wave");
   int r;  // the lane index in its group, behind an opaque move (see extend_pair)
   if constexpr (G == 16) asm volatile("v_and_b32 %0, 15, %1" : "=v"(r) : "v"((int)threadIdx.x));
   else asm volatile("v_and_b32 %0, 31, %1" : "=v"(r) : "v"((int)threadIdx.x));
@@ -910,12 +910,31 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       const uint32_t lka = LK & 0xffffu, lkb = LK >> 16;
       int ka = (int)(((lka >> KS) << 10) | (uint32_t)(j0 + (int)(lka & ((1u << KS) - 1))));
       int kb = (int)(((lkb >> KS) << 10) | (uint32_t)(j0 + (int)(lkb & ((1u << KS) - 1))));
-      ka = half_max(row_max32(ka));
-      kb = half_max(row_max32(kb));
+      if constexpr (G == 16) {  // every reduction inside the group's DPP row
+#define RED4_STEP(CTRL)                                                                   \
+  {                                                                                       \
+    const int a_ = __builtin_amdgcn_mov_dpp(ka, CTRL, 0xF, 0xF, false);                   \
+    const int b_ = __builtin_amdgcn_mov_dpp(kb, CTRL, 0xF, 0xF, false);                   \
+    const uint32_t l_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)CL, CTRL, 0xF, 0xF, false); \
+    const uint32_t h_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)CH, CTRL, 0xF, 0xF, false); \
+    ka = max(ka, a_);                                                                     \
+    kb = max(kb, b_);                                                                     \
+    CL = umin(CL, l_);                                                                    \
+    CH = smax(CH, h_);                                                                    \
+  }
+        RED4_STEP(DPP_ROW_ROR(8))
+        RED4_STEP(DPP_ROW_ROR(4))
+        RED4_STEP(DPP_ROW_ROR(2))
+        RED4_STEP(DPP_ROW_ROR(1))
+#undef RED4_STEP
+      } else {
+        ka = half_max(row_max32(ka));
+        kb = half_max(row_max32(kb));
+        CL = half_umin(CL);
+        CH = half_smax(CH);
+      }
       MROW = pk(ka >> 10, kb >> 10);
       MJ = pk(ka & 1023, kb & 1023);
-      CL = half_umin(CL);
-      CH = half_smax(CH);
     }
     // ksw.c:450-453 (meaningful on the owner of column qlen-1)
     {
@@ -975,7 +994,7 @@ __device__ __forceinline__ void extend_quad_dispatch(const DevOpt& o, const QCal
 #define EXT_QUAD(n) \
   if (n <= PMAX && cpl == n) return extend_quad<G, (n <= PMAX ? n : 1), K8>(o, A, Bc, xa, xb, ta, tbl);
   EXT_QUAD(1) EXT_QUAD(2) EXT_QUAD(3) EXT_QUAD(4) EXT_QUAD(5) EXT_QUAD(6) EXT_QUAD(7) EXT_QUAD(8) EXT_QUAD(9)
-  EXT_QUAD(10)
+  EXT_QUAD(10) EXT_QUAD(11) EXT_QUAD(12) EXT_QUAD(13) EXT_QUAD(14) EXT_QUAD(15) EXT_QUAD(16)
 #undef EXT_QUAD
 }
 

@@ -1823,7 +1823,12 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
     *ss.pool_used += 2;
   }
   if (!bin1) return;
-  if (quad) {
+  if (quad && form == 0 && !getenv("BWAGPU_AB_BIN2_FOUR")) {  // eight per wave, the row-max key widened per call (H may reach 256 and more)
+    const size_t lds8 = ext4_lds(tb_bytes, 16);
+    const int nb = resident_blocks(spec_ext4_kernel<16, kSpecBinLen[1] / 16, false>, lds8);
+    hipLaunchKernelGGL((spec_ext4_kernel<16, kSpecBinLen[1] / 16, false>), dim3(grid(nb)), dim3(kBlock), lds8, st, o,
+                       ref, b, a, l + 1, tb_bytes);
+  } else if (quad) {
     const int nb = resident_blocks(spec_ext4_kernel<32, kSpecBinLen[1] / 32, false>, lds2);
     hipLaunchKernelGGL((spec_ext4_kernel<32, kSpecBinLen[1] / 32, false>), dim3(grid(nb)), dim3(kBlock), lds2, st, o,
                        ref, b, a, l + 1, tb_bytes);
