@@ -1698,6 +1698,11 @@ int bwagpu_debug_spec_ext(bwagpu_ctx_t* ctx, void* stream, void* host_out, int32
 
 int bwagpu_debug_ext_form(int form) { return set_ext_form(form); }
 
+int bwagpu_streams_concurrent(void* a, void* b) {
+  if (!a || !b || a == b) return BWAGPU_E_INVAL;
+  return streams_concurrent((hipStream_t)a, (hipStream_t)b) ? 1 : 0;
+}
+
 int bwagpu_ctx_ext_form(bwagpu_ctx_t* ctx, int form) {
   if (!ctx) return BWAGPU_E_INVAL;
   const int prev = ctx->ext_form;

@@ -155,6 +155,7 @@ PROTOS = {
     "bwagpu_debug_ext_form": (C.c_int, [C.c_int]),
     "bwagpu_ctx_ext_form": (C.c_int, [_VP, C.c_int]),
     "bwagpu_debug_ext_kernel": (C.c_int, [_VP, C.c_int32]),
+    "bwagpu_streams_concurrent": (C.c_int, [_VP, _VP]),
     "bwagpu_bwt_sa": (C.c_int, [_VP, C.c_int64, _VP, _VP]),
     "bwagpu_sw_stream": (C.c_int, [_VP, _VP, C.c_int64, _VP, C.c_int32, C.POINTER(C.c_int32)]),
     "bwagpu_collect_intv": (C.c_int, [_VP, C.POINTER(SeedOpt), C.c_int32, _VP, _VP, C.c_int32, _VP, C.c_int64,

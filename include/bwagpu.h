@@ -545,6 +545,13 @@ int bwagpu_ctx_ext_form(bwagpu_ctx_t *ctx, int form);
    4 = four per wave with the 8-bit row-max key (<32,5,true>), 5 = four per
    wave (<32,8,false>), 2 = two per wave (spec_ext2_kernel<5>) */
 int bwagpu_debug_ext_kernel(bwagpu_ctx_t *ctx, int32_t lq_max);
+/* 1 if work on the two streams (hipStream_t, on the current device) runs
+   concurrently, 0 if they share a hardware queue (HIP maps the process's
+   streams onto GPU_MAX_HW_QUEUES queues; streams on one queue run in
+   submission order), < 0 on error.  Measured: a ~150 us spin on a, then an
+   empty kernel on b.  Callers that drive several batches at once should give
+   them concurrent streams (bench.py's caller_streams). */
+int bwagpu_streams_concurrent(void *a, void *b);
 int bwagpu_prof_intervals(bwagpu_ctx_t *ctx, double *start_ms, double *end_ms, int32_t max, int32_t *n);
 
 #ifdef __cplusplus
