@@ -512,8 +512,8 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
 // validate the flattened batch on the host (cheap O(n) checks so that a
 // malformed batch is an E_INVAL here, never an out-of-bounds access on device);
 // one pass over reads -> chains -> seeds, which also yields the longest read
-int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
-  *lq_max_out = 0;
+// the batch's dimensions and array pointers (O(1)): what the staging copy relies on
+int check_batch_header(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b) {
   if (!b) return fail(ctx, BWAGPU_E_INVAL, "batch is NULL");
   if (b->n_reads < 0 || b->n_chains < 0 || b->n_seeds < 0 || b->seq_bytes < 0)
     return fail(ctx, BWAGPU_E_INVAL, "negative batch dimension");
@@ -529,63 +529,57 @@ int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
   if (b->n_chains && (!b->chain_rid || !b->chain_frac_rep)) return fail(ctx, BWAGPU_E_INVAL, "NULL chain array");
   if (b->n_seeds && !b->seeds) return fail(ctx, BWAGPU_E_INVAL, "NULL seeds");
   if (b->seq_bytes && !b->seq) return fail(ctx, BWAGPU_E_INVAL, "NULL seq");
-  // seeds must lie inside their read and inside [0, 2*l_pac); offsets
-  // monotone.  Large batches are split over a few threads by read range.
-  const int64_t two = ctx->ref.l_pac << 1;
+  return BWAGPU_OK;
+}
+
+// reads [r0, r1) of a header-checked batch: seq_off and the offsets monotone,
+// every read at most BWAGPU_MAX_READ_LEN (*bad_read), every seed inside its
+// read and inside [0, 2*l_pac).  -> 0 ok, 1 seq_off, 2 read too long, 3 rco,
+// 4 cso, 5 seed; *lmax = the longest read.
+int check_reads(const bwagpu_batch_t* b, int64_t l_pac, int r0, int r1, int64_t* lmax, int* bad_read) {
+  const int64_t two = l_pac << 1;
   const int64_t* so = b->seq_off;
   const int32_t* rco = b->read_chain_off;
   const int32_t* cso = b->chain_seed_off;
   const bwagpu_seed_t* sd = b->seeds;
-  // 0 ok, 1 seq_off not monotone, 2 read too long (*bad_read), 3 rco, 4 cso, 5 seed
-  auto check_range = [&](int r0, int r1, int64_t* lmax, int* bad_read) -> int {
-    int64_t lm = 0;
-    for (int r = r0; r < r1; ++r) {
-      const int64_t l = so[r + 1] - so[r];
-      if (l < 0) return 1;
-      if (l > BWAGPU_MAX_READ_LEN) {
-        *bad_read = r;
-        return 2;
-      }
-      lm = std::max(lm, l);
-      // every offset is range-checked BEFORE it indexes: a range may start
-      // anywhere, and a later read's failing check must not come after an
-      // earlier read walked past the caller's arrays
-      const int c0 = rco[r], c1 = rco[r + 1];
-      if (c0 < 0 || c1 < c0 || c1 > b->n_chains) return 3;
-      bool bad_seed = false;
-      for (int c = c0; c < c1; ++c) {
-        const int k0 = cso[c], k1 = cso[c + 1];
-        if (k0 < 0 || k1 < k0 || k1 > b->n_seeds) return 4;
-        for (int k = k0; k < k1; ++k) {  // branch-free accumulation: one test per read
-          const bwagpu_seed_t& s = sd[k];
-          bad_seed |= (s.qbeg < 0) | (s.len <= 0) | ((int64_t)s.qbeg + s.len > l) | (s.rbeg < 0) | (s.rbeg + s.len > two);
-        }
-      }
-      if (bad_seed) return 5;
+  int64_t lm = 0;
+  for (int r = r0; r < r1; ++r) {
+    const int64_t l = so[r + 1] - so[r];
+    if (l < 0) return 1;
+    if (l > BWAGPU_MAX_READ_LEN) {
+      *bad_read = r;
+      return 2;
     }
-    *lmax = lm;
-    return 0;
-  };
-  const int nt = b->n_seeds >= (1 << 16) ? 4 : 1;
-  int code[4] = {0, 0, 0, 0}, bad_read[4] = {0, 0, 0, 0};
-  int64_t lmaxs[4] = {0, 0, 0, 0};
-  {
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t)
-      th.emplace_back([&, t] {
-        code[t] = check_range((int)((int64_t)b->n_reads * t / nt), (int)((int64_t)b->n_reads * (t + 1) / nt), &lmaxs[t],
-                              &bad_read[t]);
-      });
-    code[0] = check_range(0, (int)((int64_t)b->n_reads / nt), &lmaxs[0], &bad_read[0]);
-    for (auto& x : th) x.join();
+    lm = std::max(lm, l);
+    // every offset is range-checked BEFORE it indexes: a range may start
+    // anywhere, and a later read's failing check must not come after an
+    // earlier read walked past the caller's arrays
+    const int c0 = rco[r], c1 = rco[r + 1];
+    if (c0 < 0 || c1 < c0 || c1 > b->n_chains) return 3;
+    bool bad_seed = false;
+    for (int c = c0; c < c1; ++c) {
+      const int k0 = cso[c], k1 = cso[c + 1];
+      if (k0 < 0 || k1 < k0 || k1 > b->n_seeds) return 4;
+      for (int k = k0; k < k1; ++k) {  // branch-free accumulation: one test per read
+        const bwagpu_seed_t& s = sd[k];
+        bad_seed |= (s.qbeg < 0) | (s.len <= 0) | ((int64_t)s.qbeg + s.len > l) | (s.rbeg < 0) | (s.rbeg + s.len > two);
+      }
+    }
+    if (bad_seed) return 5;
   }
-  for (int t = 0; t < nt; ++t) {  // the first failing range reports, as one sequential pass would
+  *lmax = lm;
+  return 0;
+}
+
+// the first failing range's code as one sequential pass would report it
+int check_report(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, const int* code, const int* bad_read, int nt) {
+  for (int t = 0; t < nt; ++t) {
     switch (code[t]) {
       case 1: return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
       case 2: {
         char m[128];
         snprintf(m, sizeof m, "read %d has length %lld > %d", bad_read[t],
-                 (long long)(so[bad_read[t] + 1] - so[bad_read[t]]), BWAGPU_MAX_READ_LEN);
+                 (long long)(b->seq_off[bad_read[t] + 1] - b->seq_off[bad_read[t]]), BWAGPU_MAX_READ_LEN);
         return fail(ctx, BWAGPU_E_UNSUPPORTED, m);
       }
       case 3: return fail(ctx, BWAGPU_E_INVAL, "read_chain_off not monotone");
@@ -594,7 +588,90 @@ int check_batch(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
       default: break;
     }
   }
+  return BWAGPU_OK;
+}
+
+// every read, chain and seed (O(n), after check_batch_header): the longest read -> *lq_max_out
+int check_batch_seeds(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_out) {
+  *lq_max_out = 0;
+  if (b->n_reads == 0) return BWAGPU_OK;
+  const int nt = b->n_seeds >= (1 << 16) ? 4 : 1;
+  int code[4] = {0, 0, 0, 0}, bad_read[4] = {0, 0, 0, 0};
+  int64_t lmaxs[4] = {0, 0, 0, 0};
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t)
+      th.emplace_back([&, t] {
+        code[t] = check_reads(b, ctx->ref.l_pac, (int)((int64_t)b->n_reads * t / nt),
+                              (int)((int64_t)b->n_reads * (t + 1) / nt), &lmaxs[t], &bad_read[t]);
+      });
+    code[0] = check_reads(b, ctx->ref.l_pac, 0, (int)((int64_t)b->n_reads / nt), &lmaxs[0], &bad_read[0]);
+    for (auto& x : th) x.join();
+  }
+  if (int rc = check_report(ctx, b, code, bad_read, nt)) return rc;
   *lq_max_out = (int)std::max(std::max(lmaxs[0], lmaxs[1]), std::max(lmaxs[2], lmaxs[3]));
+  return BWAGPU_OK;
+}
+
+// The staging copy and the check in one pass (bwagpu_chain2aln_submit): nt
+// threads, each a read range in blocks of 1024 reads — a block's arrays are
+// copied into the pinned staging buffer h (layout L), then checked while still
+// in cache.  A block's copy ranges come from its boundary offsets, which are
+// range-checked first, so a malformed batch never makes the copy leave the
+// caller's arrays (sizes from the header); it is refused after the pass.
+int stage_and_check(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, char* h, const InLayout& L, int* lq_max_out) {
+  *lq_max_out = 0;
+  const int nr = b->n_reads;
+  if (nr == 0) return BWAGPU_OK;
+  constexpr int kBlk = 1024, kMaxT = 8;
+  const int nt = b->n_seeds >= (1 << 16) ? kMaxT : 1;
+  const int nblk = (nr + kBlk - 1) / kBlk;
+  int code[kMaxT] = {}, bad_read[kMaxT] = {};
+  int64_t lmaxs[kMaxT] = {};
+  auto work = [&](int t) {
+    // this thread's blocks: [nblk*t/nt, nblk*(t+1)/nt), in order
+    for (int k = (int)((int64_t)nblk * t / nt), ke = (int)((int64_t)nblk * (t + 1) / nt); k < ke; ++k) {
+      const int r0 = k * kBlk, r1 = std::min(nr, r0 + kBlk);
+      const int64_t b0 = b->seq_off[r0], b1 = b->seq_off[r1];
+      const int c0 = b->read_chain_off[r0], c1 = b->read_chain_off[r1];
+      if (b0 < 0 || b1 < b0 || b1 > b->seq_bytes) {
+        code[t] = 1;
+        return;
+      }
+      if (c0 < 0 || c1 < c0 || c1 > b->n_chains) {
+        code[t] = 3;
+        return;
+      }
+      const int k0 = b->chain_seed_off[c0], k1 = b->chain_seed_off[c1];
+      if (k0 < 0 || k1 < k0 || k1 > b->n_seeds) {
+        code[t] = 4;
+        return;
+      }
+      const int re = r1 == nr ? r1 + 1 : r1, ce = c1 == b->n_chains ? c1 + 1 : c1;  // the last block: the end offsets
+      memcpy(h + L.seq_off + sizeof(int64_t) * r0, b->seq_off + r0, sizeof(int64_t) * (size_t)(re - r0));
+      memcpy(h + L.rco + sizeof(int32_t) * r0, b->read_chain_off + r0, sizeof(int32_t) * (size_t)(re - r0));
+      memcpy(h + L.cso + sizeof(int32_t) * c0, b->chain_seed_off + c0, sizeof(int32_t) * (size_t)(ce - c0));
+      if (c1 > c0) {
+        memcpy(h + L.rid + sizeof(int32_t) * c0, b->chain_rid + c0, sizeof(int32_t) * (size_t)(c1 - c0));
+        memcpy(h + L.frac + sizeof(float) * c0, b->chain_frac_rep + c0, sizeof(float) * (size_t)(c1 - c0));
+      }
+      if (k1 > k0) memcpy(h + L.seeds + sizeof(bwagpu_seed_t) * k0, b->seeds + k0, sizeof(bwagpu_seed_t) * (size_t)(k1 - k0));
+      if (b1 > b0) memcpy(h + L.seq + b0, b->seq + b0, (size_t)(b1 - b0));
+      int64_t lm = 0;
+      if ((code[t] = check_reads(b, ctx->ref.l_pac, r0, r1, &lm, &bad_read[t]))) return;
+      lmaxs[t] = std::max(lmaxs[t], lm);
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  }
+  if (int rc = check_report(ctx, b, code, bad_read, nt)) return rc;
+  int64_t lm = 0;
+  for (int t = 0; t < nt; ++t) lm = std::max(lm, lmaxs[t]);
+  *lq_max_out = (int)lm;
   return BWAGPU_OK;
 }
 
@@ -889,9 +966,8 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
   int lq_max = 0;
-  int rc = check_batch(ctx, b, &lq_max);
+  int rc = check_batch_header(ctx, b);
   if (rc) return rc;
-  if ((rc = check_lds(ctx, lq_max))) return rc;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   s.t_submit = std::chrono::steady_clock::now();
   s.n_reads = b->n_reads;
@@ -916,41 +992,18 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
                       (const void*)b->seeds == (const void*)(h + L.seeds) &&
                       (const void*)b->seq == (const void*)(h + L.seq) &&
                       (const void*)b->chain_seed_off == (const void*)(h + L.cso);
+  // the staging copy (~20 MB for a C2 record) and the check of every read,
+  // chain and seed in one pass on a few threads (stage_and_check): nothing is
+  // enqueued before both are done, so a refused batch leaves no DMA reading
+  // the staging buffer
   if (!staged && b->n_reads) {
-    // the staging copy (~20 MB for a C2 record) on a few threads: one thread's
-    // memcpy into pinned pages runs at a fraction of the host's bandwidth
-    struct Piece {
-      char* dst;
-      const void* src;
-      size_t n;
-    };
-    std::vector<Piece> pieces = {
-        {h + L.seq_off, b->seq_off, sizeof(int64_t) * (size_t)(b->n_reads + 1)},
-        {h + L.rco, b->read_chain_off, sizeof(int32_t) * (size_t)(b->n_reads + 1)},
-        {h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1)},
-        {h + L.rid, b->chain_rid, sizeof(int32_t) * (size_t)b->n_chains},
-        {h + L.frac, b->chain_frac_rep, sizeof(float) * (size_t)b->n_chains},
-        {h + L.seeds, b->seeds, sizeof(bwagpu_seed_t) * (size_t)b->n_seeds},
-        {h + L.seq, b->seq, (size_t)b->seq_bytes}};
-    size_t total = 0;
-    for (const Piece& q : pieces) total += q.n;
-    const int nt = total >= ((size_t)4 << 20) ? 4 : 1;
-    auto copy_part = [&](int t) {  // byte range [total*t/nt, total*(t+1)/nt) of the concatenation
-      const size_t lo = total * (size_t)t / (size_t)nt, hi = total * (size_t)(t + 1) / (size_t)nt;
-      size_t at = 0;
-      for (const Piece& q : pieces) {
-        const size_t a = std::max(lo, at), e = std::min(hi, at + q.n);
-        if (a < e) memcpy(q.dst + (a - at), (const char*)q.src + (a - at), e - a);
-        at += q.n;
-      }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(copy_part, t);
-    copy_part(0);
-    for (auto& x : th) x.join();
-  } else if (!staged) {
-    memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
+    rc = stage_and_check(ctx, b, h, L, &lq_max);
+  } else {
+    if (!staged) memcpy(h + L.cso, b->chain_seed_off, sizeof(int32_t) * (size_t)(b->n_chains + 1));
+    rc = check_batch_seeds(ctx, b, &lq_max);
   }
+  if (rc) return rc;
+  if ((rc = check_lds(ctx, lq_max))) return rc;
 
   hipStream_t st = nullptr;
   HIPC(lazy_stream(s, &st), "hipStreamCreate");

@@ -113,6 +113,8 @@ class Engine:
     def __init__(self, device: int, opt: dict, l_pac: int, ann_offset, ann_len, pac=None,
                  pac_device_ptr: int | None = None):
         self.lib = abi.load()
+        self.device = device
+        self._args = (device, opt, l_pac, ann_offset, ann_len, pac, pac_device_ptr)
         self.opt = abi.opt_from_dict(opt)
         self._ann_off = np.ascontiguousarray(ann_offset, np.int64)
         self._ann_len = np.ascontiguousarray(ann_len, np.int32)
@@ -129,6 +131,11 @@ class Engine:
                                         C.byref(self.ctx))
         if rc != abi.OK:
             raise BwaGpuError(rc, "bwagpu_create failed")
+
+    def clone(self) -> "Engine":
+        """another context on the same device with the same options and reference
+        (a second stage worker); the FM-index is not carried over (set_bwt)"""
+        return Engine(*self._args[:5], pac=self._args[5], pac_device_ptr=self._args[6])
 
     def close(self):
         if self.ctx:

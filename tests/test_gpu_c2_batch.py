@@ -64,3 +64,32 @@ def test_reference_seeded_device_entry():
     assert np.array_equal(n, want_n)
     assert G.region_mismatch(compact(batch, regs, n), want) is None
     eng.close()
+
+
+def test_full_batch_malformed_refused():
+    """a C2-sized batch goes through the multi-threaded stage-and-check pass of
+    bwagpu_chain2aln_submit (blocks of 1024 reads on 8 threads): a bad seed deep
+    inside it, or offsets that turn back at a block boundary, are refused with
+    E_INVAL before anything is enqueued, and the same context then serves the
+    intact batch with the reference's regions"""
+    from bwagpu import workload
+    from bwagpu.engine import Batch, BwaGpuError
+    opt, ref, rbs = workload.load_fixture()
+    rb = rbs[0]
+    b = rb.batch
+    assert b.n_seeds >= 1 << 16 and b.n_reads > 8 * 1024
+    eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
+    sd = b.seeds.copy()
+    k = int(b.chain_seed_off[b.read_chain_off[40_000]])  # a seed of read 40 000 (block 39, thread 4)
+    sd[k]["qbeg"] = 10_000  # outside its read
+    bad_seed = Batch(b.seq_off, b.seq, b.read_chain_off, b.chain_seed_off, b.chain_rid, b.chain_frac_rep, sd)
+    rco = b.read_chain_off.copy()
+    rco[5 * 1024] = rco[5 * 1024 + 1] + 1  # turns back at the boundary of blocks 4 and 5
+    bad_off = Batch(b.seq_off, b.seq, rco, b.chain_seed_off, b.chain_rid, b.chain_frac_rep, b.seeds)
+    for bad in (bad_seed, bad_off):
+        with pytest.raises(BwaGpuError) as e:
+            eng.chain2aln(bad)
+        assert e.value.code == abi.E_INVAL
+    regs, n = eng.chain2aln(b)
+    assert rb.check(regs, n)
+    eng.close()

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--budget", type=int, default=-1, help="seeding tier-1 budget (-1: library default)")
+    ap.add_argument("--concurrent", type=int, default=0,
+                    help="also: N contexts on N host threads, each running seqs2chains (pipeline throughput)")
     a = ap.parse_args()
     opt, gref, rbs = workload.load_fixture()
     rb = rbs[0]
@@ -51,6 +53,30 @@ def main():
         res["seqs2regions_ms"] = round((time.perf_counter() - t0) * 1e3 / a.reps, 3)
         n, regs = eng.seqs2regions(so, sq)
         res["regions_ok"] = bool(rb.check_compact(regs, n))
+    if a.concurrent:
+        import threading
+        engs = [eng] + [Engine(0, opt, gref.l_pac, gref.ann_offset, gref.ann_len, pac=gref.pac)
+                        for _ in range(a.concurrent - 1)]
+        for e in engs[1:]:
+            e.set_bwt(hdr, words, sa, sa_intv)
+            e.seqs2chains(so, sq, copy=False)
+        for fn, key in (("seqs2chains", "conc_seqs2chains_ms_per_batch"), ("seqs2regions", "conc_seqs2regions_ms_per_batch")):
+            bar = threading.Barrier(len(engs) + 1)
+
+            def work(e):
+                bar.wait()
+                for _ in range(a.reps):
+                    getattr(e, fn)(so, sq, copy=False)
+
+            th = [threading.Thread(target=work, args=(e,)) for e in engs]
+            for t in th:
+                t.start()
+            bar.wait()
+            t0 = time.perf_counter()
+            for t in th:
+                t.join()
+            res[key] = round((time.perf_counter() - t0) * 1e3 / (a.reps * len(engs)), 3)
+        res["concurrent"] = a.concurrent
     print(json.dumps(res))
 
 
