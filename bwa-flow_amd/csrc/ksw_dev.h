@@ -787,6 +787,9 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   const int sk = 32 - __builtin_clz((unsigned)max(o.max_mat, 1));  // 2^sk > max(mat)
   const uint32_t KSH = pk(1 << sk, 1 << sk);
   const uint32_t RE = pk(e_ins * j0, e_ins * j0), RE2 = pk(e_ins * (j0 + CPL), e_ins * (j0 + CPL));
+  // the key's multiplier kept opaque: a visible power of two makes LLVM split
+  // the v_pk_mad_u16 into a shift and an add
+  const uint32_t KMUL = opq(K8 ? pk(256, 256) : pk(1 << KS, 1 << KS));
   uint32_t hh[CPL], ee[CPL], pfa[CPL], pfb[CPL], qm[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
@@ -838,16 +841,18 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     const uint32_t LEFT0 = neg15(sub(LO, ONE)) & smax(GL, 0u);  // the first-column value where lo == 0
     GL = ssat(GL, ED1);
     const uint32_t SEL = (uint32_t)ta | ((uint32_t)tbb << 16) | 0x0c040c00u;
-    const uint32_t HI1 = add(HI, ONE);
     uint32_t MB[CPL], AA[CPL], CAP[CPL], R[CPL], GEL[CPL];
     uint32_t T = 0;
+    // j <= hi  <=>  j - 1 < hi: column c's R is column c-1's "j < hi"
+    R[0] = neg15(sub(add(J0, 0xffffffffu), HI));
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const uint32_t JC = add(J0, pk(c, c));
       const uint32_t ltlo = neg15(sub(JC, LO));  // j < lo
-      R[c] = neg15(sub(JC, HI1));                // j <= hi
+      const uint32_t lthi = neg15(sub(JC, HI));  // j < hi
+      if (c + 1 < CPL) R[c + 1] = lthi;
       GEL[c] = ~ltlo;
-      CAP[c] = neg15(sub(JC, HI)) & ~ltlo;       // lo <= j < hi
+      CAP[c] = lthi & ~ltlo;                     // lo <= j < hi
       const uint32_t sb = __builtin_amdgcn_perm(pfb[c], pfa[c], SEL);
       const uint32_t mb = smin(add(hh[c], sb), mad(hh[c], KSH, 0x00800080u));  // M' + 128
       MB[c] = mb;
@@ -871,9 +876,9 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       hm[c] = umin(h, CAP[c]);
       const uint32_t en = usat(smax(ee[c], sub(MB[c], MB_OD)), ED1);
       if constexpr (K8)
-        LK = umax(LK, mad(hm[c], pk(256, 256), add(J0, pk(c, c))));
+        LK = umax(LK, mad(hm[c], KMUL, add(J0, pk(c, c))));
       else
-        LK = umax(LK, mad(hm[c], pk(1 << KS, 1 << KS), pk(c, c)));
+        LK = umax(LK, mad(hm[c], KMUL, pk(c, c)));
       ee[c] = sel(R[c], umin(en, CAP[c]), ee[c]);
       if (c > 0) hh[c] = sel(R[c], hm[c - 1], hh[c]);
       H1Q |= hm[c] & qm[c];
