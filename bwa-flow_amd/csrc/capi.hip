@@ -262,7 +262,7 @@ struct bwagpu_ctx {
   hipEvent_t a2_fork = nullptr, a2_join[kA2Streams] = {};
   // seeding (bwagpu_set_bwt / bwagpu_collect_intv): the resident FM-index and
   // the batch buffers
-  DevBuf bwt_words, sa_d, sa_in, sa_out, occ_d, sup_d;
+  DevBuf bwt_words, sa_d, sa_in, sa_out, occ_d, sup_d, sa_full;
   DevBwt bwt{};
   bool has_bwt = false;
   DevBuf sd_off, sd_seq, sd_out, sd_n, sd_scratch, sd_poff, sd_pack, sd_heavy, sd_dbg;
@@ -489,7 +489,7 @@ void destroy_ctx(bwagpu_ctx_t* ctx) {
   if (ctx->ch_cs.fork) (void)hipEventDestroy(ctx->ch_cs.fork);
   ctx->ch_slot.d_out.release(); ctx->ch_slot.d_n.release(); ctx->ch_slot.d_stats.release();
   for (DevBuf* b : {&ctx->r2_tasks, &ctx->r2_q, &ctx->r2_out, &ctx->r2_cig, &ctx->r2_md, &ctx->r2_lists, &ctx->r2_z,
-                    &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->occ_d, &ctx->sup_d, &ctx->sd_off,
+                    &ctx->r2_stats, &ctx->bwt_words, &ctx->sa_d, &ctx->sa_in, &ctx->sa_out, &ctx->occ_d, &ctx->sup_d, &ctx->sa_full, &ctx->sd_off,
                     &ctx->sd_seq, &ctx->sd_out, &ctx->sd_n, &ctx->sd_scratch, &ctx->sd_poff, &ctx->sd_pack,
                     &ctx->sd_heavy, &ctx->sd_dbg, &ctx->st_buf, &ctx->st_start, &ctx->st_q, &ctx->st_tasks, &ctx->st_lists,
                     &ctx->st_seen, &ctx->st_ctr, &ctx->st_out, &ctx->ch_npos, &ctx->ch_posoff, &ctx->ch_frac,
@@ -1850,6 +1850,8 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
   ctx->bwt.sa = nullptr;
   ctx->bwt.sa_mask = 0;
   ctx->bwt.sa_shift = 0;
+  ctx->bwt.sa_full32 = nullptr;
+  ctx->bwt.sa_full64 = nullptr;
   if (bwt->sa) {
     const int iv = bwt->sa_intv;
     if (iv < 1 || (iv & (iv - 1)) || bwt->n_sa < bwt->seq_len / (uint64_t)iv + 1)
@@ -1859,6 +1861,26 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
     ctx->bwt.sa = ctx->sa_d.as<uint64_t>();
     ctx->bwt.sa_mask = (uint64_t)iv - 1;
     while ((1 << ctx->bwt.sa_shift) < iv) ++ctx->bwt.sa_shift;
+    // every row's entry in HBM (one load per bwt_sa instead of a walk of ~sa_intv
+    // dependent occurrence lookups): 32-bit entries below 2^32 rows (chr21: 0.37
+    // GB), 64-bit above, within 8 GB and a quarter of the free memory;
+    // BWAGPU_SA_FULL=0 keeps the sampled walk
+    const char* fe = getenv("BWAGPU_SA_FULL");
+    const bool narrow = bwt->seq_len < 0xffffffffull;
+    const uint64_t bytes = (bwt->seq_len + 1) * (narrow ? 4 : 8);
+    size_t free_b = 0, total_b = 0;
+    if (!(fe && fe[0] == '0') && iv > 1 && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        bytes <= ((uint64_t)8 << 30) && bytes <= free_b / 4) {
+      HIPC(ctx->sa_full.ensure((size_t)bytes), "hipMalloc");
+      hipStream_t st = nullptr;
+      HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
+      HIPC(launch_sa_expand(ctx->bwt, narrow ? ctx->sa_full.as<uint32_t>() : nullptr,
+                            narrow ? nullptr : ctx->sa_full.as<uint64_t>(), st),
+           "sa_expand launch");
+      HIPC(hipStreamSynchronize(st), "sync");
+      if (narrow) ctx->bwt.sa_full32 = ctx->sa_full.as<uint32_t>();
+      else ctx->bwt.sa_full64 = ctx->sa_full.as<uint64_t>();
+    }
   }
   ctx->has_bwt = true;
   return BWAGPU_OK;

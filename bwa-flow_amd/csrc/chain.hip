@@ -898,47 +898,72 @@ __global__ void __launch_bounds__(256) chain_sw_apply_kernel(ChainArgs a, ChainS
 }
 
 // ---- the chains out, in bwagpu_batch_t's layout (one lane per read)
+// one wave per read, a lane per chain (64 at a time): the chains' seed offsets
+// by a wave scan of their seed counts, then each lane copies its chain's seeds.
+// (A lane per read left the repeat reads' hundreds of chains to one lane: a
+// 470 us tail per C2 batch.)
 __global__ void __launch_bounds__(256) chain_pack_kernel(ChainArgs a, ChainPack p) {
-  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int r = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int lane = (int)(threadIdx.x & 63);
   if (r >= a.n_reads) return;
   const int64_t base = a.pos_off[r];
-  int64_t co = p.oc_off[r], so = p.os_off[r];
-  p.read_chain_off[r] = (int32_t)co;
-  if (r == a.n_reads - 1) {
-    p.read_chain_off[a.n_reads] = (int32_t)p.oc_off[a.n_reads];
-    p.chain_seed_off[p.oc_off[a.n_reads]] = (int32_t)p.os_off[a.n_reads];
+  const int64_t co0 = p.oc_off[r];
+  int64_t carry = p.os_off[r];
+  if (lane == 0) {
+    p.read_chain_off[r] = (int32_t)co0;
+    if (r == a.n_reads - 1) {
+      p.read_chain_off[a.n_reads] = (int32_t)p.oc_off[a.n_reads];
+      p.chain_seed_off[p.oc_off[a.n_reads]] = (int32_t)p.os_off[a.n_reads];
+    }
   }
   const float fr = a.frac_rep[r];
-  for (int k = 0; k < a.n_out[r]; ++k, ++co) {
-    const DChain c = a.ochains[base + k];
-    bwagpu_chain_t o;
-    o.pos = c.pos;
-    o.rid = c.rid;
-    o.n = c.n;
-    o.w = c.w;
-    o.kept = c.kept;
-    o.first = c.first;
-    o.is_alt = c.is_alt;
-    o.frac_rep = fr;
-    o.pad_ = 0;
-    p.chains[co] = o;
-    p.chain_rid[co] = c.rid;
-    p.chain_frac[co] = fr;
-    p.chain_seed_off[co] = (int32_t)so;
-    for (int j = 0; j < c.n; ++j, ++so) {
-      const int q = a.oslist[base + c.soff + j];
-      bwagpu_seed_t sd;
-      sd.rbeg = (int64_t)a.rbeg[base + q];
-      sd.qbeg = a.qinfo[base + q].x;
-      sd.len = a.qinfo[base + q].y;
-      sd.score = a.score[base + q];
-      sd.pad_ = 0;
-      p.seeds[so] = sd;
+  const int nout = a.n_out[r];
+  for (int k0 = 0; k0 < nout; k0 += 64) {
+    const int k = k0 + lane;
+    const bool valid = k < nout;
+    DChain c{};
+    if (valid) c = a.ochains[base + k];
+    int incl = valid ? c.n : 0;  // inclusive scan of the seed counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      incl += lane >= o ? y : 0;
     }
+    if (valid) {
+      const int64_t co = co0 + k;
+      int64_t so = carry + incl - c.n;
+      bwagpu_chain_t out;
+      out.pos = c.pos;
+      out.rid = c.rid;
+      out.n = c.n;
+      out.w = c.w;
+      out.kept = c.kept;
+      out.first = c.first;
+      out.is_alt = c.is_alt;
+      out.frac_rep = fr;
+      out.pad_ = 0;
+      p.chains[co] = out;
+      p.chain_rid[co] = c.rid;
+      p.chain_frac[co] = fr;
+      p.chain_seed_off[co] = (int32_t)so;
+      for (int j = 0; j < c.n; ++j, ++so) {
+        const int q = a.oslist[base + c.soff + j];
+        bwagpu_seed_t sd;
+        sd.rbeg = (int64_t)a.rbeg[base + q];
+        sd.qbeg = a.qinfo[base + q].x;
+        sd.len = a.qinfo[base + q].y;
+        sd.score = a.score[base + q];
+        sd.pad_ = 0;
+        p.seeds[so] = sd;
+      }
+    }
+    carry += __shfl(incl, 63, 64);
   }
 }
 
-// exclusive scan, one workgroup: each thread sums a contiguous run
+// exclusive scan, one workgroup: each thread sums a contiguous run, eight
+// independent loads at a time (one load per iteration left every thread
+// waiting on each of its ~65 scattered loads in turn: 110 us per C2 batch)
 __global__ void __launch_bounds__(1024) scan_i32_kernel(const int32_t* __restrict__ in, int64_t* __restrict__ out,
                                                         int32_t n) {
   __shared__ int64_t part[1024];
@@ -946,7 +971,15 @@ __global__ void __launch_bounds__(1024) scan_i32_kernel(const int32_t* __restric
   const int per = (n + 1023) / 1024;
   const int b = t * per, e = min(n, b + per);
   int64_t s = 0;
-  for (int i = b; i < e; ++i) s += in[i];
+  int i = b;
+  for (; i + 8 <= e; i += 8) {
+    int v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = in[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  for (; i < e; ++i) s += in[i];
   part[t] = s;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
@@ -956,7 +989,18 @@ __global__ void __launch_bounds__(1024) scan_i32_kernel(const int32_t* __restric
     __syncthreads();
   }
   int64_t run = t ? part[t - 1] : 0;
-  for (int i = b; i < e; ++i) {
+  i = b;
+  for (; i + 8 <= e; i += 8) {
+    int v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = in[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      out[i + k] = run;
+      run += v[k];
+    }
+  }
+  for (; i < e; ++i) {
     out[i] = run;
     run += in[i];
   }
@@ -1039,7 +1083,7 @@ hipError_t launch_chain_sw_apply(const ChainArgs& a, const ChainSw& s, hipStream
 
 hipError_t launch_chain_pack(const ChainArgs& a, const ChainPack& p, hipStream_t st) {
   if (a.n_reads <= 0) return hipSuccess;
-  hipLaunchKernelGGL(chain_pack_kernel, lanes(a.n_reads), dim3(256), 0, st, a, p);
+  hipLaunchKernelGGL(chain_pack_kernel, lanes(64 * (int64_t)a.n_reads), dim3(256), 0, st, a, p);
   return hipGetLastError();
 }
 

@@ -20,6 +20,11 @@ struct DevBwt {
   const uint64_t* sa;    // sampled suffix array (NULL if not uploaded)
   uint64_t sa_mask;      // sa_intv - 1
   int sa_shift;          // log2(sa_intv)
+  // the whole suffix array, one entry per row 0..seq_len, expanded from the
+  // sample on the device (bwagpu_set_bwt) when it fits the budget: 32-bit
+  // entries while seq_len < 2^32, else 64-bit; both NULL: the sampled walk
+  const uint32_t* sa_full32;
+  const uint64_t* sa_full64;
 };
 
 // the device occurrence layout of a BWT of seq_len positions ($ removed):
@@ -54,6 +59,8 @@ inline int64_t seed_scratch_entries(int64_t bases, int32_t n_reads) { return 4 *
 hipError_t launch_collect_intv(const DevBwt& b, const SeedArgs& a, hipStream_t st);
 // bwt_sa for n positions
 hipError_t launch_bwt_sa(const DevBwt& b, int64_t n, const uint64_t* k, uint64_t* out, hipStream_t st);
+// every row's suffix array entry from the sample (b.sa set): o32 or o64 (one of them), seq_len + 1 entries
+hipError_t launch_sa_expand(const DevBwt& b, uint32_t* o32, uint64_t* o64, hipStream_t st);
 // packs the per-read slots: read r's out_n[r] intervals to dst + off[r]
 hipError_t launch_pack_intv(const SeedArgs& a, const int64_t* off, bwagpu_intv_t* dst, hipStream_t st);
 

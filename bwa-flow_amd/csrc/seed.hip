@@ -1046,24 +1046,58 @@ __global__ void __launch_bounds__(256) pack_intv_kernel(SeedArgs a, const int64_
 
 // bwt_sa (bwt.c:86-96): one lane per position; every LF step reads one
 // 64-byte occurrence block (bwt_B0 and bwt_occ of a step fall in the same one)
+// one step of bwt_sa's walk: bwt_invPsi (bwt.c:53-59), the row whose suffix
+// starts one position earlier (its SA entry is this row's minus one)
+__device__ __forceinline__ uint64_t sa_step(const DevBwt& b, uint64_t k) {
+  if (k == b.primary) return 0;
+  const uint64_t x = k - (k > b.primary);
+  const int c = base_at(b, x);  // bwt_B0
+  uint64_t cnt[4];
+  occ4(b, k, cnt);  // bwt_occ(k, c); k == seq_len gives the column total
+  return b.L2[c] + cnt[c];
+}
+
 __global__ void __launch_bounds__(256) bwt_sa_kernel(DevBwt b, int64_t n, const uint64_t* __restrict__ kin,
                                                      uint64_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t k = kin[i], steps = 0;
-  while (k & b.sa_mask) {
+  if (b.sa_full32) {  // the expanded suffix array: one load (row 0's stored -1 comes back 64-bit)
+    const uint32_t v = b.sa_full32[k];
+    out[i] = v == 0xffffffffu ? ~0ull : (uint64_t)v;
+    return;
+  }
+  if (b.sa_full64) {
+    out[i] = b.sa_full64[k];
+    return;
+  }
+  while (k & b.sa_mask) {  // bwt_sa (bwt.c:86-96): walk to a sampled row
     ++steps;
-    if (k == b.primary) {  // bwt_invPsi (bwt.c:53-59)
-      k = 0;
-      continue;
-    }
-    const uint64_t x = k - (k > b.primary);
-    const int c = base_at(b, x);  // bwt_B0
-    uint64_t cnt[4];
-    occ4(b, k, cnt);  // bwt_occ(k, c); k == seq_len gives the column total
-    k = b.L2[c] + cnt[c];
+    k = sa_step(b, k);
   }
   out[i] = steps + b.sa[k >> b.sa_shift];
+}
+
+// The whole suffix array from the sample: a thread per sampled row walks
+// bwt_sa's steps from it — each step's row has the entry one smaller — and
+// writes every row it passes until the next sampled row.  The step is a
+// permutation of the rows, so every row is written exactly once; the rows an
+// unsampled row's walk in bwt_sa_kernel would reach give the same value.  Row
+// 0 (the sentinel's suffix) keeps its stored entry, -1 (bwt_cal_sa sets it,
+// bwt.c:181), while the walk from it counts down from its true entry, seq_len.
+__global__ void __launch_bounds__(256) sa_expand_kernel(DevBwt b, uint64_t n_sampled, uint32_t* __restrict__ o32,
+                                                        uint64_t* __restrict__ o64) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_sampled) return;
+  uint64_t k = s << b.sa_shift, v = s == 0 ? b.seq_len : b.sa[s];
+  for (;;) {
+    const uint64_t w = k == 0 ? b.sa[0] : v;
+    if (o32) o32[k] = (uint32_t)w;
+    else o64[k] = w;
+    k = sa_step(b, k);
+    if (!(k & b.sa_mask)) break;
+    --v;
+  }
 }
 
 }  // namespace
@@ -1078,6 +1112,12 @@ hipError_t launch_build_occ64(const DevBwt& b, uint4* occ, uint64_t* sup, hipStr
 hipError_t launch_bwt_sa(const DevBwt& b, int64_t n, const uint64_t* k, uint64_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(bwt_sa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, b, n, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sa_expand(const DevBwt& b, uint32_t* o32, uint64_t* o64, hipStream_t st) {
+  const uint64_t n = (b.seq_len >> b.sa_shift) + 1;  // sampled rows 0, sa_intv, ... <= seq_len
+  hipLaunchKernelGGL(sa_expand_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, b, n, o32, o64);
   return hipGetLastError();
 }
 

@@ -140,3 +140,29 @@ def test_bwt_sa_of_collected_intervals(eng):
     hdr, words = G.load_seed_bwt()
     intv, sa, _, _ = G.load_seed_sa()
     assert np.array_equal(eng.bwt_sa(ks), oracle.bwt_sa(hdr, words, sa, intv, ks))
+
+
+def test_expanded_suffix_array_equals_the_walk(monkeypatch):
+    """bwagpu_set_bwt expands the sampled suffix array into every row's entry
+    (one load per bwt_sa); BWAGPU_SA_FULL=0 keeps bwt.c's walk to a sampled
+    row.  Both give the reference's values at the golden positions, and the
+    two agree at EVERY row 0..seq_len of the golden index"""
+    refd = G.load_ref()
+    opt, *_ = G.load_chain_set("c1_default")
+    hdr, words = G.load_seed_bwt()
+    intv, sa, q, want = G.load_seed_sa()
+    engs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("BWAGPU_SA_FULL", mode)
+        e = Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
+        e.set_bwt(hdr, words, sa, intv)
+        assert np.array_equal(e.bwt_sa(q), want)
+        engs[mode] = e
+    rows = np.arange(int(hdr[6]) + 1, dtype=np.uint64)
+    full, walk = engs["1"].bwt_sa(rows), engs["0"].bwt_sa(rows)
+    assert np.array_equal(full, walk)
+    # a permutation of 0..seq_len-1 plus row 0's stored -1 (bwt_cal_sa, bwt.c:181)
+    want_set = np.append(np.arange(len(rows) - 1, dtype=np.uint64), np.uint64(2**64 - 1))
+    assert np.array_equal(np.sort(full), want_set)
+    for e in engs.values():
+        e.close()
