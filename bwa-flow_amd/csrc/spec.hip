@@ -736,386 +736,6 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
 // LDS bytes of a spec_ext4_kernel workgroup
 static size_t ext4_lds(int tb_bytes, int g) { return (size_t)(kBlock / g) * (4 * (size_t)tb_bytes + 2 * kQTaskLds); }
 
-// ---------------------------------------------- the same, a task's next call inside the row loop
-// extend_quad's row loop runs until the longest of its eight calls ends: 24.5 %
-// of the call-slot cells it issued on C2 belonged to calls that had already
-// ended, and a task's two sides run in two loops, each
-// as long as its longest call.  Here, at the row where a sub-slot's call ends,
-// its result goes into the task (qtask_advance) and the sub-slot starts the
-// task's next call (the band retry, the other side) at the next row: both
-// target windows are in LDS since the task's start, so this needs no claim
-// and no gather.  A finished task's sub-slot idles until the loop ends; new
-// tasks are claimed between loops, as in spec_ext4_kernel.  The loop's column
-// count is the longer side of the wave's tasks, so every next call fits.
-// Every call's arithmetic is extend_quad's, with the row index per call (I).
-template <int G, int CPL, bool K8>
-__device__ __forceinline__ void quad_next_run(const DevOpt& o, const DevRef& ref, const DevBatch& b,
-                                                const SpecArgs& a, const int2* tlist, ShardQ& qq, bool& more,
-                                                bool& ha, bool& hb, uint8_t* tal, uint8_t* tar, uint8_t* tbl,
-                                                uint8_t* tbr, LdsQ* qa, LdsQ* qb, uint64_t kLead, uint64_t below,
-                                                const QCall& ca0, const QCall& cb0, long long& spec_cells,
-                                                const int trig) {
-  using namespace pk16;
-  int r;  // the lane index in its group, behind an opaque move (see extend_pair)
-  if constexpr (G == 16) asm volatile("v_and_b32 %0, 15, %1" : "=v"(r) : "v"((int)threadIdx.x));
-  else asm volatile("v_and_b32 %0, 31, %1" : "=v"(r) : "v"((int)threadIdx.x));
-  constexpr int KS = CPL <= 2 ? 1 : (CPL <= 4 ? 2 : (CPL <= 8 ? 3 : 4));
-  static_assert(CPL >= 1 && CPL * G <= 256, "columns per call: < 256");
-  const int e_del = o.e_del, e_ins = o.e_ins, oe_ins = o.oe_ins;
-  const int j0 = r * CPL;
-  const uint32_t J0 = pk(j0, j0);
-  const uint32_t EI1 = pk(e_ins, e_ins), ED1 = pk(e_del, e_del);
-  const uint32_t MB_OE = pk(128 + oe_ins, 128 + oe_ins), MB_OD = pk(128 + o.o_del, 128 + o.o_del);
-  const int sk = 32 - __builtin_clz((unsigned)max(o.max_mat, 1));
-  const uint32_t KSH = pk(1 << sk, 1 << sk);
-  const uint32_t RE = pk(e_ins * j0, e_ins * j0), RE2 = pk(e_ins * (j0 + CPL), e_ins * (j0 + CPL));
-  const uint32_t KMUL = opq(K8 ? pk(256, 256) : pk(1 << KS, 1 << KS));
-  uint32_t hh[CPL], ee[CPL], pfa[CPL], pfb[CPL], qm[CPL];
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) hh[c] = ee[c] = pfa[c] = pfb[c] = qm[c] = 0;
-  uint32_t LO = 0, HI = 0, IW = 0, IW1 = 0, GL = 0, EI = 0, ESC = 0, BEST = 0, BI = 0, BJ = 0, OFF = 0, I = 0;
-  uint32_t ROWS = 0, DM = 0xffffffffu, ZD = 0, ZDM = 0, TL2 = 0, QL = 0, PEND = 0;
-  int cellsa = 0, cellsb = 0, qlenA = 1, qlenB = 1, tlenA = 0, tlenB = 0, tna = 0, tnb = 0;
-  const uint8_t* tbA = tal;
-  const uint8_t* tbB = tbl;
-  // a call into one half (0: A, the low 16 bits; 1: B) of the lanes where `on`
-  auto start = [&](const int half, const QCall& c, const bool on) {
-    const uint32_t M = on ? (half ? 0xffff0000u : 0x0000ffffu) : 0u;
-#pragma unroll
-    for (int cc = 0; cc < CPL; ++cc) {
-      const int j = j0 + cc;
-      const int qv = c.q[c.qa + c.qd * min(j, c.qlen - 1)];  // qlen >= 1 for every call, idle ones too
-      const uint32_t pf = qprof_word(o, j < c.qlen ? qv : 0) ^ 0x80808080u;
-      if (half == 0) pfa[cc] = on ? pf : pfa[cc];
-      else pfb[cc] = on ? pf : pfb[cc];
-      const int v = j == 0 ? c.h0 : max(c.h0 - oe_ins - (j - 1) * e_ins, 0);  // ksw.c:392-395
-      const int hv = j <= c.qlen ? v : 0;
-      hh[cc] = sel(M, pk(hv, hv), hh[cc]);
-      ee[cc] &= ~M;
-      qm[cc] = sel(M, j == c.qlen - 1 ? 0xffffffffu : 0u, qm[cc]);
-    }
-    const int wv = min(c.w, min(band_cap_dev(c.qlen, o.max_mat, c.eb, o.o_ins, e_ins),
-                                band_cap_dev(c.qlen, o.max_mat, c.eb, o.o_del, e_del)));  // ksw.c:399-407
-    LO &= ~M;
-    HI = sel(M, pk(c.qlen, c.qlen), HI);
-    IW = sel(M, pk(-wv, -wv), IW);
-    IW1 = sel(M, pk(wv + 1, wv + 1), IW1);
-    GL = sel(M, pk(c.h0 - o.o_del - e_del, c.h0 - o.o_del - e_del), GL);
-    EI |= M;
-    ESC |= M;
-    BEST = sel(M, pk(c.h0, c.h0), BEST);
-    BI |= M;
-    BJ |= M;
-    OFF &= ~M;
-    I &= ~M;
-    ROWS = sel(M, pk(max(c.tlen, 0), max(c.tlen, 0)), ROWS);
-    const uint32_t z = c.tlen <= 0 ? 0xffffffffu : 0u;  // no rows: its result at once (PEND)
-    DM = sel(M, z, DM);
-    PEND |= M & z;
-    ZD = sel(M, pk(min(c.zdrop, 32767), min(c.zdrop, 32767)), ZD);
-    ZDM = sel(M, c.zdrop > 0 ? 0xffffffffu : 0u, ZDM);
-    TL2 = sel(M, pk(c.tlen - 2, c.tlen - 2), TL2);
-    QL = sel(M, pk(c.qlen, c.qlen), QL);
-    if (on) {
-      if (half == 0) {
-        cellsa = 0;
-        qlenA = c.qlen;
-        tbA = c.tb;
-        tlenA = c.tlen;
-        tna = c.tb[0];
-      } else {
-        cellsb = 0;
-        qlenB = c.qlen;
-        tbB = c.tb;
-        tlenB = c.tlen;
-        tnb = c.tb[0];
-      }
-    }
-  };
-  start(0, ca0, ha);
-  start(1, cb0, hb);
-  uint32_t NE = PEND;
-  PEND = 0;
-  for (;;) {
-    if (__builtin_amdgcn_ballot_w64(NE != 0)) {
-      // calls that ended: results into their tasks, then the next calls
-      const bool endA = (NE & 0xffffu) != 0, endB = (NE >> 16) != 0;
-      const int hb0 = (int)(threadIdx.x & (64 - G));  // the group's first lane
-      const uint32_t ea = __shfl(pk(lo16(EI), lo16(ESC)), hb0 + (qlenA - 1) / CPL, 64);
-      const uint32_t eb = __shfl(pk(hi16(EI), hi16(ESC)), hb0 + (qlenB - 1) / CPL, 64);
-      QCall nA = quad_idle(b.seq, tal), nB = quad_idle(b.seq, tbl);
-      bool sA = false, sB = false;
-      if (endA) {
-        const ExtOut x{lo16(BEST), lo16(BJ) + 1, lo16(BI) + 1, lo16(ea) + 1, hi16(ea), lo16(OFF)};
-        const Tally32 tt{cellsa, lo16(ROWS), 1};
-        QTask t = qload(qa);
-        if (qtask_advance(t, o, x, tt)) {
-          store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
-          spec_cells += t.cells;
-          ha = false;
-        } else {
-          nA = qtask_call(t, o, b.seq, tal, tar);
-          qpark(qa, t);
-          sA = nA.qlen < CPL * G;  // always (the loop's CPL covers the task's longer side)
-        }
-      }
-      if (endB) {
-        const ExtOut x{hi16(BEST), hi16(BJ) + 1, hi16(BI) + 1, lo16(eb) + 1, hi16(eb), hi16(OFF)};
-        const Tally32 tt{cellsb, hi16(ROWS), 1};
-        QTask t = qload(qb);
-        if (qtask_advance(t, o, x, tt)) {
-          store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
-          spec_cells += t.cells;
-          hb = false;
-        } else {
-          nB = qtask_call(t, o, b.seq, tbl, tbr);
-          qpark(qb, t);
-          sB = nB.qlen < CPL * G;
-        }
-      }
-      start(0, nA, sA);
-      start(1, nB, sB);
-      NE = PEND;  // calls of no rows: their results before any row runs
-      PEND = 0;
-      continue;
-    }
-    if (!__builtin_amdgcn_ballot_w64(DM != 0xffffffffu)) break;
-    uint32_t NEA = 0;  // the calls that ended since the rows began
-    for (;;) {
-    // one row of every live call (extend_quad's row, the row index per call)
-    const int ta = tna, tbb = tnb;
-    tna = tbA[min(lo16(I) + 1, max(tlenA - 1, 0))];  // prefetch
-    tnb = tbB[min(hi16(I) + 1, max(tlenB - 1, 0))];
-    LO = sel(DM, 0x7fff7fffu, smax(LO, IW));
-    HI = sel(DM, 0u, smin(smin(HI, IW1), QL));
-    IW = add(IW, ONE);
-    IW1 = add(IW1, ONE);
-    const uint32_t WD = usat(HI, LO);
-    const uint32_t LEFT0 = neg15(sub(LO, ONE)) & smax(GL, 0u);
-    GL = ssat(GL, ED1);
-    const uint32_t SEL = (uint32_t)ta | ((uint32_t)tbb << 16) | 0x0c040c00u;
-    uint32_t MB[CPL], AA[CPL], CAP[CPL], R[CPL], GEL[CPL];
-    uint32_t T = 0;
-    R[0] = neg15(sub(add(J0, 0xffffffffu), HI));
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const uint32_t JC = add(J0, pk(c, c));
-      const uint32_t ltlo = neg15(sub(JC, LO));
-      const uint32_t lthi = neg15(sub(JC, HI));
-      if (c + 1 < CPL) R[c + 1] = lthi;
-      GEL[c] = ~ltlo;
-      CAP[c] = lthi & ~ltlo;
-      const uint32_t sb = __builtin_amdgcn_perm(pfb[c], pfa[c], SEL);
-      const uint32_t mb = smin(add(hh[c], sb), mad(hh[c], KSH, 0x00800080u));
-      MB[c] = mb;
-      AA[c] = umin(sub(mb, MB_OE), CAP[c]);
-      T = smax(usat(T, EI1), AA[c]);
-    }
-    const uint32_t sx = grp_scan_umax<G>(add(T, RE2));
-    uint32_t EX;
-    if constexpr (G == 16) {
-      EX = mov0<DPP_ROW_SHR(1)>(sx);
-    } else {
-      EX = mov0<DPP_WAVE_SHR1>(sx);
-      EX = r == 0 ? 0u : EX;
-    }
-    uint32_t f = usat(EX, RE);
-    uint32_t LK = 0, H1Q = 0, hm[CPL];
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      if (c > 0) f = smax(usat(f, EI1), AA[c - 1]);
-      const uint32_t h = smax(smax(sub(MB[c], 0x00800080u), ee[c]), f);
-      hm[c] = umin(h, CAP[c]);
-      const uint32_t en = usat(smax(ee[c], sub(MB[c], MB_OD)), ED1);
-      if constexpr (K8)
-        LK = umax(LK, mad(hm[c], KMUL, add(J0, pk(c, c))));
-      else
-        LK = umax(LK, mad(hm[c], KMUL, pk(c, c)));
-      ee[c] = sel(R[c], umin(en, CAP[c]), ee[c]);
-      if (c > 0) hh[c] = sel(R[c], hm[c - 1], hh[c]);
-      H1Q |= hm[c] & qm[c];
-    }
-    uint32_t hs0;
-    if constexpr (G == 16) {
-      hs0 = (uint32_t)__builtin_amdgcn_update_dpp((int)LEFT0, (int)hm[CPL - 1], DPP_ROW_SHR(1), 0xF, 0xF, false);
-    } else {
-      hs0 = mov0<DPP_WAVE_SHR1>(hm[CPL - 1]);
-      hs0 = r == 0 ? LEFT0 : hs0;
-    }
-    hh[0] = sel(R[0], hs0, hh[0]);
-    uint32_t CL = 0x7fff7fffu, CH = 0xffffffffu;
-#pragma unroll
-    for (int c = CPL - 1; c >= 0; --c) {
-      const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));
-      CL = sel(nz & GEL[c], add(J0, pk(c, c)), CL);
-    }
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));
-      CH = sel(nz & R[c], add(J0, pk(c, c)), CH);
-    }
-    uint32_t MROW, MJ;
-    if constexpr (K8) {
-      uint32_t K = LK;
-      grp_red3<G>(K, CL, CH);
-      MROW = W(U(K) >> (u16x2){8, 8});
-      MJ = K & 0x00ff00ffu;
-    } else {
-      const uint32_t lka = LK & 0xffffu, lkb = LK >> 16;
-      int ka = (int)(((lka >> KS) << 10) | (uint32_t)(j0 + (int)(lka & ((1u << KS) - 1))));
-      int kb = (int)(((lkb >> KS) << 10) | (uint32_t)(j0 + (int)(lkb & ((1u << KS) - 1))));
-      if constexpr (G == 16) {
-#define RED4_STEP(CTRL)                                                                   \
-  {                                                                                       \
-    const int a_ = __builtin_amdgcn_mov_dpp(ka, CTRL, 0xF, 0xF, false);                   \
-    const int b_ = __builtin_amdgcn_mov_dpp(kb, CTRL, 0xF, 0xF, false);                   \
-    const uint32_t l_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)CL, CTRL, 0xF, 0xF, false); \
-    const uint32_t h_ = (uint32_t)__builtin_amdgcn_mov_dpp((int)CH, CTRL, 0xF, 0xF, false); \
-    ka = max(ka, a_);                                                                     \
-    kb = max(kb, b_);                                                                     \
-    CL = umin(CL, l_);                                                                    \
-    CH = smax(CH, h_);                                                                    \
-  }
-        RED4_STEP(DPP_ROW_ROR(8))
-        RED4_STEP(DPP_ROW_ROR(4))
-        RED4_STEP(DPP_ROW_ROR(2))
-        RED4_STEP(DPP_ROW_ROR(1))
-#undef RED4_STEP
-      } else {
-        ka = half_max(row_max32(ka));
-        kb = half_max(row_max32(kb));
-        CL = half_umin(CL);
-        CH = half_smax(CH);
-      }
-      MROW = pk(ka >> 10, kb >> 10);
-      MJ = pk(ka & 1023, kb & 1023);
-    }
-    {  // ksw.c:450-453 (meaningful on the owner of column qlen-1); the row index per call
-      const uint32_t AT = neg15(sub(umin(sub(smax(LO, HI), QL), ONE), ONE));
-      EI = sel(AT & ~neg15(sub(H1Q, ESC)), I, EI);
-      ESC = sel(AT, smax(ESC, H1Q), ESC);
-    }
-    cellsa += (int)(WD & 0xffffu);
-    cellsb += (int)(WD >> 16);
-    const uint32_t DMp = DM;
-    {  // ksw.c:454-465 on both calls at once
-      const uint32_t UP = neg15(sub(BEST, MROW));
-      const uint32_t DD = sub(sub(I, BI), sub(MJ, BJ));
-      const uint32_t DROP = sub(sub(BEST, MROW), smax(mul(DD, ED1), mul(sub(0u, DD), EI1)));
-      const uint32_t BRK = neg15(sub(MROW, ONE)) | (~UP & ZDM & neg15(ssat(ZD, DROP)));
-      ROWS = sel(~DM & BRK, add(I, ONE), ROWS);
-      OFF = sel(UP, smax(OFF, smax(sub(MJ, I), sub(I, MJ))), OFF);
-      BEST = sel(UP, MROW, BEST);
-      BI = sel(UP, I, BI);
-      BJ = sel(UP, MJ, BJ);
-      DM = DM | BRK | neg15(sub(TL2, I));
-      I = add(I, ONE & ~DMp);  // a call's own row index (ended calls stop counting)
-    }
-    const uint32_t NLO = smin(CL, HI);
-    LO = NLO;
-    HI = smin(add(smax(CH, sub(NLO, ONE)), pk(2, 2)), QL);
-    NEA |= DM & ~DMp;
-    asm volatile("" : "+v"(tna), "+v"(tnb));
-    // back to the sub-slots once trig of them have a call that ended, or none is live
-    const uint64_t ena = __builtin_amdgcn_ballot_w64((NEA & 0xffffu) != 0) & kLead;
-    const uint64_t enb = __builtin_amdgcn_ballot_w64((NEA >> 16) != 0) & kLead;
-    if (__popcll(ena) + __popcll(enb) >= trig || !__builtin_amdgcn_ballot_w64(DM != 0xffffffffu)) break;
-    }
-    NE = NEA;
-  }
-}
-
-// spec_ext4_kernel with the row loop refilled (quad_next_run)
-template <int G, int PMAX, bool K8>
-__global__ void __launch_bounds__(kBlock) spec_ext8n_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
-                                                            int tb_bytes, int trig) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr uint64_t kLead = G == 16 ? 0x0001000100010001ull : 0x0000000100000001ull;
-  const uint64_t below = kLead & ((1ull << ((int)threadIdx.x & (64 - G))) - 1);
-  uint8_t* const tal = lds + (size_t)(threadIdx.x / G) * (4 * (size_t)tb_bytes + 2 * kQTaskLds);
-  uint8_t* const tar = tal + tb_bytes;
-  uint8_t* const tbl = tar + tb_bytes;
-  uint8_t* const tbr = tbl + tb_bytes;
-  LdsQ* const qa = (LdsQ*)(tbr + tb_bytes);
-  LdsQ* const qb = (LdsQ*)(tbr + tb_bytes + kQTaskLds);
-  const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
-  ShardQ qq;
-  qq.init(a.qh + 8 * kQHStride * list, n);
-  bool ha = false, hb = false, more = n > 0;
-  long long spec_cells = 0;
-  for (;;) {
-    if (more) {  // every sub-slot without a seed takes the next entry: one claim for the wave
-      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha) & kLead, nb = __builtin_amdgcn_ballot_w64(!hb) & kLead;
-      const int nn = __popcll(na) + __popcll(nb);
-      if (nn > 0) {
-        int m0, cap;
-        if (qq.claim(nn, m0, cap)) {
-          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (ha ? 0 : 1);
-          if (!ha && ia < cap) {
-            QTask t;
-            qtask_start<G>(t, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
-            if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
-            else qpark(qa, t);
-            ha = t.phase < 4;
-          }
-          if (!hb && ib < cap) {
-            QTask t;
-            qtask_start<G>(t, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
-            if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
-            else qpark(qb, t);
-            hb = t.phase < 4;
-          }
-        } else {
-          more = false;
-        }
-      }
-    }
-    if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
-      if (!more) break;
-      continue;
-    }
-    QCall ca = quad_idle(b.seq, tal), cb = quad_idle(b.seq, tbl);
-    if (ha) {
-      QTask t = qload(qa);
-      ca = qtask_call(t, o, b.seq, tal, tar);
-      qpark(qa, t);
-    }
-    if (hb) {
-      QTask t = qload(qb);
-      cb = qtask_call(t, o, b.seq, tbl, tbr);
-      qpark(qb, t);
-    }
-    // the loop's columns: the longer side of every task (each next call fits)
-    int la = 1, lb = 1;
-    if (ha) {
-      const QTask t = qload(qa);
-      la = max(t.qbeg, t.lq - t.qbeg - t.len);
-    }
-    if (hb) {
-      const QTask t = qload(qb);
-      lb = max(t.qbeg, t.lq - t.qbeg - t.len);
-    }
-    int qm = 0;
-#pragma unroll
-    for (int g = 0; g < 64; g += G)
-      qm = max(qm, max(__builtin_amdgcn_readlane(la, g), __builtin_amdgcn_readlane(lb, g)));
-    const int cpl = (qm + G) / G;
-#define EXT_RUN(nn)                                                                                                \
-  if (nn <= PMAX && cpl == nn)                                                                                     \
-    quad_next_run<G, (nn <= PMAX ? nn : 1), K8>(o, ref, b, a, tl, qq, more, ha, hb, tal, tar, tbl, tbr, qa, qb, \
-                                                   kLead, below, ca, cb, spec_cells, trig);
-    EXT_RUN(1) else EXT_RUN(2) else EXT_RUN(3) else EXT_RUN(4) else EXT_RUN(5) else EXT_RUN(6) else EXT_RUN(7)
-    else EXT_RUN(8) else EXT_RUN(9) else EXT_RUN(10) else EXT_RUN(11) else EXT_RUN(12) else EXT_RUN(13)
-    else EXT_RUN(14) else EXT_RUN(15) else EXT_RUN(16)
-#undef EXT_RUN
-  }
-  if ((threadIdx.x & (G - 1)) == 0 && spec_cells)
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
-}
-
-
-
 // Task order for the pair kernel: the two seeds a wave takes should need the
 // same phases for about as long — a half whose seed has no left side, or a
 // much shorter one, idles while the other runs (EXEC).  A counting sort of
@@ -2179,17 +1799,7 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  static const bool nextrun = [] {
-    const char* e = getenv("BWAGPU_EXT_REFILL");
-    return e && e[0] == '1';
-  }();
-  static const int rf_trig = getenv("BWAGPU_RF_TRIG") ? atoi(getenv("BWAGPU_RF_TRIG")) : 1;
-  if (oct && nextrun) {
-    const size_t lds8 = ext4_lds(tb_bytes, 16);
-    const int nb = resident_blocks(spec_ext8n_kernel<16, kSpecBinLen[0] / 16, true>, lds8);
-    hipLaunchKernelGGL((spec_ext8n_kernel<16, kSpecBinLen[0] / 16, true>), dim3(grid(nb)), dim3(kBlock), lds8, st, o,
-                       ref, b, a, l + 0, tb_bytes, rf_trig);
-  } else if (oct) {
+  if (oct) {
     const size_t lds8 = ext4_lds(tb_bytes, 16);
     const int nb = resident_blocks(spec_ext4_kernel<16, kSpecBinLen[0] / 16, true>, lds8);
     hipLaunchKernelGGL((spec_ext4_kernel<16, kSpecBinLen[0] / 16, true>), dim3(grid(nb)), dim3(kBlock), lds8, st, o,
