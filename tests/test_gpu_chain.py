@@ -198,3 +198,39 @@ def test_edge_batches(engines):
     assert np.array_equal(rco, want[0]) and np.array_equal(ch, want[1]) and np.array_equal(sd, want[3])
     n, regs = eng.seqs2regions(seq_off, seq)
     assert n[0] == 0 and n[1] == 0 and n[2] == 0
+
+
+def test_two_stage_workers_on_two_contexts():
+    """bwa-flow runs SeqsToChains on several worker threads; two contexts on
+    one device (Engine.clone, each with its own copy of the index and its
+    expanded suffix array) called from two host threads at once give the
+    reference's chains and regions on every call"""
+    import threading
+    name = G.CHAIN_SETS[0]
+    opt, batch, want_regs, want_n = G.load_chain_set(name)
+    e1 = make_engine(opt)
+    e2 = e1.clone()
+    hdr, words = G.load_seed_bwt()
+    sa_intv, sa, _, _ = G.load_seed_sa()
+    e2.set_bwt(hdr, words, sa, sa_intv)
+    copt = abi.default_chainopt()
+    bad = []
+
+    def work(e, tag):
+        for k in range(4):
+            rco, ch, cso, sd = e.seqs2chains(batch.seq_off, batch.seq, (19, 10, 20), 1.5, copt)
+            if not (np.array_equal(rco, batch.read_chain_off) and np.array_equal(cso, batch.chain_seed_off) and
+                    all(np.array_equal(sd[f], batch.seeds[f]) for f in ("rbeg", "qbeg", "len", "score"))):
+                bad.append((tag, k, "chains"))
+            n, regs = e.seqs2regions(batch.seq_off, batch.seq, (19, 10, 20), 1.5, copt)
+            if not np.array_equal(n, want_n) or G.region_mismatch(regs, want_regs) is not None:
+                bad.append((tag, k, "regions"))
+
+    th = [threading.Thread(target=work, args=(e, i)) for i, e in enumerate((e1, e2))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    e1.close()
+    e2.close()
+    assert not bad, bad
