@@ -11,6 +11,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cstdio>
 #include <mutex>
 #include <new>
@@ -27,6 +30,79 @@
 using namespace bwagpu;
 
 namespace {
+
+// A persistent pool for the host-side passes over a batch (the staging copy
+// and check of bwagpu_chain2aln_submit, seeding's validation and staging):
+// creating threads per call cost 20-50 us each, and far more when several
+// stage workers submit at once.  host_parallel(nt, f) runs f(1..nt-1) on the
+// pool and f(0) on the caller, and returns when all are done; pool tasks never
+// wait on the pool, so concurrent callers cannot deadlock.
+class PassPool {
+ public:
+  static PassPool& get() {
+    static PassPool p(7);
+    return p;
+  }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+  ~PassPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  explicit PassPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+
+template <typename F>
+void host_parallel(int nt, F f) {
+  if (nt <= 1) {
+    f(0);
+    return;
+  }
+  int left = nt - 1;  // decremented under m: the caller cannot unwind before the last task released it
+  std::mutex m;
+  std::condition_variable done;
+  for (int t = 1; t < nt; ++t)
+    PassPool::get().post([&, t] {
+      f(t);
+      std::lock_guard<std::mutex> g(m);
+      if (--left == 0) done.notify_all();
+    });
+  f(0);
+  std::unique_lock<std::mutex> g(m);
+  done.wait(g, [&] { return left == 0; });
+}
+
 
 struct DevBuf {  // grow-only device buffer
   void* p = nullptr;
@@ -598,16 +674,10 @@ int check_batch_seeds(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, int* lq_max_ou
   const int nt = b->n_seeds >= (1 << 16) ? 4 : 1;
   int code[4] = {0, 0, 0, 0}, bad_read[4] = {0, 0, 0, 0};
   int64_t lmaxs[4] = {0, 0, 0, 0};
-  {
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t)
-      th.emplace_back([&, t] {
-        code[t] = check_reads(b, ctx->ref.l_pac, (int)((int64_t)b->n_reads * t / nt),
-                              (int)((int64_t)b->n_reads * (t + 1) / nt), &lmaxs[t], &bad_read[t]);
-      });
-    code[0] = check_reads(b, ctx->ref.l_pac, 0, (int)((int64_t)b->n_reads / nt), &lmaxs[0], &bad_read[0]);
-    for (auto& x : th) x.join();
-  }
+  host_parallel(nt, [&](int t) {
+    code[t] = check_reads(b, ctx->ref.l_pac, (int)((int64_t)b->n_reads * t / nt),
+                          (int)((int64_t)b->n_reads * (t + 1) / nt), &lmaxs[t], &bad_read[t]);
+  });
   if (int rc = check_report(ctx, b, code, bad_read, nt)) return rc;
   *lq_max_out = (int)std::max(std::max(lmaxs[0], lmaxs[1]), std::max(lmaxs[2], lmaxs[3]));
   return BWAGPU_OK;
@@ -662,12 +732,7 @@ int stage_and_check(bwagpu_ctx_t* ctx, const bwagpu_batch_t* b, char* h, const I
       lmaxs[t] = std::max(lmaxs[t], lm);
     }
   };
-  {
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
-  }
+  host_parallel(nt, work);
   if (int rc = check_report(ctx, b, code, bad_read, nt)) return rc;
   int64_t lm = 0;
   for (int t = 0; t < nt; ++t) lm = std::max(lm, lmaxs[t]);
@@ -1937,12 +2002,7 @@ int seed_validate(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_read
     for (; i < e; ++i) bad |= seq[i] > 4;
     base_bad[t] = bad != 0;
   };
-  {
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
-    part(0);
-    for (auto& x : th) x.join();
-  }
+  host_parallel(nt, part);
   int lb = 0, bb = 0;
   for (int t = 0; t < nt; ++t) {
     lb |= len_bad[t];
@@ -1978,10 +2038,7 @@ int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads
       memcpy(pin + ob + b0, seq + b0, b1 - b0);
       if (t == 0) memcpy(pin, seq_off, ob);
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
-    part(0);
-    for (auto& x : th) x.join();
+    host_parallel(nt, part);
     HIPC(hipMemcpyAsync(ctx->sd_off.p, pin, ob, hipMemcpyHostToDevice, st), "H2D");
     if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, pin + ob, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
     HIPC(hipEventRecord(ctx->sdh_done, st), "hipEventRecord");
