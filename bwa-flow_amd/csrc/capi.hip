@@ -1928,14 +1928,15 @@ extern "C" int bwagpu_set_bwt(bwagpu_ctx_t* ctx, const bwagpu_bwt_t* bwt) {
     while ((1 << ctx->bwt.sa_shift) < iv) ++ctx->bwt.sa_shift;
     // every row's entry in HBM (one load per bwt_sa instead of a walk of ~sa_intv
     // dependent occurrence lookups): 32-bit entries below 2^32 rows (chr21: 0.37
-    // GB), 64-bit above, within 8 GB and a quarter of the free memory;
-    // BWAGPU_SA_FULL=0 keeps the sampled walk
+    // GB), 64-bit above (GRCh38: 50 GB of the 288), within 64 GB and a quarter
+    // of the free memory; BWAGPU_SA_FULL=0 keeps the sampled walk, =64 forces
+    // 64-bit entries (tests)
     const char* fe = getenv("BWAGPU_SA_FULL");
-    const bool narrow = bwt->seq_len < 0xffffffffull;
+    const bool narrow = bwt->seq_len < 0xffffffffull && !(fe && strcmp(fe, "64") == 0);
     const uint64_t bytes = (bwt->seq_len + 1) * (narrow ? 4 : 8);
     size_t free_b = 0, total_b = 0;
-    if (!(fe && fe[0] == '0') && iv > 1 && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-        bytes <= ((uint64_t)8 << 30) && bytes <= free_b / 4) {
+    if (!(fe && strcmp(fe, "0") == 0) && iv > 1 && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        bytes <= ((uint64_t)64 << 30) && bytes <= free_b / 4) {
       HIPC(ctx->sa_full.ensure((size_t)bytes), "hipMalloc");
       hipStream_t st = nullptr;
       HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");

@@ -152,7 +152,7 @@ def test_expanded_suffix_array_equals_the_walk(monkeypatch):
     hdr, words = G.load_seed_bwt()
     intv, sa, q, want = G.load_seed_sa()
     engs = {}
-    for mode in ("1", "0"):
+    for mode in ("1", "64", "0"):  # 32-bit entries, 64-bit entries, the walk
         monkeypatch.setenv("BWAGPU_SA_FULL", mode)
         e = Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
         e.set_bwt(hdr, words, sa, intv)
@@ -161,6 +161,7 @@ def test_expanded_suffix_array_equals_the_walk(monkeypatch):
     rows = np.arange(int(hdr[6]) + 1, dtype=np.uint64)
     full, walk = engs["1"].bwt_sa(rows), engs["0"].bwt_sa(rows)
     assert np.array_equal(full, walk)
+    assert np.array_equal(engs["64"].bwt_sa(rows), walk)
     # a permutation of 0..seq_len-1 plus row 0's stored -1 (bwt_cal_sa, bwt.c:181)
     want_set = np.append(np.arange(len(rows) - 1, dtype=np.uint64), np.uint64(2**64 - 1))
     assert np.array_equal(np.sort(full), want_set)
