@@ -1973,53 +1973,88 @@ extern "C" int bwagpu_bwt_sa(bwagpu_ctx_t* ctx, int64_t n, const uint64_t* k, ui
 namespace {
 
 // the checks of bwagpu_collect_intv's arguments; *bases = the batch's bases
+// The pinned staging buffer of seeding's reads (seq_off, then the bases),
+// once the previous call's H2D out of it is done (a caller that returned
+// early on an error never synchronized its stream)
+int seed_pin(bwagpu_ctx_t* ctx, int32_t n_reads, int64_t nb, char** pin) {
+  if (ctx->sdh_done) HIPC(hipEventSynchronize(ctx->sdh_done), "hipEventSynchronize");
+  else HIPC(hipEventCreateWithFlags(&ctx->sdh_done, hipEventDisableTiming), "hipEventCreate");
+  HIPC(ctx->sdh_in.ensure(sizeof(int64_t) * ((size_t)n_reads + 1) + (size_t)nb), "hipHostMalloc");
+  *pin = ctx->sdh_in.as<char>();
+  return BWAGPU_OK;
+}
+
+// Checks a seeding batch: the read lengths and every base (nt4: 0..4), on up
+// to 8 threads for a batch of megabases.  stage: the same pass also copies
+// the reads into the pinned staging buffer (seed_pin; seed_enqueue then skips
+// its copy).  *lq_max (optional) = the longest read.
 int seed_validate(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads, const int64_t* seq_off,
-                  const uint8_t* seq, int64_t* bases) {
+                  const uint8_t* seq, int64_t* bases, bool stage = false, int* lq_max = nullptr) {
   if (!ctx->has_bwt) return fail(ctx, BWAGPU_E_INVAL, "no FM-index: call bwagpu_set_bwt first");
   if (opt->min_seed_len < 1 || opt->split_width < 0) return fail(ctx, BWAGPU_E_INVAL, "bad seeding options");
   *bases = 0;
+  if (lq_max) *lq_max = 0;
   if (n_reads == 0) return BWAGPU_OK;
   const int64_t nb = seq_off[n_reads] - seq_off[0];
   if (seq_off[0] != 0 || nb < 0 || (nb && !seq)) return fail(ctx, BWAGPU_E_INVAL, "seq_off must start at 0");
-  // the read lengths and every base (nt4: 0..4), on up to 8 threads for a
-  // batch of megabases (one thread takes ~1 ms per 10 Mbases)
+  char* pin = nullptr;
+  if (stage) {
+    int rc = seed_pin(ctx, n_reads, nb, &pin);
+    if (rc) return rc;
+  }
+  const size_t ob = sizeof(int64_t) * ((size_t)n_reads + 1);
+  // one thread takes ~1 ms per 10 Mbases
   const int nt = nb >= (1 << 22) ? 8 : 1;
   int len_bad[8] = {}, base_bad[8] = {};
+  int64_t lms[8] = {};
   auto part = [&](int t) {
+    int64_t lm = 0;
     for (int32_t r = (int32_t)((int64_t)n_reads * t / nt); r < (int32_t)((int64_t)n_reads * (t + 1) / nt); ++r) {
       const int64_t l = seq_off[r + 1] - seq_off[r];
       if (l < 0) len_bad[t] |= 1;
       if (l > BWAGPU_MAX_SEED_READ) len_bad[t] |= 2;
+      lm = std::max(lm, l);
     }
+    lms[t] = lm;
+    if (pin && t == 0) memcpy(pin, seq_off, ob);
     // eight bytes at a time: (b & 0x7f) + 0x7b carries into bit 7 iff b > 4
     int64_t i = (nb * t / nt) & ~(int64_t)7;
     const int64_t e = t == nt - 1 ? nb : (nb * (t + 1) / nt) & ~(int64_t)7;
     uint64_t bad = 0;
+    char* const dst = pin ? pin + ob : nullptr;
     for (; i + 8 <= e; i += 8) {
       uint64_t w;
       memcpy(&w, seq + i, 8);
       bad |= (((w & 0x7f7f7f7f7f7f7f7fULL) + 0x7b7b7b7b7b7b7b7bULL) | w) & 0x8080808080808080ULL;
+      if (dst) memcpy(dst + i, &w, 8);
     }
-    for (; i < e; ++i) bad |= seq[i] > 4;
+    for (; i < e; ++i) {
+      bad |= seq[i] > 4;
+      if (dst) dst[i] = (char)seq[i];
+    }
     base_bad[t] = bad != 0;
   };
   host_parallel(nt, part);
   int lb = 0, bb = 0;
+  int64_t lm = 0;
   for (int t = 0; t < nt; ++t) {
     lb |= len_bad[t];
     bb |= base_bad[t];
+    lm = std::max(lm, lms[t]);
   }
   if (lb & 1) return fail(ctx, BWAGPU_E_INVAL, "seq_off not monotone");
   if (lb & 2) return fail(ctx, BWAGPU_E_UNSUPPORTED, "read longer than BWAGPU_MAX_SEED_READ");
   if (bb) return fail(ctx, BWAGPU_E_INVAL, "read base > 4 (bases are nt4)");
   *bases = nb;
+  if (lq_max) *lq_max = (int)lm;
   return BWAGPU_OK;
 }
 
 // H2D of the reads (when upload) and mem_collect_intv into per-read slots of
 // max_per_read intervals (ctx->sd_*), enqueued on st
 int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads, const int64_t* seq_off,
-                 const uint8_t* seq, int64_t bases, int32_t max_per_read, bool upload, hipStream_t st, SeedArgs& a) {
+                 const uint8_t* seq, int64_t bases, int32_t max_per_read, bool upload, hipStream_t st, SeedArgs& a,
+                 bool staged = false) {
   HIPC(ctx->sd_off.ensure(sizeof(int64_t) * ((size_t)n_reads + 1)), "hipMalloc");
   HIPC(ctx->sd_seq.ensure((size_t)bases + 1), "hipMalloc");
   HIPC(ctx->sd_out.ensure(sizeof(bwagpu_intv_t) * (size_t)n_reads * (size_t)max_per_read), "hipMalloc");
@@ -2027,19 +2062,18 @@ int seed_enqueue(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* opt, int32_t n_reads
   HIPC(ctx->sd_scratch.ensure(sizeof(bwagpu_intv_t) * (size_t)seed_scratch_entries(bases, n_reads)), "hipMalloc");
   if (upload) {  // through a pinned staging buffer filled on a few threads (a pageable H2D runs at a fraction)
     const size_t ob = sizeof(int64_t) * ((size_t)n_reads + 1);
-    // the previous call's H2D may still read the buffer (a caller that
-    // returned early on an error never synchronized its stream)
-    if (ctx->sdh_done) HIPC(hipEventSynchronize(ctx->sdh_done), "hipEventSynchronize");
-    else HIPC(hipEventCreateWithFlags(&ctx->sdh_done, hipEventDisableTiming), "hipEventCreate");
-    HIPC(ctx->sdh_in.ensure(ob + (size_t)bases), "hipHostMalloc");
-    char* const pin = ctx->sdh_in.as<char>();
-    const int nt = bases >= (1 << 22) ? 8 : 1;
-    auto part = [&](int t) {
-      const size_t b0 = (size_t)bases * t / nt, b1 = (size_t)bases * (t + 1) / nt;
-      memcpy(pin + ob + b0, seq + b0, b1 - b0);
-      if (t == 0) memcpy(pin, seq_off, ob);
-    };
-    host_parallel(nt, part);
+    char* pin = ctx->sdh_in.as<char>();
+    if (!staged) {  // else seed_validate's pass filled it
+      int rc = seed_pin(ctx, n_reads, bases, &pin);
+      if (rc) return rc;
+      const int nt = bases >= (1 << 22) ? 8 : 1;
+      auto part = [&](int t) {
+        const size_t b0 = (size_t)bases * t / nt, b1 = (size_t)bases * (t + 1) / nt;
+        memcpy(pin + ob + b0, seq + b0, b1 - b0);
+        if (t == 0) memcpy(pin, seq_off, ob);
+      };
+      host_parallel(nt, part);
+    }
     HIPC(hipMemcpyAsync(ctx->sd_off.p, pin, ob, hipMemcpyHostToDevice, st), "H2D");
     if (bases) HIPC(hipMemcpyAsync(ctx->sd_seq.p, pin + ob, (size_t)bases, hipMemcpyHostToDevice, st), "H2D");
     HIPC(hipEventRecord(ctx->sdh_done, st), "hipEventRecord");
@@ -2080,14 +2114,14 @@ extern "C" int bwagpu_collect_intv(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* op
       (out_cap && !out))
     return BWAGPU_E_INVAL;
   int64_t bases = 0;
-  int rc = seed_validate(ctx, opt, n_reads, seq_off, seq, &bases);
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  int rc = seed_validate(ctx, opt, n_reads, seq_off, seq, &bases, true);
   if (rc) return rc;
   if (n_reads == 0) return BWAGPU_OK;
-  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   hipStream_t st = nullptr;
   HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   SeedArgs a;
-  if ((rc = seed_enqueue(ctx, opt, n_reads, seq_off, seq, bases, max_per_read, true, st, a))) return rc;
+  if ((rc = seed_enqueue(ctx, opt, n_reads, seq_off, seq, bases, max_per_read, true, st, a, true))) return rc;
   HIPC(hipMemcpyAsync(out_n, ctx->sd_n.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost, st), "D2H");
   HIPC(hipStreamSynchronize(st), "sync");
   if (const char* dp = getenv("BWAGPU_SEED_DBG")) {
@@ -2233,10 +2267,10 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
       return fail(ctx, BWAGPU_E_UNSUPPORTED, "device LDS per workgroup is smaller than the chaining arena");
   }
   int64_t bases = 0;
-  int rc = seed_validate(ctx, sopt, n_reads, seq_off, seq, &bases);
-  if (rc) return rc;
   int lq_max = 0;
-  for (int32_t r = 0; r < n_reads; ++r) lq_max = std::max<int>(lq_max, (int)(seq_off[r + 1] - seq_off[r]));
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  int rc = seed_validate(ctx, sopt, n_reads, seq_off, seq, &bases, true, &lq_max);  // + the staging copy
+  if (rc) return rc;
   *lq_max_out = lq_max;
   if (n_reads == 0) return BWAGPU_OK;
   // mem_flt_chained_seeds' gate and min_HSP_score per read length
@@ -2258,7 +2292,7 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   int32_t mpr = std::max(64, 2 * lq_max + 64);  // interval slots per read (grown on overflow)
   SeedArgs sa;
-  if ((rc = seed_enqueue(ctx, sopt, n_reads, seq_off, seq, bases, mpr, true, st, sa))) return rc;
+  if ((rc = seed_enqueue(ctx, sopt, n_reads, seq_off, seq, bases, mpr, true, st, sa, true))) return rc;
   const size_t nr = (size_t)n_reads;
   HIPC(ctx->ch_npos.ensure(sizeof(int32_t) * nr), "hipMalloc");
   HIPC(ctx->ch_posoff.ensure(sizeof(int64_t) * (nr + 1)), "hipMalloc");
