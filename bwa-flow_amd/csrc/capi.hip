@@ -2254,7 +2254,7 @@ namespace {
 
 int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_chainopt_t* copt, int32_t n_reads,
                  const int64_t* seq_off, const uint8_t* seq, bool raw, hipStream_t st, int64_t* n_chains,
-                 int64_t* n_seeds, int* lq_max_out) {
+                 int64_t* n_seeds, int* lq_max_out, bool to_host = false) {
   *n_chains = *n_seeds = 0;
   if (copt->max_occ < 1 || copt->max_chain_gap < 0 || copt->max_chain_extend < 0 || !(copt->mask_level >= 0) ||
       !(copt->drop_ratio >= 0))
@@ -2451,6 +2451,16 @@ int run_chaining(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sopt, const bwagpu_c
   ChainPack pk{ctx->ch_ocoff.as<int64_t>(), ctx->ch_osoff.as<int64_t>(), ctx->ch_rco.as<int32_t>(),
                ctx->ch_cso.as<int32_t>(), ctx->ch_rid.as<int32_t>(), ctx->ch_cfrac.as<float>(),
                ctx->ch_out.as<bwagpu_chain_t>(), ctx->ch_seeds.as<bwagpu_seed_t>()};
+  if (to_host) {  // bwagpu_seqs2chains: the chains written over PCIe into its pinned results (no D2H step)
+    HIPC(ctx->chh_rco.ensure(sizeof(int32_t) * (nr + 1)), "hipHostMalloc");
+    HIPC(ctx->chh_cso.ensure(sizeof(int32_t) * ((size_t)nc + 1)), "hipHostMalloc");
+    HIPC(ctx->chh_chains.ensure(sizeof(bwagpu_chain_t) * (size_t)std::max<int64_t>(nc, 1)), "hipHostMalloc");
+    HIPC(ctx->chh_seeds.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max<int64_t>(ns, 1)), "hipHostMalloc");
+    HIPC(hipHostGetDevicePointer((void**)&pk.read_chain_off, ctx->chh_rco.p, 0), "hipHostGetDevicePointer");
+    HIPC(hipHostGetDevicePointer((void**)&pk.chain_seed_off, ctx->chh_cso.p, 0), "hipHostGetDevicePointer");
+    HIPC(hipHostGetDevicePointer((void**)&pk.chains, ctx->chh_chains.p, 0), "hipHostGetDevicePointer");
+    HIPC(hipHostGetDevicePointer((void**)&pk.seeds, ctx->chh_seeds.p, 0), "hipHostGetDevicePointer");
+  }
   HIPC(launch_chain_pack(a, pk, st), "chain_pack launch");
   *n_chains = nc;
   *n_seeds = ns;
@@ -2481,7 +2491,7 @@ extern "C" int bwagpu_seqs2chains(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sop
   HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
   int64_t nc = 0, ns = 0;
   int lq = 0;
-  int rc = run_chaining(ctx, sopt, copt, n_reads, seq_off, seq, raw != 0, st, &nc, &ns, &lq);
+  int rc = run_chaining(ctx, sopt, copt, n_reads, seq_off, seq, raw != 0, st, &nc, &ns, &lq, true);
   if (rc) return rc;
   const size_t nr = (size_t)n_reads;
   HIPC(ctx->chh_rco.ensure(sizeof(int32_t) * (nr + 1)), "hipHostMalloc");
@@ -2489,18 +2499,7 @@ extern "C" int bwagpu_seqs2chains(bwagpu_ctx_t* ctx, const bwagpu_seedopt_t* sop
   HIPC(ctx->chh_chains.ensure(sizeof(bwagpu_chain_t) * (size_t)std::max<int64_t>(nc, 1)), "hipHostMalloc");
   HIPC(ctx->chh_seeds.ensure(sizeof(bwagpu_seed_t) * (size_t)std::max<int64_t>(ns, 1)), "hipHostMalloc");
   if (n_reads) {
-    HIPC(hipMemcpyAsync(ctx->chh_rco.p, ctx->ch_rco.p, sizeof(int32_t) * (nr + 1), hipMemcpyDeviceToHost, st), "D2H");
-    HIPC(hipMemcpyAsync(ctx->chh_cso.p, ctx->ch_cso.p, sizeof(int32_t) * ((size_t)nc + 1), hipMemcpyDeviceToHost, st),
-         "D2H");
-    if (nc)
-      HIPC(hipMemcpyAsync(ctx->chh_chains.p, ctx->ch_out.p, sizeof(bwagpu_chain_t) * (size_t)nc, hipMemcpyDeviceToHost,
-                          st),
-           "D2H");
-    if (ns)
-      HIPC(hipMemcpyAsync(ctx->chh_seeds.p, ctx->ch_seeds.p, sizeof(bwagpu_seed_t) * (size_t)ns, hipMemcpyDeviceToHost,
-                          st),
-           "D2H");
-    HIPC(hipStreamSynchronize(st), "sync");
+    HIPC(hipStreamSynchronize(st), "sync");  // chain_pack wrote the results into the pinned buffers
   } else {
     ctx->chh_rco.as<int32_t>()[0] = 0;
     ctx->chh_cso.as<int32_t>()[0] = 0;
