@@ -1011,7 +1011,7 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
     const int rep_lim = (int)floor(.1 * d.lq) + 1;  // s->len - p->seedlen0 > .1 * l_query, bwamem.c:685
     bool redo = false;
     Tally rt{0, 0, 0};
-    int nreg = 0;
+    int nreg = 0, n_inline = 0;
     for (int c = d.c0; c < d.c0 + d.nch && !redo; ++c) {
       const int s0 = uni(b.chain_seed_off[c]), ns = uni(b.chain_seed_off[c + 1]) - s0;
       if (ns == 0) continue;
@@ -1103,6 +1103,7 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
             store_ext(a.ext + pos, e);
             mem_fence_group();
             if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
+            ++n_inline;
           } else if constexpr (MODE == SEL_EMULATE) {
             set_flag(k, 2);  // pending: collected per chain below
             continue;        // its region stays unknown in this pass
@@ -1160,7 +1161,8 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
         }
       }
     }
-    if (MODE != SEL_REDO) trace_read(MODE, b.n_reads, rd, t_start, d.ns, nreg, 2);
+    // (the redo pass as pass 2, its inline extensions in the shape word's upper bits)
+    trace_read(MODE, b.n_reads, rd, t_start, d.ns, nreg, 2 | (MODE == SEL_REDO ? n_inline << 4 : 0));
     if constexpr (WRITE) {
       if (!redo) {
         a.out_n[rd] = nreg;
@@ -1372,12 +1374,14 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
         continue;
       }
       if (miss >= 0) {  // the redo pass (reads > 160 bp)
+        // round C extends the miss and every later seed without a result: the
+        // redo replay's next misses are among them (one region changes the
+        // decisions after it), and the packed kernels take them all at once
+        // instead of the redo wave one after another
         const int list = 2 * kSpecBins + spec_bin(d.lq);
-        if (r == miss) {
-          const int p = atomicAdd(&a.ctr[SPC_CNT + list], 1);
-          a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
-          a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
-        }
+        const int p = wave_append(&a.ctr[SPC_CNT + list], r >= miss && present && !computed);
+        if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
+        if (r == miss) a.redo[atomicAdd(&a.ctr[SPC_REDO_N], 1)] = rd;
         break;  // the redo pass writes this read
       }
       const bool mine = (ext >> r) & 1;
@@ -1842,12 +1846,17 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
                      l + 2, tb_bytes);
 }
 
-// prep -> round A -> emulate -> round B -> final -> redo, one stream.  The
-// final pass's misses in reads over 160 bp and in heavy reads without a pair
-// matrix (round-C lists: a handful per batch, none on C2) are computed by the
-// redo pass inline: a launch of its own for them waited ~0.18 ms per batch for
-// CU slots the other caller stream's extension kernel held, even over an
-// empty list.
+// prep -> round A -> emulate -> round B -> final -> [round C] -> redo, one
+// stream.  The final pass sends a read over 160 bp that misses an extension,
+// and a heavy read without a pair matrix, to the redo pass, and their
+// missing seeds to the round-C lists (a light read: the miss and every later
+// seed without a result).  Batches with reads over 160 bp run round C with
+// the packed kernels first (C5: one read's chain of 12 misses took the redo
+// wave 2.3 ms one extension at a time), so the redo pass mostly replays; on
+// shorter batches (C2: no such miss) round C stays unlaunched — a launch
+// waited ~0.18 ms per batch for CU slots the other caller stream's extension
+// kernel held, even over an empty list — and the redo pass extends the rare
+// misses inline.
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   if (b.n_reads == 0) return hipSuccess;
@@ -1862,6 +1871,7 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
     launch_ext_round(o, ref, b, a, 1, tb_bytes, lq_max, st, ss);
   }
   launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
+  if (b.n_chains && lq_max > kSpecBinLen[0]) launch_ext_round(o, ref, b, a, 2, tb_bytes, lq_max, st, ss);
   if (b.n_chains) launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
   return hipGetLastError();
 }

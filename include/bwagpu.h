@@ -500,7 +500,10 @@ int bwagpu_debug_sup_shift(bwagpu_ctx_t *ctx, int32_t shift);
 
 /* diagnostics: while dev_ptr != NULL every chain2aln launch on this device
    writes 8 x uint32 per read index r at dev_ptr[8r..8r+7]: start and end
-   s_memrealtime (100 MHz, lo/hi), DP rows, DP cells, HW_ID, XCC_ID.
+   s_memrealtime (100 MHz, lo/hi), DP rows, DP cells, HW_ID, XCC_ID (the
+   per-read kernels); the speculative path writes its selection passes
+   (emulate, final, redo) at dev_ptr[8 (pass n_reads + r) ..]: start / end,
+   seeds, regions, XCC_ID, shape — so the buffer needs 24 x n_reads words.
    Not part of the reference interface (the reference logs stage wall times
    with getUs(), src/util.h:34-40). */
 int bwagpu_debug_set_trace(bwagpu_ctx_t *ctx, void *dev_ptr);

@@ -33,12 +33,12 @@ st = torch.cuda.Stream()
 for _ in range(2):
     eng.chain2aln_device(c, out.data_ptr(), nn.data_ptr(), None, st.cuda_stream)
 torch.cuda.synchronize()
-tr = torch.zeros(b.n_reads * 16, dtype=torch.int32, device=dev)
+tr = torch.zeros(b.n_reads * 24, dtype=torch.int32, device=dev)  # passes emulate / final / redo
 eng.lib.bwagpu_debug_set_trace(eng.ctx, tr.data_ptr())
 eng.chain2aln_device(c, out.data_ptr(), nn.data_ptr(), None, st.cuda_stream)
 torch.cuda.synchronize()
 eng.lib.bwagpu_debug_set_trace(eng.ctx, None)
-T = tr.cpu().numpy().view(np.uint32).reshape(2, b.n_reads, 8).astype(np.int64)
+T = tr.cpu().numpy().view(np.uint32).reshape(3, b.n_reads, 8).astype(np.int64)
 res = {}
 for ps, name in ((0, "emulate"), (1, "final")):
     t0 = T[ps, :, 0] | (T[ps, :, 1] << 32)
