@@ -1501,7 +1501,8 @@ __device__ __forceinline__ void heavy_fill_missing(const DevOpt& o, const DevRef
   ChainWin cw = a.win[ck];
   cw.lo = uni64(cw.lo);
   cw.hi = uni64(cw.hi);
-  const SeedExt e = extend_seed<3>(o, ref, sk, d.lq, b.seq + d.qoff, cw, tbl, tbr);  // reads <= 192 bp
+  const SeedExt e = d.lq <= 192 ? extend_seed<3>(o, ref, sk, d.lq, b.seq + d.qoff, cw, tbl, tbr)
+                                 : extend_seed<4>(o, ref, sk, d.lq, b.seq + d.qoff, cw, tbl, tbr);  // <= 256 bp
   store_ext(a.ext + d.s0 + k, e);
   if (r == 0) atomicAdd(&a.ctr[SPC_MISS], 1);
   // region k as the containment tests see it (bwamem.c:682-696)
@@ -1630,7 +1631,7 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
             pend |= bit;  // a round-B task; its region stays unknown
             continue;
           }
-          if (d.lq > kSpecBinLen[0]) {  // longer reads: the redo pass
+          if (d.lq > kSpecBinLen[1]) {  // longer reads: the redo pass
             miss = kb + i;
             break;
           }
