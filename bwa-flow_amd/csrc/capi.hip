@@ -418,6 +418,7 @@ bool make_opt(const bwagpu_opt_t* o, DevOpt* d, std::string* why) {
   int mx = 0;  // ksw.c:397-398 — max over the m*m matrix, starting from 0
   for (int i = 0; i < 25; ++i) mx = std::max<int>(mx, o->mat[i]);
   d->max_mat = mx;
+  d->row_bound = 1;
   memcpy(d->mat, o->mat, 25);
   for (int q = 0; q < 5; ++q) {
     uint32_t w = 0;
@@ -1825,6 +1826,13 @@ int bwagpu_ctx_ext_form(bwagpu_ctx_t* ctx, int form) {
   if (!ctx) return BWAGPU_E_INVAL;
   const int prev = ctx->ext_form;
   if (form >= 0) ctx->ext_form = form > 2 ? 1 : form;
+  return prev;
+}
+
+int bwagpu_ctx_row_bound(bwagpu_ctx_t* ctx, int on) {
+  if (!ctx) return BWAGPU_E_INVAL;
+  const int prev = ctx->opt.row_bound;
+  if (on >= 0) ctx->opt.row_bound = on ? 1 : 0;
   return prev;
 }
 

@@ -12,6 +12,7 @@ namespace bwagpu {
 struct DevOpt {
   int a, o_del, e_del, o_ins, e_ins, oe_del, oe_ins;
   int pen_clip5, pen_clip3, w, zdrop, max_mat;
+  int row_bound;  // extend_quad ends a call once no later row can change its outputs
   int8_t mat[28];
   // query profile words: qprof[q] byte t = mat[t*5 + q] (t = target base 0..3),
   // qprof4[q] = mat[20 + q] (target N; only bare task lists can hold one —

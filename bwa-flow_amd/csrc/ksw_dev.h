@@ -173,6 +173,11 @@ __device__ __forceinline__ void scan_reduce(int& x, int& r) {
       : "+v"(x), "+v"(r));
 }
 
+// the row bound's period (extend_wave, extend_quad): every fourth row
+#ifndef RB_MASK
+#define RB_MASK 3
+#endif
+
 template <int CD, bool T5>
 __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const uint8_t* __restrict__ qp, int qa,
                                               int qd, int tlen, const uint8_t* tb, int w, int end_bonus, int zdrop,
@@ -334,6 +339,20 @@ __device__ __forceinline__ ExtOut extend_wave(const DevOpt& o, int qlen, const u
     vi += 1;
     lo = nlo;
     hi = nhi;
+    // the row bound of extend_quad, every fourth row: once no later cell can
+    // reach gscore (<= max), row i's own bookkeeping is the last
+    if (o.row_bound && (i & RB_MASK) == RB_MASK) {
+      int bb = (lo == 0 && gl > 0) ? gl + qlen * o.max_mat : 0;
+#pragma unroll
+      for (int c = 0; c < CD; ++c) bb = max(bb, hh[c] > 0 ? hh[c] + __mul24(qlen - jc[c], o.max_mat) : 0);
+      bb = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(bb))))));
+      if (__builtin_amdgcn_readlane(bb, 63) < __builtin_amdgcn_readfirstlane(esc)) {
+        const int rkr = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rkp))))));
+        (void)row_end(__builtin_amdgcn_readlane(rkr, 63), vi - 1);
+        rows = i + 1;
+        break;
+      }
+    }
   }
   if (rows == tlen && tlen > 0) {  // the last row's bookkeeping (its exit test is moot)
     int rkr = max_bc31(max_bc15(max_ror1(max_ror2(max_ror4(max_ror8(rkp))))));
@@ -732,6 +751,27 @@ __device__ __forceinline__ void grp_red3(uint32_t& K, uint32_t& L, uint32_t& H) 
   L = umin((uint32_t)pl[0], (uint32_t)pl[1]);
   H = smax((uint32_t)ph[0], (uint32_t)ph[1]);
 }
+// the group's umax of U and smax of S at once (two independent chains)
+template <int G>
+__device__ __forceinline__ void grp_red2(uint32_t& U, uint32_t& S) {
+#define RED2_STEP(CTRL)                                                                  \
+  {                                                                                      \
+    const uint32_t u = (uint32_t)__builtin_amdgcn_mov_dpp((int)U, CTRL, 0xF, 0xF, false); \
+    const uint32_t s = (uint32_t)__builtin_amdgcn_mov_dpp((int)S, CTRL, 0xF, 0xF, false); \
+    U = umax(U, u);                                                                      \
+    S = smax(S, s);                                                                      \
+  }
+  RED2_STEP(DPP_ROW_ROR(8))
+  RED2_STEP(DPP_ROW_ROR(4))
+  RED2_STEP(DPP_ROW_ROR(2))
+  RED2_STEP(DPP_ROW_ROR(1))
+#undef RED2_STEP
+  if constexpr (G == 16) return;
+  const auto pu = __builtin_amdgcn_permlane16_swap(U, U, false, false);
+  const auto ps = __builtin_amdgcn_permlane16_swap(S, S, false, false);
+  U = umax((uint32_t)pu[0], (uint32_t)pu[1]);
+  S = smax((uint32_t)ps[0], (uint32_t)ps[1]);
+}
 __device__ __forceinline__ uint32_t half_smax(uint32_t x) {
   x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(8), 0xF, 0xF, false));
   x = smax(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, DPP_ROW_ROR(4), 0xF, 0xF, false));
@@ -822,6 +862,11 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   const uint32_t ZD = pk(min(A.zdrop, 32767), min(Bc.zdrop, 32767));
   const uint32_t ZDM = pk(A.zdrop > 0 ? 0xffff : 0, Bc.zdrop > 0 ? 0xffff : 0);
   const uint32_t TL2 = pk(A.tlen - 2, Bc.tlen - 2);  // i + 1 >= tlen <=> tlen - 2 - i < 0
+  // row bound (below): (qlen - j) * max(mat) per column, and qlen * max(mat)
+  uint32_t KQ[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) KQ[c] = pk((A.qlen - j0 - c) * o.max_mat, (Bc.qlen - j0 - c) * o.max_mat);
+  const uint32_t QLA = pk(A.qlen * o.max_mat, Bc.qlen * o.max_mat);
   int cellsa = 0, cellsb = 0;
   int tna = A.tb[0], tnb = Bc.tb[0];
   // rows run while a call of the wave is live; the exit test is at the bottom
@@ -968,6 +1013,23 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     const uint32_t NLO = smin(CL, HI);
     LO = NLO;
     HI = smin(add(smax(CH, sub(NLO, ONE)), pk(2, 2)), QL);
+    // Row bound, every fourth row: a cell of a later row is reached from a
+    // stored diagonal value v = H(i, j-1) > 0 of column j (or from the first
+    // column's h0 - o_del - e_del (i+2) while lo == 0) by at most qlen - j
+    // matches, so no later cell exceeds B = max(v + (qlen - j) max(mat)).  (E
+    // of column j is <= H(i, j) = the diagonal value of column j+1, and 0 at
+    // and right of hi.)  Once B < gscore (<= max), no later row can move max,
+    // its cell, max_off (ksw.c:454: m > max) or gscore / max_ie (ksw.c:450-453:
+    // a tie moves max_ie), so the call ends with every output unchanged.
+    if (o.row_bound && (i & RB_MASK) == RB_MASK) {
+      uint32_t BB = neg15(sub(LO, ONE)) & neg15(sub(0u, GL)) & add(GL, QLA), SC = ESC;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) BB = umax(BB, neg15(sub(0u, hh[c])) & add(hh[c], KQ[c]));
+      grp_red2<G>(BB, SC);
+      const uint32_t STOP = neg15(sub(BB, SC)) & ~DM;  // B < gscore
+      ROWS = sel(STOP, I, ROWS);
+      DM |= STOP;
+    }
     ++i;
     // the next row's target bases stay loaded in this row (else LLVM moves the
     // loads to the next row's top, in front of their only use)

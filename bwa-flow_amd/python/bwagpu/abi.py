@@ -154,6 +154,7 @@ PROTOS = {
     "bwagpu_set_device_read_len": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_debug_ext_form": (C.c_int, [C.c_int]),
     "bwagpu_ctx_ext_form": (C.c_int, [_VP, C.c_int]),
+    "bwagpu_ctx_row_bound": (C.c_int, [_VP, C.c_int]),
     "bwagpu_debug_ext_kernel": (C.c_int, [_VP, C.c_int32]),
     "bwagpu_streams_concurrent": (C.c_int, [_VP, _VP]),
     "bwagpu_bwt_sa": (C.c_int, [_VP, C.c_int64, _VP, _VP]),

@@ -306,6 +306,11 @@ class Engine:
         """this context's extension form (bwagpu_ctx_ext_form); -> the previous one"""
         return self.lib.bwagpu_ctx_ext_form(self.ctx, int(form))
 
+    def row_bound(self, on: int = -1) -> int:
+        """this context's row bound in the packed extension kernels
+        (bwagpu_ctx_row_bound, default on); -> the previous setting"""
+        return self.lib.bwagpu_ctx_row_bound(self.ctx, int(on))
+
     def set_device_read_len(self, max_len: int):
         """bound on the read lengths of later device batches (bwagpu_set_device_read_len)"""
         self._check(self.lib.bwagpu_set_device_read_len(self.ctx, int(max_len)), "set_device_read_len")

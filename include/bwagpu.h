@@ -543,6 +543,14 @@ int bwagpu_prof_read(bwagpu_ctx_t *ctx, double *total_ms, int32_t *launches);
    Both return the previous form; form < 0 only queries. */
 int bwagpu_debug_ext_form(int form);
 int bwagpu_ctx_ext_form(bwagpu_ctx_t *ctx, int form);
+/* the packed extension kernels' row bound (default on): a ksw_extend2 call
+   ends once no later target row can change its score, qle, tle, gtle, gscore
+   or max_off (every later cell is bounded by a stored value plus max(mat) per
+   query column still ahead of it).  Results are identical either way; with
+   it off the cell and row counters (bwagpu_last_stats) count every row
+   ksw_extend2 (ksw.c:380-479) evaluates.  Returns the previous setting;
+   on < 0 only queries. */
+int bwagpu_ctx_row_bound(bwagpu_ctx_t *ctx, int on);
 /* the first length bin's extension kernel this context launches for reads of
    up to lq_max bases: 8 = eight seeds per wave (spec_ext4_kernel<16,10,true>),
    4 = four per wave with the 8-bit row-max key (<32,5,true>), 5 = four per

@@ -49,6 +49,16 @@ def make_engine(refd, opt):
     return Engine(0, opt, refd["l_pac"], refd["ann_offset"], refd["ann_len"], pac=refd["pac"])
 
 
+def assert_counts(st, ost, bound):
+    """(cells, rows, calls) against the oracle's: equal with the row bound off;
+    with it on the same calls, none of them longer"""
+    got, want = (st["cells"], st["rows"], st["ext_calls"]), tuple(int(x) for x in ost[:3])
+    if bound:
+        assert got[2] == want[2] and got[0] <= want[0] and got[1] <= want[1], (got, want)
+    else:
+        assert got == want
+
+
 @pytest.mark.parametrize("name", G.CHAIN_SETS)
 def test_chain_sets_bit_exact(refd, name, c2a_path):
     opt, batch, want, want_n = G.load_chain_set(name)
@@ -65,25 +75,32 @@ def test_chain_sets_bit_exact(refd, name, c2a_path):
 def test_ksw_extend2_tasks_bit_exact(refd, name, ext_path):
     opt, tasks, want, qp, tp = G.load_tasks(name)
     eng = make_engine(refd, opt)
-    got = eng.extend_batch(tasks, qp, tp)
-    g, w = got.view(np.int32).reshape(-1, 6), want.view(np.int32).reshape(-1, 6)
-    bad = np.nonzero((g != w).any(axis=1))[0]
-    assert len(bad) == 0, f"{len(bad)} tasks differ; first {tasks[bad[0]]}: got {got[bad[0]]} want {want[bad[0]]}"
-    # the evaluated-cell count agrees with the oracle's count of ksw.c:424 iterations
     _, cells = oracle.extend("oracle", opt, tasks, qp, tp)
-    st = eng.last_stats()
-    assert st["cells"] == cells[0] and st["rows"] == cells[1]
+    for bound in (1, 0):  # the packed kernels' row bound on (default) and off
+        eng.row_bound(bound)
+        got = eng.extend_batch(tasks, qp, tp)
+        g, w = got.view(np.int32).reshape(-1, 6), want.view(np.int32).reshape(-1, 6)
+        bad = np.nonzero((g != w).any(axis=1))[0]
+        assert len(bad) == 0, f"{len(bad)} tasks differ; first {tasks[bad[0]]}: got {got[bad[0]]} want {want[bad[0]]}"
+        st = eng.last_stats()
+        if bound:  # calls end early, never late
+            assert st["cells"] <= cells[0] and st["rows"] <= cells[1]
+        else:  # the evaluated-cell count agrees with the oracle's count of ksw.c:424 iterations
+            assert st["cells"] == cells[0] and st["rows"] == cells[1]
     eng.close()
 
 
 def test_cell_and_call_counts_match_oracle(refd, c2a_path):
-    opt, batch, _, _ = G.load_chain_set("c1_default")
+    opt, batch, want, want_n = G.load_chain_set("c1_default")
     eng = make_engine(refd, opt)
-    eng.chain2aln(batch)
-    st = eng.last_stats()
     ref = oracle.Ref(refd["l_pac"], refd["ann_offset"], refd["ann_len"], refd["pac"])
     _, _, ost = oracle.chain2aln("oracle", opt, ref, batch)
-    assert (st["cells"], st["rows"], st["ext_calls"]) == tuple(int(x) for x in ost)
+    for bound in (0, 1):
+        eng.row_bound(bound)
+        regs, n = eng.chain2aln(batch)
+        assert np.array_equal(n, want_n) and G.region_mismatch(compact(batch, regs, n), want) is None
+        st = eng.last_stats()
+        assert_counts(st, ost, bound)
 
 
 def test_slots_double_buffered(refd):
@@ -294,13 +311,15 @@ def test_synthetic_batches_vs_oracle(len_mode, min_seed, pairs, c2a_path):
     b = synth_batch(ref, 5 + len_mode, pairs, len_mode, min_seed)
     opt = abi.default_opt()
     eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
-    regs, n = eng.chain2aln(b)
-    st = eng.last_stats()
     R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
     oregs, on, ostats = oracle.chain2aln("oracle", opt, R, b, n_threads=4)
-    assert np.array_equal(n, on), f"{int((n != on).sum())} reads with a different region count"
-    assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
-    assert (st["cells"], st["rows"], st["ext_calls"]) == tuple(int(x) for x in ostats[:3])
+    for bound in (1, 0):
+        eng.row_bound(bound)
+        regs, n = eng.chain2aln(b)
+        st = eng.last_stats()
+        assert np.array_equal(n, on), f"{int((n != on).sum())} reads with a different region count"
+        assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
+        assert_counts(st, ostats, bound)
     eng.close()
 
 
@@ -373,11 +392,13 @@ def test_chain_window_past_16_bits(refd, dist, c2a_path):
     sub = batch.subset(range(400))
     b = far_seed_batch(sub, refd["ann_offset"], refd["ann_len"], dist, 120)
     eng = make_engine(refd, opt)
-    regs, n = eng.chain2aln(b)
-    st = eng.last_stats()
     ref = oracle.Ref(refd["l_pac"], refd["ann_offset"], refd["ann_len"], refd["pac"])
     oregs, on, ost = oracle.chain2aln("oracle", opt, ref, b)
-    assert np.array_equal(n, on), f"{int((n != on).sum())} reads with a different region count"
-    assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
-    assert (st["cells"], st["rows"], st["ext_calls"]) == tuple(int(x) for x in ost[:3])
+    for bound in (1, 0):
+        eng.row_bound(bound)
+        regs, n = eng.chain2aln(b)
+        st = eng.last_stats()
+        assert np.array_equal(n, on), f"{int((n != on).sum())} reads with a different region count"
+        assert G.region_mismatch(compact(b, regs, n), compact(b, oregs, on)) is None
+        assert_counts(st, ost, bound)
     eng.close()
