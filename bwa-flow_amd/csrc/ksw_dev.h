@@ -604,6 +604,19 @@ __device__ __forceinline__ ExtOut extend_pair(const DevOpt& o, int qlen, const u
     vi += 1;
     lo = nlo;
     hi = nhi;
+    // the row bound of extend_quad, every fourth row, per half (gscore lives on
+    // the owner of column qlen-1 and is <= 0 on the half's other lanes)
+    if (o.row_bound && (i & RB_MASK) == RB_MASK) {
+      int bb = (lo == 0 && gl > 0) ? gl + qlen * o.max_mat : 0;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) bb = max(bb, hh[c] > 0 ? hh[c] + __mul24(qlen - j0 - c, o.max_mat) : 0);
+      bb = half_max(row_max32(bb));
+      if (bb < half_max(row_max32(esc))) {
+        (void)row_end(half_max(row_max32(rkp)), vi - 1);
+        rows = i + 1;
+        break;
+      }
+    }
   }
   if (rows == tlen && tlen > 0) {  // the last row's bookkeeping (its exit test is moot)
     const int rkr = half_max(row_max32(rkp));
