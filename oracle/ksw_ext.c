@@ -32,10 +32,10 @@ static int gap_cap(int qlen, int best, int end_bonus, int o, int e)
   return l > 1 ? l : 1;
 }
 
-int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
-                       const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
-                       int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle,
-                       int *gscore, int *max_off, int64_t *cells)
+static int ksw_extend2_core(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
+                            const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                            int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle,
+                            int *gscore, int *max_off, int64_t *cells, int row_bound)
 {
   const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
   int32_t *hdiag, *ecol;
@@ -109,6 +109,18 @@ int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
       int drop = di > dj ? best - rmax - (di - dj) * e_del : best - rmax - (dj - di) * e_ins;
       if (drop > zdrop) break;
     }
+    /* NOT part of ksw_extend2: the row bound the GPU kernels apply
+       (ksw_dev.h extend_quad), here only to test its
+       claim on the golden calls — no later cell exceeds a stored positive
+       diagonal value plus max(mat) per query column ahead of it, so once that
+       bound is below gscore (<= best) no output can change */
+    if (row_bound) {
+      int bnd = 0;
+      for (j = lo; j <= qlen; ++j)
+        if (hdiag[j] > 0) bnd = imax(bnd, hdiag[j] + (qlen - j) * best_mat);
+      if (lo == 0 && h0 - (o_del + e_del * (i + 2)) > 0) bnd = imax(bnd, h0 - (o_del + e_del * (i + 2)) + qlen * best_mat);
+      if (bnd < end_sc) break;
+    }
     /* trim the band to the columns whose state is not all-zero */
     for (j = lo; j < hi && hdiag[j] == 0 && ecol[j] == 0; ++j)
       ;
@@ -127,6 +139,30 @@ int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *
   if (max_off) *max_off = off;
   if (cells) { cells[0] += n_cells; cells[1] += n_rows; }
   return best;
+}
+
+int oracle_ksw_extend2(int qlen, const uint8_t *query, int tlen, const uint8_t *target, int m,
+                       const int8_t *mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                       int end_bonus, int zdrop, int h0, int *qle, int *tle, int *gtle,
+                       int *gscore, int *max_off, int64_t *cells)
+{
+  return ksw_extend2_core(qlen, query, tlen, target, m, mat, o_del, e_del, o_ins, e_ins, w, end_bonus, zdrop,
+                          h0, qle, tle, gtle, gscore, max_off, cells, 0);
+}
+
+/* the same calls with the row bound (tests only: the bound's claim) */
+int oracle_extend_batch_bounded(const bwagpu_opt_t *opt, int32_t n_tasks, const bwagpu_ext_task_t *tasks,
+                                const uint8_t *qpool, const uint8_t *tpool, bwagpu_ext_result_t *results,
+                                int64_t *cells)
+{
+  for (int32_t k = 0; k < n_tasks; ++k) {
+    const bwagpu_ext_task_t *t = &tasks[k];
+    bwagpu_ext_result_t *r = &results[k];
+    r->score = ksw_extend2_core(t->qlen, qpool + t->qoff, t->tlen, tpool + t->toff, 5, opt->mat, opt->o_del,
+                                opt->e_del, opt->o_ins, opt->e_ins, t->w, t->end_bonus, t->zdrop, t->h0, &r->qle,
+                                &r->tle, &r->gtle, &r->gscore, &r->max_off, cells, 1);
+  }
+  return 0;
 }
 
 int oracle_extend_batch(const bwagpu_opt_t *opt, int32_t n_tasks, const bwagpu_ext_task_t *tasks,

@@ -43,6 +43,8 @@ def oracle_lib():
     lib.oracle_chain2aln_batch.restype = C.c_int
     lib.oracle_extend_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
     lib.oracle_extend_batch.restype = C.c_int
+    lib.oracle_extend_batch_bounded.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
+    lib.oracle_extend_batch_bounded.restype = C.c_int
     lib.oracle_align2_batch.argtypes = [C.POINTER(abi.Opt), C.c_int32, _VP, _VP, _VP, _VP, _VP]
     lib.oracle_align2_batch.restype = C.c_int
     lib.oracle_reg2aln_batch.argtypes = [C.POINTER(abi.Opt), C.POINTER(abi.Bns), _VP, C.c_int32, _VP, _VP,
@@ -125,10 +127,10 @@ def extend(which: str, opt: dict, tasks, qpool, tpool):
     qpool = np.ascontiguousarray(qpool, np.uint8)
     tpool = np.ascontiguousarray(tpool, np.uint8)
     res = np.zeros(max(len(tasks), 1), abi.EXT_RES_DTYPE)
-    if which == "oracle":
+    if which in ("oracle", "oracle_bounded"):  # oracle_bounded: with the GPU kernels' row bound (tests)
         cells = np.zeros(2, np.int64)
-        oracle_lib().oracle_extend_batch(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool),
-                                         _ptr(res), _ptr(cells))
+        fn = oracle_lib().oracle_extend_batch if which == "oracle" else oracle_lib().oracle_extend_batch_bounded
+        fn(C.byref(o), len(tasks), _ptr(tasks), _ptr(qpool), _ptr(tpool), _ptr(res), _ptr(cells))
         return res[:len(tasks)], cells
     lib = ref_lib()
     if lib is None:

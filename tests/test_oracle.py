@@ -38,6 +38,19 @@ def test_oracle_ksw_extend2_matches_reference(name):
     assert len(bad) == 0, f"{len(set(bad))} tasks differ, first {tasks[bad[0]]}: {got[bad[0]]} vs {want[bad[0]]}"
 
 
+@pytest.mark.parametrize("name", G.CHAIN_SETS + G.KSW_SETS)
+def test_row_bound_changes_no_output(name):
+    """the GPU kernels' row bound restated on the CPU:
+    ending a call once no later cell can reach gscore leaves all six outputs
+    of every recorded ksw_extend2 call as the reference's, with fewer rows"""
+    opt, tasks, want, qp, tp = G.load_tasks(name)
+    full, cells = oracle.extend("oracle", opt, tasks, qp, tp)
+    got, bcells = oracle.extend("oracle_bounded", opt, tasks, qp, tp)
+    bad = np.nonzero((got.view(np.int32).reshape(-1, 6) != want.view(np.int32).reshape(-1, 6)).any(axis=1))[0]
+    assert len(bad) == 0, f"{len(bad)} tasks differ, first {tasks[bad[0]]}: {got[bad[0]]} vs {want[bad[0]]}"
+    assert bcells[0] <= cells[0] and bcells[1] <= cells[1]
+
+
 @pytest.mark.parametrize("name", G.ALIGN2_SETS)
 def test_oracle_ksw_align2_matches_reference(name):
     opt, tasks, want, qp, tp = G.load_align2(name)
