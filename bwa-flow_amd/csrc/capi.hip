@@ -207,7 +207,16 @@ struct Slot {
   size_t in_rco = 0, in_cso = 0;  // where the batch's offsets sit in h_in
   bool slot_view = false;         // h_out holds the last batch's slot layout
   bool busy = false;
-  int32_t n_reads = 0, n_seeds = 0;
+  // the last submitted batch finished and its results are in h_dense / h_n /
+  // h_off (set by _wait; cleared by the next _submit, and never set when a
+  // submit fails)
+  bool has_results = false;
+  // the finished batch's offsets, copied out of h_in by a _stage of the next
+  // batch (which overwrites h_in) so that a later _results can still build
+  // the slot layout
+  bool kept = false;
+  std::vector<int32_t> keep_rco, keep_cso;
+  int32_t n_reads = 0, n_chains = 0, n_seeds = 0;
   std::chrono::steady_clock::time_point t_submit;
   bwagpu_stats_t last{};
   int64_t h2d = 0, d2h = 0;
@@ -802,10 +811,17 @@ void register_caller_locked(bwagpu_ctx_t* ctx, hipStream_t st) {
   ctx->callers.push_back(st);
 }
 
-hipError_t choose_side(bwagpu_ctx_t* ctx, Slot& s, hipStream_t st) {
+// *snap: the slot's streams as of this call, copied under side_mu — a later
+// caller stream may retire s.spec.side from another thread (register_caller_locked)
+// while this slot's launches are being enqueued; they use the copy (a retired
+// side stream stays alive in the graveyard until the context goes)
+hipError_t choose_side(bwagpu_ctx_t* ctx, Slot& s, hipStream_t st, SpecStreams* snap) {
   std::lock_guard<std::mutex> g(ctx->side_mu);
   register_caller_locked(ctx, st);
-  if (s.side_chosen) return hipSuccess;
+  if (s.side_chosen) {
+    *snap = s.spec;
+    return hipSuccess;
+  }
   if (!s.spec.fork) {
     hipError_t e = hipEventCreateWithFlags(&s.spec.fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.spec.join, hipEventDisableTiming);
@@ -833,6 +849,7 @@ hipError_t choose_side(bwagpu_ctx_t* ctx, Slot& s, hipStream_t st) {
   if (e != hipSuccess) return e;
   s.spec.side = pick;
   s.side_chosen = true;
+  *snap = s.spec;
   return hipSuccess;
 }
 
@@ -893,14 +910,15 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;
-  HIPC(choose_side(ctx, s, st), "side stream");
+  SpecStreams ss;
+  HIPC(choose_side(ctx, s, st, &ss), "side stream");
   a.lq_bound = lq_max;
   const int tb = tb_bytes_for(ctx->opt, std::max(lq_max, 1));
-  s.spec.form = ctx->ext_form;
-  s.spec.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
-  s.spec.pool_n = (int)ctx->prof_ev.size();
-  s.spec.pool_used = &ctx->prof_used;
-  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, s.spec), "spec chain2aln launch");
+  ss.form = ctx->ext_form;
+  ss.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
+  ss.pool_n = (int)ctx->prof_ev.size();
+  ss.pool_used = &ctx->prof_used;
+  HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, ss), "spec chain2aln launch");
   return BWAGPU_OK;
 }
 
@@ -1017,8 +1035,8 @@ namespace {
 // from a finished batch's dense results; the offsets come from the staged input
 void expand_slots(const Slot& s, bwagpu_alnreg_t* dst) {
   const char* h = s.h_in.as<const char>();
-  const int32_t* rco = (const int32_t*)(h + s.in_rco);
-  const int32_t* cso = (const int32_t*)(h + s.in_cso);
+  const int32_t* rco = s.kept ? s.keep_rco.data() : (const int32_t*)(h + s.in_rco);
+  const int32_t* cso = s.kept ? s.keep_cso.data() : (const int32_t*)(h + s.in_cso);
   const int32_t* n = s.h_n.as<const int32_t>();
   const int32_t* off = s.h_off.as<const int32_t>();
   const bwagpu_alnreg_t* src = s.h_dense.as<const bwagpu_alnreg_t>();
@@ -1031,13 +1049,15 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot already has a batch in flight");
+  // the previous batch's results end here, whether or not this submit succeeds
+  s.has_results = false;
+  s.kept = false;
+  s.slot_view = false;
   int lq_max = 0;
   int rc = check_batch_header(ctx, b);
   if (rc) return rc;
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
   s.t_submit = std::chrono::steady_clock::now();
-  s.n_reads = b->n_reads;
-  s.n_seeds = b->n_seeds;
   InLayout L;
   L.make(*b);
   HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
@@ -1120,6 +1140,10 @@ int bwagpu_chain2aln_submit(bwagpu_ctx_t* ctx, int slot, const bwagpu_batch_t* b
   s.h2d = (int64_t)L.total;
   s.in_rco = L.rco;
   s.in_cso = L.cso;
+  // the batch's sizes only once it is in flight: _wait and _results read them
+  s.n_reads = b->n_reads;
+  s.n_chains = b->n_chains;
+  s.n_seeds = b->n_seeds;
   s.busy = true;
   return BWAGPU_OK;
 }
@@ -1155,6 +1179,7 @@ int bwagpu_chain2aln_wait(bwagpu_ctx_t* ctx, int slot, bwagpu_alnreg_t* out_regs
     nap_us = std::min(nap_us * 2, 320);
   }
   s.busy = false;
+  s.has_results = true;
   const int64_t* st = s.h_stats.as<int64_t>();
   float k_ms = 0, t_ms = 0;
   (void)hipEventElapsedTime(&k_ms, s.ev1, s.ev2);
@@ -1193,6 +1218,17 @@ int bwagpu_chain2aln_stage(bwagpu_ctx_t* ctx, int slot, int32_t n_reads, int32_t
   InLayout L;
   L.make(b);
   HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  // the caller packs the next batch over h_in: the finished batch's offsets
+  // move out first, so that its _results (valid until the next _submit) can
+  // still build the slot layout
+  if (s.has_results && !s.slot_view && !s.kept && s.n_reads) {
+    const char* hp = s.h_in.as<const char>();
+    const int32_t* rco = (const int32_t*)(hp + s.in_rco);
+    s.keep_rco.assign(rco, rco + s.n_reads + 1);
+    const int32_t* cso = (const int32_t*)(hp + s.in_cso);
+    s.keep_cso.assign(cso, cso + s.n_chains + 1);
+    s.kept = true;
+  }
   HIPC(s.h_in.ensure(L.total), "hipHostMalloc(in)");
   char* h = s.h_in.as<char>();
   b.seq_off = (const int64_t*)(h + L.seq_off);
@@ -1210,6 +1246,7 @@ int bwagpu_chain2aln_results(bwagpu_ctx_t* ctx, int slot, const bwagpu_alnreg_t*
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS || !regs || !n) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot's batch still in flight (wait first)");
+  if (!s.has_results) return fail(ctx, BWAGPU_E_INVAL, "slot has no results");
   if (!s.slot_view) {  // the slot layout, built from the dense results once per batch
     HIPC(s.h_out.ensure(sizeof(bwagpu_alnreg_t) * (size_t)std::max(s.n_seeds, 1)), "hipHostMalloc(out)");
     if (s.n_seeds) expand_slots(s, s.h_out.as<bwagpu_alnreg_t>());
@@ -1225,7 +1262,7 @@ int bwagpu_chain2aln_results_dense(bwagpu_ctx_t* ctx, int slot, const bwagpu_aln
   if (!ctx || slot < 0 || slot >= BWAGPU_NUM_SLOTS || !regs || !n || !off) return BWAGPU_E_INVAL;
   Slot& s = ctx->slot[slot];
   if (s.busy) return fail(ctx, BWAGPU_E_INVAL, "slot's batch still in flight (wait first)");
-  if (!s.h_dense.p || !s.h_off.p) return fail(ctx, BWAGPU_E_INVAL, "slot has no results");
+  if (!s.has_results || !s.h_dense.p || !s.h_off.p) return fail(ctx, BWAGPU_E_INVAL, "slot has no results");
   *regs = s.h_dense.as<const bwagpu_alnreg_t>();
   *n = s.h_n.as<const int32_t>();
   *off = s.h_off.as<const int32_t>();

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "bwagpu.h"
+#include "bwagpu_debug.h"
 
 namespace bwagpu {
 

@@ -377,29 +377,6 @@ int FlatBatch::pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec)
   return BWAGPU_OK;
 }
 
-mem_alnreg_v* FlatBatch::unpack_from(const bwagpu_alnreg_t* rg, const int32_t* nn, int batch_num) const {
-  mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));
-  if (!av) throw std::runtime_error("Memory allocation failed");
-  std::atomic<bool> oom{false};
-  parallel_ranges(batch_num, [&](int r0, int r1) {
-    for (int i = r0; i < r1; ++i) {
-      const size_t k = (size_t)nn[i];
-      av[i].n = av[i].m = k;
-      av[i].a = nullptr;
-      if (k) {
-        av[i].a = (mem_alnreg_t*)malloc(sizeof(mem_alnreg_t) * k);
-        if (!av[i].a) {
-          oom = true;
-          continue;
-        }
-        memcpy(av[i].a, &rg[chain_seed_off[read_chain_off[i]]], sizeof(mem_alnreg_t) * k);
-      }
-    }
-  });
-  if (oom) throw std::runtime_error("Memory allocation failed");
-  return av;
-}
-
 mem_alnreg_v* FlatBatch::unpack_dense(const bwagpu_alnreg_t* rg, const int32_t* nn, const int32_t* off,
                                       int batch_num) {
   mem_alnreg_v* av = (mem_alnreg_v*)malloc(sizeof(mem_alnreg_v) * (size_t)(batch_num > 0 ? batch_num : 1));

@@ -88,8 +88,6 @@ struct FlatBatch {
   int pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec);
   // ~ processOutput (FPGAPipeline.cpp:29-130): regions into malloc'd mem_alnreg_v
   mem_alnreg_v* unpack(int batch_num) const;
-  // the same from a slot's pinned results in the slot layout (bwagpu_chain2aln_results)
-  mem_alnreg_v* unpack_from(const bwagpu_alnreg_t* regs, const int32_t* n, int batch_num) const;
   // ... and from the dense ones (bwagpu_chain2aln_results_dense: read i's at regs[off[i]])
   static mem_alnreg_v* unpack_dense(const bwagpu_alnreg_t* regs, const int32_t* n, const int32_t* off,
                                     int batch_num);
@@ -98,8 +96,9 @@ struct FlatBatch {
 // frees the chains of a record the way ChainsToRegions::compute does
 void freeChainsRecordChains(mem_chain_v* chains, int batch_num);
 
-// Background threads that free the records' chains (freeChainsRecordChains)
-// in arrival order, so the stage workers do not.  A record's chains come from
+// Background threads that free the records' chains (freeChainsRecordChains),
+// so the stage workers do not; with several threads records are freed in no
+// particular order.  A record's chains come from
 // one SeqsToChains worker's glibc arena; one thread per record keeps a
 // record's frees on one arena lock, and several threads free different
 // records (different arenas) at once: threads() of them, BWAGPU_REAPER_THREADS

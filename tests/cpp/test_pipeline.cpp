@@ -38,6 +38,7 @@
 
 #include "GPUPipeline.h"
 #include "cpu_stage.h"
+#include "bwagpu_debug.h"  // bwagpu_debug_fail_wait (the hang tests)
 #include "oracle.h"
 
 static std::vector<uint8_t> slurp(const std::string& p) {

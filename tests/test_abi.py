@@ -1,5 +1,5 @@
 """CPU: the C-ABI library builds for gfx950, loads, and exports exactly what
-include/bwagpu.h declares; the Python/numpy mirrors match the C layouts.
+include/bwagpu.h and include/bwagpu_debug.h declare; the Python/numpy mirrors match the C layouts.
 No compute calls here (no GPU in the CPU tier)."""
 import ctypes as C
 import os
@@ -15,10 +15,12 @@ from bwagpu import abi
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(REPO, "include", "bwagpu.h")
+# the tuning / test / profiling entries live in a header of their own
+DBG_HDR = os.path.join(REPO, "include", "bwagpu_debug.h")
 
 
 def declared_functions():
-    txt = open(HDR).read()
+    txt = open(HDR).read() + open(DBG_HDR).read()
     return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(bwagpu_\w+)\s*\(", txt, re.M)))
 
 

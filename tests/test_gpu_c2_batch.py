@@ -93,3 +93,45 @@ def test_full_batch_malformed_refused():
     regs, n = eng.chain2aln(b)
     assert rb.check(regs, n)
     eng.close()
+
+
+def test_slot_results_survive_the_next_stage():
+    """bwagpu_chain2aln_results stays valid until the slot's next _submit
+    (include/bwagpu.h): wait(NULL) -> _stage of the NEXT batch over the slot's
+    pinned input -> _results must still give the finished batch's slot layout
+    (its offsets are moved out of the staging buffer before it is overwritten);
+    a submit that is refused leaves the slot with no results at all"""
+    import ctypes as C
+    from bwagpu import workload
+    from bwagpu.engine import BwaGpuError
+    opt, ref, rbs = workload.load_fixture()
+    b0, b1 = rbs[0].batch, rbs[1].batch
+    eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
+    lib = eng.lib
+    eng.submit(1, b0)
+    assert lib.bwagpu_chain2aln_wait(eng.ctx, 1, None, None) == 0
+    view = abi.BatchC()
+    assert lib.bwagpu_chain2aln_stage(eng.ctx, 1, b1.n_reads, b1.n_chains, b1.n_seeds, int(b1.seq_off[-1]),
+                                      C.byref(view)) == 0
+    # the caller packs b1 into the pinned input (its offsets overwrite b0's)
+    for k, dt in (("read_chain_off", np.int32), ("chain_seed_off", np.int32), ("seq_off", np.int64)):
+        a = np.ascontiguousarray(getattr(b1, k), dt)
+        C.memmove(getattr(view, k), a.ctypes.data, a.nbytes)
+    rp, np_ = C.c_void_p(), C.c_void_p()
+    assert lib.bwagpu_chain2aln_results(eng.ctx, 1, C.byref(rp), C.byref(np_)) == 0
+    n = np.ctypeslib.as_array(C.cast(np_, C.POINTER(C.c_int32)), (b0.n_reads,)).copy()
+    regs = np.ctypeslib.as_array(C.cast(rp, C.POINTER(C.c_uint8)), (b0.n_seeds * 88,)).copy().view(abi.ALNREG_DTYPE)
+    assert rbs[0].check(regs, n)
+    # a refused submit on the slot: no results until a batch finishes there again
+    bad = workload.Batch(b0.seq_off, b0.seq, b0.read_chain_off, b0.chain_seed_off, b0.chain_rid,
+                         b0.chain_frac_rep, b0.seeds.copy())
+    bad.seeds[5]["qbeg"] = 10_000
+    with pytest.raises(BwaGpuError):
+        eng.submit(1, bad)
+    op = C.c_void_p()
+    assert lib.bwagpu_chain2aln_results(eng.ctx, 1, C.byref(rp), C.byref(np_)) == abi.E_INVAL
+    assert lib.bwagpu_chain2aln_results_dense(eng.ctx, 1, C.byref(rp), C.byref(np_), C.byref(op)) == abi.E_INVAL
+    eng.submit(1, b1)
+    got = eng.wait_dense(1, b1)
+    assert rbs[1].check_compact(*got)
+    eng.close()
