@@ -2,31 +2,44 @@
 """Benchmark of the MI355X seed-extension stage (bwa-flow's ChainsToRegions,
 src/Pipeline.cpp:503-544, as replaced by the GPU back end).
 
-Workload (BASELINE.json configs[1], "C2"; --workload c2_refseed, the default):
-ChainsRecords of 2x150 bp pairs seeded and chained by the REFERENCE's own
-bwa (index + mem_chain + mem_chain_flt + mem_flt_chained_seeds, exactly what
-bwa-flow's SeqsToChains hands to ChainsToRegions) on a chr21-sized synthetic
-genome (46.7 Mb, three contigs, interspersed/tandem repeats, N runs) — chr21
-itself is not available offline.  The batches come from the committed fixture
-tests/golden/c2_refseed.npz (oracle/gen_c2_fixture.py made it); the genome is
-regenerated by bwa-flow_amd/tools/synth.cpp and checked against the SHA-256 of
-the reference's pac.  Two distinct batches of 66,668 reads (10.0 Mbases,
-Pipeline.cpp:123,146) are resident in HBM before timing; step i runs batch
-i mod 2 into its own output buffers, and after the timed region EVERY step's
-output is checked bit for bit against the reference's regions (per-read counts
-+ SHA-256 of the 88-byte records).  One step = one batch through the stage
-(chain windows, seed order, containment tests, left/right ksw_extend2 with
-band retries, seedcov, regions).  --workload synth keeps round 1's generator
+Workload (BASELINE.json configs[1], "C2"; --workload c2_stream, the default):
+a STREAM of distinct ChainsRecords of 2x150 bp pairs on a chr21-sized
+synthetic genome (46.7 Mb, three contigs, interspersed/tandem repeats, N runs;
+chr21 itself is not available offline).  Global batch g holds 33,334 pairs
+(66,668 reads, 10.0 Mbases: Pipeline.cpp:123,146) drawn by
+bwa-flow_amd/tools/synth.cpp with seed STREAM_SEED + g; its chains are made by
+the device's own SeqsToChains (bwagpu_seqs2chains, bit-exact with the
+reference's mem_chain -> mem_chain_flt -> mem_flt_chained_seeds) against the
+genome's bwa index (bench_data/e2e, built once per box by the reference's
+bwa_idx_build).  The reference then checks the workload before any timing:
+its own SeqsToChains must give the same chains, and its own mem_chain2aln
+gives every batch's expected regions (oracle/_ref/libbwaref.so on the host
+cores: also the CPU baseline).  One step = one batch through the stage (chain
+windows, seed order, containment tests, left/right ksw_extend2 with band
+retries, seedcov, regions); step i runs stream batch i mod D (D = min(steps,
+--stream-batches), default 30 = 1M pairs) with every batch resident in HBM
+before timing (far more than the 256 MB MALL holds), and after the timed
+region EVERY step's output is checked bit for bit against the reference's.
+
+Side figures: "two_batch_fixture" (round 5's headline: the two
+reference-seeded batches of tests/golden/c2_refseed.npz cycled over the same
+steps), "hw_queues_4" (that figure again in a child process with HIP's default
+GPU_MAX_HW_QUEUES = 4), the PCIe-inclusive host-buffer path, the drop-in
+C++ stage end to end, CIGARs, seeding, chaining, the GRCh38-shaped regime legs
+and the whole bwa-mem pipeline against `bwa mem`.  --workload c2_refseed keeps
+the two fixture batches as the headline; --workload synth round 1's generator
 (exact-match chains along the true origin: lighter than the reference's).
 
 Multi-GPU: one process per GPU (torchrun); the packed reference is broadcast
-from rank 0 over RCCL/xGMI once; each rank runs the stage on its own copy of
-the batches (no data-path collective): weak scaling.
+from rank 0 over RCCL/xGMI once; rank r takes global batches r, r + N, r + 2N,
+... of the stream (bwa-flow's pull-scatter of read batches to workers,
+src/mpi/MPIChannel.cpp:140-200): disjoint shards, no data-path collective,
+weak scaling (D batches per rank).
 
 The CPU baseline (rank 0, N=1) is the reference's own mem_chain2aln compiled
 from /root/reference (oracle/_ref/libbwaref.so, "kind": "reference") — or our
-C restatement ("port") when that library is absent — on a bounded sample of the
-same batches, using the host cores this job may use.
+C restatement ("port") when that library is absent — over the same batches,
+using the host cores this job may use.
 """
 from __future__ import annotations
 
@@ -51,7 +64,9 @@ sys.path.insert(0, os.path.join(REPO, "bwa-flow_amd", "python"))
 # did.  INTEGRATION.md §2 gives the same setting for bwa-flow with --use_gpu.
 # Every leg also takes its caller streams through caller_streams(), which
 # keeps only streams that run concurrently with the others.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+# The hw_queues_4 side figure runs this file again as a child process with
+# BWAGPU_BENCH_KEEP_HWQ=1 and HIP's default of 4 queues.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16 and os.environ.get("BWAGPU_BENCH_KEEP_HWQ") != "1":
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 import numpy as np  # noqa: E402
@@ -71,6 +86,9 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # measured issue: 2.64 SIMD cycles per independent VALU wave-instruction at 8
 # waves/SIMD (profiles/r01e_issue_costs.json) -> 2/2.64 of the nominal peak
 VALU_ISSUE_PEAK_TOPS = VALU_PEAK_TOPS * 2.0 / 2.642
+# packed 16-bit peak: a v_pk_* lane-op does two 16-bit ops (157.3 T); the
+# extension kernel computes in packed halves, so this is its roofline peak
+PK16_PEAK_TOPS = 2 * VALU_PEAK_TOPS
 # algorithmic integer ops per evaluated cell: the reference's inner loop
 # (ksw.c:430-447) compiles (gcc -O2, x86-64; oracle/_ref/obj/ksw.o,
 # ksw_extend2+0x340..0x3ad) to 34 instructions per cell: 20 integer ALU ops
@@ -577,7 +595,7 @@ def end_to_end_stage(opt, ref, batches, checks, reps: int = 20,
     outs_r = [np.zeros(max(b.n_seeds, 1), abi.ALNREG_DTYPE) for b in batches]
     pn = (C.c_void_p * len(batches))(*[x.ctypes.data for x in outs_n])
     pr = (C.c_void_p * len(batches))(*[x.ctypes.data for x in outs_r])
-    times = np.zeros(10, np.float64)
+    times = np.zeros(12, np.float64)
     rc = lib.gpustage_run(C.byref(o), C.byref(bns), pac.ctypes.data_as(C.c_void_p), len(batches), arr, reps, 1,
                           workers, chain_mode, sink_workers, times.ctypes.data_as(C.c_void_p), C.cast(pn, C.c_void_p),
                           C.cast(pr, C.c_void_p))
@@ -592,7 +610,8 @@ def end_to_end_stage(opt, ref, batches, checks, reps: int = 20,
     nrec = max(int(times[5]), 1)
     ph = {k: round(float(v), 4) for k, v in zip(("pack_s", "submit_s", "wait_s", "post_s"), times[1:5])}
     per = {k: round(float(v) * 1e3 / nrec, 3) for k, v in zip(("pack", "submit", "wait", "post"), times[1:5])}
-    per.update(kernels=round(float(times[8]) * 1e3 / nrec, 3), h2d_and_results=round(float(times[9]) * 1e3 / nrec, 3))
+    per.update(kernels=round(float(times[8]) * 1e3 / nrec, 3), h2d_and_results=round(float(times[9]) * 1e3 / nrec, 3),
+               host_cpu_user=round(float(times[10]) * 1e3 / nrec, 3), host_cpu_sys=round(float(times[11]) * 1e3 / nrec, 3))
     own = (f"forwarded to RegionsToSam (the FPGA stage's ownership, FPGAPipeline.cpp:434); the sink stage "
            f"({sink_workers} threads) frees them"
            if chain_mode == 0 else f"freed by the stage's {os.environ.get('BWAGPU_REAPER_THREADS', '2')} reaper threads, "
@@ -710,7 +729,7 @@ def busy_ms(iv) -> float:
     return tot
 
 
-def regime_stage(dev, steps: int = 10, n_streams: int = 2) -> dict:
+def regime_stage(dev, steps: int = 10, n_streams: int = 2, ext_form: int = 0) -> dict:
     """C3 / C5 regime legs (BASELINE.json configs[2] / [4]): the
     GRCh38-shaped genome of tests/golden/c3_grch38.npz (195 contigs, l_pac
     3.1e9, the 0.78 GB pac resident in HBM, far past the 256 MB MALL) with one
@@ -767,12 +786,14 @@ def regime_stage(dev, steps: int = 10, n_streams: int = 2) -> dict:
         if name in ("c3", "c3_refseed") and ext_busy > 0:  # 150 bp: every task is in the first length bin
             ach = float(st[0]) * OPS_PER_CELL / (ext_busy * 1e-3) / 1e12
             r["roofline"] = {"bound": "valu", "kernel": DOMINANT_KERNEL, "achieved": round(ach, 3),
-                             "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tops/s", "frac": round(ach / VALU_PEAK_TOPS, 5),
+                             "peak": round(PK16_PEAK_TOPS, 1), "unit": "Tops/s", "frac": round(ach / PK16_PEAK_TOPS, 5),
+                             "frac_int32": round(ach / VALU_PEAK_TOPS, 5),
                              "avg_launch_ms": round(ext_ms / max(ext_n, 1), 4)}
         out[name] = r
 
     pac_t = torch.from_numpy(g.pac).to(dev)
     eng = Engine(dev.index or 0, opt, g.l_pac, g.ann_offset, g.ann_len, pac_device_ptr=pac_t.data_ptr())
+    eng.ext_form(ext_form)
     eng.set_device_read_len(max(int(np.diff(s.batch.seq_off).max()) for s in sets.values() if s.batch.n_reads))
     out["setup_s"] = round(time.perf_counter() - t0, 2)
     for name, s in sets.items():
@@ -785,6 +806,7 @@ def regime_stage(dev, steps: int = 10, n_streams: int = 2) -> dict:
     del g
     pac_t = torch.from_numpy(g2.pac).to(dev)
     eng = Engine(dev.index or 0, opt, g2.l_pac, g2.ann_offset, g2.ann_len, pac_device_ptr=pac_t.data_ptr())
+    eng.ext_form(ext_form)
     eng.set_device_read_len(int(np.diff(s.batch.seq_off).max()))
     run_set(eng, "c3_refseed", s)
     out["c3_refseed"].update({"l_pac": g2.l_pac, "contigs": len(g2.ann_len)})
@@ -794,7 +816,7 @@ def regime_stage(dev, steps: int = 10, n_streams: int = 2) -> dict:
     return out
 
 
-def c5_refseed_stage(pac_t, ref, dev, steps: int = 10, n_streams: int = 2) -> dict:
+def c5_refseed_stage(pac_t, ref, dev, steps: int = 10, n_streams: int = 2, ext_form: int = 0) -> dict:
     """C5 (BASELINE.json configs[4]) on chains the REFERENCE seeded: one mixed
     2x100 / 2x150 / 2x250 ChainsRecord of the chr21-sized genome
     (tests/golden/c5_refseed.npz, oracle/gen_c2_fixture.py --length mix) run
@@ -806,6 +828,7 @@ def c5_refseed_stage(pac_t, ref, dev, steps: int = 10, n_streams: int = 2) -> di
         return {"error": "c5_refseed fixture is for another genome"}
     rb = rbs[0]
     eng = Engine(dev.index or 0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac_device_ptr=pac_t.data_ptr())
+    eng.ext_form(ext_form)
     lens = np.diff(rb.batch.seq_off)
     eng.set_device_read_len(int(lens.max()))
     streams = caller_streams(dev, n_streams)
@@ -840,36 +863,411 @@ def c5_refseed_stage(pac_t, ref, dev, steps: int = 10, n_streams: int = 2) -> di
             "chain_source": "reference seeding (bwa mem_chain), chr21-sized genome"}
 
 
-def load_workload(args, rank, world, dev):
-    """-> (opt, HostRef, pac tensor on dev, [Batch], [RefBatch] or None, data text, config extras)"""
-    if args.workload == "c2_refseed":
+STREAM_SEED = 4000      # stream batch g: tools/synth.cpp reads with seed STREAM_SEED + g
+STREAM_PAIRS = 33_334   # pairs per ChainsRecord: 66,668 reads = 10.0 Mbases (Pipeline.cpp:123,146)
+
+
+def shard_ids(rank: int, world: int, per_rank: int) -> list[int]:
+    """the global stream batches rank `rank` of `world` takes: r, r + N, r + 2N, ...
+    (bwa-flow's pull-scatter hands read batches to workers in turn,
+    src/mpi/MPIChannel.cpp:140-200); the shards are disjoint and their union is
+    batches 0 .. N * per_rank - 1"""
+    return [rank + world * k for k in range(per_rank)]
+
+
+def ensure_bwa_index(local_rank: int, world: int) -> str | None:
+    """the golden genome's bwa index under bench_data/e2e (ref.fa.bwt/.sa/.pac/
+    .ann/.amb): kept when its stamp matches, else built by the reference's own
+    bwa_idx_build (oracle/_ref/sam_harness index: ~30-60 s, once per box) — the
+    index bwa-flow's SeqsToChains reads.  Local rank 0 builds, the others wait.
+    -> the index prefix, or None when it cannot be had"""
+    pre = os.path.join(E2E_DIR, "ref.fa")
+    h = os.path.join(REPO, "oracle", "_ref", "sam_harness")
+    have = os.path.exists(pre + ".bwt") and os.path.exists(pre + ".sa")
+    if not have and local_rank == 0 and os.access(h, os.X_OK):
+        import subprocess
+        os.makedirs(E2E_DIR, exist_ok=True)
+        t0 = time.perf_counter()
+        r = subprocess.run([h, "index", E2E_DIR, os.devnull, "7", "0", "150", "10000000", "1", "46709983"],
+                           cwd=REPO, capture_output=True, text=True, timeout=900)
+        log(f"[bench] bwa index of the golden genome: rc={r.returncode}, {time.perf_counter() - t0:.1f} s")
+    if world > 1:
+        dist.barrier()
+    return pre if os.path.exists(pre + ".bwt") and os.path.exists(pre + ".sa") else None
+
+
+def stream_reads(ref, g: int, pairs: int = STREAM_PAIRS) -> Batch:
+    """global stream batch g's reads (tools/synth.cpp, seed STREAM_SEED + g,
+    uniform over the genome's contigs, 0.8 % substitutions, 0.1 % indels); only
+    seq_off / seq are used"""
+    return synth_batch(ref, STREAM_SEED + g, pairs, 150)
+
+
+def stream_batches(dev, opt, ref, pac_t, index, gids: list[int], pairs: int = STREAM_PAIRS) -> tuple[list[Batch], float]:
+    """the stream's ChainsRecords `gids`: stream_reads(g), chains from the
+    DEVICE's SeqsToChains (bwagpu_seqs2chains) against `index` = a bwa index
+    prefix or (hdr, words, sa, sa_intv), on a context of its own, closed before
+    timing.  -> (batches, seconds)"""
+    t0 = time.perf_counter()
+    hdr, words, sa, sa_intv = workload.load_bwa_index(index) if isinstance(index, str) else index
+    ech = Engine(dev.index or 0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac_device_ptr=pac_t.data_ptr())
+    ech.set_bwt(hdr, words, sa, sa_intv)
+    out = []
+    for g in gids:
+        rd = stream_reads(ref, g, pairs)
+        rco, ch, cso, sd = ech.seqs2chains(rd.seq_off, rd.seq)
+        out.append(Batch(rd.seq_off, rd.seq, rco, cso, ch["rid"].copy(), ch["frac_rep"].copy(), sd))
+    ech.close()
+    torch.cuda.empty_cache()
+    return out, time.perf_counter() - t0
+
+
+def reference_answers(opt, ref, batches: list[Batch], prefix: str) -> dict:
+    """THE CHECKER (and the CPU baseline) of the stream: for every batch, the
+    reference's own SeqsToChains on the host must give the chains the device
+    made (oracle.ref_seqs2chains: ref_seqs2chains_batch), and the reference's own
+    mem_chain2aln (oracle/_ref/libbwaref.so, the host cores this job may use)
+    gives the expected regions, kept as a RefBatch (per-read counts + SHA-256 of
+    the 88-byte records) that every timed step's output is compared with.
+    -> {"checks": [RefBatch], "chains_identical": bool, "chain2aln_s": wall of
+    the reference mem_chain2aln calls, "cores": threads, "kind"}"""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    kind = "reference" if oracle.ref_lib() is not None else "port"
+    which = "ref" if kind == "reference" else "oracle"
+    cores = host_threads()
+    R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
+    checks, same, t_c2a, t_chain = [], True, 0.0, 0.0
+    for b in batches:
+        if kind == "reference":
+            t0 = time.perf_counter()
+            rco, rid, fr, cso, sd = oracle.ref_seqs2chains(prefix, b.seq_off, b.seq, n_threads=cores)
+            t_chain += time.perf_counter() - t0
+            same &= bool(np.array_equal(rco, b.read_chain_off) and np.array_equal(cso, b.chain_seed_off) and
+                         np.array_equal(rid, b.chain_rid) and np.array_equal(fr.view(np.uint32),
+                                                                         b.chain_frac_rep.view(np.uint32)) and
+                         all(np.array_equal(sd[f], b.seeds[f]) for f in ("rbeg", "qbeg", "len", "score")))
+        t0 = time.perf_counter()
+        regs, n, _ = oracle.chain2aln(which, opt, R, b, n_threads=cores)
+        t_c2a += time.perf_counter() - t0
+        c = np.ascontiguousarray(compact(b, regs, n))
+        checks.append(workload.RefBatch(b, n.astype(np.int32), hashlib.sha256(c.view(np.uint8).tobytes()).digest()))
+    return {"checks": checks, "chains_identical": same if kind == "reference" else None, "chain2aln_s": t_c2a,
+            "seqs2chains_s": t_chain, "cores": cores, "kind": kind}
+
+
+class Workload:
+    """what a rank runs: opt, host reference + its device copy, the timed
+    batches and their reference answers, the fixture's two batches (side
+    figure, warm-up, the chaining leg), the data text and config extras"""
+
+    def __init__(self, **kw):
+        self.fixture = None      # [RefBatch] of tests/golden/c2_refseed.npz (c2_* workloads)
+        self.ref_answers = None  # reference_answers() of the stream (c2_stream)
+        self.__dict__.update(kw)
+
+
+FIXTURE_DATA = ("synthetic (seeded) reads on a 46.7 Mb chr21-sized synthetic genome (3 contigs, interspersed + "
+                "tandem repeats, N runs), 2x150 bp pairs, 0.8% subs / 0.1% indels")
+
+
+def batch_stats(batches, checks) -> dict:
+    nr = sum(b.n_reads for b in batches)
+    st = dict(chains_per_read=round(sum(b.n_chains for b in batches) / nr, 3),
+              seeds_per_read=round(sum(b.n_seeds for b in batches) / nr, 3))
+    if checks:
+        st["regions_per_read"] = round(sum(int(rb.reg_n.sum()) for rb in checks) / nr, 3)
+    return st
+
+
+def load_workload(args, rank, world, dev, local: int = 0) -> Workload:
+    if args.workload in ("c2_refseed", "c2_stream"):
         opt, gref, refbatches = workload.load_fixture(with_ref=(rank == 0))
         L = int(np.load(workload.C2_FIXTURE)["genome_len"])
         ref, pac_t = broadcast_reference(gref, rank, world, dev)
         assert ref.l_pac == L
+        prefix = ensure_bwa_index(local, world) if args.workload == "c2_stream" else None
+        if args.workload == "c2_stream" and prefix is not None:
+            n_use = max(1, min(args.stream_batches, args.steps))
+            gids = shard_ids(rank, world, n_use)
+            batches, t_gen = stream_batches(dev, opt, ref, pac_t, prefix, gids)
+            t0 = time.perf_counter()
+            ans = reference_answers(opt, ref, batches, prefix)
+            t_ref = time.perf_counter() - t0
+            data = (FIXTURE_DATA + f"; a stream of {world * n_use} distinct ChainsRecords ({n_use} per GPU: global "
+                    f"batches rank + {world} k), reads from tools/synth.cpp (seed {STREAM_SEED} + batch), chains from "
+                    "the device's own SeqsToChains (bwagpu_seqs2chains) against the reference's bwa index, checked "
+                    "equal to the REFERENCE's own mem_chain/mem_chain_flt/mem_flt_chained_seeds before timing")
+            extras = dict(chain_source="device SeqsToChains, checked against the reference's", **batch_stats(
+                batches, ans["checks"]), stream_batches_per_gpu=n_use, stream_batches_total=world * n_use,
+                          stream_reads_per_gpu=sum(b.n_reads for b in batches),
+                          chains_identical_to_reference=ans["chains_identical"],
+                          setup_s={"reads_and_device_chains": round(t_gen, 2), "reference_check": round(t_ref, 2)})
+            return Workload(opt=opt, ref=ref, pac_t=pac_t, batches=batches, checks=ans["checks"], data=data,
+                            extras=extras, fixture=refbatches, ref_answers=ans, gids=gids)
+        if args.workload == "c2_stream":
+            log("[bench] no bwa index of the golden genome: the fixture's two batches are the workload")
         batches = [rb.batch for rb in refbatches]
+        checks = list(refbatches)
         if rank % len(batches):  # each rank starts at a different batch
             k = rank % len(batches)
-            batches, refbatches = batches[k:] + batches[:k], refbatches[k:] + refbatches[:k]
-        nr = sum(b.n_reads for b in batches)
-        st = dict(chains_per_read=round(sum(b.n_chains for b in batches) / nr, 3),
-                  seeds_per_read=round(sum(b.n_seeds for b in batches) / nr, 3),
-                  regions_per_read=round(sum(int(rb.reg_n.sum()) for rb in refbatches) / nr, 3))
-        data = ("synthetic (seeded) reads on a 46.7 Mb chr21-sized synthetic genome (3 contigs, interspersed + "
-                "tandem repeats, N runs), 2x150 bp pairs, 0.8% subs / 0.1% indels; chains from the REFERENCE's own "
-                "bwa index + mem_chain/mem_chain_flt/mem_flt_chained_seeds (tests/golden/c2_refseed.npz, "
-                "oracle/gen_c2_fixture.py)")
-        return opt, ref, pac_t, batches, refbatches, data, dict(chain_source="reference seeding (bwa mem_chain)", **st)
+            batches, checks = batches[k:] + batches[:k], checks[k:] + checks[:k]
+        data = (FIXTURE_DATA + "; chains from the REFERENCE's own bwa index + mem_chain/mem_chain_flt/"
+                "mem_flt_chained_seeds (tests/golden/c2_refseed.npz, oracle/gen_c2_fixture.py)")
+        return Workload(opt=opt, ref=ref, pac_t=pac_t, batches=batches, checks=checks, data=data,
+                        extras=dict(chain_source="reference seeding (bwa mem_chain)", **batch_stats(batches, checks)),
+                        fixture=refbatches)
     opt = abi.default_opt()
     ref, pac_t = shared_reference(args.ref_len, args.contigs, rank, world, dev)
     allb = rank_reads(ref, rank, args.pairs, args.read_len)
     batches = split_batches(allb, args.batch_bases)
     data = ("synthetic (seeded): 46.7 Mb chr21-sized reference, 2x150 bp pairs with 0.8% subs/0.1% indels, "
             "chains = exact-match seeds along the true origin (bwa-flow_amd/tools/synth.cpp)")
-    nr = allb.n_reads
-    return opt, ref, pac_t, batches, None, data, dict(chain_source="synth.cpp exact matches",
-                                                      chains_per_read=round(allb.n_chains / nr, 3),
-                                                      seeds_per_read=round(allb.n_seeds / nr, 3))
+    return Workload(opt=opt, ref=ref, pac_t=pac_t, batches=batches, checks=None, data=data,
+                    extras=dict(chain_source="synth.cpp exact matches", **batch_stats(batches, None)))
+
+
+def timed_steps(eng: Engine, dbs, slots, streams, steps: int, world: int, dev, prof: bool) -> dict:
+    """exactly `steps` steps (step i: batch dbs[i % len(dbs)] into its output
+    slots[i], on streams[i % len(streams)]) between a barrier + device sync on
+    each side; the job's time is the max over ranks, reads summed over ranks"""
+    stream = streams[0]
+    nb = len(dbs)
+    if prof:
+        eng.prof_start(3 * steps)  # HIP events around the dominant kernel's launches
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for x in streams[1:]:
+        x.wait_event(ev0)
+    for i in range(steps):
+        dbs[i % nb].run(eng, streams[i % len(streams)].cuda_stream, slots[i])
+    for x in streams[1:]:
+        e = torch.cuda.Event()
+        e.record(x)
+        stream.wait_event(e)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    elapsed = max(wall, gpu_s)
+    reads_done = sum(dbs[i % nb].b.n_reads for i in range(steps))
+    elapsed, total_reads = job_totals(elapsed, reads_done, world, dev)
+    r = dict(elapsed=elapsed, total_reads=total_reads, wall=wall, gpu_s=gpu_s)
+    if prof:
+        r["ext_ms"], r["ext_launches"] = eng.prof_read()
+        r["ext_iv"] = eng.prof_intervals(3 * steps)
+        eng.prof_start(0)
+    return r
+
+
+def steps_parity(dbs, slots, steps: int, world: int, dev) -> bool | None:
+    """every timed step's output against its batch's reference answer, all ranks"""
+    if any(d.check is None for d in dbs):
+        return None
+    ok = True
+    for i in range(steps):
+        d = dbs[i % len(dbs)]
+        ok &= d.check.check(*d.results(slots[i]))
+    pt = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(pt, op=dist.ReduceOp.SUM)
+    return float(pt.item()) == 0.0
+
+
+def make_slots(dbs, steps: int) -> list[int]:
+    """step i's output slot in its batch (one per run, so every step can be checked)"""
+    nb, slots = len(dbs), []
+    for i in range(steps):
+        slots.append(dbs[i % nb].add_out() if i >= nb else 0)
+    return slots
+
+
+def fixture_figure(eng: Engine, fixture, dev, streams, steps: int) -> dict:
+    """round 5's headline as a side figure: the two reference-seeded fixture
+    batches cycled over `steps` steps, same streams, parity on every step"""
+    dbs = [DevBatch(rb.batch, dev, rb) for rb in fixture]
+    slots = make_slots(dbs, steps)
+    for i in range(2 * len(dbs)):
+        dbs[i % len(dbs)].run(eng, streams[i % len(streams)].cuda_stream, 0, stats=False)
+    torch.cuda.synchronize()
+    t = timed_steps(eng, dbs, slots, streams, steps, 1, dev, prof=False)
+    par = steps_parity(dbs, slots, steps, 1, dev)
+    del dbs
+    torch.cuda.empty_cache()
+    return {"value": round(t["total_reads"] / t["elapsed"] / 1e6, 4), "unit": "Mreads/s",
+            "ms_per_step": round(t["elapsed"] / steps * 1e3, 4), "steps": steps, "distinct_batches": len(fixture),
+            "parity_all_steps": par, "streams": len(streams),
+            "workload": "tests/golden/c2_refseed.npz: 2 reference-seeded batches of 66,668 reads cycled (round 5's "
+                        "headline workload)"}
+
+
+def hw_queues_4_figure(steps: int, warmup: int, ext_form: int) -> dict:
+    """the fixture figure in a child process with HIP's default of 4 hardware
+    queues per process (GPU_MAX_HW_QUEUES unset: what a bwa-flow process gets
+    without INTEGRATION.md §2's setting); the parent's figure runs at 16"""
+    import subprocess
+    env = dict(os.environ, BWAGPU_BENCH_KEEP_HWQ="1")
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--workload", "c2_refseed", "--steps", str(steps),
+                        "--warmup", str(warmup), "--ext-form", str(ext_form), "--headline-only"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": f"rc={r.returncode} {r.stderr[-300:]}"}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": d["value"], "unit": "Mreads/s", "ms_per_step": d["ms_per_step"],
+            "parity_all_steps": d["parity_all_steps"], "gpu_max_hw_queues": 4, "streams": d["config"]["streams"],
+            "workload": "the two_batch_fixture workload, in a child process"}
+
+
+def headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapsed, total_reads, cells, cells_all,
+                  ext_ms, ext_launches, ext_busy_ms, parity) -> dict:
+    """rank 0's JSON line: the headline, its roofline (the dominant kernel, VALU
+    bound: packed 16-bit peak, the int32 figure beside it) and the HBM view"""
+    dev = dbs[0].dev
+    nb = len(dbs)
+    batches = [d.b for d in dbs]
+    # ---- launch-sequence duration (HIP events on the launch stream), outside the timed region
+    per = []
+    for i in range(min(nb, 8)):
+        a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        dbs[i].run(eng, sptr, 0, stats=False)
+        b_.record(stream)
+        torch.cuda.synchronize()
+        per.append(a.elapsed_time(b_) / 1e3)
+    launch_s = float(np.mean(per))
+    # the same kernel with the GPU to itself: each distinct batch (up to 8) alone
+    # on one stream, its first-bin launches (rounds A, B, C) timed by HIP events
+    n_iso = min(nb, 8)
+    iso, ext_tasks, tasks_ab = [], [], []
+    for i in range(n_iso):
+        eng.prof_start(3)
+        dbs[i].run(eng, sptr, 0, stats=False)
+        torch.cuda.synchronize()
+        iso.append([round(float(e - a), 4) for a, e in eng.prof_intervals(3)])
+        sc = np.zeros(8, np.int64)  # tasks of rounds A / B / C (bwagpu_debug_spec_counters)
+        eng.lib.bwagpu_debug_spec_counters(eng.ctx, ctypes.c_void_p(sptr), sc.ctypes.data_as(ctypes.c_void_p))
+        ext_tasks.append(int(sc[0] + sc[1]))
+        tasks_ab.append([int(sc[0]), int(sc[1])])
+    eng.prof_start(0)
+    runs = {j: sum(1 for i in range(args.steps) if i % nb == j) for j in range(nb)}
+    # the cells ksw_extend2 itself evaluates (ksw.c:424 iterations): each distinct
+    # batch that ran once more, untimed, with the row bound off (bwagpu_ctx_row_bound)
+    ref_cells = {}
+    prev_bound = eng.row_bound(0)
+    for i in range(nb):
+        if not runs[i]:
+            continue
+        st0 = torch.zeros(4, dtype=torch.int64, device=dev)
+        out, nn = dbs[i].outs[0]
+        eng.chain2aln_device(dbs[i].c, out.data_ptr(), nn.data_ptr(), st0.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        ref_cells[i] = int(st0.cpu().numpy()[0])
+    eng.row_bound(prev_bound)
+    # algorithmic HBM bytes of one launch sequence (batch average): inputs read
+    # once, regions + counts written once, 2-bit reference rows read (rows/4
+    # bytes), per-chain window + per-seed scratch written and read once
+    alg, ext_alg, cells_batch = [], [], []
+    for j, d in enumerate(dbs):
+        if not runs[j]:
+            continue
+        s = d.stats.cpu().numpy()
+        nreg = int(d.results(0)[1].sum())
+        alg.append(d.in_bytes + nreg * 88 + d.b.n_reads * 4 + (int(s[1]) // runs[j]) / 4 +
+                   2 * (d.b.n_chains * 16 + d.b.n_seeds * 8))
+        cells_batch.append(float(s[0]) / runs[j])
+    alg_bytes = float(np.mean(alg))
+    # the extension kernel's own algorithmic bytes per launch (rounds A and B: two
+    # launches per batch): per task its list entry 8 B, seed 24 B, chain window
+    # 16 B, owner read 4 B, read offsets 16 B, the read's bases (lq B) and the
+    # 48-byte SeedExt it writes; the 2-bit target rows the reference's DP reads
+    # (stats rows / 4 B)
+    for j in range(n_iso):
+        s = dbs[j].stats.cpu().numpy()
+        lq = float(dbs[j].b.seq_off[-1]) / max(dbs[j].b.n_reads, 1)
+        ext_alg.append((ext_tasks[j] * (8 + 24 + 16 + 4 + 16 + lq + 48) + (int(s[1]) // max(runs[j], 1)) / 4) / 2)
+    ext_alg_bytes = float(np.mean(ext_alg))
+    cells_step = cells / args.steps
+    cells_ref_step = sum(ref_cells[i % nb] for i in range(args.steps)) / args.steps
+    ext_avg_ms = ext_ms / max(ext_launches, 1)
+    # the dominant kernel's VALU roofline: algorithmic ops of the timed steps
+    # over the busy union of its launches in those steps
+    ach = cells * OPS_PER_CELL / (ext_busy_ms * 1e-3) / 1e12 if ext_busy_ms > 0 else None
+
+    global DOMINANT_KERNEL
+    DOMINANT_KERNEL = eng.ext_kernel(max(int(np.diff(b.seq_off).max()) for b in batches if b.n_reads))
+    traffic, traffic_src, pmc = load_traffic(args.workload)
+    iso_ms = [sum(x) for x in iso]
+    frac_iso = (float(np.sum(cells_batch[:n_iso])) * OPS_PER_CELL / (float(np.sum(iso_ms)) * 1e-3) / 1e12 /
+                PK16_PEAK_TOPS if iso and sum(iso_ms) > 0 else None)
+    value = total_reads / elapsed / 1e6
+    stream_wl = W.ref_answers is not None
+    wl_text = ("STAGE-ONLY (the SW-extend stage, ChainsToRegions: mem_chain2aln + ksw_extend2, on the GPU; seeding, "
+               "pairing and SAM are not in this number: end_to_end_align is the whole pipeline) C2: 2x150 bp pairs vs "
+               "a chr21-sized reference, ChainsRecords of 66,668 reads, inputs resident in HBM; " +
+               (f"a stream of {nb} distinct batches per GPU ({sum(b.n_reads for b in batches)} reads), each timed "
+                f"step a different batch until the stream is used up" if stream_wl else
+                f"{nb} distinct reference-seeded batches cycled"))
+    return {
+        "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": W.data,
+        "config": {"workload": wl_text if args.workload != "synth" else
+                   "STAGE-ONLY C2 (synth chains): SW-extend stage on GPU, inputs resident in HBM",
+                   "reads_per_batch": int(np.mean([b.n_reads for b in batches])), "distinct_batches": nb,
+                   "distinct_batches_timed": min(nb, args.steps),
+                   "batch_bases": args.batch_bases, "read_len": 150 if args.workload != "synth" else args.read_len,
+                   "parallelism": f"dp{world}", "streams": len(streams),
+                   "sharding": (f"rank r runs global stream batches r, r+{world}, ... (disjoint shards)"
+                                if stream_wl else "every rank runs the same batches"), **W.extras},
+        "gcups": round(cells_all / elapsed / 1e9, 3),
+        # the same over the cells the reference's ksw_extend2 evaluates (the row
+        # bound ends calls early: those rows' cells are never computed)
+        "gcups_reference_cells": round(cells_ref_step * args.steps * world / elapsed / 1e9, 3),
+        "row_bound": bool(eng.row_bound(-1)),
+        "stage_only": True,
+        "parity_all_steps": parity,
+        "roofline": {"bound": "valu", "kernel": DOMINANT_KERNEL,
+                     # the kernel computes in packed 16-bit halves (v_pk_*: two DP cells per
+                     # lane-op, issued at ~4 cycles per wave-instruction like every 3-input /
+                     # DPP op it uses, DESIGN.md §3 round 5): the peak is the packed-16 one
+                     "achieved": round(ach, 3) if ach else None, "peak": round(PK16_PEAK_TOPS, 1), "unit": "Tops/s",
+                     "frac": round(ach / PK16_PEAK_TOPS, 5) if ach else None,
+                     "arith": "int16x2 packed (v_pk_*), int32 guards and row-end state",
+                     "peak_int32": round(VALU_PEAK_TOPS, 1),
+                     "frac_int32": round(ach / VALU_PEAK_TOPS, 5) if ach else None,
+                     "peak_measured_issue_int32": round(VALU_ISSUE_PEAK_TOPS, 1),
+                     "frac_denominator": "busy union of the kernel's launch intervals (HIP events)",
+                     "cells": "computed cells (the row bound's skipped rows are not counted)",
+                     "ops_per_cell": OPS_PER_CELL, "cells_per_step": round(cells_step),
+                     "cells_per_step_reference": round(cells_ref_step),
+                     # busy time: the union of the kernel's launch intervals in the timed steps
+                     # (HIP events on the launching streams), <= ms_per_step
+                     "kernel_ms_per_step": round(ext_busy_ms / args.steps, 4),
+                     "kernel_sum_ms_per_step": round(ext_ms / args.steps, 4), "launches_timed": ext_launches,
+                     "avg_launch_ms": round(ext_avg_ms, 4),
+                     # the kernel alone on the GPU (one stream, one batch at a time)
+                     "isolated_launch_ms": iso, "frac_isolated": round(frac_iso, 5) if frac_iso else None,
+                     "tasks_round_a_b": tasks_ab,
+                     "traffic": traffic, "traffic_source": traffic_src, "pmc": pmc,
+                     "alg_bytes_per_launch": round(ext_alg_bytes),
+                     "traffic_over_alg": round(traffic / ext_alg_bytes, 3) if traffic and ext_alg_bytes else None,
+                     "formula": "cells_per_step * ops_per_cell / kernel_ms_per_step (busy union) / peak "
+                                "(DESIGN.md §5)",
+                     "frac_step": round(cells_step * OPS_PER_CELL / (elapsed / args.steps) / 1e12 / PK16_PEAK_TOPS, 5)},
+        "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / launch_s / 1e9, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg_bytes / launch_s / 1e9 / HBM_PEAK_GBS, 6),
+                         "alg_bytes_per_launch_sequence": round(alg_bytes), "launch_sequence_ms": round(launch_s * 1e3, 4),
+                         "kernel": "whole SW-stage launch sequence (all kernels of one batch)"},
+    }
 
 
 def main():
@@ -877,7 +1275,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2_refseed", choices=("c2_refseed", "synth"))
+    ap.add_argument("--workload", default="c2_stream", choices=("c2_stream", "c2_refseed", "synth"))
+    ap.add_argument("--stream-batches", type=int, default=30,
+                    help="c2_stream: distinct ChainsRecords per GPU (30 = 1M pairs); step i runs batch i mod "
+                         "min(this, steps)")
     ap.add_argument("--pairs", type=int, default=1_000_000, help="synth: read pairs per GPU (C2: 1M)")
     ap.add_argument("--ref-len", type=int, default=46_709_983, help="synth: reference length (chr21: 46.7 Mb)")
     ap.add_argument("--contigs", type=int, default=1)
@@ -892,6 +1293,8 @@ def main():
     ap.add_argument("--no-seeding", action="store_true", help="skip the seeding (mem_collect_intv) line")
     ap.add_argument("--no-regime", action="store_true", help="skip the C3/C5 GRCh38-regime legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the whole-pipeline end-to-end align leg")
+    ap.add_argument("--no-hwq4", action="store_true", help="skip the GPU_MAX_HW_QUEUES=4 side figure")
+    ap.add_argument("--headline-only", action="store_true", help="the headline line only (no side legs)")
     ap.add_argument("--e2e-pairs", type=int, default=300_000)
     ap.add_argument("--no-prof", action="store_true", help="no HIP events around the dominant kernel (A/B of their cost)")
     ap.add_argument("--ext-form", type=int, default=0, choices=(0, 1, 2),
@@ -902,8 +1305,10 @@ def main():
                          "one stream per stage worker): batch i+1's launches overlap batch i's tail; 3 since the row "
                          "bound (2 / 3 / 4: 45.7-46.3 / 48.0-51.2 / 42.8-43.8 Mreads/s, gpurun_out/r6z)")
     args = ap.parse_args()
+    if args.headline_only:
+        args.no_cpu = args.no_host_path = args.no_cigar = args.no_seeding = args.no_regime = True
+        args.no_e2e = args.no_hwq4 = True
 
-    abi.load().bwagpu_debug_ext_form(args.ext_form)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -912,24 +1317,27 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    def new_engine(opt_, l_pac, ann_offset, ann_len, pac_ptr) -> Engine:
+        """a context with this run's extension form (bwagpu_ctx_ext_form)"""
+        e = Engine(local, opt_, l_pac, ann_offset, ann_len, pac_device_ptr=pac_ptr)
+        e.ext_form(args.ext_form)
+        return e
+
     # reference: on rank 0, broadcast over RCCL (xGMI) at start-up only
     t0 = time.perf_counter()
-    opt, ref, pac_t, batches, checks, data, wl = load_workload(args, rank, world, dev)
+    W = load_workload(args, rank, world, dev, local)
+    opt, ref, pac_t, batches, checks = W.opt, W.ref, W.pac_t, W.batches, W.checks
     setup_s = time.perf_counter() - t0
-    eng = Engine(local, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac_device_ptr=pac_t.data_ptr())
+    eng = new_engine(opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac_t.data_ptr())
     # the producer of the resident batches knows their longest read (bwagpu_set_device_read_len)
     eng.set_device_read_len(max(int(np.diff(b.seq_off).max()) for b in batches if b.n_reads))
     dbs = [DevBatch(b, dev, checks[i] if checks else None) for i, b in enumerate(batches)]
     nb = len(dbs)
-    # step i runs batch i % nb into its own output buffers
-    slots = []
-    for i in range(args.steps):
-        d = dbs[i % nb]
-        slots.append(d.add_out() if i >= nb else 0)
+    slots = make_slots(dbs, args.steps)
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: {nb} batches, {sum(b.n_reads for b in batches)} reads, "
         f"{sum(b.n_chains for b in batches)} chains, {sum(b.n_seeds for b in batches)} seeds "
-        f"(load+upload+bcast {setup_s:.1f} s)")
+        f"(setup {setup_s:.1f} s)")
 
     # a dedicated stream: the engine launches on it and every HIP event below is
     # recorded on it (the null stream would leave the engine on its own stream)
@@ -937,44 +1345,24 @@ def main():
     stream = streams[0]
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+    # warm-up: on the fixture's batches when there are any, so that the timed
+    # stream batches start cold (not in the MALL)
+    wdbs = [DevBatch(rb.batch, dev) for rb in W.fixture] if W.fixture and W.ref_answers else dbs
     for i in range(args.warmup):
-        dbs[i % nb].run(eng, streams[i % len(streams)].cuda_stream, 0, stats=False)
+        wdbs[i % len(wdbs)].run(eng, streams[i % len(streams)].cuda_stream, 0, stats=False)
     torch.cuda.synchronize()
+    if wdbs is not dbs:
+        del wdbs
     for d in dbs:
         d.stats.zero_()
-    if not args.no_prof:
-        eng.prof_start(3 * args.steps)  # HIP events around the dominant kernel's launches
 
     # ---- timed region: exactly K steps
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for x in streams[1:]:
-        x.wait_event(ev0)
-    for i in range(args.steps):
-        dbs[i % nb].run(eng, streams[i % len(streams)].cuda_stream, slots[i])
-    for x in streams[1:]:
-        e = torch.cuda.Event()
-        e.record(x)
-        stream.wait_event(e)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    gpu_s = ev0.elapsed_time(ev1) / 1e3
-    elapsed = max(wall, gpu_s)
-    reads_done = sum(dbs[i % nb].b.n_reads for i in range(args.steps))
-    elapsed, total_reads = job_totals(elapsed, reads_done, world, dev)
-    ext_ms, ext_launches = eng.prof_read()
-    ext_iv = eng.prof_intervals(3 * args.steps)
-    eng.prof_start(0)
-    # the dominant kernel's busy time: the union of its launch intervals (the two
+    T = timed_steps(eng, dbs, slots, streams, args.steps, world, dev, prof=not args.no_prof)
+    elapsed, total_reads = T["elapsed"], T["total_reads"]
+    ext_ms, ext_launches = T.get("ext_ms", 0.0), T.get("ext_launches", 0)
+    # the dominant kernel's busy time: the union of its launch intervals (the
     # caller streams' launches overlap; their summed durations can exceed the wall)
-    ext_busy_ms = busy_ms(ext_iv)
+    ext_busy_ms = busy_ms(T.get("ext_iv", []))
 
     # per-step counters (cells/rows/calls) of the timed steps
     cells = rows = calls = 0
@@ -990,152 +1378,28 @@ def main():
     cells_all = float(ctot[0].item())
 
     # bit-exact check of EVERY timed step's output against the reference's regions
-    parity = None
-    if checks:
-        parity = True
-        for i in range(args.steps):
-            regs, n = dbs[i % nb].results(slots[i])
-            parity &= dbs[i % nb].check.check(regs, n)
-        pt = torch.tensor([0.0 if parity else 1.0], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(pt, op=dist.ReduceOp.SUM)
-        parity = float(pt.item()) == 0.0
+    parity = steps_parity(dbs, slots, args.steps, world, dev) if checks else None
 
-    # ---- launch-sequence duration (HIP events on the launch stream), outside the timed region
-    per = []
-    for i in range(min(nb, 8)):
-        a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        dbs[i].run(eng, sptr, 0, stats=False)
-        b_.record(stream)
-        torch.cuda.synchronize()
-        per.append(a.elapsed_time(b_) / 1e3)
-    launch_s = float(np.mean(per))
-    # the same kernel with the GPU to itself: each distinct batch alone on one
-    # stream, its first-bin launches (rounds A, B, C) timed by HIP events
-    iso, ext_tasks, tasks_ab = [], [], []
-    for i in range(nb):
-        eng.prof_start(3)
-        dbs[i].run(eng, sptr, 0, stats=False)
-        torch.cuda.synchronize()
-        iso.append([round(float(e - a), 4) for a, e in eng.prof_intervals(3)])
-        sc = np.zeros(8, np.int64)  # tasks of rounds A / B / C (bwagpu_debug_spec_counters)
-        eng.lib.bwagpu_debug_spec_counters(eng.ctx, ctypes.c_void_p(sptr), sc.ctypes.data_as(ctypes.c_void_p))
-        ext_tasks.append(int(sc[0] + sc[1]))
-        tasks_ab.append([int(sc[0]), int(sc[1])])
-    eng.prof_start(0)
-    # the cells ksw_extend2 itself evaluates (ksw.c:424 iterations): each distinct
-    # batch once more, untimed, with the row bound off (bwagpu_ctx_row_bound)
-    ref_cells = []
-    prev_bound = eng.row_bound(0)
-    for i in range(nb):
-        st0 = torch.zeros(4, dtype=torch.int64, device=dev)
-        out, nn = dbs[i].outs[0]
-        eng.chain2aln_device(dbs[i].c, out.data_ptr(), nn.data_ptr(), st0.data_ptr(), sptr)
-        torch.cuda.synchronize()
-        ref_cells.append(int(st0.cpu().numpy()[0]))
-    eng.row_bound(prev_bound)
-    # algorithmic HBM bytes of one launch sequence (batch average): inputs read
-    # once, regions + counts written once, 2-bit reference rows read (rows/4
-    # bytes), per-chain window + per-seed scratch written and read once
-    regs0, n0 = dbs[0].results(0)
-    runs = {j: sum(1 for i in range(args.steps) if i % nb == j) for j in range(nb)}
-    alg = []
-    for j, d in enumerate(dbs):
-        s = d.stats.cpu().numpy()
-        nreg = int(d.results(0)[1].sum())
-        alg.append(d.in_bytes + nreg * 88 + d.b.n_reads * 4 + (int(s[1]) // max(runs[j], 1)) / 4 +
-                   2 * (d.b.n_chains * 16 + d.b.n_seeds * 8))
-    alg_bytes = float(np.mean(alg))
-    # the extension kernel's own algorithmic bytes per launch (rounds A and B: two
-    # launches per batch): per task its list entry 8 B, seed 24 B, chain window
-    # 16 B, owner read 4 B, read offsets 16 B, the read's bases (lq B) and the
-    # 48-byte SeedExt it writes; the 2-bit target rows the reference's DP reads
-    # (stats rows / 4 B)
-    ext_alg = []
-    for j, d in enumerate(dbs):
-        s = d.stats.cpu().numpy()
-        lq = float(d.b.seq_off[-1]) / max(d.b.n_reads, 1)
-        ext_alg.append((ext_tasks[j] * (8 + 24 + 16 + 4 + 16 + lq + 48) + (int(s[1]) // max(runs[j], 1)) / 4) / 2)
-    ext_alg_bytes = float(np.mean(ext_alg))
-    cells_step = cells / args.steps
-    cells_ref_step = sum(ref_cells[i % nb] for i in range(args.steps)) / args.steps
-    ext_avg_ms = ext_ms / max(ext_launches, 1)
-    # the dominant kernel's VALU roofline: algorithmic ops of the timed steps
-    # over the summed duration of its launches in those steps
-    ach = cells * OPS_PER_CELL / (ext_busy_ms * 1e-3) / 1e12 if ext_busy_ms > 0 else None
-
-    global DOMINANT_KERNEL
-    DOMINANT_KERNEL = eng.ext_kernel(max(int(np.diff(b.seq_off).max()) for b in batches if b.n_reads))
-    traffic, traffic_src, pmc = load_traffic(args.workload)
-    # algorithmic cells of one run of each distinct batch (its timed runs' total / runs)
-    cells_batch = [float(d.stats.cpu().numpy()[0]) / max(runs[j], 1) for j, d in enumerate(dbs)]
-    iso_ms = [sum(x) for x in iso]
-    frac_iso = (float(np.sum(cells_batch)) * OPS_PER_CELL / (float(np.sum(iso_ms)) * 1e-3) / 1e12 / VALU_PEAK_TOPS
-                if iso and sum(iso_ms) > 0 else None)
     result = None
     if rank == 0:
-        value = total_reads / elapsed / 1e6
-        result = {
-            "metric": METRIC, "value": round(value, 4), "unit": "Mreads/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": data,
-            "config": {"workload": ("STAGE-ONLY (the SW-extend stage, ChainsToRegions: mem_chain2aln + ksw_extend2, on "
-                                    "the GPU; seeding, pairing and SAM are not in this number: end_to_end_align is the "
-                                    "whole pipeline) C2: 2x150 bp pairs vs a chr21-sized reference, reference-seeded "
-                                    "ChainsRecords of 66,668 reads, inputs resident in HBM")
-                       if args.workload == "c2_refseed" else
-                       "STAGE-ONLY C2 (synth chains): SW-extend stage on GPU, inputs resident in HBM",
-                       "reads_per_batch": int(np.mean([b.n_reads for b in batches])), "distinct_batches": nb,
-                       "batch_bases": args.batch_bases, "read_len": 150 if args.workload == "c2_refseed" else args.read_len,
-                       "parallelism": f"dp{world}", "streams": args.streams, **wl},
-            "gcups": round(cells_all / elapsed / 1e9, 3),
-            # the same over the cells the reference's ksw_extend2 evaluates (the row
-            # bound ends calls early: those rows' cells are never computed)
-            "gcups_reference_cells": round(cells_ref_step * args.steps * world / elapsed / 1e9, 3),
-            "row_bound": bool(prev_bound),
-            "stage_only": True,
-            "parity_all_steps": parity,
-            "roofline": {"bound": "valu", "kernel": DOMINANT_KERNEL,
-                         "achieved": round(ach, 3) if ach else None, "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tops/s",
-                         "frac": round(ach / VALU_PEAK_TOPS, 5) if ach else None,
-                         "peak_measured_issue": round(VALU_ISSUE_PEAK_TOPS, 1),
-                         "frac_measured_issue": round(ach / VALU_ISSUE_PEAK_TOPS, 5) if ach else None,
-                         # the kernel computes in packed 16-bit halves (v_pk_*, two DP cells per
-                         # lane-op) with 32-bit guards: its frac against the packed-16 peak too
-                         "arith": "int16x2 packed (v_pk_*), int32 guards and row-end state",
-                         "peak_pk16": round(2 * VALU_PEAK_TOPS, 1),
-                         "frac_pk16": round(ach / (2 * VALU_PEAK_TOPS), 5) if ach else None,
-                         "frac_denominator": "busy union of the kernel's launch intervals (since r04e; "
-                                             "r04d and earlier: summed launch durations)",
-                         "ops_per_cell": OPS_PER_CELL, "cells_per_step": round(cells_step),
-                         "cells_per_step_reference": round(cells_ref_step),
-                         # busy time: the union of the kernel's launch intervals in the timed steps
-                         # (HIP events on the launching streams), <= ms_per_step
-                         "kernel_ms_per_step": round(ext_busy_ms / args.steps, 4),
-                         "kernel_sum_ms_per_step": round(ext_ms / args.steps, 4), "launches_timed": ext_launches,
-                         "avg_launch_ms": round(ext_avg_ms, 4),
-                         # the kernel alone on the GPU (one stream, one batch at a time)
-                         "isolated_launch_ms": iso, "frac_isolated": round(frac_iso, 5) if frac_iso else None,
-                         "tasks_round_a_b": tasks_ab,
-                         "traffic": traffic, "traffic_source": traffic_src, "pmc": pmc,
-                         "alg_bytes_per_launch": round(ext_alg_bytes),
-                         "traffic_over_alg": round(traffic / ext_alg_bytes, 3) if traffic and ext_alg_bytes else None,
-                         "formula": "cells_per_step * ops_per_cell / kernel_ms_per_step (busy union) / peak "
-                                    "(DESIGN.md §5)",
-                         # the same ops over the step's wall time: the launches of the two caller
-                         # streams overlap and share the GPU (the kernel runs at 2 workgroups per CU)
-                         "frac_step": round(cells_step * OPS_PER_CELL / (elapsed / args.steps) / 1e12 / VALU_PEAK_TOPS, 5)},
-            "roofline_hbm": {"bound": "hbm", "achieved": round(alg_bytes / launch_s / 1e9, 3), "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(alg_bytes / launch_s / 1e9 / HBM_PEAK_GBS, 6),
-                             "alg_bytes_per_launch_sequence": round(alg_bytes), "launch_sequence_ms": round(launch_s * 1e3, 4),
-                             "kernel": "whole SW-stage launch sequence (all kernels of one batch)"},
-        }
-    if rank == 0 and world == 1 and not args.no_host_path:
-        result["host_buffer_path"] = host_path_rate(eng, batches, 24, checks, depth=args.host_slots)
+        result = headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapsed, total_reads,
+                               cells, cells_all, ext_ms, ext_launches, ext_busy_ms, parity)
+    regs0, n0 = dbs[0].results(0)
+    fix_checks = W.fixture if W.fixture else checks
+    if rank == 0 and world == 1 and W.fixture and W.ref_answers and not args.headline_only:
         try:  # a side line: a failure here must not cost the headline line
-            result["end_to_end"] = end_to_end_stage(opt, ref, batches, checks, chain_mode=1)
-            e2f = end_to_end_stage(opt, ref, batches, checks, chain_mode=0)
+            result["two_batch_fixture"] = fixture_figure(eng, W.fixture, dev, streams, args.steps)
+        except Exception as e:
+            result["two_batch_fixture"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_host_path:
+        # host buffers through submit/wait: every distinct batch once at least
+        result["host_buffer_path"] = host_path_rate(eng, batches, max(24, nb), checks, depth=args.host_slots)
+        try:  # a side line: a failure here must not cost the headline line
+            e2_batches = batches[:min(nb, 20)]
+            e2_checks = checks[:len(e2_batches)] if checks else None
+            reps = max(2, 40 // len(e2_batches))
+            result["end_to_end"] = end_to_end_stage(opt, ref, e2_batches, e2_checks, reps=reps, chain_mode=1)
+            e2f = end_to_end_stage(opt, ref, e2_batches, e2_checks, reps=reps, chain_mode=0)
             result["end_to_end"]["chains_forwarded"] = {k: e2f.get(k) for k in ("value", "ms_per_record",
                                                                                 "parity_last_rep", "chains", "error")
                                                         if k in e2f}
@@ -1150,8 +1414,8 @@ def main():
         except Exception as e:
             result["cigar_stage"] = {"error": repr(e)}
     # the whole-pipeline leg first: its harness builds the chr21-sized genome's
-    # bwa index (bench_data/e2e) on a fresh box, which the seeding and chaining
-    # legs then read
+    # bwa index (bench_data/e2e) on a fresh box when the stream has not, which
+    # the seeding and chaining legs then read
     if rank == 0 and world == 1 and not args.no_e2e:
         try:  # a side line: a failure here must not cost the headline line
             e2e = end_to_end_align(args.e2e_pairs)
@@ -1160,35 +1424,44 @@ def main():
         except Exception as e:
             result["end_to_end_align"] = {"error": repr(e)}
     seeding = None
+    fix_b0 = fix_checks[0].batch if fix_checks else dbs[0].b
     if rank == 0 and world == 1 and not args.no_seeding:
         try:  # a side line: a failure here must not cost the headline line
-            seeding = seeding_stage(eng, dbs[0].b)
+            seeding = seeding_stage(eng, fix_b0)
             if seeding is not None:
                 result["seeding_stage"] = {k: v for k, v in seeding.items() if k != "_check"}
         except Exception as e:
             result["seeding_stage"] = {"error": repr(e)}
-        if checks:
+        if fix_checks:
             try:  # a side line: a failure here must not cost the headline line
-                chaining = chaining_stage(eng, checks[0])
+                chaining = chaining_stage(eng, fix_checks[0])  # reference chains: the fixture's
                 if chaining is not None:
                     result["chaining_stage"] = chaining
             except Exception as e:
                 result["chaining_stage"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_regime:
         try:  # a side line: a failure here must not cost the headline line
-            result["regime_grch38"] = regime_stage(dev)
+            result["regime_grch38"] = regime_stage(dev, ext_form=args.ext_form)
         except Exception as e:
             result["regime_grch38"] = {"error": repr(e)}
-    if rank == 0 and world == 1 and not args.no_regime and args.workload == "c2_refseed":
+    if rank == 0 and world == 1 and not args.no_regime and args.workload != "synth":
         try:  # a side line: a failure here must not cost the headline line
-            result["c5_refseed"] = c5_refseed_stage(pac_t, ref, dev)
+            result["c5_refseed"] = c5_refseed_stage(pac_t, ref, dev, ext_form=args.ext_form)
         except Exception as e:
             result["c5_refseed"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_hwq4 and W.fixture:
+        try:  # a side line: a failure here must not cost the headline line
+            h4 = hw_queues_4_figure(args.steps, args.warmup, args.ext_form)
+            h16 = result.get("two_batch_fixture") or {}
+            h4["gpu_max_hw_queues_16_same_workload"] = h16.get("value")
+            result["hw_queues_4"] = h4
+        except Exception as e:
+            result["hw_queues_4"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu:
         if seeding is not None:
             try:
-                port = seeding_cpu_baseline(dbs[0].b, *seeding["_check"])
-                refb = ref_seeding_baseline(dbs[0].b, 0)
+                port = seeding_cpu_baseline(fix_b0, *seeding["_check"])
+                refb = ref_seeding_baseline(fix_b0, 0)
                 result["seeding_stage"]["cpu_baseline"] = refb if refb is not None else port
                 result["seeding_stage"]["parity_gpu_vs_cpu"] = port["parity_gpu_vs_cpu"]
                 if refb is not None:
@@ -1198,7 +1471,7 @@ def main():
                 result["seeding_stage"]["cpu_baseline"] = {"error": repr(e)}
         if "chaining_stage" in result and "error" not in result["chaining_stage"]:
             try:
-                refc = ref_seeding_baseline(dbs[0].b, 1)
+                refc = ref_seeding_baseline(fix_b0, 1)
                 if refc is not None:
                     ch = result["chaining_stage"]
                     refc["matches_gpu"] = refc["count"] == ch["chains"]
@@ -1206,7 +1479,10 @@ def main():
                     ch["speedup_vs_cpu_seqs2chains"] = round(ch["seqs2chains_Mreads_per_s"] / refc["value"], 2)
             except Exception as e:
                 result["chaining_stage"]["cpu_baseline"] = {"error": repr(e)}
-        cb = cpu_baseline(opt, ref, batches, args.cpu_budget, [d.results(0) for d in dbs], checks)
+        if W.ref_answers is not None:
+            cb = stream_cpu_baseline(opt, ref, batches, W.ref_answers)
+        else:
+            cb = cpu_baseline(opt, ref, batches, args.cpu_budget, [d.results(0) for d in dbs], checks)
         result["cpu_baseline"] = cb
         result["speedup_vs_cpu"] = round(result["value"] / cb["value"], 2)
         # the CPU side scaled linearly to every CPU of the host (optimistic for the CPU)
@@ -1229,6 +1505,29 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     eng.close()
+
+
+def stream_cpu_baseline(opt, ref, batches, ans) -> dict:
+    """the CPU baseline of the stream: the reference's mem_chain2aln already ran
+    over every batch on the host cores (reference_answers, before timing: it made
+    the expected regions), plus batch 0 again on one thread"""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    which = "ref" if ans["kind"] == "reference" else "oracle"
+    R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
+    t0 = time.perf_counter()
+    oracle.chain2aln(which, opt, R, batches[0], n_threads=1)
+    t1c = time.perf_counter() - t0
+    reads = sum(b.n_reads for b in batches)
+    return dict(value=reads / ans["chain2aln_s"] / 1e6, unit="Mreads/s", cores=ans["cores"], cpu=cpu_model(),
+                kind=ans["kind"], host_cpus=os.cpu_count(), value_1core=round(batches[0].n_reads / t1c / 1e6, 5),
+                sample_1core=f"batch 0 ({batches[0].n_reads} reads) on one thread, {t1c:.2f} s",
+                sample=f"every stream batch once ({len(batches)} distinct, {reads} reads), "
+                       f"{ans['chain2aln_s']:.2f} s wall on {ans['cores']} threads "
+                       f"({'oracle/_ref/libbwaref.so: the reference mem_chain2aln' if ans['kind'] == 'reference' else 'oracle/liboracle.so'}); "
+                       "its regions are the expected output every timed step is checked against",
+                reference_seqs2chains_s=round(ans["seqs2chains_s"], 3),
+                chains_identical_to_reference=ans["chains_identical"])
 
 
 if __name__ == "__main__":

@@ -231,9 +231,21 @@ class HostPool {
 };
 }  // namespace
 
+// threads that malloc the records' mem_alnreg_v (unpack_dense):
+// BWAGPU_UNPACK_THREADS, default host_threads().  Every region array is freed
+// later by another stage's threads (RegionsToSam), so each malloc takes a chunk
+// a remote free put back into its arena; more threads are not always faster
+int unpack_threads() {
+  static const int n = [] {
+    const char* e = getenv("BWAGPU_UNPACK_THREADS");
+    return std::max(1, std::min(e ? atoi(e) : host_threads(), host_threads()));
+  }();
+  return n;
+}
+
 template <typename F>
-static void parallel_ranges(int n, F f) {  // f(begin, end) over [0, n) in host_threads() pieces
-  const int t = std::min(host_threads(), std::max(1, n / 2048));
+static void parallel_ranges(int n, F f, int max_t = 0) {  // f(begin, end) over [0, n) in <= max_t pieces
+  const int t = std::min(max_t > 0 ? max_t : host_threads(), std::max(1, n / 2048));
   if (t <= 1) {
     f(0, n);
     return;
@@ -319,17 +331,26 @@ void FlatBatch::pack(const ChainsRecord& rec) {
 
 int FlatBatch::pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec) {
   const int nr = rec.batch_num;
-  // pass 1: per-read counts -> offsets (kept here: unpack needs them)
+  // pass 1, on the pool: per-read counts (bases, chains, seeds) in place, then
+  // their prefix sums -> offsets (kept here: unpack needs them).  Reading every
+  // chain's seed count is a pointer chase per read; serial it cost ~1 ms a record
   seq_off.assign((size_t)nr + 1, 0);
   read_chain_off.assign((size_t)nr + 1, 0);
-  std::vector<int64_t> seed_base((size_t)nr + 1, 0);
+  seed_base.assign((size_t)nr + 1, 0);
+  parallel_ranges(nr, [&](int r0, int r1) {
+    for (int i = r0; i < r1; ++i) {
+      const mem_chain_v& cv = rec.chains[i];
+      int64_t ns = 0;
+      for (size_t j = 0; j < cv.n; ++j) ns += cv.a[j].n;
+      seq_off[i + 1] = rec.seqs[i].l_seq;
+      read_chain_off[i + 1] = (int32_t)cv.n;
+      seed_base[i + 1] = ns;
+    }
+  });
   for (int i = 0; i < nr; ++i) {
-    const mem_chain_v& cv = rec.chains[i];
-    int64_t ns = 0;
-    for (size_t j = 0; j < cv.n; ++j) ns += cv.a[j].n;
-    seq_off[i + 1] = seq_off[i] + rec.seqs[i].l_seq;
-    read_chain_off[i + 1] = read_chain_off[i] + (int32_t)cv.n;
-    seed_base[i + 1] = seed_base[i] + ns;
+    seq_off[i + 1] += seq_off[i];
+    read_chain_off[i + 1] += read_chain_off[i];
+    seed_base[i + 1] += seed_base[i];
   }
   const int32_t nc = read_chain_off[nr];
   const int64_t ns = seed_base[nr];
@@ -346,9 +367,9 @@ int FlatBatch::pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec)
   memcpy(v_so, seq_off.data(), sizeof(int64_t) * ((size_t)nr + 1));
   memcpy(v_rco, read_chain_off.data(), sizeof(int32_t) * ((size_t)nr + 1));
   v_cso[0] = 0;
-  chain_seed_off.resize((size_t)nc + 1);
-  chain_seed_off[0] = 0;
-  // pass 2: every read's bases, chains and seeds, in place in pinned memory
+  // pass 2: every read's bases, chains and seeds, in place in pinned memory;
+  // mem_seed_t and bwagpu_seed_t are the same 24 bytes (records.h), so a
+  // chain's seeds go in one copy
   parallel_ranges(nr, [&](int r0, int r1) {
     for (int i = r0; i < r1; ++i) {
       const bseq1_t& s = rec.seqs[i];
@@ -360,17 +381,9 @@ int FlatBatch::pack_staged(bwagpu_ctx_t* ctx, int slot, const ChainsRecord& rec)
         const size_t ci = (size_t)read_chain_off[i] + j;
         v_rid[ci] = ch.rid;
         v_fr[ci] = ch.frac_rep;
-        for (int k = 0; k < ch.n; ++k) {
-          bwagpu_seed_t& t = v_sd[(size_t)so + k];
-          t.rbeg = ch.seeds[k].rbeg;
-          t.qbeg = ch.seeds[k].qbeg;
-          t.len = ch.seeds[k].len;
-          t.score = ch.seeds[k].score;
-          t.pad_ = 0;
-        }
+        if (ch.n > 0) memcpy(v_sd + so, ch.seeds, sizeof(bwagpu_seed_t) * (size_t)ch.n);
         so += ch.n;
         v_cso[ci + 1] = (int32_t)so;
-        chain_seed_off[ci + 1] = (int32_t)so;
       }
     }
   });
@@ -396,7 +409,7 @@ mem_alnreg_v* FlatBatch::unpack_dense(const bwagpu_alnreg_t* rg, const int32_t* 
         memcpy(av[i].a, &rg[off[i]], sizeof(mem_alnreg_t) * k);
       }
     }
-  });
+  }, unpack_threads());
   if (oom) throw std::runtime_error("Memory allocation failed");
   return av;
 }

@@ -80,6 +80,7 @@ struct FlatBatch {
   std::vector<bwagpu_seed_t> seeds;
   std::vector<bwagpu_alnreg_t> regs;  // output slots (one per seed)
   std::vector<int32_t> n;             // regions per read
+  std::vector<int64_t> seed_base;     // pack_staged: each read's first seed
   bwagpu_batch_t c{};
 
   void pack(const ChainsRecord& rec);  // ~ packReadData (FPGAPipeline.cpp:194-343)

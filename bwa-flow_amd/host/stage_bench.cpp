@@ -12,6 +12,7 @@
 // The records are built before the clock starts (that is SeqsToChains' work).
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 
 #include <chrono>
 #include <thread>
@@ -101,7 +102,9 @@ extern "C" {
 // totals (pack, submit, wait, post; summed over workers), times[5] = records
 // on the GPU, times[6] = records the CPU fallback took, times[7] = stage
 // workers (contexts) used, times[8..9] = device kernels / H2D + results (HIP
-// events, summed over the GPU records).  The regions of the LAST rep of batch
+// events, summed over the GPU records), times[10..11] = the process's user /
+// system CPU seconds over the timed run (getrusage: every thread's, the sink's
+// and the chain frees' included).  The regions of the LAST rep of batch
 // k go to out_n[k][r] / out_regs[k] (compact, read order).  Returns 0, or the
 // number of records whose chains were not where the mode puts them.  A
 // warm-up pass of min(reps, 2) x n_batches records runs first, untimed.
@@ -161,6 +164,8 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
       }
       t_end = std::chrono::steady_clock::now();
     });
+    struct rusage ru0;
+    getrusage(RUSAGE_SELF, &ru0);
     const auto t0 = std::chrono::steady_clock::now();
     auto* in = pipe.input<ChainsRecord>();
     for (auto& r : recs) in->push(r);
@@ -168,7 +173,12 @@ int gpustage_run(const bwagpu_opt_t* opt, const bwagpu_bns_t* bns, const uint8_t
     consumer.join();
     pipe.wait();  // the workers are done, and the last one drained the stage's chain frees
     t_end = std::max(t_end, std::chrono::steady_clock::now());
+    struct rusage ru1;
+    getrusage(RUSAGE_SELF, &ru1);
+    auto secs = [](const timeval& a, const timeval& b) { return (double)(b.tv_sec - a.tv_sec) + 1e-6 * (double)(b.tv_usec - a.tv_usec); };
     if (t) {
+      t[10] = secs(ru0.ru_utime, ru1.ru_utime);
+      t[11] = secs(ru0.ru_stime, ru1.ru_stime);
       t[0] = std::chrono::duration<double>(t_end - t0).count();
       stage.phase_seconds(t + 1);
       t[5] = stage.records_on_gpu();

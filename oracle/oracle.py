@@ -121,6 +121,41 @@ def chain2aln(which: str, opt: dict, ref: Ref, batch: Batch, n_threads: int = 1)
     return regs[:batch.n_seeds], n[:batch.n_reads], st
 
 
+def ref_seqs2chains(prefix: str, seq_off, seq, n_threads: int = 1):
+    """the REFERENCE's SeqsToChains (mem_chain -> mem_chain_flt ->
+    mem_flt_chained_seeds, src/bwa_wrapper.cpp:105-115) over a batch of reads
+    against the bwa index at `prefix` (oracle/_ref/libbwaref.so
+    ref_seqs2chains_batch) -> (read_chain_off, chain_rid, chain_frac_rep,
+    chain_seed_off, seeds) in the bwagpu_batch_t layout"""
+    lib = ref_lib()
+    if lib is None:
+        raise RuntimeError("oracle/_ref/libbwaref.so not available")
+    fn = lib.ref_seqs2chains_batch
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_char_p, C.c_int32, _VP, _VP, C.c_int, _VP, C.c_int64, _VP, _VP, _VP, C.c_int64, _VP,
+                   C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    seq_off = np.ascontiguousarray(seq_off, np.int64)
+    seq = np.ascontiguousarray(seq, np.uint8)
+    n = len(seq_off) - 1
+    cap_c, cap_s = 4 * n + 16, 16 * n + 64
+    while True:
+        rco = np.zeros(n + 1, np.int32)
+        rid = np.zeros(cap_c, np.int32)
+        fr = np.zeros(cap_c, np.float32)
+        cso = np.zeros(cap_c + 1, np.int32)
+        sd = np.zeros(cap_s, abi.SEED_DTYPE)
+        nc, ns = C.c_int64(), C.c_int64()
+        rc = fn(prefix.encode(), n, _ptr(seq_off), _ptr(seq), int(n_threads), _ptr(rco), cap_c, _ptr(rid), _ptr(fr),
+                _ptr(cso), cap_s, _ptr(sd), C.byref(nc), C.byref(ns))
+        if rc == -2:
+            cap_c, cap_s = int(nc.value) + 16, int(ns.value) + 64
+            continue
+        if rc != 0:
+            raise RuntimeError(f"ref_seqs2chains_batch rc={rc} (index {prefix})")
+        c, k = int(nc.value), int(ns.value)
+        return rco, rid[:c], fr[:c], cso[:c + 1], sd[:k]
+
+
 def extend(which: str, opt: dict, tasks, qpool, tpool):
     o = abi.opt_from_dict(opt)
     tasks = np.ascontiguousarray(tasks, abi.EXT_TASK_DTYPE)

@@ -286,6 +286,7 @@ typedef struct {
   volatile int next;
   pthread_mutex_t mu;
   int64_t count;
+  ref_chain_v *keep; /* mode 2: every read's chains, kept for the caller */
 } sjob_t;
 
 static void *sworker(void *arg)
@@ -311,6 +312,10 @@ static void *sworker(void *arg)
         c.n = mem_chain_flt(j->opt, (int)c.n, c.a);
         mem_flt_chained_seeds(j->opt, g_idx->bns, g_idx->pac, len, q, (int)c.n, c.a);
         cnt += (int64_t)c.n;
+        if (j->mode == 2) {
+          j->keep[r] = c;
+          continue;
+        }
         for (size_t k = 0; k < c.n; ++k) free(c.a[k].seeds);
         free(c.a);
       }
@@ -324,22 +329,28 @@ static void *sworker(void *arg)
   return 0;
 }
 
-double ref_seeding_bench(const char *prefix, int mode, int32_t n_reads, const int64_t *seq_off, const uint8_t *seq,
-                         int n_threads, int reps, int64_t *out_count)
+static int load_index(const char *prefix)
 {
   if (!g_idx || strcmp(prefix, g_prefix) != 0) {
     if (g_idx) bwa_idx_destroy(g_idx);
     bwa_verbose = 1;
     g_idx = bwa_idx_load(prefix, BWA_IDX_ALL);
-    if (!g_idx) return -1.0;
+    if (!g_idx) return -1;
     snprintf(g_prefix, sizeof g_prefix, "%s", prefix);
   }
+  return 0;
+}
+
+double ref_seeding_bench(const char *prefix, int mode, int32_t n_reads, const int64_t *seq_off, const uint8_t *seq,
+                         int n_threads, int reps, int64_t *out_count)
+{
+  if (load_index(prefix) < 0) return -1.0;
   mem_opt_t *opt = mem_opt_init();
   struct timeval a, b;
   gettimeofday(&a, 0);
   int64_t count = 0;
   for (int rep = 0; rep < reps; ++rep) {
-    sjob_t j = {opt, mode, n_reads, seq_off, seq, 0, PTHREAD_MUTEX_INITIALIZER, 0};
+    sjob_t j = {opt, mode == 2 ? 1 : mode, n_reads, seq_off, seq, 0, PTHREAD_MUTEX_INITIALIZER, 0, 0};
     pthread_t th[256];
     const int nt = n_threads < 1 ? 1 : n_threads > 256 ? 256 : n_threads;
     for (int t = 0; t < nt; ++t) pthread_create(&th[t], 0, sworker, &j);
@@ -350,4 +361,60 @@ double ref_seeding_bench(const char *prefix, int mode, int32_t n_reads, const in
   free(opt);
   if (out_count) *out_count = count;
   return (b.tv_sec - a.tv_sec) + 1e-6 * (b.tv_usec - a.tv_usec);
+}
+
+/* The reference's SeqsToChains (mem_chain -> mem_chain_flt ->
+   mem_flt_chained_seeds, src/bwa_wrapper.cpp:105-115, default mem_opt_t) over
+   a batch of reads on n_threads, its chains flattened in read order into the
+   bwagpu_batch_t layout (chain_rid / chain_frac_rep / chain_seed_off / seeds).
+   The checker of bench.py's C2 stream, whose chains the device makes
+   (bwagpu_seqs2chains).  Returns 0; -1 when the index does not load; -2 when
+   cap_chains / cap_seeds are too small (*n_chains / *n_seeds: what is needed). */
+int ref_seqs2chains_batch(const char *prefix, int32_t n_reads, const int64_t *seq_off, const uint8_t *seq,
+                          int n_threads, int32_t *read_chain_off, int64_t cap_chains, int32_t *chain_rid,
+                          float *chain_frac_rep, int32_t *chain_seed_off, int64_t cap_seeds, bwagpu_seed_t *seeds,
+                          int64_t *n_chains, int64_t *n_seeds)
+{
+  if (load_index(prefix) < 0) return -1;
+  mem_opt_t *opt = mem_opt_init();
+  ref_chain_v *keep = (ref_chain_v *)calloc(n_reads > 0 ? n_reads : 1, sizeof(ref_chain_v));
+  sjob_t j = {opt, 2, n_reads, seq_off, seq, 0, PTHREAD_MUTEX_INITIALIZER, 0, keep};
+  pthread_t th[256];
+  const int nt = n_threads < 1 ? 1 : n_threads > 256 ? 256 : n_threads;
+  for (int t = 0; t < nt; ++t) pthread_create(&th[t], 0, sworker, &j);
+  for (int t = 0; t < nt; ++t) pthread_join(th[t], 0);
+  int64_t nc = 0, ns = 0;
+  for (int32_t r = 0; r < n_reads; ++r) {
+    nc += (int64_t)keep[r].n;
+    for (size_t k = 0; k < keep[r].n; ++k) ns += keep[r].a[k].n;
+  }
+  int rc = 0;
+  if (nc > cap_chains || ns > cap_seeds) {
+    rc = -2;
+  } else {
+    int64_t c = 0, s = 0;
+    read_chain_off[0] = 0;
+    chain_seed_off[0] = 0;
+    for (int32_t r = 0; r < n_reads; ++r) {
+      for (size_t k = 0; k < keep[r].n; ++k, ++c) {
+        const ref_chain_t *ch = &keep[r].a[k];
+        chain_rid[c] = ch->rid;
+        chain_frac_rep[c] = ch->frac_rep;
+        memcpy(seeds + s, ch->seeds, sizeof(bwagpu_seed_t) * (size_t)ch->n);
+        for (int i = 0; i < ch->n; ++i) seeds[s + i].pad_ = 0;
+        s += ch->n;
+        chain_seed_off[c + 1] = (int32_t)s;
+      }
+      read_chain_off[r + 1] = (int32_t)c;
+    }
+  }
+  for (int32_t r = 0; r < n_reads; ++r) {
+    for (size_t k = 0; k < keep[r].n; ++k) free(keep[r].a[k].seeds);
+    free(keep[r].a);
+  }
+  free(keep);
+  free(opt);
+  *n_chains = nc;
+  *n_seeds = ns;
+  return rc;
 }

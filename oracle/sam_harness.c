@@ -791,7 +791,7 @@ static void feeder_done(feeder_t *f)
 int main(int argc, char *argv[])
 {
   if (argc < 7) {
-    fprintf(stderr, "usage: sam_harness <ref|split|gpu> <workdir> <out.sam> <seed> <n_pairs> <150|100|250|mix> "
+    fprintf(stderr, "usage: sam_harness <ref|split|gpu|index> <workdir> <out.sam> <seed> <n_pairs> <150|100|250|mix> "
                     "[batch_bases] [threads] [genome_len]\n");
     return 1;
   }
@@ -806,7 +806,9 @@ int main(int argc, char *argv[])
   const int is_seed = is_chain || !strcmp(mode, "gpuseed");
   const int is_sam = is_seed || !strcmp(mode, "gpusam"), is_gpu = is_sam || !strcmp(mode, "gpu"),
             is_ref = !strcmp(mode, "ref");
-  if (!is_gpu && !is_ref && strcmp(mode, "split")) { fprintf(stderr, "unknown mode %s\n", mode); return 1; }
+  /* index: build (or find, by its stamp) the genome's bwa index in <workdir> and stop */
+  const int is_index = !strcmp(mode, "index");
+  if (!is_gpu && !is_ref && !is_index && strcmp(mode, "split")) { fprintf(stderr, "unknown mode %s\n", mode); return 1; }
   if (is_gpu) gpu_load();
   if (is_sam) gpusam_load();
 
@@ -847,6 +849,7 @@ int main(int argc, char *argv[])
     sf = fopen(stamp, "w");
     if (sf) { fputs(want, sf); fclose(sf); }
   }
+  if (is_index) { free(g); return 0; }
   bwaidx_t *idx = bwa_idx_load(fa, BWA_IDX_ALL);
   if (!idx) { fprintf(stderr, "index load failed\n"); return 1; }
   { /* every mode starts with the index's pages resident (outside the timed part) */

@@ -2,7 +2,9 @@
 group standing in for RCCL.  bench.py's data path has exactly one
 collective — the start-up broadcast of the packed reference + contig table
 from rank 0 — and the whole-job totals (max time, summed
-reads) at the end; shards are independent (weak scaling)."""
+reads) at the end; shards are independent (weak scaling): rank r takes the
+stream's global batches r, r + N, ... (the reference's pull-scatter,
+src/mpi/MPIChannel.cpp:140-200)."""
 import os
 import socket
 import sys
@@ -66,7 +68,8 @@ def _worker_fixture(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     args = argparse.Namespace(workload="c2_refseed")
-    opt, ref, pac_t, batches, checks, data, wl = bench.load_workload(args, rank, world, torch.device("cpu"))
+    W = bench.load_workload(args, rank, world, torch.device("cpu"))
+    ref, batches, checks = W.ref, W.batches, W.checks
     # a 195-contig table (the GRCh38 layout) through the same broadcast
     from bwagpu.synth import _load
     import ctypes as C
@@ -110,3 +113,56 @@ def test_shards_are_deterministic():
     a = bench.rank_reads(ref, 1, 200, 150)
     b = bench.rank_reads(ref, 1, 200, 150)
     assert np.array_equal(a.seq, b.seq) and np.array_equal(a.seeds, b.seeds)
+
+
+def test_stream_shards_partition_the_stream():
+    """bench.shard_ids: for every world size the ranks' shards are disjoint and
+    their union is exactly the stream's first world * per_rank batches"""
+    import bench
+    for world in (1, 2, 3, 4, 8):
+        for per in (1, 2, 15, 30):
+            shards = [bench.shard_ids(r, world, per) for r in range(world)]
+            flat = [g for sh in shards for g in sh]
+            assert len(flat) == len(set(flat)) == world * per
+            assert sorted(flat) == list(range(world * per))
+            assert all(len(sh) == per for sh in shards)
+
+
+def _worker_stream(rank, world, port, out_dir):
+    """each rank draws the reads of its own stream shard (bench.stream_reads)
+    on the broadcast genome; rank 0 gathers which global batches were made"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    ref, _ = bench.shared_reference(400_000, 3, rank, world, torch.device("cpu"))
+    gids = bench.shard_ids(rank, world, 3)
+    digests = {g: __import__("hashlib").sha256(bench.stream_reads(ref, g, 300).seq.tobytes()).hexdigest()
+               for g in gids}
+    got = [None] * world
+    dist.all_gather_object(got, digests)
+    if rank == 0:
+        import json
+        json.dump(got, open(os.path.join(out_dir, "stream.json"), "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_stream_shards_gloo(tmp_path):
+    """world_size 2: the shards the two ranks generate are disjoint, their union
+    is the whole stream, and each batch is the one a single process makes for
+    the same global index (the stream does not depend on the world size)"""
+    import json
+    import hashlib
+    import bench
+    from bwagpu.synth import SynthRef
+    world = 2
+    mp.spawn(_worker_stream, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = json.load(open(os.path.join(tmp_path, "stream.json")))
+    ids = [int(g) for d in got for g in d]
+    assert sorted(ids) == list(range(6)) and len(set(ids)) == 6
+    assert set(int(g) for g in got[0]) == {0, 2, 4} and set(int(g) for g in got[1]) == {1, 3, 5}
+    ref = SynthRef(42, 400_000, 3)
+    merged = {int(g): h for d in got for g, h in d.items()}
+    for g in range(6):
+        assert merged[g] == hashlib.sha256(bench.stream_reads(ref, g, 300).seq.tobytes()).hexdigest()
+    assert len(set(merged.values())) == 6

@@ -85,3 +85,73 @@ def test_two_rank_shards_merge_to_single_rank(tmp_path):
     assert all(o > 0 for o in owners)  # both ranks processed records
     assert np.array_equal(n, want_n)
     assert G.region_mismatch(regs, want_regs) is None
+
+
+def _worker_stream(rank, world, port, out_dir):
+    """bench.py's stream path on one GPU with two ranks: rank r takes global
+    batches r, r + 2 (bench.shard_ids), makes their chains with the device's
+    SeqsToChains (bench.stream_batches) and their regions with the device's
+    ChainsToRegions, and checks both against the oracle restatement (chains:
+    oracle/chain.c, pinned by the reference's chain dumps; regions: the
+    oracle's mem_chain2aln); rank 0 gathers every batch's regions"""
+    for p in (os.path.join(REPO, "bwa-flow_amd", "python"), os.path.join(REPO, "tests"), REPO,
+              os.path.join(REPO, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import hashlib
+    import bench
+    import golden_io as G
+    import oracle
+    from bwagpu import abi
+    from bwagpu.engine import Engine, compact
+    dev = torch.device("cuda:0")
+    refd = G.load_ref() if rank == 0 else None
+
+    class Src:
+        pass
+    if rank == 0:
+        Src.l_pac, Src.pac, Src.ann_offset, Src.ann_len = refd["l_pac"], refd["pac"], refd["ann_offset"], refd["ann_len"]
+    ref, pac_t = bench.broadcast_reference(Src if rank == 0 else None, rank, world, torch.device("cpu"))
+    pac_d = torch.from_numpy(np.ascontiguousarray(ref.pac)).to(dev)
+    hdr, words = G.load_seed_bwt()
+    sa_intv, sa, _, _ = G.load_seed_sa()
+    opt = abi.default_opt()
+    gids = bench.shard_ids(rank, world, 2)
+    batches, _ = bench.stream_batches(dev, opt, ref, pac_d, (hdr, words, sa, sa_intv), gids, pairs=400)
+    R = oracle.Ref(ref.l_pac, ref.ann_offset, ref.ann_len, ref.pac)
+    eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
+    mine, ok = {}, True
+    for g, b in zip(gids, batches):
+        rco, ch, cso, sd = oracle.seqs2chains(opt, abi.default_chainopt(), np.array([19, 10, 20], np.int32), 1.5, R,
+                                              None, hdr, words, sa, sa_intv, b.seq_off, b.seq)
+        ok &= bool(np.array_equal(rco, b.read_chain_off) and np.array_equal(cso, b.chain_seed_off) and
+                   np.array_equal(ch["rid"], b.chain_rid) and
+                   all(np.array_equal(sd[f], b.seeds[f]) for f in ("rbeg", "qbeg", "len", "score")))
+        regs, n = eng.chain2aln(b)
+        oregs, on, _ = oracle.chain2aln("oracle", opt, R, b)
+        got = compact(b, regs, n)
+        ok &= bool(np.array_equal(n, on) and np.array_equal(got.view(np.uint8), compact(b, oregs, on).view(np.uint8)))
+        mine[g] = hashlib.sha256(got.view(np.uint8).tobytes()).hexdigest()
+    eng.close()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (mine, ok))
+    if rank == 0:
+        import json
+        json.dump(gathered, open(os.path.join(out_dir, "stream.json"), "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_stream_shards(tmp_path):
+    """the shards are disjoint, cover the stream, and every batch's chains and
+    regions equal the oracle's on whichever rank ran it"""
+    import json
+    world = 2
+    mp.spawn(_worker_stream, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = json.load(open(os.path.join(tmp_path, "stream.json")))
+    ids = [int(g) for mine, _ in got for g in mine]
+    assert sorted(ids) == [0, 1, 2, 3]
+    assert all(ok for _, ok in got)
+    assert len({h for mine, _ in got for h in mine.values()}) == 4
