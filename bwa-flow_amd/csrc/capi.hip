@@ -181,7 +181,7 @@ struct Slot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
-  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks;
+  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks, d_ftask;
   SpecStreams spec;  // created on first use (choose_side)
   bool side_chosen = false;
   void release_scratch() {
@@ -191,6 +191,7 @@ struct Slot {
     d_qh.release();
     d_sorth.release();
     d_stasks.release();
+    d_ftask.release();
     if (spec.side) (void)hipStreamSynchronize(spec.side);
     if (spec.side) (void)hipStreamDestroy(spec.side);
     if (spec.fork) (void)hipEventDestroy(spec.fork);
@@ -878,6 +879,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_sorth.ensure(sizeof(int32_t) * kSortWords), "hipMalloc(sorth)");
   HIPC(hipMemsetAsync(s.d_sorth.p, 0, sizeof(int32_t) * kSortWords, st), "memset sorth");
   HIPC(s.d_stasks.ensure(sizeof(int2) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(stasks)");
+  HIPC(s.d_ftask.ensure(sizeof(FatTask) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(ftask)");
   // pair matrices of heavy reads: sum over them of 2 * ns * ceil(ns / 64) words,
   // <= 2 * ns_total * (1 + ns_max / 64); reads that do not fit take the per-seed kernel
   const int64_t mat_words = std::max<int64_t>(1 << 20, 16 * (int64_t)ns);
@@ -907,6 +909,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.qh = s.d_qh.as<int32_t>();
   a.sorth = s.d_sorth.as<int32_t>();
   a.stasks = s.d_stasks.as<int2>();
+  a.ftask = s.d_ftask.as<FatTask>();
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;
@@ -1811,6 +1814,25 @@ int bwagpu_debug_fail_wait(bwagpu_ctx_t* ctx, int after_n_waits, int code) {
   return BWAGPU_OK;
 }
 
+
+int bwagpu_debug_occupancy(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
+  if (!ctx || !out) return BWAGPU_E_INVAL;
+  HIPC(hipSetDevice(ctx->device), "hipSetDevice");
+  hipStream_t st = (hipStream_t)stream;
+  if (!st) HIPC(lazy_stream(ctx->slot[0], &st), "hipStreamCreate");
+  int k = 0;
+  while (k < BWAGPU_NUM_SLOTS && ctx->dev_stream[k] != st) ++k;
+  if (k == BWAGPU_NUM_SLOTS || !ctx->dev_scratch[k].d_ctr.p) return fail(ctx, BWAGPU_E_INVAL, "no device-entry batch on this stream");
+  HIPC(hipStreamSynchronize(st), "hipStreamSynchronize");
+  int32_t c[SPC_WORDS];
+  HIPC(hipMemcpy(c, ctx->dev_scratch[k].d_ctr.p, sizeof c, hipMemcpyDeviceToHost), "hipMemcpy(ctr)");
+  memcpy(out, c + 32, 8 * sizeof(int64_t));
+#ifdef BWAGPU_OCC_DIAG
+  return BWAGPU_OK;
+#else
+  return fail(ctx, BWAGPU_E_UNSUPPORTED, "built without BWAGPU_OCC_DIAG");
+#endif
+}
 
 int bwagpu_debug_spec_counters(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   if (!ctx || !out) return BWAGPU_E_INVAL;

@@ -178,6 +178,19 @@ __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_se
   return round == 0 ? (size_t)bin * n_chains
                     : (size_t)kSpecBins * n_chains + ((size_t)(round - 1) * kSpecBins + bin) * n_seeds;
 }
+// An extension task of the first two length bins with everything its start
+// needs (spec_sort_scatter writes it beside stasks): the packed kernels read
+// one 32-byte record per claimed task instead of the chain list entry -> seed,
+// window, owner read -> read offsets (three dependent round trips), and read it
+// one generation ahead (spec_ext4_kernel)
+struct FatTask {
+  int64_t rbeg, qoff;  // the seed's rbeg, its read's first base in DevBatch::seq
+  int32_t pos;         // the seed's slot (SeedExt output)
+  int32_t dlo, dhi;    // its chain's window: [rbeg - dlo, rbeg + dhi)
+  uint32_t qls;        // qbeg | len << 10 | lq << 20 (each <= BWAGPU_MAX_READ_LEN)
+};
+static_assert(sizeof(FatTask) == 32, "FatTask layout");
+static_assert(BWAGPU_MAX_READ_LEN < 1024, "FatTask packs qbeg / len / lq in 10 bits each");
 struct SpecArgs {
   int lq_bound;               // reads longer than this set ERR_LEN and are skipped
   ChainWin* win;              // per chain
@@ -201,6 +214,7 @@ struct SpecArgs {
   int32_t* qh;                // kQHWords: sharded queue heads of the extension task lists
   int32_t* sorth;             // kSortWords, zeroed per batch: per (round, bin < 2) key histograms / cursors
   int2* stasks;               // the C = 3 / 4 lists sorted by key (same offsets as tasks), for the pair kernel
+  FatTask* ftask;             // the same lists as FatTask records (the packed kernels)
   bwagpu_alnreg_t* out;
   int32_t* out_n;
   int64_t* stats;

@@ -1270,7 +1270,10 @@ struct ShardQ {
     while (tried < 8) {
       cap = n > shard ? (n - shard + 7) >> 3 : 0;
       int32_t* h = heads + shard * kQHStride;
-      if (__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cap) {
+      // the wave's own shard is claimed from at once (one round trip); an
+      // exhausted head only grows past cap.  Other shards are read first, so
+      // that waves that have run dry do not hammer every head with atomics
+      if (tried == 0 || __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cap) {
         int v = 0;
         if ((threadIdx.x & 63) == 0) v = atomicAdd(h, K);
         v = __builtin_amdgcn_readfirstlane(__shfl(v, 0, 64));

@@ -511,6 +511,74 @@ __device__ __forceinline__ void qtask_start(QTask& t, const DevOpt& o, const Dev
   t.cells = t.rows = t.calls = 0;
 }
 
+#ifdef BWAGPU_OCC_DIAG
+// Occupancy of one extend_quad generation (a diagnostic build's counters,
+// bwagpu_debug_occupancy): the wave runs rows until its longest call ends and
+// CPL x G columns per call for its longest query; of those call-slot cells,
+// the ones of calls that already ended, the ones beyond a live call's query,
+// outside ksw's band, and the cells computed.  int64 counters at ctr words
+// 32..47: generations, rows run, call-slot rows, live call rows, slot cells,
+// live slot cells, query cells, computed cells.
+template <int G>
+__device__ __forceinline__ void occ_diag(const SpecArgs& a, const QCall& ca, const QCall& cb, const Tally32& ta,
+                                         const Tally32& tb) {
+  int qm = 0, rm = 0;
+  long long lr = 0, lq = 0, cc = 0;
+#pragma unroll
+  for (int g = 0; g < 64; g += G) {
+    const int qa = __builtin_amdgcn_readlane(ca.qlen, g), qb = __builtin_amdgcn_readlane(cb.qlen, g);
+    const int ra = __builtin_amdgcn_readlane(ta.rows, g), rb = __builtin_amdgcn_readlane(tb.rows, g);
+    qm = max(qm, max(qa, qb));
+    rm = max(rm, max(ra, rb));
+    lr += ra + rb;
+    lq += (long long)ra * (qa + 1) + (long long)rb * (qb + 1);
+    cc += __builtin_amdgcn_readlane(ta.cells, g) + __builtin_amdgcn_readlane(tb.cells, g);
+  }
+  const int cpl = (qm + G) / G;
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(a.ctr + 32);
+    atomicAdd(c + 0, 1ull);
+    atomicAdd(c + 1, (unsigned long long)rm);
+    atomicAdd(c + 2, (unsigned long long)rm * (2 * 64 / G));
+    atomicAdd(c + 3, (unsigned long long)lr);
+    atomicAdd(c + 4, (unsigned long long)rm * 128ull * cpl);
+    atomicAdd(c + 5, (unsigned long long)lr * G * cpl);
+    atomicAdd(c + 6, (unsigned long long)lq);
+    atomicAdd(c + 7, (unsigned long long)cc);
+  }
+}
+#endif
+
+// the same from the task's FatTask record (spec_sort_scatter)
+template <int G>
+__device__ __forceinline__ void qtask_start_fat(QTask& t, const DevOpt& o, const DevRef& ref, const FatTask& f,
+                                                uint8_t* tl, uint8_t* tr) {
+  t.pos = f.pos;
+  t.rbeg = f.rbeg;
+  t.wlo = f.rbeg - f.dlo;
+  t.whi = f.rbeg + f.dhi;
+  t.qoff = f.qoff;
+  t.qbeg = (int)(f.qls & 1023u);
+  t.len = (int)((f.qls >> 10) & 1023u);
+  t.lq = (int)(f.qls >> 20);
+  const int qlenL = t.qbeg, qlenR = t.lq - (t.qbeg + t.len);
+  const int64_t x0R = t.rbeg + t.len;
+  fill_two_half<G>(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, f.dlo, o.w << 1, o.pen_clip5) : 0, tr, x0R,
+                   qlenR ? rows_needed(o, qlenR, (int)(t.whi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
+  t.phase = qlenL != 0 ? 0 : (qlenR != 0 ? 2 : 4);
+  const int sc = qlenL != 0 ? -1 : t.len * o.a;  // bwamem.c:753
+  t.score = sc;
+  t.truesc = sc;
+  t.qb = 0;
+  t.qe = t.lq;
+  t.sc0 = 0;
+  t.aw0 = o.w;
+  t.aw1 = o.w;
+  t.rb = t.rbeg;
+  t.re = t.rbeg + t.len;
+  t.cells = t.rows = t.calls = 0;
+}
+
 // the ksw_extend2 call of the task's phase (0/1: left try 0/1, 2/3: right)
 __device__ __forceinline__ QCall qtask_call(QTask& t, const DevOpt& o, const uint8_t* seq, const uint8_t* tl,
                                             const uint8_t* tr) {
@@ -643,6 +711,13 @@ __device__ __forceinline__ QTask qload(LdsQ* p) {
 // Extension tasks of one list (in pair order, spec_sort_*), two per G-lane
 // group: four (G = 32) or eight (G = 16) per wave.
 // PMAX = the bin's largest CPL: ceil(read length / G).
+// Every sub-slot keeps its NEXT task's FatTask record in registers, claimed and
+// loaded one generation ahead: the loads run while the current generation's
+// DP runs (the row loop has no global memory operation), so a sub-slot whose
+// task ends starts the next at once — only its target rows (fill_two_half)
+// are fetched at the call boundary.  At one wave per SIMD nothing else hides a
+// generation start's dependent loads (the claim, the task entry, its seed,
+// window and read).
 template <int G, int PMAX, bool K8>
 __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
                                                            int tb_bytes) {
@@ -658,32 +733,46 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
   LdsQ* const qa = (LdsQ*)(tbr + tb_bytes);
   LdsQ* const qb = (LdsQ*)(tbr + tb_bytes + kQTaskLds);
   const int n = uni(__hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const int2* tl = a.stasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  const FatTask* fl = a.ftask + spec_list_off(list, b.n_chains, b.n_seeds);
   ShardQ qq;
   qq.init(a.qh + 8 * kQHStride * list, n);
-  bool ha = false, hb = false, more = n > 0;
+  // ha / hb: the sub-slot has a task (state parked in LDS); pa / pb: its next
+  // task's record (fa / fb) is claimed and loaded (or in flight)
+  bool ha = false, hb = false, pa = false, pb = false, more = n > 0;
+  FatTask fa{}, fb{};
   long long spec_cells = 0;
   for (;;) {
-    if (more) {  // every sub-slot without a seed takes the next entry: one claim for the wave
-      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha) & kLead, nb = __builtin_amdgcn_ballot_w64(!hb) & kLead;
+    // sub-slots without a task start their prefetched one
+    if (!ha && pa) {
+      QTask t;
+      qtask_start_fat<G>(t, o, ref, fa, tal, tar);
+      if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));  // a whole-read seed (bwamem.c:753, 781)
+      else qpark(qa, t);
+      ha = t.phase < 4;
+      pa = false;
+    }
+    if (!hb && pb) {
+      QTask t;
+      qtask_start_fat<G>(t, o, ref, fb, tbl, tbr);
+      if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
+      else qpark(qb, t);
+      hb = t.phase < 4;
+      pb = false;
+    }
+    if (more) {  // every sub-slot without a next task claims one: one claim for the wave
+      const uint64_t na = __builtin_amdgcn_ballot_w64(!pa) & kLead, nb = __builtin_amdgcn_ballot_w64(!pb) & kLead;
       const int nn = __popcll(na) + __popcll(nb);
       if (nn > 0) {
         int m0, cap;
         if (qq.claim(nn, m0, cap)) {
-          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (ha ? 0 : 1);
-          if (!ha && ia < cap) {
-            QTask t;
-            qtask_start<G>(t, o, ref, b, a, tl[qq.shard + 8 * ia], tal, tar);
-            if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));  // a whole-read seed (bwamem.c:753, 781)
-            else qpark(qa, t);
-            ha = t.phase < 4;
+          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (pa ? 0 : 1);
+          if (!pa && ia < cap) {  // loaded now, used at a later call boundary
+            fa = fl[qq.shard + 8 * ia];
+            pa = true;
           }
-          if (!hb && ib < cap) {
-            QTask t;
-            qtask_start<G>(t, o, ref, b, a, tl[qq.shard + 8 * ib], tbl, tbr);
-            if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
-            else qpark(qb, t);
-            hb = t.phase < 4;
+          if (!pb && ib < cap) {
+            fb = fl[qq.shard + 8 * ib];
+            pb = true;
           }
         } else {
           more = false;
@@ -691,7 +780,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
       }
     }
     if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
-      if (!more) break;
+      if (!more && !__builtin_amdgcn_ballot_w64(pa || pb)) break;
       continue;
     }
     QCall ca = quad_idle(b.seq, tal), cb = quad_idle(b.seq, tbl);
@@ -708,6 +797,9 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
     ExtOut xa, xb;
     Tally32 ta{0, 0, 0}, tb{0, 0, 0};
     extend_quad_dispatch<G, PMAX, K8>(o, ca, cb, xa, xb, ta, tb);
+#ifdef BWAGPU_OCC_DIAG
+    occ_diag<G>(a, ca, cb, ta, tb);
+#endif
     if (ha) {
       QTask t = qload(qa);
       if (qtask_advance(t, o, xa, ta)) {
@@ -756,6 +848,22 @@ __device__ __forceinline__ int pair_key(const DevBatch& b, const SpecArgs& a, in
   // descending: the longest tasks first, so the grid's tail is short ones
   const int hi = max(ql, qr), lo = min(ql, qr);
   return (kSortKeys - 1) - ((hi >> 3) << 5 | (lo >> 3));
+}
+
+// the task's FatTask record (engine.h): its seed, its chain's window, its read
+__device__ __forceinline__ FatTask fat_task(const DevBatch& b, const SpecArgs& a, int2 tk) {
+  const bwagpu_seed_t sd = a.prog[tk.x];
+  const ChainWin cw = a.win[tk.y];
+  const int rd = a.chain_read[tk.y];
+  FatTask f;
+  f.rbeg = sd.rbeg;
+  f.qoff = b.seq_off[rd];
+  f.pos = tk.x;
+  f.dlo = (int32_t)(sd.rbeg - cw.lo);
+  f.dhi = (int32_t)(cw.hi - sd.rbeg);
+  const int lq = (int)(b.seq_off[rd + 1] - f.qoff);
+  f.qls = (uint32_t)sd.qbeg | (uint32_t)sd.len << 10 | (uint32_t)lq << 20;
+  return f;
 }
 
 __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
@@ -813,6 +921,7 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
   const size_t off = spec_list_off(list, b.n_chains, b.n_seeds);
   const int2* tl = a.tasks + off;
   int2* out = a.stasks + off;
+  FatTask* fout = a.ftask + off;
   const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
   const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
   constexpr int kPer = 16;  // entries per thread held across the barrier
@@ -837,7 +946,11 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < kPer; ++m)
-      if (keys[m] >= 0) out[cnt[keys[m]] + rank[m]] = tk[m];
+      if (keys[m] >= 0) {
+        const int at = cnt[keys[m]] + rank[m];
+        out[at] = tk[m];
+        fout[at] = fat_task(b, a, tk[m]);
+      }
     __syncthreads();
     for (int k = threadIdx.x; k < kSortKeys; k += 256) cnt[k] = 0;
     __syncthreads();

@@ -145,6 +145,7 @@ PROTOS = {
     "bwagpu_prof_start": (C.c_int, [_VP, C.c_int]),
     "bwagpu_debug_fail_wait": (C.c_int, [_VP, C.c_int, C.c_int]),
     "bwagpu_debug_spec_counters": (C.c_int, [_VP, _VP, _VP]),
+    "bwagpu_debug_occupancy": (C.c_int, [_VP, _VP, _VP]),
     "bwagpu_debug_spec_ext": (C.c_int, [_VP, _VP, _VP, C.c_int32]),
     "bwagpu_prof_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "bwagpu_prof_intervals": (C.c_int, [_VP, _VP, _VP, C.c_int32, C.POINTER(C.c_int32)]),

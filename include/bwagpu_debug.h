@@ -62,6 +62,12 @@ int bwagpu_prof_start(bwagpu_ctx_t *ctx, int max_launches);
    redo pass computed inline, out[5] reads with > 64 seeds, out[6] reads left
    to the redo pass, out[7] seeds of heavy reads with pair matrices */
 int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
+/* diagnostics of a library built with -DBWAGPU_OCC_DIAG (else
+   BWAGPU_E_UNSUPPORTED): the packed extension kernels' occupancy over the last
+   device-entry batch on `stream`, out[0..7] = generations (extend_quad calls
+   of a wave), rows run, call-slot rows, live call rows, call-slot cells, live
+   call-slot cells, cells inside the live calls' queries, computed cells */
+int bwagpu_debug_occupancy(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
 /* diagnostics: the per-seed extension records (48 B each: rb, re, qb, qe,
    score, truesc, w, cells, rows, calls + 1; calls == 0: not computed) of the
    last device-entry batch on `stream`, n = its seed count */
