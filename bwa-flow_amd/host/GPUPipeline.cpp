@@ -13,6 +13,7 @@
 #include <chrono>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <thread>
 
@@ -533,15 +534,61 @@ void ChainReaper::run() {
   }
 }
 
+// ----------------------------------------------------------------- PostPool
+int PostPool::threads() {
+  static const int n = [] {
+    const char* e = getenv("BWAGPU_POST_THREADS");
+    return std::max(0, std::min(e ? atoi(e) : 3, 16));
+  }();
+  return n;
+}
+
+PostPool::~PostPool() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : th_)
+    if (t.joinable()) t.join();  // run() finishes what is queued before it returns
+}
+
+void PostPool::post(std::function<void()> f) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!started_) {
+      started_ = true;
+      for (int k = 0; k < threads(); ++k) th_.emplace_back([this] { run(); });
+    }
+    q_.push_back(std::move(f));
+  }
+  cv_.notify_one();
+}
+
+void PostPool::run() {
+  std::unique_lock<std::mutex> g(mu_);
+  for (;;) {
+    cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+    if (q_.empty()) return;
+    auto f = std::move(q_.front());
+    q_.pop_front();
+    g.unlock();
+    f();
+    g.lock();
+  }
+}
+
 // ------------------------------------------------------- ChainsToRegionsGPU
 // records a worker keeps in flight (its context's slots in use): every slot
 // is a stream of its own, and with its selection side stream each takes a
 // hardware queue (GPU_MAX_HW_QUEUES = 4 by default); BWAGPU_STAGE_SLOTS
-// (1..BWAGPU_NUM_SLOTS, default 2)
+// (1..BWAGPU_NUM_SLOTS, default 3 with a PostPool, else 2)
 int stage_slots() {
   static const int n = [] {
     const char* e = getenv("BWAGPU_STAGE_SLOTS");
-    return std::max(1, std::min(e ? atoi(e) : 2, BWAGPU_NUM_SLOTS));
+    // with a PostPool a third slot keeps the device fed while a finished
+    // record is being posted from another
+    return std::max(1, std::min(e ? atoi(e) : (PostPool::threads() > 0 ? 3 : 2), BWAGPU_NUM_SLOTS));
   }();
   return n;
 }
@@ -561,6 +608,26 @@ void ChainsToRegionsGPU::retire() {
     reaper_.drain();  // the stage is done when its chains are freed
     if (cpu_stage_) cpu_stage_->setUseAccx(false);
   }
+}
+
+void ChainsToRegionsGPU::post_record(int wid, const ChainsRecord& rec, const bwagpu_alnreg_t* rg,
+                                     const int32_t* nn, const int32_t* off) {
+  const auto t0 = std::chrono::steady_clock::now();
+  RegionsRecord out;
+  out.start_idx = rec.start_idx;
+  out.batch_num = rec.batch_num;
+  out.seqs = rec.seqs;
+  out.alnreg = FlatBatch::unpack_dense(rg, nn, off, rec.batch_num);
+  if (own_ == ChainOwnership::kForward) {
+    out.chains = rec.chains;  // RegionsToSam frees them (Pipeline.cpp:559)
+  } else {
+    reaper_.release(rec.chains, rec.batch_num);
+    out.chains = nullptr;
+  }
+  ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  n_gpu_.fetch_add(1);
+  if (wid < kMaxWorkers) per_worker_[wid].fetch_add(1);
+  pushOutput(out);
 }
 
 void ChainsToRegionsGPU::compute(int wid) {
@@ -587,6 +654,17 @@ void ChainsToRegionsGPU::compute(int wid) {
   std::deque<Job> inflight;
   long long submitted = 0;
   bool more = true;
+  // slots whose finished record a PostPool thread is still turning into
+  // regions (its results are read from the slot's pinned buffers)
+  const bool async_post = PostPool::threads() > 0;
+  std::unique_ptr<std::atomic<int>[]> posting(new std::atomic<int>[nslots]);
+  for (int k = 0; k < nslots; ++k) posting[k].store(0);
+  auto settle = [&](int k) {  // slot k's record posted
+    while (posting[k].load(std::memory_order_acquire)) std::this_thread::sleep_for(std::chrono::microseconds(10));
+  };
+  auto settle_all = [&] {
+    for (int k = 0; k < nslots; ++k) settle(k);
+  };
   auto fail_all = [&](const char* what, int rc) {
     // fpgaHangError / fpgaResultsError path: recompute what is in flight on
     // the CPU, push it, retire this worker
@@ -594,6 +672,7 @@ void ChainsToRegionsGPU::compute(int wid) {
     (void)rc;
     for (auto& j : inflight) pushOutput(on_cpu(j.rec));
     inflight.clear();
+    settle_all();
     retire();
   };
   for (;;) {
@@ -612,6 +691,7 @@ void ChainsToRegionsGPU::compute(int wid) {
       }
       if (ready) {
         const int sl = (int)(submitted % nslots);
+        settle(sl);
         inflight.push_back(Job{rec, &flats[sl], sl});
         Job& j = inflight.back();
         auto t0 = std::chrono::steady_clock::now();
@@ -656,10 +736,6 @@ void ChainsToRegionsGPU::compute(int wid) {
       fail_all("wait", rc);
       return;
     }
-    RegionsRecord out;
-    out.start_idx = j.rec.start_idx;
-    out.batch_num = j.rec.batch_num;
-    out.seqs = j.rec.seqs;
     const bwagpu_alnreg_t* rg = nullptr;
     const int32_t* nn = nullptr;
     const int32_t* off = nullptr;
@@ -672,18 +748,19 @@ void ChainsToRegionsGPU::compute(int wid) {
       dev_ns_[0] += (long long)(ds.kernel_ms * 1e6);
       dev_ns_[1] += (long long)((ds.total_ms - ds.kernel_ms) * 1e6);
     }
-    out.alnreg = FlatBatch::unpack_dense(rg, nn, off, j.rec.batch_num);
-    if (own_ == ChainOwnership::kForward) {
-      out.chains = j.rec.chains;  // RegionsToSam frees them (Pipeline.cpp:559)
+    if (async_post) {
+      const int sl = j.slot;
+      posting[sl].store(1, std::memory_order_release);
+      std::atomic<int>* flag = &posting[sl];
+      poster_.post([this, wid, rec = j.rec, rg, nn, off, flag] {
+        post_record(wid, rec, rg, nn, off);
+        flag->store(0, std::memory_order_release);
+      });
     } else {
-      reaper_.release(j.rec.chains, j.rec.batch_num);
-      out.chains = nullptr;
+      post_record(wid, j.rec, rg, nn, off);
     }
-    ns_[3] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
-    n_gpu_.fetch_add(1);
-    if (wid < kMaxWorkers) per_worker_[wid].fetch_add(1);
     inflight.pop_front();
-    pushOutput(out);
   }
+  settle_all();  // every record of this worker is downstream before it retires
   retire();
 }

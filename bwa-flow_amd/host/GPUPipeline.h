@@ -18,6 +18,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -132,6 +133,29 @@ class ChainReaper {
   std::vector<std::thread> th_;
 };
 
+// Threads that finish records for the stage workers (BWAGPU_POST_THREADS,
+// default 3; 0 = on the worker itself): the malloc'd mem_alnreg_v of a record
+// (FlatBatch::unpack_dense), its chains handed on or to the reaper, and the
+// push to the next stage — while the worker packs and submits its next record
+// into another slot.  A slot is reused only once its record has been posted.
+class PostPool {
+ public:
+  PostPool() = default;
+  ~PostPool();
+  PostPool(const PostPool&) = delete;
+  PostPool& operator=(const PostPool&) = delete;
+  void post(std::function<void()> f);
+  static int threads();
+
+ private:
+  void run();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false, started_ = false;
+  std::vector<std::thread> th_;
+};
+
 // Who frees a record's chains once its regions are made.  kFree (the
 // default) frees them on the stage's reaper threads; kForward hands them on
 // exactly as the FPGA stage does.  Either is correct under RegionsToSam,
@@ -170,7 +194,8 @@ class ChainsToRegionsGPU
   // enqueue / dequeue / post totals FPGAPipeline.cpp:557-578 prints):
   // [0] pack (ChainsRecord -> flat arrays), [1] submit (pinned staging + H2D +
   // launches), [2] wait (device time not hidden + D2H), [3] post (malloc'd
-  // mem_alnreg_v + freeing the chains, or handing them to the reaper)
+  // mem_alnreg_v + freeing the chains, or handing them to the reaper; on the
+  // PostPool's threads when it has any)
   void phase_seconds(double out[4]) const {
     for (int i = 0; i < 4; ++i) out[i] = (double)ns_[i].load() * 1e-9;
   }
@@ -183,6 +208,9 @@ class ChainsToRegionsGPU
  private:
   RegionsRecord on_cpu(const ChainsRecord& rec);
   void retire();
+  // a finished record's regions -> its RegionsRecord, pushed downstream
+  void post_record(int wid, const ChainsRecord& rec, const bwagpu_alnreg_t* rg, const int32_t* nn,
+                   const int32_t* off);
 
   std::atomic<int> n_active_;
   ChainsToRegions* cpu_stage_;
@@ -193,4 +221,5 @@ class ChainsToRegionsGPU
   std::atomic<long long> dev_ns_[2] = {};
   ChainOwnership own_;
   ChainReaper reaper_;
+  PostPool poster_;
 };

@@ -168,7 +168,9 @@ class Stage : public StageBase {
   }
 };
 
-inline void idle_wait() { std::this_thread::sleep_for(std::chrono::microseconds(10)); }
+// the reference's MapStage idles 100 us between polls of its input queue
+// (kflow/include/kflow/MapStage.h:186-189)
+inline void idle_wait() { std::this_thread::sleep_for(std::chrono::microseconds(100)); }
 
 // CPU stage with an optional accelerator back end (ChainsToRegions is one)
 template <typename U, typename V, int IN_DEPTH = 64, int OUT_DEPTH = 64>

@@ -25,3 +25,6 @@ B="$GRAFT_REPO_ROOT/bench.py --headline-only --workload c2_refseed --steps 5 --w
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $OUT/pmc_a -o a --output-format csv -- python3 $B > $OUT/pmc_a.json 2> $OUT/pmc_a.err || exit 6
 cd $GRAFT_REPO_ROOT
 echo done > $OUT/rc.txt
+timeout -k 10 900 python -u tools_dev/e2e_sweep.py 20 1 2 > $OUT/e2e_sweep.jsonl 2> $OUT/e2e_sweep.err; rc=$?
+[ $rc -ge 124 ] && exit $rc
+echo done2 > $OUT/rc2.txt
