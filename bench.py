@@ -614,7 +614,7 @@ def end_to_end_stage(opt, ref, batches, checks, reps: int = 20,
                host_cpu_user=round(float(times[10]) * 1e3 / nrec, 3), host_cpu_sys=round(float(times[11]) * 1e3 / nrec, 3))
     own = (f"forwarded to RegionsToSam (the FPGA stage's ownership, FPGAPipeline.cpp:434); the sink stage "
            f"({sink_workers} threads) frees them"
-           if chain_mode == 0 else f"freed by the stage's {os.environ.get('BWAGPU_REAPER_THREADS', '2')} reaper threads, "
+           if chain_mode == 0 else f"freed by the stage's {os.environ.get('BWAGPU_REAPER_THREADS', '4')} reaper threads, "
            "NULL forwarded (the CPU stage's ownership, Pipeline.cpp:526-537)")
     return {"value": round(reads / times[0] / 1e6, 4), "unit": "Mreads/s", "records": int(times[5]),
             "cpu_fallback_records": int(times[6]), "wall_s": round(float(times[0]), 4), "phases": ph,

@@ -910,6 +910,11 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.sorth = s.d_sorth.as<int32_t>();
   a.stasks = s.d_stasks.as<int2>();
   a.ftask = s.d_ftask.as<FatTask>();
+  static const int ext_prefetch = [] {  // A/B knob of the claim-ahead
+    const char* e = getenv("BWAGPU_EXT_PREFETCH");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  a.ext_prefetch = ext_prefetch;
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;
@@ -1826,7 +1831,7 @@ int bwagpu_debug_occupancy(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   HIPC(hipStreamSynchronize(st), "hipStreamSynchronize");
   int32_t c[SPC_WORDS];
   HIPC(hipMemcpy(c, ctx->dev_scratch[k].d_ctr.p, sizeof c, hipMemcpyDeviceToHost), "hipMemcpy(ctr)");
-  memcpy(out, c + 32, 8 * sizeof(int64_t));
+  memcpy(out, c + 32, 12 * sizeof(int64_t));
 #ifdef BWAGPU_OCC_DIAG
   return BWAGPU_OK;
 #else

@@ -215,6 +215,8 @@ struct SpecArgs {
   int32_t* sorth;             // kSortWords, zeroed per batch: per (round, bin < 2) key histograms / cursors
   int2* stasks;               // the C = 3 / 4 lists sorted by key (same offsets as tasks), for the pair kernel
   FatTask* ftask;             // the same lists as FatTask records (the packed kernels)
+  int ext_prefetch;           // spec_ext4_kernel: claim next tasks a generation ahead while more than
+                              // ext_prefetch x 8 x (waves per XCD) remain (0: on demand)
   bwagpu_alnreg_t* out;
   int32_t* out_n;
   int64_t* stats;

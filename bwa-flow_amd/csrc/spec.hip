@@ -741,7 +741,17 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
   bool ha = false, hb = false, pa = false, pb = false, more = n > 0;
   FatTask fa{}, fb{};
   long long spec_cells = 0;
+  // claim-ahead while plenty of the list is left (a.ext_prefetch): near the
+  // end, tasks held ahead by a busy wave would idle the others
+  const int ahead_min = a.ext_prefetch * 8 * (int)((gridDim.x * (kBlock / 64) + 7) / 8);
+  int rem = n;
+#ifdef BWAGPU_OCC_DIAG
+  unsigned long long tw[4] = {0, 0, 0, 0};
+#endif
   for (;;) {
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
     // sub-slots without a task start their prefetched one
     if (!ha && pa) {
       QTask t;
@@ -759,26 +769,51 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
       hb = t.phase < 4;
       pb = false;
     }
-    if (more) {  // every sub-slot without a next task claims one: one claim for the wave
-      const uint64_t na = __builtin_amdgcn_ballot_w64(!pa) & kLead, nb = __builtin_amdgcn_ballot_w64(!pb) & kLead;
+    if (more) {  // one claim for the wave: sub-slots without a next task (ahead) / without a task (on demand)
+      const bool ahead = ahead_min > 0 && rem > ahead_min;
+      const bool wa = ahead ? !pa : (!ha && !pa), wb = ahead ? !pb : (!hb && !pb);
+      const uint64_t na = __builtin_amdgcn_ballot_w64(wa) & kLead, nb = __builtin_amdgcn_ballot_w64(wb) & kLead;
       const int nn = __popcll(na) + __popcll(nb);
       if (nn > 0) {
         int m0, cap;
         if (qq.claim(nn, m0, cap)) {
-          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (pa ? 0 : 1);
-          if (!pa && ia < cap) {  // loaded now, used at a later call boundary
+          rem = (cap - m0 - nn) * 8;
+          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (wa ? 1 : 0);
+          if (wa && ia < cap) {
             fa = fl[qq.shard + 8 * ia];
             pa = true;
           }
-          if (!pb && ib < cap) {
+          if (wb && ib < cap) {
             fb = fl[qq.shard + 8 * ib];
             pb = true;
+          }
+          if (!ahead) {  // on demand: start them now
+            if (!ha && pa) {
+              QTask t;
+              qtask_start_fat<G>(t, o, ref, fa, tal, tar);
+              if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
+              else qpark(qa, t);
+              ha = t.phase < 4;
+              pa = false;
+            }
+            if (!hb && pb) {
+              QTask t;
+              qtask_start_fat<G>(t, o, ref, fb, tbl, tbr);
+              if (t.phase >= 4) store_ext_half<G>(a.ext + t.pos, qtask_ext(t));
+              else qpark(qb, t);
+              hb = t.phase < 4;
+              pb = false;
+            }
           }
         } else {
           more = false;
         }
       }
     }
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    tw[0] += c1 - c0;
+#endif
     if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
       if (!more && !__builtin_amdgcn_ballot_w64(pa || pb)) break;
       continue;
@@ -796,8 +831,14 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
     }
     ExtOut xa, xb;
     Tally32 ta{0, 0, 0}, tb{0, 0, 0};
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+    tw[1] += c2 - c1;
+#endif
     extend_quad_dispatch<G, PMAX, K8>(o, ca, cb, xa, xb, ta, tb);
 #ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+    tw[2] += c3 - c2;
     occ_diag<G>(a, ca, cb, ta, tb);
 #endif
     if (ha) {
@@ -820,9 +861,17 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
         qpark(qb, t);
       }
     }
+#ifdef BWAGPU_OCC_DIAG
+    tw[3] += __builtin_amdgcn_s_memtime() - c3;
+#endif
   }
   if ((threadIdx.x & (G - 1)) == 0 && spec_cells)
     atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+#ifdef BWAGPU_OCC_DIAG
+  // shader-clock cycles of the waves: task starts + claims, call setup, DP (extend_quad), result advance
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 4; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 48) + k, tw[k]);
+#endif
 }
 
 // LDS bytes of a spec_ext4_kernel workgroup

@@ -462,7 +462,9 @@ static bool reaper_enabled() {
 int ChainReaper::threads() {
   static const int n = [] {
     const char* e = getenv("BWAGPU_REAPER_THREADS");
-    return std::max(1, std::min(e ? atoi(e) : 2, 16));
+    // 4: a record's ~170 k chain frees cost ~8-14 ms of CPU (remote frees into
+    // the producers' arenas); with 2 threads they capped the stage
+    return std::max(1, std::min(e ? atoi(e) : 4, 16));
   }();
   return n;
 }
@@ -538,7 +540,9 @@ void ChainReaper::run() {
 int PostPool::threads() {
   static const int n = [] {
     const char* e = getenv("BWAGPU_POST_THREADS");
-    return std::max(0, std::min(e ? atoi(e) : 3, 16));
+    // default 0: on the box's 16 cores the measured gain was within the
+    // host's run-to-run noise (tools_dev/e2e_sweep.py, gpurun_out/r06c)
+    return std::max(0, std::min(e ? atoi(e) : 0, 16));
   }();
   return n;
 }

@@ -104,7 +104,7 @@ void freeChainsRecordChains(mem_chain_v* chains, int batch_num);
 // one SeqsToChains worker's glibc arena; one thread per record keeps a
 // record's frees on one arena lock, and several threads free different
 // records (different arenas) at once: threads() of them, BWAGPU_REAPER_THREADS
-// (default 2).  drain() returns once everything queued is freed.
+// (default 4).  drain() returns once everything queued is freed.
 // BWAGPU_CHAIN_REAPER=0 frees inline on the worker instead.
 class ChainReaper {
  public:
@@ -134,7 +134,7 @@ class ChainReaper {
 };
 
 // Threads that finish records for the stage workers (BWAGPU_POST_THREADS,
-// default 3; 0 = on the worker itself): the malloc'd mem_alnreg_v of a record
+// default 0 = on the worker itself): the malloc'd mem_alnreg_v of a record
 // (FlatBatch::unpack_dense), its chains handed on or to the reaper, and the
 // push to the next stage — while the worker packs and submits its next record
 // into another slot.  A slot is reused only once its record has been posted.

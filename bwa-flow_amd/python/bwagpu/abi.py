@@ -194,6 +194,8 @@ def load() -> C.CDLL:
         raise RuntimeError(f"bwagpu: HIP engine library missing at {p}; run __graft_entry__.build()")
     lib = C.CDLL(p)
     for name, (res, args) in PROTOS.items():
+        if name.startswith("bwagpu_debug_") and not hasattr(lib, name):
+            continue  # an A/B build of an older tree (BWAGPU_LIB) may lack a newer diagnostic
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
