@@ -302,6 +302,71 @@ __device__ __forceinline__ void fill_two_half(uint8_t* tbl, int64_t x0l, int nl,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The same gather in ONE memory round trip (the packed kernels' task starts):
+// lane r of the group takes rows [r R, r R + R) of each side, R = ceil(n / G)
+// <= 32, i.e. a run of <= 32 consecutive bases of one strand, and loads the
+// three aligned words of the pac that hold them (<= 9 bytes from a word
+// boundary); each row's base is a 2-bit field of those words.  fill_two_half
+// takes 4 rows per side per lane per pass, one dependent round trip per pass
+// (5-6 for a 150 bp read's windows).  A run that leaves the pac's last 12
+// bytes, or would straddle the two strands (a chain window never does), takes
+// the per-row loads of fill_two_half's kind.
+template <int G>
+__device__ __forceinline__ void fill_side_run(uint8_t* tb, int64_t x0, int dir, int k0, int k1, const DevRef& ref,
+                                              int64_t pac_bytes) {
+  if (k1 <= k0) return;
+  const int64_t two1 = (ref.l_pac << 1) - 1;
+  const int64_t xa = x0 + (int64_t)dir * k0, xb = x0 + (int64_t)dir * (k1 - 1);
+  const bool rev = xa >= ref.l_pac;
+  const int64_t fa = rev ? two1 - xa : xa, fb = rev ? two1 - xb : xb;
+  const int64_t fmin = fa < fb ? fa : fb;
+  const int64_t w0 = (fmin >> 2) & ~(int64_t)3;  // first byte of the aligned words
+  const bool fast = (xb >= ref.l_pac) == rev && fmin >= 0 && (fa > fb ? fa : fb) < ref.l_pac && w0 + 12 <= pac_bytes;
+  const int df = (dir > 0) == !rev ? 1 : -1;  // f along the run
+  if (fast) {
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(ref.pac + w0);
+    const uint32_t d0 = pw[0], d1 = pw[1], d2 = pw[2];
+    const int o0 = (int)(fa - (w0 << 2));  // the first row's base offset in the 48 loaded bases
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      if (k0 + j >= k1) break;
+      const int o = o0 + df * j;
+      const uint32_t w = o < 16 ? d0 : (o < 32 ? d1 : d2);
+      const int bit = ((o >> 2) & 3) * 8 + 6 - 2 * (o & 3);
+      const uint32_t bse = (w >> bit) & 3u;
+      tb[k0 + j] = (uint8_t)(rev ? 3u - bse : bse);
+    }
+  } else {
+    for (int k = k0; k < k1; ++k) {
+      const int64_t x = x0 + (int64_t)dir * k;
+      const bool rv = x >= ref.l_pac;
+      int64_t f = rv ? two1 - x : x;
+      f = f < 0 ? 0 : (f >= ref.l_pac ? ref.l_pac - 1 : f);
+      const int bse = (ref.pac[f >> 2] >> ((~f & 3) << 1)) & 3;
+      tb[k] = (uint8_t)(rv ? 3 - bse : bse);
+    }
+  }
+}
+
+template <int G>
+__device__ __forceinline__ void fill_two_fast(uint8_t* tbl, int64_t x0l, int nl, uint8_t* tbr, int64_t x0r, int nr,
+                                              const DevRef& ref) {
+  const int n = max(nl, nr);
+  const int R = (n + G - 1) / G;
+  if (R > 32) {  // options with bands wider than the packed kernels' defaults
+    fill_two_half<G>(tbl, x0l, nl, tbr, x0r, nr, ref);
+    return;
+  }
+  const int r = (int)(threadIdx.x & (G - 1));
+  const int64_t pac_bytes = (ref.l_pac >> 2) + 1;  // bwa.c:281-282
+  const int k0 = r * R;
+  fill_side_run<G>(tbl, x0l, -1, k0, min(k0 + R, nl), ref, pac_bytes);
+  fill_side_run<G>(tbr, x0r, 1, k0, min(k0 + R, nr), ref, pac_bytes);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One half's task and the state of its extension, in LDS for the whole task:
 // re-read (volatile, LDS address space) around every call, so that none of it
 // occupies VGPRs across the DP loop.
@@ -520,7 +585,7 @@ __device__ __forceinline__ void qtask_start(QTask& t, const DevOpt& o, const Dev
 // 32..47: generations, rows run, call-slot rows, live call rows, slot cells,
 // live slot cells, query cells, computed cells.
 template <int G>
-__device__ __forceinline__ void occ_diag(const SpecArgs& a, const QCall& ca, const QCall& cb, const Tally32& ta,
+__device__ __forceinline__ void occ_diag(unsigned long long* acc, const QCall& ca, const QCall& cb, const Tally32& ta,
                                          const Tally32& tb) {
   int qm = 0, rm = 0;
   long long lr = 0, lq = 0, cc = 0;
@@ -535,17 +600,16 @@ __device__ __forceinline__ void occ_diag(const SpecArgs& a, const QCall& ca, con
     cc += __builtin_amdgcn_readlane(ta.cells, g) + __builtin_amdgcn_readlane(tb.cells, g);
   }
   const int cpl = (qm + G) / G;
-  if ((threadIdx.x & 63) == 0) {
-    unsigned long long* c = reinterpret_cast<unsigned long long*>(a.ctr + 32);
-    atomicAdd(c + 0, 1ull);
-    atomicAdd(c + 1, (unsigned long long)rm);
-    atomicAdd(c + 2, (unsigned long long)rm * (2 * 64 / G));
-    atomicAdd(c + 3, (unsigned long long)lr);
-    atomicAdd(c + 4, (unsigned long long)rm * 128ull * cpl);
-    atomicAdd(c + 5, (unsigned long long)lr * G * cpl);
-    atomicAdd(c + 6, (unsigned long long)lq);
-    atomicAdd(c + 7, (unsigned long long)cc);
-  }
+  // summed per wave in registers, added to ctr words 32.. once at the kernel's end
+  // (atomics here would put their round trips on the next generation start)
+  acc[0] += 1ull;
+  acc[1] += (unsigned long long)rm;
+  acc[2] += (unsigned long long)rm * (2 * 64 / G);
+  acc[3] += (unsigned long long)lr;
+  acc[4] += (unsigned long long)rm * 128ull * cpl;
+  acc[5] += (unsigned long long)lr * G * cpl;
+  acc[6] += (unsigned long long)lq;
+  acc[7] += (unsigned long long)cc;
 }
 #endif
 
@@ -658,7 +722,13 @@ __device__ __forceinline__ SeedExt qtask_ext(const QTask& t) {
 // no room on the SIMD.
 static_assert(sizeof(QTask) <= 112, "QTask layout");
 constexpr int kQTaskLds = 112;
-typedef volatile __attribute__((address_space(3))) QTask LdsQ;
+// Not volatile: a volatile access makes the memory legalizer wait for every
+// outstanding global access first (s_waitcnt vmcnt(0) at each qload / qpark:
+// the SeedExt stores and the task loads of the other sub-slots, ~30 % of the
+// waves' cycles outside the DP in the diagnostic build's clock split).  An
+// empty asm with a memory clobber after the stores and before the loads keeps
+// the state really parked in LDS (LLVM may not carry it in VGPRs across it).
+typedef __attribute__((address_space(3))) QTask LdsQ;
 __device__ __forceinline__ void qpark(LdsQ* p, const QTask& t) {
   p->rbeg = t.rbeg;
   p->wlo = t.wlo;
@@ -681,8 +751,10 @@ __device__ __forceinline__ void qpark(LdsQ* p, const QTask& t) {
   p->cells = t.cells;
   p->rows = t.rows;
   p->calls = t.calls;
+  asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ QTask qload(LdsQ* p) {
+  asm volatile("" ::: "memory");
   QTask t;
   t.rbeg = p->rbeg;
   t.wlo = p->wlo;
@@ -746,7 +818,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
   const int ahead_min = a.ext_prefetch * 8 * (int)((gridDim.x * (kBlock / 64) + 7) / 8);
   int rem = n;
 #ifdef BWAGPU_OCC_DIAG
-  unsigned long long tw[4] = {0, 0, 0, 0};
+  unsigned long long tw[4] = {0, 0, 0, 0}, occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   for (;;) {
 #ifdef BWAGPU_OCC_DIAG
@@ -839,7 +911,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
 #ifdef BWAGPU_OCC_DIAG
     const unsigned long long c3 = __builtin_amdgcn_s_memtime();
     tw[2] += c3 - c2;
-    occ_diag<G>(a, ca, cb, ta, tb);
+    occ_diag<G>(occ, ca, cb, ta, tb);
 #endif
     if (ha) {
       QTask t = qload(qa);
@@ -869,8 +941,10 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
     atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
 #ifdef BWAGPU_OCC_DIAG
   // shader-clock cycles of the waves: task starts + claims, call setup, DP (extend_quad), result advance
-  if ((threadIdx.x & 63) == 0)
+  if ((threadIdx.x & 63) == 0) {
+    for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 32) + k, occ[k]);
     for (int k = 0; k < 4; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 48) + k, tw[k]);
+  }
 #endif
 }
 
