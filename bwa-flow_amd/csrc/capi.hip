@@ -1831,7 +1831,7 @@ int bwagpu_debug_occupancy(bwagpu_ctx_t* ctx, void* stream, int64_t* out) {
   HIPC(hipStreamSynchronize(st), "hipStreamSynchronize");
   int32_t c[SPC_WORDS];
   HIPC(hipMemcpy(c, ctx->dev_scratch[k].d_ctr.p, sizeof c, hipMemcpyDeviceToHost), "hipMemcpy(ctr)");
-  memcpy(out, c + 32, 12 * sizeof(int64_t));
+  memcpy(out, c + 32, 14 * sizeof(int64_t));
 #ifdef BWAGPU_OCC_DIAG
   return BWAGPU_OK;
 #else

@@ -627,7 +627,7 @@ __device__ __forceinline__ void qtask_start_fat(QTask& t, const DevOpt& o, const
   t.lq = (int)(f.qls >> 20);
   const int qlenL = t.qbeg, qlenR = t.lq - (t.qbeg + t.len);
   const int64_t x0R = t.rbeg + t.len;
-  fill_two_half<G>(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, f.dlo, o.w << 1, o.pen_clip5) : 0, tr, x0R,
+  fill_two_fast<G>(tl, t.rbeg - 1, qlenL ? rows_needed(o, qlenL, f.dlo, o.w << 1, o.pen_clip5) : 0, tr, x0R,
                    qlenR ? rows_needed(o, qlenR, (int)(t.whi - x0R), o.w << 1, o.pen_clip3) : 0, ref);
   t.phase = qlenL != 0 ? 0 : (qlenR != 0 ? 2 : 4);
   const int sc = qlenL != 0 ? -1 : t.len * o.a;  // bwamem.c:753
@@ -818,7 +818,7 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
   const int ahead_min = a.ext_prefetch * 8 * (int)((gridDim.x * (kBlock / 64) + 7) / 8);
   int rem = n;
 #ifdef BWAGPU_OCC_DIAG
-  unsigned long long tw[4] = {0, 0, 0, 0}, occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tw[6] = {0, 0, 0, 0, 0, 0}, occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   for (;;) {
 #ifdef BWAGPU_OCC_DIAG
@@ -848,7 +848,15 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
       const int nn = __popcll(na) + __popcll(nb);
       if (nn > 0) {
         int m0, cap;
-        if (qq.claim(nn, m0, cap)) {
+#ifdef BWAGPU_OCC_DIAG
+        const unsigned long long ca0 = __builtin_amdgcn_s_memtime();
+#endif
+        const bool got = qq.claim(nn, m0, cap);
+#ifdef BWAGPU_OCC_DIAG
+        const unsigned long long ca1 = __builtin_amdgcn_s_memtime();
+        tw[4] += ca1 - ca0;
+#endif
+        if (got) {
           rem = (cap - m0 - nn) * 8;
           const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (wa ? 1 : 0);
           if (wa && ia < cap) {
@@ -859,6 +867,10 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
             fb = fl[qq.shard + 8 * ib];
             pb = true;
           }
+#ifdef BWAGPU_OCC_DIAG
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the task records, timed on their own
+          tw[5] += __builtin_amdgcn_s_memtime() - ca1;
+#endif
           if (!ahead) {  // on demand: start them now
             if (!ha && pa) {
               QTask t;
@@ -940,10 +952,11 @@ __global__ void __launch_bounds__(kBlock) spec_ext4_kernel(DevOpt o, DevRef ref,
   if ((threadIdx.x & (G - 1)) == 0 && spec_cells)
     atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
 #ifdef BWAGPU_OCC_DIAG
-  // shader-clock cycles of the waves: task starts + claims, call setup, DP (extend_quad), result advance
+  // shader-clock cycles of the waves: task starts + claims, call setup, DP (extend_quad), result
+  // advance; of the first, the claims' and the task records' own
   if ((threadIdx.x & 63) == 0) {
     for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 32) + k, occ[k]);
-    for (int k = 0; k < 4; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 48) + k, tw[k]);
+    for (int k = 0; k < 6; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 48) + k, tw[k]);
   }
 #endif
 }

@@ -68,7 +68,8 @@ int bwagpu_debug_spec_counters(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
    of a wave), rows run, call-slot rows, live call rows, call-slot cells, live
    call-slot cells, cells inside the live calls' queries, computed cells;
    out[8..11] = the waves' shader-clock cycles in task starts + claims, call
-   setup, the DP (extend_quad) and the result advance (out: 12 entries) */
+   setup, the DP (extend_quad) and the result advance, out[12..13] = of the
+   first, the claims' and the task records' own (out: 14 entries) */
 int bwagpu_debug_occupancy(bwagpu_ctx_t *ctx, void *stream, int64_t *out);
 /* diagnostics: the per-seed extension records (48 B each: rb, re, qb, qe,
    score, truesc, w, cells, rows, calls + 1; calls == 0: not computed) of the

@@ -1,14 +1,27 @@
 #!/bin/bash
-# parity of the extension kernels after a row-loop change, then the headline
+# round 6: one-round-trip target gather (fill_two_fast) — parity, A/B against
+# lib/ab1, the clock split of both diag builds
 set -o pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r6f}
-mkdir -p $OUT
+T=${1:-r06f}
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_c2_batch.py tests/test_gpu_c3.py > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 6; }
-tail -1 $OUT/tests.log
-for k in 1 2; do
-  timeout -k 10 300 python -u bench.py --no-cpu --no-cigar --no-e2e --no-seeding --no-host-path > $OUT/b.json 2> $OUT/b.err || { tail $OUT/b.err; exit 5; }
-  python3 -c "
-import json;d=json.load(open('$OUT/b.json'));r=d['roofline'];c=d.get('c5_refseed',{})
-print(d['value'], d['ms_per_step'], d['parity_all_steps'], r.get('kernel_ms_per_step'), r['isolated_launch_ms'], c.get('ms_per_batch'), c.get('parity_all_steps'), {k:(v['ms_per_batch'], v['parity_all_steps']) for k,v in d.get('regime_grch38',{}).items() if isinstance(v,dict) and 'ms_per_batch' in v})"
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$T
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c2_batch.py tests/test_gpu_c3.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+for rep in 1 2 3; do
+for V in ab1 new; do
+  unset BWAGPU_LIB
+  [ $V = ab1 ] && export BWAGPU_LIB=$GRAFT_REPO_ROOT/bwa-flow_amd/lib/ab1/libbwagpu.so
+  timeout -k 10 300 python -u bench.py --headline-only --workload c2_refseed > $OUT/fix_${V}_$rep.json 2> $OUT/fix_${V}_$rep.err || exit 3
+  python3 -c "import json;d=json.load(open('$OUT/fix_${V}_$rep.json'));print('$V', d['value'], d['parity_all_steps'], d['roofline']['isolated_launch_ms'])"
 done
+done
+for V in ab1diag diag; do
+BWAGPU_LIB=$GRAFT_REPO_ROOT/bwa-flow_amd/lib/$V/libbwagpu.so timeout -k 10 300 python -u tools_dev/occ_diag.py 1 > $OUT/occ_$V.json 2> $OUT/occ_$V.err || exit 5
+python3 -c "import json;d=json.load(open('$OUT/occ_$V.json'));b=d['batch0'];print('$V', b['split'], b['cycle_split'], b['cycles_per_generation'], b['parity'])"
+done
+unset BWAGPU_LIB
+timeout -k 10 300 python -u bench.py --headline-only > $OUT/str.json 2> $OUT/str.err || exit 6
+python3 -c "import json;d=json.load(open('$OUT/str.json'));print('stream', d['value'], d['parity_all_steps'], d['roofline']['frac'])"
+echo done > $OUT/rc.txt

@@ -25,7 +25,8 @@ from bwagpu.engine import Engine  # noqa: E402
 
 FIELDS = ("seq_off", "seq", "read_chain_off", "chain_seed_off", "chain_rid", "chain_frac_rep", "seeds")
 KEYS = ("generations", "rows_run", "call_slot_rows", "live_call_rows", "slot_cells", "live_slot_cells",
-        "query_cells", "computed_cells", "cyc_start_claim", "cyc_setup", "cyc_dp", "cyc_advance")
+        "query_cells", "computed_cells", "cyc_start_claim", "cyc_setup", "cyc_dp", "cyc_advance", "cyc_claim",
+        "cyc_taskrec")
 
 
 def main():
@@ -47,7 +48,7 @@ def main():
         nn = torch.zeros(b.n_reads, dtype=torch.int32, device=dev)
         st = torch.cuda.Stream()
         eng.chain2aln_device(c, regs.data_ptr(), nn.data_ptr(), None, st.cuda_stream)
-        oc = np.zeros(12, np.int64)
+        oc = np.zeros(14, np.int64)
         rc = eng.lib.bwagpu_debug_occupancy(eng.ctx, C.c_void_p(st.cuda_stream), oc.ctypes.data_as(C.c_void_p))
         if rc != 0:
             raise SystemExit(f"bwagpu_debug_occupancy rc={rc}: {eng.lib.bwagpu_last_error(eng.ctx)}")
@@ -57,7 +58,7 @@ def main():
                       "beyond_q": round((d["live_slot_cells"] - d["query_cells"]) / S, 4),
                       "out_band": round((d["query_cells"] - d["computed_cells"]) / S, 4),
                       "computed": round(d["computed_cells"] / S, 4)}
-        cyc = sum(d[k] for k in KEYS[8:])
+        cyc = sum(d[k] for k in KEYS[8:12])
         d["cycle_split"] = {k[4:]: round(d[k] / max(cyc, 1), 4) for k in KEYS[8:]}
         d["cycles_per_generation"] = {k[4:]: round(d[k] / max(d["generations"], 1), 1) for k in KEYS[8:]}
         d["row_occupancy"] = round(d["live_call_rows"] / max(d["call_slot_rows"], 1), 4)
