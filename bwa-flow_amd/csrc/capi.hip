@@ -181,7 +181,7 @@ struct Slot {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
   DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
-  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks, d_ftask;
+  DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks, d_ftask, d_ftaskR;
   SpecStreams spec;  // created on first use (choose_side)
   bool side_chosen = false;
   void release_scratch() {
@@ -192,6 +192,7 @@ struct Slot {
     d_sorth.release();
     d_stasks.release();
     d_ftask.release();
+    d_ftaskR.release();
     if (spec.side) (void)hipStreamSynchronize(spec.side);
     if (spec.side) (void)hipStreamDestroy(spec.side);
     if (spec.fork) (void)hipEventDestroy(spec.fork);
@@ -880,6 +881,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(hipMemsetAsync(s.d_sorth.p, 0, sizeof(int32_t) * kSortWords, st), "memset sorth");
   HIPC(s.d_stasks.ensure(sizeof(int2) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(stasks)");
   HIPC(s.d_ftask.ensure(sizeof(FatTask) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(ftask)");
+  HIPC(s.d_ftaskR.ensure(sizeof(FatTask) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(ftaskR)");
   // pair matrices of heavy reads: sum over them of 2 * ns * ceil(ns / 64) words,
   // <= 2 * ns_total * (1 + ns_max / 64); reads that do not fit take the per-seed kernel
   const int64_t mat_words = std::max<int64_t>(1 << 20, 16 * (int64_t)ns);
@@ -910,6 +912,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.sorth = s.d_sorth.as<int32_t>();
   a.stasks = s.d_stasks.as<int2>();
   a.ftask = s.d_ftask.as<FatTask>();
+  a.ftaskR = s.d_ftaskR.as<FatTask>();
   static const int ext_prefetch = [] {  // A/B knob of the claim-ahead
     const char* e = getenv("BWAGPU_EXT_PREFETCH");
     return e ? std::max(0, atoi(e)) : 0;

@@ -159,6 +159,9 @@ enum {
   SPC_MATW64 = 28,    // int64 at words 28-29: uint64 words of heavy-read pair matrices handed out
   SPC_HCOLS = 30,     // columns (seeds) of heavy reads with a pair matrix
   SPC_LONG_N = 31,    // chains with more than kOrderLane seeds (ordered by spec_order_kernel)
+  // words 32-59: the packed kernels' occupancy counters (-DBWAGPU_OCC_DIAG)
+  SPC_LCNT = 64,      // [list] phased extension: tasks with a left side (spec_side4_kernel's left list)
+  SPC_RCNT = 73,      // [list] ... with a right side
   SPC_WORDS = 128
 };
 // sharded queue heads of the extension task lists (SpecArgs::qh, zeroed per
@@ -168,10 +171,13 @@ enum {
 // MI355X_MICROARCH.md "dequeue"; measured here: 7.9 -> 6.6 ms per C2 batch
 // when the nine lists' heads moved off the two shared lines)
 constexpr int kQHStride = 32;
-constexpr int kQHWords = kSpecRounds * kSpecBins * 8 * kQHStride;
+constexpr int kQHWords = 2 * kSpecRounds * kSpecBins * 8 * kQHStride;  // x 2: the phased extension's right lists
 // pair-kernel task order (spec_sort_*): 1024 keys = (left qlen / 8, right qlen / 8)
 constexpr int kSortKeys = 1024;
-constexpr int kSortWords = kSpecRounds * 2 * kSortKeys;
+// (the phased extension sorts each list twice, by the left and by the right
+// side's query length: its second histograms follow at kSortWordsR)
+constexpr int kSortWordsR = kSpecRounds * 2 * kSortKeys;
+constexpr int kSortWords = 2 * kSortWordsR;
 // task list `list` (= round * kSpecBins + bin) starts at this entry of SpecArgs::tasks
 __host__ __device__ inline size_t spec_list_off(int list, int n_chains, int n_seeds) {
   const int round = list / kSpecBins, bin = list % kSpecBins;
@@ -214,7 +220,9 @@ struct SpecArgs {
   int32_t* qh;                // kQHWords: sharded queue heads of the extension task lists
   int32_t* sorth;             // kSortWords, zeroed per batch: per (round, bin < 2) key histograms / cursors
   int2* stasks;               // the C = 3 / 4 lists sorted by key (same offsets as tasks), for the pair kernel
-  FatTask* ftask;             // the same lists as FatTask records (the packed kernels)
+  FatTask* ftask;             // the same lists as FatTask records (the packed kernels); the phased
+                              // extension: the tasks with a left side, by that side's length
+  FatTask* ftaskR;            // the phased extension: the tasks with a right side, by its length
   int ext_prefetch;           // spec_ext4_kernel: claim next tasks a generation ahead while more than
                               // ext_prefetch x 8 x (waves per XCD) remain (0: on demand)
   bwagpu_alnreg_t* out;

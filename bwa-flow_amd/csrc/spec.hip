@@ -1093,6 +1093,411 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
   }
 }
 
+// ---------------------------------------------- phased extension (round 6)
+// The extension tasks of the first two length bins run as two launches per
+// round: every task's LEFT call(s) (ksw_extend2 with the band retry,
+// bwamem.c:717-751), then every task's RIGHT call(s) (752-792, h0 = the left
+// score).  Each launch takes calls in the order of their own query length
+// (longest first), so the eight calls of a wave have about the same length:
+// with a task's left and right calls in one wave generation after another
+// (spec_ext4_kernel), a wave ran until its longest call ended while shorter
+// ones had ended (25 % of its call-slot cells) and set its columns by its
+// longest query (10 %), tools_dev/occ_diag.py.  Lists: the tasks with a left
+// side (FatTask, key = left query length) and those with a right side; a
+// whole-read seed (neither side) is written by the scatter itself.
+__device__ __forceinline__ int side_key(int qlen) { return 255 - min(qlen, 255); }  // descending
+
+__global__ void __launch_bounds__(256) spec_sort2_count(DevBatch b, SpecArgs a, int round) {
+  sel_prio();
+  __shared__ int hist[2][256];
+  __shared__ int tot[2];
+  const int list = round * kSpecBins + (int)blockIdx.y;
+  int32_t* ghL = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  int32_t* ghR = ghL + kSortWordsR;
+  for (int k = threadIdx.x; k < 2 * 256; k += 256) hist[k >> 8][k & 255] = 0;
+  if (threadIdx.x < 2) tot[threadIdx.x] = 0;
+  __syncthreads();
+  const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int2* tl = a.tasks + spec_list_off(list, b.n_chains, b.n_seeds);
+  const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) {
+    const FatTask f = fat_task(b, a, tl[i]);
+    const int qb = (int)(f.qls & 1023u), ln = (int)((f.qls >> 10) & 1023u), lq = (int)(f.qls >> 20);
+    const int qr = lq - qb - ln;
+    if (qb > 0) atomicAdd(&hist[0][side_key(qb)], 1);
+    if (qr > 0) atomicAdd(&hist[1][side_key(qr)], 1);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 2 * 256; k += 256) {
+    const int c = hist[k >> 8][k & 255];
+    if (c) {
+      atomicAdd((k >> 8) ? &ghR[k & 255] : &ghL[k & 255], c);
+      atomicAdd(&tot[k >> 8], c);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && tot[threadIdx.x])
+    atomicAdd(&a.ctr[(threadIdx.x ? SPC_RCNT : SPC_LCNT) + list], tot[threadIdx.x]);
+}
+
+// exclusive scan of the 256 keys of each (side, bin) histogram: one block each
+__global__ void __launch_bounds__(256) spec_sort2_scan(SpecArgs a, int round) {
+  sel_prio();
+  __shared__ int part[256];
+  int32_t* gh = a.sorth + (round * 2 + ((int)blockIdx.x & 1)) * kSortKeys + ((int)blockIdx.x >> 1) * kSortWordsR;
+  const int t = (int)threadIdx.x;
+  const int v = gh[t];
+  part[t] = v;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int x = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  gh[t] = part[t] - v;  // the key's first position (a cursor from here on)
+}
+
+__global__ void __launch_bounds__(256) spec_sort2_scatter(DevOpt o, DevBatch b, SpecArgs a, int round) {
+  sel_prio();
+  __shared__ int cnt[2][256];
+  const int list = round * kSpecBins + (int)blockIdx.y;
+  int32_t* ghL = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  int32_t* ghR = ghL + kSortWordsR;
+  for (int k = threadIdx.x; k < 2 * 256; k += 256) cnt[k >> 8][k & 255] = 0;
+  __syncthreads();
+  const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const size_t off = spec_list_off(list, b.n_chains, b.n_seeds);
+  const int2* tl = a.tasks + off;
+  FatTask* foL = a.ftask + off;
+  FatTask* foR = a.ftaskR + off;
+  const int chunk = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  constexpr int kPer = 8;  // entries per thread held across the barrier
+  int kl[kPer], kr[kPer], rl[kPer], rr[kPer];
+  FatTask ft[kPer];
+  for (int base = i0; base < i1; base += 256 * kPer) {
+#pragma unroll
+    for (int m = 0; m < kPer; ++m) {
+      const int i = base + m * 256 + (int)threadIdx.x;
+      kl[m] = kr[m] = -1;
+      if (i < i1) {
+        ft[m] = fat_task(b, a, tl[i]);
+        const int qb = (int)(ft[m].qls & 1023u), ln = (int)((ft[m].qls >> 10) & 1023u), lq = (int)(ft[m].qls >> 20);
+        const int qr = lq - qb - ln;
+        if (qb > 0) {
+          kl[m] = side_key(qb);
+          rl[m] = atomicAdd(&cnt[0][kl[m]], 1);
+        }
+        if (qr > 0) {
+          kr[m] = side_key(qr);
+          rr[m] = atomicAdd(&cnt[1][kr[m]], 1);
+        }
+        if (qb == 0 && qr == 0) {  // a whole-read seed (bwamem.c:753, 781): no ksw_extend2 call
+          SeedExt e;
+          e.rb = ft[m].rbeg;
+          e.re = ft[m].rbeg + ln;
+          e.qb = 0;
+          e.qe = lq;
+          e.score = e.truesc = ln * o.a;
+          e.w = o.w;
+          e.cells = e.rows = 0;
+          e.calls = 1;
+          a.ext[ft[m].pos] = e;
+        }
+      }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 2 * 256; k += 256) {
+      const int c = cnt[k >> 8][k & 255];
+      cnt[k >> 8][k & 255] = c ? atomicAdd((k >> 8) ? &ghR[k & 255] : &ghL[k & 255], c) : 0;  // this pass's range
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < kPer; ++m) {
+      if (kl[m] >= 0) foL[cnt[0][kl[m]] + rl[m]] = ft[m];
+      if (kr[m] >= 0) foR[cnt[1][kr[m]] + rr[m]] = ft[m];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 2 * 256; k += 256) cnt[k >> 8][k & 255] = 0;
+    __syncthreads();
+  }
+}
+
+// One side of a task in flight (LDS, per sub-slot, between its calls).
+struct SideTask {
+  int64_t rbeg, qoff, rb;
+  int32_t pos, dlo, dhi, qbeg, len, lq;
+  int32_t tt, score, h0, truesc, qb, aw0, cells, rows, calls, pad_;
+};
+static_assert(sizeof(SideTask) <= 96, "SideTask layout");
+constexpr int kSideLds = 96;
+typedef __attribute__((address_space(3))) SideTask LdsS;
+#define SIDE_FIELDS(X) X(rbeg) X(qoff) X(rb) X(pos) X(dlo) X(dhi) X(qbeg) X(len) X(lq) X(tt) X(score) X(h0) \
+  X(truesc) X(qb) X(aw0) X(cells) X(rows) X(calls)
+__device__ __forceinline__ void spark(LdsS* p, const SideTask& t) {
+#define X(f) p->f = t.f;
+  SIDE_FIELDS(X)
+#undef X
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ SideTask sload(LdsS* p) {
+  asm volatile("" ::: "memory");
+  SideTask t;
+#define X(f) t.f = p->f;
+  SIDE_FIELDS(X)
+#undef X
+  return t;
+}
+#undef SIDE_FIELDS
+
+// a sub-slot's start: the side's target rows into its LDS buffer, the state
+// of the side's first call (a right side reads what the left launch left in
+// the seed's SeedExt slot)
+template <int G, bool RIGHT>
+__device__ __forceinline__ void side_start(SideTask& t, const DevOpt& o, const DevRef& ref, const SpecArgs& a,
+                                           const FatTask& f, uint8_t* tb) {
+  t.rbeg = f.rbeg;
+  t.qoff = f.qoff;
+  t.pos = f.pos;
+  t.dlo = f.dlo;
+  t.dhi = f.dhi;
+  t.qbeg = (int)(f.qls & 1023u);
+  t.len = (int)((f.qls >> 10) & 1023u);
+  t.lq = (int)(f.qls >> 20);
+  t.tt = 0;
+  const int64_t pac_bytes = (ref.l_pac >> 2) + 1;
+  const int r = (int)(threadIdx.x & (G - 1));
+  if constexpr (!RIGHT) {
+    const int n = rows_needed(o, t.qbeg, t.dlo, o.w << 1, o.pen_clip5);
+    const int R = (n + G - 1) / G;
+    if (R <= 32) fill_side_run<G>(tb, t.rbeg - 1, -1, r * R, min(r * R + R, n), ref, pac_bytes);
+    else fill_two_half<G>(tb, t.rbeg - 1, n, tb, 0, 0, ref);
+    t.score = -1;  // bwamem.c:753 (a left side: the retry test compares with -1)
+    t.h0 = t.len * o.a;
+    t.truesc = -1;
+    t.qb = 0;
+    t.rb = t.rbeg;
+    t.aw0 = o.w;
+    t.cells = t.rows = t.calls = 0;
+  } else {
+    const int64_t x0 = t.rbeg + t.len;
+    const int qr = t.lq - t.qbeg - t.len;
+    const int n = rows_needed(o, qr, (int)(t.rbeg + t.dhi - x0), o.w << 1, o.pen_clip3);
+    const int R = (n + G - 1) / G;
+    if (R <= 32) fill_side_run<G>(tb, x0, 1, r * R, min(r * R + R, n), ref, pac_bytes);
+    else fill_two_half<G>(tb, 0, 0, tb, x0, n, ref);
+    if (t.qbeg > 0) {  // the left launch's result (the same wave wrote... another wave did: SeedExt slot)
+      const SeedExt e = a.ext[t.pos];
+      t.score = e.score;
+      t.truesc = e.truesc;
+      t.qb = e.qb;
+      t.rb = e.rb;
+      t.aw0 = e.w;
+      t.cells = e.cells;
+      t.rows = e.rows;
+      t.calls = e.calls;
+    } else {
+      t.score = t.truesc = t.len * o.a;  // bwamem.c:753
+      t.qb = 0;
+      t.rb = t.rbeg;
+      t.aw0 = o.w;
+      t.cells = t.rows = t.calls = 0;
+    }
+    t.h0 = t.score;  // sc0 (bwamem.c:761)
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool RIGHT>
+__device__ __forceinline__ QCall side_call(const SideTask& t, const DevOpt& o, const uint8_t* seq, const uint8_t* tb) {
+  QCall q;
+  if constexpr (!RIGHT) {
+    q.qlen = t.qbeg;
+    q.tlen = t.dlo;
+    q.qa = t.qbeg - 1;
+    q.qd = -1;
+    q.eb = o.pen_clip5;
+  } else {
+    const int64_t x0 = t.rbeg + t.len;
+    q.qlen = t.lq - t.qbeg - t.len;
+    q.tlen = (int)(t.rbeg + t.dhi - x0);
+    q.qa = t.qbeg + t.len;
+    q.qd = 1;
+    q.eb = o.pen_clip3;
+  }
+  q.h0 = t.h0;
+  q.w = o.w << t.tt;
+  q.zdrop = o.zdrop;
+  q.q = seq + t.qoff;
+  q.tb = tb;
+  q.tlen = rows_needed(o, q.qlen, q.tlen, q.w, q.eb);  // as qtask_call
+  return q;
+}
+
+// the call's result (bwamem.c:737-751 / 770-792); true = the side is done,
+// its result written to the seed's SeedExt slot (partial after a left side
+// with a right side to come, else final)
+template <int G, bool RIGHT>
+__device__ __forceinline__ bool side_advance(SideTask& t, const DevOpt& o, const SpecArgs& a, const ExtOut& x,
+                                             const Tally32& tl, long long& spec_cells) {
+  t.cells += tl.cells;
+  t.rows += tl.rows;
+  t.calls += tl.calls;
+  const int prev = t.score;
+  t.score = x.score;
+  const int aw = o.w << t.tt;
+  if (t.tt == 0 && !(x.score == prev || x.max_off < (aw >> 1) + (aw >> 2))) {  // the band retry (MAX_BAND_TRY)
+    t.tt = 1;
+    return false;
+  }
+  const int eb = RIGHT ? o.pen_clip3 : o.pen_clip5;
+  const bool local = x.gscore <= 0 || x.gscore <= x.score - eb;
+  SeedExt e;
+  if constexpr (!RIGHT) {
+    const int qr = t.lq - t.qbeg - t.len;
+    e.rb = t.rbeg - (local ? x.tle : x.gtle);
+    e.qb = local ? t.qbeg - x.qle : 0;
+    e.score = t.score;
+    e.truesc = local ? x.score : x.gscore;
+    if (qr != 0) {  // partial: the right launch goes on from here
+      e.re = 0;
+      e.qe = 0;
+      e.w = aw;
+      e.cells = t.cells;
+      e.rows = t.rows;
+      e.calls = t.calls;
+    } else {
+      e.re = t.rbeg + t.len;
+      e.qe = t.lq;
+      e.w = max(aw, o.w);
+      e.cells = t.cells;
+      e.rows = t.rows;
+      e.calls = t.calls + 1;  // + 1: a computed slot is never all-zero
+      spec_cells += t.cells;
+    }
+  } else {
+    e.rb = t.rb;
+    e.qb = t.qb;
+    e.qe = local ? t.qbeg + t.len + x.qle : t.lq;
+    e.re = t.rbeg + t.len + (local ? x.tle : x.gtle);
+    e.score = t.score;
+    e.truesc = t.truesc + (local ? x.score : x.gscore) - t.h0;
+    e.w = max(t.aw0, aw);
+    e.cells = t.cells;
+    e.rows = t.rows;
+    e.calls = t.calls + 1;
+    spec_cells += t.cells;
+  }
+  store_ext_half<G>(a.ext + t.pos, e);
+  return true;
+}
+
+// The phased extension's kernel: one side (RIGHT = false: left calls, true:
+// right calls) of the tasks of one list, eight calls per wave (G = 16) or four
+// (G = 32) in the packed 16-bit DP (extend_quad), claimed in the list's
+// order (the side's query length, longest first).
+template <int G, int PMAX, bool K8, bool RIGHT>
+__global__ void __launch_bounds__(kBlock) spec_side4_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                            int tb_bytes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr uint64_t kLead = G == 16 ? 0x0001000100010001ull : 0x0000000100000001ull;
+  const uint64_t below = kLead & ((1ull << ((int)threadIdx.x & (64 - G))) - 1);
+  // per group: A's and B's target rows, then their states
+  uint8_t* const ta_ = lds + (size_t)(threadIdx.x / G) * (2 * (size_t)tb_bytes + 2 * kSideLds);
+  uint8_t* const tb_ = ta_ + tb_bytes;
+  LdsS* const sa = (LdsS*)(tb_ + tb_bytes);
+  LdsS* const sb = (LdsS*)(tb_ + tb_bytes + kSideLds);
+  const int n = uni(__hip_atomic_load(&a.ctr[(RIGHT ? SPC_RCNT : SPC_LCNT) + list], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT));
+  const FatTask* fl = (RIGHT ? a.ftaskR : a.ftask) + spec_list_off(list, b.n_chains, b.n_seeds);
+  ShardQ qq;
+  qq.init(a.qh + 8 * kQHStride * (RIGHT ? kSpecRounds * kSpecBins + list : list) , n);
+  bool ha = false, hb = false, more = n > 0;
+  long long spec_cells = 0;
+#ifdef BWAGPU_OCC_DIAG
+  unsigned long long tw[6] = {0, 0, 0, 0, 0, 0}, occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  for (;;) {
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (more) {  // every sub-slot without a call takes the next entry: one claim for the wave
+      const uint64_t na = __builtin_amdgcn_ballot_w64(!ha) & kLead, nb = __builtin_amdgcn_ballot_w64(!hb) & kLead;
+      const int nn = __popcll(na) + __popcll(nb);
+      if (nn > 0) {
+        int m0, cap;
+        if (qq.claim(nn, m0, cap)) {
+          const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (ha ? 0 : 1);
+          if (!ha && ia < cap) {
+            SideTask t;
+            side_start<G, RIGHT>(t, o, ref, a, fl[qq.shard + 8 * ia], ta_);
+            spark(sa, t);
+            ha = true;
+          }
+          if (!hb && ib < cap) {
+            SideTask t;
+            side_start<G, RIGHT>(t, o, ref, a, fl[qq.shard + 8 * ib], tb_);
+            spark(sb, t);
+            hb = true;
+          }
+        } else {
+          more = false;
+        }
+      }
+    }
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    tw[0] += c1 - c0;
+#endif
+    if (!__builtin_amdgcn_ballot_w64(ha || hb)) {
+      if (!more) break;
+      continue;
+    }
+    QCall ca = quad_idle(b.seq, ta_), cb = quad_idle(b.seq, tb_);
+    if (ha) ca = side_call<RIGHT>(sload(sa), o, b.seq, ta_);
+    if (hb) cb = side_call<RIGHT>(sload(sb), o, b.seq, tb_);
+    ExtOut xa, xb;
+    Tally32 tla{0, 0, 0}, tlb{0, 0, 0};
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+    tw[1] += c2 - c1;
+#endif
+    extend_quad_dispatch<G, PMAX, K8>(o, ca, cb, xa, xb, tla, tlb);
+#ifdef BWAGPU_OCC_DIAG
+    const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+    tw[2] += c3 - c2;
+    occ_diag<G>(occ, ca, cb, tla, tlb);
+#endif
+    if (ha) {
+      SideTask t = sload(sa);
+      if (side_advance<G, RIGHT>(t, o, a, xa, tla, spec_cells)) ha = false;
+      else spark(sa, t);
+    }
+    if (hb) {
+      SideTask t = sload(sb);
+      if (side_advance<G, RIGHT>(t, o, a, xb, tlb, spec_cells)) hb = false;
+      else spark(sb, t);
+    }
+#ifdef BWAGPU_OCC_DIAG
+    tw[3] += __builtin_amdgcn_s_memtime() - c3;
+#endif
+  }
+#ifdef BWAGPU_OCC_DIAG
+  if ((threadIdx.x & 63) == 0) {
+    for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 32) + k, occ[k]);
+    for (int k = 0; k < 4; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 48) + k, tw[k]);
+  }
+#endif
+  if ((threadIdx.x & (G - 1)) == 0 && spec_cells)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+}
+
+static size_t side4_lds(int tb_bytes, int g) { return (size_t)(kBlock / g) * (2 * (size_t)tb_bytes + 2 * kSideLds); }
+
 // The pair kernel's grid: its waves pull tasks from the queue, so the grid
 // only sets its occupancy.  2 workgroups per CU (8 waves per CU, 2 per SIMD)
 // instead of the resident capacity (5 per SIMD): the batch on the other caller
@@ -2036,6 +2441,29 @@ bool quad_rows_ok(const DevOpt& o, long rows) {
 // stream's extension kernel holds, and its stream waits with it.  Round C
 // (mispredicted seeds of long reads: rare) runs on small grids for the same
 // reason.
+// the phased extension (spec_side4_kernel; BWAGPU_EXT_PHASED=0: the task
+// state machine of spec_ext4_kernel)
+static bool ext_phased() {
+  static const bool on = [] {
+    const char* e = getenv("BWAGPU_EXT_PHASED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// one side launch of the phased extension for list l: G calls per group
+template <int G, int PMAX, bool K8>
+static void launch_side_pair(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int l,
+                             int tb_bytes, hipStream_t st, int grid_cap, int round) {
+  const size_t lds = side4_lds(tb_bytes, G);
+  const int nb = resident_blocks(spec_side4_kernel<G, PMAX, K8, false>, lds);
+  const int gr = round == 2 ? std::min(nb, 64) : std::min(nb, grid_cap);
+  hipLaunchKernelGGL((spec_side4_kernel<G, PMAX, K8, false>), dim3(gr), dim3(kBlock), lds, st, o, ref, b, a, l,
+                     tb_bytes);
+  hipLaunchKernelGGL((spec_side4_kernel<G, PMAX, K8, true>), dim3(gr), dim3(kBlock), lds, st, o, ref, b, a, l,
+                     tb_bytes);
+}
+
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
                              int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
@@ -2046,6 +2474,31 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const auto grid = [round, quad](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb, quad); };
   const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]), oct = key8 && form == 0;
   const size_t lds2 = quad ? ext4_lds(tb_bytes, 32) : ext2_lds(tb_bytes);
+  if (quad && ext_phased()) {
+    hipLaunchKernelGGL(spec_sort2_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
+    hipLaunchKernelGGL(spec_sort2_scan, dim3(4), dim3(256), 0, st, a, round);
+    hipLaunchKernelGGL(spec_sort2_scatter, dim3(256, 2), dim3(256), 0, st, o, b, a, round);
+    const int cap = ext2_grid(1 << 30, true);
+    const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
+    if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
+    if (oct) launch_side_pair<16, kSpecBinLen[0] / 16, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
+    else if (key8) launch_side_pair<32, kSpecBinLen[0] / 32, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
+    else launch_side_pair<32, kSpecBinLen[1] / 32, false>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
+    if (prof) {
+      (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
+      *ss.pool_used += 2;
+    }
+    if (bin1) {
+      if (form == 0) launch_side_pair<16, kSpecBinLen[1] / 16, false>(o, ref, b, a, l + 1, tb_bytes, st, cap, round);
+      else launch_side_pair<32, kSpecBinLen[1] / 32, false>(o, ref, b, a, l + 1, tb_bytes, st, cap, round);
+    }
+    if (bin2) {
+      const int nb = resident_blocks(spec_ext_kernel<16>, lds);
+      hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(round == 2 ? std::min(nb, 64) : nb), dim3(kBlock), lds, st, o, ref,
+                         b, a, l + 2, tb_bytes);
+    }
+    return;
+  }
   // the first two length bins' lists in pair order (spec_sort_*), then two,
   // four or eight seeds per wave; the third (reads > 256 bp) one seed per wave
   hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
