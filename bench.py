@@ -97,7 +97,9 @@ PK16_PEAK_TOPS = 2 * VALU_PEAK_TOPS
 # H max 2, row max + argmax 3, E 4, F 4, profile lookup 1.
 OPS_PER_CELL = 17
 # the first-bin extension launch of every round (set in run_stage from the options)
-DOMINANT_KERNEL = "spec_ext4_kernel<16, 10, true>"  # "spec_ext2_kernel<5>" with --ext-form 1
+# the phased pair (left + right side launches); "spec_ext4_kernel<16, 10, true>"
+# with BWAGPU_EXT_PHASED=0, "spec_ext2_kernel<5>" with --ext-form 1 (engine.ext_kernel)
+DOMINANT_KERNEL = "spec_side4_kernel<16, 10, true>"
 
 
 def caller_streams(dev, n: int, tries: int = 16) -> list:
@@ -1254,6 +1256,8 @@ def headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapse
                      "kernel_ms_per_step": round(ext_busy_ms / args.steps, 4),
                      "kernel_sum_ms_per_step": round(ext_ms / args.steps, 4), "launches_timed": ext_launches,
                      "avg_launch_ms": round(ext_avg_ms, 4),
+                     "launch_unit": ("one round's left + right side launches (the phased pair, HIP events "
+                                     "bracket both)" if "side4" in DOMINANT_KERNEL else "one launch per round"),
                      # the kernel alone on the GPU (one stream, one batch at a time)
                      "isolated_launch_ms": iso, "frac_isolated": round(frac_iso, 5) if frac_iso else None,
                      "tasks_round_a_b": tasks_ab,

@@ -1002,11 +1002,12 @@ __device__ __forceinline__ FatTask fat_task(const DevBatch& b, const SpecArgs& a
   return f;
 }
 
-__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, int round, int bin0) {
   sel_prio();
   __shared__ int hist[kSortKeys];
-  const int list = round * kSpecBins + (int)blockIdx.y;
-  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  const int bin = bin0 + (int)blockIdx.y;
+  const int list = round * kSpecBins + bin;
+  int32_t* gh = a.sorth + (round * 2 + bin) * kSortKeys;
   for (int k = threadIdx.x; k < kSortKeys; k += 256) hist[k] = 0;
   __syncthreads();
   const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1019,10 +1020,10 @@ __global__ void __launch_bounds__(256) spec_sort_count(DevBatch b, SpecArgs a, i
     if (hist[k]) atomicAdd(&gh[k], hist[k]);
 }
 
-__global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round, int bin0) {
   sel_prio();
   __shared__ int part[256];
-  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.x) * kSortKeys;
+  int32_t* gh = a.sorth + (round * 2 + bin0 + (int)blockIdx.x) * kSortKeys;
   const int t = (int)threadIdx.x;  // 4 keys per thread
   int v[4], s = 0;
 #pragma unroll
@@ -1046,11 +1047,12 @@ __global__ void __launch_bounds__(256) spec_sort_scan(SpecArgs a, int round) {
   }
 }
 
-__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a, int round, int bin0) {
   sel_prio();
   __shared__ int cnt[kSortKeys];
-  const int list = round * kSpecBins + (int)blockIdx.y;
-  int32_t* gh = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  const int bin = bin0 + (int)blockIdx.y;
+  const int list = round * kSpecBins + bin;
+  int32_t* gh = a.sorth + (round * 2 + bin) * kSortKeys;
   for (int k = threadIdx.x; k < kSortKeys; k += 256) cnt[k] = 0;
   __syncthreads();
   const int n = __hip_atomic_load(&a.ctr[SPC_CNT + list], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1107,12 +1109,13 @@ __global__ void __launch_bounds__(256) spec_sort_scatter(DevBatch b, SpecArgs a,
 // whole-read seed (neither side) is written by the scatter itself.
 __device__ __forceinline__ int side_key(int qlen) { return 255 - min(qlen, 255); }  // descending
 
-__global__ void __launch_bounds__(256) spec_sort2_count(DevBatch b, SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort2_count(DevBatch b, SpecArgs a, int round, int bin0) {
   sel_prio();
   __shared__ int hist[2][256];
   __shared__ int tot[2];
-  const int list = round * kSpecBins + (int)blockIdx.y;
-  int32_t* ghL = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  const int bin = bin0 + (int)blockIdx.y;
+  const int list = round * kSpecBins + bin;
+  int32_t* ghL = a.sorth + (round * 2 + bin) * kSortKeys;
   int32_t* ghR = ghL + kSortWordsR;
   for (int k = threadIdx.x; k < 2 * 256; k += 256) hist[k >> 8][k & 255] = 0;
   if (threadIdx.x < 2) tot[threadIdx.x] = 0;
@@ -1142,10 +1145,12 @@ __global__ void __launch_bounds__(256) spec_sort2_count(DevBatch b, SpecArgs a, 
 }
 
 // exclusive scan of the 256 keys of each (side, bin) histogram: one block each
-__global__ void __launch_bounds__(256) spec_sort2_scan(SpecArgs a, int round) {
+// (bins bin0 .. bin0 + nbins - 1)
+__global__ void __launch_bounds__(256) spec_sort2_scan(SpecArgs a, int round, int bin0, int nbins) {
   sel_prio();
   __shared__ int part[256];
-  int32_t* gh = a.sorth + (round * 2 + ((int)blockIdx.x & 1)) * kSortKeys + ((int)blockIdx.x >> 1) * kSortWordsR;
+  const int bin = bin0 + (int)blockIdx.x % nbins, side = (int)blockIdx.x / nbins;
+  int32_t* gh = a.sorth + (round * 2 + bin) * kSortKeys + side * kSortWordsR;
   const int t = (int)threadIdx.x;
   const int v = gh[t];
   part[t] = v;
@@ -1159,11 +1164,12 @@ __global__ void __launch_bounds__(256) spec_sort2_scan(SpecArgs a, int round) {
   gh[t] = part[t] - v;  // the key's first position (a cursor from here on)
 }
 
-__global__ void __launch_bounds__(256) spec_sort2_scatter(DevOpt o, DevBatch b, SpecArgs a, int round) {
+__global__ void __launch_bounds__(256) spec_sort2_scatter(DevOpt o, DevBatch b, SpecArgs a, int round, int bin0) {
   sel_prio();
   __shared__ int cnt[2][256];
-  const int list = round * kSpecBins + (int)blockIdx.y;
-  int32_t* ghL = a.sorth + (round * 2 + (int)blockIdx.y) * kSortKeys;
+  const int bin = bin0 + (int)blockIdx.y;
+  const int list = round * kSpecBins + bin;
+  int32_t* ghL = a.sorth + (round * 2 + bin) * kSortKeys;
   int32_t* ghR = ghL + kSortWordsR;
   for (int k = threadIdx.x; k < 2 * 256; k += 256) cnt[k >> 8][k & 255] = 0;
   __syncthreads();
@@ -2403,12 +2409,27 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
 // every score of the bin fits the packed ranges, else two per wave
 // (spec_ext2_kernel, 32-bit).  Form 1 (bwagpu_ctx_ext_form, per context)
 // forces two per wave, 2 four per wave in the first bin too (tests, A/B).
+// the phased extension (spec_side4_kernel) per length bin: BWAGPU_EXT_PHASED
+// is a mask (bit 0: the first bin, bit 1: the second); unset = 1.  The second
+// bin (161-256 bp) stays on the task state machine of spec_ext4_kernel by
+// default: its calls run ~250 rows, so the tail of each side launch (one long
+// call on a nearly empty chip) cost more than the phasing saved (C5: 3.42 ms
+// per batch with both bins phased, 2.81 with neither, r06h).
+static int ext_phased_mask() {
+  static const int m = [] {
+    const char* e = getenv("BWAGPU_EXT_PHASED");
+    return e && e[0] ? atoi(e) & 3 : 1;
+  }();
+  return m;
+}
+
 static std::atomic<int> g_ext_form{0};
 int ext_form() { return g_ext_form.load(std::memory_order_relaxed); }
 int ext_kernel_for(const DevOpt& o, int form, int tb_bytes) {  // launch_ext_round's choice, first bin
   const bool quad = form != 1 && quad_scores_ok(o, kSpecBinLen[1]) && quad_rows_ok(o, tb_bytes);
   const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]);
-  return key8 ? (form == 0 ? 8 : 4) : (quad ? 5 : 2);
+  const int k = key8 ? (form == 0 ? 8 : 4) : (quad ? 5 : 2);
+  return quad && (ext_phased_mask() & 1) ? 10 + k : k;  // 1x: the phased pair (spec_side4_kernel)
 }
 int set_ext_form(int form) {  // the default of contexts made later; -> the previous one (form < 0: query only)
   const int prev = g_ext_form.load(std::memory_order_relaxed);
@@ -2436,21 +2457,6 @@ bool quad_rows_ok(const DevOpt& o, long rows) {
   return rows >= 0 && rows < 16384 && (rows + 256) * std::max(o.e_del, o.e_ins) < 28672;
 }
 
-// Only the bins the batch's longest read reaches are launched: a persistent
-// grid over an empty list still waits for CU slots that the other caller
-// stream's extension kernel holds, and its stream waits with it.  Round C
-// (mispredicted seeds of long reads: rare) runs on small grids for the same
-// reason.
-// the phased extension (spec_side4_kernel; BWAGPU_EXT_PHASED=0: the task
-// state machine of spec_ext4_kernel)
-static bool ext_phased() {
-  static const bool on = [] {
-    const char* e = getenv("BWAGPU_EXT_PHASED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // one side launch of the phased extension for list l: G calls per group
 template <int G, int PMAX, bool K8>
 static void launch_side_pair(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int l,
@@ -2464,6 +2470,27 @@ static void launch_side_pair(const DevOpt& o, const DevRef& ref, const DevBatch&
                      tb_bytes);
 }
 
+// the length bins' lists in the order their kernels take them: pair order
+// (spec_sort_*) for the task state machine, one list per side in its query
+// length order (spec_sort2_*) for the phased launches
+static void launch_sort(const DevOpt& o, const DevBatch& b, const SpecArgs& a, int round, bool phased, int bin0,
+                        int nbins, hipStream_t st) {
+  if (phased) {
+    hipLaunchKernelGGL(spec_sort2_count, dim3(256, nbins), dim3(256), 0, st, b, a, round, bin0);
+    hipLaunchKernelGGL(spec_sort2_scan, dim3(2 * nbins), dim3(256), 0, st, a, round, bin0, nbins);
+    hipLaunchKernelGGL(spec_sort2_scatter, dim3(256, nbins), dim3(256), 0, st, o, b, a, round, bin0);
+  } else {
+    hipLaunchKernelGGL(spec_sort_count, dim3(256, nbins), dim3(256), 0, st, b, a, round, bin0);
+    hipLaunchKernelGGL(spec_sort_scan, dim3(nbins), dim3(256), 0, st, a, round, bin0);
+    hipLaunchKernelGGL(spec_sort_scatter, dim3(256, nbins), dim3(256), 0, st, b, a, round, bin0);
+  }
+}
+
+// Only the bins the batch's longest read reaches are launched: a persistent
+// grid over an empty list still waits for CU slots that the other caller
+// stream's extension kernel holds, and its stream waits with it.  Round C
+// (mispredicted seeds of long reads: rare) runs on small grids for the same
+// reason.
 static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int round,
                              int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
@@ -2474,39 +2501,22 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const auto grid = [round, quad](int nb) { return round == 2 ? std::min(nb, 64) : ext2_grid(nb, quad); };
   const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]), oct = key8 && form == 0;
   const size_t lds2 = quad ? ext4_lds(tb_bytes, 32) : ext2_lds(tb_bytes);
-  if (quad && ext_phased()) {
-    hipLaunchKernelGGL(spec_sort2_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
-    hipLaunchKernelGGL(spec_sort2_scan, dim3(4), dim3(256), 0, st, a, round);
-    hipLaunchKernelGGL(spec_sort2_scatter, dim3(256, 2), dim3(256), 0, st, o, b, a, round);
-    const int cap = ext2_grid(1 << 30, true);
-    const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
-    if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
+  const int pm = quad ? ext_phased_mask() : 0;
+  const bool p0 = pm & 1, p1 = (pm >> 1) & 1;
+  if (!bin1 || p0 == p1) {
+    launch_sort(o, b, a, round, p0, 0, bin1 ? 2 : 1, st);
+  } else {
+    launch_sort(o, b, a, round, p0, 0, 1, st);
+    launch_sort(o, b, a, round, p1, 1, 1, st);
+  }
+  const int cap = ext2_grid(1 << 30, true);
+  const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
+  if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
+  if (p0) {
     if (oct) launch_side_pair<16, kSpecBinLen[0] / 16, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
     else if (key8) launch_side_pair<32, kSpecBinLen[0] / 32, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
     else launch_side_pair<32, kSpecBinLen[1] / 32, false>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
-    if (prof) {
-      (void)hipEventRecord(ss.pool[*ss.pool_used + 1], st);
-      *ss.pool_used += 2;
-    }
-    if (bin1) {
-      if (form == 0) launch_side_pair<16, kSpecBinLen[1] / 16, false>(o, ref, b, a, l + 1, tb_bytes, st, cap, round);
-      else launch_side_pair<32, kSpecBinLen[1] / 32, false>(o, ref, b, a, l + 1, tb_bytes, st, cap, round);
-    }
-    if (bin2) {
-      const int nb = resident_blocks(spec_ext_kernel<16>, lds);
-      hipLaunchKernelGGL(spec_ext_kernel<16>, dim3(round == 2 ? std::min(nb, 64) : nb), dim3(kBlock), lds, st, o, ref,
-                         b, a, l + 2, tb_bytes);
-    }
-    return;
-  }
-  // the first two length bins' lists in pair order (spec_sort_*), then two,
-  // four or eight seeds per wave; the third (reads > 256 bp) one seed per wave
-  hipLaunchKernelGGL(spec_sort_count, dim3(256, 2), dim3(256), 0, st, b, a, round);
-  hipLaunchKernelGGL(spec_sort_scan, dim3(2), dim3(256), 0, st, a, round);
-  hipLaunchKernelGGL(spec_sort_scatter, dim3(256, 2), dim3(256), 0, st, b, a, round);
-  const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
-  if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
-  if (oct) {
+  } else if (oct) {
     const size_t lds8 = ext4_lds(tb_bytes, 16);
     const int nb = resident_blocks(spec_ext4_kernel<16, kSpecBinLen[0] / 16, true>, lds8);
     hipLaunchKernelGGL((spec_ext4_kernel<16, kSpecBinLen[0] / 16, true>), dim3(grid(nb)), dim3(kBlock), lds8, st, o,
@@ -2529,7 +2539,10 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
     *ss.pool_used += 2;
   }
   if (!bin1) return;
-  if (quad && form == 0) {  // eight per wave, the row-max key widened per call (H may reach 256 and more)
+  if (p1) {
+    if (form == 0) launch_side_pair<16, kSpecBinLen[1] / 16, false>(o, ref, b, a, l + 1, tb_bytes, st, cap, round);
+    else launch_side_pair<32, kSpecBinLen[1] / 32, false>(o, ref, b, a, l + 1, tb_bytes, st, cap, round);
+  } else if (quad && form == 0) {  // eight per wave, the row-max key widened per call (H may reach 256 and more)
     const size_t lds8 = ext4_lds(tb_bytes, 16);
     const int nb = resident_blocks(spec_ext4_kernel<16, kSpecBinLen[1] / 16, false>, lds8);
     hipLaunchKernelGGL((spec_ext4_kernel<16, kSpecBinLen[1] / 16, false>), dim3(grid(nb)), dim3(kBlock), lds8, st, o,

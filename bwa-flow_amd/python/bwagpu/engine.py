@@ -291,7 +291,10 @@ class Engine:
 
     # bwagpu_debug_ext_kernel codes -> the first bin's extension kernel
     EXT_KERNELS = {8: "spec_ext4_kernel<16, 10, true>", 4: "spec_ext4_kernel<32, 5, true>",
-                   5: "spec_ext4_kernel<32, 8, false>", 2: "spec_ext2_kernel<5>"}
+                   5: "spec_ext4_kernel<32, 8, false>", 2: "spec_ext2_kernel<5>",
+                   # the phased pair: one "launch" = its left and right side launches
+                   18: "spec_side4_kernel<16, 10, true>", 14: "spec_side4_kernel<32, 5, true>",
+                   15: "spec_side4_kernel<32, 8, false>"}
 
     def ext_kernel(self, lq_max: int = 256) -> str:
         """the first length bin's extension kernel this context launches for

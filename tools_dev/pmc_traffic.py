@@ -36,6 +36,16 @@ for sub, c in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
         e = out["per_launch"].setdefault(k, {"dispatches": len(v)})
         e["fetch_bytes" if c == "FETCH_SIZE" else "write_bytes"] = sum(v) / len(v)
         tot[c] += sum(v)
+# the phased extension's side pair (spec_side4_kernel<G, P, K8, false|true>:
+# every left call, then every right call) is one "launch" of the dominant
+# kernel: its entry sums the two sides' per-dispatch bytes
+for k in [k for k in out["per_launch"] if k.startswith("spec_side4_kernel<") and k.endswith(", false>")]:
+    r = k[:-len(", false>")] + ", true>"
+    if r in out["per_launch"]:
+        L, R = out["per_launch"][k], out["per_launch"][r]
+        out["per_launch"][k[:-len(", false>")] + ">"] = {
+            "dispatches": min(L["dispatches"], R["dispatches"]), "pair": "left + right side launch",
+            **{f: L.get(f, 0.0) + R.get(f, 0.0) for f in ("fetch_bytes", "write_bytes")}}
 for k, e in out["per_launch"].items():
     e["traffic_bytes"] = e.get("fetch_bytes", 0.0) + e.get("write_bytes", 0.0)
     e["traffic_bytes_fetch_x2"] = 2 * e.get("fetch_bytes", 0.0) + e.get("write_bytes", 0.0)

@@ -6,7 +6,8 @@
 Launch sequences are split at spec_reads_kernel (the first launch of every
 mem_chain2aln batch) in launch (correlation) order; sequences warmup ..
 warmup+steps-1 are the timed steps.  For the named kernel (default the
-dominant spec_ext2_kernel<5>) it prints the SUM of its launch durations and the
+dominant spec_ext2_kernel<5>; a name without its last template argument
+takes both sides of the phased pair) it prints the SUM of its launch durations and the
 UNION of its launch intervals inside the timed window (the busy time: overlapping
 launches of the two caller streams count once), per step, beside the window's
 wall time per step; then each kernel family's union per step.  --timeline K
@@ -64,7 +65,11 @@ def analyse(path, warmup=3, steps=20, kernel="spec_ext2_kernel<5>"):
     t0 = min(r["s"] for r in timed)
     t1 = max(r["e"] for r in timed)
     wall = (t1 - t0) / 1e6
-    k = [(r["s"], r["e"]) for r in timed if r["name"] == kernel]
+    # a name without its last template argument (spec_side4_kernel<16, 10, true>)
+    # takes every instance (the phased pair's left and right sides)
+    pre = kernel[:-1] + ", "
+    k = [(r["s"], r["e"]) for r in timed if r["name"] == kernel or r["name"].startswith(pre)]
+    per = 2 if any(r["name"].startswith(pre) for r in timed) else 1  # launches per pair
     fam = defaultdict(list)
     for r in timed:
         fam[r["name"]].append((r["s"], r["e"]))
@@ -76,6 +81,7 @@ def analyse(path, warmup=3, steps=20, kernel="spec_ext2_kernel<5>"):
         "kernel_sum_ms_per_step": round(sum(e - s for s, e in k) / 1e6 / steps, 4),
         "kernel_busy_ms_per_step": round(union(k) / 1e6 / steps, 4),
         "kernel_avg_launch_ms": round(sum(e - s for s, e in k) / 1e6 / max(len(k), 1), 4),
+        "kernel_avg_pair_ms": round(per * sum(e - s for s, e in k) / 1e6 / max(len(k), 1), 4),
         "families_busy_ms_per_step": {n: round(union(v) / 1e6 / steps, 4)
                                       for n, v in sorted(fam.items(), key=lambda x: -union(x[1]))},
     }
