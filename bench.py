@@ -97,7 +97,8 @@ PK16_PEAK_TOPS = 2 * VALU_PEAK_TOPS
 # H max 2, row max + argmax 3, E 4, F 4, profile lookup 1.
 OPS_PER_CELL = 17
 # the first-bin extension launch of every round (set in run_stage from the options)
-# the phased pair (left + right side launches); "spec_ext4_kernel<16, 10, true>"
+# the phased pair (left + right side launches; "spec_sidep_kernel<16, 10, true>"
+# with BWAGPU_EXT_PRODUCER=1), "spec_ext4_kernel<16, 10, true>"
 # with BWAGPU_EXT_PHASED=0, "spec_ext2_kernel<5>" with --ext-form 1 (engine.ext_kernel)
 DOMINANT_KERNEL = "spec_side4_kernel<16, 10, true>"
 
@@ -782,7 +783,10 @@ def regime_stage(dev, steps: int = 10, n_streams: int = 2, ext_form: int = 0) ->
              "ms_per_batch": round(el * 1e3 / steps, 4), "value": round(s.batch.n_reads * steps / el / 1e6, 4),
              "unit": "Mreads/s", "gcups": round(float(st[0]) / el / 1e9, 3),
              "parity_all_steps": why is None, "coverage": s.coverage,
-             "ext_busy_ms_per_batch": round(ext_busy / steps, 4)}
+             "ext_busy_ms_per_batch": round(ext_busy / steps, 4),
+             "batch": ("tests/golden/c3_refseed.npz (the C2 fixture's batch 0 in the GRCh38-shaped regime)"
+                       if name == "c3_refseed" else f"tests/golden/c3_grch38.npz set {name!r}") +
+                      f", the same batch every step"}
         if why:
             r["mismatch"] = why
         if name in ("c3", "c3_refseed") and ext_busy > 0:  # 150 bp: every task is in the first length bin
@@ -1257,7 +1261,7 @@ def headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapse
                      "kernel_sum_ms_per_step": round(ext_ms / args.steps, 4), "launches_timed": ext_launches,
                      "avg_launch_ms": round(ext_avg_ms, 4),
                      "launch_unit": ("one round's left + right side launches (the phased pair, HIP events "
-                                     "bracket both)" if "side4" in DOMINANT_KERNEL else "one launch per round"),
+                                     "bracket both)" if "spec_side" in DOMINANT_KERNEL else "one launch per round"),
                      # the kernel alone on the GPU (one stream, one batch at a time)
                      "isolated_launch_ms": iso, "frac_isolated": round(frac_iso, 5) if frac_iso else None,
                      "tasks_round_a_b": tasks_ab,

@@ -1162,7 +1162,7 @@ __device__ __forceinline__ int64_t uni64(int64_t v) {
 // under exactly that key; GPU worker threads of several contexts call this
 // concurrently.
 template <typename K>
-static int resident_blocks(K kernel, size_t lds) {
+static int resident_blocks(K kernel, size_t lds, int block = kBlock) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
   struct Key {
@@ -1181,7 +1181,7 @@ static int resident_blocks(K kernel, size_t lds) {
   }
   int ncu = 0, per = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1024;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kBlock, lds) != hipSuccess || per < 1) per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, lds) != hipSuccess || per < 1) per = 1;
   std::lock_guard<std::mutex> g(mu);
   return cache[key] = per * ncu;
 }

@@ -1504,6 +1504,276 @@ __global__ void __launch_bounds__(kBlock) spec_side4_kernel(DevOpt o, DevRef ref
 
 static size_t side4_lds(int tb_bytes, int g) { return (size_t)(kBlock / g) * (2 * (size_t)tb_bytes + 2 * kSideLds); }
 
+// ------------------------------------ the side kernel with a producer wave
+// spec_side4_kernel's waves spent 17.5 % of their cycles at call starts: the
+// claim, then the FatTask, then the target rows, three dependent round trips
+// with nothing to hide them at one wave per SIMD (tools_dev/occ_diag.py,
+// r06h).  spec_sidep_kernel pairs every DP wave with a producer wave that
+// does only that: every call slot has a second buffer (the side's state, its
+// target rows and its query bytes, all in LDS), and the producer keeps those
+// filled, so a DP wave's next call starts from LDS.  A DP wave claims and
+// fills its own first calls (as spec_side4_kernel) while its producer fills
+// the second buffers.  Buffer b = k * 32 + group * 2 + half (k: which of the
+// slot's two): kBufBusy = the DP wave's, kBufEmpty = the producer's to fill,
+// kBufReady = filled.  A producer raises its `ex` once it leaves (the queue's
+// tail: BWAGPU_SIDEP_RETIRE), after its last kBufReady; the DP wave then
+// claims for itself.
+constexpr int kBufEmpty = 0, kBufReady = 1, kBufBusy = 2;
+__host__ __device__ constexpr int sidep_buf_bytes(int tb_bytes, int qb) { return (tb_bytes + qb + kSideLds + 15) & ~15; }
+
+__device__ __forceinline__ int lds_ld(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// a buffer state after every LDS access of this wave before it (the DP's reads
+// of the rows; the producer's writes of them): lgkmcnt only, so that the
+// wave's outstanding global stores (SeedExt) are not waited for
+__device__ __forceinline__ void lds_publish(int* p, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// a call slot's buffer: target rows (tb_bytes) | query bytes in column order (qb) | SideTask
+template <int G, bool RIGHT>
+__device__ __forceinline__ void side_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
+                                          const FatTask& f, uint8_t* buf, int tb_bytes, int qb) {
+  const int r = (int)(threadIdx.x & (G - 1));
+  const int qbeg = (int)(f.qls & 1023u), len = (int)((f.qls >> 10) & 1023u), lq = (int)(f.qls >> 20);
+  const int qlen = min(RIGHT ? lq - qbeg - len : qbeg, qb);
+  const uint8_t* q = b.seq + f.qoff + (RIGHT ? qbeg + len : qbeg - 1);
+  uint8_t* const qd = buf + tb_bytes;
+  for (int j = r; j < qlen; j += G) qd[j] = q[RIGHT ? j : -j];
+  SideTask t;
+  side_start<G, RIGHT>(t, o, ref, a, f, buf);
+  spark((LdsS*)(qd + qb), t);
+}
+
+__device__ __forceinline__ FatTask shfl_fat(const FatTask& f, int src) {
+  FatTask g;
+  g.rbeg = (int64_t)((uint64_t)(uint32_t)__shfl((int)(f.rbeg >> 32), src, 64) << 32 | (uint32_t)__shfl((int)f.rbeg, src, 64));
+  g.qoff = (int64_t)((uint64_t)(uint32_t)__shfl((int)(f.qoff >> 32), src, 64) << 32 | (uint32_t)__shfl((int)f.qoff, src, 64));
+  g.pos = __shfl(f.pos, src, 64);
+  g.dlo = __shfl(f.dlo, src, 64);
+  g.dhi = __shfl(f.dhi, src, 64);
+  g.qls = (uint32_t)__shfl((int)f.qls, src, 64);
+  return g;
+}
+
+template <int G, int PMAX>
+static size_t sidep_lds(int tb_bytes) {
+  constexpr int nbuf = 4 * (kBlock / G);
+  return (size_t)nbuf * sidep_buf_bytes(tb_bytes, PMAX * G) + 4 * (size_t)(nbuf + 4);
+}
+
+template <int G, int PMAX, bool K8, bool RIGHT>
+__global__ void __launch_bounds__(2 * kBlock) spec_sidep_kernel(DevOpt o, DevRef ref, DevBatch b, SpecArgs a, int list,
+                                                                int tb_bytes, int retire) {
+  static_assert(G == 16, "a producer wave per DP wave: 2 buffers x 2 halves x 4 groups = 16 buffers");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int QB = PMAX * G;            // query bytes per buffer (the widest call's columns)
+  constexpr int NBUF = 4 * (kBlock / G);  // 64
+  const int SB = sidep_buf_bytes(tb_bytes, QB);
+  int* const st = reinterpret_cast<int*>(lds + (size_t)NBUF * SB);
+  int* const ex = st + NBUF;  // per DP wave: its producer has left
+  for (int k = threadIdx.x; k < NBUF + 4; k += 2 * kBlock) st[k] = k < NBUF / 2 ? kBufBusy : kBufEmpty;
+  __syncthreads();
+  const int n = uni(__hip_atomic_load(&a.ctr[(RIGHT ? SPC_RCNT : SPC_LCNT) + list], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT));
+  const FatTask* fl = (RIGHT ? a.ftaskR : a.ftask) + spec_list_off(list, b.n_chains, b.n_seeds);
+  int32_t* const heads = a.qh + 8 * kQHStride * (RIGHT ? kSpecRounds * kSpecBins + list : list);
+  ShardQ qq;
+  qq.init(heads, n);
+#ifdef BWAGPU_OCC_DIAG
+  unsigned long long tw[6] = {0, 0, 0, 0, 0, 0}, occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  const int lane = (int)(threadIdx.x & 63);
+  if (threadIdx.x >= kBlock) {  // ---- a producer wave: DP wave pw's 16 buffers, lane l < 16 = buffer bmap(l)
+    // above the DP wave it shares a SIMD with: the arbiter prefers the older
+    // of two ready waves, and a DP wave is nearly always ready
+    __builtin_amdgcn_s_setprio(2);
+    const int pw = (int)(threadIdx.x - kBlock) >> 6;
+    const auto bmap = [pw](int l) { return (l >> 3) << 5 | (4 * pw + ((l >> 1) & 3)) << 1 | (l & 1); };
+    const uint64_t below = (1ull << lane) - 1;
+    bool more = n > 0;
+    while (more) {
+#ifdef BWAGPU_OCC_DIAG
+      const unsigned long long p0 = __builtin_amdgcn_s_memtime();
+#endif
+      const uint64_t em = __builtin_amdgcn_ballot_w64(lane < 16 && lds_ld(st + bmap(lane & 15)) == kBufEmpty);
+      if (!em) {
+        __builtin_amdgcn_s_sleep(2);
+#ifdef BWAGPU_OCC_DIAG
+        tw[5] += __builtin_amdgcn_s_memtime() - p0;
+#endif
+        continue;
+      }
+      int m0, cap;
+      if (!qq.claim(__popcll(em), m0, cap)) break;
+      const int idx = m0 + __popcll(em & below);
+      const bool mine = ((em >> lane) & 1) && idx < cap;
+      uint64_t v = __builtin_amdgcn_ballot_w64(mine);
+      FatTask f{};
+      if (mine) f = fl[qq.shard + 8 * idx];
+      while (v) {  // four buffers at a time, a group of G lanes each
+        int bsel = -1;
+#pragma unroll
+        for (int g = 0; g < 64 / G; ++g) {
+          const int bq = v ? __builtin_ctzll(v) : -1;
+          v &= v - 1;
+          bsel = lane / G == g ? bq : bsel;
+        }
+        const FatTask g = shfl_fat(f, max(bsel, 0));
+        const int bb = bmap(max(bsel, 0));
+        if (bsel >= 0) side_prep<G, RIGHT>(o, ref, b, a, g, lds + (size_t)bb * SB, tb_bytes, QB);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the buffers' rows, query and state first
+        if (bsel >= 0) __hip_atomic_store(st + bb, kBufReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#ifdef BWAGPU_OCC_DIAG
+      tw[4] += __builtin_amdgcn_s_memtime() - p0;
+#endif
+      // the queue's tail goes to the DP waves' own claims: a call claimed ahead
+      // waits behind its slot's current one while other slots run dry
+      if (cap - m0 - __popcll(em) < retire) break;
+    }
+    lds_publish(ex + pw, 1);
+  } else {  // ---- a DP wave: eight call slots, half A / B of four groups
+    const int gi = (int)threadIdx.x / G, gw = lane / G;
+    const auto bidx = [gi](int h, int k) { return (k << 5) | (gi << 1) | h; };
+    const auto bufp = [&](int h, int k) { return lds + (size_t)bidx(h, k) * SB; };
+    constexpr uint64_t kLead = 0x0001000100010001ull;  // each group's first lane
+    const uint64_t below = kLead & ((1ull << (lane & (64 - G))) - 1);
+    bool ha = false, hb = false, fa = false, fb = false, dry = false;
+    int ka = 0, kb = 0;  // the buffer of the slot's call (or its last one)
+    long long spec_cells = 0;
+    {  // the first calls: this wave's own claim (the producer fills the second buffers meanwhile)
+      int m0, cap;
+      if (n > 0 && qq.claim(2 * (64 / G), m0, cap)) {
+        const int ia = m0 + 2 * gw, ib = ia + 1;
+        if (ia < cap) {
+          side_prep<G, RIGHT>(o, ref, b, a, fl[qq.shard + 8 * ia], bufp(0, 0), tb_bytes, QB);
+          ha = true;
+        }
+        if (ib < cap) {
+          side_prep<G, RIGHT>(o, ref, b, a, fl[qq.shard + 8 * ib], bufp(1, 0), tb_bytes, QB);
+          hb = true;
+        }
+      }
+      lds_publish(st + bidx(0, 0), ha ? kBufBusy : kBufEmpty);  // a slot without a first call: the producer's
+      lds_publish(st + bidx(1, 0), hb ? kBufBusy : kBufEmpty);
+    }
+    for (;;) {
+#ifdef BWAGPU_OCC_DIAG
+      const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+      // a slot without a call takes a filled buffer: its other one (filled
+      // while this call ran), else the one it just gave back (the producer may
+      // have refilled that first).  Once the producer has left (`ex`, after
+      // its last kBufReady) and neither is filled, the wave claims for the slot
+      // itself (the queue's tail), into the slot's free buffer.
+      const auto take = [&](int h, int& k, bool& has, bool& own, bool last) {
+        own = false;
+        if (has) return;
+        const int so = lds_ld(st + bidx(h, k ^ 1)), sk = lds_ld(st + bidx(h, k));
+        if (so == kBufReady) {
+          has = true;
+          k ^= 1;
+        } else if (sk == kBufReady) {
+          has = true;
+        } else {
+          own = last;
+        }
+      };
+      for (;;) {
+        const bool last = __hip_atomic_load(ex + (threadIdx.x >> 6), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;  // before the states
+        bool oa, ob;
+        take(0, ka, ha, oa, last && !fa);
+        take(1, kb, hb, ob, last && !fb);
+        const uint64_t na = __builtin_amdgcn_ballot_w64(oa) & kLead, nb = __builtin_amdgcn_ballot_w64(ob) & kLead;
+        if (na | nb) {
+          int m0, cap;
+          if (!dry && qq.claim(__popcll(na) + __popcll(nb), m0, cap)) {
+            const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (oa ? 1 : 0);
+            if (oa && ia < cap) {
+              side_prep<G, RIGHT>(o, ref, b, a, fl[qq.shard + 8 * ia], bufp(0, ka), tb_bytes, QB);
+              ha = true;
+            }
+            if (ob && ib < cap) {
+              side_prep<G, RIGHT>(o, ref, b, a, fl[qq.shard + 8 * ib], bufp(1, kb), tb_bytes, QB);
+              hb = true;
+            }
+          } else {
+            dry = true;
+            fa = fa || oa;
+            fb = fb || ob;
+          }
+        }
+        if (!__builtin_amdgcn_ballot_w64((!ha && !fa) || (!hb && !fb))) break;
+        if (!(na | nb)) __builtin_amdgcn_s_sleep(1);
+      }
+      if (!__builtin_amdgcn_ballot_w64(ha || hb)) break;
+#ifdef BWAGPU_OCC_DIAG
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      tw[0] += c1 - c0;
+#endif
+      uint8_t* const pa = bufp(0, ka);
+      uint8_t* const pb = bufp(1, kb);
+      LdsS* const sa = (LdsS*)(pa + tb_bytes + QB);
+      LdsS* const sb = (LdsS*)(pb + tb_bytes + QB);
+      QCall ca = quad_idle(pa + tb_bytes, pa), cb = quad_idle(pb + tb_bytes, pb);  // every query pointer in LDS
+      if (ha) {
+        ca = side_call<RIGHT>(sload(sa), o, b.seq, pa);
+        ca.q = pa + tb_bytes;
+        ca.qa = 0;
+        ca.qd = 1;
+      }
+      if (hb) {
+        cb = side_call<RIGHT>(sload(sb), o, b.seq, pb);
+        cb.q = pb + tb_bytes;
+        cb.qa = 0;
+        cb.qd = 1;
+      }
+      ExtOut xa, xb;
+      Tally32 tla{0, 0, 0}, tlb{0, 0, 0};
+#ifdef BWAGPU_OCC_DIAG
+      const unsigned long long c2 = __builtin_amdgcn_s_memtime();
+      tw[1] += c2 - c1;
+#endif
+      extend_quad_dispatch<G, PMAX, K8>(o, ca, cb, xa, xb, tla, tlb);
+#ifdef BWAGPU_OCC_DIAG
+      const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+      tw[2] += c3 - c2;
+      occ_diag<G>(occ, ca, cb, tla, tlb);
+#endif
+      if (ha) {
+        SideTask t = sload(sa);
+        if (side_advance<G, RIGHT>(t, o, a, xa, tla, spec_cells)) {
+          ha = false;
+          lds_publish(st + bidx(0, ka), kBufEmpty);
+        } else {
+          spark(sa, t);
+        }
+      }
+      if (hb) {
+        SideTask t = sload(sb);
+        if (side_advance<G, RIGHT>(t, o, a, xb, tlb, spec_cells)) {
+          hb = false;
+          lds_publish(st + bidx(1, kb), kBufEmpty);
+        } else {
+          spark(sb, t);
+        }
+      }
+#ifdef BWAGPU_OCC_DIAG
+      tw[3] += __builtin_amdgcn_s_memtime() - c3;
+#endif
+    }
+    if ((threadIdx.x & (G - 1)) == 0 && spec_cells)
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
+  }
+#ifdef BWAGPU_OCC_DIAG
+  if (lane == 0) {
+    for (int k = 0; k < 8; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 32) + k, occ[k]);
+    for (int k = 0; k < 6; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + 48) + k, tw[k]);
+  }
+#endif
+}
+
 // The pair kernel's grid: its waves pull tasks from the queue, so the grid
 // only sets its occupancy.  2 workgroups per CU (8 waves per CU, 2 per SIMD)
 // instead of the resident capacity (5 per SIMD): the batch on the other caller
@@ -2423,13 +2693,25 @@ static int ext_phased_mask() {
   return m;
 }
 
+// the phased pair with producer waves (spec_sidep_kernel; the first bin's
+// eight-per-wave form only): BWAGPU_EXT_PRODUCER=1.  Off by default: it lost
+// on every A/B (C2 43.6-47.4 vs 50.9-54.5 Mreads/s)
+static bool ext_producer() {
+  static const bool on = [] {
+    const char* e = getenv("BWAGPU_EXT_PRODUCER");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 static std::atomic<int> g_ext_form{0};
 int ext_form() { return g_ext_form.load(std::memory_order_relaxed); }
 int ext_kernel_for(const DevOpt& o, int form, int tb_bytes) {  // launch_ext_round's choice, first bin
   const bool quad = form != 1 && quad_scores_ok(o, kSpecBinLen[1]) && quad_rows_ok(o, tb_bytes);
   const bool key8 = quad && quad_key8_ok(o, kSpecBinLen[0]);
   const int k = key8 ? (form == 0 ? 8 : 4) : (quad ? 5 : 2);
-  return quad && (ext_phased_mask() & 1) ? 10 + k : k;  // 1x: the phased pair (spec_side4_kernel)
+  if (!quad || !(ext_phased_mask() & 1)) return k;
+  // the phased pair: 28 with the producer wave (spec_sidep_kernel), 1x spec_side4_kernel
+  return k == 8 && ext_producer() && sidep_lds<16, kSpecBinLen[0] / 16>(tb_bytes) <= 64 * 1024 ? 28 : 10 + k;
 }
 int set_ext_form(int form) {  // the default of contexts made later; -> the previous one (form < 0: query only)
   const int prev = g_ext_form.load(std::memory_order_relaxed);
@@ -2468,6 +2750,26 @@ static void launch_side_pair(const DevOpt& o, const DevRef& ref, const DevBatch&
                      tb_bytes);
   hipLaunchKernelGGL((spec_side4_kernel<G, PMAX, K8, true>), dim3(gr), dim3(kBlock), lds, st, o, ref, b, a, l,
                      tb_bytes);
+}
+
+template <int G, int PMAX, bool K8>
+static bool launch_sidep_pair(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int l,
+                              int tb_bytes, hipStream_t st, int grid_cap, int round) {
+  const size_t lds = sidep_lds<G, PMAX>(tb_bytes);
+  if (!ext_producer() || lds > 64 * 1024) return false;
+  // the producer leaves its shard's last `retire` entries to the DP waves'
+  // own claims (BWAGPU_SIDEP_RETIRE; 1 024 = one call per call slot of an XCD)
+  static const int retire = [] {
+    const char* e = getenv("BWAGPU_SIDEP_RETIRE");
+    return e && e[0] ? std::max(atoi(e), 0) : 1024;
+  }();
+  const int nb = resident_blocks(spec_sidep_kernel<G, PMAX, K8, false>, lds, 2 * kBlock);
+  const int gr = round == 2 ? std::min(nb, 64) : std::min(nb, grid_cap);
+  hipLaunchKernelGGL((spec_sidep_kernel<G, PMAX, K8, false>), dim3(gr), dim3(2 * kBlock), lds, st, o, ref, b, a, l,
+                     tb_bytes, retire);
+  hipLaunchKernelGGL((spec_sidep_kernel<G, PMAX, K8, true>), dim3(gr), dim3(2 * kBlock), lds, st, o, ref, b, a, l,
+                     tb_bytes, retire);
+  return true;
 }
 
 // the length bins' lists in the order their kernels take them: pair order
@@ -2513,8 +2815,10 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
   const bool prof = ss.pool && *ss.pool_used + 2 <= ss.pool_n;
   if (prof) (void)hipEventRecord(ss.pool[*ss.pool_used], st);
   if (p0) {
-    if (oct) launch_side_pair<16, kSpecBinLen[0] / 16, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
-    else if (key8) launch_side_pair<32, kSpecBinLen[0] / 32, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
+    if (oct) {
+      if (!launch_sidep_pair<16, kSpecBinLen[0] / 16, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round))
+        launch_side_pair<16, kSpecBinLen[0] / 16, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
+    } else if (key8) launch_side_pair<32, kSpecBinLen[0] / 32, true>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
     else launch_side_pair<32, kSpecBinLen[1] / 32, false>(o, ref, b, a, l + 0, tb_bytes, st, cap, round);
   } else if (oct) {
     const size_t lds8 = ext4_lds(tb_bytes, 16);

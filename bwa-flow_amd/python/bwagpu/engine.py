@@ -294,7 +294,7 @@ class Engine:
                    5: "spec_ext4_kernel<32, 8, false>", 2: "spec_ext2_kernel<5>",
                    # the phased pair: one "launch" = its left and right side launches
                    18: "spec_side4_kernel<16, 10, true>", 14: "spec_side4_kernel<32, 5, true>",
-                   15: "spec_side4_kernel<32, 8, false>"}
+                   15: "spec_side4_kernel<32, 8, false>", 28: "spec_sidep_kernel<16, 10, true>"}
 
     def ext_kernel(self, lq_max: int = 256) -> str:
         """the first length bin's extension kernel this context launches for

@@ -98,7 +98,9 @@ int bwagpu_ctx_row_bound(bwagpu_ctx_t *ctx, int on);
    4 = four per wave with the 8-bit row-max key (<32,5,true>), 5 = four per
    wave (<32,8,false>), 2 = two per wave (spec_ext2_kernel<5>); 18 / 14 / 15 =
    the same shapes as the phased pair spec_side4_kernel<G,PMAX,K8,{false,true}>
-   (every left call, then every right call; BWAGPU_EXT_PHASED bit 0) */
+   (every left call, then every right call; BWAGPU_EXT_PHASED bit 0); 28 = the
+   eight-per-wave pair with a producer wave, spec_sidep_kernel<16,10,true,*>
+   (BWAGPU_EXT_PRODUCER) */
 int bwagpu_debug_ext_kernel(bwagpu_ctx_t *ctx, int32_t lq_max);
 /* 1 if work on the two streams (hipStream_t, on the current device) runs
    concurrently, 0 if they share a hardware queue (HIP maps the process's

@@ -9,6 +9,8 @@ cells beyond a live call's query, outside ksw's band, and computed
   beyond_q   columns past a live call's own query (columns set by the longest)
   out_band   inside the query but outside ksw's band
   computed   cells computed (the row bound's live rows only)
+With spec_sidep_kernel (the producer wave) start_claim is a DP wave's wait for
+its next buffer, and claim / taskrec are the producer wave's busy / idle cycles.
     BWAGPU_LIB=bwa-flow_amd/lib/diag/libbwagpu.so python tools_dev/occ_diag.py [row_bound 0|1]"""
 import ctypes as C
 import json
@@ -35,7 +37,8 @@ def main():
     opt, ref, bs = workload.load_fixture()
     eng = Engine(0, opt, ref.l_pac, ref.ann_offset, ref.ann_len, pac=ref.pac)
     eng.row_bound(bound)
-    out = {"row_bound": bound, "lib": abi.lib_path()}
+    out = {"row_bound": bound, "lib": abi.lib_path(), "kernel": eng.ext_kernel(160),
+           "env": {k: v for k, v in os.environ.items() if k.startswith("BWAGPU_")}}
     for k, rb in enumerate(bs):
         b = rb.batch
         t = {f: torch.from_numpy(np.ascontiguousarray(getattr(b, f)).view(np.uint8).copy()).to(dev) for f in FIELDS}

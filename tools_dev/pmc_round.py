@@ -31,7 +31,7 @@ for sub in ("pmc_a", "pmc_b"):
             if sub == "pmc_a":
                 disp[k].add(r["Dispatch_Id"])
 n_seq = len(disp.get("spec_reads_kernel", ())) or 1
-for k in [k for k in tot if k.startswith("spec_side4_kernel<") and k.endswith(", false>")]:  # the phased pair
+for k in [k for k in tot if k.startswith(("spec_side4_kernel<", "spec_sidep_kernel<")) and k.endswith(", false>")]:  # the phased pair
     r, pk = k[:-len(", false>")] + ", true>", k[:-len(", false>")] + ">"
     if r in tot:
         for n in set(tot[k]) | set(tot[r]):
@@ -46,7 +46,7 @@ for k, c in sorted(tot.items(), key=lambda x: -x[1].get("SQ_WAVE_CYCLES", 0)):
         e["share_active"] = round(c.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4)
         e["share_wait_inst"] = round(c.get("SQ_WAIT_INST_ANY", 0) / wc, 4)
         e["share_wait_any"] = round(c.get("SQ_WAIT_ANY", 0) / wc, 4)
-    if k.startswith("spec_ext") or (k.startswith("spec_side4") and k.count(",") == 2):
+    if k.startswith("spec_ext") or (k.startswith(("spec_side4", "spec_sidep")) and k.count(",") == 2):
         e["valu_lane_ops_per_cell"] = round(c["SQ_INSTS_VALU"] / n_seq * 64 / cells, 2)
         e["lds_insts_per_kcell"] = round(c.get("SQ_INSTS_LDS", 0) / n_seq / cells * 1e3, 3)
         if c.get("SQ_INSTS_LDS"):

@@ -39,7 +39,7 @@ for sub, c in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
 # the phased extension's side pair (spec_side4_kernel<G, P, K8, false|true>:
 # every left call, then every right call) is one "launch" of the dominant
 # kernel: its entry sums the two sides' per-dispatch bytes
-for k in [k for k in out["per_launch"] if k.startswith("spec_side4_kernel<") and k.endswith(", false>")]:
+for k in [k for k in out["per_launch"] if k.startswith(("spec_side4_kernel<", "spec_sidep_kernel<")) and k.endswith(", false>")]:
     r = k[:-len(", false>")] + ", true>"
     if r in out["per_launch"]:
         L, R = out["per_launch"][k], out["per_launch"][r]
