@@ -1153,7 +1153,7 @@ def headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapse
     # the same kernel with the GPU to itself: each distinct batch (up to 8) alone
     # on one stream, its first-bin launches (rounds A, B, C) timed by HIP events
     n_iso = min(nb, 8)
-    iso, ext_tasks, tasks_ab = [], [], []
+    iso, ext_tasks, tasks_ab, misses = [], [], [], []
     for i in range(n_iso):
         eng.prof_start(3)
         dbs[i].run(eng, sptr, 0, stats=False)
@@ -1163,6 +1163,7 @@ def headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapse
         eng.lib.bwagpu_debug_spec_counters(eng.ctx, ctypes.c_void_p(sptr), sc.ctypes.data_as(ctypes.c_void_p))
         ext_tasks.append(int(sc[0] + sc[1]))
         tasks_ab.append([int(sc[0]), int(sc[1])])
+        misses.append(int(sc[4]))
     eng.prof_start(0)
     runs = {j: sum(1 for i in range(args.steps) if i % nb == j) for j in range(nb)}
     # the cells ksw_extend2 itself evaluates (ksw.c:424 iterations): each distinct
@@ -1265,6 +1266,8 @@ def headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapse
                      # the kernel alone on the GPU (one stream, one batch at a time)
                      "isolated_launch_ms": iso, "frac_isolated": round(frac_iso, 5) if frac_iso else None,
                      "tasks_round_a_b": tasks_ab,
+                     # extensions the selection passes computed inline (a round-B prediction missed them)
+                     "inline_extensions": misses,
                      "traffic": traffic, "traffic_source": traffic_src, "pmc": pmc,
                      "alg_bytes_per_launch": round(ext_alg_bytes),
                      "traffic_over_alg": round(traffic / ext_alg_bytes, 3) if traffic and ext_alg_bytes else None,

@@ -180,14 +180,14 @@ struct Slot {
   hipError_t stream_err = hipSuccess;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   DevBuf d_in, d_win, d_srt, d_prog, d_desc, d_out, d_n, d_stats, d_lists, d_counts;
-  DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo;  // speculative path
+  DevBuf d_cread, d_ext, d_tasks, d_ctr, d_regpos, d_skipf, d_heavy, d_redo, d_rbits;  // speculative path
   DevBuf d_schain, d_hinfo, d_mat, d_cov, d_colent, d_qh, d_longc, d_sorth, d_stasks, d_ftask, d_ftaskR;
   SpecStreams spec;  // created on first use (choose_side)
   bool side_chosen = false;
   void release_scratch() {
     d_win.release(); d_srt.release(); d_prog.release(); d_desc.release(); d_lists.release(); d_counts.release();
     d_cread.release(); d_ext.release(); d_tasks.release(); d_ctr.release(); d_regpos.release(); d_skipf.release();
-    d_heavy.release(); d_redo.release(); d_schain.release(); d_hinfo.release(); d_mat.release(); d_cov.release(); d_colent.release(); d_longc.release();
+    d_heavy.release(); d_redo.release(); d_rbits.release(); d_schain.release(); d_hinfo.release(); d_mat.release(); d_cov.release(); d_colent.release(); d_longc.release();
     d_qh.release();
     d_sorth.release();
     d_stasks.release();
@@ -869,6 +869,8 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_skipf.ensure(sizeof(int32_t) * ns), "hipMalloc(skipf)");
   HIPC(s.d_heavy.ensure(sizeof(int32_t) * nr), "hipMalloc(heavy)");
   HIPC(s.d_redo.ensure(sizeof(int32_t) * nr), "hipMalloc(redo)");
+  HIPC(s.d_rbits.ensure(sizeof(uint32_t) * (nr / 32 + 1)), "hipMalloc(rbits)");
+  HIPC(hipMemsetAsync(s.d_rbits.p, 0, sizeof(uint32_t) * (nr / 32 + 1), st), "memset rbits");
   HIPC(s.d_desc.ensure(sizeof(ReadDesc) * nr), "hipMalloc(desc)");
   HIPC(s.d_schain.ensure(sizeof(int32_t) * ns), "hipMalloc(seedchain)");
   HIPC(s.d_hinfo.ensure(sizeof(int4) * nr), "hipMalloc(hinfo)");
@@ -900,6 +902,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   a.skipf = s.d_skipf.as<int32_t>();
   a.heavy = s.d_heavy.as<int32_t>();
   a.redo = s.d_redo.as<int32_t>();
+  a.rbits = s.d_rbits.as<uint32_t>();
   a.rdesc = s.d_desc.as<ReadDesc>();
   a.seedchain = s.d_schain.as<int32_t>();
   a.hinfo = s.d_hinfo.as<int4>();
@@ -918,6 +921,16 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
     return e ? std::max(0, atoi(e)) : 0;
   }();
   a.ext_prefetch = ext_prefetch;
+  static const int risky_first = [] {  // A/B knob (neutral, off)
+    const char* e = getenv("BWAGPU_LIGHT_RISKY_FIRST");
+    return e && e[0] == '1';
+  }();
+  a.risky_first = risky_first;
+  static const int emu_strict = [] {  // A/B knob (0: misses extended inline)
+    const char* e = getenv("BWAGPU_EMU_STRICT");
+    return !(e && e[0] == '0');
+  }();
+  a.emu_strict = emu_strict;
   a.out = d_out;
   a.out_n = d_n;
   a.stats = d_stats;

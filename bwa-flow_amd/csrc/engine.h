@@ -162,6 +162,7 @@ enum {
   // words 32-59: the packed kernels' occupancy counters (-DBWAGPU_OCC_DIAG)
   SPC_LCNT = 64,      // [list] phased extension: tasks with a left side (spec_side4_kernel's left list)
   SPC_RCNT = 73,      // [list] ... with a right side
+  SPC_LIGHT_CUR = 82, // the final light pass's cursor over the reads without a round-B task
   SPC_WORDS = 128
 };
 // sharded queue heads of the extension task lists (SpecArgs::qh, zeroed per
@@ -209,6 +210,7 @@ struct SpecArgs {
   int32_t* skipf;             // per seed slot: skip flags of chains > 256 seeds
   int32_t* heavy;             // reads with > kSelLight seeds
   int32_t* redo;              // reads the final pass left to the redo pass
+  uint32_t* rbits;            // per read, a bit: the emulate pass left it a round-B task (zeroed per batch)
   ReadDesc* rdesc;            // per read (spec_reads_kernel)
   int32_t* seedchain;         // per seed slot: its chain
   int4* hinfo;                // per heavy-list entry: rd, matrix word offset (-1: none), first column, ns
@@ -223,6 +225,8 @@ struct SpecArgs {
   FatTask* ftask;             // the same lists as FatTask records (the packed kernels); the phased
                               // extension: the tasks with a left side, by that side's length
   FatTask* ftaskR;            // the phased extension: the tasks with a right side, by its length
+  int risky_first;            // spec_select_light<SEL_FINAL>: reads with a round-B task first (BWAGPU_LIGHT_RISKY_FIRST)
+  int emu_strict;             // spec_select_light<SEL_EMULATE>: round-B tasks for uncertain skips too (BWAGPU_EMU_STRICT)
   int ext_prefetch;           // spec_ext4_kernel: claim next tasks a generation ahead while more than
                               // ext_prefetch x 8 x (waves per XCD) remain (0: on demand)
   bwagpu_alnreg_t* out;

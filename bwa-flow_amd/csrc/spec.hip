@@ -2144,15 +2144,56 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
   const uint64_t lt_mask = r ? (~0ull >> (64 - r)) : 0ull;  // lanes below r
   Tally tl{0, 0, 0};
   // static deal: wave w takes reads w, w + NW, ... (light reads cost about the
-  // same; no queue atomics), the next read's descriptor in flight meanwhile
+  // same; no queue atomics), the next read's descriptor in flight meanwhile.
+  // The final pass first takes, in its static share, only the reads the
+  // emulate pass left a round-B task in (rbits): only those can miss, and a
+  // miss is extended inline (one wave, ~0.1 ms per extension, cascades of
+  // several in a read) — so they start first, and every other read is claimed
+  // afterwards in chunks of kLightChunk by whichever wave is free, instead of
+  // waiting behind a wave's misses in its static share.
   const int NW = (int)gridDim.x * (kBlock / 64);
-  int rd = (int)blockIdx.x * (kBlock / 64) + uni((int)(threadIdx.x >> 6));
+  const int w0 = (int)blockIdx.x * (kBlock / 64) + uni((int)(threadIdx.x >> 6));
+  constexpr int kLightChunk = 16;
+  int ph = 0, cb = 0, ce = 0, pbase = w0 - 64 * NW;
+  uint64_t pm = 0;
+  const auto risky = [&](int x) { return ((a.rbits[x >> 5] >> (x & 31)) & 1u) != 0; };
+  const auto next_read = [&]() -> int {
+    if (ph == 0) {  // this wave's static share, the reads with a round-B task, 64 at a time
+      for (;;) {
+        if (pm) {
+          const int i = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          return pbase + i * NW;
+        }
+        pbase += 64 * NW;
+        if (pbase >= b.n_reads) break;
+        const int x = pbase + r * NW;
+        pm = __builtin_amdgcn_ballot_w64(x < b.n_reads && risky(x));
+      }
+      ph = 1;
+    }
+    for (;;) {  // the rest, claimed
+      if (cb >= ce) {
+        int c = 0;
+        if (r == 0) c = atomicAdd(&a.ctr[SPC_LIGHT_CUR], kLightChunk);
+        c = __builtin_amdgcn_readfirstlane(__shfl(c, 0, 64));
+        if (c >= b.n_reads) return b.n_reads;
+        cb = c;
+        ce = min(c + kLightChunk, b.n_reads);
+      }
+      const int y = cb++;
+      if (!risky(y)) return y;
+    }
+  };
+  const bool dyn = MODE == SEL_FINAL && a.risky_first;
+  int rd = dyn ? next_read() : w0;
   ReadDesc dn{};
   if (rd < b.n_reads) dn = a.rdesc[rd];
-  for (; rd < b.n_reads; rd += NW) {
+  for (int nx; rd < b.n_reads; rd = nx) {
     const uint64_t t_start = g_trace ? __builtin_amdgcn_s_memrealtime() : 0;
     const ReadDesc d = uniform_desc(dn);
-    if (rd + NW < b.n_reads) dn = a.rdesc[rd + NW];
+    nx = dyn ? next_read() : rd + NW;
+    if (nx < b.n_reads) dn = a.rdesc[nx];
     if (d.ns > kSelLight || d.nch > kSelLight) continue;  // the heavy kernel's read
     if (d.lq > a.lq_bound) continue;                      // flagged by spec_reads_kernel
     if (d.ns == 0) {
@@ -2258,7 +2299,11 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
       }
     }
     // ---- 2. the sequential decisions, on scalar masks
-    uint64_t ext = 0, skip = pad_m, pend = 0;
+    // (emulate) unc: the seeds from the first pending one on, whose decisions
+    // the final pass may take otherwise; a seed skipped here but maybe not
+    // there gets a round-B task too (spend) — the final pass then never
+    // misses on a light read (a miss is extended inline by one wave)
+    uint64_t ext = 0, skip = pad_m, pend = 0, spend = 0, unc = 0;
     int miss = -1;
     for (int k = 0; k < d.ns; ++k) {
       const uint64_t bit = 1ull << k;
@@ -2270,12 +2315,18 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
         const uint64_t om = ((uint64_t)__builtin_amdgcn_readlane(o_hi, it) << 32 | (uint32_t)__builtin_amdgcn_readlane(o_lo, it)) >> sh & fld;
         if (!(om & ~skip)) {  // skipped: srt[k] = 0 (bwamem.c:709)
           skip |= bit;
+          // certainly skipped in the final pass too iff a region of a seed
+          // decided before any pending one holds it and no seed it overlaps
+          // has an uncertain decision
+          if (MODE == SEL_EMULATE && a.emu_strict && !(computed_m & bit) && (!(cm & ext & ~unc) || (om & unc)))
+            spend |= bit;
           continue;
         }
       }
       if (!(computed_m & bit)) {
         if (MODE == SEL_EMULATE) {
           pend |= bit;  // a round-B task; its region stays unknown in this pass
+          unc |= ~(bit - 1);
           continue;
         }
         miss = k;
@@ -2286,9 +2337,10 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
     // ---- 3. outputs
     if constexpr (MODE == SEL_EMULATE) {
       const int list = kSpecBins + spec_bin(d.lq);
-      const bool pnd = (pend >> r) & 1;
+      const bool pnd = ((pend | spend) >> r) & 1;
       const int p = wave_append(&a.ctr[SPC_CNT + list], pnd);
       if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
+      if (pend && r == 0) atomicOr(&a.rbits[rd >> 5], 1u << (rd & 31));  // the final pass takes it first
     } else {
       if (miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
         const bwagpu_seed_t sm = uni_seed(a.prog[d.s0 + miss]);
@@ -2524,28 +2576,43 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
     // 64 * bw + r over its row's earlier words; only the in-block word is
     // decided seed by seed, on scalar masks.  (One seed per step cost ~256 ns:
     // a dependent row load, a ballot and a branch per seed.)
-    uint64_t ext_w = 0, pend_w = 0;
+    // (emulate, BWAGPU_EMU_STRICT) as in spec_select_light: the seeds from
+    // the first pending one (fp) on are uncertain (unc_w: lane w's word), and
+    // a seed skipped here that the final pass might extend gets a round-B task
+    uint64_t ext_w = 0, pend_w = 0, unc_w = 0;
+    const bool strict = MODE == SEL_EMULATE && a.emu_strict;
+    int fp = ns;
     int miss = -1;
     for (int bw = 0; bw < nw && miss < 0; ++bw) {
       const int kb = 64 * bw, k = kb + r;
       const bool valid = k < ns;
       const int64_t row = tri_off(valid ? k : ns - 1);
-      bool cb = false;
-      for (int w = 0; w < bw; ++w) cb |= (C[row + w] & lane64(ext_w, w)) != 0;
+      bool cb = false, cbc = false;
+      for (int w = 0; w < bw; ++w) {
+        const uint64_t x = C[row + w] & lane64(ext_w, w);
+        cb |= x != 0;
+        if (strict) cbc |= (x & ~lane64(unc_w, w)) != 0;  // held by a region decided before fp
+      }
       uint64_t cin = valid && r > 0 ? C[row + bw] : 0;
       // O matters only where a region contains seed k
-      bool need = valid && (cb || cin != 0), ob = false;
+      bool need = valid && (cb || cin != 0), ob = false, ou = false;
       uint64_t oin = 0;
       if (__builtin_amdgcn_ballot_w64(need)) {
         if (need) {
-          for (int w = 0; w < bw; ++w) ob |= (O[row + w] & ~lane64(skip_w, w)) != 0;
+          for (int w = 0; w < bw; ++w) {
+            const uint64_t x = O[row + w];
+            ob |= (x & ~lane64(skip_w, w)) != 0;
+            if (strict) ou |= (x & lane64(unc_w, w)) != 0;  // overlaps a seed of uncertain decision
+          }
           oin = r > 0 ? O[row + bw] : 0;
         }
       }
       const uint64_t cbm = __builtin_amdgcn_ballot_w64(valid && cb);
       uint64_t obm = __builtin_amdgcn_ballot_w64(valid && ob);
+      const uint64_t cbcm = __builtin_amdgcn_ballot_w64(valid && cbc), oum = __builtin_amdgcn_ballot_w64(valid && ou);
       const uint64_t pres = lane64(present_w, bw);
-      uint64_t comp = lane64(computed_w, bw), skp = lane64(skip_w, bw), ext = 0, pend = 0;
+      uint64_t comp = lane64(computed_w, bw), skp = lane64(skip_w, bw), ext = 0, pend = 0, spend = 0;
+      uint64_t uncb = fp < kb ? ~0ull : 0ull;  // this block's uncertain seeds
       const int nb = min(64, ns - kb);
       for (int i = 0; i < nb; ++i) {
         const uint64_t bit = 1ull << i;
@@ -2553,12 +2620,17 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
         if ((cbm & bit) || (lane64(cin, i) & ext)) {
           if (!(obm & bit) && !(lane64(oin, i) & ~skp)) {  // skipped: srt[k] = 0 (bwamem.c:709)
             skp |= bit;
+            if (strict && !(comp & bit) &&
+                (!((cbcm & bit) || (lane64(cin, i) & ext & ~uncb)) || (oum & bit) || (lane64(oin, i) & uncb)))
+              spend |= bit;
             continue;
           }
         }
         if (!(comp & bit)) {
           if (MODE == SEL_EMULATE) {
             pend |= bit;  // a round-B task; its region stays unknown
+            uncb |= ~(bit - 1);
+            fp = min(fp, kb + i);
             continue;
           }
           if (d.lq > kSpecBinLen[1]) {  // longer reads: the redo pass
@@ -2582,7 +2654,8 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
       }
       ext_w = r == bw ? ext : ext_w;
       skip_w = r == bw ? skp : skip_w;
-      pend_w = r == bw ? pend : pend_w;
+      pend_w = r == bw ? pend | spend : pend_w;
+      unc_w = r == bw ? uncb : unc_w;
       computed_w = r == bw ? comp : computed_w;
     }
     int nreg = 0;
