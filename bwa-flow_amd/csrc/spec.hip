@@ -2124,11 +2124,20 @@ __global__ void __launch_bounds__(64) spec_select_kernel(DevOpt o, DevRef ref, D
 // round-B task (pending: neither extended nor skipped, as in the per-seed
 // form); SEL_FINAL sends the read to the redo pass.
 // A misprediction in the final pass of a light read (a seed the replay must
-// extend has no result: ~10-20 per C2 batch) is extended inline, which takes
-// the kernel to 129 VGPRs (3 waves per SIMD).  Sending it to the redo pass
-// like one of a longer read instead (82 VGPRs) is bit-exact, but measured
-// 19.8-19.9 vs 21.6-21.7 Mreads/s on C2 in round 3 and 29.4-30.2 vs 36.9-37.3
-// in round 4.
+// extend has no result: 10-30 per C2 batch before round 6's strict emulation)
+// was extended inline, which took the kernel to 129 VGPRs (3 waves per SIMD);
+// sending it to the redo pass instead lost in rounds 3-4 (19.8-19.9 vs
+// 21.6-21.7 Mreads/s on C2, then 29.4-30.2 vs 36.9-37.3), while
+// the misses were there to extend.
+// With the strict emulation (BWAGPU_EMU_STRICT, default) a light read's final
+// pass has no miss; -DBWAGPU_LIGHT_INLINE=0 leaves the inline extension out
+// (84 VGPRs instead of 131, no LDS rows; a miss, with BWAGPU_EMU_STRICT=0,
+// then goes to the redo pass like one of a longer read), but the larger
+// resident grid competes with the other records' extension kernels: C2
+// fixture 49.3 / 50.6 vs 51.0 / 52.5 Mreads/s, stream 50.5 vs 51.8 (r06p).
+#ifndef BWAGPU_LIGHT_INLINE
+#define BWAGPU_LIGHT_INLINE 1
+#endif
 template <int MODE>
 __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref, DevBatch b, SpecArgs a,
                                                             int tb_bytes) {
@@ -2299,10 +2308,10 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
       }
     }
     // ---- 2. the sequential decisions, on scalar masks
-    // (emulate) unc: the seeds from the first pending one on, whose decisions
-    // the final pass may take otherwise; a seed skipped here but maybe not
-    // there gets a round-B task too (spend) — the final pass then never
-    // misses on a light read (a miss is extended inline by one wave)
+    // (emulate) unc: the seeds whose decisions the final pass may take
+    // otherwise — the pending ones, every seed extended after one, and every
+    // skip that is not certain; a seed skipped here but maybe not there gets
+    // a round-B task too (spend), so the final pass never misses
     uint64_t ext = 0, skip = pad_m, pend = 0, spend = 0, unc = 0;
     int miss = -1;
     for (int k = 0; k < d.ns; ++k) {
@@ -2318,21 +2327,24 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
           // certainly skipped in the final pass too iff a region of a seed
           // decided before any pending one holds it and no seed it overlaps
           // has an uncertain decision
-          if (MODE == SEL_EMULATE && a.emu_strict && !(computed_m & bit) && (!(cm & ext & ~unc) || (om & unc)))
-            spend |= bit;
+          if (MODE == SEL_EMULATE && a.emu_strict && (!(cm & ext & ~unc) || (om & unc))) {
+            unc |= bit;
+            if (!(computed_m & bit)) spend |= bit;
+          }
           continue;
         }
       }
       if (!(computed_m & bit)) {
         if (MODE == SEL_EMULATE) {
           pend |= bit;  // a round-B task; its region stays unknown in this pass
-          unc |= ~(bit - 1);
+          unc |= bit;
           continue;
         }
         miss = k;
         break;
       }
       ext |= bit;
+      if (MODE == SEL_EMULATE && pend) unc |= bit;  // a pending seed's region may hold it
     }
     // ---- 3. outputs
     if constexpr (MODE == SEL_EMULATE) {
@@ -2342,7 +2354,7 @@ __global__ void __launch_bounds__(kBlock) spec_select_light(DevOpt o, DevRef ref
       if (p >= 0) a.tasks[spec_list_off(list, b.n_chains, b.n_seeds) + p] = make_int2(d.s0 + r, d.c0 + cid);
       if (pend && r == 0) atomicOr(&a.rbits[rd >> 5], 1u << (rd & 31));  // the final pass takes it first
     } else {
-      if (miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
+      if (BWAGPU_LIGHT_INLINE && miss >= 0 && d.lq <= kSpecBinLen[0]) {  // extend seed `miss` here, then the read again
         const bwagpu_seed_t sm = uni_seed(a.prog[d.s0 + miss]);
         const int cm_id = uni(__shfl(cid, miss, 64));
         ChainWin cw = a.win[d.c0 + cm_id];
@@ -2576,9 +2588,10 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
     // 64 * bw + r over its row's earlier words; only the in-block word is
     // decided seed by seed, on scalar masks.  (One seed per step cost ~256 ns:
     // a dependent row load, a ballot and a branch per seed.)
-    // (emulate, BWAGPU_EMU_STRICT) as in spec_select_light: the seeds from
-    // the first pending one (fp) on are uncertain (unc_w: lane w's word), and
-    // a seed skipped here that the final pass might extend gets a round-B task
+    // (emulate, BWAGPU_EMU_STRICT) as in spec_select_light: the seeds of
+    // uncertain decision (unc_w: lane w's word) — pending, extended after the
+    // first pending one (fp), or skipped without certainty — and a seed
+    // skipped here that the final pass might extend gets a round-B task
     uint64_t ext_w = 0, pend_w = 0, unc_w = 0;
     const bool strict = MODE == SEL_EMULATE && a.emu_strict;
     int fp = ns;
@@ -2612,7 +2625,7 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
       const uint64_t cbcm = __builtin_amdgcn_ballot_w64(valid && cbc), oum = __builtin_amdgcn_ballot_w64(valid && ou);
       const uint64_t pres = lane64(present_w, bw);
       uint64_t comp = lane64(computed_w, bw), skp = lane64(skip_w, bw), ext = 0, pend = 0, spend = 0;
-      uint64_t uncb = fp < kb ? ~0ull : 0ull;  // this block's uncertain seeds
+      uint64_t uncb = 0;  // this block's seeds of uncertain decision
       const int nb = min(64, ns - kb);
       for (int i = 0; i < nb; ++i) {
         const uint64_t bit = 1ull << i;
@@ -2620,16 +2633,17 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
         if ((cbm & bit) || (lane64(cin, i) & ext)) {
           if (!(obm & bit) && !(lane64(oin, i) & ~skp)) {  // skipped: srt[k] = 0 (bwamem.c:709)
             skp |= bit;
-            if (strict && !(comp & bit) &&
-                (!((cbcm & bit) || (lane64(cin, i) & ext & ~uncb)) || (oum & bit) || (lane64(oin, i) & uncb)))
-              spend |= bit;
+            if (strict && (!((cbcm & bit) || (lane64(cin, i) & ext & ~uncb)) || (oum & bit) || (lane64(oin, i) & uncb))) {
+              uncb |= bit;
+              if (!(comp & bit)) spend |= bit;
+            }
             continue;
           }
         }
         if (!(comp & bit)) {
           if (MODE == SEL_EMULATE) {
             pend |= bit;  // a round-B task; its region stays unknown
-            uncb |= ~(bit - 1);
+            uncb |= bit;
             fp = min(fp, kb + i);
             continue;
           }
@@ -2651,6 +2665,7 @@ __global__ void __launch_bounds__(64) spec_scan_kernel(DevOpt o, DevRef ref, Dev
           }
         }
         ext |= bit;
+        if (strict && fp < kb + i) uncb |= bit;  // a pending seed's region may hold it
       }
       ext_w = r == bw ? ext : ext_w;
       skip_w = r == bw ? skp : skip_w;
@@ -2727,8 +2742,8 @@ static void launch_select(const DevOpt& o, const DevRef& ref, const DevBatch& b,
     (void)hipStreamWaitEvent(ss.side, ss.fork, 0);
     hs = ss.side;
   }
-  if (MODE != SEL_REDO) {
-    const size_t lds = (size_t)(kBlock / 64) * 2 * tb_bytes;
+  if (MODE != SEL_REDO) {  // target rows in LDS only for the final pass's inline extension
+    const size_t lds = BWAGPU_LIGHT_INLINE && MODE == SEL_FINAL ? (size_t)(kBlock / 64) * 2 * tb_bytes : 0;
     const int nb = resident_blocks(spec_select_light<MODE>, lds);
     hipLaunchKernelGGL((spec_select_light<MODE>), dim3(nb), dim3(kBlock), lds, st, o, ref, b, a, tb_bytes);
   }
