@@ -1402,6 +1402,18 @@ __device__ __forceinline__ bool side_advance(SideTask& t, const DevOpt& o, const
   return true;
 }
 
+// a side's query bytes into LDS in column order (qd[j] = column j), so the DP
+// has no global load (its prologue read them from HBM: a dependent round trip
+// per generation)
+template <int G, bool RIGHT>
+__device__ __forceinline__ void side_query(const DevBatch& b, const FatTask& f, uint8_t* qd, int qb) {
+  const int r = (int)(threadIdx.x & (G - 1));
+  const int qbeg = (int)(f.qls & 1023u), len = (int)((f.qls >> 10) & 1023u), lq = (int)(f.qls >> 20);
+  const int qlen = min(RIGHT ? lq - qbeg - len : qbeg, qb);
+  const uint8_t* q = b.seq + f.qoff + (RIGHT ? qbeg + len : qbeg - 1);
+  for (int j = r; j < qlen; j += G) qd[j] = q[RIGHT ? j : -j];
+}
+
 // The phased extension's kernel: one side (RIGHT = false: left calls, true:
 // right calls) of the tasks of one list, eight calls per wave (G = 16) or four
 // (G = 32) in the packed 16-bit DP (extend_quad), claimed in the list's
@@ -1412,11 +1424,14 @@ __global__ void __launch_bounds__(kBlock) spec_side4_kernel(DevOpt o, DevRef ref
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr uint64_t kLead = G == 16 ? 0x0001000100010001ull : 0x0000000100000001ull;
   const uint64_t below = kLead & ((1ull << ((int)threadIdx.x & (64 - G))) - 1);
-  // per group: A's and B's target rows, then their states
-  uint8_t* const ta_ = lds + (size_t)(threadIdx.x / G) * (2 * (size_t)tb_bytes + 2 * kSideLds);
+  // per group: A's and B's target rows, their states, their query bytes
+  constexpr int QB = PMAX * G;
+  uint8_t* const ta_ = lds + (size_t)(threadIdx.x / G) * (2 * (size_t)tb_bytes + 2 * kSideLds + 2 * QB);
   uint8_t* const tb_ = ta_ + tb_bytes;
   LdsS* const sa = (LdsS*)(tb_ + tb_bytes);
   LdsS* const sb = (LdsS*)(tb_ + tb_bytes + kSideLds);
+  uint8_t* const qa_ = tb_ + tb_bytes + 2 * kSideLds;
+  uint8_t* const qb_ = qa_ + QB;
   const int n = uni(__hip_atomic_load(&a.ctr[(RIGHT ? SPC_RCNT : SPC_LCNT) + list], __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT));
   const FatTask* fl = (RIGHT ? a.ftaskR : a.ftask) + spec_list_off(list, b.n_chains, b.n_seeds);
@@ -1440,13 +1455,17 @@ __global__ void __launch_bounds__(kBlock) spec_side4_kernel(DevOpt o, DevRef ref
           const int ia = m0 + __popcll(na & below) + __popcll(nb & below), ib = ia + (ha ? 0 : 1);
           if (!ha && ia < cap) {
             SideTask t;
-            side_start<G, RIGHT>(t, o, ref, a, fl[qq.shard + 8 * ia], ta_);
+            const FatTask f = fl[qq.shard + 8 * ia];
+            side_query<G, RIGHT>(b, f, qa_, QB);
+            side_start<G, RIGHT>(t, o, ref, a, f, ta_);
             spark(sa, t);
             ha = true;
           }
           if (!hb && ib < cap) {
             SideTask t;
-            side_start<G, RIGHT>(t, o, ref, a, fl[qq.shard + 8 * ib], tb_);
+            const FatTask f = fl[qq.shard + 8 * ib];
+            side_query<G, RIGHT>(b, f, qb_, QB);
+            side_start<G, RIGHT>(t, o, ref, a, f, tb_);
             spark(sb, t);
             hb = true;
           }
@@ -1463,9 +1482,19 @@ __global__ void __launch_bounds__(kBlock) spec_side4_kernel(DevOpt o, DevRef ref
       if (!more) break;
       continue;
     }
-    QCall ca = quad_idle(b.seq, ta_), cb = quad_idle(b.seq, tb_);
-    if (ha) ca = side_call<RIGHT>(sload(sa), o, b.seq, ta_);
-    if (hb) cb = side_call<RIGHT>(sload(sb), o, b.seq, tb_);
+    QCall ca = quad_idle(qa_, ta_), cb = quad_idle(qb_, tb_);  // every query pointer in LDS
+    if (ha) {
+      ca = side_call<RIGHT>(sload(sa), o, b.seq, ta_);
+      ca.q = qa_;
+      ca.qa = 0;
+      ca.qd = 1;
+    }
+    if (hb) {
+      cb = side_call<RIGHT>(sload(sb), o, b.seq, tb_);
+      cb.q = qb_;
+      cb.qa = 0;
+      cb.qd = 1;
+    }
     ExtOut xa, xb;
     Tally32 tla{0, 0, 0}, tlb{0, 0, 0};
 #ifdef BWAGPU_OCC_DIAG
@@ -1502,7 +1531,9 @@ __global__ void __launch_bounds__(kBlock) spec_side4_kernel(DevOpt o, DevRef ref
     atomicAdd(reinterpret_cast<unsigned long long*>(a.ctr + SPC_SPEC64), (unsigned long long)spec_cells);
 }
 
-static size_t side4_lds(int tb_bytes, int g) { return (size_t)(kBlock / g) * (2 * (size_t)tb_bytes + 2 * kSideLds); }
+static size_t side4_lds(int tb_bytes, int g, int pmax) {
+  return (size_t)(kBlock / g) * (2 * (size_t)tb_bytes + 2 * kSideLds + 2 * (size_t)pmax * g);
+}
 
 // ------------------------------------ the side kernel with a producer wave
 // spec_side4_kernel's waves spent 17.5 % of their cycles at call starts: the
@@ -1534,12 +1565,8 @@ __device__ __forceinline__ void lds_publish(int* p, int v) {
 template <int G, bool RIGHT>
 __device__ __forceinline__ void side_prep(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                           const FatTask& f, uint8_t* buf, int tb_bytes, int qb) {
-  const int r = (int)(threadIdx.x & (G - 1));
-  const int qbeg = (int)(f.qls & 1023u), len = (int)((f.qls >> 10) & 1023u), lq = (int)(f.qls >> 20);
-  const int qlen = min(RIGHT ? lq - qbeg - len : qbeg, qb);
-  const uint8_t* q = b.seq + f.qoff + (RIGHT ? qbeg + len : qbeg - 1);
   uint8_t* const qd = buf + tb_bytes;
-  for (int j = r; j < qlen; j += G) qd[j] = q[RIGHT ? j : -j];
+  side_query<G, RIGHT>(b, f, qd, qb);
   SideTask t;
   side_start<G, RIGHT>(t, o, ref, a, f, buf);
   spark((LdsS*)(qd + qb), t);
@@ -2831,7 +2858,7 @@ bool quad_rows_ok(const DevOpt& o, long rows) {
 template <int G, int PMAX, bool K8>
 static void launch_side_pair(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a, int l,
                              int tb_bytes, hipStream_t st, int grid_cap, int round) {
-  const size_t lds = side4_lds(tb_bytes, G);
+  const size_t lds = side4_lds(tb_bytes, G, PMAX);
   const int nb = resident_blocks(spec_side4_kernel<G, PMAX, K8, false>, lds);
   const int gr = round == 2 ? std::min(nb, 64) : std::min(nb, grid_cap);
   hipLaunchKernelGGL((spec_side4_kernel<G, PMAX, K8, false>), dim3(gr), dim3(kBlock), lds, st, o, ref, b, a, l,
@@ -2964,7 +2991,10 @@ static void launch_ext_round(const DevOpt& o, const DevRef& ref, const DevBatch&
 // shorter batches (C2: no such miss) round C stays unlaunched — a launch
 // waited ~0.18 ms per batch for CU slots the other caller stream's extension
 // kernel held, even over an empty list — and the redo pass extends the rare
-// misses inline.
+// misses inline.  With the strict emulation (BWAGPU_EMU_STRICT, default) the
+// light and matrix-heavy reads have no miss left, so round C stays unlaunched
+// on every batch; a heavy read without a matrix can still miss, and the redo
+// pass extends that inline.
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss) {
   if (b.n_reads == 0) return hipSuccess;
@@ -2979,7 +3009,7 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
     launch_ext_round(o, ref, b, a, 1, tb_bytes, lq_max, st, ss);
   }
   launch_select<SEL_FINAL>(o, ref, b, a, tb_bytes, st, ss);
-  if (b.n_chains && lq_max > kSpecBinLen[0]) launch_ext_round(o, ref, b, a, 2, tb_bytes, lq_max, st, ss);
+  if (b.n_chains && lq_max > kSpecBinLen[0] && !a.emu_strict) launch_ext_round(o, ref, b, a, 2, tb_bytes, lq_max, st, ss);
   if (b.n_chains) launch_select<SEL_REDO>(o, ref, b, a, tb_bytes, st, ss);
   return hipGetLastError();
 }
