@@ -765,6 +765,7 @@ def regime_stage(dev, steps: int = 10, n_streams: int = 2, ext_form: int = 0) ->
             x.wait_event(ev0)
         for i in range(steps):
             d.run(eng, streams[i % n_streams].cuda_stream, i)
+        t_enq = time.perf_counter() - t1
         for x in streams[1:]:
             e = torch.cuda.Event()
             e.record(x)
@@ -784,6 +785,8 @@ def regime_stage(dev, steps: int = 10, n_streams: int = 2, ext_form: int = 0) ->
              "unit": "Mreads/s", "gcups": round(float(st[0]) / el / 1e9, 3),
              "parity_all_steps": why is None, "coverage": s.coverage,
              "ext_busy_ms_per_batch": round(ext_busy / steps, 4),
+             # the host's enqueue of the batches' launches (~30 each): near ms_per_batch = launch-bound
+             "host_enqueue_ms_per_batch": round(t_enq * 1e3 / steps, 4),
              "batch": ("tests/golden/c3_refseed.npz (the C2 fixture's batch 0 in the GRCh38-shaped regime)"
                        if name == "c3_refseed" else f"tests/golden/c3_grch38.npz set {name!r}") +
                       f", the same batch every step"}
@@ -1051,6 +1054,7 @@ def timed_steps(eng: Engine, dbs, slots, streams, steps: int, world: int, dev, p
         x.wait_event(ev0)
     for i in range(steps):
         dbs[i % nb].run(eng, streams[i % len(streams)].cuda_stream, slots[i])
+    t_enq = time.perf_counter() - t0  # the host's enqueue of every step's ~30 launches
     for x in streams[1:]:
         e = torch.cuda.Event()
         e.record(x)
@@ -1064,7 +1068,7 @@ def timed_steps(eng: Engine, dbs, slots, streams, steps: int, world: int, dev, p
     elapsed = max(wall, gpu_s)
     reads_done = sum(dbs[i % nb].b.n_reads for i in range(steps))
     elapsed, total_reads = job_totals(elapsed, reads_done, world, dev)
-    r = dict(elapsed=elapsed, total_reads=total_reads, wall=wall, gpu_s=gpu_s)
+    r = dict(elapsed=elapsed, total_reads=total_reads, wall=wall, gpu_s=gpu_s, enqueue_s=t_enq)
     if prof:
         r["ext_ms"], r["ext_launches"] = eng.prof_read()
         r["ext_iv"] = eng.prof_intervals(3 * steps)
@@ -1395,6 +1399,9 @@ def main():
     if rank == 0:
         result = headline_line(args, world, W, eng, dbs, slots, streams, stream, sptr, elapsed, total_reads,
                                cells, cells_all, ext_ms, ext_launches, ext_busy_ms, parity)
+        # the host's enqueue of the timed steps' launches (~30 per batch), per step: near
+        # ms_per_step would mean the stage is launch-bound on this host
+        result["host_enqueue_ms_per_step"] = round(T["enqueue_s"] * 1e3 / args.steps, 4)
     regs0, n0 = dbs[0].results(0)
     fix_checks = W.fixture if W.fixture else checks
     if rank == 0 and world == 1 and W.fixture and W.ref_answers and not args.headline_only:
