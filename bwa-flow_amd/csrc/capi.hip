@@ -870,7 +870,6 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_heavy.ensure(sizeof(int32_t) * nr), "hipMalloc(heavy)");
   HIPC(s.d_redo.ensure(sizeof(int32_t) * nr), "hipMalloc(redo)");
   HIPC(s.d_rbits.ensure(sizeof(uint32_t) * (nr / 32 + 1)), "hipMalloc(rbits)");
-  HIPC(hipMemsetAsync(s.d_rbits.p, 0, sizeof(uint32_t) * (nr / 32 + 1), st), "memset rbits");
   HIPC(s.d_desc.ensure(sizeof(ReadDesc) * nr), "hipMalloc(desc)");
   HIPC(s.d_schain.ensure(sizeof(int32_t) * ns), "hipMalloc(seedchain)");
   HIPC(s.d_hinfo.ensure(sizeof(int4) * nr), "hipMalloc(hinfo)");
@@ -878,9 +877,7 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   HIPC(s.d_colent.ensure(sizeof(int32_t) * ns), "hipMalloc(colent)");
   HIPC(s.d_longc.ensure(sizeof(int32_t) * nc), "hipMalloc(longc)");
   HIPC(s.d_qh.ensure(sizeof(int32_t) * kQHWords), "hipMalloc(qh)");
-  HIPC(hipMemsetAsync(s.d_qh.p, 0, sizeof(int32_t) * kQHWords, st), "memset qh");
   HIPC(s.d_sorth.ensure(sizeof(int32_t) * kSortWords), "hipMalloc(sorth)");
-  HIPC(hipMemsetAsync(s.d_sorth.p, 0, sizeof(int32_t) * kSortWords, st), "memset sorth");
   HIPC(s.d_stasks.ensure(sizeof(int2) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(stasks)");
   HIPC(s.d_ftask.ensure(sizeof(FatTask) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(ftask)");
   HIPC(s.d_ftaskR.ensure(sizeof(FatTask) * kSpecBins * (nc + (kSpecRounds - 1) * ns)), "hipMalloc(ftaskR)");
@@ -888,9 +885,6 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   // <= 2 * ns_total * (1 + ns_max / 64); reads that do not fit take the per-seed kernel
   const int64_t mat_words = std::max<int64_t>(1 << 20, 16 * (int64_t)ns);
   HIPC(s.d_mat.ensure(sizeof(uint64_t) * (size_t)mat_words), "hipMalloc(mat)");
-  HIPC(hipMemsetAsync(s.d_ctr.p, 0, sizeof(int32_t) * SPC_WORDS, st), "memset ctr");
-  if (db.n_seeds) HIPC(hipMemsetAsync(s.d_ext.p, 0, sizeof(SeedExt) * (size_t)db.n_seeds, st), "memset ext");
-  if (db.n_reads) HIPC(hipMemsetAsync(d_n, 0, sizeof(int32_t) * db.n_reads, st), "memset out_n");
   SpecArgs a;
   a.win = s.d_win.as<ChainWin>();
   a.chain_read = s.d_cread.as<int32_t>();
@@ -942,6 +936,9 @@ int enqueue_spec(bwagpu_ctx_t* ctx, Slot& s, const DevBatch& db, int lq_max, bwa
   ss.pool = ctx->prof_ev.empty() ? nullptr : ctx->prof_ev.data();
   ss.pool_n = (int)ctx->prof_ev.size();
   ss.pool_used = &ctx->prof_used;
+  // the batch's zeroed state (counters, queue heads, sort histograms, the
+  // round-B bits, SeedExt slots, region counts): one launch, not six memsets
+  HIPC(launch_spec_clear(a, db.n_reads, db.n_seeds, st), "spec clear");
   HIPC(launch_spec_chain2aln(ctx->opt, ctx->ref, db, a, tb, lq_max, st, ss), "spec chain2aln launch");
   return BWAGPU_OK;
 }

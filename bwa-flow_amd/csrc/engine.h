@@ -259,6 +259,7 @@ bool quad_bound_ok(const DevOpt& o, long hb);
 bool quad_rows_ok(const DevOpt& o, long rows);
 bool quad_key8_ok(const DevOpt& o, int lq);
 int ext_form();
+hipError_t launch_spec_clear(const SpecArgs& a, int n_reads, int n_seeds, hipStream_t st);
 hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBatch& b, const SpecArgs& a,
                                  int tb_bytes, int lq_max, hipStream_t st, const SpecStreams& ss);
 // LDS bytes per workgroup of the largest spec launch; regions the redo pass

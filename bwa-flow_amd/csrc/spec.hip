@@ -3014,6 +3014,36 @@ hipError_t launch_spec_chain2aln(const DevOpt& o, const DevRef& ref, const DevBa
   return hipGetLastError();
 }
 
+// a batch's zeroed state in one launch (blockIdx.y = which array)
+__global__ void __launch_bounds__(256) spec_clear_kernel(SpecArgs a, int nr, int ns) {
+  const int t0 = (int)(blockIdx.x * 256 + threadIdx.x), nt = (int)(gridDim.x * 256);
+  switch (blockIdx.y) {
+    case 0:
+      for (int i = t0; i < 3 * ns; i += nt) reinterpret_cast<uint4*>(a.ext)[i] = make_uint4(0, 0, 0, 0);  // 48 B each
+      break;
+    case 1:
+      for (int i = t0; i < nr; i += nt) a.out_n[i] = 0;
+      break;
+    case 2:
+      for (int i = t0; i < nr / 32 + 1; i += nt) a.rbits[i] = 0;
+      break;
+    case 3:
+      for (int i = t0; i < kQHWords; i += nt) a.qh[i] = 0;
+      break;
+    case 4:
+      for (int i = t0; i < kSortWords; i += nt) a.sorth[i] = 0;
+      break;
+    default:
+      for (int i = t0; i < SPC_WORDS; i += nt) a.ctr[i] = 0;
+  }
+}
+static_assert(sizeof(SeedExt) == 48, "spec_clear_kernel clears SeedExt as three uint4");
+
+hipError_t launch_spec_clear(const SpecArgs& a, int n_reads, int n_seeds, hipStream_t st) {
+  hipLaunchKernelGGL(spec_clear_kernel, dim3(256, 6), dim3(256), 0, st, a, n_reads, n_seeds);
+  return hipGetLastError();
+}
+
 size_t spec_select_lds(int tb_bytes) { return (size_t)kSelHeavyLds + 0 * tb_bytes; }
 int spec_redo_cap(int tb_bytes) { return sel_heavy_cap(SEL_REDO, tb_bytes); }
 
