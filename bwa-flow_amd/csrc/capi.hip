@@ -840,7 +840,7 @@ hipError_t choose_side(bwagpu_ctx_t* ctx, Slot& s, hipStream_t st, SpecStreams* 
     if ((e = hipStreamCreateWithFlags(&c, hipStreamNonBlocking)) != hipSuccess) break;
     bool ok = true;
     for (hipStream_t a : avoid)
-      if (!streams_concurrent(a, c)) {
+      if (!streams_concurrent(c, a)) {  // spin on the candidate, never on a caller stream
         ok = false;
         break;
       }

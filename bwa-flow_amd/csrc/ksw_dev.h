@@ -822,7 +822,9 @@ __device__ __forceinline__ QCall quad_idle(const uint8_t* seq, const uint8_t* tb
 // (every H < 256: quad_key8_ok); else H << KS | c widened to H << 10 | j per call.
 // G = the lanes of a group (two calls): 32 (four calls per wave) or 16 (eight
 // calls per wave, K8 only: every scan and reduction stays inside a DPP row).
-template <int G, int CPL, bool K8>
+// SYM: o_del == o_ins, so E's and F's gap-open terms share one subtraction of
+// the biased M per column.
+template <int G, int CPL, bool K8, bool SYM>
 __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, const QCall& Bc, ExtOut& xa, ExtOut& xb,
                                             Tally32& ta, Tally32& tbl) {
   using namespace pk16;
@@ -836,7 +838,10 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
   const int j0 = r * CPL;
   const uint32_t J0 = pk(j0, j0);
   const uint32_t EI1 = pk(e_ins, e_ins), ED1 = pk(e_del, e_del);
-  const uint32_t MB_OE = pk(128 + oe_ins, 128 + oe_ins), MB_OD = pk(128 + o.o_del, 128 + o.o_del);
+  // F's gap open from the biased M (the e_ins of F(j+1) = max(F(j), M(j) - o_ins)
+  // - e_ins is taken after the max), E's likewise with o_del
+  const uint32_t MB_OI = pk(128 + o.o_ins, 128 + o.o_ins), OI1 = pk(o.o_ins, o.o_ins);
+  const uint32_t MB_OD = SYM ? MB_OI : pk(128 + o.o_del, 128 + o.o_del);
   const int sk = 32 - __builtin_clz((unsigned)max(o.max_mat, 1));  // 2^sk > max(mat)
   const uint32_t KSH = pk(1 << sk, 1 << sk);
   const uint32_t RE = pk(e_ins * j0, e_ins * j0), RE2 = pk(e_ins * (j0 + CPL), e_ins * (j0 + CPL));
@@ -899,7 +904,9 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     const uint32_t LEFT0 = neg15(sub(LO, ONE)) & smax(GL, 0u);  // the first-column value where lo == 0
     GL = ssat(GL, ED1);
     const uint32_t SEL = (uint32_t)ta | ((uint32_t)tbb << 16) | 0x0c040c00u;
-    uint32_t MB[CPL], AA[CPL], CAP[CPL], R[CPL], GEL[CPL];
+    // XO: M' + 128 (M - o_ins with SYM, which E reads too); AA: M - o_ins in
+    // the band, 0 out of it
+    uint32_t XO[CPL], AA[CPL], CAP[CPL], R[CPL];
     uint32_t T = 0;
     // j <= hi  <=>  j - 1 < hi: column c's R is column c-1's "j < hi"
     R[0] = neg15(sub(add(J0, 0xffffffffu), HI));
@@ -909,13 +916,13 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       const uint32_t ltlo = neg15(sub(JC, LO));  // j < lo
       const uint32_t lthi = neg15(sub(JC, HI));  // j < hi
       if (c + 1 < CPL) R[c + 1] = lthi;
-      GEL[c] = ~ltlo;
       CAP[c] = lthi & ~ltlo;                     // lo <= j < hi
       const uint32_t sb = __builtin_amdgcn_perm(pfb[c], pfa[c], SEL);
       const uint32_t mb = smin(add(hh[c], sb), mad(hh[c], KSH, 0x00800080u));  // M' + 128
-      MB[c] = mb;
-      AA[c] = umin(sub(mb, MB_OE), CAP[c]);
-      T = smax(usat(T, EI1), AA[c]);
+      const uint32_t xi = sub(mb, MB_OI);
+      XO[c] = SYM ? xi : mb;
+      AA[c] = umin(xi, CAP[c]);
+      T = usat(smax(T, AA[c]), EI1);  // max(T - e_ins, M - oe_ins, 0)
     }
     const uint32_t sx = grp_scan_umax<G>(add(T, RE2));
     uint32_t EX;
@@ -929,10 +936,12 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     uint32_t LK = 0, H1Q = 0, hm[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      if (c > 0) f = smax(usat(f, EI1), AA[c - 1]);
-      const uint32_t h = smax(smax(sub(MB[c], 0x00800080u), ee[c]), f);
+      if (c > 0) f = usat(smax(f, AA[c - 1]), EI1);
+      const uint32_t m = SYM ? add(XO[c], OI1) : sub(XO[c], 0x00800080u);  // M
+      const uint32_t xd = SYM ? XO[c] : sub(XO[c], MB_OD);                   // M - o_del
+      const uint32_t h = smax(smax(m, ee[c]), f);
       hm[c] = umin(h, CAP[c]);
-      const uint32_t en = usat(smax(ee[c], sub(MB[c], MB_OD)), ED1);
+      const uint32_t en = usat(smax(ee[c], xd), ED1);
       if constexpr (K8)
         LK = umax(LK, mad(hm[c], KMUL, add(J0, pk(c, c))));
       else
@@ -949,17 +958,21 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
       hs0 = r == 0 ? LEFT0 : hs0;
     }
     hh[0] = sel(R[0], hs0, hh[0]);
-    // band trim candidates: first non-zero column >= lo, last non-zero <= hi
-    uint32_t CL = 0x7fff7fffu, CH = 0xffffffffu;
+    // band trim candidates (ksw.c:466-469): the first and the last column j <=
+    // hi whose stored H or E is non-zero (H, E >= 0).  No lower bound is
+    // needed: every column left of lo was just written with H = E = 0 (out of
+    // the band, j <= hi), and a live call has lo <= hi (else its row maximum is
+    // 0 and it ends in this row).  CH carries last + 1 ("none": 0).
+    uint32_t CL = 0x7fff7fffu, CH = 0;
 #pragma unroll
     for (int c = CPL - 1; c >= 0; --c) {
-      const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));  // 0xffff where H or E is non-zero (both >= 0)
-      CL = sel(nz & GEL[c], add(J0, pk(c, c)), CL);
+      const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));  // 0xffff where H or E is non-zero
+      CL = sel(nz, add(J0, pk(c, c)), CL);
     }
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const uint32_t nz = neg15(sub(0u, hh[c] | ee[c]));
-      CH = sel(nz & R[c], add(J0, pk(c, c)), CH);
+      CH = sel(nz & R[c], add(J0, pk(c + 1, c + 1)), CH);
     }
     // the row maxima (ksw.c:433: the LAST column of the maximum) and the trim,
     // reduced over the half: MROW = the row's max H, MJ = its column
@@ -1025,7 +1038,7 @@ __device__ __forceinline__ void extend_quad(const DevOpt& o, const QCall& A, con
     // the next row's band (ksw.c:466-469)
     const uint32_t NLO = smin(CL, HI);
     LO = NLO;
-    HI = smin(add(smax(CH, sub(NLO, ONE)), pk(2, 2)), QL);
+    HI = smin(add(smax(CH, NLO), ONE), QL);  // min(max(last, lo - 1) + 2, qlen)
     // Row bound, every fourth row: a cell of a later row is reached from a
     // stored diagonal value v = H(i, j-1) > 0 of column j (or from the first
     // column's h0 - o_del - e_del (i+2) while lo == 0) by at most qlen - j
@@ -1071,8 +1084,15 @@ __device__ __forceinline__ void extend_quad_dispatch(const DevOpt& o, const QCal
   for (int g = 0; g < 64; g += G)
     qm = max(qm, max(__builtin_amdgcn_readlane(A.qlen, g), __builtin_amdgcn_readlane(Bc.qlen, g)));
   const int cpl = (qm + G) / G;
-#define EXT_QUAD(n) \
-  if (n <= PMAX && cpl == n) return extend_quad<G, (n <= PMAX ? n : 1), K8>(o, A, Bc, xa, xb, ta, tbl);
+#ifndef BWAGPU_QUAD_SYM
+#define BWAGPU_QUAD_SYM 1
+#endif
+  const bool sym = BWAGPU_QUAD_SYM && o.o_del == o.o_ins;  // bwa's defaults: 6 / 6
+#define EXT_QUAD(n)                                                                            \
+  if (n <= PMAX && cpl == n) {                                                                 \
+    if (sym) return extend_quad<G, (n <= PMAX ? n : 1), K8, true>(o, A, Bc, xa, xb, ta, tbl);  \
+    return extend_quad<G, (n <= PMAX ? n : 1), K8, false>(o, A, Bc, xa, xb, ta, tbl);          \
+  }
   EXT_QUAD(1) EXT_QUAD(2) EXT_QUAD(3) EXT_QUAD(4) EXT_QUAD(5) EXT_QUAD(6) EXT_QUAD(7) EXT_QUAD(8) EXT_QUAD(9)
   EXT_QUAD(10) EXT_QUAD(11) EXT_QUAD(12) EXT_QUAD(13) EXT_QUAD(14) EXT_QUAD(15) EXT_QUAD(16)
 #undef EXT_QUAD
